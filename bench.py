@@ -1,0 +1,188 @@
+"""Benchmark: Hamming pair-comparisons/s, 737,280-barcode all-pairs histogram (BASELINE.json).
+
+One step = the whole hot path of Barcodes.summarize_hamming_distances on device-
+resident codes: build the bit-sliced selection table, count this rank's share of the
+all-pairs work items, all-reduce the subset counts over RCCL (N > 1), copy them to
+the host, invert them to the exact histogram and compute the numpy-exact summary.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Rank 0 prints one JSON line.  `value` = all pairs of the whole job / max-over-ranks
+wall time of the K timed steps.  `roofline` prices the dominant kernel
+(allpairs_count) with the algorithmic op count of SURVEY.md §8(d) (4 int32 ops per
+16-bp pair) over its average duration, measured with HIP events on the stream the
+kernel runs on.  `cpu_baseline` times the C oracle restatement (test infrastructure,
+never the product) on a bounded row sample of the same workload, rank 0 only.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from sctools_amd import _lib, synthetic  # noqa: E402
+
+VALU_PEAK_OPS = 256 * 128 * 2.4e9  # 256 CU x 4 SIMD32 x 32 lanes/clk x 2.4 GHz = 78.6 Tops/s
+ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-bit code word
+ISSUED_OPS_PER_PAIR = {8: 55.5 / 32}  # VALU instrs per 32-pair group in the .s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 5])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample time")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(codes, target_s):
+    """C oracle (OpenMP popcount restatement of encodings.py:113-121) on rows [0, R)."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    n = codes.size
+    lib = O.c_oracle()
+    # calibrate on a small sample, then size the sample to ~target_s
+    rows = 64
+    t = time.perf_counter()
+    O.c_hist_rows(codes, 0, rows, threads=threads)
+    dt = max(time.perf_counter() - t, 1e-6)
+    rows = int(min(n - 1, max(rows, rows * target_s / dt)))
+    t = time.perf_counter()
+    O.c_hist_rows(codes, 0, rows, threads=threads)
+    dt = time.perf_counter() - t
+    pairs = rows * (n - 1) - rows * (rows - 1) // 2
+    # the scalar loop itself (1 core), short sample
+    srow = 16
+    t = time.perf_counter()
+    O.c_hist_rows(codes, 0, srow, scalar=True)
+    sdt = time.perf_counter() - t
+    spairs = srow * (n - 1) - srow * (srow - 1) // 2
+    return {"value": pairs / dt, "unit": "pairs/s", "cores": lib.oracle_threads() if threads == 0 else threads,
+            "kind": "port",
+            "sample": "C oracle popcount (oracle/sct_oracle.c) over rows [0,%d) of the same %d-code set: "
+                      "%d pairs in %.2f s" % (rows, n, pairs, dt),
+            "scalar_1core_pairs_per_s": spairs / sdt,
+            "python_reference_1core_pairs_per_s": 752540.0}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    _lib.check(_lib.lib().sct_set_device(dev.index))
+
+    n, L, seed = synthetic.CONFIGS[args.config]
+    codes = synthetic.whitelist_codes(n, L, seed)
+    d_codes = torch.from_numpy(codes.view(np.int64)).to(dev)
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 2 * L)
+    b = plan.items * rank // world
+    e = plan.items * (rank + 1) // world
+    counts = torch.zeros(plan.nbins, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    kernel_ms = []
+
+    def step(record):
+        counts.zero_()
+        plan.build(sptr)
+        if record:
+            ev0.record(stream)
+        plan.count(counts.data_ptr(), b, e, 0, sptr)
+        if record:
+            ev1.record(stream)
+        if world > 1:
+            dist.all_reduce(counts)
+        host = counts.cpu().numpy().view(np.uint64)  # synchronises the stream
+        if record:
+            kernel_ms.append(ev0.elapsed_time(ev1))
+        hist = _lib.counts_to_hist(host)
+        return hist, _lib.summary_from_hist(hist)
+
+    for _ in range(args.warmup):
+        hist, summ = step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        hist, summ = step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    pairs_total = plan.pairs
+    assert int(hist.sum()) == pairs_total, "histogram does not cover every pair"
+    my_pairs = plan.range_pairs(b, e)
+    kms = float(np.mean(kernel_ms))
+    achieved = my_pairs * ALGO_OPS_PER_PAIR / (kms * 1e-3)
+    issued = my_pairs * ISSUED_OPS_PER_PAIR.get(L // 2, float("nan")) / (kms * 1e-3)
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_allpairs_r01.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        out = {
+            "metric": "Hamming pair-comparisons/sec, 737K 10x whitelist all-pairs, 1-8 GPUs",
+            "value": pairs_total * args.steps / elapsed,
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded uniform random unique 16-bp codes, sctools_amd/synthetic.py)",
+            "config": {"workload": "config %d: %d-barcode all-pairs TwoBit Hamming histogram + summary"
+                                   % (args.config, n),
+                       "barcodes": n, "barcode_length": L, "pairs": pairs_total,
+                       "parallelism": "item-range shards, RCCL all-reduce of %d subset counts" % plan.nbins
+                       if world > 1 else "single GPU"},
+            "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
+                         "unit": "Tops/s", "frac": achieved / VALU_PEAK_OPS, "traffic": traffic,
+                         "kernel": "allpairs_count_kernel<8>", "kernel_ms": kms,
+                         "algo_ops_per_pair": ALGO_OPS_PER_PAIR,
+                         "issued_valu_ops_per_pair": ISSUED_OPS_PER_PAIR.get(L // 2),
+                         "issued_frac": issued / VALU_PEAK_OPS},
+            "summary": dict(zip(("minimum", "p25", "median", "p75", "maximum", "average"),
+                                [float(x) for x in summ])),
+        }
+        if not args.no_cpu and world == 1:
+            out["cpu_baseline"] = cpu_baseline(codes, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    plan.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

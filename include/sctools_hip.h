@@ -1,0 +1,161 @@
+/*
+ * sctools_hip.h — C ABI of libsctools_hip.so, the MI355X (gfx950) barcode hot path.
+ *
+ * The reference (dpeerlab/sctools) is pure Python and has no FFI of its own; each
+ * entry point below replaces the Python function cited next to it, and the Python
+ * drop-in (sctools_amd.encodings / sctools_amd.barcode) binds them with ctypes
+ * (INTEGRATION.md shows the binding).  Conventions:
+ *   - every function returns an int status: SCT_OK (0) or a negative SCT_E_* code;
+ *     sct_last_error() returns a thread-local message for the last failure;
+ *   - "device" functions take device pointers and a hipStream_t passed as void*
+ *     (NULL = the default stream) and are asynchronous on that stream;
+ *   - "_host" functions take host pointers, run on the current device and return
+ *     only when results are back in host memory;
+ *   - codes wider than 64 bits are `words` little-endian uint64 limbs per record
+ *     (limb 0 holds bits 0..63 of the Python int);
+ *   - no function retains a caller pointer after it returns (plans own their
+ *     device buffers and hold no host pointers).
+ */
+#ifndef SCTOOLS_HIP_H
+#define SCTOOLS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCT_OK 0
+#define SCT_E_INVALID (-1)   /* bad argument (maps to ValueError)             */
+#define SCT_E_HIP (-2)       /* HIP runtime failure / no device (RuntimeError) */
+#define SCT_E_NOMEM (-3)     /* device allocation failed (MemoryError)         */
+#define SCT_E_RANGE (-4)     /* value outside what the kernel supports         */
+
+/* ---------------------------------------------------------------- library */
+int sct_version(void);                 /* ABI version, currently 1 */
+const char* sct_last_error(void);      /* thread-local, never NULL */
+int sct_device_count(int* count);      /* HIP devices visible to this process */
+int sct_set_device(int device);        /* select the device for later calls (hipSetDevice) */
+
+/* ---------------------------------------------------------------- encoders
+ * kind = 2 (TwoBit) or 3 (ThreeBit).
+ * Replaces TwoBit.encode  (src/sctools/encodings.py:75-88, map :53-69) and
+ *          ThreeBit.encode (src/sctools/encodings.py:155-167, map :139-149).
+ * n records of L bytes, record r starting at seqs + r*stride (stride >= L).
+ * codes : n*words uint64, words = ceil(kind*L/64) (at least 1); MSB-first packing
+ *         exactly as the reference's `encoded <<= bits; encoded += map[byte]`.
+ * gc    : nullable; n uint8 = GC count of the record (requires L <= 255).
+ *         TwoBit: C/c/G/g bytes (the ambiguous positions are counted after the
+ *         host fills them, see flags). ThreeBit: popcount of bit 0 of each triplet
+ *         (encodings.py:182-192), i.e. C/c/G/g bytes.
+ * flags : nullable (TwoBit); n uint8, bit0 = an IUPAC-ambiguous byte was seen
+ *         (encoded as 0, to be drawn by the caller's random.randint(0,3) in order,
+ *         encodings.py:69), bit1 = an invalid byte was seen (reference raises
+ *         KeyError, encodings.py:68).  ThreeBit never flags (any byte -> N=6).
+ */
+int sct_encode(int kind, const uint8_t* seqs, int64_t n, int64_t stride, int L,
+               uint64_t* codes, uint8_t* gc, uint8_t* flags, void* stream);
+int sct_encode_host(int kind, const uint8_t* seqs, int64_t n, int64_t stride, int L,
+                    uint64_t* codes, uint8_t* gc, uint8_t* flags);
+
+/* ---------------------------------------------------------------- decoders
+ * TwoBit(L).decode (encodings.py:90-100): exactly L bytes from the LSB upward,
+ * bits above 2L ignored.  out: n*L bytes.
+ */
+int sct_decode2(const uint64_t* codes, int64_t n, int words, int L, uint8_t* out, void* stream);
+int sct_decode2_host(const uint64_t* codes, int64_t n, int words, int L, uint8_t* out);
+/* ThreeBit.decode (encodings.py:169-180): bytes up to the highest non-zero triplet.
+ * out: n*maxlen bytes, record r's sequence right-aligned in its maxlen slot
+ * (so it ends at out[(r+1)*maxlen-1]); lengths[r] = its length;
+ * bad[r] = -1, or the value (0, 5 or 7) of the lowest-order triplet below the top
+ * non-zero one that has no decoding (the reference raises KeyError(value)).
+ * maxlen must be >= ceil(64*words/3).
+ */
+int sct_decode3(const uint64_t* codes, int64_t n, int words, int maxlen, uint8_t* out,
+                int32_t* lengths, int32_t* bad, void* stream);
+int sct_decode3_host(const uint64_t* codes, int64_t n, int words, int maxlen, uint8_t* out,
+                     int32_t* lengths, int32_t* bad);
+
+/* ---------------------------------------------------------------- gc_content
+ * TwoBit(L).gc_content (encodings.py:102-111): low bit of each of the L 2-bit groups.
+ * ThreeBit.gc_content  (encodings.py:182-192): bit 0 of every triplet of the code.
+ * kind 2 uses L; kind 3 ignores it.  out: n int32.
+ */
+int sct_gc_content(int kind, const uint64_t* codes, int64_t n, int words, int L, int32_t* out,
+                   void* stream);
+int sct_gc_content_host(int kind, const uint64_t* codes, int64_t n, int words, int L, int32_t* out);
+
+/* ---------------------------------------------------------------- element-wise Hamming
+ * TwoBit.hamming_distance (encodings.py:113-121) / ThreeBit.hamming_distance
+ * (encodings.py:194-202) of a[r] vs b[r]: number of non-zero 2-bit (3-bit) groups
+ * of a^b.  out: n int32.
+ */
+int sct_hamming_pairs(int kind, const uint64_t* a, const uint64_t* b, int64_t n, int words,
+                      int32_t* out, void* stream);
+int sct_hamming_pairs_host(int kind, const uint64_t* a, const uint64_t* b, int64_t n, int words,
+                           int32_t* out);
+
+/* ---------------------------------------------------------------- all-pairs histogram
+ * Replaces the pair loop of Barcodes.summarize_hamming_distances
+ * (src/sctools/barcode.py:42-43: itertools.combinations + TwoBit.hamming_distance).
+ *
+ * A plan holds the bit-sliced selection table of n device-resident uint64 codes
+ * (the TwoBit distance is taken over the low `code_bits` bits, code_bits in
+ * [1, 64]; every code must be < 2^code_bits).  The unordered pairs i<j are cut
+ * into `items` equal work items (row block x column chunk) so that callers can
+ * shard them: any partition of [0, items) into ranges, counted on any number of
+ * devices and summed, gives the same result.
+ *
+ * sct_allpairs_count ACCUMULATES (atomic add) nbins uint64 "subset counts" into
+ * d_counts: d_counts[0] += pairs counted, d_counts[m] += #pairs whose distance d
+ * has all bits of m set (d & m == m), m = 1..nbins-1.  The counts are linear, so
+ * they may be summed across devices (RCCL all-reduce) before sct_counts_to_hist.
+ */
+typedef struct sct_allpairs_plan sct_allpairs_plan;
+
+int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int code_bits,
+                             sct_allpairs_plan** plan);
+int sct_allpairs_plan_destroy(sct_allpairs_plan* plan);
+/* nbins = max distance + 1 = 2*ceil(code_bits/4)+1; items = number of work items */
+int sct_allpairs_plan_info(const sct_allpairs_plan* plan, int* nbins, int64_t* items,
+                           int64_t* pairs);
+/* (Re)build the selection table from the codes the plan was created on. */
+int sct_allpairs_build(sct_allpairs_plan* plan, void* stream);
+/* Count work items [item_begin, item_end).  grid = 0 picks the persistent grid size. */
+int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
+                       uint64_t* d_counts, int grid, void* stream);
+/* Pairs contained in work items [item_begin, item_end) (host arithmetic). */
+int sct_allpairs_range_pairs(const sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
+                             int64_t* pairs);
+
+/* Host: subset counts -> histogram (exact Moebius inversion), hist[d] for d < nbins. */
+int sct_counts_to_hist(const uint64_t* counts, int nbins, uint64_t* hist);
+
+/* One-shot, host pointers, current device: histogram of TwoBit distances over all
+ * unordered pairs of the n codes.  hist must hold nbins = 2*ceil(code_bits/4)+1. */
+int sct_hamming_hist_allpairs_host(const uint64_t* codes, int64_t n, int code_bits,
+                                   uint64_t* hist, int nbins);
+
+/* ---------------------------------------------------------------- base frequency
+ * Replaces Barcodes.base_frequency (src/sctools/barcode.py:48-70): out[p*4 + v] =
+ * number of codes whose base p (0 = first, MSB-first TwoBit packing) has 2-bit value
+ * v (A 0, C 1, T 2, G 3); bases above bit 63 read as 0, as the reference's uint64
+ * keys >>= 2 loop does.  out: L*4 uint64, overwritten.  L <= 1024.
+ */
+int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint64_t* out, void* stream);
+int sct_base_frequency_host(const uint64_t* codes, int64_t n, int L, uint64_t* out);
+
+/* ---------------------------------------------------------------- summary
+ * Replaces barcode.py:44-46 (np.percentile(distances,[0,25,50,75,100]) with numpy's
+ * default 'linear' method, then np.mean) computed from the histogram alone,
+ * bit-exact in float64.  out[0..5] = minimum, 25th percentile, median,
+ * 75th percentile, maximum, average.  Returns SCT_E_RANGE when the histogram is
+ * empty (the reference raises IndexError).
+ */
+int sct_summary_from_hist(const uint64_t* hist, int nbins, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SCTOOLS_HIP_H */

@@ -1,0 +1,266 @@
+"""ctypes binding of libsctools_hip.so (C ABI declared in include/sctools_hip.h).
+
+This is the only route from the Python drop-in to the hardware: every compute call
+of ``sctools_amd.encodings`` / ``sctools_amd.barcode`` lands here and then in a HIP
+kernel.  There is no CPU fallback: if the shared library is missing the import of
+this module's ``lib()`` raises, and HIP failures (no device, launch errors) surface
+as ``RuntimeError`` with the library's message.
+"""
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SCTOOLS_HIP_LIB") or os.path.join(_HERE, "libsctools_hip.so")
+
+SCT_OK = 0
+SCT_E_INVALID = -1
+SCT_E_HIP = -2
+SCT_E_NOMEM = -3
+SCT_E_RANGE = -4
+
+_i32, _i64, _dbl = ctypes.c_int, ctypes.c_int64, ctypes.c_double
+_vp = ctypes.c_void_p
+_p64 = ctypes.POINTER(ctypes.c_uint64)
+
+# name -> argtypes (restype is int unless listed in _RESTYPES); mirrors include/sctools_hip.h
+SIGNATURES = {
+    "sct_version": [],
+    "sct_last_error": [],
+    "sct_device_count": [ctypes.POINTER(_i32)],
+    "sct_set_device": [_i32],
+    "sct_encode": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
+    "sct_encode_host": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp],
+    "sct_decode2": [_vp, _i64, _i32, _i32, _vp, _vp],
+    "sct_decode2_host": [_vp, _i64, _i32, _i32, _vp],
+    "sct_decode3": [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp],
+    "sct_decode3_host": [_vp, _i64, _i32, _i32, _vp, _vp, _vp],
+    "sct_gc_content": [_i32, _vp, _i64, _i32, _i32, _vp, _vp],
+    "sct_gc_content_host": [_i32, _vp, _i64, _i32, _i32, _vp],
+    "sct_hamming_pairs": [_i32, _vp, _vp, _i64, _i32, _vp, _vp],
+    "sct_hamming_pairs_host": [_i32, _vp, _vp, _i64, _i32, _vp],
+    "sct_allpairs_plan_create": [_vp, _i64, _i32, ctypes.POINTER(_vp)],
+    "sct_allpairs_plan_destroy": [_vp],
+    "sct_allpairs_plan_info": [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i64), ctypes.POINTER(_i64)],
+    "sct_allpairs_build": [_vp, _vp],
+    "sct_allpairs_count": [_vp, _i64, _i64, _vp, _i32, _vp],
+    "sct_allpairs_range_pairs": [_vp, _i64, _i64, ctypes.POINTER(_i64)],
+    "sct_counts_to_hist": [_vp, _i32, _vp],
+    "sct_hamming_hist_allpairs_host": [_vp, _i64, _i32, _vp, _i32],
+    "sct_summary_from_hist": [_vp, _i32, _vp],
+    "sct_base_frequency": [_vp, _i64, _i32, _vp, _vp],
+    "sct_base_frequency_host": [_vp, _i64, _i32, _vp],
+}
+_RESTYPES = {"sct_last_error": ctypes.c_char_p}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class LibraryMissing(ImportError):
+    pass
+
+
+def lib():
+    """Load libsctools_hip.so once; raise LibraryMissing (an ImportError) if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise LibraryMissing(
+                    "libsctools_hip.so not found at %s: build it with "
+                    "`python -c 'import __graft_entry__; __graft_entry__.build()'` "
+                    "(there is no CPU fallback)" % LIB_PATH)
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, args in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.argtypes = args
+                fn.restype = _RESTYPES.get(name, _i32)
+            _lib = handle
+    return _lib
+
+
+def last_error():
+    msg = lib().sct_last_error()
+    return msg.decode("utf-8", "replace") if msg else ""
+
+
+def check(rc):
+    if rc == SCT_OK:
+        return
+    msg = last_error()
+    if rc == SCT_E_NOMEM:
+        raise MemoryError(msg)
+    if rc in (SCT_E_INVALID, SCT_E_RANGE):
+        raise ValueError(msg)
+    raise RuntimeError(msg)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_vp) if a is not None else None
+
+
+# ------------------------------------------------------------------ int <-> limbs
+def words_for_bits(bits):
+    return max(1, -(-int(bits) // 64))
+
+
+def ints_to_limbs(values, words=None):
+    """Python ints (>= 0) -> (n, words) uint64 little-endian limbs."""
+    values = list(values)
+    if words is None:
+        words = words_for_bits(max((int(v).bit_length() for v in values), default=0))
+    if words == 1:
+        return np.array(values, dtype=np.uint64).reshape(-1, 1)
+    buf = b"".join(int(v).to_bytes(8 * words, "little") for v in values)
+    return np.frombuffer(buf, dtype="<u8").reshape(-1, words).astype(np.uint64)
+
+
+def limbs_to_ints(limbs):
+    limbs = np.ascontiguousarray(limbs, dtype=np.uint64)
+    if limbs.ndim == 1 or limbs.shape[1] == 1:
+        return [int(x) for x in limbs.reshape(-1).tolist()]
+    return [int.from_bytes(row.astype("<u8").tobytes(), "little") for row in limbs]
+
+
+# ------------------------------------------------------------------ entry points
+def encode(kind, seqs, L):
+    """(n, L) uint8 array -> (codes (n, words) uint64, gc uint8|None, flags uint8)."""
+    seqs = np.ascontiguousarray(seqs, dtype=np.uint8).reshape(-1, L) if L else np.zeros((len(seqs), 0), np.uint8)
+    n = seqs.shape[0]
+    words = words_for_bits(kind * L)
+    codes = np.zeros((n, words), dtype=np.uint64)
+    flags = np.zeros(n, dtype=np.uint8)
+    gc = np.zeros(n, dtype=np.uint8) if L <= 255 else None
+    check(lib().sct_encode_host(kind, _ptr(seqs), n, L, L, _ptr(codes), _ptr(gc), _ptr(flags)))
+    return codes, gc, flags
+
+
+def decode2(codes, L):
+    codes = np.ascontiguousarray(codes, dtype=np.uint64)
+    codes2 = codes.reshape(codes.shape[0], -1)
+    out = np.zeros((codes2.shape[0], L), dtype=np.uint8)
+    check(lib().sct_decode2_host(_ptr(codes2), codes2.shape[0], codes2.shape[1], L, _ptr(out)))
+    return out
+
+
+def decode3(codes):
+    codes = np.ascontiguousarray(codes, dtype=np.uint64)
+    codes2 = codes.reshape(codes.shape[0], -1)
+    n, words = codes2.shape
+    maxlen = (64 * words + 2) // 3
+    out = np.zeros((n, maxlen), dtype=np.uint8)
+    lengths = np.zeros(n, dtype=np.int32)
+    bad = np.zeros(n, dtype=np.int32)
+    check(lib().sct_decode3_host(_ptr(codes2), n, words, maxlen, _ptr(out), _ptr(lengths), _ptr(bad)))
+    return out, lengths, bad
+
+
+def gc_content(kind, codes, L=0):
+    codes = np.ascontiguousarray(codes, dtype=np.uint64)
+    codes2 = codes.reshape(codes.shape[0], -1)
+    out = np.zeros(codes2.shape[0], dtype=np.int32)
+    check(lib().sct_gc_content_host(kind, _ptr(codes2), codes2.shape[0], codes2.shape[1], L, _ptr(out)))
+    return out
+
+
+def hamming_pairs(kind, a, b):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    a2 = a.reshape(a.shape[0], -1)
+    b2 = b.reshape(b.shape[0], -1)
+    if a2.shape != b2.shape:
+        raise ValueError("operand shapes differ: %s vs %s" % (a2.shape, b2.shape))
+    out = np.zeros(a2.shape[0], dtype=np.int32)
+    check(lib().sct_hamming_pairs_host(kind, _ptr(a2), _ptr(b2), a2.shape[0], a2.shape[1], _ptr(out)))
+    return out
+
+
+def nbins_for_bits(code_bits):
+    return 2 * ((max(1, int(code_bits)) + 3) // 4) + 1
+
+
+def hamming_hist_allpairs(codes, code_bits=None):
+    """Histogram (uint64[nbins]) of TwoBit distances over all unordered pairs of codes."""
+    codes = np.ascontiguousarray(codes, dtype=np.uint64).reshape(-1)
+    if code_bits is None:
+        code_bits = int(np.bitwise_or.reduce(codes)).bit_length() if codes.size else 1
+    code_bits = max(1, code_bits)
+    nbins = nbins_for_bits(code_bits)
+    hist = np.zeros(nbins, dtype=np.uint64)
+    check(lib().sct_hamming_hist_allpairs_host(_ptr(codes), codes.size, code_bits, _ptr(hist), nbins))
+    return hist
+
+
+def counts_to_hist(counts):
+    counts = np.ascontiguousarray(counts, dtype=np.uint64).reshape(-1)
+    hist = np.zeros_like(counts)
+    check(lib().sct_counts_to_hist(_ptr(counts), counts.size, _ptr(hist)))
+    return hist
+
+
+def summary_from_hist(hist):
+    """6 float64: minimum, 25th, median, 75th percentile, maximum, average (bit-exact numpy)."""
+    hist = np.ascontiguousarray(hist, dtype=np.uint64).reshape(-1)
+    out = np.zeros(6, dtype=np.float64)
+    rc = lib().sct_summary_from_hist(_ptr(hist), hist.size, _ptr(out))
+    if rc == SCT_E_RANGE and int(hist.sum()) == 0:
+        # np.percentile of an empty list (barcode.py:45 with < 2 unique barcodes)
+        raise IndexError("index -1 is out of bounds for axis 0 with size 0")
+    check(rc)
+    return out
+
+
+def base_frequency(codes, L):
+    codes = np.ascontiguousarray(codes, dtype=np.uint64).reshape(-1)
+    out = np.zeros((L, 4), dtype=np.uint64)
+    check(lib().sct_base_frequency_host(_ptr(codes), codes.size, L, _ptr(out)))
+    return out
+
+
+def device_count():
+    c = _i32(0)
+    rc = lib().sct_device_count(ctypes.byref(c))
+    return c.value if rc == SCT_OK else 0
+
+
+# ------------------------------------------------------------------ device-pointer plan API
+class AllPairsPlan:
+    """Owns an sct_allpairs_plan over device-resident codes (a torch.uint64/int64 tensor
+    or a raw device pointer).  Used by the benchmark and the sharded driver."""
+
+    def __init__(self, d_codes_ptr, n, code_bits=0):
+        self._lib = lib()
+        self._h = _vp()
+        check(self._lib.sct_allpairs_plan_create(_vp(d_codes_ptr), n, code_bits, ctypes.byref(self._h)))
+        nb, items, pairs = _i32(0), _i64(0), _i64(0)
+        check(self._lib.sct_allpairs_plan_info(self._h, ctypes.byref(nb), ctypes.byref(items), ctypes.byref(pairs)))
+        self.nbins, self.items, self.pairs = nb.value, items.value, pairs.value
+
+    def build(self, stream=0):
+        check(self._lib.sct_allpairs_build(self._h, _vp(stream)))
+
+    def count(self, d_counts_ptr, begin=0, end=None, grid=0, stream=0):
+        end = self.items if end is None else end
+        check(self._lib.sct_allpairs_count(self._h, begin, end, _vp(d_counts_ptr), grid, _vp(stream)))
+
+    def range_pairs(self, begin, end):
+        p = _i64(0)
+        check(self._lib.sct_allpairs_range_pairs(self._h, begin, end, ctypes.byref(p)))
+        return p.value
+
+    def close(self):
+        if self._h:
+            self._lib.sct_allpairs_plan_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,555 @@
+// All-pairs TwoBit Hamming-distance histogram for gfx950 (MI355X).
+//
+// Replaces the O(n^2) pair loop of Barcodes.summarize_hamming_distances
+// (src/sctools/barcode.py:42-43), whose per-pair distance is
+// TwoBit.hamming_distance (src/sctools/encodings.py:113-121): the number of non-zero
+// 2-bit groups of a^b.  The kernel never materialises a distance: it produces, for
+// every pair, the distance's bits as bit-planes and counts them.
+//
+// Data layout
+//   codes  : n uint64 TwoBit codes (plan-owned copy), code < 2^(4*NPP).
+//   table  : [group pair h][nibble pp < NPP][combo c < 16] -> uint4 {s0_a, s1_a, s0_b, s1_b}
+//            for the two 32-code groups a = 2h, b = 2h+1:
+//            bit k of s0/s1 = bit 0/1 of  [base_{2pp}(code_{32g+k}) != c&3] +
+//                                         [base_{2pp+1}(code_{32g+k}) != c>>2]
+//            i.e. for a query whose nibble pp equals c, the 2-bit mismatch count of
+//            positions 2pp, 2pp+1 against all 32 codes of the group, bit-sliced.
+//            One (h, pp) row is 16 x 16 B = one LDS bank row, so the lanes' ds_read_b128
+//            (4 cycles, full LDS rate) never conflict; two groups per read also keeps the
+//            compiler from pairing b64 reads into the half-rate ds_read2st64_b64.
+//   LDS    : one column chunk = CT groups of the table (32 KiB), resident while a
+//            workgroup walks consecutive row blocks of that chunk.
+//
+// Work decomposition
+//   Unordered pairs i<j are covered by items (row block r of RB=256 queries,
+//   column chunk c of CB=32*CT codes), enumerated chunk-major: chunk c holds rows
+//   r < R(c) = ceil((min((c+1)CB, n) - 1) / RB).  A launch counts any item range
+//   [begin, end); each workgroup takes a contiguous sub-range, so it loads a chunk
+//   into LDS once and reuses it for every row block of that chunk it visits.
+//
+// Per (query lane, group of 32 codes):
+//   NPP ds_read_b64 select the lane's {s0,s1} planes (the lane's nibble is the LDS
+//   offset: no VALU work to form mismatches), a carry-save adder tree of v_bitop3
+//   full adders (2 VALU ops each) sums them into B planes d_0..d_{B-1} of the 32
+//   distances, and counts[m] += popcount(AND_{b in m} d_b) for m = 1..2*NPP
+//   (v_bcnt_u32_b32 accumulates in place).  sct_counts_to_hist inverts the counts.
+#include <algorithm>
+
+#include "sct_common.h"
+
+namespace {
+
+constexpr int RB = 256;  // rows (queries) per item == workgroup size
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+
+// c += popcount(x) as ONE v_bcnt_u32_b32 (the compiler otherwise re-associates two
+// groups' counts into bcnt + bcnt + v_add3, one extra VALU op per pair of counts).
+__device__ __forceinline__ void bcnt_acc(uint32_t& c, uint32_t x) {
+  asm("v_bcnt_u32_b32 %0, %1, %0" : "+v"(c) : "v"(x));
+}
+
+constexpr int bitlen(int v) {
+  int b = 0;
+  while ((1 << b) <= v) ++b;
+  return b;
+}
+
+template <int NPP>
+struct Geom {
+  static constexpr int G = 2 * NPP;         // max distance
+  static constexpr int B = bitlen(G);       // distance bit-planes
+  static constexpr int CT = NPP <= 8 ? 32 : 16;  // groups per column chunk
+  static constexpr int CB = 32 * CT;        // codes per column chunk
+  static constexpr int K = CB / RB;         // row blocks per chunk step
+  static constexpr int TILE = CT / 2 * NPP * 16;  // uint4 entries per chunk (32 KiB at NPP 8/16)
+};
+
+// Reduce N equal-weight planes to one; writes N/2 carries (next weight).
+template <int N>
+__device__ __forceinline__ uint32_t reduce_col(const uint32_t* in, uint32_t* carry) {
+  uint32_t acc = in[0];
+  int c = 0;
+#pragma unroll
+  for (int k = 1; k + 1 < N; k += 2) {
+    const uint32_t b = in[k], e = in[k + 1];
+    carry[c++] = maj3(acc, b, e);
+    acc = xor3(acc, b, e);
+  }
+  if constexpr (N >= 2 && (N % 2) == 0) {
+    const uint32_t b = in[N - 1];
+    carry[c++] = acc & b;
+    acc ^= b;
+  }
+  return acc;
+}
+
+template <int W, int N, int B>
+__device__ __forceinline__ void reduce_upper(const uint32_t* in, uint32_t (&d)[B]) {
+  if constexpr (W < B) {
+    if constexpr (N == 0) {
+      d[W] = 0;
+      reduce_upper<W + 1, 0, B>(in, d);
+    } else {
+      constexpr int NC = N / 2;
+      uint32_t carry[NC > 0 ? NC : 1];
+      d[W] = reduce_col<N>(in, carry);
+      reduce_upper<W + 1, NC, B>(carry, d);
+    }
+  }
+  // carries beyond plane B-1 are provably zero (sum <= 2*NPP < 2^B) and are dropped
+}
+
+// Sum NPP 2-bit numbers {s1,s0} into B bit-planes d.
+template <int NPP, int B>
+__device__ __forceinline__ void adder_tree(const uint32_t (&s0)[NPP], const uint32_t (&s1)[NPP],
+                                           uint32_t (&d)[B]) {
+  constexpr int C0 = NPP / 2;
+  uint32_t c0[C0 > 0 ? C0 : 1];
+  d[0] = reduce_col<NPP>(s0, c0);
+  constexpr int N1 = NPP + C0;
+  uint32_t col1[N1];
+#pragma unroll
+  for (int k = 0; k < NPP; ++k) col1[k] = s1[k];
+#pragma unroll
+  for (int k = 0; k < C0; ++k) col1[NPP + k] = c0[k];
+  reduce_upper<1, N1, B>(col1, d);
+}
+
+// cnt[m-1] += popcount(AND of planes in m), m = 1..G
+template <int G, int B>
+__device__ __forceinline__ void count_subsets(const uint32_t (&d)[B], uint32_t (&cnt)[G]) {
+  uint32_t P[G + 1];
+#pragma unroll
+  for (int m = 1; m <= G; ++m) {
+    const int low = m & (-m);
+    const int lb = __builtin_ctz(m);
+    const int rest = m ^ low;
+    P[m] = rest ? (P[rest] & d[lb]) : d[lb];
+    bcnt_acc(cnt[m - 1], P[m]);
+  }
+}
+
+struct ItemCursor {
+  int64_t c, r;
+};
+
+// items of chunk c (c < nchunks-1): (c+1)*K; prefix P(c) = K*c*(c+1)/2
+__device__ __forceinline__ ItemCursor locate_item(int64_t t, int64_t K, int64_t nchunks) {
+  double x = sqrt(8.0 * (double)t / (double)K + 1.0);
+  int64_t c = (int64_t)((x - 1.0) * 0.5);
+  if (c > nchunks - 1) c = nchunks - 1;
+  if (c < 0) c = 0;
+  while (c > 0 && K * c * (c + 1) / 2 > t) --c;
+  while (c < nchunks - 1 && K * (c + 1) * (c + 2) / 2 <= t) ++c;
+  return {c, t - K * c * (c + 1) / 2};
+}
+
+// valid-pair mask of the 32 codes j0..j0+31 for row i: i < j < n (and i < n)
+__device__ __forceinline__ uint32_t pair_mask(int64_t i, int64_t jg, int64_t n) {
+  int64_t lo = i + 1 - jg, hi = n - jg;
+  lo = lo < 0 ? 0 : (lo > 32 ? 32 : lo);
+  hi = hi < 0 ? 0 : (hi > 32 ? 32 : hi);
+  uint32_t mask = (uint32_t)(((1ull << hi) - 1ull) & ~((1ull << lo) - 1ull));
+  return i < n ? mask : 0u;
+}
+
+template <int NPP, bool MASKED>
+__device__ __forceinline__ void one_group(const uint32_t (&s0)[NPP], const uint32_t (&s1)[NPP],
+                                          int64_t i, int64_t jg, int64_t n,
+                                          uint32_t (&cnt)[2 * NPP], uint32_t& cnt0) {
+  constexpr int B = Geom<NPP>::B;
+  uint32_t d[B];
+  adder_tree<NPP, B>(s0, s1, d);
+  if constexpr (MASKED) {
+    const uint32_t mask = pair_mask(i, jg, n);
+#pragma unroll
+    for (int b = 0; b < B; ++b) d[b] &= mask;
+    cnt0 += __popc(mask);
+  }
+  count_subsets<2 * NPP, B>(d, cnt);
+}
+
+template <int NPP, bool MASKED>
+__device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uint64_t q, int64_t i,
+                                             int64_t j0, int64_t n, uint32_t (&cnt)[2 * NPP],
+                                             uint32_t& cnt0) {
+  using Gm = Geom<NPP>;
+  int off[NPP];
+#pragma unroll
+  for (int pp = 0; pp < NPP; ++pp) off[pp] = pp * 16 + (int)((q >> (4 * pp)) & 15u);
+
+#pragma unroll 2
+  for (int h = 0; h < Gm::CT / 2; ++h) {
+    uint32_t s0a[NPP], s1a[NPP], s0b[NPP], s1b[NPP];
+#pragma unroll
+    for (int pp = 0; pp < NPP; ++pp) {
+      const uint4 e = tile[h * NPP * 16 + off[pp]];
+      s0a[pp] = e.x;
+      s1a[pp] = e.y;
+      s0b[pp] = e.z;
+      s1b[pp] = e.w;
+    }
+    one_group<NPP, MASKED>(s0a, s1a, i, j0 + 64 * h, n, cnt, cnt0);
+    one_group<NPP, MASKED>(s0b, s1b, i, j0 + 64 * h + 32, n, cnt, cnt0);
+  }
+  if constexpr (!MASKED) cnt0 += Gm::CB;
+}
+
+template <int NPP>
+__global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __restrict__ codes,
+                                                            const uint4* __restrict__ table,
+                                                            int64_t n, int64_t nchunks,
+                                                            int64_t item_begin, int64_t item_end,
+                                                            unsigned long long* __restrict__ out) {
+  using Gm = Geom<NPP>;
+  constexpr int G = Gm::G;
+  __shared__ __attribute__((aligned(16))) uint4 tile[Gm::TILE];
+
+  const int tid = threadIdx.x;
+  const int64_t total = item_end - item_begin;
+  const int64_t t0 = item_begin + total * (int64_t)blockIdx.x / gridDim.x;
+  const int64_t t1 = item_begin + total * (int64_t)(blockIdx.x + 1) / gridDim.x;
+
+  uint32_t cnt[G];
+#pragma unroll
+  for (int m = 0; m < G; ++m) cnt[m] = 0;
+  uint32_t cnt0 = 0;
+
+  if (t0 < t1) {
+    ItemCursor cur = locate_item(t0, Gm::K, nchunks);
+    int64_t loaded = -1;
+    const int64_t last_rows = ((n - 1) + RB - 1) / RB;  // R(last chunk)
+    for (int64_t t = t0; t < t1; ++t) {
+      const int64_t c = cur.c, r = cur.r;
+      if (c != loaded) {
+        __syncthreads();  // previous chunk no longer read
+        const uint4* src = table + c * Gm::TILE;
+#pragma unroll
+        for (int k = tid; k < Gm::TILE; k += RB) tile[k] = src[k];
+        __syncthreads();
+        loaded = c;
+      }
+      const int64_t i = r * RB + tid;
+      const uint64_t q = i < n ? codes[i] : 0ull;
+      const int64_t j0 = c * Gm::CB;
+      const bool masked = ((r + 1) * RB > j0) || (j0 + Gm::CB > n);
+      if (masked)
+        process_item<NPP, true>(tile, q, i, j0, n, cnt, cnt0);
+      else
+        process_item<NPP, false>(tile, q, i, j0, n, cnt, cnt0);
+      // advance the cursor
+      const int64_t rows_c = (c == nchunks - 1) ? last_rows : (c + 1) * Gm::K;
+      if (++cur.r >= rows_c) {
+        cur.c += 1;
+        cur.r = 0;
+      }
+    }
+  }
+
+  // ---- workgroup reduction: wave butterfly (DPP/swizzle lowering of shfl_xor), LDS, atomics
+  __syncthreads();
+  unsigned long long* red = reinterpret_cast<unsigned long long*>(tile);  // [RB/64][G+1]
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int m = 0; m <= G; ++m) {
+    unsigned long long v = (m == 0) ? cnt0 : cnt[m - 1];
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s, 64);
+    if (lane == 0) red[wave * (G + 1) + m] = v;
+  }
+  __syncthreads();
+  if (tid <= G) {
+    unsigned long long s = 0;
+#pragma unroll
+    for (int w = 0; w < RB / 64; ++w) s += red[w * (G + 1) + tid];
+    if (s) atomicAdd(out + tid, s);
+  }
+}
+
+// table[h][pp][c] = bit-sliced 2-bit mismatch counts of nibble pp of the 64 codes of
+// group pair h against combo c (see file header).  One thread per entry.
+__global__ void allpairs_build_kernel(const uint64_t* __restrict__ codes, int64_t n, int npp,
+                                      int64_t entries, uint4* __restrict__ table) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= entries) return;
+  const int c = (int)(idx & 15);
+  const int pp = (int)((idx >> 4) % npp);
+  const int64_t h = (idx >> 4) / npp;
+  uint32_t s[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) {
+      const int64_t j = h * 64 + half * 32 + k;
+      const uint64_t code = j < n ? codes[j] : 0ull;
+      const uint32_t x = (uint32_t)((code >> (4 * pp)) & 15u) ^ (uint32_t)c;
+      const uint32_t m0 = (x & 3u) != 0u, m1 = (x >> 2) != 0u;
+      s[2 * half] |= (m0 ^ m1) << k;
+      s[2 * half + 1] |= (m0 & m1) << k;
+    }
+  }
+  table[idx] = make_uint4(s[0], s[1], s[2], s[3]);
+}
+
+__global__ void or_reduce_kernel(const uint64_t* __restrict__ codes, int64_t n,
+                                 unsigned long long* out) {
+  unsigned long long v = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    v |= codes[i];
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) v |= __shfl_xor(v, s, 64);
+  if ((threadIdx.x & 63) == 0 && v) atomicOr(out, v);
+}
+
+int ct_for(int npp) { return npp <= 8 ? 32 : 16; }
+
+}  // namespace
+
+struct sct_allpairs_plan {
+  int device = 0;
+  int64_t n = 0;
+  int code_bits = 0;
+  int npp = 0;
+  int nbins = 0;
+  int ct = 0;
+  int64_t cb = 0;
+  int64_t nchunks = 0;
+  int64_t items = 0;
+  int grid = 0;
+  uint64_t* d_codes = nullptr;
+  uint4* d_table = nullptr;
+  int64_t table_entries = 0;
+};
+
+namespace {
+
+int64_t rows_of_chunk(const sct_allpairs_plan* p, int64_t c) {
+  const int64_t maxj = std::min<int64_t>((c + 1) * p->cb, p->n) - 1;
+  return maxj <= 0 ? 0 : (maxj + RB - 1) / RB;
+}
+
+template <int NPP>
+int launch_count(sct_allpairs_plan* p, int64_t b, int64_t e, uint64_t* d_counts, int grid,
+                 hipStream_t s) {
+  if (grid <= 0) grid = p->grid;
+  const int64_t total = e - b;
+  if (grid > total) grid = (int)total;
+  // per-lane u32 counters: at most ceil(items/grid) items of CB pairs per lane
+  if ((double)sct::ceil_div(total, grid) * Geom<NPP>::CB >= 4.0e9)
+    return sct::fail(SCT_E_RANGE, "too many items per workgroup for 32-bit lane counters; raise grid");
+  hipLaunchKernelGGL(allpairs_count_kernel<NPP>, dim3(grid), dim3(RB), 0, s, p->d_codes, p->d_table,
+                     p->n, p->nchunks, b, e, reinterpret_cast<unsigned long long*>(d_counts));
+  SCT_LAUNCH_CHECK();
+  return SCT_OK;
+}
+
+template <int NPP>
+int occupancy_grid(int cus) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, allpairs_count_kernel<NPP>, RB, 0) !=
+          hipSuccess ||
+      per_cu <= 0)
+    per_cu = 4;
+  return cus * per_cu;
+}
+
+#define SCT_NPP_SWITCH(npp, FN, ...)     \
+  switch (npp) {                         \
+    case 1: return FN<1>(__VA_ARGS__);   \
+    case 2: return FN<2>(__VA_ARGS__);   \
+    case 3: return FN<3>(__VA_ARGS__);   \
+    case 4: return FN<4>(__VA_ARGS__);   \
+    case 5: return FN<5>(__VA_ARGS__);   \
+    case 6: return FN<6>(__VA_ARGS__);   \
+    case 7: return FN<7>(__VA_ARGS__);   \
+    case 8: return FN<8>(__VA_ARGS__);   \
+    case 9: return FN<9>(__VA_ARGS__);   \
+    case 10: return FN<10>(__VA_ARGS__); \
+    case 11: return FN<11>(__VA_ARGS__); \
+    case 12: return FN<12>(__VA_ARGS__); \
+    case 13: return FN<13>(__VA_ARGS__); \
+    case 14: return FN<14>(__VA_ARGS__); \
+    case 15: return FN<15>(__VA_ARGS__); \
+    case 16: return FN<16>(__VA_ARGS__); \
+    default: break;                      \
+  }
+
+int grid_for(int npp, int cus) {
+  SCT_NPP_SWITCH(npp, occupancy_grid, cus);
+  return cus * 4;
+}
+
+int dispatch_count(sct_allpairs_plan* p, int64_t b, int64_t e, uint64_t* d, int grid,
+                   hipStream_t s) {
+  SCT_NPP_SWITCH(p->npp, launch_count, p, b, e, d, grid, s);
+  return sct::fail(SCT_E_RANGE, "unsupported npp %d", p->npp);
+}
+
+}  // namespace
+
+extern "C" int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int code_bits,
+                                        sct_allpairs_plan** plan) {
+  SCT_CHECK(plan != nullptr, "plan is NULL");
+  *plan = nullptr;
+  SCT_CHECK(n >= 0, "n must be >= 0");
+  SCT_CHECK(n == 0 || d_codes != nullptr, "codes is NULL");
+  SCT_CHECK(code_bits <= 64, "code_bits %d > 64: codes wider than 64 bits are not supported",
+            code_bits);
+  auto* p = new sct_allpairs_plan();
+  auto cleanup = [&](int rc) {
+    sct_allpairs_plan_destroy(p);
+    return rc;
+  };
+  hipError_t e = hipGetDevice(&p->device);
+  if (e != hipSuccess) return cleanup(sct::fail(SCT_E_HIP, "hipGetDevice: %s", hipGetErrorString(e)));
+  p->n = n;
+  unsigned long long orv = 0;
+  if (n > 0) {
+    e = hipMalloc(&p->d_codes, (size_t)n * 8);
+    if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "hipMalloc codes: %s", hipGetErrorString(e)));
+    e = hipMemcpy(p->d_codes, d_codes, (size_t)n * 8, hipMemcpyDefault);
+    if (e != hipSuccess) return cleanup(sct::fail(SCT_E_HIP, "copy codes: %s", hipGetErrorString(e)));
+    unsigned long long* d_or = nullptr;
+    e = hipMalloc(&d_or, 8);
+    if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "hipMalloc: %s", hipGetErrorString(e)));
+    (void)hipMemset(d_or, 0, 8);
+    const int blocks = (int)std::min<int64_t>(1024, sct::ceil_div(n, 256));
+    hipLaunchKernelGGL(or_reduce_kernel, dim3(blocks), dim3(256), 0, 0, p->d_codes, n, d_or);
+    e = hipMemcpy(&orv, d_or, 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d_or);
+    if (e != hipSuccess) return cleanup(sct::fail(SCT_E_HIP, "or-reduce: %s", hipGetErrorString(e)));
+  }
+  int need = 0;
+  while (need < 64 && (orv >> need)) ++need;
+  if (code_bits <= 0) code_bits = need;
+  if (need > code_bits)
+    return cleanup(sct::fail(SCT_E_RANGE, "a code needs %d bits but code_bits=%d", need, code_bits));
+  if (code_bits < 1) code_bits = 1;
+  p->code_bits = code_bits;
+  p->npp = (code_bits + 3) / 4;
+  p->nbins = 2 * p->npp + 1;
+  p->ct = ct_for(p->npp);
+  p->cb = 32LL * p->ct;
+  p->nchunks = n > 0 ? sct::ceil_div(n, p->cb) : 0;
+  p->items = 0;
+  if (n >= 2) {
+    const int64_t K = p->cb / RB;
+    const int64_t last = p->nchunks - 1;
+    p->items = K * last * (last + 1) / 2 + rows_of_chunk(p, last);
+  }
+  p->table_entries = p->nchunks * (p->ct / 2) * (int64_t)p->npp * 16;
+  if (p->table_entries > 0) {
+    e = hipMalloc(&p->d_table, (size_t)p->table_entries * sizeof(uint4));
+    if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "hipMalloc table: %s", hipGetErrorString(e)));
+  }
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  p->grid = grid_for(p->npp, cus);
+  *plan = p;
+  return SCT_OK;
+}
+
+extern "C" int sct_allpairs_plan_destroy(sct_allpairs_plan* plan) {
+  if (!plan) return SCT_OK;
+  if (plan->d_codes) (void)hipFree(plan->d_codes);
+  if (plan->d_table) (void)hipFree(plan->d_table);
+  delete plan;
+  return SCT_OK;
+}
+
+extern "C" int sct_allpairs_plan_info(const sct_allpairs_plan* plan, int* nbins, int64_t* items,
+                                      int64_t* pairs) {
+  SCT_CHECK(plan != nullptr, "plan is NULL");
+  if (nbins) *nbins = plan->nbins;
+  if (items) *items = plan->items;
+  if (pairs) *pairs = plan->n * (plan->n - 1) / 2;
+  return SCT_OK;
+}
+
+extern "C" int sct_allpairs_build(sct_allpairs_plan* plan, void* stream) {
+  SCT_CHECK(plan != nullptr, "plan is NULL");
+  if (plan->table_entries == 0) return SCT_OK;
+  const int64_t blocks = sct::ceil_div(plan->table_entries, 256);
+  hipLaunchKernelGGL(allpairs_build_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     sct::as_stream(stream), plan->d_codes, plan->n, plan->npp,
+                     plan->table_entries, plan->d_table);
+  SCT_LAUNCH_CHECK();
+  return SCT_OK;
+}
+
+extern "C" int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
+                                  uint64_t* d_counts, int grid, void* stream) {
+  SCT_CHECK(plan != nullptr, "plan is NULL");
+  SCT_CHECK(d_counts != nullptr, "counts is NULL");
+  SCT_CHECK(0 <= item_begin && item_begin <= item_end && item_end <= plan->items,
+            "item range [%lld, %lld) outside [0, %lld)", (long long)item_begin,
+            (long long)item_end, (long long)plan->items);
+  if (item_begin == item_end) return SCT_OK;
+  return dispatch_count(plan, item_begin, item_end, d_counts, grid, sct::as_stream(stream));
+}
+
+extern "C" int sct_allpairs_range_pairs(const sct_allpairs_plan* plan, int64_t item_begin,
+                                        int64_t item_end, int64_t* pairs) {
+  SCT_CHECK(plan != nullptr && pairs != nullptr, "NULL pointer");
+  SCT_CHECK(0 <= item_begin && item_begin <= item_end && item_end <= plan->items,
+            "item range outside the plan");
+  const int64_t n = plan->n;
+  int64_t total = 0, c = 0, base = 0;
+  while (c < plan->nchunks && base + rows_of_chunk(plan, c) <= item_begin) base += rows_of_chunk(plan, c++);
+  int64_t r = item_begin - base;
+  for (int64_t t = item_begin; t < item_end; ++t) {
+    // pairs of item (c, r) = #{(i, j): i in row block r, j in chunk c, i < j < n}
+    const int64_t jlo = c * plan->cb, jhi = std::min<int64_t>((c + 1) * plan->cb, n);
+    const int64_t ilo = r * RB, ihi = std::min<int64_t>((r + 1) * RB, n);
+    const int64_t a_hi = std::min(ihi, jlo);  // rows i < jlo see the whole chunk
+    if (a_hi > ilo) total += (a_hi - ilo) * (jhi - jlo);
+    const int64_t b_lo = std::max(ilo, jlo), b_hi = std::min(ihi, jhi - 1);  // i in chunk: jhi-1-i
+    if (b_hi > b_lo) total += (b_hi - b_lo) * (2 * jhi - 1 - b_lo - b_hi) / 2;
+    if (++r >= rows_of_chunk(plan, c)) {
+      ++c;
+      r = 0;
+    }
+  }
+  *pairs = total;
+  return SCT_OK;
+}
+
+extern "C" int sct_hamming_hist_allpairs_host(const uint64_t* codes, int64_t n, int code_bits,
+                                              uint64_t* hist, int nbins) {
+  SCT_CHECK(hist != nullptr, "hist is NULL");
+  SCT_CHECK(n >= 0 && (n == 0 || codes != nullptr), "bad codes");
+  sct::DevBuf dcodes, dcounts;
+  SCT_HIP(dcodes.alloc((size_t)n * 8));
+  if (n) SCT_HIP(hipMemcpy(dcodes.p, codes, (size_t)n * 8, hipMemcpyHostToDevice));
+  sct_allpairs_plan* plan = nullptr;
+  int rc = sct_allpairs_plan_create((const uint64_t*)dcodes.p, n, code_bits, &plan);
+  if (rc != SCT_OK) return rc;
+  struct Guard {
+    sct_allpairs_plan* p;
+    ~Guard() { sct_allpairs_plan_destroy(p); }
+  } guard{plan};
+  if (plan->nbins != nbins)
+    return sct::fail(SCT_E_INVALID, "hist holds %d bins, plan needs %d", nbins, plan->nbins);
+  SCT_HIP(dcounts.alloc((size_t)nbins * 8));
+  SCT_HIP(hipMemset(dcounts.p, 0, (size_t)nbins * 8));
+  rc = sct_allpairs_build(plan, nullptr);
+  if (rc != SCT_OK) return rc;
+  rc = sct_allpairs_count(plan, 0, plan->items, (uint64_t*)dcounts.p, 0, nullptr);
+  if (rc != SCT_OK) return rc;
+  uint64_t counts[129];
+  SCT_HIP(hipMemcpy(counts, dcounts.p, (size_t)nbins * 8, hipMemcpyDeviceToHost));
+  const int64_t expect = n * (n - 1) / 2;
+  if ((int64_t)counts[0] != (n >= 2 ? expect : 0))
+    return sct::fail(SCT_E_HIP, "pair count mismatch: counted %llu, expected %lld",
+                     (unsigned long long)counts[0], (long long)expect);
+  return sct_counts_to_hist(counts, nbins, hist);
+}

@@ -1,0 +1,447 @@
+// Element-wise encoding kernels for gfx950: encode (TwoBit/ThreeBit + GC + flags),
+// decode, gc_content and pairwise Hamming distance.  All are one-record-per-lane,
+// HBM-bound streaming kernels; the byte->code map is a 256-entry LDS table.
+//
+// Reference semantics (src/sctools/encodings.py):
+//   TwoBit map      :53-69   A/a 0, C/c 1, T/t 2, G/g 3; IUPAC ambiguity -> random
+//                            (flagged here, drawn by the Python caller in order);
+//                            anything else -> KeyError (flagged here)
+//   TwoBit.encode   :75-88   MSB-first, 2 bits per byte
+//   TwoBit.decode   :90-100  exactly L bases from the LSB upward
+//   TwoBit.gc       :102-111 low bit of each of the L groups
+//   TwoBit.hamming  :113-121 non-zero 2-bit groups of a^b
+//   ThreeBit map    :139-149 C 1, A 2, G 3, T 4, N 6, any other byte -> 6
+//   ThreeBit.encode :155-167 MSB-first, 3 bits per byte
+//   ThreeBit.decode :169-180 triplets up to the top non-zero one; 0/5/7 -> KeyError
+//   ThreeBit.gc     :182-192 bit 0 of every triplet
+//   ThreeBit.hamming:194-202 non-zero 3-bit groups of a^b
+#include <algorithm>
+
+#include "sct_common.h"
+
+namespace {
+
+constexpr int WG = 256;
+constexpr uint8_t F_AMBIG = 0x40, F_INVALID = 0x80;
+
+// LUT entry: low 3 bits = code, 0x40 = IUPAC ambiguous (TwoBit), 0x80 = invalid (TwoBit)
+__host__ __device__ inline uint8_t lut_entry(int kind, int c) {
+  if (kind == 2) {
+    switch (c) {
+      case 'A': case 'a': return 0;
+      case 'C': case 'c': return 1;
+      case 'T': case 't': return 2;
+      case 'G': case 'g': return 3;
+      case 'M': case 'R': case 'W': case 'S': case 'Y': case 'K': case 'V': case 'H': case 'D':
+      case 'B': case 'N': case 'm': case 'r': case 'w': case 's': case 'y': case 'k': case 'v':
+      case 'h': case 'd': case 'b': case 'n':
+        return F_AMBIG;
+      default: return F_INVALID;
+    }
+  }
+  switch (c) {
+    case 'C': case 'c': return 1;
+    case 'A': case 'a': return 2;
+    case 'G': case 'g': return 3;
+    case 'T': case 't': return 4;
+    default: return 6;  // N/n and every other byte
+  }
+}
+
+__device__ __forceinline__ void fill_lut(uint8_t* lut, int kind) {
+  for (int c = threadIdx.x; c < 256; c += blockDim.x) lut[c] = lut_entry(kind, c);
+  __syncthreads();
+}
+
+// Read byte p of a record either through aligned dwords or bytes.
+struct RecordReader {
+  const uint8_t* rec;
+  bool dw;
+  uint32_t cache;
+  int cache_k;
+  __device__ __forceinline__ uint32_t byte(int p) {
+    if (dw) {
+      const int k = p >> 2;
+      if (k != cache_k) {
+        cache = *reinterpret_cast<const uint32_t*>(rec + 4 * k);
+        cache_k = k;
+      }
+      return (cache >> (8 * (p & 3))) & 0xFFu;
+    }
+    return rec[p];
+  }
+};
+
+__global__ __launch_bounds__(WG) void encode_kernel(int kind, const uint8_t* __restrict__ seqs,
+                                                    int64_t n, int64_t stride, int L, int words,
+                                                    bool dword_path, uint64_t* __restrict__ codes,
+                                                    uint8_t* __restrict__ gc,
+                                                    uint8_t* __restrict__ flags) {
+  __shared__ uint8_t lut[256];
+  fill_lut(lut, kind);
+  const int bits = kind;
+  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
+    RecordReader rd{seqs + r * stride, dword_path, 0u, -1};
+    uint32_t fl = 0;
+    uint64_t* out = codes + r * words;
+    uint32_t g = 0;
+    if (words == 1) {
+      uint64_t code = 0;
+      for (int p = 0; p < L; ++p) {
+        const uint32_t e = lut[rd.byte(p)];
+        code = (code << bits) | (e & 7u);
+        fl |= e;
+      }
+      out[0] = code;
+      const uint64_t m = bits == 2 ? 0x5555555555555555ull : 0x9249249249249249ull;
+      g = __popcll(code & m);
+    } else {
+      // LSB-first over positions so limbs complete in order; a triplet may straddle limbs.
+      uint64_t cur = 0, nxt = 0;
+      int wcur = 0;
+      for (int p = L - 1; p >= 0; --p) {
+        const uint32_t e = lut[rd.byte(p)];
+        fl |= e;
+        const uint64_t v = e & 7u;
+        g += (uint32_t)(v & 1u);
+        const int64_t pos = (int64_t)bits * (L - 1 - p);
+        const int w = (int)(pos >> 6), off = (int)(pos & 63);
+        while (w > wcur) {
+          out[wcur++] = cur;
+          cur = nxt;
+          nxt = 0;
+        }
+        cur |= v << off;
+        if (off + bits > 64) nxt |= v >> (64 - off);
+      }
+      out[wcur++] = cur;
+      if (wcur < words) out[wcur++] = nxt;
+      while (wcur < words) out[wcur++] = 0;
+    }
+    if (gc) gc[r] = (uint8_t)g;
+    if (flags) flags[r] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
+  }
+}
+
+__device__ __forceinline__ uint64_t limb(const uint64_t* w, int words, int i) {
+  return i < words ? w[i] : 0ull;
+}
+
+// value of the `width`-bit group starting at bit `pos` of a multi-limb integer
+__device__ __forceinline__ uint32_t group_at(const uint64_t* w, int words, int64_t pos, int width) {
+  const int i = (int)(pos >> 6), off = (int)(pos & 63);
+  uint64_t v = limb(w, words, i) >> off;
+  if (off + width > 64) v |= limb(w, words, i + 1) << (64 - off);
+  return (uint32_t)(v & ((1u << width) - 1u));
+}
+
+__global__ __launch_bounds__(WG) void decode2_kernel(const uint64_t* __restrict__ codes, int64_t n,
+                                                     int words, int L, uint8_t* __restrict__ out) {
+  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
+    const uint64_t* w = codes + r * words;
+    uint8_t* o = out + r * L;
+    for (int p = 0; p < L; ++p) {
+      const int64_t pos = 2LL * (L - 1 - p);
+      const uint32_t v = pos < 64LL * words ? group_at(w, words, pos, 2) : 0u;
+      o[p] = (uint8_t)("ACTG"[v]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(WG) void decode3_kernel(const uint64_t* __restrict__ codes, int64_t n,
+                                                     int words, int maxlen, uint8_t* __restrict__ out,
+                                                     int32_t* __restrict__ lengths,
+                                                     int32_t* __restrict__ bad) {
+  const int ntrip = (64 * words + 2) / 3;
+  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
+    const uint64_t* w = codes + r * words;
+    int top = -1;
+    for (int t = ntrip - 1; t >= 0; --t)
+      if (group_at(w, words, 3LL * t, 3) != 0u) {
+        top = t;
+        break;
+      }
+    int32_t err = -1;
+    uint8_t* o = out + r * maxlen;
+    for (int t = 0; t <= top; ++t) {
+      const uint32_t v = group_at(w, words, 3LL * t, 3);
+      uint8_t ch = 0;
+      switch (v) {
+        case 1: ch = 'C'; break;
+        case 2: ch = 'A'; break;
+        case 3: ch = 'G'; break;
+        case 4: ch = 'T'; break;
+        case 6: ch = 'N'; break;
+        default:
+          if (err < 0) err = (int32_t)v;
+          break;
+      }
+      o[maxlen - 1 - t] = ch;
+    }
+    lengths[r] = top + 1;
+    bad[r] = err;
+  }
+}
+
+// bit-0-of-each-triplet mask for limb i (64*i mod 3 shifts the pattern)
+__device__ __forceinline__ uint64_t m3(int i) {
+  switch (i % 3) {
+    case 0: return 0x9249249249249249ull;
+    case 1: return 0x4924924924924924ull;
+    default: return 0x2492492492492492ull;
+  }
+}
+
+__global__ __launch_bounds__(WG) void gc_kernel(int kind, const uint64_t* __restrict__ codes,
+                                                int64_t n, int words, int L,
+                                                int32_t* __restrict__ out) {
+  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
+    const uint64_t* w = codes + r * words;
+    int32_t g = 0;
+    for (int i = 0; i < words; ++i) {
+      uint64_t m;
+      if (kind == 2) {
+        const int64_t lo = 64LL * i, rem = 2LL * L - lo;  // bits of the L groups inside this limb
+        if (rem <= 0) break;
+        m = 0x5555555555555555ull;
+        if (rem < 64) m &= (1ull << rem) - 1ull;
+      } else {
+        m = m3(i);
+      }
+      g += __popcll(w[i] & m);
+    }
+    out[r] = g;
+  }
+}
+
+__global__ __launch_bounds__(WG) void hamming_kernel(int kind, const uint64_t* __restrict__ a,
+                                                     const uint64_t* __restrict__ b, int64_t n,
+                                                     int words, int32_t* __restrict__ out) {
+  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
+    const uint64_t* x = a + r * words;
+    const uint64_t* y = b + r * words;
+    int32_t d = 0;
+    if (kind == 2) {
+      for (int i = 0; i < words; ++i) {
+        const uint64_t v = x[i] ^ y[i];
+        d += __popcll((v | (v >> 1)) & 0x5555555555555555ull);
+      }
+    } else {
+      uint64_t v = x[0] ^ y[0];
+      for (int i = 0; i < words; ++i) {
+        const uint64_t nx = i + 1 < words ? (x[i + 1] ^ y[i + 1]) : 0ull;
+        const uint64_t s = v | ((v >> 1) | (nx << 63)) | ((v >> 2) | (nx << 62));
+        d += __popcll(s & m3(i));
+        v = nx;
+      }
+    }
+    out[r] = d;
+  }
+}
+
+// per-position base counts: LDS u32 tallies per workgroup, one u64 atomic per bin
+__global__ __launch_bounds__(WG) void base_frequency_kernel(const uint64_t* __restrict__ codes,
+                                                            int64_t n, int L,
+                                                            unsigned long long* __restrict__ out) {
+  extern __shared__ uint32_t tally[];  // [L][4]
+  for (int k = threadIdx.x; k < 4 * L; k += WG) tally[k] = 0u;
+  __syncthreads();
+  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
+    const uint64_t code = codes[r];
+    for (int p = 0; p < L; ++p) {
+      const int sh = 2 * (L - 1 - p);
+      const uint32_t v = sh < 64 ? (uint32_t)((code >> sh) & 3u) : 0u;
+      atomicAdd(&tally[4 * p + v], 1u);
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 4 * L; k += WG)
+    if (tally[k]) atomicAdd(out + k, (unsigned long long)tally[k]);
+}
+
+unsigned grid_for(int64_t n) {
+  const int64_t b = sct::ceil_div(n, WG);
+  return (unsigned)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+int words_for(int bits, int L) {
+  const int64_t w = sct::ceil_div((int64_t)bits * L, 64);
+  return (int)(w > 0 ? w : 1);
+}
+
+}  // namespace
+
+extern "C" int sct_encode(int kind, const uint8_t* seqs, int64_t n, int64_t stride, int L,
+                          uint64_t* codes, uint8_t* gc, uint8_t* flags, void* stream) {
+  SCT_CHECK(kind == 2 || kind == 3, "kind must be 2 or 3");
+  SCT_CHECK(n >= 0 && L >= 0 && stride >= L, "bad n/L/stride");
+  SCT_CHECK(gc == nullptr || L <= 255, "gc output needs L <= 255");
+  if (n == 0) return SCT_OK;
+  SCT_CHECK(codes != nullptr && (L == 0 || seqs != nullptr), "NULL pointer");
+  const bool dw = (L % 4 == 0) && (stride % 4 == 0) && ((uintptr_t)seqs % 4 == 0);
+  hipLaunchKernelGGL(encode_kernel, dim3(grid_for(n)), dim3(WG), 0, sct::as_stream(stream), kind,
+                     seqs, n, stride, L, words_for(kind, L), dw, codes, gc, flags);
+  SCT_LAUNCH_CHECK();
+  return SCT_OK;
+}
+
+extern "C" int sct_decode2(const uint64_t* codes, int64_t n, int words, int L, uint8_t* out,
+                           void* stream) {
+  SCT_CHECK(n >= 0 && words >= 1 && L >= 0, "bad n/words/L");
+  if (n == 0 || L == 0) return SCT_OK;
+  SCT_CHECK(codes && out, "NULL pointer");
+  hipLaunchKernelGGL(decode2_kernel, dim3(grid_for(n)), dim3(WG), 0, sct::as_stream(stream), codes,
+                     n, words, L, out);
+  SCT_LAUNCH_CHECK();
+  return SCT_OK;
+}
+
+extern "C" int sct_decode3(const uint64_t* codes, int64_t n, int words, int maxlen, uint8_t* out,
+                           int32_t* lengths, int32_t* bad, void* stream) {
+  SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
+  SCT_CHECK(maxlen >= (64 * words + 2) / 3, "maxlen %d < %d", maxlen, (64 * words + 2) / 3);
+  if (n == 0) return SCT_OK;
+  SCT_CHECK(codes && out && lengths && bad, "NULL pointer");
+  hipLaunchKernelGGL(decode3_kernel, dim3(grid_for(n)), dim3(WG), 0, sct::as_stream(stream), codes,
+                     n, words, maxlen, out, lengths, bad);
+  SCT_LAUNCH_CHECK();
+  return SCT_OK;
+}
+
+extern "C" int sct_gc_content(int kind, const uint64_t* codes, int64_t n, int words, int L,
+                              int32_t* out, void* stream) {
+  SCT_CHECK(kind == 2 || kind == 3, "kind must be 2 or 3");
+  SCT_CHECK(n >= 0 && words >= 1 && L >= 0, "bad n/words/L");
+  if (n == 0) return SCT_OK;
+  SCT_CHECK(codes && out, "NULL pointer");
+  hipLaunchKernelGGL(gc_kernel, dim3(grid_for(n)), dim3(WG), 0, sct::as_stream(stream), kind, codes,
+                     n, words, L, out);
+  SCT_LAUNCH_CHECK();
+  return SCT_OK;
+}
+
+extern "C" int sct_hamming_pairs(int kind, const uint64_t* a, const uint64_t* b, int64_t n,
+                                 int words, int32_t* out, void* stream) {
+  SCT_CHECK(kind == 2 || kind == 3, "kind must be 2 or 3");
+  SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
+  if (n == 0) return SCT_OK;
+  SCT_CHECK(a && b && out, "NULL pointer");
+  hipLaunchKernelGGL(hamming_kernel, dim3(grid_for(n)), dim3(WG), 0, sct::as_stream(stream), kind, a,
+                     b, n, words, out);
+  SCT_LAUNCH_CHECK();
+  return SCT_OK;
+}
+
+extern "C" int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint64_t* out,
+                                  void* stream) {
+  SCT_CHECK(n >= 0 && L >= 0 && L <= 1024, "bad n/L");
+  SCT_CHECK(out != nullptr && (n == 0 || codes != nullptr), "NULL pointer");
+  if (L == 0) return SCT_OK;
+  SCT_HIP(hipMemsetAsync(out, 0, (size_t)L * 4 * 8, sct::as_stream(stream)));
+  if (n == 0) return SCT_OK;
+  const unsigned blocks = std::min<unsigned>(grid_for(n), 1024u);
+  hipLaunchKernelGGL(base_frequency_kernel, dim3(blocks), dim3(WG), (size_t)L * 16,
+                     sct::as_stream(stream), codes, n, L, reinterpret_cast<unsigned long long*>(out));
+  SCT_LAUNCH_CHECK();
+  return SCT_OK;
+}
+
+// ---------------------------------------------------------------- host-pointer wrappers
+namespace {
+template <typename T>
+int to_dev(sct::DevBuf& d, const T* h, size_t count) {
+  SCT_HIP(d.alloc(count * sizeof(T)));
+  if (count) SCT_HIP(hipMemcpy(d.p, h, count * sizeof(T), hipMemcpyHostToDevice));
+  return SCT_OK;
+}
+template <typename T>
+int from_dev(T* h, const sct::DevBuf& d, size_t count) {
+  if (count) SCT_HIP(hipMemcpy(h, d.p, count * sizeof(T), hipMemcpyDeviceToHost));
+  return SCT_OK;
+}
+#define SCT_TRY(x)              \
+  do {                          \
+    int rc_ = (x);              \
+    if (rc_ != SCT_OK) return rc_; \
+  } while (0)
+}  // namespace
+
+extern "C" int sct_encode_host(int kind, const uint8_t* seqs, int64_t n, int64_t stride, int L,
+                               uint64_t* codes, uint8_t* gc, uint8_t* flags) {
+  SCT_CHECK(kind == 2 || kind == 3, "kind must be 2 or 3");
+  SCT_CHECK(n >= 0 && L >= 0 && stride >= L, "bad n/L/stride");
+  if (n == 0) return SCT_OK;
+  const int words = words_for(kind, L);
+  sct::DevBuf ds, dc, dg, df;
+  const size_t in_bytes = (size_t)((n - 1) * stride + L);
+  SCT_TRY(to_dev(ds, seqs, in_bytes));
+  SCT_HIP(dc.alloc((size_t)n * words * 8));
+  if (gc) SCT_HIP(dg.alloc((size_t)n));
+  if (flags) SCT_HIP(df.alloc((size_t)n));
+  SCT_TRY(sct_encode(kind, (const uint8_t*)ds.p, n, stride, L, (uint64_t*)dc.p,
+                     gc ? (uint8_t*)dg.p : nullptr, flags ? (uint8_t*)df.p : nullptr, nullptr));
+  SCT_TRY(from_dev(codes, dc, (size_t)n * words));
+  if (gc) SCT_TRY(from_dev(gc, dg, (size_t)n));
+  if (flags) SCT_TRY(from_dev(flags, df, (size_t)n));
+  return SCT_OK;
+}
+
+extern "C" int sct_base_frequency_host(const uint64_t* codes, int64_t n, int L, uint64_t* out) {
+  SCT_CHECK(n >= 0 && L >= 0 && L <= 1024, "bad n/L");
+  if (L == 0) return SCT_OK;
+  sct::DevBuf dc, dout;
+  SCT_TRY(to_dev(dc, codes, (size_t)n));
+  SCT_HIP(dout.alloc((size_t)L * 4 * 8));
+  SCT_TRY(sct_base_frequency((const uint64_t*)dc.p, n, L, (uint64_t*)dout.p, nullptr));
+  return from_dev(out, dout, (size_t)L * 4);
+}
+
+extern "C" int sct_decode2_host(const uint64_t* codes, int64_t n, int words, int L, uint8_t* out) {
+  SCT_CHECK(n >= 0 && words >= 1 && L >= 0, "bad n/words/L");
+  if (n == 0 || L == 0) return SCT_OK;
+  sct::DevBuf dc, dout;
+  SCT_TRY(to_dev(dc, codes, (size_t)n * words));
+  SCT_HIP(dout.alloc((size_t)n * L));
+  SCT_TRY(sct_decode2((const uint64_t*)dc.p, n, words, L, (uint8_t*)dout.p, nullptr));
+  return from_dev(out, dout, (size_t)n * L);
+}
+
+extern "C" int sct_decode3_host(const uint64_t* codes, int64_t n, int words, int maxlen,
+                                uint8_t* out, int32_t* lengths, int32_t* bad) {
+  SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
+  if (n == 0) return SCT_OK;
+  sct::DevBuf dc, dout, dl, db;
+  SCT_TRY(to_dev(dc, codes, (size_t)n * words));
+  SCT_HIP(dout.alloc((size_t)n * maxlen));
+  SCT_HIP(dl.alloc((size_t)n * 4));
+  SCT_HIP(db.alloc((size_t)n * 4));
+  SCT_TRY(sct_decode3((const uint64_t*)dc.p, n, words, maxlen, (uint8_t*)dout.p, (int32_t*)dl.p,
+                      (int32_t*)db.p, nullptr));
+  SCT_TRY(from_dev(out, dout, (size_t)n * maxlen));
+  SCT_TRY(from_dev(lengths, dl, (size_t)n));
+  return from_dev(bad, db, (size_t)n);
+}
+
+extern "C" int sct_gc_content_host(int kind, const uint64_t* codes, int64_t n, int words, int L,
+                                   int32_t* out) {
+  SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
+  if (n == 0) return SCT_OK;
+  sct::DevBuf dc, dout;
+  SCT_TRY(to_dev(dc, codes, (size_t)n * words));
+  SCT_HIP(dout.alloc((size_t)n * 4));
+  SCT_TRY(sct_gc_content(kind, (const uint64_t*)dc.p, n, words, L, (int32_t*)dout.p, nullptr));
+  return from_dev(out, dout, (size_t)n);
+}
+
+extern "C" int sct_hamming_pairs_host(int kind, const uint64_t* a, const uint64_t* b, int64_t n,
+                                      int words, int32_t* out) {
+  SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
+  if (n == 0) return SCT_OK;
+  sct::DevBuf da, db, dout;
+  SCT_TRY(to_dev(da, a, (size_t)n * words));
+  SCT_TRY(to_dev(db, b, (size_t)n * words));
+  SCT_HIP(dout.alloc((size_t)n * 4));
+  SCT_TRY(sct_hamming_pairs(kind, (const uint64_t*)da.p, (const uint64_t*)db.p, n, words,
+                            (int32_t*)dout.p, nullptr));
+  return from_dev(out, dout, (size_t)n);
+}

@@ -1,0 +1,300 @@
+"""Drop-in for ``sctools.encodings`` (src/sctools/encodings.py) on MI355X.
+
+Same classes, attributes and method signatures as the reference; every encode,
+decode, gc_content and hamming_distance call runs as a HIP kernel through
+``libsctools_hip.so`` (scalar methods are batches of one).  Batch methods
+(``*_array``) take and return numpy arrays.
+
+The only host-side step is the reference's own RNG contract: TwoBit draws
+``random.randint(0, 3)`` from the GLOBAL ``random`` module for every IUPAC
+ambiguity code, in record order and left to right (encodings.py:63-69).  The
+kernel encodes such bases as 0 and flags the record; the flagged records are then
+walked here, in order, drawing exactly the numbers the reference would draw (and
+raising its KeyError at the first invalid byte, after the draws that precede it).
+"""
+
+import random
+
+import numpy as np
+
+from . import _lib
+
+__all__ = ["Encoding", "TwoBit", "ThreeBit"]
+
+_AMBIGUOUS = frozenset(b"MRWSYKVHDBNmrwsykvhdbn")  # encodings.py:61
+_VALID2 = {ord("A"): 0, ord("C"): 1, ord("T"): 2, ord("G"): 3,
+           ord("a"): 0, ord("c"): 1, ord("t"): 2, ord("g"): 3}  # encodings.py:58-59
+
+
+def _as_bytes(seq):
+    """bytes-like -> bytes, mirroring what iterating the reference's input yields."""
+    if isinstance(seq, (bytes, bytearray, memoryview)):
+        return bytes(seq)
+    if isinstance(seq, np.ndarray) and seq.dtype == np.uint8:
+        return seq.tobytes()
+    return bytes(seq)  # iterable of ints in [0, 255]
+
+
+def _records(seqs):
+    """Batch input -> (n, L) uint8 array of equal-length records."""
+    if isinstance(seqs, np.ndarray):
+        if seqs.dtype.kind == "S":
+            L = seqs.dtype.itemsize
+            return np.frombuffer(np.ascontiguousarray(seqs).tobytes(), dtype=np.uint8).reshape(-1, L)
+        if seqs.dtype == np.uint8 and seqs.ndim == 2:
+            return np.ascontiguousarray(seqs)
+        raise TypeError("expected an 'S<L>' array or an (n, L) uint8 array")
+    seqs = [_as_bytes(s) for s in seqs]
+    if not seqs:
+        return np.zeros((0, 0), dtype=np.uint8)
+    L = len(seqs[0])
+    if any(len(s) != L for s in seqs):
+        raise ValueError("encode_array needs equal-length records; use encode() per record")
+    return np.frombuffer(b"".join(seqs), dtype=np.uint8).reshape(len(seqs), L)
+
+
+def _fill_ambiguous(recs, codes, gc, flags):
+    """Walk flagged TwoBit records in order: draw random.randint(0,3) per ambiguous
+    byte (encodings.py:69) and raise the reference's KeyError on an invalid one (:68)."""
+    hot = np.flatnonzero(flags)
+    if hot.size == 0:
+        return
+    L = recs.shape[1]
+    words = codes.shape[1]
+    for r in hot.tolist():
+        rec = recs[r]
+        add = 0
+        for p in range(L):
+            byte = int(rec[p])
+            if byte in _VALID2:
+                continue
+            if byte not in _AMBIGUOUS:
+                raise KeyError('%s is not a valid IUPAC nucleotide code' % chr(byte))
+            v = random.randint(0, 3)
+            add |= v << (2 * (L - 1 - p))
+            if gc is not None:
+                gc[r] += v & 1
+        if add:
+            if words == 1:
+                codes[r, 0] |= np.uint64(add)
+            else:
+                full = _lib.limbs_to_ints(codes[r:r + 1])[0] | add
+                codes[r] = _lib.ints_to_limbs([full], words)[0]
+
+
+def _limbs_of(values):
+    """ints / uint64 array -> (n, words) uint64 limbs (rejects negatives)."""
+    if isinstance(values, np.ndarray) and values.dtype.kind in "ui":
+        if values.dtype.kind == "i" and values.size and values.min() < 0:
+            raise ValueError("encoded values must be non-negative")
+        return np.ascontiguousarray(values.astype(np.uint64, copy=False).reshape(values.shape[0], -1))
+    values = [int(v) for v in values]
+    if any(v < 0 for v in values):
+        raise ValueError("encoded values must be non-negative")
+    return _lib.ints_to_limbs(values)
+
+
+class Encoding:
+    """Abstract base class for DNA encodings (encodings.py:4-33)."""
+
+    encoding_map = NotImplemented
+    decoding_map = NotImplemented
+    bits_per_base = NotImplemented
+
+    @classmethod
+    def encode(cls, bytes_encoded):
+        raise NotImplementedError
+
+    def decode(self, integer_encoded):
+        raise NotImplementedError
+
+    def gc_content(self, integer_encoded):
+        raise NotImplementedError
+
+    @staticmethod
+    def hamming_distance(a, b):
+        raise NotImplementedError
+
+
+class TwoBit(Encoding):
+    """2-bit DNA encoding (encodings.py:36-121); ambiguous bases are randomised.
+
+    :param int sequence_length: number of nucleotides that are being encoded
+    """
+
+    def __init__(self, sequence_length):
+        self.sequence_length = sequence_length
+
+    class TwoBitEncodingMap:
+        """Read-only dict look-alike (encodings.py:53-69), kept for API parity."""
+
+        map_ = dict(_VALID2)
+        iupac_ambiguous = set(_AMBIGUOUS)
+
+        def __getitem__(self, byte):
+            try:
+                return self.map_[byte]
+            except KeyError:
+                if byte not in self.iupac_ambiguous:
+                    raise KeyError('%s is not a valid IUPAC nucleotide code' % chr(byte))
+                return random.randint(0, 3)
+
+    encoding_map = TwoBitEncodingMap()
+    decoding_map = {0: b'A', 1: b'C', 2: b'T', 3: b'G'}
+    bits_per_base = 2
+
+    # ------------------------------------------------------------ batch API
+    @classmethod
+    def encode_array(cls, seqs, return_gc=False):
+        """Encode equal-length records -> uint64 codes ((n,) if 2L <= 64 else (n, words)).
+
+        Draws random numbers for ambiguous bases exactly as n calls of encode() would."""
+        recs = _records(seqs)
+        codes, gc, flags = _lib.encode(2, recs, recs.shape[1])
+        _fill_ambiguous(recs, codes, gc, flags)
+        out = codes[:, 0] if codes.shape[1] == 1 else codes
+        return (out, gc) if return_gc else out
+
+    def decode_array(self, codes):
+        """codes -> 'S<L>' array of decoded barcodes (encodings.py:90-100)."""
+        limbs = _limbs_of(codes)
+        raw = _lib.decode2(limbs, self.sequence_length)
+        return raw.view("S%d" % max(1, self.sequence_length)).reshape(-1) if self.sequence_length else \
+            np.array([b""] * limbs.shape[0], dtype="S1")
+
+    def gc_content_array(self, codes):
+        return _lib.gc_content(2, _limbs_of(codes), self.sequence_length)
+
+    @staticmethod
+    def hamming_distance_array(a, b):
+        la, lb = _limbs_of(a), _limbs_of(b)
+        w = max(la.shape[1], lb.shape[1])
+        return _lib.hamming_pairs(2, _pad(la, w), _pad(lb, w))
+
+    # ------------------------------------------------------------ reference API
+    @classmethod
+    def encode(cls, bytes_encoded):
+        """encodings.py:75-88 (batch of one)."""
+        if isinstance(bytes_encoded, str):
+            if not bytes_encoded:
+                return 0
+            # the reference indexes its byte map with a str and then calls chr() on it
+            raise TypeError("'str' object cannot be interpreted as an integer")
+        seq = _as_bytes(bytes_encoded)
+        recs = np.frombuffer(seq, dtype=np.uint8).reshape(1, len(seq))
+        codes, gc, flags = _lib.encode(2, recs, len(seq))
+        _fill_ambiguous(recs, codes, gc, flags)
+        return _lib.limbs_to_ints(codes)[0]
+
+    def decode(self, integer_encoded):
+        """encodings.py:90-100 (batch of one)."""
+        limbs = _limbs_of([integer_encoded])
+        return _lib.decode2(limbs, self.sequence_length)[0].tobytes()
+
+    def gc_content(self, integer_encoded):
+        """encodings.py:102-111 (batch of one)."""
+        return int(_lib.gc_content(2, _limbs_of([integer_encoded]), self.sequence_length)[0])
+
+    @staticmethod
+    def hamming_distance(a, b):
+        """encodings.py:113-121 (batch of one)."""
+        return _hamming1(2, a, b)
+
+
+class ThreeBit(Encoding):
+    """3-bit DNA encoding (encodings.py:124-202); N stays distinct, length is implicit."""
+
+    def __init__(self, *args, **kwargs):
+        pass
+
+    class ThreeBitEncodingMap:
+        """encodings.py:139-149, kept for API parity."""
+
+        map_ = {ord('C'): 1, ord('A'): 2, ord('G'): 3, ord('T'): 4, ord('N'): 6,
+                ord('c'): 1, ord('a'): 2, ord('g'): 3, ord('t'): 4, ord('n'): 6}
+
+        def __getitem__(self, byte):
+            try:
+                return self.map_[byte]
+            except KeyError:
+                return 6
+
+    encoding_map = ThreeBitEncodingMap()
+    decoding_map = {1: b'C', 2: b'A', 3: b'G', 4: b'T', 6: b'N'}
+    bits_per_base = 3
+
+    # ------------------------------------------------------------ batch API
+    @classmethod
+    def encode_array(cls, seqs, return_gc=False):
+        recs = _records(seqs)
+        codes, gc, _ = _lib.encode(3, recs, recs.shape[1])
+        out = codes[:, 0] if codes.shape[1] == 1 else codes
+        return (out, gc) if return_gc else out
+
+    @classmethod
+    def decode_array(cls, codes):
+        """codes -> list of bytes; raises KeyError like the reference on a bad triplet."""
+        out, lengths, bad = _lib.decode3(_limbs_of(codes))
+        res = []
+        w = out.shape[1]
+        for r in range(out.shape[0]):
+            if bad[r] >= 0:
+                raise KeyError(int(bad[r]))
+            res.append(out[r, w - lengths[r]:].tobytes())
+        return res
+
+    @classmethod
+    def gc_content_array(cls, codes):
+        return _lib.gc_content(3, _limbs_of(codes))
+
+    @staticmethod
+    def hamming_distance_array(a, b):
+        la, lb = _limbs_of(a), _limbs_of(b)
+        w = max(la.shape[1], lb.shape[1])
+        return _lib.hamming_pairs(3, _pad(la, w), _pad(lb, w))
+
+    # ------------------------------------------------------------ reference API
+    @classmethod
+    def encode(cls, bytes_encoded):
+        """encodings.py:155-167 (batch of one)."""
+        if isinstance(bytes_encoded, str):
+            # iterating a str yields str characters: none is in the byte map -> all N (6)
+            seq = b"N" * len(bytes_encoded)
+        else:
+            seq = _as_bytes(bytes_encoded)
+        recs = np.frombuffer(seq, dtype=np.uint8).reshape(1, len(seq))
+        codes, _, _ = _lib.encode(3, recs, len(seq))
+        return _lib.limbs_to_ints(codes)[0]
+
+    @classmethod
+    def decode(cls, integer_encoded):
+        """encodings.py:169-180 (batch of one)."""
+        return cls.decode_array([integer_encoded])[0]
+
+    @classmethod
+    def gc_content(cls, integer_encoded):
+        """encodings.py:182-192 (batch of one)."""
+        return int(_lib.gc_content(3, _limbs_of([integer_encoded]))[0])
+
+    @staticmethod
+    def hamming_distance(a, b):
+        """encodings.py:194-202 (batch of one)."""
+        return _hamming1(3, a, b)
+
+
+def _pad(limbs, words):
+    if limbs.shape[1] == words:
+        return limbs
+    out = np.zeros((limbs.shape[0], words), dtype=np.uint64)
+    out[:, :limbs.shape[1]] = limbs
+    return out
+
+
+def _hamming1(kind, a, b):
+    a, b = int(a), int(b)
+    if a < 0 or b < 0:
+        raise ValueError("encoded values must be non-negative")
+    words = _lib.words_for_bits(max(a.bit_length(), b.bit_length()))
+    la = _lib.ints_to_limbs([a], words)
+    lb = _lib.ints_to_limbs([b], words)
+    return int(_lib.hamming_pairs(kind, la, lb)[0])

@@ -1,0 +1,287 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Runs only in the build container, where the read-only reference lives at
+/root/reference. It imports the reference's ``encodings``/``barcode``/``stats``
+modules through a loader shim: a stub ``sctools`` package so
+``__init__.py`` (which needs pysam) never executes, plus the Python-3.10
+``collections.Mapping`` alias that ``barcode.py:2`` needs. Nothing from the
+reference is copied into the repository: only input/output vectors are written.
+
+Usage:  python tests/golden/gen_golden.py [--skip-10k]
+"""
+
+import argparse
+import collections
+import collections.abc
+import importlib
+import itertools
+import json
+import os
+import random
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference/src/sctools"
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from sctools_amd import synthetic  # noqa: E402  (seeded generator, no reference code)
+
+
+def load_reference():
+    if not os.path.isdir(REF):
+        raise SystemExit("reference not present at %s; golden fixtures cannot be regenerated" % REF)
+    collections.Mapping = collections.abc.Mapping  # barcode.py:2 on py3.10
+    pkg = types.ModuleType("sctools")
+    pkg.__path__ = [REF]
+    sys.modules["sctools"] = pkg
+    enc = importlib.import_module("sctools.encodings")
+    bc = importlib.import_module("sctools.barcode")
+    st = importlib.import_module("sctools.stats")
+    return enc, bc, st
+
+
+def exc_record(e):
+    return {"type": type(e).__name__, "args": [a if isinstance(a, (str, int)) else repr(a) for a in e.args]}
+
+
+def fhex(x):
+    return float(x).hex()
+
+
+def summary_record(s):
+    return {k: fhex(v) for k, v in s.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--skip-10k", action="store_true")
+    args = ap.parse_args()
+    enc, bc, st = load_reference()
+    TwoBit, ThreeBit = enc.TwoBit, enc.ThreeBit
+    rng = random.Random(20261015)
+    out = {}
+
+    # ---------------------------------------------------------------- encode
+    alph_ok = b"ACGTacgt"
+    alph_amb = b"MRWSYKVHDBNmrwsykvhdbn"
+    alph_bad = b"PXZ.-\n\r 0uU*\x00\xff\x80E"
+    enc_cases = []
+    # TwoBit: deterministic (no ambiguous bytes) and invalid-byte cases
+    for L in (0, 1, 2, 4, 8, 15, 16, 21, 22, 28, 31, 32, 33, 40, 64, 100):
+        for _ in range(12):
+            seq = bytes(rng.choice(alph_ok) for _ in range(L))
+            rec = {"enc": 2, "seq": seq.hex(), "L": L}
+            rec["code"] = str(TwoBit.encode(seq))
+            enc_cases.append(rec)
+        if L:
+            for _ in range(4):
+                seq = bytearray(rng.choice(alph_ok) for _ in range(L))
+                seq[rng.randrange(L)] = rng.choice(alph_bad)
+                seq = bytes(seq)
+                rec = {"enc": 2, "seq": seq.hex(), "L": L}
+                try:
+                    TwoBit.encode(seq)
+                    raise AssertionError("expected KeyError")
+                except KeyError as e:
+                    rec["error"] = exc_record(e)
+                enc_cases.append(rec)
+    # ThreeBit: any byte allowed
+    for L in (0, 1, 2, 4, 8, 15, 16, 21, 22, 25, 28, 40, 64, 100):
+        for _ in range(16):
+            pool = alph_ok + b"Nn" + alph_amb + alph_bad
+            seq = bytes(rng.choice(pool if rng.random() < 0.2 else alph_ok) for _ in range(L))
+            enc_cases.append({"enc": 3, "seq": seq.hex(), "L": L, "code": str(ThreeBit.encode(seq))})
+    # reference test vectors (test_encodings.py:8-9, 51-59)
+    for s in (b"ACGTTTGAGATGAGATATAGANNNN", b"ACGTP", b"AGCGCGAT"):
+        enc_cases.append({"enc": 3, "seq": s.hex(), "L": len(s), "code": str(ThreeBit.encode(s))})
+    out["encode"] = enc_cases
+
+    # TwoBit ambiguous bytes: random.randint(0,3) on the GLOBAL RNG (encodings.py:69)
+    amb_cases = []
+    for seed in (0, 1, 7, 42, 1234, 99991):
+        random.seed(seed)
+        batch = []
+        for _ in range(20):
+            L = rng.choice((4, 16, 28))
+            seq = bytes(rng.choice(alph_ok + alph_amb) if rng.random() < 0.5 else rng.choice(alph_ok)
+                        for _ in range(L))
+            batch.append(seq)
+        random.seed(seed)
+        codes = [str(TwoBit.encode(s)) for s in batch]
+        after = random.getrandbits(32)
+        amb_cases.append({"seed": seed, "seqs": [s.hex() for s in batch], "codes": codes, "after": after})
+    # an ambiguous prefix followed by an invalid byte: draws happen before the KeyError
+    random.seed(5)
+    batch = [b"NNAC", b"ACGTNRYP", b"ACGT"]
+    random.seed(5)
+    got = []
+    err = None
+    for s in batch:
+        try:
+            got.append(str(TwoBit.encode(s)))
+        except KeyError as e:
+            err = exc_record(e)
+            break
+    amb_cases.append({"seed": 5, "seqs": [s.hex() for s in batch], "codes": got, "error": err,
+                      "after": random.getrandbits(32)})
+    out["encode_ambiguous"] = amb_cases
+
+    # ---------------------------------------------------------------- decode / gc
+    dec2 = []
+    for L in (1, 2, 4, 8, 16, 21, 28, 32, 33, 40):
+        for _ in range(20):
+            code = rng.getrandbits(2 * L)
+            if rng.random() < 0.25:
+                code |= rng.getrandbits(8) << (2 * L)  # bits above 2L are ignored by decode/gc
+            dec2.append({"L": L, "code": str(code), "decoded": TwoBit(L).decode(code).hex(),
+                         "gc": TwoBit(L).gc_content(code)})
+    out["decode2"] = dec2
+    dec3 = []
+    for L in (0, 1, 2, 4, 8, 16, 21, 22, 28, 40):
+        for _ in range(20):
+            seq = bytes(rng.choice(b"ACGTN") for _ in range(L))
+            code = ThreeBit.encode(seq)
+            dec3.append({"code": str(code), "decoded": ThreeBit.decode(code).hex(),
+                         "gc": ThreeBit.gc_content(code)})
+    # invalid triplets (0, 5, 7) below the top non-zero triplet -> KeyError
+    for code in (0b101, 0b111, 0b001_000_010, 0b010_101, 0b100_111_001, 0o12345670, 0o70000):
+        rec = {"code": str(code), "gc": ThreeBit.gc_content(code)}
+        try:
+            rec["decoded"] = ThreeBit.decode(code).hex()
+        except KeyError as e:
+            rec["error"] = exc_record(e)
+        dec3.append(rec)
+    out["decode3"] = dec3
+
+    # ---------------------------------------------------------------- hamming
+    ham = []
+    for _ in range(8000):
+        bits = rng.choice((2, 8, 16, 32, 48, 56, 63, 64, 65, 84, 100, 128))
+        a = rng.getrandbits(bits)
+        if rng.random() < 0.3:  # near neighbours
+            b = a ^ (rng.getrandbits(3) << (rng.randrange(bits)))
+        else:
+            b = rng.getrandbits(rng.choice((bits, max(1, bits // 2))))
+        ham.append([str(a), str(b), TwoBit.hamming_distance(a, b), ThreeBit.hamming_distance(a, b)])
+    out["hamming"] = ham
+
+    # reference test: 7 fixed 4-bp barcodes (test_encodings.py:62-91)
+    simple = [b"ACGT", b"ACGG", b"ACGA", b"ACGC", b"TCGT", b"CCGT", b"GCGT"]
+    out["simple_barcodes"] = {
+        "seqs": [s.hex() for s in simple],
+        "two": [TwoBit.hamming_distance(TwoBit.encode(a), TwoBit.encode(b))
+                for a, b in itertools.combinations(simple, 2)],
+        "three": [ThreeBit.hamming_distance(ThreeBit.encode(a), ThreeBit.encode(b))
+                  for a, b in itertools.combinations(simple, 2)],
+    }
+
+    # ---------------------------------------------------------------- barcode sets
+    wl_path = os.path.join(REF, "test", "data", "1k-august-2016.txt")
+    with open(wl_path, "rb") as f:
+        raw = f.read()
+    bset = bc.Barcodes.from_whitelist(wl_path, 16)
+    keys = list(bset)
+    dists = [TwoBit.hamming_distance(a, b) for a, b in itertools.combinations(keys, 2)]
+    out["whitelist_1k"] = {
+        "codes": [str(k) for k in keys],
+        "hist": np.bincount(dists, minlength=17).tolist(),
+        "summary": summary_record(bset.summarize_hamming_distances()),
+        "base_frequency": bset.base_frequency().tolist(),
+        "effective_diversity": [fhex(x) for x in bset.effective_diversity()],
+    }
+    lines = raw.split(b"\n")[:50]
+    first50 = {}
+    for mode in ("bytes", "strings"):
+        if mode == "bytes":
+            s = bc.Barcodes.from_iterable_bytes([l.strip() for l in lines], barcode_length=16)
+        else:
+            s = bc.Barcodes.from_iterable_strings([l.decode().strip() for l in lines], barcode_length=16)
+        first50[mode] = {"codes": [str(k) for k in s], "summary": summary_record(s.summarize_hamming_distances())}
+    out["first50"] = first50
+    s = bc.Barcodes.from_iterable_encoded([0, 1, 2, 3, 4, 5, 6, 7], barcode_length=2)
+    out["encoded_0_7"] = {"decoded": [encodings_hex for encodings_hex in
+                                      (TwoBit(2).decode(b).hex() for b in s)],
+                          "summary": summary_record(s.summarize_hamming_distances())}
+
+    # small random sets (fractional percentiles, duplicates removed by Counter)
+    small = []
+    for _ in range(3000):
+        n = rng.randint(2, 40)
+        L = rng.randint(1, 16)
+        codes = [rng.getrandbits(2 * L) for _ in range(n)]
+        if rng.random() < 0.1:
+            codes += codes[: rng.randint(1, n)]  # duplicates
+        sset = bc.Barcodes.from_iterable_encoded(codes, barcode_length=L)
+        try:
+            summ = summary_record(sset.summarize_hamming_distances())
+            err = None
+        except Exception as e:  # < 2 unique codes
+            summ, err = None, exc_record(e)
+        small.append({"L": L, "codes": [str(c) for c in codes], "summary": summ, "error": err})
+    # wider codes (ThreeBit-encoded keys are summarised with TwoBit distance, barcode.py:43)
+    for _ in range(200):
+        n = rng.randint(2, 30)
+        L = rng.randint(8, 21)
+        codes = [ThreeBit.encode(bytes(rng.choice(b"ACGTN") for _ in range(L))) for _ in range(n)]
+        sset = bc.Barcodes.from_iterable_encoded(codes, barcode_length=L)
+        try:
+            summ, err = summary_record(sset.summarize_hamming_distances()), None
+        except Exception as e:
+            summ, err = None, exc_record(e)
+        small.append({"L": L, "codes": [str(c) for c in codes], "summary": summ, "error": err})
+    out["small_sets"] = small
+
+    # error behaviour
+    errs = {}
+    try:
+        bc.Barcodes.from_iterable_encoded([5], barcode_length=4).summarize_hamming_distances()
+    except Exception as e:
+        errs["single"] = exc_record(e)
+    try:
+        bc.Barcodes([1, 2, 3], 4)
+    except Exception as e:
+        errs["not_mapping"] = exc_record(e)
+    out["errors"] = errs
+
+    # stats.base4_entropy (stats.py:4-27), reference test vectors + random rows
+    ent = []
+    for row in ([1, 0, 0, 0], [1000, 0, 0, 0], [.25, .25, .25, .25], [20, 20, 20, 20]):
+        ent.append({"x": row, "axis": 0, "out": fhex(st.base4_entropy(row, axis=0))})
+    mat = np.random.default_rng(3).integers(0, 50, size=(16, 4))
+    ent.append({"x": mat.tolist(), "axis": 1, "out": [fhex(v) for v in st.base4_entropy(mat)]})
+    out["entropy"] = ent
+
+    # ThreeBit of real R1 cell barcodes (bases 0:16, platform.py:36), some contain N
+    cbs = []
+    with open(os.path.join(REF, "test", "data", "test_r1.fastq"), "rb") as f:
+        for i, line in enumerate(f):
+            if i % 4 == 1:
+                cb = line[:16]
+                cbs.append([cb.hex(), str(ThreeBit.encode(cb))])
+    out["r1_cell_barcodes"] = cbs
+
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+    print("wrote golden.json")
+
+    # ---------------------------------------------------------------- config 1 (10k)
+    if not args.skip_10k:
+        n, L, seed = synthetic.CONFIGS[1]
+        codes = synthetic.whitelist_codes(n, L, seed)
+        sset = bc.Barcodes.from_iterable_encoded([int(c) for c in codes], barcode_length=L)
+        summ = sset.summarize_hamming_distances()
+        ks = list(sset)
+        hist = np.zeros(17, dtype=np.int64)
+        for a, b in itertools.combinations(ks, 2):
+            hist[TwoBit.hamming_distance(a, b)] += 1
+        with open(os.path.join(HERE, "config1_10k.json"), "w") as f:
+            json.dump({"n": n, "L": L, "seed": seed, "codes_sha_first": [str(int(c)) for c in codes[:8]],
+                       "hist": hist.tolist(), "summary": summary_record(summ)}, f)
+        print("wrote config1_10k.json")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,303 @@
+"""GPU parity: the HIP path (through the C ABI / Python drop-in) against the golden
+fixtures generated from the reference and against the oracle restatement.
+Integer/byte/index work: every comparison is bit-exact."""
+
+import random
+
+import numpy as np
+import pytest
+
+from conftest import fromhex
+from oracle import oracle as O
+from sctools_amd import _lib, barcode, encodings, synthetic
+
+pytestmark = pytest.mark.gpu
+
+TwoBit, ThreeBit = encodings.TwoBit, encodings.ThreeBit
+
+
+# ---------------------------------------------------------------- encodings vs golden
+def test_encode_golden(golden):
+    for rec in golden["encode"]:
+        seq = bytes.fromhex(rec["seq"])
+        enc = TwoBit if rec["enc"] == 2 else ThreeBit
+        if "error" in rec:
+            with pytest.raises(KeyError) as ei:
+                enc.encode(seq)
+            assert list(ei.value.args) == rec["error"]["args"]
+        else:
+            assert enc.encode(seq) == int(rec["code"]), rec
+
+
+def test_encode_array_golden(golden):
+    # batch path: group the deterministic cases by (encoder, length)
+    groups = {}
+    for rec in golden["encode"]:
+        if "error" in rec or rec["L"] == 0:
+            continue
+        groups.setdefault((rec["enc"], rec["L"]), []).append(rec)
+    for (kind, L), recs in groups.items():
+        enc = TwoBit if kind == 2 else ThreeBit
+        seqs = [bytes.fromhex(r["seq"]) for r in recs]
+        codes, gc = enc.encode_array(seqs, return_gc=True)
+        got = _lib.limbs_to_ints(codes.reshape(len(seqs), -1))
+        assert got == [int(r["code"]) for r in recs]
+        if L <= 255:
+            want_gc = [s.upper().count(b"C") + s.upper().count(b"G") for s in seqs]
+            assert gc.tolist() == want_gc
+
+
+def test_two_bit_ambiguous_rng_order(golden):
+    for case in golden["encode_ambiguous"]:
+        random.seed(case["seed"])
+        seqs = [bytes.fromhex(s) for s in case["seqs"]]
+        got = []
+        if case.get("error"):
+            with pytest.raises(KeyError) as ei:
+                for s in seqs:
+                    got.append(str(TwoBit.encode(s)))
+            assert list(ei.value.args) == case["error"]["args"]
+        else:
+            got = [str(TwoBit.encode(s)) for s in seqs]
+        assert got == case["codes"]
+        assert random.getrandbits(32) == case["after"]  # same number of draws
+
+
+def test_two_bit_ambiguous_batch_matches_sequential(golden):
+    for case in golden["encode_ambiguous"]:
+        if case.get("error"):
+            continue
+        seqs = [bytes.fromhex(s) for s in case["seqs"]]
+        by_len = {}
+        for s in seqs:
+            by_len.setdefault(len(s), []).append(s)
+        for L, group in by_len.items():
+            random.seed(case["seed"] + L)
+            seq_codes = [TwoBit.encode(s) for s in group]
+            after_seq = random.getrandbits(32)
+            random.seed(case["seed"] + L)
+            arr = TwoBit.encode_array(group)
+            after_arr = random.getrandbits(32)
+            assert _lib.limbs_to_ints(arr.reshape(len(group), -1)) == seq_codes
+            assert after_seq == after_arr
+
+
+def test_decode_gc_golden(golden):
+    for rec in golden["decode2"]:
+        t = TwoBit(rec["L"])
+        code = int(rec["code"])
+        assert t.decode(code) == bytes.fromhex(rec["decoded"])
+        assert t.gc_content(code) == rec["gc"]
+    for rec in golden["decode3"]:
+        code = int(rec["code"])
+        assert ThreeBit.gc_content(code) == rec["gc"]
+        if "error" in rec:
+            with pytest.raises(KeyError) as ei:
+                ThreeBit.decode(code)
+            assert list(ei.value.args) == rec["error"]["args"]
+        else:
+            assert ThreeBit.decode(code) == bytes.fromhex(rec["decoded"])
+
+
+def test_decode_array_golden(golden):
+    by_L = {}
+    for rec in golden["decode2"]:
+        by_L.setdefault(rec["L"], []).append(rec)
+    for L, recs in by_L.items():
+        codes = _lib.ints_to_limbs([int(r["code"]) for r in recs])
+        t = TwoBit(L)
+        assert [bytes(x) for x in t.decode_array(codes)] == [bytes.fromhex(r["decoded"]) for r in recs]
+        assert t.gc_content_array(codes).tolist() == [r["gc"] for r in recs]
+
+
+def test_hamming_golden(golden):
+    rows = golden["hamming"]
+    for a, b, d2, d3 in rows[:400]:
+        assert TwoBit.hamming_distance(int(a), int(b)) == d2
+        assert ThreeBit.hamming_distance(int(a), int(b)) == d3
+    # batch path over all rows, grouped by limb count
+    a = [int(r[0]) for r in rows]
+    b = [int(r[1]) for r in rows]
+    words = _lib.words_for_bits(max(max(x.bit_length() for x in a), max(x.bit_length() for x in b)))
+    la, lb = _lib.ints_to_limbs(a, words), _lib.ints_to_limbs(b, words)
+    assert TwoBit.hamming_distance_array(la, lb).tolist() == [r[2] for r in rows]
+    assert ThreeBit.hamming_distance_array(la, lb).tolist() == [r[3] for r in rows]
+
+
+def test_reference_simple_barcodes(golden):
+    sb = golden["simple_barcodes"]
+    seqs = [bytes.fromhex(s) for s in sb["seqs"]]
+    import itertools
+    for enc, key in ((TwoBit, "two"), (ThreeBit, "three")):
+        e = enc(4)
+        codes = [e.encode(s) for s in seqs]
+        assert [e.hamming_distance(x, y) for x, y in itertools.combinations(codes, 2)] == sb[key]
+
+
+def test_reference_roundtrips():
+    # test_encodings.py:27-59 on the drop-in
+    seq = b'ACGTTTGAGATGAGATATAGANNNN'
+    t2 = TwoBit(len(seq))
+    assert t2.decode(t2.encode(seq))[:4] == seq[:4]
+    assert ThreeBit.decode(ThreeBit.encode(seq)) == seq
+    s = b'AGCGCGAT'
+    assert t2.gc_content(t2.encode(s)) == s.count(b'C') + s.count(b'G')
+    assert ThreeBit.gc_content(ThreeBit.encode(seq)) == seq.count(b'C') + seq.count(b'G')
+    with pytest.raises(KeyError):
+        t2.encode(b'ACGTP')
+    assert ThreeBit.decode(ThreeBit.encode(b'ACGTP')) == b'ACGTN'
+
+
+# ---------------------------------------------------------------- barcode sets vs golden
+def test_whitelist_1k(golden, tmp_path):
+    wl = golden["whitelist_1k"]
+    codes = [int(c) for c in wl["codes"]]
+    p = tmp_path / "1k.txt"
+    p.write_bytes(b"".join(TwoBit(16).decode(c) + b"\n" for c in codes))
+    bset = barcode.Barcodes.from_whitelist(str(p), 16)
+    assert list(bset) == codes
+    assert bset.hamming_histogram().astype(np.int64).tolist() == wl["hist"]
+    summ = bset.summarize_hamming_distances()
+    assert summ == fromhex(wl["summary"])
+    assert all(isinstance(v, np.float64) for v in summ.values())
+    assert bset.base_frequency().tolist() == wl["base_frequency"]
+    assert [float(x) for x in bset.effective_diversity()] == [float.fromhex(x) for x in wl["effective_diversity"]]
+
+
+def test_first50_and_encoded(golden):
+    for mode, rec in golden["first50"].items():
+        codes = [int(c) for c in rec["codes"]]
+        s = barcode.ObservedBarcodeSet.from_iterable_encoded(codes, 16)
+        assert s.summarize_hamming_distances() == fromhex(rec["summary"])
+        seqs = [TwoBit(16).decode(c) for c in codes]
+        if mode == "bytes":
+            s2 = barcode.Barcodes.from_iterable_bytes(seqs, 16)
+        else:
+            s2 = barcode.Barcodes.from_iterable_strings([x.decode() for x in seqs], 16)
+        assert list(s2) == codes
+    rec = golden["encoded_0_7"]
+    s = barcode.Barcodes.from_iterable_encoded([0, 1, 2, 3, 4, 5, 6, 7], barcode_length=2)
+    assert [TwoBit(2).decode(b).hex() for b in s] == rec["decoded"]
+    assert s.summarize_hamming_distances() == fromhex(rec["summary"])
+
+
+def test_small_sets_summary(golden):
+    for rec in golden["small_sets"]:
+        s = barcode.Barcodes.from_iterable_encoded([int(c) for c in rec["codes"]], rec["L"])
+        if rec["error"]:
+            with pytest.raises(IndexError) as ei:
+                s.summarize_hamming_distances()
+            assert list(ei.value.args) == rec["error"]["args"]
+        else:
+            assert s.summarize_hamming_distances() == fromhex(rec["summary"]), rec
+
+
+def test_errors(golden):
+    with pytest.raises(IndexError):
+        barcode.Barcodes.from_iterable_encoded([5], barcode_length=4).summarize_hamming_distances()
+    with pytest.raises(TypeError) as ei:
+        barcode.Barcodes([1, 2, 3], 4)
+    assert list(ei.value.args) == golden["errors"]["not_mapping"]["args"]
+
+
+def test_config1_10k(golden_10k):
+    n, L, seed = golden_10k["n"], golden_10k["L"], golden_10k["seed"]
+    codes = synthetic.whitelist_codes(n, L, seed)
+    s = barcode.PriorBarcodeSet.from_iterable_encoded(codes.tolist(), L)
+    assert s.hamming_histogram().astype(np.int64).tolist() == golden_10k["hist"]
+    assert s.summarize_hamming_distances() == fromhex(golden_10k["summary"])
+
+
+# ---------------------------------------------------------------- all-pairs kernel vs oracle
+@pytest.mark.parametrize("n", [2, 3, 31, 32, 33, 63, 64, 65, 255, 256, 257, 511, 512, 513,
+                               1023, 1024, 1025, 2047, 2049, 4100])
+def test_allpairs_sizes(n):
+    rng = np.random.default_rng(n)
+    codes = np.unique(rng.integers(0, 2 ** 32, size=n + 64, dtype=np.uint64))[:n]
+    rng.shuffle(codes)
+    hist = _lib.hamming_hist_allpairs(codes, 32)
+    ref = O.c_hist_rows(codes)[: hist.size]
+    assert hist.astype(np.int64).tolist() == ref.tolist()
+    assert int(hist.sum()) == n * (n - 1) // 2
+
+
+@pytest.mark.parametrize("bits", list(range(1, 65)))
+def test_allpairs_code_widths(bits):
+    rng = np.random.default_rng(bits)
+    hi = 2 ** bits
+    n = min(hi, 1500)
+    codes = np.unique(rng.integers(0, hi, size=n, dtype=np.uint64, endpoint=False)) if bits < 64 else \
+        np.unique(rng.integers(0, 2 ** 63, size=n, dtype=np.uint64) * np.uint64(2) + np.uint64(1))
+    hist = _lib.hamming_hist_allpairs(codes)
+    ref = O.c_hist_rows(codes)
+    nb = hist.size
+    assert hist.astype(np.int64).tolist() == ref[:nb].tolist()
+    assert ref[nb:].sum() == 0
+
+
+def test_allpairs_duplicates_and_clusters():
+    # duplicates give distance 0; clustered codes exercise every low bin
+    base = synthetic.whitelist_codes(700, 16, seed=3)
+    near = base ^ (np.uint64(1) << (np.arange(700, dtype=np.uint64) % np.uint64(32)))
+    codes = np.concatenate([base, near, base[:50]])
+    hist = _lib.hamming_hist_allpairs(codes, 32)
+    ref = O.c_hist_rows(codes)[:17]
+    assert hist.astype(np.int64).tolist() == ref.tolist()
+    assert hist[0] >= 50
+
+
+def test_allpairs_shards_sum_to_whole():
+    torch = pytest.importorskip("torch")
+    codes = synthetic.whitelist_codes(20_000, 16, seed=9)
+    d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32)
+    plan.build()
+    full = torch.zeros(plan.nbins, dtype=torch.int64, device="cuda")
+    plan.count(full.data_ptr())
+    parts = torch.zeros(plan.nbins, dtype=torch.int64, device="cuda")
+    cuts = [0, 7, plan.items // 3, plan.items // 2 + 5, plan.items - 1, plan.items]
+    total_pairs = 0
+    for b, e in zip(cuts[:-1], cuts[1:]):
+        one = torch.zeros(plan.nbins, dtype=torch.int64, device="cuda")
+        plan.count(one.data_ptr(), b, e, grid=37)
+        torch.cuda.synchronize()
+        pairs = plan.range_pairs(b, e)
+        ref = np.zeros(65, dtype=np.int64)
+        np_ = np.zeros(1, dtype=np.int64)
+        O.c_oracle().oracle_hist_items(codes.ctypes.data, codes.size, 256, 1024, ref.ctypes.data,
+                                       b, e, np_.ctypes.data, 0)
+        assert int(one[0].item()) == pairs == int(np_[0])
+        hist_one = _lib.counts_to_hist(one.cpu().numpy().view(np.uint64))
+        assert hist_one.astype(np.int64).tolist() == ref[: plan.nbins].tolist()
+        parts += one
+        total_pairs += pairs
+    torch.cuda.synchronize()
+    assert torch.equal(full, parts)
+    assert total_pairs == plan.pairs == codes.size * (codes.size - 1) // 2
+    plan.close()
+
+
+def test_allpairs_737k_properties():
+    """Full config-2 size: size-independent checks + exact parity on a 60k-row prefix."""
+    torch = pytest.importorskip("torch")
+    n, L, seed = synthetic.CONFIGS[2]
+    codes = synthetic.whitelist_codes(n, L, seed)
+    d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 32)
+    plan.build()
+    counts = torch.zeros(plan.nbins, dtype=torch.int64, device="cuda")
+    plan.count(counts.data_ptr())
+    c = counts.cpu().numpy().view(np.uint64)
+    assert int(c[0]) == n * (n - 1) // 2
+    hist = _lib.counts_to_hist(c)
+    assert int(hist.sum()) == n * (n - 1) // 2
+    # twice gives the same (integer atomics are order independent)
+    counts2 = torch.zeros_like(counts)
+    plan.count(counts2.data_ptr(), grid=333)
+    assert torch.equal(counts, counts2)
+    # exact parity on the items that cover rows < 60k against chunk < 60k columns:
+    sub = codes[:60_000]
+    hs = _lib.hamming_hist_allpairs(sub, 32)
+    ref = O.c_hist_rows(sub)[:17]
+    assert hs.astype(np.int64).tolist() == ref.tolist()
+    plan.close()
