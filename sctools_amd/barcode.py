@@ -67,7 +67,11 @@ class Barcodes:
     def hamming_histogram(self):
         """np.uint64 histogram H[d] of TwoBit distances over all unordered pairs."""
         codes = self.codes_array()
-        return _lib.hamming_hist_allpairs(codes)
+        hist = _lib.hamming_hist_allpairs(codes)
+        want = (self._barcode_length + 1) if isinstance(self._barcode_length, int) else 0
+        if want > hist.size:  # bins up to the barcode length, as np.bincount(minlength=L+1)
+            hist = np.concatenate([hist, np.zeros(want - hist.size, dtype=hist.dtype)])
+        return hist
 
     def summarize_hamming_distances(self):
         """returns descriptive statistics on hamming distances between pairs of barcodes

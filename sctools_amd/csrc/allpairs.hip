@@ -33,6 +33,8 @@
 //   full adders (2 VALU ops each) sums them into B planes d_0..d_{B-1} of the 32
 //   distances, and counts[m] += popcount(AND_{b in m} d_b) for m = 1..2*NPP
 //   (v_bcnt_u32_b32 accumulates in place).  sct_counts_to_hist inverts the counts.
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "sct_common.h"
@@ -70,23 +72,29 @@ struct Geom {
   static constexpr int TILE = CT / 2 * NPP * 16;  // uint4 entries per chunk (32 KiB at NPP 8/16)
 };
 
-// Reduce N equal-weight planes to one; writes N/2 carries (next weight).
+// Reduce N equal-weight planes to one; writes N/2 carries (next weight).  Balanced
+// (Wallace) order: each level compresses every disjoint triple with a full adder in
+// parallel, so the dependent depth is ~log_{3/2}(N) levels instead of N/2.  Same
+// op count as a linear chain: floor((N-1)/2) full adders + one half adder if N even.
 template <int N>
 __device__ __forceinline__ uint32_t reduce_col(const uint32_t* in, uint32_t* carry) {
-  uint32_t acc = in[0];
-  int c = 0;
+  if constexpr (N == 1) {
+    return in[0];
+  } else if constexpr (N == 2) {
+    carry[0] = in[0] & in[1];
+    return in[0] ^ in[1];
+  } else {
+    constexpr int T = N / 3, R = N % 3;
+    uint32_t next[T + R];
 #pragma unroll
-  for (int k = 1; k + 1 < N; k += 2) {
-    const uint32_t b = in[k], e = in[k + 1];
-    carry[c++] = maj3(acc, b, e);
-    acc = xor3(acc, b, e);
+    for (int t = 0; t < T; ++t) {
+      carry[t] = maj3(in[3 * t], in[3 * t + 1], in[3 * t + 2]);
+      next[t] = xor3(in[3 * t], in[3 * t + 1], in[3 * t + 2]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) next[T + r] = in[3 * T + r];
+    return reduce_col<T + R>(next, carry + T);
   }
-  if constexpr (N >= 2 && (N % 2) == 0) {
-    const uint32_t b = in[N - 1];
-    carry[c++] = acc & b;
-    acc ^= b;
-  }
-  return acc;
 }
 
 template <int W, int N, int B>
@@ -175,7 +183,7 @@ __device__ __forceinline__ void one_group(const uint32_t (&s0)[NPP], const uint3
   count_subsets<2 * NPP, B>(d, cnt);
 }
 
-template <int NPP, bool MASKED>
+template <int NPP, bool MASKED, int UNROLL>
 __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uint64_t q, int64_t i,
                                              int64_t j0, int64_t n, uint32_t (&cnt)[2 * NPP],
                                              uint32_t& cnt0) {
@@ -184,7 +192,7 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
 #pragma unroll
   for (int pp = 0; pp < NPP; ++pp) off[pp] = pp * 16 + (int)((q >> (4 * pp)) & 15u);
 
-#pragma unroll 2
+#pragma unroll UNROLL
   for (int h = 0; h < Gm::CT / 2; ++h) {
     uint32_t s0a[NPP], s1a[NPP], s0b[NPP], s1b[NPP];
 #pragma unroll
@@ -201,30 +209,43 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
   if constexpr (!MASKED) cnt0 += Gm::CB;
 }
 
-template <int NPP>
+template <int NPP, int UNROLL>
 __global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __restrict__ codes,
                                                             const uint4* __restrict__ table,
                                                             int64_t n, int64_t nchunks,
                                                             int64_t item_begin, int64_t item_end,
+                                                            int64_t grab,
+                                                            unsigned long long* __restrict__ queue,
                                                             unsigned long long* __restrict__ out) {
   using Gm = Geom<NPP>;
   constexpr int G = Gm::G;
   __shared__ __attribute__((aligned(16))) uint4 tile[Gm::TILE];
+  __shared__ int64_t s_grab;
 
   const int tid = threadIdx.x;
-  const int64_t total = item_end - item_begin;
-  const int64_t t0 = item_begin + total * (int64_t)blockIdx.x / gridDim.x;
-  const int64_t t1 = item_begin + total * (int64_t)(blockIdx.x + 1) / gridDim.x;
-
   uint32_t cnt[G];
 #pragma unroll
   for (int m = 0; m < G; ++m) cnt[m] = 0;
   uint32_t cnt0 = 0;
+  const int64_t last_rows = ((n - 1) + RB - 1) / RB;  // R(last chunk)
+  int64_t loaded = -1;
 
-  if (t0 < t1) {
+  // Dynamic schedule: each workgroup pulls `grab` consecutive items at a time from a
+  // device-scope counter (zeroed by a memset node before every launch); consecutive
+  // items share a column chunk, so the LDS tile is reloaded only at chunk seams.
+  for (;;) {
+    __syncthreads();  // everyone is done with s_grab (and, below, with the tile)
+    if (tid == 0)
+      s_grab = item_begin + (int64_t)__hip_atomic_fetch_add(queue, (unsigned long long)grab,
+                                                             __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int64_t t0 = s_grab;
+    if (t0 >= item_end) break;
+    const int64_t t1 = t0 + grab < item_end ? t0 + grab : item_end;
     ItemCursor cur = locate_item(t0, Gm::K, nchunks);
-    int64_t loaded = -1;
-    const int64_t last_rows = ((n - 1) + RB - 1) / RB;  // R(last chunk)
+    int64_t i = cur.r * RB + tid;
+    uint64_t q = i < n ? codes[i] : 0ull;
     for (int64_t t = t0; t < t1; ++t) {
       const int64_t c = cur.c, r = cur.r;
       if (c != loaded) {
@@ -235,20 +256,22 @@ __global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __re
         __syncthreads();
         loaded = c;
       }
-      const int64_t i = r * RB + tid;
-      const uint64_t q = i < n ? codes[i] : 0ull;
-      const int64_t j0 = c * Gm::CB;
-      const bool masked = ((r + 1) * RB > j0) || (j0 + Gm::CB > n);
-      if (masked)
-        process_item<NPP, true>(tile, q, i, j0, n, cnt, cnt0);
-      else
-        process_item<NPP, false>(tile, q, i, j0, n, cnt, cnt0);
-      // advance the cursor
+      // advance the cursor and prefetch the next item's query while this one computes
       const int64_t rows_c = (c == nchunks - 1) ? last_rows : (c + 1) * Gm::K;
       if (++cur.r >= rows_c) {
         cur.c += 1;
         cur.r = 0;
       }
+      const int64_t i_next = cur.r * RB + tid;
+      const uint64_t q_next = (t + 1 < t1 && i_next < n) ? codes[i_next] : 0ull;
+      const int64_t j0 = c * Gm::CB;
+      const bool masked = ((r + 1) * RB > j0) || (j0 + Gm::CB > n);
+      if (masked)
+        process_item<NPP, true, UNROLL>(tile, q, i, j0, n, cnt, cnt0);
+      else
+        process_item<NPP, false, UNROLL>(tile, q, i, j0, n, cnt, cnt0);
+      q = q_next;
+      i = i_next;
     }
   }
 
@@ -326,6 +349,9 @@ struct sct_allpairs_plan {
   uint64_t* d_codes = nullptr;
   uint4* d_table = nullptr;
   int64_t table_entries = 0;
+  int variant = 2;  // group-pair unroll of the count kernel (SCT_ALLPAIRS_UNROLL=1|2)
+  int64_t grab = 16;  // items per work-queue pull (SCT_ALLPAIRS_GRAB)
+  unsigned long long* d_queue = nullptr;  // work-queue head, zeroed before every launch
 };
 
 namespace {
@@ -338,26 +364,35 @@ int64_t rows_of_chunk(const sct_allpairs_plan* p, int64_t c) {
 template <int NPP>
 int launch_count(sct_allpairs_plan* p, int64_t b, int64_t e, uint64_t* d_counts, int grid,
                  hipStream_t s) {
+  const int variant = p->variant;
   if (grid <= 0) grid = p->grid;
   const int64_t total = e - b;
   if (grid > total) grid = (int)total;
-  // per-lane u32 counters: at most ceil(items/grid) items of CB pairs per lane
-  if ((double)sct::ceil_div(total, grid) * Geom<NPP>::CB >= 4.0e9)
-    return sct::fail(SCT_E_RANGE, "too many items per workgroup for 32-bit lane counters; raise grid");
-  hipLaunchKernelGGL(allpairs_count_kernel<NPP>, dim3(grid), dim3(RB), 0, s, p->d_codes, p->d_table,
-                     p->n, p->nchunks, b, e, reinterpret_cast<unsigned long long*>(d_counts));
+  // per-lane u32 counters: a workgroup sees at most (items) * CB pairs per lane
+  if ((double)total * Geom<NPP>::CB >= 4.0e9)
+    return sct::fail(SCT_E_RANGE, "item range too large for 32-bit lane counters; split it");
+  SCT_HIP(hipMemsetAsync(p->d_queue, 0, sizeof(unsigned long long), s));
+  if (variant == 1)
+    hipLaunchKernelGGL((allpairs_count_kernel<NPP, 1>), dim3(grid), dim3(RB), 0, s, p->d_codes,
+                       p->d_table, p->n, p->nchunks, b, e, p->grab, p->d_queue,
+                       reinterpret_cast<unsigned long long*>(d_counts));
+  else
+    hipLaunchKernelGGL((allpairs_count_kernel<NPP, 2>), dim3(grid), dim3(RB), 0, s, p->d_codes,
+                       p->d_table, p->n, p->nchunks, b, e, p->grab, p->d_queue,
+                       reinterpret_cast<unsigned long long*>(d_counts));
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
 
 template <int NPP>
-int occupancy_grid(int cus) {
+int occupancy_grid(int cus, int variant) {
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, allpairs_count_kernel<NPP>, RB, 0) !=
-          hipSuccess ||
-      per_cu <= 0)
-    per_cu = 4;
-  return cus * per_cu;
+  const hipError_t e =
+      variant == 1
+          ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, allpairs_count_kernel<NPP, 1>, RB, 0)
+          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, allpairs_count_kernel<NPP, 2>, RB, 0);
+  if (e != hipSuccess || per_cu <= 0) per_cu = 4;
+  return cus * per_cu;  // persistent: every workgroup resident, pulling from the queue
 }
 
 #define SCT_NPP_SWITCH(npp, FN, ...)     \
@@ -381,8 +416,8 @@ int occupancy_grid(int cus) {
     default: break;                      \
   }
 
-int grid_for(int npp, int cus) {
-  SCT_NPP_SWITCH(npp, occupancy_grid, cus);
+int grid_for(int npp, int cus, int variant) {
+  SCT_NPP_SWITCH(npp, occupancy_grid, cus, variant);
   return cus * 4;
 }
 
@@ -449,11 +484,22 @@ extern "C" int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int 
     e = hipMalloc(&p->d_table, (size_t)p->table_entries * sizeof(uint4));
     if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "hipMalloc table: %s", hipGetErrorString(e)));
   }
+  e = hipMalloc(&p->d_queue, sizeof(unsigned long long));
+  if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "hipMalloc queue: %s", hipGetErrorString(e)));
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess ||
       cus <= 0)
     cus = 256;
-  p->grid = grid_for(p->npp, cus);
+  if (const char* v = getenv("SCT_ALLPAIRS_UNROLL")) p->variant = atoi(v) == 1 ? 1 : 2;
+  p->grid = grid_for(p->npp, cus, p->variant);
+  if (const char* g = getenv("SCT_ALLPAIRS_GRAB")) {
+    const int gg = atoi(g);
+    if (gg > 0) p->grab = gg;
+  }
+  if (const char* g = getenv("SCT_ALLPAIRS_GRID")) {
+    const int gg = atoi(g);
+    if (gg > 0) p->grid = gg;
+  }
   *plan = p;
   return SCT_OK;
 }
@@ -462,6 +508,7 @@ extern "C" int sct_allpairs_plan_destroy(sct_allpairs_plan* plan) {
   if (!plan) return SCT_OK;
   if (plan->d_codes) (void)hipFree(plan->d_codes);
   if (plan->d_table) (void)hipFree(plan->d_table);
+  if (plan->d_queue) (void)hipFree(plan->d_queue);
   delete plan;
   return SCT_OK;
 }
