@@ -124,6 +124,11 @@ int sct_allpairs_build(sct_allpairs_plan* plan, void* stream);
 /* Count work items [item_begin, item_end).  grid = 0 picks the persistent grid size. */
 int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
                        uint64_t* d_counts, int grid, void* stream);
+/* Host-only (no device needed): the plan geometry for n codes of code_bits bits, i.e.
+ * what sct_allpairs_plan_info would report, plus rows per item and codes per column
+ * chunk.  Lets shard drivers partition [0, items) before touching a GPU. */
+int sct_allpairs_geometry(int64_t n, int code_bits, int* nbins, int64_t* items, int* rows_per_item,
+                          int* cols_per_item);
 /* Pairs contained in work items [item_begin, item_end) (host arithmetic). */
 int sct_allpairs_range_pairs(const sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
                              int64_t* pairs);

@@ -48,6 +48,8 @@ SIGNATURES = {
     "sct_allpairs_build": [_vp, _vp],
     "sct_allpairs_count": [_vp, _i64, _i64, _vp, _i32, _vp],
     "sct_allpairs_range_pairs": [_vp, _i64, _i64, ctypes.POINTER(_i64)],
+    "sct_allpairs_geometry": [_i64, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i64),
+                              ctypes.POINTER(_i32), ctypes.POINTER(_i32)],
     "sct_counts_to_hist": [_vp, _i32, _vp],
     "sct_hamming_hist_allpairs_host": [_vp, _i64, _i32, _vp, _i32],
     "sct_summary_from_hist": [_vp, _i32, _vp],
@@ -221,6 +223,14 @@ def base_frequency(codes, L):
     out = np.zeros((L, 4), dtype=np.uint64)
     check(lib().sct_base_frequency_host(_ptr(codes), codes.size, L, _ptr(out)))
     return out
+
+
+def allpairs_geometry(n, code_bits):
+    """Host-only plan geometry: dict(nbins, items, rows_per_item, cols_per_item)."""
+    nb, it, rb, cb = _i32(0), _i64(0), _i32(0), _i32(0)
+    check(lib().sct_allpairs_geometry(n, code_bits, ctypes.byref(nb), ctypes.byref(it),
+                                      ctypes.byref(rb), ctypes.byref(cb)))
+    return {"nbins": nb.value, "items": it.value, "rows_per_item": rb.value, "cols_per_item": cb.value}
 
 
 def device_count():

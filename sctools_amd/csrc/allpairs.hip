@@ -183,7 +183,7 @@ __device__ __forceinline__ void one_group(const uint32_t (&s0)[NPP], const uint3
   count_subsets<2 * NPP, B>(d, cnt);
 }
 
-template <int NPP, bool MASKED, int UNROLL>
+template <int NPP, bool MASKED, int UNROLL, bool PIPE>
 __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uint64_t q, int64_t i,
                                              int64_t j0, int64_t n, uint32_t (&cnt)[2 * NPP],
                                              uint32_t& cnt0) {
@@ -192,25 +192,65 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
 #pragma unroll
   for (int pp = 0; pp < NPP; ++pp) off[pp] = pp * 16 + (int)((q >> (4 * pp)) & 15u);
 
-#pragma unroll UNROLL
-  for (int h = 0; h < Gm::CT / 2; ++h) {
-    uint32_t s0a[NPP], s1a[NPP], s0b[NPP], s1b[NPP];
+  if constexpr (PIPE) {
+    // register ping-pong: the ds_read_b128s of the next group pair are in flight while
+    // the current one is reduced and counted (two named buffers, no copies)
+    uint4 A[NPP], B[NPP];
+    auto load = [&](uint4 (&buf)[NPP], int h) {
 #pragma unroll
-    for (int pp = 0; pp < NPP; ++pp) {
-      const uint4 e = tile[h * NPP * 16 + off[pp]];
-      s0a[pp] = e.x;
-      s1a[pp] = e.y;
-      s0b[pp] = e.z;
-      s1b[pp] = e.w;
+      for (int pp = 0; pp < NPP; ++pp) buf[pp] = tile[h * NPP * 16 + off[pp]];
+    };
+    auto work = [&](const uint4 (&buf)[NPP], int h) {
+      uint32_t s0a[NPP], s1a[NPP], s0b[NPP], s1b[NPP];
+#pragma unroll
+      for (int pp = 0; pp < NPP; ++pp) {
+        s0a[pp] = buf[pp].x;
+        s1a[pp] = buf[pp].y;
+        s0b[pp] = buf[pp].z;
+        s1b[pp] = buf[pp].w;
+      }
+      one_group<NPP, MASKED>(s0a, s1a, i, j0 + 64 * h, n, cnt, cnt0);
+      one_group<NPP, MASKED>(s0b, s1b, i, j0 + 64 * h + 32, n, cnt, cnt0);
+    };
+    static_assert((Gm::CT / 2) % 2 == 0, "ping-pong needs an even number of group pairs");
+    load(A, 0);
+#pragma unroll 1
+    for (int h = 0; h < Gm::CT / 2; h += 2) {
+      load(B, h + 1);
+      work(A, h);
+      if (h + 2 < Gm::CT / 2) load(A, h + 2);
+      work(B, h + 1);
     }
-    one_group<NPP, MASKED>(s0a, s1a, i, j0 + 64 * h, n, cnt, cnt0);
-    one_group<NPP, MASKED>(s0b, s1b, i, j0 + 64 * h + 32, n, cnt, cnt0);
+  } else {
+#pragma unroll UNROLL
+    for (int h = 0; h < Gm::CT / 2; ++h) {
+      uint32_t s0a[NPP], s1a[NPP], s0b[NPP], s1b[NPP];
+#pragma unroll
+      for (int pp = 0; pp < NPP; ++pp) {
+        const uint4 e = tile[h * NPP * 16 + off[pp]];
+        s0a[pp] = e.x;
+        s1a[pp] = e.y;
+        s0b[pp] = e.z;
+        s1b[pp] = e.w;
+      }
+      one_group<NPP, MASKED>(s0a, s1a, i, j0 + 64 * h, n, cnt, cnt0);
+      one_group<NPP, MASKED>(s0b, s1b, i, j0 + 64 * h + 32, n, cnt, cnt0);
+    }
   }
   if constexpr (!MASKED) cnt0 += Gm::CB;
 }
 
-template <int NPP, int UNROLL>
-__global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __restrict__ codes,
+// Count-kernel variants (A/B-selectable with SCT_ALLPAIRS_VARIANT):
+//   1: one group pair per loop trip      2: two group pairs per trip (default)
+//   3: 1 + register-prefetched LDS reads 4: 1 built for 5 waves/SIMD (<= 96 VGPRs)
+template <int V> struct Variant;
+template <> struct Variant<1> { static constexpr int UNROLL = 1, MINW = 1; static constexpr bool PIPE = false; };
+template <> struct Variant<2> { static constexpr int UNROLL = 2, MINW = 1; static constexpr bool PIPE = false; };
+template <> struct Variant<3> { static constexpr int UNROLL = 1, MINW = 1; static constexpr bool PIPE = true; };
+template <> struct Variant<4> { static constexpr int UNROLL = 1, MINW = 5; static constexpr bool PIPE = false; };
+
+template <int NPP, int V>
+__global__ __launch_bounds__(RB, Variant<V>::MINW) void allpairs_count_kernel(const uint64_t* __restrict__ codes,
                                                             const uint4* __restrict__ table,
                                                             int64_t n, int64_t nchunks,
                                                             int64_t item_begin, int64_t item_end,
@@ -267,9 +307,9 @@ __global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __re
       const int64_t j0 = c * Gm::CB;
       const bool masked = ((r + 1) * RB > j0) || (j0 + Gm::CB > n);
       if (masked)
-        process_item<NPP, true, UNROLL>(tile, q, i, j0, n, cnt, cnt0);
+        process_item<NPP, true, Variant<V>::UNROLL, Variant<V>::PIPE>(tile, q, i, j0, n, cnt, cnt0);
       else
-        process_item<NPP, false, UNROLL>(tile, q, i, j0, n, cnt, cnt0);
+        process_item<NPP, false, Variant<V>::UNROLL, Variant<V>::PIPE>(tile, q, i, j0, n, cnt, cnt0);
       q = q_next;
       i = i_next;
     }
@@ -349,7 +389,7 @@ struct sct_allpairs_plan {
   uint64_t* d_codes = nullptr;
   uint4* d_table = nullptr;
   int64_t table_entries = 0;
-  int variant = 2;  // group-pair unroll of the count kernel (SCT_ALLPAIRS_UNROLL=1|2)
+  int variant = 2;  // count-kernel variant (SCT_ALLPAIRS_VARIANT=1..4, see Variant<>)
   int64_t grab = 16;  // items per work-queue pull (SCT_ALLPAIRS_GRAB)
   unsigned long long* d_queue = nullptr;  // work-queue head, zeroed before every launch
 };
@@ -372,26 +412,40 @@ int launch_count(sct_allpairs_plan* p, int64_t b, int64_t e, uint64_t* d_counts,
   if ((double)total * Geom<NPP>::CB >= 4.0e9)
     return sct::fail(SCT_E_RANGE, "item range too large for 32-bit lane counters; split it");
   SCT_HIP(hipMemsetAsync(p->d_queue, 0, sizeof(unsigned long long), s));
-  if (variant == 1)
-    hipLaunchKernelGGL((allpairs_count_kernel<NPP, 1>), dim3(grid), dim3(RB), 0, s, p->d_codes,
-                       p->d_table, p->n, p->nchunks, b, e, p->grab, p->d_queue,
-                       reinterpret_cast<unsigned long long*>(d_counts));
-  else
-    hipLaunchKernelGGL((allpairs_count_kernel<NPP, 2>), dim3(grid), dim3(RB), 0, s, p->d_codes,
-                       p->d_table, p->n, p->nchunks, b, e, p->grab, p->d_queue,
-                       reinterpret_cast<unsigned long long*>(d_counts));
+#define SCT_LAUNCH_V(V)                                                                         \
+  hipLaunchKernelGGL((allpairs_count_kernel<NPP, V>), dim3(grid), dim3(RB), 0, s, p->d_codes,   \
+                     p->d_table, p->n, p->nchunks, b, e, p->grab, p->d_queue,                    \
+                     reinterpret_cast<unsigned long long*>(d_counts))
+  switch (variant) {
+    case 1: SCT_LAUNCH_V(1); break;
+    case 3: SCT_LAUNCH_V(3); break;
+    case 4: SCT_LAUNCH_V(4); break;
+    default: SCT_LAUNCH_V(2); break;
+  }
+#undef SCT_LAUNCH_V
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
 
+template <int NPP, int V>
+int occupancy_of() {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, allpairs_count_kernel<NPP, V>, RB, 0) !=
+          hipSuccess ||
+      per_cu <= 0)
+    per_cu = 4;
+  return per_cu;
+}
+
 template <int NPP>
 int occupancy_grid(int cus, int variant) {
-  int per_cu = 0;
-  const hipError_t e =
-      variant == 1
-          ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, allpairs_count_kernel<NPP, 1>, RB, 0)
-          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, allpairs_count_kernel<NPP, 2>, RB, 0);
-  if (e != hipSuccess || per_cu <= 0) per_cu = 4;
+  int per_cu;
+  switch (variant) {
+    case 1: per_cu = occupancy_of<NPP, 1>(); break;
+    case 3: per_cu = occupancy_of<NPP, 3>(); break;
+    case 4: per_cu = occupancy_of<NPP, 4>(); break;
+    default: per_cu = occupancy_of<NPP, 2>(); break;
+  }
   return cus * per_cu;  // persistent: every workgroup resident, pulling from the queue
 }
 
@@ -490,7 +544,10 @@ extern "C" int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int 
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess ||
       cus <= 0)
     cus = 256;
-  if (const char* v = getenv("SCT_ALLPAIRS_UNROLL")) p->variant = atoi(v) == 1 ? 1 : 2;
+  if (const char* v = getenv("SCT_ALLPAIRS_VARIANT")) {
+    const int vv = atoi(v);
+    if (vv >= 1 && vv <= 4) p->variant = vv;
+  }
   p->grid = grid_for(p->npp, cus, p->variant);
   if (const char* g = getenv("SCT_ALLPAIRS_GRAB")) {
     const int gg = atoi(g);
@@ -542,6 +599,26 @@ extern "C" int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, i
             (long long)item_end, (long long)plan->items);
   if (item_begin == item_end) return SCT_OK;
   return dispatch_count(plan, item_begin, item_end, d_counts, grid, sct::as_stream(stream));
+}
+
+extern "C" int sct_allpairs_geometry(int64_t n, int code_bits, int* nbins, int64_t* items,
+                                     int* rows_per_item, int* cols_per_item) {
+  SCT_CHECK(n >= 0, "n must be >= 0");
+  SCT_CHECK(code_bits >= 1 && code_bits <= 64, "code_bits %d outside [1, 64]", code_bits);
+  const int npp = (code_bits + 3) / 4;
+  const int64_t cb = 32LL * ct_for(npp);
+  const int64_t nchunks = n > 0 ? sct::ceil_div(n, cb) : 0;
+  int64_t it = 0;
+  if (n >= 2) {
+    const int64_t K = cb / RB, last = nchunks - 1;
+    const int64_t maxj = std::min<int64_t>((last + 1) * cb, n) - 1;
+    it = K * last * (last + 1) / 2 + (maxj <= 0 ? 0 : (maxj + RB - 1) / RB);
+  }
+  if (nbins) *nbins = 2 * npp + 1;
+  if (items) *items = it;
+  if (rows_per_item) *rows_per_item = RB;
+  if (cols_per_item) *cols_per_item = (int)cb;
+  return SCT_OK;
 }
 
 extern "C" int sct_allpairs_range_pairs(const sct_allpairs_plan* plan, int64_t item_begin,

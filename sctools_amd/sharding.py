@@ -1,0 +1,65 @@
+"""Multi-GPU all-pairs histogram: one process per GPU, RCCL all-reduce of the counts.
+
+The unordered pairs of a code set are cut into ``items`` equal work items (row block
+x column chunk, see sctools_amd/csrc/allpairs.hip).  Rank r of W counts the
+contiguous item range ``item_range(items, r, W)`` on its own GPU against its own
+replica of the codes (a few MB, so every rank holds them all), producing ``nbins``
+uint64 subset counts.  The counts are linear in the pairs, so ONE all-reduce(sum)
+of ``nbins`` int64 over RCCL (torch.distributed backend "nccl" on ROCm) combines the
+ranks; every rank then inverts the summed counts to the exact histogram.  Integer
+sums are order independent, so the result is bit-identical for any W.
+
+The reference (barcode.py:39-46) has no parallelism at all; this is new.
+"""
+
+import numpy as np
+
+from . import _lib
+
+__all__ = ["item_range", "combine_counts", "allpairs_histogram_sharded"]
+
+
+def item_range(items, rank, world):
+    """Contiguous, balanced shard [begin, end) of [0, items) for `rank` of `world`."""
+    if not 0 <= rank < world:
+        raise ValueError("rank %d outside world of %d" % (rank, world))
+    return items * rank // world, items * (rank + 1) // world
+
+
+def combine_counts(counts, group=None):
+    """Sum per-rank subset counts (a torch int64 tensor, in place) over the process
+    group and return the exact histogram as np.uint64 on every rank."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+    host = counts.detach().cpu().numpy().astype(np.int64).view(np.uint64)
+    return _lib.counts_to_hist(host)
+
+
+def allpairs_histogram_sharded(codes, code_bits=None, group=None, device=None, stream=None):
+    """Histogram of TwoBit distances over all unordered pairs of `codes` (np.uint64 or a
+    torch tensor), sharded over the ranks of `group` (one GPU each).  Call on every rank
+    with the same codes."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    if isinstance(codes, np.ndarray):
+        d_codes = torch.from_numpy(np.ascontiguousarray(codes, dtype=np.uint64).view(np.int64)).to(device)
+    else:
+        d_codes = codes.to(device=device, dtype=torch.int64).contiguous()
+    n = int(d_codes.numel())
+    if code_bits is None:
+        orv = int(np.bitwise_or.reduce(d_codes.cpu().numpy().view(np.uint64))) if n else 0
+        code_bits = max(1, orv.bit_length())
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, code_bits)
+    try:
+        s = (stream or torch.cuda.current_stream(device)).cuda_stream
+        b, e = item_range(plan.items, rank, world)
+        counts = torch.zeros(plan.nbins, dtype=torch.int64, device=device)
+        plan.build(s)
+        plan.count(counts.data_ptr(), b, e, 0, s)
+        return combine_counts(counts, group)
+    finally:
+        plan.close()

@@ -1,0 +1,81 @@
+"""CPU, world_size 2 (gloo): the multi-GPU orchestration — item partition, count
+all-reduce, inversion — without a GPU.  Each rank's per-shard subset counts come from
+the C oracle's independent enumeration of the same work items (test-only stand-in
+for the kernel, which has its own GPU parity tests); the product code under test is
+sctools_amd.sharding.item_range / combine_counts and the library's geometry and
+Moebius inversion."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+from sctools_amd import _lib, sharding, synthetic
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _shard_counts(codes, geo, b, e):
+    hist = np.zeros(65, dtype=np.int64)
+    pairs = np.zeros(1, dtype=np.int64)
+    O.c_oracle().oracle_hist_items(codes.ctypes.data, codes.size, geo["rows_per_item"],
+                                   geo["cols_per_item"], hist.ctypes.data, b, e, pairs.ctypes.data, 1)
+    nb = geo["nbins"]
+    counts = np.zeros(nb, dtype=np.int64)
+    for m in range(nb):
+        counts[m] = sum(int(hist[d]) for d in range(nb) if (d & m) == m)
+    assert counts[0] == pairs[0]
+    return counts
+
+
+def _worker(rank, world, port, n, seed, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        codes = synthetic.whitelist_codes(n, 16, seed)
+        geo = _lib.allpairs_geometry(n, 32)
+        b, e = sharding.item_range(geo["items"], rank, world)
+        counts = torch.from_numpy(_shard_counts(codes, geo, b, e))
+        hist = sharding.combine_counts(counts)
+        np.save(out_path % rank, hist.astype(np.int64))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 2500), (3, 1300)])
+def test_sharded_histogram_matches_oracle(tmp_path, world, n):
+    port = _free_port()
+    out = str(tmp_path / "hist_%d.npy")
+    mp.spawn(_worker, args=(world, port, n, 17, out), nprocs=world, join=True)
+    codes = synthetic.whitelist_codes(n, 16, 17)
+    ref = O.c_hist_rows(codes)[:17]
+    for r in range(world):
+        assert np.load(out % r).tolist() == ref.tolist()
+
+
+def test_item_range_partitions():
+    for items in (0, 1, 7, 1038240):
+        for world in (1, 2, 3, 4, 8):
+            ranges = [sharding.item_range(items, r, world) for r in range(world)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == items
+            assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+            sizes = [e - b for b, e in ranges]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_geometry_item_count_matches_oracle_enumeration():
+    for n in (2, 100, 1024, 1025, 5000, 737_280):
+        geo = _lib.allpairs_geometry(n, 32)
+        rb, cb = geo["rows_per_item"], geo["cols_per_item"]
+        nch = -(-n // cb)
+        items = sum(max(0, -(-(min((c + 1) * cb, n) - 1) // rb)) for c in range(nch))
+        assert geo["items"] == items

@@ -4,7 +4,7 @@ Variants are selected at plan creation through SCT_ALLPAIRS_UNROLL / SCT_ALLPAIR
 each round times every variant once (HIP events on the launch stream); prints the
 median and min per variant and checks that all variants produce identical counts.
 
-  python tools/ab_allpairs.py --config 2 --rounds 7 --variants "unroll=2" "unroll=1" "unroll=1,grid=2048"
+  python tools/ab_allpairs.py --config 2 --rounds 7 --variants "v=2" "v=1" "v=1,grid=2048"
 """
 
 import argparse
@@ -24,7 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--variants", nargs="+", default=["unroll=2", "unroll=1"])
+    ap.add_argument("--variants", nargs="+", default=["v=2", "v=1"])
     a = ap.parse_args()
     n, L, seed = synthetic.CONFIGS[a.config]
     codes = synthetic.whitelist_codes(n, L, seed)
@@ -32,7 +32,7 @@ def main():
     plans = []
     for v in a.variants:
         kv = dict(x.split("=") for x in v.split(","))
-        os.environ["SCT_ALLPAIRS_UNROLL"] = kv.get("unroll", "2")
+        os.environ["SCT_ALLPAIRS_VARIANT"] = kv.get("v", "2")
         for key in ("grid", "grab"):
             env = "SCT_ALLPAIRS_" + key.upper()
             if key in kv:
