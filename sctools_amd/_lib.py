@@ -66,8 +66,26 @@ class LibraryMissing(ImportError):
     pass
 
 
+def _torch_hip_runtime():
+    """Path of the HIP runtime bundled with torch (found without importing torch)."""
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return None
+    if spec is None or not spec.submodule_search_locations:
+        return None
+    path = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    return path if os.path.exists(path) else None
+
+
 def lib():
-    """Load libsctools_hip.so once; raise LibraryMissing (an ImportError) if absent."""
+    """Load libsctools_hip.so once; raise LibraryMissing (an ImportError) if absent.
+
+    torch ships its own libamdhip64 with the same SONAME (libamdhip64.so.7) as ROCm's;
+    two HIP runtimes in one process break each other ("No HIP GPUs are available").
+    So when torch is installed its runtime is loaded first (RTLD_GLOBAL) and this
+    library binds to it, whatever the import order."""
     global _lib
     if _lib is not None:
         return _lib
@@ -78,6 +96,9 @@ def lib():
                     "libsctools_hip.so not found at %s: build it with "
                     "`python -c 'import __graft_entry__; __graft_entry__.build()'` "
                     "(there is no CPU fallback)" % LIB_PATH)
+            rt = os.environ.get("SCTOOLS_HIP_RUNTIME") or _torch_hip_runtime()
+            if rt:
+                ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
             handle = ctypes.CDLL(LIB_PATH)
             for name, args in SIGNATURES.items():
                 fn = getattr(handle, name)
