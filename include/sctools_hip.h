@@ -150,6 +150,26 @@ int sct_hamming_hist_allpairs_host(const uint64_t* codes, int64_t n, int code_bi
 int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint64_t* out, void* stream);
 int sct_base_frequency_host(const uint64_t* codes, int64_t n, int L, uint64_t* out);
 
+/* ---------------------------------------------------------------- nearest whitelist
+ * No reference function exists; the contract is the brute-force
+ * composition of the reference's distance (kind 2: TwoBit.hamming_distance,
+ * encodings.py:113-121; kind 3: ThreeBit.hamming_distance, encodings.py:194-202):
+ *   index[i] = j  if exactly one whitelist index j attains d_min(q_i) <= max_d,
+ *            = -2 if several indices attain it, -1 if d_min > max_d;
+ *   dist[i]  = d_min if <= max_d, else 255.
+ * The plan is an exact pigeonhole index (max_d+1 position blocks, CSR buckets per block);
+ * it copies nothing from the caller after create returns (the whitelist is bucketed).
+ * code_bits: bits covered by the block split (whitelist codes < 2^code_bits).
+ */
+typedef struct sct_nearest_plan sct_nearest_plan;
+int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, int64_t nw, int code_bits,
+                            int max_d, void* stream, sct_nearest_plan** plan);
+int sct_nearest_plan_destroy(sct_nearest_plan* plan);
+int sct_nearest_query(sct_nearest_plan* plan, const uint64_t* d_queries, int64_t nq,
+                      int32_t* d_index, uint8_t* d_dist, void* stream);
+int sct_nearest_host(int kind, const uint64_t* whitelist, int64_t nw, const uint64_t* queries,
+                     int64_t nq, int code_bits, int max_d, int32_t* index, uint8_t* dist);
+
 /* ---------------------------------------------------------------- summary
  * Replaces barcode.py:44-46 (np.percentile(distances,[0,25,50,75,100]) with numpy's
  * default 'linear' method, then np.mean) computed from the histogram alone,

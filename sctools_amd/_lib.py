@@ -53,6 +53,10 @@ SIGNATURES = {
     "sct_counts_to_hist": [_vp, _i32, _vp],
     "sct_hamming_hist_allpairs_host": [_vp, _i64, _i32, _vp, _i32],
     "sct_summary_from_hist": [_vp, _i32, _vp],
+    "sct_nearest_plan_create": [_i32, _vp, _i64, _i32, _i32, _vp, ctypes.POINTER(_vp)],
+    "sct_nearest_plan_destroy": [_vp],
+    "sct_nearest_query": [_vp, _vp, _i64, _vp, _vp, _vp],
+    "sct_nearest_host": [_i32, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _vp],
     "sct_base_frequency": [_vp, _i64, _i32, _vp, _vp],
     "sct_base_frequency_host": [_vp, _i64, _i32, _vp],
 }
@@ -252,6 +256,44 @@ def allpairs_geometry(n, code_bits):
     check(lib().sct_allpairs_geometry(n, code_bits, ctypes.byref(nb), ctypes.byref(it),
                                       ctypes.byref(rb), ctypes.byref(cb)))
     return {"nbins": nb.value, "items": it.value, "rows_per_item": rb.value, "cols_per_item": cb.value}
+
+
+def nearest(kind, whitelist, queries, max_d=1, code_bits=None):
+    """Brute-force-equivalent nearest whitelist entry -> (index int32, dist uint8)."""
+    wl = np.ascontiguousarray(whitelist, dtype=np.uint64).reshape(-1)
+    q = np.ascontiguousarray(queries, dtype=np.uint64).reshape(-1)
+    if code_bits is None:
+        code_bits = max(1, int(np.bitwise_or.reduce(wl)).bit_length() if wl.size else 1)
+    index = np.zeros(q.size, dtype=np.int32)
+    dist = np.zeros(q.size, dtype=np.uint8)
+    check(lib().sct_nearest_host(kind, _ptr(wl), wl.size, _ptr(q), q.size, code_bits, max_d,
+                                 _ptr(index), _ptr(dist)))
+    return index, dist
+
+
+class NearestPlan:
+    """Device-resident pigeonhole index of a whitelist (sct_nearest_plan)."""
+
+    def __init__(self, kind, d_whitelist_ptr, nw, code_bits, max_d, stream=0):
+        self._lib = lib()
+        self._h = _vp()
+        check(self._lib.sct_nearest_plan_create(kind, _vp(d_whitelist_ptr), nw, code_bits, max_d,
+                                                _vp(stream), ctypes.byref(self._h)))
+
+    def query(self, d_queries_ptr, nq, d_index_ptr, d_dist_ptr, stream=0):
+        check(self._lib.sct_nearest_query(self._h, _vp(d_queries_ptr), nq, _vp(d_index_ptr),
+                                          _vp(d_dist_ptr), _vp(stream)))
+
+    def close(self):
+        if self._h:
+            self._lib.sct_nearest_plan_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def device_count():

@@ -19,7 +19,7 @@ from . import _lib
 from .encodings import TwoBit
 from .stats import base4_entropy
 
-__all__ = ["Barcodes", "ObservedBarcodeSet", "PriorBarcodeSet"]
+__all__ = ["Barcodes", "ObservedBarcodeSet", "PriorBarcodeSet", "nearest_whitelist"]
 
 _SUMMARY_KEYS = ('minimum', '25th percentile', 'median', '75th percentile', 'maximum', 'average')
 
@@ -79,6 +79,13 @@ class Barcodes:
         hist = self.hamming_histogram()
         values = _lib.summary_from_hist(hist)  # IndexError for < 2 barcodes, as numpy raises
         return dict(zip(_SUMMARY_KEYS, [np.float64(v) for v in values]))
+
+    def nearest(self, queries, max_distance=1):
+        """For each TwoBit-encoded query, the index (in iteration order) of the unique
+        closest barcode of this set within ``max_distance`` (TwoBit.hamming_distance),
+        -2 for a tie, -1 for none; and that distance (255 for none)."""
+        return nearest_whitelist(queries, self.codes_array(), max_distance=max_distance,
+                                 encoding='TwoBit')
 
     def base_frequency(self, weighted=False):
         """(barcode_length, 4) uint64 base counts by position, columns A, C, T, G
@@ -146,6 +153,26 @@ def _encode_lines(seqs):
     for i in sorted(pending):
         out[i] = TwoBit.encode(seqs[i])  # batch of one: draws in record order
     return out
+
+
+def nearest_whitelist(queries, whitelist, max_distance=1, encoding='ThreeBit'):
+    """Whitelist error correction (no reference counterpart).
+
+    Same result as the brute force over the reference's distance
+    (``ThreeBit.hamming_distance``, encodings.py:194-202, or ``TwoBit.hamming_distance``,
+    encodings.py:113-121): for each query the unique whitelist index at the minimal
+    distance d <= max_distance, -2 if several indices share it, -1 if none; plus d
+    (255 when none).  Codes are non-negative ints below 2**64 in the given encoding.
+
+    :return (np.ndarray[int32], np.ndarray[uint8]): index, distance
+    """
+    kind = {'ThreeBit': 3, 'TwoBit': 2, 3: 3, 2: 2}[encoding]
+    wl = np.ascontiguousarray(np.asarray(whitelist, dtype=np.uint64)).reshape(-1)
+    q = np.ascontiguousarray(np.asarray(queries, dtype=np.uint64)).reshape(-1)
+    if wl.size == 0:
+        return np.full(q.size, -1, np.int32), np.full(q.size, 255, np.uint8)
+    bits = max(int(np.bitwise_or.reduce(wl)).bit_length(), kind * (max_distance + 1))
+    return _lib.nearest(kind, wl, q, max_d=max_distance, code_bits=min(64, bits))
 
 
 class ObservedBarcodeSet(Barcodes):

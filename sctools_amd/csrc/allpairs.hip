@@ -183,7 +183,7 @@ __device__ __forceinline__ void one_group(const uint32_t (&s0)[NPP], const uint3
   count_subsets<2 * NPP, B>(d, cnt);
 }
 
-template <int NPP, bool MASKED, int UNROLL, bool PIPE>
+template <int NPP, bool MASKED, int UNROLL>
 __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uint64_t q, int64_t i,
                                              int64_t j0, int64_t n, uint32_t (&cnt)[2 * NPP],
                                              uint32_t& cnt0) {
@@ -192,36 +192,7 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
 #pragma unroll
   for (int pp = 0; pp < NPP; ++pp) off[pp] = pp * 16 + (int)((q >> (4 * pp)) & 15u);
 
-  if constexpr (PIPE) {
-    // register ping-pong: the ds_read_b128s of the next group pair are in flight while
-    // the current one is reduced and counted (two named buffers, no copies)
-    uint4 A[NPP], B[NPP];
-    auto load = [&](uint4 (&buf)[NPP], int h) {
-#pragma unroll
-      for (int pp = 0; pp < NPP; ++pp) buf[pp] = tile[h * NPP * 16 + off[pp]];
-    };
-    auto work = [&](const uint4 (&buf)[NPP], int h) {
-      uint32_t s0a[NPP], s1a[NPP], s0b[NPP], s1b[NPP];
-#pragma unroll
-      for (int pp = 0; pp < NPP; ++pp) {
-        s0a[pp] = buf[pp].x;
-        s1a[pp] = buf[pp].y;
-        s0b[pp] = buf[pp].z;
-        s1b[pp] = buf[pp].w;
-      }
-      one_group<NPP, MASKED>(s0a, s1a, i, j0 + 64 * h, n, cnt, cnt0);
-      one_group<NPP, MASKED>(s0b, s1b, i, j0 + 64 * h + 32, n, cnt, cnt0);
-    };
-    static_assert((Gm::CT / 2) % 2 == 0, "ping-pong needs an even number of group pairs");
-    load(A, 0);
-#pragma unroll 1
-    for (int h = 0; h < Gm::CT / 2; h += 2) {
-      load(B, h + 1);
-      work(A, h);
-      if (h + 2 < Gm::CT / 2) load(A, h + 2);
-      work(B, h + 1);
-    }
-  } else {
+  {
 #pragma unroll UNROLL
     for (int h = 0; h < Gm::CT / 2; ++h) {
       uint32_t s0a[NPP], s1a[NPP], s0b[NPP], s1b[NPP];
@@ -240,21 +211,46 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
   if constexpr (!MASKED) cnt0 += Gm::CB;
 }
 
-// Count-kernel variants (A/B-selectable with SCT_ALLPAIRS_VARIANT):
-//   1: one group pair per loop trip      2: two group pairs per trip (default)
-//   3: 1 + register-prefetched LDS reads 4: 1 built for 5 waves/SIMD (<= 96 VGPRs)
-template <int V> struct Variant;
-template <> struct Variant<1> { static constexpr int UNROLL = 1, MINW = 1; static constexpr bool PIPE = false; };
-template <> struct Variant<2> { static constexpr int UNROLL = 2, MINW = 1; static constexpr bool PIPE = false; };
-template <> struct Variant<3> { static constexpr int UNROLL = 1, MINW = 1; static constexpr bool PIPE = true; };
-template <> struct Variant<4> { static constexpr int UNROLL = 1, MINW = 5; static constexpr bool PIPE = false; };
+// Count-kernel variants (A/B-selectable with SCT_ALLPAIRS_VARIANT): 1 = one group pair
+// per loop trip (108 VGPRs), 2 = two per trip (default, 124 VGPRs, 4 waves/SIMD).
+// Register prefetch / ping-pong variants measured slower and were dropped.
+template <int V> struct Variant { static constexpr int UNROLL = V; };
+
+// Workgroup reduction of the per-lane counters: 64-lane butterfly (shfl_xor, lowered to
+// DPP/ds_swizzle/ds_bpermute), then LDS across the waves, then one u64 atomic per counter;
+// the lane counters restart at 0.  `red` aliases the LDS tile (callers sync first).
+template <int G>
+__device__ __forceinline__ void flush_counts(uint32_t (&cnt)[G], uint32_t& cnt0,
+                                             unsigned long long* red,
+                                             unsigned long long* __restrict__ out) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m <= G; ++m) {
+    unsigned long long v = (m == 0) ? cnt0 : cnt[m - 1];
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s, 64);
+    if (lane == 0) red[wave * (G + 1) + m] = v;
+  }
+  __syncthreads();
+  if (tid <= G) {
+    unsigned long long s = 0;
+#pragma unroll
+    for (int w = 0; w < RB / 64; ++w) s += red[w * (G + 1) + tid];
+    if (s) atomicAdd(out + tid, s);
+  }
+#pragma unroll
+  for (int m = 0; m < G; ++m) cnt[m] = 0;
+  cnt0 = 0;
+  __syncthreads();
+}
 
 template <int NPP, int V>
-__global__ __launch_bounds__(RB, Variant<V>::MINW) void allpairs_count_kernel(const uint64_t* __restrict__ codes,
+__global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __restrict__ codes,
                                                             const uint4* __restrict__ table,
                                                             int64_t n, int64_t nchunks,
                                                             int64_t item_begin, int64_t item_end,
-                                                            int64_t grab,
+                                                            int64_t grab, int64_t flush_items,
                                                             unsigned long long* __restrict__ queue,
                                                             unsigned long long* __restrict__ out) {
   using Gm = Geom<NPP>;
@@ -269,6 +265,9 @@ __global__ __launch_bounds__(RB, Variant<V>::MINW) void allpairs_count_kernel(co
   uint32_t cnt0 = 0;
   const int64_t last_rows = ((n - 1) + RB - 1) / RB;  // R(last chunk)
   int64_t loaded = -1;
+  // a lane adds at most CB pairs per item to each u32 counter: flush before 2^32
+  // (flush_items <= 0xFFFFFFFF / CB; the host may pass less to exercise the path)
+  int64_t since_flush = 0;
 
   // Dynamic schedule: each workgroup pulls `grab` consecutive items at a time from a
   // device-scope counter (zeroed by a memset node before every launch); consecutive
@@ -283,6 +282,12 @@ __global__ __launch_bounds__(RB, Variant<V>::MINW) void allpairs_count_kernel(co
     const int64_t t0 = s_grab;
     if (t0 >= item_end) break;
     const int64_t t1 = t0 + grab < item_end ? t0 + grab : item_end;
+    if (since_flush + (t1 - t0) > flush_items) {  // wave-uniform, practically never taken
+      flush_counts<G>(cnt, cnt0, reinterpret_cast<unsigned long long*>(tile), out);
+      loaded = -1;  // the flush used the tile as scratch
+      since_flush = 0;
+    }
+    since_flush += t1 - t0;
     ItemCursor cur = locate_item(t0, Gm::K, nchunks);
     int64_t i = cur.r * RB + tid;
     uint64_t q = i < n ? codes[i] : 0ull;
@@ -307,32 +312,15 @@ __global__ __launch_bounds__(RB, Variant<V>::MINW) void allpairs_count_kernel(co
       const int64_t j0 = c * Gm::CB;
       const bool masked = ((r + 1) * RB > j0) || (j0 + Gm::CB > n);
       if (masked)
-        process_item<NPP, true, Variant<V>::UNROLL, Variant<V>::PIPE>(tile, q, i, j0, n, cnt, cnt0);
+        process_item<NPP, true, Variant<V>::UNROLL>(tile, q, i, j0, n, cnt, cnt0);
       else
-        process_item<NPP, false, Variant<V>::UNROLL, Variant<V>::PIPE>(tile, q, i, j0, n, cnt, cnt0);
+        process_item<NPP, false, Variant<V>::UNROLL>(tile, q, i, j0, n, cnt, cnt0);
       q = q_next;
       i = i_next;
     }
   }
 
-  // ---- workgroup reduction: wave butterfly (DPP/swizzle lowering of shfl_xor), LDS, atomics
-  __syncthreads();
-  unsigned long long* red = reinterpret_cast<unsigned long long*>(tile);  // [RB/64][G+1]
-  const int lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-  for (int m = 0; m <= G; ++m) {
-    unsigned long long v = (m == 0) ? cnt0 : cnt[m - 1];
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s, 64);
-    if (lane == 0) red[wave * (G + 1) + m] = v;
-  }
-  __syncthreads();
-  if (tid <= G) {
-    unsigned long long s = 0;
-#pragma unroll
-    for (int w = 0; w < RB / 64; ++w) s += red[w * (G + 1) + tid];
-    if (s) atomicAdd(out + tid, s);
-  }
+  flush_counts<G>(cnt, cnt0, reinterpret_cast<unsigned long long*>(tile), out);
 }
 
 // table[h][pp][c] = bit-sliced 2-bit mismatch counts of nibble pp of the 64 codes of
@@ -389,8 +377,9 @@ struct sct_allpairs_plan {
   uint64_t* d_codes = nullptr;
   uint4* d_table = nullptr;
   int64_t table_entries = 0;
-  int variant = 2;  // count-kernel variant (SCT_ALLPAIRS_VARIANT=1..4, see Variant<>)
+  int variant = 2;  // count-kernel variant (SCT_ALLPAIRS_VARIANT=1|2, see Variant<>)
   int64_t grab = 16;  // items per work-queue pull (SCT_ALLPAIRS_GRAB)
+  int64_t flush_items = 0;  // test hook: flush lane counters more often (SCT_ALLPAIRS_FLUSH_ITEMS)
   unsigned long long* d_queue = nullptr;  // work-queue head, zeroed before every launch
 };
 
@@ -408,18 +397,16 @@ int launch_count(sct_allpairs_plan* p, int64_t b, int64_t e, uint64_t* d_counts,
   if (grid <= 0) grid = p->grid;
   const int64_t total = e - b;
   if (grid > total) grid = (int)total;
-  // per-lane u32 counters: a workgroup sees at most (items) * CB pairs per lane
-  if ((double)total * Geom<NPP>::CB >= 4.0e9)
-    return sct::fail(SCT_E_RANGE, "item range too large for 32-bit lane counters; split it");
+  SCT_CHECK(p->grab > 0 && p->grab * Geom<NPP>::CB < 0xFFFFFFFFLL, "grab too large");
+  int64_t flush = 0xFFFFFFFFLL / Geom<NPP>::CB - p->grab;
+  if (p->flush_items > 0 && p->flush_items < flush) flush = p->flush_items;
   SCT_HIP(hipMemsetAsync(p->d_queue, 0, sizeof(unsigned long long), s));
 #define SCT_LAUNCH_V(V)                                                                         \
   hipLaunchKernelGGL((allpairs_count_kernel<NPP, V>), dim3(grid), dim3(RB), 0, s, p->d_codes,   \
-                     p->d_table, p->n, p->nchunks, b, e, p->grab, p->d_queue,                    \
+                     p->d_table, p->n, p->nchunks, b, e, p->grab, flush, p->d_queue,             \
                      reinterpret_cast<unsigned long long*>(d_counts))
   switch (variant) {
     case 1: SCT_LAUNCH_V(1); break;
-    case 3: SCT_LAUNCH_V(3); break;
-    case 4: SCT_LAUNCH_V(4); break;
     default: SCT_LAUNCH_V(2); break;
   }
 #undef SCT_LAUNCH_V
@@ -442,8 +429,6 @@ int occupancy_grid(int cus, int variant) {
   int per_cu;
   switch (variant) {
     case 1: per_cu = occupancy_of<NPP, 1>(); break;
-    case 3: per_cu = occupancy_of<NPP, 3>(); break;
-    case 4: per_cu = occupancy_of<NPP, 4>(); break;
     default: per_cu = occupancy_of<NPP, 2>(); break;
   }
   return cus * per_cu;  // persistent: every workgroup resident, pulling from the queue
@@ -546,9 +531,10 @@ extern "C" int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int 
     cus = 256;
   if (const char* v = getenv("SCT_ALLPAIRS_VARIANT")) {
     const int vv = atoi(v);
-    if (vv >= 1 && vv <= 4) p->variant = vv;
+    if (vv >= 1 && vv <= 2) p->variant = vv;
   }
   p->grid = grid_for(p->npp, cus, p->variant);
+  if (const char* f = getenv("SCT_ALLPAIRS_FLUSH_ITEMS")) p->flush_items = atoll(f);
   if (const char* g = getenv("SCT_ALLPAIRS_GRAB")) {
     const int gg = atoi(g);
     if (gg > 0) p->grab = gg;

@@ -263,6 +263,39 @@ def main():
                 cbs.append([cb.hex(), str(ThreeBit.encode(cb))])
     out["r1_cell_barcodes"] = cbs
 
+    # nearest whitelist, composed from the reference's own distances (no reference
+    # function exists): 1k list as ThreeBit/TwoBit whitelist, queries =
+    # real R1 cell barcodes + perturbed whitelist members (substitution, N, two edits)
+    wl_seqs = [l for l in raw.split(b"\n") if l]
+    near = {}
+    for name, enc in (("three", ThreeBit), ("two", TwoBit)):
+        wl_codes = [enc.encode(x) for x in wl_seqs]
+        qseqs = [bytes.fromhex(c[0]) for c in cbs] if name == "three" else []
+        for k in range(120):
+            base = bytearray(wl_seqs[rng.randrange(len(wl_seqs))])
+            for _ in range(k % 3):
+                pos = rng.randrange(16)
+                base[pos] = rng.choice(b"ACGTN" if name == "three" else b"ACGT")
+            qseqs.append(bytes(base))
+        qcodes = [enc.encode(x) for x in qseqs]
+        res = {}
+        for max_d in (0, 1, 2):
+            idx, dist = [], []
+            for q in qcodes:
+                ds = [enc.hamming_distance(q, w) for w in wl_codes]
+                m = min(ds)
+                if m <= max_d:
+                    hits = [j for j, d in enumerate(ds) if d == m]
+                    idx.append(hits[0] if len(hits) == 1 else -2)
+                    dist.append(m)
+                else:
+                    idx.append(-1)
+                    dist.append(255)
+            res[str(max_d)] = {"index": idx, "dist": dist}
+        near[name] = {"whitelist": [str(c) for c in wl_codes], "queries": [str(c) for c in qcodes],
+                      "result": res}
+    out["nearest"] = near
+
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(out, f, separators=(",", ":"))
     print("wrote golden.json")

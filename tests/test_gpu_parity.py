@@ -301,3 +301,97 @@ def test_allpairs_737k_properties():
     ref = O.c_hist_rows(sub)[:17]
     assert hs.astype(np.int64).tolist() == ref.tolist()
     plan.close()
+
+
+# ---------------------------------------------------------------- nearest whitelist
+def test_nearest_golden(golden):
+    for name, enc in (("three", "ThreeBit"), ("two", "TwoBit")):
+        rec = golden["nearest"][name]
+        wl = np.array([int(c) for c in rec["whitelist"]], dtype=np.uint64)
+        q = np.array([int(c) for c in rec["queries"]], dtype=np.uint64)
+        for md, want in rec["result"].items():
+            idx, dist = barcode.nearest_whitelist(q, wl, max_distance=int(md), encoding=enc)
+            assert idx.tolist() == want["index"], (name, md)
+            assert dist.tolist() == want["dist"], (name, md)
+
+
+def _config4_queries(wl_seqs, nq, rng, alphabet=b"ACGT"):
+    """50% exact whitelist draws, 25% one substitution, 15% one N, 10% random."""
+    L = wl_seqs.shape[1]
+    picks = wl_seqs[rng.integers(0, wl_seqs.shape[0], nq)].copy()
+    kind = rng.random(nq)
+    pos = rng.integers(0, L, nq)
+    sub = (kind >= 0.5) & (kind < 0.75)
+    picks[sub, pos[sub]] = np.frombuffer(alphabet, np.uint8)[rng.integers(0, len(alphabet), sub.sum())]
+    nn = (kind >= 0.75) & (kind < 0.9)
+    picks[nn, pos[nn]] = ord("N")
+    rnd = kind >= 0.9
+    picks[rnd] = np.frombuffer(alphabet, np.uint8)[rng.integers(0, len(alphabet), (rnd.sum(), L))]
+    return picks
+
+
+@pytest.mark.parametrize("kind,max_d", [(3, 0), (3, 1), (3, 2), (3, 3), (2, 0), (2, 1), (2, 2)])
+def test_nearest_vs_bruteforce(kind, max_d):
+    rng = np.random.default_rng(100 + 10 * kind + max_d)
+    wl_codes2 = synthetic.whitelist_codes(3000, 16, seed=kind * 7 + max_d)
+    wl_seqs = synthetic.decode_ascii(wl_codes2, 16)
+    q_seqs = _config4_queries(wl_seqs, 4000, rng, b"ACGT" if kind == 3 else b"ACGT")
+    if kind == 2:
+        q_seqs[q_seqs == ord("N")] = ord("A")
+    enc = ThreeBit if kind == 3 else TwoBit
+    wl = enc.encode_array(wl_seqs)
+    q = enc.encode_array(q_seqs)
+    idx, dist = barcode.nearest_whitelist(q, wl, max_distance=max_d, encoding=kind)
+    ridx, rdist = O.nearest_bruteforce(kind, wl, q, max_d)
+    assert np.array_equal(idx, ridx)
+    assert np.array_equal(dist, rdist)
+
+
+def test_nearest_ties_and_edges():
+    # two whitelist codes at distance 2; the midpoint query is at distance 1 from both
+    a = ThreeBit.encode(b"ACGTACGTACGTACGT")
+    b = ThreeBit.encode(b"ACGTACGTACGTACTA")
+    mid = ThreeBit.encode(b"ACGTACGTACGTACTT")
+    wl = np.array([a, b], dtype=np.uint64)
+    idx, dist = barcode.nearest_whitelist([mid, a, b, ThreeBit.encode(b"N" * 16)], wl, 1)
+    assert idx.tolist() == [-2, 0, 1, -1]
+    assert dist.tolist() == [1, 0, 0, 255]
+    # duplicated whitelist entries are distinct indices -> tie
+    idx, dist = barcode.nearest_whitelist([a], np.array([a, a], dtype=np.uint64), 0)
+    assert idx.tolist() == [-2] and dist.tolist() == [0]
+    # empty inputs
+    idx, dist = barcode.nearest_whitelist([], wl, 1)
+    assert idx.size == 0
+    idx, dist = barcode.nearest_whitelist([a], np.array([], dtype=np.uint64), 1)
+    assert idx.tolist() == [-1]
+
+
+def test_barcodes_nearest_method(golden):
+    rec = golden["nearest"]["two"]
+    s = barcode.PriorBarcodeSet.from_iterable_encoded([int(c) for c in rec["whitelist"]], 16)
+    idx, dist = s.nearest(np.array([int(c) for c in rec["queries"]], dtype=np.uint64), 1)
+    assert idx.tolist() == rec["result"]["1"]["index"]
+
+
+def test_allpairs_counter_flush_path(monkeypatch):
+    # force the in-kernel u32 -> u64 counter flush after every work-queue pull
+    monkeypatch.setenv("SCT_ALLPAIRS_FLUSH_ITEMS", "1")
+    monkeypatch.setenv("SCT_ALLPAIRS_GRAB", "3")
+    codes = synthetic.whitelist_codes(9000, 16, seed=21)
+    hist = _lib.hamming_hist_allpairs(codes, 32)
+    assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
+
+
+@pytest.mark.parametrize("L", [4, 15, 16, 21, 28, 32])
+def test_encode_tiled_matches_bytewise(L):
+    rng = np.random.default_rng(L)
+    n = 100_003
+    seqs = np.frombuffer(b"ACGTacgt", np.uint8)[rng.integers(0, 8, (n, L))]
+    for enc, ref in ((TwoBit, O.two_bit_encode), (ThreeBit, O.three_bit_encode)):
+        if enc is ThreeBit and L > 21:
+            continue
+        codes, gc = enc.encode_array(seqs, return_gc=True)
+        for r in list(range(0, n, 997)) + [n - 1]:
+            s = seqs[r].tobytes()
+            assert int(codes[r]) == ref(s)
+            assert int(gc[r]) == s.upper().count(b"C") + s.upper().count(b"G")

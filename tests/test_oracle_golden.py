@@ -112,3 +112,14 @@ def test_item_enumeration_covers_all_pairs():
                           pairs.ctypes.data, 1)
     assert int(pairs[0]) == 3000 * 2999 // 2
     assert hist.tolist() == ref.tolist()
+
+
+def test_nearest_bruteforce(golden):
+    for name, kind in (("three", 3), ("two", 2)):
+        rec = golden["nearest"][name]
+        wl = [int(c) for c in rec["whitelist"]]
+        q = [int(c) for c in rec["queries"]]
+        for md, want in rec["result"].items():
+            idx, dist = O.nearest_bruteforce(kind, wl, q, int(md))
+            assert idx.tolist() == want["index"]
+            assert dist.tolist() == want["dist"]

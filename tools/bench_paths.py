@@ -1,0 +1,186 @@
+"""Secondary measurements for SURVEY.md §8(d) rows other than the headline
+(bench.py): the HBM-bound encoder, nearest-whitelist correction (config 4) and the
+3.69M all-pairs (config 5), one GPU.  Prints one JSON object per measurement.
+
+  python tools/bench_paths.py [--reads 1000000000] [--queries 100000000] [--skip-allpairs5]
+
+Encoder (config 5 read stream): reads are random 28-bp ACGT records generated on the
+device; one launch of sct_encode(kind=2) writes codes (uint64), GC (uint8) and flags
+(uint8).  Algorithmic bytes/read = 28 + 8 + 1 + 1 = 38.
+Nearest (config 4): whitelist = the config-2 737,280 codes re-encoded as ThreeBit;
+100M queries = 50% exact whitelist draws, 25% one substitution, 15% one N, 10% random,
+built on the device from the seeded whitelist.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from sctools_amd import _lib, synthetic  # noqa: E402
+
+HBM_PEAK = 8.0e12
+
+
+def timed(fn, reps, stream):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts)), float(np.min(ts))
+
+
+def bench_encode(n_reads, L=28):
+    dev = torch.device("cuda")
+    s = torch.cuda.current_stream()
+    lut = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev).manual_seed(5)
+    seqs = lut[torch.randint(0, 4, (n_reads, L), device=dev, dtype=torch.uint8, generator=g).long()] \
+        if n_reads * L <= 2 ** 31 else None
+    if seqs is None:  # build in slices to bound the int64 index temporaries
+        seqs = torch.empty((n_reads, L), dtype=torch.uint8, device=dev)
+        step = 2 ** 26
+        for a in range(0, n_reads, step):
+            b = min(n_reads, a + step)
+            seqs[a:b] = lut[torch.randint(0, 4, (b - a, L), device=dev, generator=g).long()]
+    codes = torch.empty(n_reads, dtype=torch.int64, device=dev)
+    gc = torch.empty(n_reads, dtype=torch.uint8, device=dev)
+    flags = torch.empty(n_reads, dtype=torch.uint8, device=dev)
+    lib = _lib.lib()
+
+    def run():
+        _lib.check(lib.sct_encode(2, _lib._vp(seqs.data_ptr()), n_reads, L, L, _lib._vp(codes.data_ptr()),
+                                  _lib._vp(gc.data_ptr()), _lib._vp(flags.data_ptr()), _lib._vp(s.cuda_stream)))
+
+    med, mn = timed(run, 5, s)
+    # spot-check parity of a slice against a host re-encode through the drop-in's batch path
+    k = 4096
+    host = seqs[:k].cpu().numpy()
+    ref = np.zeros(k, dtype=np.uint64)
+    for p in range(L):
+        v = np.array([0, 0, 0, 0], dtype=np.uint64)
+        ch = host[:, p]
+        val = np.select([ch == 65, ch == 67, ch == 84, ch == 71], [0, 1, 2, 3]).astype(np.uint64)
+        ref = (ref << np.uint64(2)) | val
+        del v
+    assert np.array_equal(codes[:k].cpu().numpy().view(np.uint64), ref), "encode parity"
+    byts = n_reads * (L + 8 + 1 + 1)
+    del seqs, codes, gc, flags
+    torch.cuda.empty_cache()
+    return {"path": "encode TwoBit+GC (config 5 read stream)", "reads": n_reads, "L": L,
+            "median_ms": med, "min_ms": mn, "reads_per_s": n_reads / (med * 1e-3),
+            "roofline": {"bound": "hbm", "achieved": byts / (med * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": byts / (med * 1e-3) / HBM_PEAK,
+                         "bytes_per_read": L + 10}}
+
+
+def two_to_three(codes2, L=16):
+    """TwoBit codes -> ThreeBit codes of the same sequence (A0 C1 T2 G3 -> A2 C1 T4 G3)."""
+    m = np.array([2, 1, 4, 3], dtype=np.uint64)
+    out = np.zeros(codes2.size, dtype=np.uint64)
+    for p in range(L):
+        v = (codes2 >> np.uint64(2 * p)) & np.uint64(3)
+        out |= m[v.astype(np.intp)] << np.uint64(3 * p)
+    return out
+
+
+def bench_nearest(nq, max_d=1):
+    dev = torch.device("cuda")
+    s = torch.cuda.current_stream()
+    n, L, seed = synthetic.CONFIGS[2]
+    wl = two_to_three(synthetic.whitelist_codes(n, L, seed), L)
+    d_wl = torch.from_numpy(wl.view(np.int64)).to(dev)
+    g = torch.Generator(device=dev).manual_seed(4)
+    pick = torch.randint(0, n, (nq,), device=dev, generator=g)
+    q = d_wl[pick].clone()
+    kind = torch.rand(nq, device=dev, generator=g)
+    pos = torch.randint(0, L, (nq,), device=dev, generator=g) * 3
+    base = torch.randint(1, 5, (nq,), device=dev, generator=g)
+    clear = ~(torch.full_like(q, 7) << pos)
+    sub = (kind >= 0.5) & (kind < 0.75)
+    q = torch.where(sub, (q & clear) | (base << pos), q)
+    nmask = (kind >= 0.75) & (kind < 0.9)
+    q = torch.where(nmask, (q & clear) | (torch.full_like(q, 6) << pos), q)
+    rnd = kind >= 0.9
+    r = torch.zeros_like(q)
+    for p in range(L):
+        r |= torch.randint(1, 5, (nq,), device=dev, generator=g) << (3 * p)
+    q = torch.where(rnd, r, q)
+    idx = torch.empty(nq, dtype=torch.int32, device=dev)
+    dist = torch.empty(nq, dtype=torch.uint8, device=dev)
+    t0 = time.perf_counter()
+    plan = _lib.NearestPlan(3, d_wl.data_ptr(), n, 3 * L, max_d, s.cuda_stream)
+    torch.cuda.synchronize()
+    build_ms = (time.perf_counter() - t0) * 1e3
+
+    def run():
+        plan.query(q.data_ptr(), nq, idx.data_ptr(), dist.data_ptr(), s.cuda_stream)
+
+    med, mn = timed(run, 5, s)
+    # parity spot check against the oracle brute force on a sample
+    from oracle import oracle as O
+    samp = torch.randint(0, nq, (2000,), device=dev, generator=g)
+    ridx, rdist = O.nearest_bruteforce(3, wl, q[samp].cpu().numpy().view(np.uint64), max_d)
+    assert np.array_equal(idx[samp].cpu().numpy(), ridx) and np.array_equal(dist[samp].cpu().numpy(), rdist)
+    hist = torch.bincount(idx.clamp(min=-2).add(2).clamp(max=2).long(), minlength=3).tolist()
+    plan.close()
+    byts = nq * (8 + 4 + 1)
+    return {"path": "nearest whitelist ThreeBit max_d=%d (config 4)" % max_d, "whitelist": n, "queries": nq,
+            "median_ms": med, "min_ms": mn, "queries_per_s": nq / (med * 1e-3), "index_build_ms": build_ms,
+            "brute_force_equiv_pairs_per_s": nq * n / (med * 1e-3),
+            "outcome_counts": {"tie": hist[0], "none": hist[1], "hit": hist[2]},
+            "roofline": {"bound": "hbm", "achieved": byts / (med * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": byts / (med * 1e-3) / HBM_PEAK, "bytes_per_query": 13,
+                         "note": "stream bytes only; bucket reads are L2/MALL-resident"}}
+
+
+def bench_allpairs5():
+    dev = torch.device("cuda")
+    s = torch.cuda.current_stream()
+    n, L, seed = synthetic.CONFIGS[5]
+    codes = synthetic.whitelist_codes(n, L, seed)
+    d = torch.from_numpy(codes.view(np.int64)).to(dev)
+    plan = _lib.AllPairsPlan(d.data_ptr(), n, 2 * L)
+    counts = torch.zeros(plan.nbins, dtype=torch.int64, device=dev)
+
+    def run():
+        counts.zero_()
+        plan.build(s.cuda_stream)
+        plan.count(counts.data_ptr(), stream=s.cuda_stream)
+
+    med, mn = timed(run, 3, s)
+    hist = _lib.counts_to_hist(counts.cpu().numpy().view(np.uint64))
+    assert int(hist.sum()) == plan.pairs
+    plan.close()
+    return {"path": "all-pairs histogram config 5 (3,686,400 codes)", "pairs": plan.pairs, "median_ms": med,
+            "min_ms": mn, "pairs_per_s": plan.pairs / (med * 1e-3), "hist": [int(x) for x in hist]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=1_000_000_000)
+    ap.add_argument("--queries", type=int, default=100_000_000)
+    ap.add_argument("--skip-allpairs5", action="store_true")
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    _lib.check(_lib.lib().sct_set_device(0))
+    print(json.dumps(bench_encode(a.reads)), flush=True)
+    print(json.dumps(bench_nearest(a.queries, 1)), flush=True)
+    if not a.skip_allpairs5:
+        print(json.dumps(bench_allpairs5()), flush=True)
+
+
+if __name__ == "__main__":
+    main()
