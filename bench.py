@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 5])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     return ap.parse_args()
 
 
@@ -91,8 +92,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one process per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share them
+        local_dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local_dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())

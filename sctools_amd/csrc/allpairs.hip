@@ -167,13 +167,23 @@ __device__ __forceinline__ uint32_t pair_mask(int64_t i, int64_t jg, int64_t n) 
   return i < n ? mask : 0u;
 }
 
-template <int NPP, bool MASKED>
+template <int NPP, bool MASKED, int ABL = 0>
 __device__ __forceinline__ void one_group(const uint32_t (&s0)[NPP], const uint32_t (&s1)[NPP],
                                           int64_t i, int64_t jg, int64_t n,
                                           uint32_t (&cnt)[2 * NPP], uint32_t& cnt0) {
   constexpr int B = Geom<NPP>::B;
   uint32_t d[B];
-  adder_tree<NPP, B>(s0, s1, d);
+  if constexpr (ABL == 2) {  // ablation: no adder tree (planes straight into counting)
+#pragma unroll
+    for (int b = 0; b < B; ++b) d[b] = s0[b % NPP] ^ s1[(b + 1) % NPP];
+  } else {
+    adder_tree<NPP, B>(s0, s1, d);
+  }
+  if constexpr (ABL == 1) {  // ablation: no counting (keep the planes live, 1 op each)
+#pragma unroll
+    for (int b = 0; b < B; ++b) cnt[b] ^= d[b];
+    return;
+  }
   if constexpr (MASKED) {
     const uint32_t mask = pair_mask(i, jg, n);
 #pragma unroll
@@ -183,7 +193,7 @@ __device__ __forceinline__ void one_group(const uint32_t (&s0)[NPP], const uint3
   count_subsets<2 * NPP, B>(d, cnt);
 }
 
-template <int NPP, bool MASKED, int UNROLL>
+template <int NPP, bool MASKED, int UNROLL, int ABL = 0>
 __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uint64_t q, int64_t i,
                                              int64_t j0, int64_t n, uint32_t (&cnt)[2 * NPP],
                                              uint32_t& cnt0) {
@@ -198,14 +208,20 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
       uint32_t s0a[NPP], s1a[NPP], s0b[NPP], s1b[NPP];
 #pragma unroll
       for (int pp = 0; pp < NPP; ++pp) {
-        const uint4 e = tile[h * NPP * 16 + off[pp]];
+        uint4 e;
+        if constexpr (ABL == 3) {  // ablation: no LDS reads (lane-varying fake planes)
+          e = make_uint4(off[pp] * 0x9E3779B9u + h, off[pp] ^ (h * 0x85EBCA6Bu), off[pp] + 77u * h,
+                         off[pp] * 3u - h);
+        } else {
+          e = tile[h * NPP * 16 + off[pp]];
+        }
         s0a[pp] = e.x;
         s1a[pp] = e.y;
         s0b[pp] = e.z;
         s1b[pp] = e.w;
       }
-      one_group<NPP, MASKED>(s0a, s1a, i, j0 + 64 * h, n, cnt, cnt0);
-      one_group<NPP, MASKED>(s0b, s1b, i, j0 + 64 * h + 32, n, cnt, cnt0);
+      one_group<NPP, MASKED, ABL>(s0a, s1a, i, j0 + 64 * h, n, cnt, cnt0);
+      one_group<NPP, MASKED, ABL>(s0b, s1b, i, j0 + 64 * h + 32, n, cnt, cnt0);
     }
   }
   if constexpr (!MASKED) cnt0 += Gm::CB;
@@ -214,7 +230,13 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
 // Count-kernel variants (A/B-selectable with SCT_ALLPAIRS_VARIANT): 1 = one group pair
 // per loop trip (108 VGPRs), 2 = two per trip (default, 124 VGPRs, 4 waves/SIMD).
 // Register prefetch / ping-pong variants measured slower and were dropped.
-template <int V> struct Variant { static constexpr int UNROLL = V; };
+template <int V> struct Variant { static constexpr int UNROLL = V, ABL = 0; };
+#ifdef SCT_ABLATION
+// ablation builds (wrong results, timing only): 11 no counting, 12 no tree, 13 no LDS reads
+template <> struct Variant<11> { static constexpr int UNROLL = 2, ABL = 1; };
+template <> struct Variant<12> { static constexpr int UNROLL = 2, ABL = 2; };
+template <> struct Variant<13> { static constexpr int UNROLL = 2, ABL = 3; };
+#endif
 
 // Workgroup reduction of the per-lane counters: 64-lane butterfly (shfl_xor, lowered to
 // DPP/ds_swizzle/ds_bpermute), then LDS across the waves, then one u64 atomic per counter;
@@ -312,9 +334,9 @@ __global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __re
       const int64_t j0 = c * Gm::CB;
       const bool masked = ((r + 1) * RB > j0) || (j0 + Gm::CB > n);
       if (masked)
-        process_item<NPP, true, Variant<V>::UNROLL>(tile, q, i, j0, n, cnt, cnt0);
+        process_item<NPP, true, Variant<V>::UNROLL, Variant<V>::ABL>(tile, q, i, j0, n, cnt, cnt0);
       else
-        process_item<NPP, false, Variant<V>::UNROLL>(tile, q, i, j0, n, cnt, cnt0);
+        process_item<NPP, false, Variant<V>::UNROLL, Variant<V>::ABL>(tile, q, i, j0, n, cnt, cnt0);
       q = q_next;
       i = i_next;
     }
@@ -407,6 +429,11 @@ int launch_count(sct_allpairs_plan* p, int64_t b, int64_t e, uint64_t* d_counts,
                      reinterpret_cast<unsigned long long*>(d_counts))
   switch (variant) {
     case 1: SCT_LAUNCH_V(1); break;
+#ifdef SCT_ABLATION
+    case 11: if constexpr (NPP == 8) SCT_LAUNCH_V(11); break;
+    case 12: if constexpr (NPP == 8) SCT_LAUNCH_V(12); break;
+    case 13: if constexpr (NPP == 8) SCT_LAUNCH_V(13); break;
+#endif
     default: SCT_LAUNCH_V(2); break;
   }
 #undef SCT_LAUNCH_V
@@ -531,7 +558,7 @@ extern "C" int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int 
     cus = 256;
   if (const char* v = getenv("SCT_ALLPAIRS_VARIANT")) {
     const int vv = atoi(v);
-    if (vv >= 1 && vv <= 2) p->variant = vv;
+    if ((vv >= 1 && vv <= 2) || (vv >= 11 && vv <= 13)) p->variant = vv;
   }
   p->grid = grid_for(p->npp, cus, p->variant);
   if (const char* f = getenv("SCT_ALLPAIRS_FLUSH_ITEMS")) p->flush_items = atoll(f);

@@ -127,54 +127,60 @@ __global__ __launch_bounds__(WG) void encode_kernel(int kind, const uint8_t* __r
 // coalesced 16-byte loads into LDS, then each lane packs its record from LDS (dword reads
 // when L % 4 == 0, conflict-free for odd L/4) through the LDS byte LUT.  The staging
 // turns the per-lane, L-byte-strided global loads of encode_kernel into full-line reads.
-template <int BITS>
+template <int BITS, int R>
 __global__ __launch_bounds__(WG) void encode_tiled_kernel(const uint8_t* __restrict__ seqs,
                                                           int64_t n, int L,
                                                           uint64_t* __restrict__ codes,
                                                           uint8_t* __restrict__ gc,
                                                           uint8_t* __restrict__ flags) {
   __shared__ uint8_t lut[256];
-  extern __shared__ __attribute__((aligned(16))) uint4 stage4[];  // WG * L bytes
+  extern __shared__ __attribute__((aligned(16))) uint4 stage4[];  // R * WG * L bytes
   fill_lut(lut, BITS);
   const uint8_t* stage = reinterpret_cast<const uint8_t*>(stage4);
   const int tid = threadIdx.x;
-  const int64_t ntiles = (n + WG - 1) / WG;
+  constexpr int TILE = R * WG;  // records per workgroup iteration: R in flight per lane
+  const int64_t ntiles = (n + TILE - 1) / TILE;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t r0 = tile * WG;
-    const int64_t nrec = n - r0 < WG ? n - r0 : WG;
+    const int64_t r0 = tile * TILE;
+    const int64_t nrec = n - r0 < TILE ? n - r0 : TILE;
     const int64_t nbytes = nrec * L;
-    const uint8_t* src = seqs + r0 * L;  // 16-byte aligned: WG * L is a multiple of 16
+    const uint8_t* src = seqs + r0 * L;  // 16-byte aligned: TILE * L is a multiple of 16
     const int64_t n16 = nbytes >> 4;
     for (int64_t k = tid; k < n16; k += WG) stage4[k] = reinterpret_cast<const uint4*>(src)[k];
     for (int64_t k = (n16 << 4) + tid; k < nbytes; k += WG)
       reinterpret_cast<uint8_t*>(stage4)[k] = src[k];
     __syncthreads();
-    if (tid < nrec) {
-      const uint8_t* rec = stage + tid * L;
-      uint64_t code = 0;
-      uint32_t fl = 0;
-      if ((L & 3) == 0) {
-        const uint32_t* rw = reinterpret_cast<const uint32_t*>(rec);
-        for (int k = 0; k < (L >> 2); ++k) {
-          const uint32_t w = rw[k];
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const uint32_t e = lut[(w >> (8 * b)) & 0xFFu];
+    for (int rr = 0; rr < R; ++rr) {
+      const int lr = rr * WG + tid;  // consecutive lanes -> consecutive records (coalesced stores)
+      if (lr < nrec) {
+        const uint8_t* rec = stage + (int64_t)lr * L;
+        uint64_t code = 0;
+        uint32_t fl = 0;
+        if ((L & 3) == 0) {
+          const uint32_t* rw = reinterpret_cast<const uint32_t*>(rec);
+          for (int k = 0; k < (L >> 2); ++k) {
+            const uint32_t w = rw[k];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const uint32_t e = lut[(w >> (8 * b)) & 0xFFu];
+              code = (code << BITS) | (e & 7u);
+              fl |= e;
+            }
+          }
+        } else {
+          for (int p = 0; p < L; ++p) {
+            const uint32_t e = lut[rec[p]];
             code = (code << BITS) | (e & 7u);
             fl |= e;
           }
         }
-      } else {
-        for (int p = 0; p < L; ++p) {
-          const uint32_t e = lut[rec[p]];
-          code = (code << BITS) | (e & 7u);
-          fl |= e;
-        }
+        const int64_t r = r0 + lr;
+        codes[r] = code;
+        if (gc)
+          gc[r] = (uint8_t)__popcll(code & (BITS == 2 ? 0x5555555555555555ull : 0x9249249249249249ull));
+        if (flags) flags[r] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
       }
-      const int64_t r = r0 + tid;
-      codes[r] = code;
-      if (gc) gc[r] = (uint8_t)__popcll(code & (BITS == 2 ? 0x5555555555555555ull : 0x9249249249249249ull));
-      if (flags) flags[r] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
     }
     __syncthreads();
   }
@@ -337,12 +343,14 @@ extern "C" int sct_encode(int kind, const uint8_t* seqs, int64_t n, int64_t stri
   SCT_CHECK(codes != nullptr && (L == 0 || seqs != nullptr), "NULL pointer");
   const int words = words_for(kind, L);
   if (stride == L && words == 1 && L > 0 && L <= 64 && (uintptr_t)seqs % 16 == 0) {
-    const size_t lds = (size_t)WG * L;
+    constexpr int R = 4;  // 4 x 256 records staged per iteration (28 KiB at L = 28)
+    const size_t lds = (size_t)R * WG * L;
+    const unsigned grid = (unsigned)std::min<int64_t>(sct::ceil_div(n, R * WG), 4096);
     if (kind == 2)
-      hipLaunchKernelGGL(encode_tiled_kernel<2>, dim3(grid_for(n)), dim3(WG), lds,
+      hipLaunchKernelGGL((encode_tiled_kernel<2, R>), dim3(grid), dim3(WG), lds,
                          sct::as_stream(stream), seqs, n, L, codes, gc, flags);
     else
-      hipLaunchKernelGGL(encode_tiled_kernel<3>, dim3(grid_for(n)), dim3(WG), lds,
+      hipLaunchKernelGGL((encode_tiled_kernel<3, R>), dim3(grid), dim3(WG), lds,
                          sct::as_stream(stream), seqs, n, L, codes, gc, flags);
     SCT_LAUNCH_CHECK();
     return SCT_OK;

@@ -263,6 +263,35 @@ def main():
                 cbs.append([cb.hex(), str(ThreeBit.encode(cb))])
     out["r1_cell_barcodes"] = cbs
 
+    # from_whitelist line semantics (barcode.py:96-97: binary lines, last byte chopped)
+    import tempfile
+    wl_cases = []
+    variants = {
+        "lf": b"ACGTACGTACGTACGT\nTTTTCCCCGGGGAAAA\nACGTACGTACGTACGT\n",
+        "no_final_newline": b"ACGTACGTACGTACGT\nTTTTCCCCGGGGAAAA",
+        "crlf": b"ACGTACGTACGTACGT\r\nTTTTCCCCGGGGAAAA\r\n",
+        "empty_lines": b"ACGT\n\nACGT\n\n",
+        "ambiguous": b"ACGTNNNN\nACGTRYKM\n",
+        "lowercase": b"acgtacgtacgtacgt\nggggcccc\n",
+        "ragged": b"ACGT\nACGTACGT\nA\n",
+    }
+    for name, content in variants.items():
+        with tempfile.NamedTemporaryFile(delete=False) as tf:
+            tf.write(content)
+            path = tf.name
+        random.seed(11)
+        rec = {"name": name, "content": content.hex()}
+        try:
+            b = bc.Barcodes.from_whitelist(path, 16)
+            rec["codes"] = [str(k) for k in b]
+            rec["counts"] = [b[k] for k in b]
+        except Exception as e:
+            rec["error"] = exc_record(e)
+        rec["after"] = random.getrandbits(32)
+        os.unlink(path)
+        wl_cases.append(rec)
+    out["from_whitelist"] = wl_cases
+
     # nearest whitelist, composed from the reference's own distances (no reference
     # function exists): 1k list as ThreeBit/TwoBit whitelist, queries =
     # real R1 cell barcodes + perturbed whitelist members (substitution, N, two edits)

@@ -395,3 +395,19 @@ def test_encode_tiled_matches_bytewise(L):
             s = seqs[r].tobytes()
             assert int(codes[r]) == ref(s)
             assert int(gc[r]) == s.upper().count(b"C") + s.upper().count(b"G")
+
+
+def test_from_whitelist_line_semantics(golden, tmp_path):
+    for rec in golden["from_whitelist"]:
+        p = tmp_path / (rec["name"] + ".txt")
+        p.write_bytes(bytes.fromhex(rec["content"]))
+        random.seed(11)
+        if "error" in rec:
+            with pytest.raises(KeyError) as ei:
+                barcode.Barcodes.from_whitelist(str(p), 16)
+            assert list(ei.value.args) == rec["error"]["args"], rec["name"]
+        else:
+            b = barcode.Barcodes.from_whitelist(str(p), 16)
+            assert [str(k) for k in b] == rec["codes"], rec["name"]
+            assert [b[k] for k in b] == rec["counts"], rec["name"]
+        assert random.getrandbits(32) == rec["after"], rec["name"]

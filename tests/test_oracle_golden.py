@@ -123,3 +123,17 @@ def test_nearest_bruteforce(golden):
             idx, dist = O.nearest_bruteforce(kind, wl, q, int(md))
             assert idx.tolist() == want["index"]
             assert dist.tolist() == want["dist"]
+
+
+def test_from_whitelist_semantics_oracle(golden):
+    from collections import Counter
+    for rec in golden["from_whitelist"]:
+        lines = bytes.fromhex(rec["content"]).splitlines(keepends=True)
+        random.seed(11)
+        try:
+            c = Counter(O.two_bit_encode(ln[:-1]) for ln in lines)
+            assert "error" not in rec
+            assert [str(k) for k in c] == rec["codes"] and list(c.values()) == rec["counts"]
+        except KeyError as e:
+            assert list(e.args) == rec["error"]["args"]
+        assert random.getrandbits(32) == rec["after"]
