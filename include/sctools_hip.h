@@ -58,6 +58,13 @@ int sct_encode(int kind, const uint8_t* seqs, int64_t n, int64_t stride, int L,
 int sct_encode_host(int kind, const uint8_t* seqs, int64_t n, int64_t stride, int L,
                     uint64_t* codes, uint8_t* gc, uint8_t* flags);
 
+/* Host-resident stream of n records (stride L, one limb: L <= 32 TwoBit / 21 ThreeBit):
+ * chunks of `chunk` records (<= 0: 16M) pipeline H2D / encode / D2H over 3 streams; the
+ * caller's buffers are page-locked in place for the call unless already pinned.  gc and
+ * flags are required.  Returns when all outputs are in host memory. */
+int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, int L, uint64_t* codes,
+                           uint8_t* gc, uint8_t* flags, int64_t chunk);
+
 /* ---------------------------------------------------------------- decoders
  * TwoBit(L).decode (encodings.py:90-100): exactly L bytes from the LSB upward,
  * bits above 2L ignored.  out: n*L bytes.

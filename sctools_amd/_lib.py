@@ -34,6 +34,7 @@ SIGNATURES = {
     "sct_set_device": [_i32],
     "sct_encode": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
     "sct_encode_host": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp],
+    "sct_encode_stream_host": [_i32, _vp, _i64, _i32, _vp, _vp, _vp, _i64],
     "sct_decode2": [_vp, _i64, _i32, _i32, _vp, _vp],
     "sct_decode2_host": [_vp, _i64, _i32, _i32, _vp],
     "sct_decode3": [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp],
@@ -165,6 +166,18 @@ def encode(kind, seqs, L):
     flags = np.zeros(n, dtype=np.uint8)
     gc = np.zeros(n, dtype=np.uint8) if L <= 255 else None
     check(lib().sct_encode_host(kind, _ptr(seqs), n, L, L, _ptr(codes), _ptr(gc), _ptr(flags)))
+    return codes, gc, flags
+
+
+def encode_stream(kind, seqs, chunk=0):
+    """Host (n, L) uint8 records -> (codes uint64[n], gc uint8[n], flags uint8[n]) through the
+    pipelined H2D/encode/D2H stream (one limb per code)."""
+    seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
+    n, L = seqs.shape
+    codes = np.empty(n, dtype=np.uint64)
+    gc = np.empty(n, dtype=np.uint8)
+    flags = np.empty(n, dtype=np.uint8)
+    check(lib().sct_encode_stream_host(kind, _ptr(seqs), n, L, _ptr(codes), _ptr(gc), _ptr(flags), chunk))
     return codes, gc, flags
 
 

@@ -473,6 +473,72 @@ extern "C" int sct_base_frequency_host(const uint64_t* codes, int64_t n, int L, 
   return from_dev(out, dout, (size_t)L * 4);
 }
 
+// Host-resident stream (config 5): records live in host memory; chunks flow through
+// NSTAGE device buffers on NSTAGE streams so that the H2D copy of one chunk, the encode
+// of another and the D2H copy of a third overlap (PCIe-bound: L + 10 bytes per read cross
+// the link).  Caller buffers are page-locked in place for the call unless already pinned.
+extern "C" int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, int L,
+                                      uint64_t* codes, uint8_t* gc, uint8_t* flags,
+                                      int64_t chunk) {
+  SCT_CHECK(kind == 2 || kind == 3, "kind must be 2 or 3");
+  SCT_CHECK(n >= 0 && L >= 1 && words_for(kind, L) == 1, "stream encode needs 1 <= L and one limb");
+  SCT_CHECK(gc != nullptr && flags != nullptr && codes != nullptr && seqs != nullptr, "NULL pointer");
+  if (n == 0) return SCT_OK;
+  if (chunk <= 0) chunk = 1 << 24;
+  chunk = std::min<int64_t>(chunk, n);
+  constexpr int NSTAGE = 3;
+  struct Reg {
+    void* p = nullptr;
+    ~Reg() {
+      if (p) (void)hipHostUnregister(p);
+    }
+  } reg[4];
+  auto pin = [&](Reg& r, const void* ptr, size_t bytes) -> int {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, ptr) == hipSuccess && at.type != hipMemoryTypeUnregistered)
+      return SCT_OK;  // already pinned or device-visible
+    (void)hipGetLastError();
+    SCT_HIP(hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault));
+    r.p = const_cast<void*>(ptr);
+    return SCT_OK;
+  };
+  int rc;
+  if ((rc = pin(reg[0], seqs, (size_t)n * L)) != SCT_OK) return rc;
+  if ((rc = pin(reg[1], codes, (size_t)n * 8)) != SCT_OK) return rc;
+  if ((rc = pin(reg[2], gc, (size_t)n)) != SCT_OK) return rc;
+  if ((rc = pin(reg[3], flags, (size_t)n)) != SCT_OK) return rc;
+  sct::DevBuf din[NSTAGE], dcode[NSTAGE], dgc[NSTAGE], dfl[NSTAGE];
+  hipStream_t st[NSTAGE] = {};
+  struct Streams {
+    hipStream_t* s;
+    ~Streams() {
+      for (int k = 0; k < NSTAGE; ++k)
+        if (s[k]) (void)hipStreamDestroy(s[k]);
+    }
+  } guard{st};
+  for (int k = 0; k < NSTAGE; ++k) {
+    SCT_HIP(hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking));
+    SCT_HIP(din[k].alloc((size_t)chunk * L));
+    SCT_HIP(dcode[k].alloc((size_t)chunk * 8));
+    SCT_HIP(dgc[k].alloc((size_t)chunk));
+    SCT_HIP(dfl[k].alloc((size_t)chunk));
+  }
+  int64_t c = 0;
+  for (int64_t r0 = 0; r0 < n; r0 += chunk, ++c) {
+    const int k = (int)(c % NSTAGE);  // stage k's previous chunk is ordered before on st[k]
+    const int64_t m = std::min<int64_t>(chunk, n - r0);
+    SCT_HIP(hipMemcpyAsync(din[k].p, seqs + r0 * L, (size_t)m * L, hipMemcpyHostToDevice, st[k]));
+    rc = sct_encode(kind, (const uint8_t*)din[k].p, m, L, L, (uint64_t*)dcode[k].p, (uint8_t*)dgc[k].p,
+                    (uint8_t*)dfl[k].p, st[k]);
+    if (rc != SCT_OK) return rc;
+    SCT_HIP(hipMemcpyAsync(codes + r0, dcode[k].p, (size_t)m * 8, hipMemcpyDeviceToHost, st[k]));
+    SCT_HIP(hipMemcpyAsync(gc + r0, dgc[k].p, (size_t)m, hipMemcpyDeviceToHost, st[k]));
+    SCT_HIP(hipMemcpyAsync(flags + r0, dfl[k].p, (size_t)m, hipMemcpyDeviceToHost, st[k]));
+  }
+  for (int k = 0; k < NSTAGE; ++k) SCT_HIP(hipStreamSynchronize(st[k]));
+  return SCT_OK;
+}
+
 extern "C" int sct_decode2_host(const uint64_t* codes, int64_t n, int words, int L, uint8_t* out) {
   SCT_CHECK(n >= 0 && words >= 1 && L >= 0, "bad n/words/L");
   if (n == 0 || L == 0) return SCT_OK;

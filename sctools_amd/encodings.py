@@ -53,6 +53,18 @@ def _records(seqs):
     return np.frombuffer(b"".join(seqs), dtype=np.uint8).reshape(len(seqs), L)
 
 
+_STREAM_MIN_RECORDS = 1 << 20
+
+
+def _encode_records(kind, recs):
+    """Large one-limb batches go through the pipelined H2D/encode/D2H stream."""
+    n, L = recs.shape
+    if n >= _STREAM_MIN_RECORDS and 1 <= L and kind * L <= 64:
+        codes, gc, flags = _lib.encode_stream(kind, recs)
+        return codes.reshape(n, 1), gc, flags
+    return _lib.encode(kind, recs, L)
+
+
 def _fill_ambiguous(recs, codes, gc, flags):
     """Walk flagged TwoBit records in order: draw random.randint(0,3) per ambiguous
     byte (encodings.py:69) and raise the reference's KeyError on an invalid one (:68)."""
@@ -150,7 +162,7 @@ class TwoBit(Encoding):
 
         Draws random numbers for ambiguous bases exactly as n calls of encode() would."""
         recs = _records(seqs)
-        codes, gc, flags = _lib.encode(2, recs, recs.shape[1])
+        codes, gc, flags = _encode_records(2, recs)
         _fill_ambiguous(recs, codes, gc, flags)
         out = codes[:, 0] if codes.shape[1] == 1 else codes
         return (out, gc) if return_gc else out
@@ -227,7 +239,7 @@ class ThreeBit(Encoding):
     @classmethod
     def encode_array(cls, seqs, return_gc=False):
         recs = _records(seqs)
-        codes, gc, _ = _lib.encode(3, recs, recs.shape[1])
+        codes, gc, _ = _encode_records(3, recs)
         out = codes[:, 0] if codes.shape[1] == 1 else codes
         return (out, gc) if return_gc else out
 

@@ -411,3 +411,26 @@ def test_from_whitelist_line_semantics(golden, tmp_path):
             assert [str(k) for k in b] == rec["codes"], rec["name"]
             assert [b[k] for k in b] == rec["counts"], rec["name"]
         assert random.getrandbits(32) == rec["after"], rec["name"]
+
+
+def test_encode_stream_pipeline():
+    rng = np.random.default_rng(55)
+    n, L = 3_000_017, 28
+    seqs = np.frombuffer(b"ACGTacgtN", np.uint8)[rng.integers(0, 9, (n, L))]
+    codes, gc, flags = _lib.encode_stream(2, seqs, chunk=700_001)
+    c2, g2, f2 = _lib.encode(2, seqs[:200_000], L)
+    assert np.array_equal(codes[:200_000], c2[:, 0]) and np.array_equal(gc[:200_000], g2)
+    assert np.array_equal(flags[:200_000], f2)
+    for r in range(0, n, 99_991):
+        s = seqs[r].tobytes()
+        if b"N" not in s:
+            assert int(codes[r]) == O.two_bit_encode(s)
+            assert flags[r] == 0
+        else:
+            assert flags[r] == 1
+    # the drop-in batch path routes >= 1M records through the stream
+    random.seed(3)
+    a = TwoBit.encode_array(seqs[:1_100_000])
+    random.seed(3)
+    b = [TwoBit.encode(seqs[r].tobytes()) for r in range(0, 1000)]
+    assert a[:1000].tolist() == b

@@ -86,6 +86,41 @@ def bench_encode(n_reads, L=28):
                          "bytes_per_read": L + 10}}
 
 
+def bench_encode_stream(n_reads, L=28):
+    """Host-resident reads (pinned by the caller, as a streaming reader would): the
+    PCIe-inclusive rate of sct_encode_stream_host."""
+    dev = torch.device("cuda")
+    lut = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev).manual_seed(6)
+    host = torch.empty((n_reads, L), dtype=torch.uint8, pin_memory=True)
+    step = 2 ** 25
+    for a in range(0, n_reads, step):
+        b = min(n_reads, a + step)
+        host[a:b] = lut[torch.randint(0, 4, (b - a, L), device=dev, generator=g).long()].cpu()
+    codes = torch.empty(n_reads, dtype=torch.int64, pin_memory=True)
+    gc = torch.empty(n_reads, dtype=torch.uint8, pin_memory=True)
+    flags = torch.empty(n_reads, dtype=torch.uint8, pin_memory=True)
+    lib = _lib.lib()
+    ts = []
+    for _ in range(3):
+        t = time.perf_counter()
+        _lib.check(lib.sct_encode_stream_host(2, _lib._vp(host.data_ptr()), n_reads, L, _lib._vp(codes.data_ptr()),
+                                              _lib._vp(gc.data_ptr()), _lib._vp(flags.data_ptr()), 1 << 24))
+        ts.append(time.perf_counter() - t)
+    sec = float(np.median(ts))
+    k = 1000
+    ref = np.zeros(k, dtype=np.uint64)
+    hv = host[:k].numpy()
+    for p in range(L):
+        ch = hv[:, p]
+        ref = (ref << np.uint64(2)) | np.select([ch == 65, ch == 67, ch == 84, ch == 71], [0, 1, 2, 3]).astype(np.uint64)
+    assert np.array_equal(codes[:k].numpy().view(np.uint64), ref), "stream encode parity"
+    return {"path": "encode TwoBit+GC host-resident stream (PCIe-inclusive, config 5)", "reads": n_reads,
+            "L": L, "median_s": sec, "reads_per_s": n_reads / sec,
+            "pcie_bytes_per_s": n_reads * (L + 10) / sec,
+            "note": "H2D L bytes + D2H 10 bytes per read over PCIe Gen5 x16 (63 GB/s spec per direction)"}
+
+
 def two_to_three(codes2, L=16):
     """TwoBit codes -> ThreeBit codes of the same sequence (A0 C1 T2 G3 -> A2 C1 T4 G3)."""
     m = np.array([2, 1, 4, 3], dtype=np.uint64)
@@ -173,10 +208,13 @@ def main():
     ap.add_argument("--reads", type=int, default=1_000_000_000)
     ap.add_argument("--queries", type=int, default=100_000_000)
     ap.add_argument("--skip-allpairs5", action="store_true")
+    ap.add_argument("--stream-reads", type=int, default=250_000_000)
     a = ap.parse_args()
     torch.cuda.set_device(0)
     _lib.check(_lib.lib().sct_set_device(0))
     print(json.dumps(bench_encode(a.reads)), flush=True)
+    if a.stream_reads:
+        print(json.dumps(bench_encode_stream(a.stream_reads)), flush=True)
     print(json.dumps(bench_nearest(a.queries, 1)), flush=True)
     if not a.skip_allpairs5:
         print(json.dumps(bench_allpairs5()), flush=True)
