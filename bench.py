@@ -35,9 +35,12 @@ from sctools_amd import _lib, sharding, synthetic  # noqa: E402
 # int32 ops; measured 121 lane-ops/clk/CU for v_xor_b32 by tools/valu_peak.hip / valu_banks.hip).
 VALU_PEAK_OPS = 256 * 128 * 2.4e9
 ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-bit code word
-# Issue slots the bit-sliced kernel spends per 32 pairs at 16 bp: 33 v_bitop3
-# (1 slot), 16 v_bcnt_u32_b32 (2 slots: half rate on gfx950), 6 v_xor/v_and (1 slot).
-ISSUE_SLOTS_PER_PAIR = {8: (33 + 2 * 16 + 6) / 32.0}
+# VALU issue slots the bit-sliced count kernel spends per pair at 16 bp, from its unmasked
+# loop (v_bcnt_u32_b32 counts 2: half rate on gfx950), per count scheme:
+#   SUBSETS: 33 v_bitop3 + 16 v_bcnt + 6 v_xor/v_and + 2 address v_add per 32 pairs;
+#   MOMENTS: 29 v_bitop3 + 13 v_bcnt + 7 v_xor/v_and + 2 address v_add per 32 pairs.
+ISSUE_SLOTS_PER_PAIR = {_lib.SCHEME_SUBSETS: (33 + 2 * 16 + 6 + 2) / 32.0,
+                        _lib.SCHEME_MOMENTS: (29 + 2 * 13 + 7 + 2) / 32.0}
 
 
 def parse():
@@ -109,24 +112,32 @@ def main():
     d_codes = torch.from_numpy(codes.view(np.int64)).to(dev)
     plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 2 * L)
     b, e = sharding.item_range(plan.items, rank, world)
-    counts = torch.zeros(plan.nbins, dtype=torch.int64, device=dev)
+    counts = torch.zeros(plan.ncounts, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     kernel_ms = []
 
+    evm = torch.cuda.Event(enable_timing=True)
+    moments_ms = []
+
     def step(record):
         counts.zero_()
         plan.build(sptr)
+        if record:
+            evm.record(stream)
+        plan.moments(counts.data_ptr(), rank, world, sptr)  # MOMENTS scheme: this rank's share
         if record:
             ev0.record(stream)
         plan.count(counts.data_ptr(), b, e, 0, sptr)
         if record:
             ev1.record(stream)
-        hist = sharding.combine_counts(counts)  # RCCL all-reduce (N > 1), D2H, exact inversion
+        # RCCL all-reduce (N > 1), D2H, exact inversion
+        hist = sharding.combine_counts(counts, None, plan.scheme, plan.nbins)
         if record:
             kernel_ms.append(ev0.elapsed_time(ev1))
+            moments_ms.append(evm.elapsed_time(ev0))
         return hist, _lib.summary_from_hist(hist)
 
     for _ in range(args.warmup):
@@ -151,7 +162,8 @@ def main():
     my_pairs = plan.range_pairs(b, e)
     kms = float(np.mean(kernel_ms))
     achieved = my_pairs * ALGO_OPS_PER_PAIR / (kms * 1e-3)
-    slots = my_pairs * ISSUE_SLOTS_PER_PAIR.get(L // 2, float("nan")) / (kms * 1e-3)
+    slots_per_pair = ISSUE_SLOTS_PER_PAIR[plan.scheme] if L == 16 else float("nan")
+    slots = my_pairs * slots_per_pair / (kms * 1e-3)
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_allpairs_r01.json")
     if os.path.exists(pmc):
@@ -175,18 +187,20 @@ def main():
             "config": {"workload": "config %d: %d-barcode all-pairs TwoBit Hamming histogram + summary"
                                    % (args.config, n),
                        "barcodes": n, "barcode_length": L, "pairs": pairs_total,
-                       "parallelism": "item-range shards, RCCL all-reduce of %d subset counts" % plan.nbins
+                       "parallelism": "item-range + moment shards, RCCL all-reduce of %d counts" % plan.ncounts
                        if world > 1 else "single GPU"},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
                          "unit": "Tops/s", "frac": achieved / VALU_PEAK_OPS, "traffic": traffic,
                          "kernel": "allpairs_count_kernel<8>", "kernel_ms": kms,
                          "algo_ops_per_pair": ALGO_OPS_PER_PAIR,
-                         "issue_slots_per_pair": ISSUE_SLOTS_PER_PAIR.get(L // 2),
+                         "issue_slots_per_pair": slots_per_pair,
+                         "scheme": {0: "subsets", 1: "moments"}[plan.scheme],
+                         "moments_ms": float(np.mean(moments_ms)),
                          "issue_slot_frac": slots / VALU_PEAK_OPS,
                          "note": "frac > 1: the bit-sliced kernel needs %.2f VALU issue slots per "
                                  "pair where SURVEY 8(d)'s formulation needs 4 ops (5 slots: "
                                  "v_bcnt is half rate); issue_slot_frac is the VALU utilisation"
-                                 % ISSUE_SLOTS_PER_PAIR.get(L // 2, float("nan"))},
+                                 % slots_per_pair},
             "summary": dict(zip(("minimum", "p25", "median", "p75", "maximum", "average"),
                                 [float(x) for x in summ])),
         }

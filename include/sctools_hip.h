@@ -113,24 +113,53 @@ int sct_hamming_pairs_host(int kind, const uint64_t* a, const uint64_t* b, int64
  * shard them: any partition of [0, items) into ranges, counted on any number of
  * devices and summed, gives the same result.
  *
- * sct_allpairs_count ACCUMULATES (atomic add) nbins uint64 "subset counts" into
- * d_counts: d_counts[0] += pairs counted, d_counts[m] += #pairs whose distance d
- * has all bits of m set (d & m == m), m = 1..nbins-1.  The counts are linear, so
- * they may be summed across devices (RCCL all-reduce) before sct_counts_to_hist.
+ * Two count schemes (a plan has one, fixed at creation):
+ *
+ * SCT_ALLPAIRS_SUBSETS (any code width): sct_allpairs_count ACCUMULATES (atomic add)
+ *   ncounts = nbins uint64 "subset counts" into d_counts: d_counts[0] += pairs counted,
+ *   d_counts[m] += #pairs whose distance d has all bits of m set (d & m == m),
+ *   m = 1..nbins-1.  Every item range is self-contained: its counts invert alone.
+ *
+ * SCT_ALLPAIRS_MOMENTS (codes of 29..32 bits = 16 bases, the 10x barcode width): the
+ *   count kernel accumulates d_counts[0] += pairs and d_counts[1+i] += #pairs whose
+ *   d mod 16 has all bits of kMomProducts[i] set (13 products, sct_common.h), and
+ *   sct_allpairs_moments accumulates d_counts[14+k-1] += M_k = sum over ALL pairs of
+ *   C(16 - d, k), k = 1..3 (pairs agreeing on k chosen positions, from the codes'
+ *   position marginals).  ncounts = 17; only the counts of the WHOLE job (every item
+ *   counted once, every moment part added once) invert.  13 products instead of 16
+ *   cut the count kernel's VALU work per pair.
+ *
+ * The counts are linear, so they may be summed across devices (RCCL all-reduce)
+ * before sct_counts_to_hist_ex.
  */
 typedef struct sct_allpairs_plan sct_allpairs_plan;
 
+#define SCT_ALLPAIRS_AUTO (-1)    /* MOMENTS where supported, else SUBSETS */
+#define SCT_ALLPAIRS_SUBSETS 0
+#define SCT_ALLPAIRS_MOMENTS 1
+
+/* = sct_allpairs_plan_create_ex(..., SCT_ALLPAIRS_AUTO, plan) */
 int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int code_bits,
                              sct_allpairs_plan** plan);
+int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, int code_bits, int scheme,
+                                sct_allpairs_plan** plan);
 int sct_allpairs_plan_destroy(sct_allpairs_plan* plan);
 /* nbins = max distance + 1 = 2*ceil(code_bits/4)+1; items = number of work items */
 int sct_allpairs_plan_info(const sct_allpairs_plan* plan, int* nbins, int64_t* items,
                            int64_t* pairs);
+/* scheme of the plan, length of its counts vector, and its code width */
+int sct_allpairs_plan_scheme(const sct_allpairs_plan* plan, int* scheme, int* ncounts,
+                             int* code_bits);
 /* (Re)build the selection table from the codes the plan was created on. */
 int sct_allpairs_build(sct_allpairs_plan* plan, void* stream);
 /* Count work items [item_begin, item_end).  grid = 0 picks the persistent grid size. */
 int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
                        uint64_t* d_counts, int grid, void* stream);
+/* MOMENTS scheme: add part `part` of `nparts` of the agreement moments to d_counts
+ * (the position subsets are split into nparts shares; summing every part once gives
+ * M_1..M_3).  SUBSETS scheme: no-op. */
+int sct_allpairs_moments(sct_allpairs_plan* plan, int part, int nparts, uint64_t* d_counts,
+                         void* stream);
 /* Host-only (no device needed): the plan geometry for n codes of code_bits bits, i.e.
  * what sct_allpairs_plan_info would report, plus rows per item and codes per column
  * chunk.  Lets shard drivers partition [0, items) before touching a GPU. */
@@ -140,8 +169,12 @@ int sct_allpairs_geometry(int64_t n, int code_bits, int* nbins, int64_t* items, 
 int sct_allpairs_range_pairs(const sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
                              int64_t* pairs);
 
-/* Host: subset counts -> histogram (exact Moebius inversion), hist[d] for d < nbins. */
+/* Host: SUBSETS counts -> histogram (exact Moebius inversion), hist[d] for d < nbins. */
 int sct_counts_to_hist(const uint64_t* counts, int nbins, uint64_t* hist);
+/* Host: counts of either scheme -> histogram (MOMENTS: exact rational solve of the
+ * 17 x 17 system, checked integral and non-negative).  nbins must be the plan's. */
+int sct_counts_to_hist_ex(int scheme, const uint64_t* counts, int ncounts, uint64_t* hist,
+                          int nbins);
 
 /* One-shot, host pointers, current device: histogram of TwoBit distances over all
  * unordered pairs of the n codes.  hist must hold nbins = 2*ceil(code_bits/4)+1. */

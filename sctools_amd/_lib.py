@@ -22,6 +22,11 @@ SCT_E_HIP = -2
 SCT_E_NOMEM = -3
 SCT_E_RANGE = -4
 
+# all-pairs count schemes (include/sctools_hip.h)
+SCHEME_AUTO = -1
+SCHEME_SUBSETS = 0
+SCHEME_MOMENTS = 1
+
 _i32, _i64, _dbl = ctypes.c_int, ctypes.c_int64, ctypes.c_double
 _vp = ctypes.c_void_p
 _p64 = ctypes.POINTER(ctypes.c_uint64)
@@ -44,6 +49,9 @@ SIGNATURES = {
     "sct_hamming_pairs": [_i32, _vp, _vp, _i64, _i32, _vp, _vp],
     "sct_hamming_pairs_host": [_i32, _vp, _vp, _i64, _i32, _vp],
     "sct_allpairs_plan_create": [_vp, _i64, _i32, ctypes.POINTER(_vp)],
+    "sct_allpairs_plan_create_ex": [_vp, _i64, _i32, _i32, ctypes.POINTER(_vp)],
+    "sct_allpairs_plan_scheme": [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32), ctypes.POINTER(_i32)],
+    "sct_allpairs_moments": [_vp, _i32, _i32, _vp, _vp],
     "sct_allpairs_plan_destroy": [_vp],
     "sct_allpairs_plan_info": [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i64), ctypes.POINTER(_i64)],
     "sct_allpairs_build": [_vp, _vp],
@@ -52,6 +60,7 @@ SIGNATURES = {
     "sct_allpairs_geometry": [_i64, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i64),
                               ctypes.POINTER(_i32), ctypes.POINTER(_i32)],
     "sct_counts_to_hist": [_vp, _i32, _vp],
+    "sct_counts_to_hist_ex": [_i32, _vp, _i32, _vp, _i32],
     "sct_hamming_hist_allpairs_host": [_vp, _i64, _i32, _vp, _i32],
     "sct_summary_from_hist": [_vp, _i32, _vp],
     "sct_nearest_plan_create": [_i32, _vp, _i64, _i32, _i32, _vp, ctypes.POINTER(_vp)],
@@ -237,10 +246,12 @@ def hamming_hist_allpairs(codes, code_bits=None):
     return hist
 
 
-def counts_to_hist(counts):
+def counts_to_hist(counts, scheme=SCHEME_SUBSETS, nbins=None):
+    """Counts of an all-pairs plan (either scheme) -> exact histogram (uint64[nbins])."""
     counts = np.ascontiguousarray(counts, dtype=np.uint64).reshape(-1)
-    hist = np.zeros_like(counts)
-    check(lib().sct_counts_to_hist(_ptr(counts), counts.size, _ptr(hist)))
+    nbins = counts.size if nbins is None else nbins
+    hist = np.zeros(nbins, dtype=np.uint64)
+    check(lib().sct_counts_to_hist_ex(scheme, _ptr(counts), counts.size, _ptr(hist), nbins))
     return hist
 
 
@@ -318,22 +329,36 @@ def device_count():
 # ------------------------------------------------------------------ device-pointer plan API
 class AllPairsPlan:
     """Owns an sct_allpairs_plan over device-resident codes (a torch.uint64/int64 tensor
-    or a raw device pointer).  Used by the benchmark and the sharded driver."""
+    or a raw device pointer).  Used by the benchmark and the sharded driver.
 
-    def __init__(self, d_codes_ptr, n, code_bits=0):
+    ``ncounts`` is the length of the uint64 counts vector that ``moments`` and ``count``
+    accumulate into; ``counts_to_hist`` inverts the counts of the whole job."""
+
+    def __init__(self, d_codes_ptr, n, code_bits=0, scheme=SCHEME_AUTO):
         self._lib = lib()
         self._h = _vp()
-        check(self._lib.sct_allpairs_plan_create(_vp(d_codes_ptr), n, code_bits, ctypes.byref(self._h)))
+        check(self._lib.sct_allpairs_plan_create_ex(_vp(d_codes_ptr), n, code_bits, scheme,
+                                                    ctypes.byref(self._h)))
         nb, items, pairs = _i32(0), _i64(0), _i64(0)
         check(self._lib.sct_allpairs_plan_info(self._h, ctypes.byref(nb), ctypes.byref(items), ctypes.byref(pairs)))
         self.nbins, self.items, self.pairs = nb.value, items.value, pairs.value
+        sc, nc, cb = _i32(0), _i32(0), _i32(0)
+        check(self._lib.sct_allpairs_plan_scheme(self._h, ctypes.byref(sc), ctypes.byref(nc), ctypes.byref(cb)))
+        self.scheme, self.ncounts, self.code_bits = sc.value, nc.value, cb.value
 
     def build(self, stream=0):
         check(self._lib.sct_allpairs_build(self._h, _vp(stream)))
 
+    def moments(self, d_counts_ptr, part=0, nparts=1, stream=0):
+        """MOMENTS scheme: add moment share `part` of `nparts` (no-op for SUBSETS)."""
+        check(self._lib.sct_allpairs_moments(self._h, part, nparts, _vp(d_counts_ptr), _vp(stream)))
+
     def count(self, d_counts_ptr, begin=0, end=None, grid=0, stream=0):
         end = self.items if end is None else end
         check(self._lib.sct_allpairs_count(self._h, begin, end, _vp(d_counts_ptr), grid, _vp(stream)))
+
+    def counts_to_hist(self, counts):
+        return counts_to_hist(counts, self.scheme, self.nbins)
 
     def range_pairs(self, begin, end):
         p = _i64(0)

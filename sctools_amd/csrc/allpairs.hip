@@ -36,6 +36,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "sct_common.h"
 
@@ -110,7 +111,8 @@ __device__ __forceinline__ void reduce_upper(const uint32_t* in, uint32_t (&d)[B
       reduce_upper<W + 1, NC, B>(carry, d);
     }
   }
-  // carries beyond plane B-1 are provably zero (sum <= 2*NPP < 2^B) and are dropped
+  // carries beyond plane B-1 are dropped: zero when B = bitlen(2*NPP) (SUBSETS); the
+  // MOMENTS scheme drops plane 4 on purpose (B = 4 keeps d mod 16)
 }
 
 // Sum NPP 2-bit numbers {s1,s0} into B bit-planes d.
@@ -143,6 +145,30 @@ __device__ __forceinline__ void count_subsets(const uint32_t (&d)[B], uint32_t (
   }
 }
 
+// MOMENTS scheme: cnt[i] += popcount(AND of the planes in kMomProducts[i]) over the
+// four planes of d mod 16 (the d4 carry is never formed).  9 ANDs (three as one
+// v_bitop3 3-input AND) + 13 v_bcnt per 32 pairs, against 11 + 16 for count_subsets.
+__device__ __forceinline__ uint32_t and3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x80);
+}
+__device__ __forceinline__ void count_mom(const uint32_t (&d)[4], uint32_t (&cnt)[sct::kMomNProd]) {
+  static_assert(sct::kMomNProd == 13, "product list changed: update count_mom");
+  const uint32_t p7 = and3(d[0], d[1], d[2]);
+  bcnt_acc(cnt[0], d[0]);                    // 1
+  bcnt_acc(cnt[1], d[1]);                    // 2
+  bcnt_acc(cnt[2], d[0] & d[1]);             // 3
+  bcnt_acc(cnt[3], d[2]);                    // 4
+  bcnt_acc(cnt[4], d[0] & d[2]);             // 5
+  bcnt_acc(cnt[5], d[1] & d[2]);             // 6
+  bcnt_acc(cnt[6], p7);                      // 7
+  bcnt_acc(cnt[7], d[3]);                    // 8
+  bcnt_acc(cnt[8], d[0] & d[3]);             // 9
+  bcnt_acc(cnt[9], d[1] & d[3]);             // 10
+  bcnt_acc(cnt[10], and3(d[0], d[1], d[3])); // 11
+  bcnt_acc(cnt[11], and3(d[0], d[2], d[3])); // 13
+  bcnt_acc(cnt[12], p7 & d[3]);              // 15
+}
+
 struct ItemCursor {
   int64_t c, r;
 };
@@ -167,11 +193,18 @@ __device__ __forceinline__ uint32_t pair_mask(int64_t i, int64_t jg, int64_t n) 
   return i < n ? mask : 0u;
 }
 
-template <int NPP, bool MASKED, int ABL = 0>
+// counters per lane: SUBSETS 2*NPP subset products, MOMENTS kMomNProd products
+template <int NPP, bool MOM>
+struct NCount {
+  static constexpr int value = MOM ? sct::kMomNProd : 2 * NPP;
+};
+
+template <int NPP, bool MASKED, bool MOM, int ABL = 0>
 __device__ __forceinline__ void one_group(const uint32_t (&s0)[NPP], const uint32_t (&s1)[NPP],
                                           int64_t i, int64_t jg, int64_t n,
-                                          uint32_t (&cnt)[2 * NPP], uint32_t& cnt0) {
-  constexpr int B = Geom<NPP>::B;
+                                          uint32_t (&cnt)[NCount<NPP, MOM>::value], uint32_t& cnt0) {
+  // MOMENTS keeps 4 planes: the carry into plane 4 is dropped, leaving d mod 16
+  constexpr int B = MOM ? 4 : Geom<NPP>::B;
   uint32_t d[B];
   if constexpr (ABL == 2) {  // ablation: no adder tree (planes straight into counting)
 #pragma unroll
@@ -190,12 +223,16 @@ __device__ __forceinline__ void one_group(const uint32_t (&s0)[NPP], const uint3
     for (int b = 0; b < B; ++b) d[b] &= mask;
     cnt0 += __popc(mask);
   }
-  count_subsets<2 * NPP, B>(d, cnt);
+  if constexpr (MOM)
+    count_mom(d, cnt);
+  else
+    count_subsets<2 * NPP, B>(d, cnt);
 }
 
-template <int NPP, bool MASKED, int UNROLL, int ABL = 0>
+template <int NPP, bool MASKED, bool MOM, int UNROLL, int ABL = 0>
 __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uint64_t q, int64_t i,
-                                             int64_t j0, int64_t n, uint32_t (&cnt)[2 * NPP],
+                                             int64_t j0, int64_t n,
+                                             uint32_t (&cnt)[NCount<NPP, MOM>::value],
                                              uint32_t& cnt0) {
   using Gm = Geom<NPP>;
   int off[NPP];
@@ -220,17 +257,20 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
         s0b[pp] = e.z;
         s1b[pp] = e.w;
       }
-      one_group<NPP, MASKED, ABL>(s0a, s1a, i, j0 + 64 * h, n, cnt, cnt0);
-      one_group<NPP, MASKED, ABL>(s0b, s1b, i, j0 + 64 * h + 32, n, cnt, cnt0);
+      one_group<NPP, MASKED, MOM, ABL>(s0a, s1a, i, j0 + 64 * h, n, cnt, cnt0);
+      one_group<NPP, MASKED, MOM, ABL>(s0b, s1b, i, j0 + 64 * h + 32, n, cnt, cnt0);
     }
   }
   if constexpr (!MASKED) cnt0 += Gm::CB;
 }
 
 // Count-kernel variants (A/B-selectable with SCT_ALLPAIRS_VARIANT): 1 = one group pair
-// per loop trip (108 VGPRs), 2 = two per trip (default, 124 VGPRs, 4 waves/SIMD).
+// per loop trip (108 VGPRs), 2 = two per trip (124 VGPRs, 4 waves/SIMD), 3 = the chunk's
+// group pairs fully unrolled (LDS offsets become immediates: no address VALU).
 // Register prefetch / ping-pong variants measured slower and were dropped.
 template <int V> struct Variant { static constexpr int UNROLL = V, ABL = 0; };
+template <> struct Variant<3> { static constexpr int UNROLL = 16, ABL = 0; };
+template <> struct Variant<4> { static constexpr int UNROLL = 4, ABL = 0; };
 #ifdef SCT_ABLATION
 // ablation builds (wrong results, timing only): 11 no counting, 12 no tree, 13 no LDS reads
 template <> struct Variant<11> { static constexpr int UNROLL = 2, ABL = 1; };
@@ -242,7 +282,7 @@ template <> struct Variant<13> { static constexpr int UNROLL = 2, ABL = 3; };
 // DPP/ds_swizzle/ds_bpermute), then LDS across the waves, then one u64 atomic per counter;
 // the lane counters restart at 0.  `red` aliases the LDS tile (callers sync first).
 template <int G>
-__device__ __forceinline__ void flush_counts(uint32_t (&cnt)[G], uint32_t& cnt0,
+__device__ __forceinline__ void flush_counts(uint32_t (&cnt)[G], uint32_t& cnt0,  // G counters
                                              unsigned long long* red,
                                              unsigned long long* __restrict__ out) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -267,7 +307,7 @@ __device__ __forceinline__ void flush_counts(uint32_t (&cnt)[G], uint32_t& cnt0,
   __syncthreads();
 }
 
-template <int NPP, int V>
+template <int NPP, int V, bool MOM>
 __global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __restrict__ codes,
                                                             const uint4* __restrict__ table,
                                                             int64_t n, int64_t nchunks,
@@ -276,7 +316,7 @@ __global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __re
                                                             unsigned long long* __restrict__ queue,
                                                             unsigned long long* __restrict__ out) {
   using Gm = Geom<NPP>;
-  constexpr int G = Gm::G;
+  constexpr int G = NCount<NPP, MOM>::value;  // lane counters besides the pair count
   __shared__ __attribute__((aligned(16))) uint4 tile[Gm::TILE];
   __shared__ int64_t s_grab;
 
@@ -334,9 +374,11 @@ __global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __re
       const int64_t j0 = c * Gm::CB;
       const bool masked = ((r + 1) * RB > j0) || (j0 + Gm::CB > n);
       if (masked)
-        process_item<NPP, true, Variant<V>::UNROLL, Variant<V>::ABL>(tile, q, i, j0, n, cnt, cnt0);
+        process_item<NPP, true, MOM, Variant<V>::UNROLL, Variant<V>::ABL>(tile, q, i, j0, n, cnt,
+                                                                          cnt0);
       else
-        process_item<NPP, false, Variant<V>::UNROLL, Variant<V>::ABL>(tile, q, i, j0, n, cnt, cnt0);
+        process_item<NPP, false, MOM, Variant<V>::UNROLL, Variant<V>::ABL>(tile, q, i, j0, n, cnt,
+                                                                           cnt0);
       q = q_next;
       i = i_next;
     }
@@ -381,6 +423,173 @@ __global__ void or_reduce_kernel(const uint64_t* __restrict__ codes, int64_t n,
   if ((threadIdx.x & 63) == 0 && v) atomicOr(out, v);
 }
 
+// ---------------------------------------------------------------- agreement moments
+// M_k = #(pair, k-set of positions S) with the pair agreeing on all of S
+//     = sum over pairs of C(16 - d, k) = sum_{|S|=k} sum_{pattern} C(count_S(pattern), 2),
+// k = 1..3.  Only the 3-position marginals are counted (560 position triples x 64
+// patterns = 35,840 bins); the 2- and 1-position marginals are sums of triple bins.
+// No atomics: the codes are first transposed into position/base bitmasks
+//   masks[w][4p + a] bit k = [base p of code 32w + k == a]            (moments_masks_kernel)
+// and every marginal bin is a popcount of an AND of three of them
+//   count(p,a, q,b, r,c) = sum_w popcount(masks[w][4p+a] & masks[w][4q+b] & masks[w][4r+c])
+// (moments_count_kernel: a workgroup stages kMomWR words of masks in LDS; each thread
+// owns one triple and one base b of its middle position and sweeps all words, 16
+// bitop3 + 16 v_bcnt per word for its 16 bins).  Partial bins per word range are summed
+// by moments_reduce_kernel; moments_finalize_kernel turns bins into C(count, 2).
+constexpr int kMomWR = 256;     // mask words (8,192 codes) per LDS range: 64 KiB
+constexpr int kMomTri = 64;     // triples per workgroup (4 threads each)
+constexpr int kMomNTri = 560;   // C(16, 3)
+constexpr int kMomNPair = 120;  // C(16, 2)
+
+struct MomTriple {
+  uint32_t shifts;  // p | q << 8 | r << 16, p < q < r (base positions)
+};
+
+// marginal of a pair/single read off one triple: the triple, and the slot(s) kept
+struct MomSource {
+  int32_t tri;
+  int32_t slot;  // pair: the free slot (summed); single: the kept slot
+};
+
+// one wave per 64 codes (= 2 mask words): lane l builds masks[.][l] from 64 ballots
+__global__ __launch_bounds__(256) void moments_masks_kernel(const uint64_t* __restrict__ codes,
+                                                            int64_t n, int64_t nwords,
+                                                            uint32_t* __restrict__ masks) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t w0 = wave * 2;
+  if (w0 >= nwords) return;
+  const int64_t i = w0 * 32 + lane;
+  const bool valid = i < n;
+  const uint32_t c = valid ? (uint32_t)codes[i] : 0u;
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int pa = 0; pa < 64; ++pa) {
+    const uint64_t b = __ballot(valid && ((c >> (2 * (pa >> 2))) & 3u) == (uint32_t)(pa & 3));
+    if (lane == pa) {
+      lo = (uint32_t)b;
+      hi = (uint32_t)(b >> 32);
+    }
+  }
+  masks[w0 * 64 + lane] = lo;
+  if (w0 + 1 < nwords) masks[(w0 + 1) * 64 + lane] = hi;
+}
+
+// grid (word ranges, triple blocks); partial[range][tri * 64 + (a << 4 | b << 2 | c)]
+__global__ __launch_bounds__(256) void moments_count_kernel(const uint32_t* __restrict__ masks,
+                                                            int64_t nwords,
+                                                            const MomTriple* __restrict__ tri,
+                                                            int tri0, int tri1,
+                                                            uint32_t* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) uint32_t m[kMomWR * 64];
+  const int64_t wbeg = (int64_t)blockIdx.x * kMomWR;
+  const int nw = (int)min<int64_t>(kMomWR, nwords - wbeg);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(masks + wbeg * 64);
+    uint4* dst = reinterpret_cast<uint4*>(m);
+    for (int k = threadIdx.x; k < nw * 16; k += 256) dst[k] = src[k];
+  }
+  __syncthreads();
+  const int t = tri0 + blockIdx.y * kMomTri + (threadIdx.x >> 2);
+  if (t >= tri1) return;
+  const int b = threadIdx.x & 3;
+  const uint32_t sh = tri[t].shifts;
+  const int p = sh & 255, q = (sh >> 8) & 255, r = (sh >> 16) & 255;
+  uint32_t cnt[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) cnt[k] = 0u;
+  const uint4* m4 = reinterpret_cast<const uint4*>(m);
+  for (int w = 0; w < nw; ++w) {
+    const uint4 P = m4[w * 16 + p];
+    const uint4 R = m4[w * 16 + r];
+    const uint32_t Q = m[w * 64 + 4 * q + b];
+    const uint32_t pa[4] = {P.x, P.y, P.z, P.w};
+    const uint32_t rc[4] = {R.x, R.y, R.z, R.w};
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) bcnt_acc(cnt[a * 4 + c], and3(pa[a], Q, rc[c]));
+  }
+  uint32_t* out = partial + (int64_t)blockIdx.x * kMomNTri * 64 + (int64_t)t * 64;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) out[(a << 4) | (b << 2) | c] = cnt[a * 4 + c];
+}
+
+// ghist[bin] = sum over word ranges of partial[range][bin], bins [b0, b1)
+__global__ __launch_bounds__(256) void moments_reduce_kernel(const uint32_t* __restrict__ partial,
+                                                             int nranges, int b0, int b1,
+                                                             unsigned* __restrict__ ghist) {
+  const int k = b0 + blockIdx.x * 256 + threadIdx.x;
+  if (k >= b1) return;
+  unsigned s = 0;
+  for (int rg = 0; rg < nranges; ++rg) s += partial[(int64_t)rg * kMomNTri * 64 + k];
+  ghist[k] = s;
+}
+
+__device__ __forceinline__ unsigned long long pairs_of(unsigned long long c) {
+  return c * (c - (c > 0ull)) / 2ull;
+}
+
+// Triples [tri0, tri1) are complete in ghist.  Adds to out[0..2] (M1, M2, M3):
+//   M3 += C(bin, 2) over those triples' bins;
+//   M2 += C(pair bin, 2) for the pairs whose source triple lies in the range (4-bin sums);
+//   M1 += C(single bin, 2) likewise (16-bin sums).
+__global__ __launch_bounds__(256) void moments_finalize_kernel(const unsigned* __restrict__ ghist,
+                                                               int tri0, int tri1,
+                                                               const MomSource* __restrict__ pair_src,
+                                                               const MomSource* __restrict__ single_src,
+                                                               unsigned long long* __restrict__ out) {
+  unsigned long long acc[3] = {0ull, 0ull, 0ull};
+  const int nb3 = (tri1 - tri0) * 64;
+  const int total = nb3 + kMomNPair * 16 + sct::kMomG * 4;
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < total; k += gridDim.x * 256) {
+    if (k < nb3) {
+      acc[2] += pairs_of(ghist[(int64_t)tri0 * 64 + k]);
+    } else if (k < nb3 + kMomNPair * 16) {
+      const int j = k - nb3, pr = j >> 4, ab = j & 15;
+      const MomSource src = pair_src[pr];
+      if (src.tri < tri0 || src.tri >= tri1) continue;
+      // kept slots in order, free slot f: bin = digits (slot0, slot1, slot2), 2 bits each
+      const int f = src.slot;
+      unsigned long long c = 0;
+      for (int v = 0; v < 4; ++v) {
+        int dig[3], kk = 0;
+        for (int sl = 0; sl < 3; ++sl) dig[sl] = (sl == f) ? v : ((kk++ == 0) ? (ab >> 2) : (ab & 3));
+        c += ghist[(int64_t)src.tri * 64 + (dig[0] << 4) + (dig[1] << 2) + dig[2]];
+      }
+      acc[1] += pairs_of(c);
+    } else {
+      const int j = k - nb3 - kMomNPair * 16, p = j >> 2, a = j & 3;
+      const MomSource src = single_src[p];
+      if (src.tri < tri0 || src.tri >= tri1) continue;
+      unsigned long long c = 0;
+      for (int v = 0; v < 16; ++v) {
+        int dig[3], kk = 0;
+        for (int sl = 0; sl < 3; ++sl) dig[sl] = (sl == src.slot) ? a : ((kk++ == 0) ? (v >> 2) : (v & 3));
+        c += ghist[(int64_t)src.tri * 64 + (dig[0] << 4) + (dig[1] << 2) + dig[2]];
+      }
+      acc[0] += pairs_of(c);
+    }
+  }
+  __shared__ unsigned long long red[3][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    unsigned long long v = acc[o];
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s, 64);
+    if (lane == 0) red[o][wave] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const unsigned long long v = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] +
+                                 red[threadIdx.x][3];
+    if (v) atomicAdd(out + threadIdx.x, v);
+  }
+}
+
 int ct_for(int npp) { return npp <= 8 ? 32 : 16; }
 
 }  // namespace
@@ -399,10 +608,20 @@ struct sct_allpairs_plan {
   uint64_t* d_codes = nullptr;
   uint4* d_table = nullptr;
   int64_t table_entries = 0;
-  int variant = 2;  // count-kernel variant (SCT_ALLPAIRS_VARIANT=1|2, see Variant<>)
+  int variant = 2;  // count-kernel variant (SCT_ALLPAIRS_VARIANT=1..4, see Variant<>)
   int64_t grab = 16;  // items per work-queue pull (SCT_ALLPAIRS_GRAB)
   int64_t flush_items = 0;  // test hook: flush lane counters more often (SCT_ALLPAIRS_FLUSH_ITEMS)
   unsigned long long* d_queue = nullptr;  // work-queue head, zeroed before every launch
+  int scheme = SCT_ALLPAIRS_SUBSETS;
+  int ncounts = 0;
+  // MOMENTS scheme: position triples, pair/single sources, and the global triple bins
+  MomTriple* d_mtri = nullptr;
+  MomSource* d_msrc = nullptr;  // kMomNPair pair sources, then kMomG single sources
+  unsigned* d_mhist = nullptr;
+  uint32_t* d_mmasks = nullptr;    // [nwords][64] position/base bitmasks
+  uint32_t* d_mpartial = nullptr;  // [nranges][560 * 64] partial bins
+  int64_t mom_nwords = 0;
+  int mom_nranges = 0;
 };
 
 namespace {
@@ -423,40 +642,66 @@ int launch_count(sct_allpairs_plan* p, int64_t b, int64_t e, uint64_t* d_counts,
   int64_t flush = 0xFFFFFFFFLL / Geom<NPP>::CB - p->grab;
   if (p->flush_items > 0 && p->flush_items < flush) flush = p->flush_items;
   SCT_HIP(hipMemsetAsync(p->d_queue, 0, sizeof(unsigned long long), s));
-#define SCT_LAUNCH_V(V)                                                                         \
-  hipLaunchKernelGGL((allpairs_count_kernel<NPP, V>), dim3(grid), dim3(RB), 0, s, p->d_codes,   \
-                     p->d_table, p->n, p->nchunks, b, e, p->grab, flush, p->d_queue,             \
+#define SCT_LAUNCH_V(V, MOM)                                                                      \
+  hipLaunchKernelGGL((allpairs_count_kernel<NPP, V, MOM>), dim3(grid), dim3(RB), 0, s, p->d_codes, \
+                     p->d_table, p->n, p->nchunks, b, e, p->grab, flush, p->d_queue,               \
                      reinterpret_cast<unsigned long long*>(d_counts))
-  switch (variant) {
-    case 1: SCT_LAUNCH_V(1); break;
+  if (p->scheme == SCT_ALLPAIRS_MOMENTS) {
+    if constexpr (NPP == 8) {
+      switch (variant) {
+        case 1: SCT_LAUNCH_V(1, true); break;
+        case 3: SCT_LAUNCH_V(3, true); break;
+        case 4: SCT_LAUNCH_V(4, true); break;
+        default: SCT_LAUNCH_V(2, true); break;
+      }
+    } else {
+      return sct::fail(SCT_E_INVALID, "MOMENTS scheme needs 16-base codes");
+    }
+  } else {
+    switch (variant) {
+      case 1: SCT_LAUNCH_V(1, false); break;
+      case 3: if constexpr (NPP == 8) { SCT_LAUNCH_V(3, false); break; } else { SCT_LAUNCH_V(2, false); break; }
 #ifdef SCT_ABLATION
-    case 11: if constexpr (NPP == 8) SCT_LAUNCH_V(11); break;
-    case 12: if constexpr (NPP == 8) SCT_LAUNCH_V(12); break;
-    case 13: if constexpr (NPP == 8) SCT_LAUNCH_V(13); break;
+      case 11: if constexpr (NPP == 8) SCT_LAUNCH_V(11, false); break;
+      case 12: if constexpr (NPP == 8) SCT_LAUNCH_V(12, false); break;
+      case 13: if constexpr (NPP == 8) SCT_LAUNCH_V(13, false); break;
 #endif
-    default: SCT_LAUNCH_V(2); break;
+      default: SCT_LAUNCH_V(2, false); break;
+    }
   }
 #undef SCT_LAUNCH_V
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
 
-template <int NPP, int V>
+template <int NPP, int V, bool MOM>
 int occupancy_of() {
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, allpairs_count_kernel<NPP, V>, RB, 0) !=
-          hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, allpairs_count_kernel<NPP, V, MOM>, RB,
+                                                   0) != hipSuccess ||
       per_cu <= 0)
     per_cu = 4;
   return per_cu;
 }
 
 template <int NPP>
-int occupancy_grid(int cus, int variant) {
+int occupancy_grid(int cus, int variant, int scheme) {
   int per_cu;
+  if constexpr (NPP == 8) {
+    if (scheme == SCT_ALLPAIRS_MOMENTS) {
+      switch (variant) {
+        case 1: per_cu = occupancy_of<NPP, 1, true>(); break;
+        case 3: per_cu = occupancy_of<NPP, 3, true>(); break;
+        case 4: per_cu = occupancy_of<NPP, 4, true>(); break;
+        default: per_cu = occupancy_of<NPP, 2, true>(); break;
+      }
+      return cus * per_cu;
+    }
+    if (variant == 3) return cus * occupancy_of<NPP, 3, false>();
+  }
   switch (variant) {
-    case 1: per_cu = occupancy_of<NPP, 1>(); break;
-    default: per_cu = occupancy_of<NPP, 2>(); break;
+    case 1: per_cu = occupancy_of<NPP, 1, false>(); break;
+    default: per_cu = occupancy_of<NPP, 2, false>(); break;
   }
   return cus * per_cu;  // persistent: every workgroup resident, pulling from the queue
 }
@@ -482,8 +727,8 @@ int occupancy_grid(int cus, int variant) {
     default: break;                      \
   }
 
-int grid_for(int npp, int cus, int variant) {
-  SCT_NPP_SWITCH(npp, occupancy_grid, cus, variant);
+int grid_for(int npp, int cus, int variant, int scheme) {
+  SCT_NPP_SWITCH(npp, occupancy_grid, cus, variant, scheme);
   return cus * 4;
 }
 
@@ -493,11 +738,53 @@ int dispatch_count(sct_allpairs_plan* p, int64_t b, int64_t e, uint64_t* d, int 
   return sct::fail(SCT_E_RANGE, "unsupported npp %d", p->npp);
 }
 
+// The 560 position triples p < q < r (lexicographic), and for every pair / single the
+// triple its marginal is read from: pair (p,q) -> (p,q,r) with r the smallest other
+// position (slot of r summed); single p -> (p,q,r) with q, r the two smallest others.
+void mom_layout(std::vector<MomTriple>& tri, std::vector<MomSource>& src) {
+  static_assert(sct::kMomOrder == 3, "moment layout assumes order 3");
+  tri.clear();
+  src.clear();
+  int index[16][16][16];
+  for (int p = 0; p < sct::kMomG; ++p)
+    for (int q = p + 1; q < sct::kMomG; ++q)
+      for (int r = q + 1; r < sct::kMomG; ++r) {
+        index[p][q][r] = (int)tri.size();
+        tri.push_back(MomTriple{(uint32_t)p | (uint32_t)q << 8 | (uint32_t)r << 16});
+      }
+  auto sorted_source = [&](int a, int b, int c, int special) {
+    int v[3] = {a, b, c};
+    std::sort(v, v + 3);
+    const int slot = v[0] == special ? 0 : (v[1] == special ? 1 : 2);
+    return MomSource{index[v[0]][v[1]][v[2]], slot};
+  };
+  for (int p = 0; p < sct::kMomG; ++p)
+    for (int q = p + 1; q < sct::kMomG; ++q) {
+      int r = 0;
+      while (r == p || r == q) ++r;
+      src.push_back(sorted_source(p, q, r, r));  // free slot = r's
+    }
+  for (int p = 0; p < sct::kMomG; ++p) {
+    int o[2], k = 0;
+    for (int x = 0; x < sct::kMomG && k < 2; ++x)
+      if (x != p) o[k++] = x;
+    src.push_back(sorted_source(p, o[0], o[1], p));  // kept slot = p's
+  }
+}
+
 }  // namespace
 
 extern "C" int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int code_bits,
                                         sct_allpairs_plan** plan) {
+  return sct_allpairs_plan_create_ex(d_codes, n, code_bits, SCT_ALLPAIRS_AUTO, plan);
+}
+
+extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, int code_bits,
+                                           int scheme, sct_allpairs_plan** plan) {
   SCT_CHECK(plan != nullptr, "plan is NULL");
+  SCT_CHECK(scheme == SCT_ALLPAIRS_AUTO || scheme == SCT_ALLPAIRS_SUBSETS ||
+                scheme == SCT_ALLPAIRS_MOMENTS,
+            "unknown scheme %d", scheme);
   *plan = nullptr;
   SCT_CHECK(n >= 0, "n must be >= 0");
   SCT_CHECK(n == 0 || d_codes != nullptr, "codes is NULL");
@@ -552,15 +839,48 @@ extern "C" int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int 
   }
   e = hipMalloc(&p->d_queue, sizeof(unsigned long long));
   if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "hipMalloc queue: %s", hipGetErrorString(e)));
+  // MOMENTS needs 16-base codes (29..32 bits); AUTO picks it there
+  // (u32 marginal bins and u64 M_3 <= C(n,2)*560 bound n; 1e8 codes is far beyond a whitelist)
+  const bool mom_ok = p->npp * 2 == sct::kMomG && n <= 100000000LL;
+  if (scheme == SCT_ALLPAIRS_MOMENTS && !mom_ok)
+    return cleanup(sct::fail(SCT_E_INVALID, "MOMENTS scheme needs code_bits in 29..32 (got %d) "
+                             "and n <= 1e8", code_bits));
+  if (const char* v = getenv("SCT_ALLPAIRS_SCHEME"))
+    if (scheme == SCT_ALLPAIRS_AUTO) scheme = atoi(v) == 0 ? SCT_ALLPAIRS_SUBSETS : SCT_ALLPAIRS_AUTO;
+  p->scheme = (scheme == SCT_ALLPAIRS_MOMENTS || (scheme == SCT_ALLPAIRS_AUTO && mom_ok))
+                  ? SCT_ALLPAIRS_MOMENTS
+                  : SCT_ALLPAIRS_SUBSETS;
+  p->ncounts = p->scheme == SCT_ALLPAIRS_MOMENTS ? sct::kMomNCounts : p->nbins;
+  if (p->scheme == SCT_ALLPAIRS_MOMENTS) {
+    std::vector<MomTriple> tri;
+    std::vector<MomSource> src;
+    mom_layout(tri, src);
+    e = hipMalloc(&p->d_mtri, tri.size() * sizeof(MomTriple));
+    if (e == hipSuccess) e = hipMalloc(&p->d_msrc, src.size() * sizeof(MomSource));
+    if (e == hipSuccess) e = hipMalloc(&p->d_mhist, (size_t)kMomNTri * 64 * sizeof(unsigned));
+    p->mom_nwords = sct::ceil_div(std::max<int64_t>(n, 1), 32);
+    p->mom_nranges = (int)sct::ceil_div(p->mom_nwords, kMomWR);
+    if (e == hipSuccess) e = hipMalloc(&p->d_mmasks, (size_t)(p->mom_nwords + 1) * 64 * sizeof(uint32_t));
+    if (e == hipSuccess)
+      e = hipMalloc(&p->d_mpartial, (size_t)p->mom_nranges * kMomNTri * 64 * sizeof(uint32_t));
+    if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "hipMalloc moments: %s", hipGetErrorString(e)));
+    e = hipMemcpy(p->d_mtri, tri.data(), tri.size() * sizeof(MomTriple), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_msrc, src.data(), src.size() * sizeof(MomSource), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return cleanup(sct::fail(SCT_E_HIP, "copy moments layout: %s", hipGetErrorString(e)));
+  }
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess ||
       cus <= 0)
     cus = 256;
+  // defaults measured on MI355X: MOMENTS unroll 4, SUBSETS@16 bases full unroll
+  p->variant = p->scheme == SCT_ALLPAIRS_MOMENTS ? 4 : (p->npp == 8 ? 3 : 2);
   if (const char* v = getenv("SCT_ALLPAIRS_VARIANT")) {
     const int vv = atoi(v);
-    if ((vv >= 1 && vv <= 2) || (vv >= 11 && vv <= 13)) p->variant = vv;
+    if ((vv >= 1 && vv <= 3) || (vv == 4 && p->scheme == SCT_ALLPAIRS_MOMENTS) || (vv >= 11 && vv <= 13 && p->scheme == SCT_ALLPAIRS_SUBSETS))
+      p->variant = vv;
   }
-  p->grid = grid_for(p->npp, cus, p->variant);
+  p->grid = grid_for(p->npp, cus, p->variant, p->scheme);
   if (const char* f = getenv("SCT_ALLPAIRS_FLUSH_ITEMS")) p->flush_items = atoll(f);
   if (const char* g = getenv("SCT_ALLPAIRS_GRAB")) {
     const int gg = atoi(g);
@@ -579,6 +899,11 @@ extern "C" int sct_allpairs_plan_destroy(sct_allpairs_plan* plan) {
   if (plan->d_codes) (void)hipFree(plan->d_codes);
   if (plan->d_table) (void)hipFree(plan->d_table);
   if (plan->d_queue) (void)hipFree(plan->d_queue);
+  if (plan->d_mtri) (void)hipFree(plan->d_mtri);
+  if (plan->d_msrc) (void)hipFree(plan->d_msrc);
+  if (plan->d_mhist) (void)hipFree(plan->d_mhist);
+  if (plan->d_mmasks) (void)hipFree(plan->d_mmasks);
+  if (plan->d_mpartial) (void)hipFree(plan->d_mpartial);
   delete plan;
   return SCT_OK;
 }
@@ -589,6 +914,46 @@ extern "C" int sct_allpairs_plan_info(const sct_allpairs_plan* plan, int* nbins,
   if (nbins) *nbins = plan->nbins;
   if (items) *items = plan->items;
   if (pairs) *pairs = plan->n * (plan->n - 1) / 2;
+  return SCT_OK;
+}
+
+extern "C" int sct_allpairs_plan_scheme(const sct_allpairs_plan* plan, int* scheme, int* ncounts,
+                                        int* code_bits) {
+  SCT_CHECK(plan != nullptr, "plan is NULL");
+  if (scheme) *scheme = plan->scheme;
+  if (ncounts) *ncounts = plan->ncounts;
+  if (code_bits) *code_bits = plan->code_bits;
+  return SCT_OK;
+}
+
+extern "C" int sct_allpairs_moments(sct_allpairs_plan* plan, int part, int nparts,
+                                    uint64_t* d_counts, void* stream) {
+  SCT_CHECK(plan != nullptr, "plan is NULL");
+  SCT_CHECK(nparts >= 1 && 0 <= part && part < nparts, "part %d of %d", part, nparts);
+  if (plan->scheme != SCT_ALLPAIRS_MOMENTS || plan->n < 2) return SCT_OK;
+  SCT_CHECK(d_counts != nullptr, "counts is NULL");
+  // part p histograms triples [560p/P, 560(p+1)/P) and owns the pairs/singles read off them
+  const int t0 = (int)((int64_t)kMomNTri * part / nparts);
+  const int t1 = (int)((int64_t)kMomNTri * (part + 1) / nparts);
+  if (t0 == t1) return SCT_OK;
+  hipStream_t s = sct::as_stream(stream);
+  const int64_t nwaves = sct::ceil_div(plan->mom_nwords, 2);
+  hipLaunchKernelGGL(moments_masks_kernel, dim3((unsigned)sct::ceil_div(nwaves, 4)), dim3(256), 0, s,
+                     plan->d_codes, plan->n, plan->mom_nwords, plan->d_mmasks);
+  SCT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(moments_count_kernel, dim3(plan->mom_nranges, (unsigned)sct::ceil_div(t1 - t0, kMomTri)),
+                     dim3(256), 0, s, plan->d_mmasks, plan->mom_nwords, plan->d_mtri, t0, t1,
+                     plan->d_mpartial);
+  SCT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(moments_reduce_kernel, dim3((unsigned)sct::ceil_div((t1 - t0) * 64, 256)), dim3(256), 0,
+                     s, plan->d_mpartial, plan->mom_nranges, t0 * 64, t1 * 64, plan->d_mhist);
+  SCT_LAUNCH_CHECK();
+  const int work = (t1 - t0) * 64 + kMomNPair * 16 + sct::kMomG * 4;
+  const int fblocks = (int)std::min<int64_t>(160, sct::ceil_div(work, 256));
+  hipLaunchKernelGGL(moments_finalize_kernel, dim3(fblocks), dim3(256), 0, s, plan->d_mhist, t0, t1,
+                     plan->d_msrc, plan->d_msrc + kMomNPair,
+                     reinterpret_cast<unsigned long long*>(d_counts) + 1 + sct::kMomNProd);
+  SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
 
@@ -676,17 +1041,20 @@ extern "C" int sct_hamming_hist_allpairs_host(const uint64_t* codes, int64_t n, 
   } guard{plan};
   if (plan->nbins != nbins)
     return sct::fail(SCT_E_INVALID, "hist holds %d bins, plan needs %d", nbins, plan->nbins);
-  SCT_HIP(dcounts.alloc((size_t)nbins * 8));
-  SCT_HIP(hipMemset(dcounts.p, 0, (size_t)nbins * 8));
+  const int nc = plan->ncounts;
+  SCT_HIP(dcounts.alloc((size_t)nc * 8));
+  SCT_HIP(hipMemset(dcounts.p, 0, (size_t)nc * 8));
   rc = sct_allpairs_build(plan, nullptr);
+  if (rc != SCT_OK) return rc;
+  rc = sct_allpairs_moments(plan, 0, 1, (uint64_t*)dcounts.p, nullptr);
   if (rc != SCT_OK) return rc;
   rc = sct_allpairs_count(plan, 0, plan->items, (uint64_t*)dcounts.p, 0, nullptr);
   if (rc != SCT_OK) return rc;
   uint64_t counts[129];
-  SCT_HIP(hipMemcpy(counts, dcounts.p, (size_t)nbins * 8, hipMemcpyDeviceToHost));
+  SCT_HIP(hipMemcpy(counts, dcounts.p, (size_t)nc * 8, hipMemcpyDeviceToHost));
   const int64_t expect = n * (n - 1) / 2;
   if ((int64_t)counts[0] != (n >= 2 ? expect : 0))
     return sct::fail(SCT_E_HIP, "pair count mismatch: counted %llu, expected %lld",
                      (unsigned long long)counts[0], (long long)expect);
-  return sct_counts_to_hist(counts, nbins, hist);
+  return sct_counts_to_hist_ex(plan->scheme, counts, nc, hist, nbins);
 }

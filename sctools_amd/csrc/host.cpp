@@ -3,6 +3,8 @@
 #include <math.h>
 #include <string.h>
 
+#include <utility>
+
 #include "sct_common.h"
 
 namespace sct {
@@ -61,6 +63,111 @@ extern "C" int sct_counts_to_hist(const uint64_t* counts, int nbins, uint64_t* h
   for (int d = 0; d < nbins; ++d) {
     if (f[d] < 0) return sct::fail(SCT_E_RANGE, "inconsistent subset counts (bin %d < 0)", d);
     hist[d] = (uint64_t)f[d];
+  }
+  return SCT_OK;
+}
+
+// ---------------------------------------------------------------- MOMENTS inversion
+// The 17 MOMENTS functionals of hist[0..16] (counts layout in sctools_hip.h):
+//   row 0: 1 (pairs);  rows 1..13: prod of bits kMomProducts[r-1] of (d mod 16);
+//   rows 14..16: C(16 - d, k), k = 1..3 (agreement moments).
+// A is fixed and non-singular, so hist = adj(A) counts / det(A).  adj and det come from a
+// fraction-free (Bareiss) Gauss-Jordan elimination of [A | I] in __int128 (every division
+// is exact; |minors| < 1e14), checked once against A adj(A) = det I.
+namespace {
+
+constexpr int kN = sct::kMomNCounts;
+static_assert(kN == sct::kMomG + 1, "MOMENTS system must be square");
+
+int64_t binom(int64_t a, int k) {
+  if (a < k) return 0;
+  int64_t r = 1;
+  for (int j = 0; j < k; ++j) r = r * (a - j) / (j + 1);
+  return r;
+}
+
+int64_t mom_row(int r, int d) {
+  if (r == 0) return 1;
+  if (r <= sct::kMomNProd) {
+    const int m = sct::kMomProducts[r - 1];
+    return ((d & 15) & m) == m ? 1 : 0;
+  }
+  return binom(sct::kMomG - d, r - sct::kMomNProd);
+}
+
+struct MomInverse {
+  bool ok = false;
+  __int128 det = 0;
+  __int128 adj[kN][kN];  // A^-1 = adj / det (row i of adj gives hist[i])
+  MomInverse() {
+    __int128 M[kN][2 * kN];
+    for (int i = 0; i < kN; ++i)
+      for (int j = 0; j < 2 * kN; ++j)
+        M[i][j] = j < kN ? (__int128)mom_row(i, j) : (__int128)(j - kN == i);
+    __int128 prev = 1;
+    for (int k = 0; k < kN; ++k) {
+      int p = k;
+      while (p < kN && M[p][k] == 0) ++p;
+      if (p == kN) return;  // singular
+      if (p != k)
+        for (int j = 0; j < 2 * kN; ++j) std::swap(M[p][j], M[k][j]);
+      for (int i = 0; i < kN; ++i) {
+        if (i == k) continue;
+        for (int j = 0; j < 2 * kN; ++j) {
+          if (j == k) continue;
+          const __int128 v = M[k][k] * M[i][j] - M[i][k] * M[k][j];
+          if (v % prev != 0) return;  // not exact: refuse rather than round
+          M[i][j] = v / prev;
+        }
+        M[i][k] = 0;
+      }
+      prev = M[k][k];
+    }
+    // every diagonal entry now equals det (up to the row swaps' sign, already applied)
+    det = M[kN - 1][kN - 1];
+    for (int i = 0; i < kN; ++i) {
+      if (M[i][i] != det) return;
+      for (int j = 0; j < kN; ++j) adj[i][j] = M[i][kN + j];
+    }
+    // check A adj = det I
+    for (int i = 0; i < kN; ++i)
+      for (int j = 0; j < kN; ++j) {
+        __int128 s = 0;
+        for (int t = 0; t < kN; ++t) s += (__int128)mom_row(i, t) * adj[t][j];
+        if (s != (i == j ? det : 0)) return;
+      }
+    ok = det != 0;
+  }
+};
+
+const MomInverse& mom_inverse() {
+  static const MomInverse inv;  // thread-safe one-time init
+  return inv;
+}
+
+}  // namespace
+
+extern "C" int sct_counts_to_hist_ex(int scheme, const uint64_t* counts, int ncounts,
+                                     uint64_t* hist, int nbins) {
+  SCT_CHECK(counts && hist, "NULL pointer");
+  if (scheme == SCT_ALLPAIRS_SUBSETS) {
+    SCT_CHECK(ncounts == nbins, "SUBSETS counts hold nbins values (%d != %d)", ncounts, nbins);
+    return sct_counts_to_hist(counts, nbins, hist);
+  }
+  SCT_CHECK(scheme == SCT_ALLPAIRS_MOMENTS, "unknown scheme %d", scheme);
+  SCT_CHECK(ncounts == kN && nbins == kN, "MOMENTS counts/hist hold %d values (got %d, %d)", kN,
+            ncounts, nbins);
+  const MomInverse& inv = mom_inverse();
+  if (!inv.ok) return sct::fail(SCT_E_HIP, "MOMENTS system inverse unavailable");
+  for (int i = 0; i < kN; ++i) {
+    __int128 s = 0;
+    for (int j = 0; j < kN; ++j) s += inv.adj[i][j] * (__int128)counts[j];
+    if (s % inv.det != 0)
+      return sct::fail(SCT_E_RANGE, "inconsistent MOMENTS counts (bin %d not integral)", i);
+    const __int128 h = s / inv.det;
+    if (h < 0 || h > (__int128)UINT64_MAX)
+      return sct::fail(SCT_E_RANGE, "inconsistent MOMENTS counts (bin %d out of range)", i);
+    hist[i] = (uint64_t)h;
   }
   return SCT_OK;
 }

@@ -37,6 +37,18 @@ struct DevBuf {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Moment-assisted all-pairs scheme (SCT_ALLPAIRS_MOMENTS, 16-base TwoBit codes):
+// the count kernel accumulates only these 13 subset products of the distance bits
+// d0..d3 (d mod 16), and the agreement moments M_k = sum over pairs of C(16 - d, k),
+// k = 1..kMomOrder, are counted from the codes' 1/2/3-position marginals.  With the
+// pair count, that is 1 + 13 + 3 = 17 independent linear functionals of hist[0..16]
+// (the product set is a minimum one for moments of order <= 3).
+constexpr int kMomG = 16;  // base positions (distance 0..16)
+constexpr int kMomOrder = 3;
+constexpr int kMomNProd = 13;
+constexpr int kMomProducts[kMomNProd] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15};
+constexpr int kMomNCounts = 1 + kMomNProd + kMomOrder;  // [pairs, products..., M1, M2, M3]
+
 }  // namespace sct
 
 #define SCT_HIP(call)                                                                        \

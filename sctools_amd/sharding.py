@@ -3,11 +3,12 @@
 The unordered pairs of a code set are cut into ``items`` equal work items (row block
 x column chunk, see sctools_amd/csrc/allpairs.hip).  Rank r of W counts the
 contiguous item range ``item_range(items, r, W)`` on its own GPU against its own
-replica of the codes (a few MB, so every rank holds them all), producing ``nbins``
-uint64 subset counts.  The counts are linear in the pairs, so ONE all-reduce(sum)
-of ``nbins`` int64 over RCCL (torch.distributed backend "nccl" on ROCm) combines the
-ranks; every rank then inverts the summed counts to the exact histogram.  Integer
-sums are order independent, so the result is bit-identical for any W.
+replica of the codes (a few MB, so every rank holds them all) and, in the MOMENTS
+scheme, moment share r of W, producing ``ncounts`` uint64 counts.  The counts are
+linear in the pairs, so ONE all-reduce(sum) of ``ncounts`` int64 over RCCL
+(torch.distributed backend "nccl" on ROCm) combines the ranks; every rank then
+inverts the summed counts to the exact histogram.  Integer sums are order
+independent, so the result is bit-identical for any W.
 
 The reference (barcode.py:39-46) has no parallelism at all; this is new.
 """
@@ -26,14 +27,14 @@ def item_range(items, rank, world):
     return items * rank // world, items * (rank + 1) // world
 
 
-def combine_counts(counts, group=None):
-    """Sum per-rank subset counts (a torch int64 tensor, in place) over the process
-    group and return the exact histogram as np.uint64 on every rank."""
+def combine_counts(counts, group=None, scheme=_lib.SCHEME_SUBSETS, nbins=None):
+    """Sum per-rank counts (a torch int64 tensor, in place) over the process group and
+    return the exact histogram as np.uint64 on every rank."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
     host = counts.detach().cpu().numpy().astype(np.int64).view(np.uint64)
-    return _lib.counts_to_hist(host)
+    return _lib.counts_to_hist(host, scheme, nbins)
 
 
 def allpairs_histogram_sharded(codes, code_bits=None, group=None, device=None, stream=None):
@@ -57,9 +58,10 @@ def allpairs_histogram_sharded(codes, code_bits=None, group=None, device=None, s
     try:
         s = (stream or torch.cuda.current_stream(device)).cuda_stream
         b, e = item_range(plan.items, rank, world)
-        counts = torch.zeros(plan.nbins, dtype=torch.int64, device=device)
+        counts = torch.zeros(plan.ncounts, dtype=torch.int64, device=device)
         plan.build(s)
+        plan.moments(counts.data_ptr(), rank, world, s)
         plan.count(counts.data_ptr(), b, e, 0, s)
-        return combine_counts(counts, group)
+        return combine_counts(counts, group, plan.scheme, plan.nbins)
     finally:
         plan.close()

@@ -250,7 +250,9 @@ def test_allpairs_shards_sum_to_whole():
     torch = pytest.importorskip("torch")
     codes = synthetic.whitelist_codes(20_000, 16, seed=9)
     d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
-    plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32)
+    # per-range inversion needs self-contained counts: the SUBSETS scheme
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=_lib.SCHEME_SUBSETS)
+    assert plan.scheme == _lib.SCHEME_SUBSETS and plan.ncounts == plan.nbins
     plan.build()
     full = torch.zeros(plan.nbins, dtype=torch.int64, device="cuda")
     plan.count(full.data_ptr())
@@ -278,28 +280,69 @@ def test_allpairs_shards_sum_to_whole():
 
 
 def test_allpairs_737k_properties():
-    """Full config-2 size: size-independent checks + exact parity on a 60k-row prefix."""
+    """Full config-2 size: size-independent checks, the two count schemes agree, and
+    exact parity on a 60k-code prefix."""
     torch = pytest.importorskip("torch")
     n, L, seed = synthetic.CONFIGS[2]
     codes = synthetic.whitelist_codes(n, L, seed)
     d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
-    plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 32)
-    plan.build()
-    counts = torch.zeros(plan.nbins, dtype=torch.int64, device="cuda")
-    plan.count(counts.data_ptr())
-    c = counts.cpu().numpy().view(np.uint64)
-    assert int(c[0]) == n * (n - 1) // 2
-    hist = _lib.counts_to_hist(c)
-    assert int(hist.sum()) == n * (n - 1) // 2
-    # twice gives the same (integer atomics are order independent)
-    counts2 = torch.zeros_like(counts)
-    plan.count(counts2.data_ptr(), grid=333)
-    assert torch.equal(counts, counts2)
-    # exact parity on the items that cover rows < 60k against chunk < 60k columns:
+    hists = {}
+    for scheme in (_lib.SCHEME_MOMENTS, _lib.SCHEME_SUBSETS):
+        plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 32, scheme=scheme)
+        assert plan.scheme == scheme
+        plan.build()
+        counts = torch.zeros(plan.ncounts, dtype=torch.int64, device="cuda")
+        plan.moments(counts.data_ptr())
+        plan.count(counts.data_ptr())
+        c = counts.cpu().numpy().view(np.uint64)
+        assert int(c[0]) == n * (n - 1) // 2
+        hist = plan.counts_to_hist(c)
+        assert int(hist.sum()) == n * (n - 1) // 2
+        # twice gives the same (integer atomics are order independent)
+        counts2 = torch.zeros_like(counts)
+        plan.moments(counts2.data_ptr())
+        plan.count(counts2.data_ptr(), grid=333)
+        assert torch.equal(counts, counts2)
+        hists[scheme] = hist.tolist()
+        plan.close()
+    assert hists[_lib.SCHEME_MOMENTS] == hists[_lib.SCHEME_SUBSETS]
+    # the mean distance is fixed by the per-position base counts alone (first moment)
+    bases = (codes[:, None] >> (2 * np.arange(16, dtype=np.uint64))) & np.uint64(3)
+    agree = sum(int(np.bincount(bases[:, p].astype(np.int64), minlength=4).astype(object).dot(
+        np.bincount(bases[:, p].astype(np.int64), minlength=4).astype(object) - 1)) // 2 for p in range(16))
+    h = hists[_lib.SCHEME_MOMENTS]
+    assert sum(d * x for d, x in enumerate(h)) == 16 * (n * (n - 1) // 2) - agree
+    # exact parity on a 60k prefix
     sub = codes[:60_000]
     hs = _lib.hamming_hist_allpairs(sub, 32)
     ref = O.c_hist_rows(sub)[:17]
     assert hs.astype(np.int64).tolist() == ref.tolist()
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 64, 255, 1025, 4100, 20_000])
+def test_allpairs_moments_scheme_matches_oracle(n):
+    """MOMENTS scheme (13 products + agreement moments) vs the C oracle, including
+    duplicates (d = 0) and complementary codes (d = 16), which share d mod 16 = 0."""
+    torch = pytest.importorskip("torch")
+    codes = synthetic.whitelist_codes(max(2, n - n // 8), 16, seed=n)
+    extra = []
+    if n >= 5:
+        extra = [codes[0], codes[1] ^ np.uint64(0xAAAAAAAA), codes[1] ^ np.uint64(0xFFFFFFFF)]
+    codes = np.concatenate([codes, np.array(extra, dtype=np.uint64)])[:max(n, 2)]
+    d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=_lib.SCHEME_MOMENTS)
+    plan.build()
+    counts = torch.zeros(plan.ncounts, dtype=torch.int64, device="cuda")
+    for part in range(3):  # moment shares, as three ranks would add them
+        plan.moments(counts.data_ptr(), part, 3)
+    items = plan.items
+    for b, e in ((0, items // 2), (items // 2, items)):
+        plan.count(counts.data_ptr(), b, e, grid=29)
+    hist = plan.counts_to_hist(counts.cpu().numpy().view(np.uint64))
+    ref = O.c_hist_rows(codes)[:17]
+    assert hist.astype(np.int64).tolist() == ref.tolist()
+    # the one-shot host entry point picks MOMENTS for 16-base codes
+    assert _lib.hamming_hist_allpairs(codes, 32).astype(np.int64).tolist() == ref.tolist()
     plan.close()
 
 

@@ -1,10 +1,11 @@
 """Interleaved A/B timing of all-pairs count-kernel variants in ONE process.
 
-Variants are selected at plan creation through SCT_ALLPAIRS_UNROLL / SCT_ALLPAIRS_GRID;
-each round times every variant once (HIP events on the launch stream); prints the
-median and min per variant and checks that all variants produce identical counts.
+Variants are selected at plan creation through SCT_ALLPAIRS_VARIANT / _GRID / _GRAB and
+the count scheme (s=0 SUBSETS, s=1 MOMENTS); each round times every variant once (HIP
+events on the launch stream: the count kernel, and the moments pass separately); prints
+the median and min per variant and checks that all variants give identical histograms.
 
-  python tools/ab_allpairs.py --config 2 --rounds 7 --variants "v=2" "v=1" "v=1,grid=2048"
+  python tools/ab_allpairs.py --config 2 --rounds 7 --variants "v=2,s=0" "v=3,s=1" "v=1,grid=2048"
 """
 
 import argparse
@@ -39,29 +40,34 @@ def main():
                 os.environ[env] = kv[key]
             else:
                 os.environ.pop(env, None)
-        p = _lib.AllPairsPlan(d.data_ptr(), n, 2 * L)
+        p = _lib.AllPairsPlan(d.data_ptr(), n, 2 * L, scheme=int(kv.get("s", "-1")))
         p.build()
         plans.append((v, p))
     s = torch.cuda.current_stream()
     times = {v: [] for v, _ in plans}
+    mtimes = {v: [] for v, _ in plans}
     ref = None
     for _ in range(a.rounds):
         for v, p in plans:
-            c = torch.zeros(p.nbins, dtype=torch.int64, device="cuda")
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            c = torch.zeros(p.ncounts, dtype=torch.int64, device="cuda")
+            em, e0, e1 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            em.record(s)
+            p.moments(c.data_ptr(), stream=s.cuda_stream)
             e0.record(s)
             p.count(c.data_ptr(), stream=s.cuda_stream)
             e1.record(s)
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1))
-            cc = c.cpu().numpy()
+            mtimes[v].append(em.elapsed_time(e0))
             if int(dict(x.split("=") for x in v.split(",")).get("v", "2")) >= 10:
                 continue  # ablation builds compute wrong counts by design
+            h = p.counts_to_hist(c.cpu().numpy().view(np.uint64))
             if ref is None:
-                ref = cc
-            assert np.array_equal(ref, cc), v
+                ref = h
+            assert np.array_equal(ref, h), v
     pairs = plans[0][1].pairs
     out = {v: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+               "moments_ms": float(np.median(mtimes[v])), "scheme": dict(plans)[v].scheme,
                "pairs_per_s": pairs / (np.median(t) * 1e-3)} for v, t in times.items()}
     print(json.dumps(out, indent=1))
 

@@ -188,15 +188,16 @@ def bench_allpairs5():
     codes = synthetic.whitelist_codes(n, L, seed)
     d = torch.from_numpy(codes.view(np.int64)).to(dev)
     plan = _lib.AllPairsPlan(d.data_ptr(), n, 2 * L)
-    counts = torch.zeros(plan.nbins, dtype=torch.int64, device=dev)
+    counts = torch.zeros(plan.ncounts, dtype=torch.int64, device=dev)
 
     def run():
         counts.zero_()
         plan.build(s.cuda_stream)
+        plan.moments(counts.data_ptr(), stream=s.cuda_stream)
         plan.count(counts.data_ptr(), stream=s.cuda_stream)
 
     med, mn = timed(run, 3, s)
-    hist = _lib.counts_to_hist(counts.cpu().numpy().view(np.uint64))
+    hist = plan.counts_to_hist(counts.cpu().numpy().view(np.uint64))
     assert int(hist.sum()) == plan.pairs
     plan.close()
     return {"path": "all-pairs histogram config 5 (3,686,400 codes)", "pairs": plan.pairs, "median_ms": med,
