@@ -37,10 +37,10 @@ VALU_PEAK_OPS = 256 * 128 * 2.4e9
 ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-bit code word
 # VALU issue slots the bit-sliced count kernel spends per pair at 16 bp, from its unmasked
 # loop (v_bcnt_u32_b32 counts 2: half rate on gfx950), per count scheme:
-#   SUBSETS: 33 v_bitop3 + 16 v_bcnt + 6 v_xor/v_and + 2 address v_add per 32 pairs;
-#   MOMENTS: 29 v_bitop3 + 13 v_bcnt + 7 v_xor/v_and + 2 address v_add per 32 pairs.
-ISSUE_SLOTS_PER_PAIR = {_lib.SCHEME_SUBSETS: (33 + 2 * 16 + 6 + 2) / 32.0,
-                        _lib.SCHEME_MOMENTS: (29 + 2 * 13 + 7 + 2) / 32.0}
+#   SUBSETS (nibble tables, full unroll): 33 v_bitop3 + 16 v_bcnt + 6 v_xor/v_and per 32 pairs;
+#   MOMENTS (triple tables, unroll 2): 24 v_bitop3 + 13 v_bcnt + 4 v_xor/v_and + 1.5 v_add.
+ISSUE_SLOTS_PER_PAIR = {_lib.SCHEME_SUBSETS: (33 + 2 * 16 + 6) / 32.0,
+                        _lib.SCHEME_MOMENTS: (24 + 2 * 13 + 4 + 1.5) / 32.0}
 
 
 def parse():
@@ -165,7 +165,7 @@ def main():
     slots_per_pair = ISSUE_SLOTS_PER_PAIR[plan.scheme] if L == 16 else float("nan")
     slots = my_pairs * slots_per_pair / (kms * 1e-3)
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_allpairs_r01.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_allpairs_latest.json")  # tools/summarize_profile.py
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")

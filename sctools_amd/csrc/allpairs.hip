@@ -38,6 +38,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "sct_common.h"
 
 namespace {
@@ -57,21 +59,58 @@ __device__ __forceinline__ void bcnt_acc(uint32_t& c, uint32_t x) {
   asm("v_bcnt_u32_b32 %0, %1, %0" : "+v"(c) : "v"(x));
 }
 
+// VGPR banks: a v_bitop3_b32 whose three sources sit in one bank (register index mod 4)
+// issues at half rate on gfx950 (profiles/valu_banks_r01.json).  A b128 LDS read lands in
+// 4 consecutive registers, so the same component of three reads is three same-bank
+// sources -- exactly the adder tree's first level.  The table therefore stores nibble
+// pp's four planes rotated by pp mod 4 (slot (k + pp) % 4 holds plane k), which puts the
+// planes of consecutive nibbles in consecutive banks; the kernel un-rotates at compile
+// time (no instructions).
+__host__ __device__ constexpr int plane_slot(int plane, int pp) { return (plane + pp) & 3; }
+__device__ __forceinline__ uint32_t comp(const uint4& e, int slot) {
+  return slot == 0 ? e.x : (slot == 1 ? e.y : (slot == 2 ? e.z : e.w));
+}
+
 constexpr int bitlen(int v) {
   int b = 0;
   while ((1 << b) <= v) ++b;
   return b;
 }
 
-template <int NPP>
+// Lookup layout of one group pair (64 codes) in the selection table.
+//   nibble layout (SUBSETS): NPP lookups, lookup g = the query's nibble g (bases 2g, 2g+1),
+//     16 entries each;
+//   triple layout (MOMENTS, 16 bases): 6 lookups -- bases {0,1} and {2,3} (16 entries
+//     each) and the triples {4,5,6} {7,8,9} {10,11,12} {13,14,15} (64 entries each): 16
+//     2-bit inputs to the adder tree become 6, and with the codes sorted the lanes of a
+//     wave share their high bases, so the 64-entry lookups of the high triples broadcast
+//     instead of bank-conflicting.
+constexpr int kTriNL = 6;
+constexpr int kTriRow = 2 * 16 + 4 * 64;  // uint4 entries per group pair
+__host__ __device__ constexpr int tri_base(int g) { return g < 2 ? 16 * g : 32 + 64 * (g - 2); }
+__host__ __device__ constexpr int tri_shift(int g) { return g < 2 ? 4 * g : 8 + 6 * (g - 2); }
+__host__ __device__ constexpr int tri_width(int g) { return g < 2 ? 4 : 6; }
+
+template <int NPP, bool MOM = false>
 struct Geom {
-  static constexpr int G = 2 * NPP;         // max distance
-  static constexpr int B = bitlen(G);       // distance bit-planes
-  static constexpr int CT = NPP <= 8 ? 32 : 16;  // groups per column chunk
-  static constexpr int CB = 32 * CT;        // codes per column chunk
-  static constexpr int K = CB / RB;         // row blocks per chunk step
-  static constexpr int TILE = CT / 2 * NPP * 16;  // uint4 entries per chunk (32 KiB at NPP 8/16)
+  static constexpr int G = 2 * NPP;                  // max distance
+  static constexpr int B = MOM ? 4 : bitlen(G);      // distance bit-planes (MOMENTS: d mod 16)
+  static constexpr int CT = MOM ? 16 : (NPP <= 8 ? 32 : 16);  // groups per column chunk
+  static constexpr int CB = 32 * CT;                 // codes per column chunk
+  static constexpr int K = CB / RB;                  // row blocks per chunk step
+  static constexpr int NL = MOM ? kTriNL : NPP;      // lookups per group pair
+  static constexpr int ROW = MOM ? kTriRow : NPP * 16;  // uint4 entries per group pair
+  static constexpr int TILE = CT / 2 * ROW;          // uint4 per chunk (32 / 36 KiB)
 };
+
+// LDS offset (uint4 units, within a group-pair row) of lookup g for query q
+template <int NPP, bool MOM>
+__device__ __forceinline__ int lookup_off(uint64_t q, int g) {
+  if constexpr (MOM)
+    return tri_base(g) + (int)((q >> tri_shift(g)) & ((1u << tri_width(g)) - 1u));
+  else
+    return g * 16 + (int)((q >> (4 * g)) & 15u);
+}
 
 // Reduce N equal-weight planes to one; writes N/2 carries (next weight).  Balanced
 // (Wallace) order: each level compresses every disjoint triple with a full adder in
@@ -200,17 +239,18 @@ struct NCount {
 };
 
 template <int NPP, bool MASKED, bool MOM, int ABL = 0>
-__device__ __forceinline__ void one_group(const uint32_t (&s0)[NPP], const uint32_t (&s1)[NPP],
+__device__ __forceinline__ void one_group(const uint32_t (&s0)[Geom<NPP, MOM>::NL],
+                                          const uint32_t (&s1)[Geom<NPP, MOM>::NL],
                                           int64_t i, int64_t jg, int64_t n,
                                           uint32_t (&cnt)[NCount<NPP, MOM>::value], uint32_t& cnt0) {
-  // MOMENTS keeps 4 planes: the carry into plane 4 is dropped, leaving d mod 16
-  constexpr int B = MOM ? 4 : Geom<NPP>::B;
+  constexpr int NL = Geom<NPP, MOM>::NL;
+  constexpr int B = Geom<NPP, MOM>::B;  // MOMENTS: the carry into plane 4 is dropped (d mod 16)
   uint32_t d[B];
   if constexpr (ABL == 2) {  // ablation: no adder tree (planes straight into counting)
 #pragma unroll
-    for (int b = 0; b < B; ++b) d[b] = s0[b % NPP] ^ s1[(b + 1) % NPP];
+    for (int b = 0; b < B; ++b) d[b] = s0[b % NL] ^ s1[(b + 1) % NL];
   } else {
-    adder_tree<NPP, B>(s0, s1, d);
+    adder_tree<NL, B>(s0, s1, d);
   }
   if constexpr (ABL == 1) {  // ablation: no counting (keep the planes live, 1 op each)
 #pragma unroll
@@ -234,48 +274,52 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
                                              int64_t j0, int64_t n,
                                              uint32_t (&cnt)[NCount<NPP, MOM>::value],
                                              uint32_t& cnt0) {
-  using Gm = Geom<NPP>;
-  int off[NPP];
+  using Gm = Geom<NPP, MOM>;
+  constexpr int NL = Gm::NL;
+  int off[NL];
 #pragma unroll
-  for (int pp = 0; pp < NPP; ++pp) off[pp] = pp * 16 + (int)((q >> (4 * pp)) & 15u);
+  for (int g = 0; g < NL; ++g) off[g] = lookup_off<NPP, MOM>(q, g);
+  uint4 e0[NL];
+  if constexpr (ABL == 3) {  // ablation: no LDS reads after the first group pair
+#pragma unroll
+    for (int g = 0; g < NL; ++g) e0[g] = tile[off[g]];
+  }
 
-  {
-#pragma unroll UNROLL
-    for (int h = 0; h < Gm::CT / 2; ++h) {
-      uint32_t s0a[NPP], s1a[NPP], s0b[NPP], s1b[NPP];
+  constexpr int U = UNROLL < Gm::CT / 2 ? UNROLL : Gm::CT / 2;
+#pragma unroll U
+  for (int h = 0; h < Gm::CT / 2; ++h) {
+    uint32_t s0a[NL], s1a[NL], s0b[NL], s1b[NL];
 #pragma unroll
-      for (int pp = 0; pp < NPP; ++pp) {
-        uint4 e;
-        if constexpr (ABL == 3) {  // ablation: no LDS reads (lane-varying fake planes)
-          e = make_uint4(off[pp] * 0x9E3779B9u + h, off[pp] ^ (h * 0x85EBCA6Bu), off[pp] + 77u * h,
-                         off[pp] * 3u - h);
-        } else {
-          e = tile[h * NPP * 16 + off[pp]];
-        }
-        s0a[pp] = e.x;
-        s1a[pp] = e.y;
-        s0b[pp] = e.z;
-        s1b[pp] = e.w;
+    for (int g = 0; g < NL; ++g) {
+      uint4 e;
+      if constexpr (ABL == 3) {
+        e = e0[g];
+        asm volatile("" : "+v"(e.x), "+v"(e.y), "+v"(e.z), "+v"(e.w));  // opaque: no CSE
+      } else {
+        e = tile[h * Gm::ROW + off[g]];
       }
-      one_group<NPP, MASKED, MOM, ABL>(s0a, s1a, i, j0 + 64 * h, n, cnt, cnt0);
-      one_group<NPP, MASKED, MOM, ABL>(s0b, s1b, i, j0 + 64 * h + 32, n, cnt, cnt0);
+      s0a[g] = comp(e, plane_slot(0, g));
+      s1a[g] = comp(e, plane_slot(1, g));
+      s0b[g] = comp(e, plane_slot(2, g));
+      s1b[g] = comp(e, plane_slot(3, g));
     }
+    one_group<NPP, MASKED, MOM, ABL>(s0a, s1a, i, j0 + 64 * h, n, cnt, cnt0);
+    one_group<NPP, MASKED, MOM, ABL>(s0b, s1b, i, j0 + 64 * h + 32, n, cnt, cnt0);
   }
   if constexpr (!MASKED) cnt0 += Gm::CB;
 }
 
-// Count-kernel variants (A/B-selectable with SCT_ALLPAIRS_VARIANT): 1 = one group pair
-// per loop trip (108 VGPRs), 2 = two per trip (124 VGPRs, 4 waves/SIMD), 3 = the chunk's
-// group pairs fully unrolled (LDS offsets become immediates: no address VALU).
-// Register prefetch / ping-pong variants measured slower and were dropped.
+// Count-kernel variants (A/B-selectable with SCT_ALLPAIRS_VARIANT): the group-pair loop
+// unrolled 1, 2, fully (3: LDS offsets become immediates) or 4 times.  A software-
+// pipelined form (next group pair's reads issued before this one's counting) and forced
+// occupancy (amdgpu_waves_per_eu) measured no faster and were dropped.
 template <int V> struct Variant { static constexpr int UNROLL = V, ABL = 0; };
 template <> struct Variant<3> { static constexpr int UNROLL = 16, ABL = 0; };
-template <> struct Variant<4> { static constexpr int UNROLL = 4, ABL = 0; };
 #ifdef SCT_ABLATION
 // ablation builds (wrong results, timing only): 11 no counting, 12 no tree, 13 no LDS reads
-template <> struct Variant<11> { static constexpr int UNROLL = 2, ABL = 1; };
-template <> struct Variant<12> { static constexpr int UNROLL = 2, ABL = 2; };
-template <> struct Variant<13> { static constexpr int UNROLL = 2, ABL = 3; };
+template <> struct Variant<11> { static constexpr int UNROLL = 4, ABL = 1; };
+template <> struct Variant<12> { static constexpr int UNROLL = 4, ABL = 2; };
+template <> struct Variant<13> { static constexpr int UNROLL = 4, ABL = 3; };
 #endif
 
 // Workgroup reduction of the per-lane counters: 64-lane butterfly (shfl_xor, lowered to
@@ -315,7 +359,7 @@ __global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __re
                                                             int64_t grab, int64_t flush_items,
                                                             unsigned long long* __restrict__ queue,
                                                             unsigned long long* __restrict__ out) {
-  using Gm = Geom<NPP>;
+  using Gm = Geom<NPP, MOM>;
   constexpr int G = NCount<NPP, MOM>::value;  // lane counters besides the pair count
   __shared__ __attribute__((aligned(16))) uint4 tile[Gm::TILE];
   __shared__ int64_t s_grab;
@@ -409,7 +453,42 @@ __global__ void allpairs_build_kernel(const uint64_t* __restrict__ codes, int64_
       s[2 * half + 1] |= (m0 & m1) << k;
     }
   }
-  table[idx] = make_uint4(s[0], s[1], s[2], s[3]);
+  uint32_t r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[plane_slot(k, pp)] = s[k];
+  table[idx] = make_uint4(r[0], r[1], r[2], r[3]);
+}
+
+// Triple layout (MOMENTS): entry (h, lookup g, value c) = bit-sliced mismatch counts
+// (0..3) of the bases of lookup g of the 64 codes of group pair h against the query's
+// bases c (c's digits in the same MSB-first order as the code).  One thread per entry.
+__global__ void allpairs_build_tri_kernel(const uint64_t* __restrict__ codes, int64_t n,
+                                          int64_t entries, uint4* __restrict__ table) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= entries) return;
+  const int64_t h = idx / kTriRow;
+  const int e = (int)(idx - h * kTriRow);
+  int g = 0;
+  while (g + 1 < kTriNL && e >= tri_base(g + 1)) ++g;
+  const uint32_t c = (uint32_t)(e - tri_base(g));
+  const int shift = tri_shift(g), nb = tri_width(g) / 2;
+  uint32_t s[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) {
+      const int64_t j = h * 64 + half * 32 + k;
+      const uint32_t x = (j < n ? (uint32_t)(codes[j] >> shift) : 0u) ^ c;
+      uint32_t m = 0;
+      for (int t = 0; t < nb; ++t) m += ((x >> (2 * t)) & 3u) != 0u;
+      s[2 * half] |= (m & 1u) << k;
+      s[2 * half + 1] |= (m >> 1) << k;
+    }
+  }
+  uint32_t r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[plane_slot(k, g)] = s[k];
+  table[idx] = make_uint4(r[0], r[1], r[2], r[3]);
 }
 
 __global__ void or_reduce_kernel(const uint64_t* __restrict__ codes, int64_t n,
@@ -590,7 +669,14 @@ __global__ __launch_bounds__(256) void moments_finalize_kernel(const unsigned* _
   }
 }
 
-int ct_for(int npp) { return npp <= 8 ? 32 : 16; }
+// groups per column chunk: nibble layout 32 (16 above 8 nibbles), triple layout 16
+int ct_for(int npp, bool tri) { return tri ? 16 : (npp <= 8 ? 32 : 16); }
+bool mom_supported(int npp, int64_t n) { return npp * 2 == sct::kMomG && n <= 100000000LL; }
+// what SCT_ALLPAIRS_AUTO resolves to (SCT_ALLPAIRS_SCHEME=0 in the environment forces SUBSETS)
+bool auto_moments(int npp, int64_t n) {
+  const char* v = getenv("SCT_ALLPAIRS_SCHEME");
+  return mom_supported(npp, n) && !(v && atoi(v) == 0);
+}
 
 }  // namespace
 
@@ -606,6 +692,9 @@ struct sct_allpairs_plan {
   int64_t items = 0;
   int grid = 0;
   uint64_t* d_codes = nullptr;
+  uint64_t* d_sorted = nullptr;  // MOMENTS: the codes sorted (rows of a wave share high bases)
+  void* d_sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
   uint4* d_table = nullptr;
   int64_t table_entries = 0;
   int variant = 2;  // count-kernel variant (SCT_ALLPAIRS_VARIANT=1..4, see Variant<>)
@@ -631,78 +720,72 @@ int64_t rows_of_chunk(const sct_allpairs_plan* p, int64_t c) {
   return maxj <= 0 ? 0 : (maxj + RB - 1) / RB;
 }
 
+// The count kernel instantiations a plan can launch: (variant, scheme) -> kernel.
+// SUBSETS: variants 1, 2 (and 3 = full unroll at 16 bases); MOMENTS (16 bases only):
+// 1, 2, 3, 4; ablation builds add 11..13 at 16 bases.
+template <int NPP>
+struct CountKernels {
+  using Fn = void (*)(const uint64_t*, const uint4*, int64_t, int64_t, int64_t, int64_t, int64_t,
+                      int64_t, unsigned long long*, unsigned long long*);
+  static Fn get(int variant, int scheme) {
+    if constexpr (NPP == 8) {
+      if (scheme == SCT_ALLPAIRS_MOMENTS) {
+        switch (variant) {
+          case 1: return allpairs_count_kernel<NPP, 1, true>;
+          case 3: return allpairs_count_kernel<NPP, 3, true>;
+          case 4: return allpairs_count_kernel<NPP, 4, true>;
+#ifdef SCT_ABLATION
+          case 11: return allpairs_count_kernel<NPP, 11, true>;
+          case 12: return allpairs_count_kernel<NPP, 12, true>;
+          case 13: return allpairs_count_kernel<NPP, 13, true>;
+#endif
+          default: return allpairs_count_kernel<NPP, 2, true>;
+        }
+      }
+      switch (variant) {
+        case 1: return allpairs_count_kernel<NPP, 1, false>;
+        case 3: return allpairs_count_kernel<NPP, 3, false>;
+#ifdef SCT_ABLATION
+        case 11: return allpairs_count_kernel<NPP, 11, false>;
+        case 12: return allpairs_count_kernel<NPP, 12, false>;
+        case 13: return allpairs_count_kernel<NPP, 13, false>;
+#endif
+        default: return allpairs_count_kernel<NPP, 2, false>;
+      }
+    } else {
+      if (scheme == SCT_ALLPAIRS_MOMENTS) return nullptr;
+      return variant == 1 ? allpairs_count_kernel<NPP, 1, false> : allpairs_count_kernel<NPP, 2, false>;
+    }
+  }
+};
+
 template <int NPP>
 int launch_count(sct_allpairs_plan* p, int64_t b, int64_t e, uint64_t* d_counts, int grid,
                  hipStream_t s) {
-  const int variant = p->variant;
+  auto fn = CountKernels<NPP>::get(p->variant, p->scheme);
+  if (!fn) return sct::fail(SCT_E_INVALID, "MOMENTS scheme needs 16-base codes");
   if (grid <= 0) grid = p->grid;
   const int64_t total = e - b;
   if (grid > total) grid = (int)total;
-  SCT_CHECK(p->grab > 0 && p->grab * Geom<NPP>::CB < 0xFFFFFFFFLL, "grab too large");
-  int64_t flush = 0xFFFFFFFFLL / Geom<NPP>::CB - p->grab;
+  SCT_CHECK(p->grab > 0 && p->grab * p->cb < 0xFFFFFFFFLL, "grab too large");
+  // a lane adds at most cb pairs per item to each u32 counter: flush before 2^32
+  int64_t flush = 0xFFFFFFFFLL / p->cb - p->grab;
   if (p->flush_items > 0 && p->flush_items < flush) flush = p->flush_items;
   SCT_HIP(hipMemsetAsync(p->d_queue, 0, sizeof(unsigned long long), s));
-#define SCT_LAUNCH_V(V, MOM)                                                                      \
-  hipLaunchKernelGGL((allpairs_count_kernel<NPP, V, MOM>), dim3(grid), dim3(RB), 0, s, p->d_codes, \
-                     p->d_table, p->n, p->nchunks, b, e, p->grab, flush, p->d_queue,               \
-                     reinterpret_cast<unsigned long long*>(d_counts))
-  if (p->scheme == SCT_ALLPAIRS_MOMENTS) {
-    if constexpr (NPP == 8) {
-      switch (variant) {
-        case 1: SCT_LAUNCH_V(1, true); break;
-        case 3: SCT_LAUNCH_V(3, true); break;
-        case 4: SCT_LAUNCH_V(4, true); break;
-        default: SCT_LAUNCH_V(2, true); break;
-      }
-    } else {
-      return sct::fail(SCT_E_INVALID, "MOMENTS scheme needs 16-base codes");
-    }
-  } else {
-    switch (variant) {
-      case 1: SCT_LAUNCH_V(1, false); break;
-      case 3: if constexpr (NPP == 8) { SCT_LAUNCH_V(3, false); break; } else { SCT_LAUNCH_V(2, false); break; }
-#ifdef SCT_ABLATION
-      case 11: if constexpr (NPP == 8) SCT_LAUNCH_V(11, false); break;
-      case 12: if constexpr (NPP == 8) SCT_LAUNCH_V(12, false); break;
-      case 13: if constexpr (NPP == 8) SCT_LAUNCH_V(13, false); break;
-#endif
-      default: SCT_LAUNCH_V(2, false); break;
-    }
-  }
-#undef SCT_LAUNCH_V
+  const uint64_t* codes = p->d_sorted ? p->d_sorted : p->d_codes;
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(RB), 0, s, codes, p->d_table, p->n, p->nchunks, b, e,
+                     p->grab, flush, p->d_queue, reinterpret_cast<unsigned long long*>(d_counts));
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
 
-template <int NPP, int V, bool MOM>
-int occupancy_of() {
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, allpairs_count_kernel<NPP, V, MOM>, RB,
-                                                   0) != hipSuccess ||
-      per_cu <= 0)
-    per_cu = 4;
-  return per_cu;
-}
-
 template <int NPP>
 int occupancy_grid(int cus, int variant, int scheme) {
-  int per_cu;
-  if constexpr (NPP == 8) {
-    if (scheme == SCT_ALLPAIRS_MOMENTS) {
-      switch (variant) {
-        case 1: per_cu = occupancy_of<NPP, 1, true>(); break;
-        case 3: per_cu = occupancy_of<NPP, 3, true>(); break;
-        case 4: per_cu = occupancy_of<NPP, 4, true>(); break;
-        default: per_cu = occupancy_of<NPP, 2, true>(); break;
-      }
-      return cus * per_cu;
-    }
-    if (variant == 3) return cus * occupancy_of<NPP, 3, false>();
-  }
-  switch (variant) {
-    case 1: per_cu = occupancy_of<NPP, 1, false>(); break;
-    default: per_cu = occupancy_of<NPP, 2, false>(); break;
-  }
+  int per_cu = 0;
+  auto fn = CountKernels<NPP>::get(variant, scheme);
+  if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, RB, 0) != hipSuccess ||
+      per_cu <= 0)
+    per_cu = 4;
   return cus * per_cu;  // persistent: every workgroup resident, pulling from the queue
 }
 
@@ -823,7 +906,19 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
   p->code_bits = code_bits;
   p->npp = (code_bits + 3) / 4;
   p->nbins = 2 * p->npp + 1;
-  p->ct = ct_for(p->npp);
+  // MOMENTS needs 16-base codes (29..32 bits); AUTO picks it there
+  // (u32 marginal bins and u64 M_3 <= C(n,2)*560 bound n; 1e8 codes is far beyond a whitelist)
+  const bool mom_ok = mom_supported(p->npp, n);
+  if (scheme == SCT_ALLPAIRS_MOMENTS && !mom_ok)
+    return cleanup(sct::fail(SCT_E_INVALID, "MOMENTS scheme needs code_bits in 29..32 (got %d) "
+                             "and n <= 1e8", code_bits));
+  p->scheme = (scheme == SCT_ALLPAIRS_MOMENTS ||
+               (scheme == SCT_ALLPAIRS_AUTO && auto_moments(p->npp, n)))
+                  ? SCT_ALLPAIRS_MOMENTS
+                  : SCT_ALLPAIRS_SUBSETS;
+  p->ncounts = p->scheme == SCT_ALLPAIRS_MOMENTS ? sct::kMomNCounts : p->nbins;
+  const bool tri = p->scheme == SCT_ALLPAIRS_MOMENTS;
+  p->ct = ct_for(p->npp, tri);
   p->cb = 32LL * p->ct;
   p->nchunks = n > 0 ? sct::ceil_div(n, p->cb) : 0;
   p->items = 0;
@@ -832,25 +927,22 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
     const int64_t last = p->nchunks - 1;
     p->items = K * last * (last + 1) / 2 + rows_of_chunk(p, last);
   }
-  p->table_entries = p->nchunks * (p->ct / 2) * (int64_t)p->npp * 16;
+  p->table_entries = p->nchunks * (p->ct / 2) * (int64_t)(tri ? kTriRow : p->npp * 16);
   if (p->table_entries > 0) {
     e = hipMalloc(&p->d_table, (size_t)p->table_entries * sizeof(uint4));
     if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "hipMalloc table: %s", hipGetErrorString(e)));
   }
   e = hipMalloc(&p->d_queue, sizeof(unsigned long long));
   if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "hipMalloc queue: %s", hipGetErrorString(e)));
-  // MOMENTS needs 16-base codes (29..32 bits); AUTO picks it there
-  // (u32 marginal bins and u64 M_3 <= C(n,2)*560 bound n; 1e8 codes is far beyond a whitelist)
-  const bool mom_ok = p->npp * 2 == sct::kMomG && n <= 100000000LL;
-  if (scheme == SCT_ALLPAIRS_MOMENTS && !mom_ok)
-    return cleanup(sct::fail(SCT_E_INVALID, "MOMENTS scheme needs code_bits in 29..32 (got %d) "
-                             "and n <= 1e8", code_bits));
-  if (const char* v = getenv("SCT_ALLPAIRS_SCHEME"))
-    if (scheme == SCT_ALLPAIRS_AUTO) scheme = atoi(v) == 0 ? SCT_ALLPAIRS_SUBSETS : SCT_ALLPAIRS_AUTO;
-  p->scheme = (scheme == SCT_ALLPAIRS_MOMENTS || (scheme == SCT_ALLPAIRS_AUTO && mom_ok))
-                  ? SCT_ALLPAIRS_MOMENTS
-                  : SCT_ALLPAIRS_SUBSETS;
-  p->ncounts = p->scheme == SCT_ALLPAIRS_MOMENTS ? sct::kMomNCounts : p->nbins;
+  if (tri && n > 0) {
+    // sorted row order: the lanes of a wave then share their high bases
+    e = hipMalloc(&p->d_sorted, (size_t)n * 8);
+    if (e == hipSuccess)
+      e = hipcub::DeviceRadixSort::SortKeys(nullptr, p->sort_tmp_bytes, (const uint64_t*)nullptr,
+                                            (uint64_t*)nullptr, (int)n, 0, 32);
+    if (e == hipSuccess) e = hipMalloc(&p->d_sort_tmp, std::max<size_t>(p->sort_tmp_bytes, 16));
+    if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "sort buffers: %s", hipGetErrorString(e)));
+  }
   if (p->scheme == SCT_ALLPAIRS_MOMENTS) {
     std::vector<MomTriple> tri;
     std::vector<MomSource> src;
@@ -873,11 +965,11 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess ||
       cus <= 0)
     cus = 256;
-  // defaults measured on MI355X: MOMENTS unroll 4, SUBSETS@16 bases full unroll
-  p->variant = p->scheme == SCT_ALLPAIRS_MOMENTS ? 4 : (p->npp == 8 ? 3 : 2);
+  // defaults measured on MI355X: MOMENTS unroll 2, SUBSETS@16 bases full unroll
+  p->variant = p->scheme == SCT_ALLPAIRS_MOMENTS ? 2 : (p->npp == 8 ? 3 : 2);
   if (const char* v = getenv("SCT_ALLPAIRS_VARIANT")) {
     const int vv = atoi(v);
-    if ((vv >= 1 && vv <= 3) || (vv == 4 && p->scheme == SCT_ALLPAIRS_MOMENTS) || (vv >= 11 && vv <= 13 && p->scheme == SCT_ALLPAIRS_SUBSETS))
+    if ((vv >= 1 && vv <= 3) || (vv == 4 && p->scheme == SCT_ALLPAIRS_MOMENTS) || (vv >= 11 && vv <= 13))
       p->variant = vv;
   }
   p->grid = grid_for(p->npp, cus, p->variant, p->scheme);
@@ -897,6 +989,8 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
 extern "C" int sct_allpairs_plan_destroy(sct_allpairs_plan* plan) {
   if (!plan) return SCT_OK;
   if (plan->d_codes) (void)hipFree(plan->d_codes);
+  if (plan->d_sorted) (void)hipFree(plan->d_sorted);
+  if (plan->d_sort_tmp) (void)hipFree(plan->d_sort_tmp);
   if (plan->d_table) (void)hipFree(plan->d_table);
   if (plan->d_queue) (void)hipFree(plan->d_queue);
   if (plan->d_mtri) (void)hipFree(plan->d_mtri);
@@ -960,10 +1054,18 @@ extern "C" int sct_allpairs_moments(sct_allpairs_plan* plan, int part, int npart
 extern "C" int sct_allpairs_build(sct_allpairs_plan* plan, void* stream) {
   SCT_CHECK(plan != nullptr, "plan is NULL");
   if (plan->table_entries == 0) return SCT_OK;
+  hipStream_t s = sct::as_stream(stream);
   const int64_t blocks = sct::ceil_div(plan->table_entries, 256);
-  hipLaunchKernelGGL(allpairs_build_kernel, dim3((unsigned)blocks), dim3(256), 0,
-                     sct::as_stream(stream), plan->d_codes, plan->n, plan->npp,
-                     plan->table_entries, plan->d_table);
+  if (plan->scheme == SCT_ALLPAIRS_MOMENTS) {
+    size_t bytes = plan->sort_tmp_bytes;
+    SCT_HIP(hipcub::DeviceRadixSort::SortKeys(plan->d_sort_tmp, bytes, (const uint64_t*)plan->d_codes,
+                                              plan->d_sorted, (int)plan->n, 0, 32, s));
+    hipLaunchKernelGGL(allpairs_build_tri_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                       plan->d_sorted, plan->n, plan->table_entries, plan->d_table);
+  } else {
+    hipLaunchKernelGGL(allpairs_build_kernel, dim3((unsigned)blocks), dim3(256), 0, s, plan->d_codes,
+                       plan->n, plan->npp, plan->table_entries, plan->d_table);
+  }
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
@@ -984,7 +1086,7 @@ extern "C" int sct_allpairs_geometry(int64_t n, int code_bits, int* nbins, int64
   SCT_CHECK(n >= 0, "n must be >= 0");
   SCT_CHECK(code_bits >= 1 && code_bits <= 64, "code_bits %d outside [1, 64]", code_bits);
   const int npp = (code_bits + 3) / 4;
-  const int64_t cb = 32LL * ct_for(npp);
+  const int64_t cb = 32LL * ct_for(npp, auto_moments(npp, n));
   const int64_t nchunks = n > 0 ? sct::ceil_div(n, cb) : 0;
   int64_t it = 0;
   if (n >= 2) {
