@@ -461,34 +461,50 @@ __global__ void allpairs_build_kernel(const uint64_t* __restrict__ codes, int64_
 
 // Triple layout (MOMENTS): entry (h, lookup g, value c) = bit-sliced mismatch counts
 // (0..3) of the bases of lookup g of the 64 codes of group pair h against the query's
-// bases c (c's digits in the same MSB-first order as the code).  One thread per entry.
-__global__ void allpairs_build_tri_kernel(const uint64_t* __restrict__ codes, int64_t n,
-                                          int64_t entries, uint4* __restrict__ table) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= entries) return;
-  const int64_t h = idx / kTriRow;
-  const int e = (int)(idx - h * kTriRow);
-  int g = 0;
-  while (g + 1 < kTriNL && e >= tri_base(g + 1)) ++g;
-  const uint32_t c = (uint32_t)(e - tri_base(g));
-  const int shift = tri_shift(g), nb = tri_width(g) / 2;
-  uint32_t s[4] = {0u, 0u, 0u, 0u};
+// bases c.  A workgroup builds 4 group pairs: each wave transposes its 64 codes into
+// base bit-planes with 32 ballots (lane k = code k, so ballot = both groups' planes),
+// then every thread forms entries from the planes held in LDS: per base, mismatch =
+// (lo ^ c_lo) | (hi ^ c_hi), and the 2-3 mismatch planes are summed by a half/full adder.
+__global__ __launch_bounds__(256) void allpairs_build_tri_kernel(const uint64_t* __restrict__ codes,
+                                                                 int64_t n, int64_t ngp,
+                                                                 uint4* __restrict__ table) {
+  __shared__ uint64_t planes[4][32];  // [wave][2 * base + bit], group a = low 32 bits
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t h0 = (int64_t)blockIdx.x * 4;
+  {
+    const int64_t j = (h0 + wave) * 64 + lane;
+    const uint32_t code = j < n ? (uint32_t)codes[j] : 0u;
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-#pragma unroll 8
     for (int k = 0; k < 32; ++k) {
-      const int64_t j = h * 64 + half * 32 + k;
-      const uint32_t x = (j < n ? (uint32_t)(codes[j] >> shift) : 0u) ^ c;
-      uint32_t m = 0;
-      for (int t = 0; t < nb; ++t) m += ((x >> (2 * t)) & 3u) != 0u;
-      s[2 * half] |= (m & 1u) << k;
-      s[2 * half + 1] |= (m >> 1) << k;
+      const uint64_t b = __ballot((code >> k) & 1u);
+      if (lane == k) planes[wave][k] = b;
     }
   }
-  uint32_t r[4];
+  __syncthreads();
+  const int64_t nh = ngp - h0 < 4 ? ngp - h0 : 4;
+  for (int t = threadIdx.x; t < nh * kTriRow; t += 256) {
+    const int w = t / kTriRow, e = t - w * kTriRow;
+    const int g = e < 32 ? (e >> 4) : 2 + ((e - 32) >> 6);
+    const uint32_t c = (uint32_t)(e - tri_base(g));
+    const int base0 = tri_shift(g) / 2, nb = tri_width(g) / 2;
+    uint64_t mm[3];
+    for (int k = 0; k < 3; ++k) {
+      if (k < nb) {
+        const uint64_t lo = planes[w][2 * (base0 + k)], hi = planes[w][2 * (base0 + k) + 1];
+        const uint32_t d = (c >> (2 * k)) & 3u;
+        mm[k] = (lo ^ ((d & 1u) ? ~0ull : 0ull)) | (hi ^ ((d & 2u) ? ~0ull : 0ull));
+      } else {
+        mm[k] = 0ull;
+      }
+    }
+    const uint64_t s0 = mm[0] ^ mm[1] ^ mm[2];
+    const uint64_t s1 = (mm[0] & mm[1]) | (mm[2] & (mm[0] ^ mm[1]));
+    const uint32_t sv[4] = {(uint32_t)s0, (uint32_t)s1, (uint32_t)(s0 >> 32), (uint32_t)(s1 >> 32)};
+    uint32_t r[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) r[plane_slot(k, g)] = s[k];
-  table[idx] = make_uint4(r[0], r[1], r[2], r[3]);
+    for (int k = 0; k < 4; ++k) r[plane_slot(k, g)] = sv[k];
+    table[(h0 + w) * kTriRow + e] = make_uint4(r[0], r[1], r[2], r[3]);
+  }
 }
 
 __global__ void or_reduce_kernel(const uint64_t* __restrict__ codes, int64_t n,
@@ -1060,8 +1076,9 @@ extern "C" int sct_allpairs_build(sct_allpairs_plan* plan, void* stream) {
     size_t bytes = plan->sort_tmp_bytes;
     SCT_HIP(hipcub::DeviceRadixSort::SortKeys(plan->d_sort_tmp, bytes, (const uint64_t*)plan->d_codes,
                                               plan->d_sorted, (int)plan->n, 0, 32, s));
-    hipLaunchKernelGGL(allpairs_build_tri_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
-                       plan->d_sorted, plan->n, plan->table_entries, plan->d_table);
+    const int64_t ngp = plan->table_entries / kTriRow;
+    hipLaunchKernelGGL(allpairs_build_tri_kernel, dim3((unsigned)sct::ceil_div(ngp, 4)), dim3(256), 0,
+                       s, plan->d_sorted, plan->n, ngp, plan->d_table);
   } else {
     hipLaunchKernelGGL(allpairs_build_kernel, dim3((unsigned)blocks), dim3(256), 0, s, plan->d_codes,
                        plan->n, plan->npp, plan->table_entries, plan->d_table);

@@ -9,7 +9,7 @@ import pytest
 
 from conftest import fromhex
 from oracle import oracle as O
-from sctools_amd import synthetic
+from sctools_amd import _lib, synthetic
 
 
 def test_encode(golden):
@@ -137,3 +137,28 @@ def test_from_whitelist_semantics_oracle(golden):
         except KeyError as e:
             assert list(e.args) == rec["error"]["args"]
         assert random.getrandbits(32) == rec["after"]
+
+
+# ---------------------------------------------------------------- MOMENTS scheme identities
+def test_moments_identity_on_reference_histograms(golden, golden_10k):
+    """The agreement moments counted from position marginals (what the MOMENTS scheme's
+    moments pass computes) equal sum_d hist[d] C(16-d, k) on the reference's own golden
+    histograms, and the 17 MOMENTS counts of those histograms invert exactly through
+    the library's host solver (no GPU)."""
+    wl = golden["whitelist_1k"]
+    codes = np.array([int(c) for c in wl["codes"]], dtype=np.uint64)
+    assert O.moments_from_marginals(codes) == O.moments_from_hist(wl["hist"])
+    assert _lib.counts_to_hist(O.moment_counts_from_hist(wl["hist"]), _lib.SCHEME_MOMENTS,
+                               17).tolist() == wl["hist"]
+    c10 = synthetic.whitelist_codes(golden_10k["n"], golden_10k["L"], golden_10k["seed"])
+    h10 = golden_10k["hist"]
+    assert O.moments_from_marginals(c10) == O.moments_from_hist(h10)
+    assert _lib.counts_to_hist(O.moment_counts_from_hist(h10), _lib.SCHEME_MOMENTS,
+                               17).tolist() == list(h10)
+
+
+def test_moments_solver_rejects_inconsistent_counts():
+    c = O.moment_counts_from_hist([0, 3, 5, 0, 0, 7, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 1])
+    c[14] += 1  # M_1 off by one: no integral histogram
+    with pytest.raises(ValueError):
+        _lib.counts_to_hist(c, _lib.SCHEME_MOMENTS, 17)

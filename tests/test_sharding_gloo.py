@@ -37,6 +37,43 @@ def _shard_counts(codes, geo, b, e):
     return counts
 
 
+def _shard_moment_counts(codes, geo, b, e, rank):
+    """MOMENTS-scheme counts of one rank: the 13 products of its item range, plus (rank 0
+    here; the kernel splits them by position triple) the whole job's agreement moments."""
+    hist = np.zeros(65, dtype=np.int64)
+    pairs = np.zeros(1, dtype=np.int64)
+    O.c_oracle().oracle_hist_items(codes.ctypes.data, codes.size, geo["rows_per_item"],
+                                   geo["cols_per_item"], hist.ctypes.data, b, e, pairs.ctypes.data, 1)
+    c = O.moment_counts_from_hist(hist[:17]).astype(np.int64)
+    c[14:] = O.moments_from_marginals(codes) if rank == 0 else 0
+    return c
+
+
+def _worker_moments(rank, world, port, n, seed, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        codes = synthetic.whitelist_codes(n, 16, seed)
+        geo = _lib.allpairs_geometry(n, 32)  # AUTO = MOMENTS at 16 bases: 512-code chunks
+        assert geo["cols_per_item"] == 512
+        b, e = sharding.item_range(geo["items"], rank, world)
+        counts = torch.from_numpy(_shard_moment_counts(codes, geo, b, e, rank))
+        hist = sharding.combine_counts(counts, None, _lib.SCHEME_MOMENTS, 17)
+        np.save(out_path % rank, hist.astype(np.int64))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 1800)])
+def test_sharded_moments_histogram_matches_oracle(tmp_path, world, n):
+    port = _free_port()
+    out = str(tmp_path / "mhist_%d.npy")
+    mp.spawn(_worker_moments, args=(world, port, n, 23, out), nprocs=world, join=True)
+    ref = O.c_hist_rows(synthetic.whitelist_codes(n, 16, 23))[:17]
+    for r in range(world):
+        assert np.load(out % r).tolist() == ref.tolist()
+
+
 def _worker(rank, world, port, n, seed, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)

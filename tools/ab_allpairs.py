@@ -46,11 +46,14 @@ def main():
     s = torch.cuda.current_stream()
     times = {v: [] for v, _ in plans}
     mtimes = {v: [] for v, _ in plans}
+    btimes = {v: [] for v, _ in plans}
     ref = None
     for _ in range(a.rounds):
         for v, p in plans:
             c = torch.zeros(p.ncounts, dtype=torch.int64, device="cuda")
-            em, e0, e1 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            eb, em, e0, e1 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+            eb.record(s)
+            p.build(s.cuda_stream)
             em.record(s)
             p.moments(c.data_ptr(), stream=s.cuda_stream)
             e0.record(s)
@@ -59,6 +62,7 @@ def main():
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1))
             mtimes[v].append(em.elapsed_time(e0))
+            btimes[v].append(eb.elapsed_time(em))
             if int(dict(x.split("=") for x in v.split(",")).get("v", "2")) >= 10:
                 continue  # ablation builds compute wrong counts by design
             h = p.counts_to_hist(c.cpu().numpy().view(np.uint64))
@@ -67,7 +71,8 @@ def main():
             assert np.array_equal(ref, h), v
     pairs = plans[0][1].pairs
     out = {v: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
-               "moments_ms": float(np.median(mtimes[v])), "scheme": dict(plans)[v].scheme,
+               "moments_ms": float(np.median(mtimes[v])), "build_ms": float(np.median(btimes[v])),
+               "scheme": dict(plans)[v].scheme,
                "pairs_per_s": pairs / (np.median(t) * 1e-3)} for v, t in times.items()}
     print(json.dumps(out, indent=1))
 
