@@ -983,6 +983,8 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
     cus = 256;
   // defaults measured on MI355X: MOMENTS unroll 2, SUBSETS@16 bases full unroll
   p->variant = p->scheme == SCT_ALLPAIRS_MOMENTS ? 2 : (p->npp == 8 ? 3 : 2);
+  // MOMENTS: 32 items per pull halves the chunk re-staging (L2 -> LDS) at no cost in time
+  if (p->scheme == SCT_ALLPAIRS_MOMENTS) p->grab = 32;
   if (const char* v = getenv("SCT_ALLPAIRS_VARIANT")) {
     const int vv = atoi(v);
     if ((vv >= 1 && vv <= 3) || (vv == 4 && p->scheme == SCT_ALLPAIRS_MOMENTS) || (vv >= 11 && vv <= 13))

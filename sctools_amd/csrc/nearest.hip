@@ -11,13 +11,17 @@
 //
 // Algorithm (exact pigeonhole index): split the G base positions into P = max_d + 1
 // contiguous blocks; any w with dist(q, w) <= max_d agrees with q exactly on at least
-// one block.  For each block the whitelist is bucketed by that block's bits (CSR:
-// offsets[key] .. offsets[key+1] into (code, index) arrays, built by a histogram /
-// exclusive-scan / scatter on the GPU); a query probes its P buckets and verifies every
-// candidate with the full distance, so false candidates (and 24-bit key truncation for
-// very wide blocks) never change the result.  A code found through several blocks has
-// one index, so it is never counted as a tie with itself.
+// one block.  For each block the whitelist is bucketed by a multiplicative hash of that
+// block's bits into ~nw/2 buckets (CSR: offsets[b] .. offsets[b+1] into 16-byte
+// {code, index} entries, built by a histogram / exclusive-scan / scatter on the GPU).
+// A query issues all P bucket-offset loads before it reads any entry (one dependent
+// random access per probe, the offset tables are a few MB and L2/MALL-resident), then
+// verifies every entry of its P buckets with the full distance, so hash collisions never
+// change the result.  A code found through several blocks has one index, so it is never
+// counted as a tie with itself.
 #include <hipcub/hipcub.hpp>
+
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -27,16 +31,18 @@ namespace {
 
 constexpr int WG = 256;
 constexpr int MAX_PARTS = 8;
-constexpr int KEY_BITS_MAX = 24;
 
 struct Part {
-  int lo_bit;    // first bit of the block in the code
-  int nbits;     // bits of the block
-  int key_bits;  // min(nbits, 24): keys are the block's low key_bits bits
+  uint64_t mask;  // the block's bits, in place
+  uint64_t mul;   // multiplicative hash (0 when there is a single bucket)
+  int lo_bit;     // first bit of the block in the code
+  int nbits;      // bits of the block (<= 64)
+  int shift;      // 64 - log2(buckets), in [1, 63]
 };
 
-__device__ __forceinline__ uint32_t part_key(uint64_t code, Part p) {
-  return (uint32_t)((code >> p.lo_bit) & ((1ull << p.key_bits) - 1ull));
+// branch-free (uniform branches would split the probes' loads into separate waits)
+__device__ __forceinline__ uint32_t part_bucket(uint64_t code, Part p) {
+  return (uint32_t)((((code & p.mask) >> p.lo_bit) * p.mul) >> p.shift);
 }
 
 __device__ __forceinline__ int dist2(uint64_t a, uint64_t b) {
@@ -55,51 +61,103 @@ struct Parts {
 __global__ void key_hist_kernel(const uint64_t* __restrict__ wl, int64_t nw, Part part,
                                 uint32_t* __restrict__ counts) {
   for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j < nw; j += (int64_t)gridDim.x * WG)
-    atomicAdd(&counts[part_key(wl[j], part)], 1u);
+    atomicAdd(&counts[part_bucket(wl[j], part)], 1u);
 }
 
+// entries: codes[pos] (8 B, what a probe scans) and index[pos] (read only for a new best);
+// index bit 31 = the code occurs more than once in the whitelist (mark_dups_kernel)
 __global__ void key_scatter_kernel(const uint64_t* __restrict__ wl, int64_t nw, Part part,
-                                   uint32_t* __restrict__ cursor, uint64_t* __restrict__ b_codes,
-                                   int32_t* __restrict__ b_index) {
+                                   uint32_t* __restrict__ cursor, uint64_t* __restrict__ codes,
+                                   uint32_t* __restrict__ index) {
   for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j < nw; j += (int64_t)gridDim.x * WG) {
     const uint64_t w = wl[j];
-    const uint32_t pos = atomicAdd(&cursor[part_key(w, part)], 1u);
-    b_codes[pos] = w;
-    b_index[pos] = (int32_t)j;
+    const uint32_t pos = atomicAdd(&cursor[part_bucket(w, part)], 1u);
+    codes[pos] = w;
+    index[pos] = (uint32_t)j;
   }
 }
 
-template <int KIND>
-__global__ __launch_bounds__(WG) void nearest_query_kernel(
-    const uint64_t* __restrict__ queries, int64_t nq, int nparts, Parts parts,
-    const uint32_t* const* __restrict__ offsets, const uint64_t* const* __restrict__ b_codes,
-    const int32_t* const* __restrict__ b_index, int max_d, int32_t* __restrict__ out_index,
-    uint8_t* __restrict__ out_dist) {
-  for (int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x; i < nq; i += (int64_t)gridDim.x * WG) {
-    const uint64_t q = queries[i];
-    int best_d = max_d + 1, best_j = -1;
-    bool tie = false;
-    for (int p = 0; p < nparts; ++p) {
-      const uint32_t key = part_key(q, parts.p[p]);
-      const uint32_t* off = offsets[p];
-      const uint32_t lo = off[key], hi = off[key + 1];
-      const uint64_t* bc = b_codes[p];
-      const int32_t* bi = b_index[p];
-      for (uint32_t t = lo; t < hi; ++t) {
-        const int d = KIND == 2 ? dist2(q, bc[t]) : dist3(q, bc[t]);
+// bucket b's entries are [range[b].x, range[b].y): one 8-byte load per probe
+__global__ void ranges_kernel(const uint32_t* __restrict__ offsets, int64_t nbuckets,
+                              uint2* __restrict__ range) {
+  const int64_t b = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (b < nbuckets) range[b] = make_uint2(offsets[b], offsets[b + 1]);
+}
+
+// one thread per bucket of part 0 (identical codes share every bucket): flag duplicates
+__global__ void mark_dups_kernel(const uint2* __restrict__ range, int64_t nbuckets,
+                                 const uint64_t* __restrict__ codes, uint32_t* __restrict__ index) {
+  const int64_t b = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (b >= nbuckets) return;
+  const uint2 r = range[b];
+  for (uint32_t t = r.x; t < r.y; ++t)
+    for (uint32_t u = r.x; u < r.y; ++u)
+      if (u != t && codes[u] == codes[t]) {
+        index[t] |= 0x80000000u;
+        break;
+      }
+}
+
+// Per-probe tables, passed by value (kernarg -> SGPRs) so every load is a global load.
+struct Tables {
+  Part part[MAX_PARTS];
+  const uint2* range[MAX_PARTS];
+  const uint64_t* code[MAX_PARTS];
+  const uint32_t* index[MAX_PARTS];
+};
+
+template <int KIND, int NP>
+__global__ __launch_bounds__(WG) void nearest_query_kernel(const uint64_t* __restrict__ queries,
+                                                           int64_t nq, Tables tb, int max_d,
+                                                           int32_t* __restrict__ out_index,
+                                                           uint8_t* __restrict__ out_dist) {
+  const int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (i >= nq) return;
+  const uint64_t q = queries[i];
+  uint2 r[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) r[p] = tb.range[p][part_bucket(q, tb.part[p])];  // all in flight
+  int best_d = max_d + 1, best_j = -1;
+  bool tie = false, exact_unique = false;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    // an exact hit on a code that occurs once cannot tie (every other code is >= 1 away):
+    // the remaining probes' entry reads are skipped
+    if (exact_unique) break;
+    for (uint32_t t = r[p].x; t < r[p].y; ++t) {
+      const uint64_t w = tb.code[p][t];
+      const int d = KIND == 2 ? dist2(q, w) : dist3(q, w);
+      if (d <= best_d && d <= max_d) {  // rare: only candidates within max_d read their index
+        const uint32_t jf = tb.index[p][t];
+        const int j = (int)(jf & 0x7FFFFFFFu);
         if (d < best_d) {
           best_d = d;
-          best_j = bi[t];
+          best_j = j;
           tie = false;
-        } else if (d == best_d) {
-          const int j = bi[t];
-          if (j != best_j) tie = true;
+          exact_unique = d == 0 && !(jf >> 31);
+        } else if (j != best_j) {
+          tie = true;
         }
       }
     }
-    out_index[i] = best_j < 0 ? -1 : (tie ? -2 : best_j);
-    out_dist[i] = best_j < 0 ? (uint8_t)255 : (uint8_t)best_d;
   }
+  out_index[i] = best_j < 0 ? -1 : (tie ? -2 : best_j);
+  out_dist[i] = best_j < 0 ? (uint8_t)255 : (uint8_t)best_d;
+}
+
+template <int KIND>
+void launch_query(int np, unsigned blocks, hipStream_t s, const uint64_t* q, int64_t nq,
+                  const Tables& tb, int max_d, int32_t* idx, uint8_t* dist) {
+#define SCT_NQ(NP)                                                                                 \
+  case NP:                                                                                         \
+    hipLaunchKernelGGL((nearest_query_kernel<KIND, NP>), dim3(blocks), dim3(WG), 0, s, q, nq, tb, \
+                       max_d, idx, dist);                                                          \
+    break;
+  switch (np) {
+    SCT_NQ(1) SCT_NQ(2) SCT_NQ(3) SCT_NQ(4) SCT_NQ(5) SCT_NQ(6) SCT_NQ(7) SCT_NQ(8)
+    default: break;
+  }
+#undef SCT_NQ
 }
 
 unsigned grid_for(int64_t n, int64_t cap = 16384) {
@@ -113,25 +171,18 @@ struct sct_nearest_plan {
   int kind = 2, max_d = 0, nparts = 0, code_bits = 0;
   int64_t nw = 0;
   Parts parts{};
-  uint32_t* d_offsets[MAX_PARTS] = {};
-  uint64_t* d_bcodes[MAX_PARTS] = {};
-  int32_t* d_bindex[MAX_PARTS] = {};
-  // device copies of the pointer tables above
-  const uint32_t** d_off_tab = nullptr;
-  const uint64_t** d_code_tab = nullptr;
-  const int32_t** d_idx_tab = nullptr;
+  uint2* d_range[MAX_PARTS] = {};
+  uint64_t* d_code[MAX_PARTS] = {};
+  uint32_t* d_index[MAX_PARTS] = {};
 };
 
 extern "C" int sct_nearest_plan_destroy(sct_nearest_plan* p) {
   if (!p) return SCT_OK;
   for (int k = 0; k < MAX_PARTS; ++k) {
-    if (p->d_offsets[k]) (void)hipFree(p->d_offsets[k]);
-    if (p->d_bcodes[k]) (void)hipFree(p->d_bcodes[k]);
-    if (p->d_bindex[k]) (void)hipFree(p->d_bindex[k]);
+    if (p->d_range[k]) (void)hipFree(p->d_range[k]);
+    if (p->d_code[k]) (void)hipFree(p->d_code[k]);
+    if (p->d_index[k]) (void)hipFree(p->d_index[k]);
   }
-  if (p->d_off_tab) (void)hipFree(p->d_off_tab);
-  if (p->d_code_tab) (void)hipFree(p->d_code_tab);
-  if (p->d_idx_tab) (void)hipFree(p->d_idx_tab);
   delete p;
   return SCT_OK;
 }
@@ -159,54 +210,56 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
   p->nw = nw;
   p->code_bits = code_bits;
   p->nparts = max_d + 1;
+  // ~PER entries per bucket (8-byte codes: 8 per 64-byte line); fewer, fuller buckets keep
+  // the range table L2-resident (SCT_NEAREST_PER overrides, for A/B)
+  int per = 2;
+  if (const char* v = getenv("SCT_NEAREST_PER")) per = std::max(1, atoi(v));
+  int lg = 0;
+  while (lg < 28 && (1LL << lg) * per < nw) ++lg;
+  const int64_t nbuckets = 1LL << lg;
   for (int k = 0; k < p->nparts; ++k) {
     const int pos_lo = G * k / p->nparts, pos_hi = G * (k + 1) / p->nparts;
     Part& pt = p->parts.p[k];
     pt.lo_bit = pos_lo * kind;
     pt.nbits = std::min(64, pos_hi * kind) - pt.lo_bit;
-    pt.key_bits = std::min(pt.nbits, KEY_BITS_MAX);
+    pt.mask = (pt.nbits >= 64 ? ~0ull : ((1ull << pt.nbits) - 1ull)) << pt.lo_bit;
+    pt.mul = lg == 0 ? 0ull : 0x9E3779B97F4A7C15ull;
+    pt.shift = lg == 0 ? 63 : 64 - lg;
   }
   size_t scan_bytes = 0;
-  for (int k = 0; k < p->nparts; ++k) {
-    size_t b = 0;
-    const int nkeys = 1 << p->parts.p[k].key_bits;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           nkeys + 1, s);
-    scan_bytes = std::max(scan_bytes, b);
-  }
-  sct::DevBuf scan_tmp, cursor;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                         (int)(nbuckets + 1), s);
+  sct::DevBuf scan_tmp, cursor, offsets;
   hipError_t e = scan_tmp.alloc(scan_bytes);
-  if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "scan temp: %s", hipGetErrorString(e)));
-  e = cursor.alloc(((size_t)1 << KEY_BITS_MAX) * 4 + 8);
-  if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "cursor: %s", hipGetErrorString(e)));
+  if (e == hipSuccess) e = cursor.alloc((size_t)(nbuckets + 1) * 4);
+  if (e == hipSuccess) e = offsets.alloc((size_t)(nbuckets + 1) * 4);
+  if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "scratch: %s", hipGetErrorString(e)));
   for (int k = 0; k < p->nparts; ++k) {
     const Part pt = p->parts.p[k];
-    const int64_t nkeys = 1LL << pt.key_bits;
-    e = hipMalloc(&p->d_offsets[k], (size_t)(nkeys + 1) * 4);
-    if (e == hipSuccess) e = hipMalloc(&p->d_bcodes[k], (size_t)std::max<int64_t>(nw, 1) * 8);
-    if (e == hipSuccess) e = hipMalloc(&p->d_bindex[k], (size_t)std::max<int64_t>(nw, 1) * 4);
+    e = hipMalloc(&p->d_range[k], (size_t)nbuckets * 8);
+    if (e == hipSuccess) e = hipMalloc(&p->d_code[k], (size_t)std::max<int64_t>(nw, 1) * 8);
+    if (e == hipSuccess) e = hipMalloc(&p->d_index[k], (size_t)std::max<int64_t>(nw, 1) * 4);
     if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "bucket arrays: %s", hipGetErrorString(e)));
     uint32_t* counts = (uint32_t*)cursor.p;
-    SCT_HIP(hipMemsetAsync(counts, 0, (size_t)(nkeys + 1) * 4, s));
+    uint32_t* off = (uint32_t*)offsets.p;
+    SCT_HIP(hipMemsetAsync(counts, 0, (size_t)(nbuckets + 1) * 4, s));
     if (nw)
       hipLaunchKernelGGL(key_hist_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_whitelist, nw,
                          pt, counts);
     size_t b = scan_bytes;
-    e = hipcub::DeviceScan::ExclusiveSum(scan_tmp.p, b, counts, p->d_offsets[k], nkeys + 1, s);
+    e = hipcub::DeviceScan::ExclusiveSum(scan_tmp.p, b, counts, off, (int)(nbuckets + 1), s);
     if (e != hipSuccess) return fail_with(sct::fail(SCT_E_HIP, "scan: %s", hipGetErrorString(e)));
-    SCT_HIP(hipMemcpyAsync(counts, p->d_offsets[k], (size_t)nkeys * 4, hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(ranges_kernel, dim3((unsigned)sct::ceil_div(nbuckets, WG)), dim3(WG), 0, s, off,
+                       nbuckets, p->d_range[k]);
+    SCT_HIP(hipMemcpyAsync(counts, off, (size_t)nbuckets * 4, hipMemcpyDeviceToDevice, s));
     if (nw)
       hipLaunchKernelGGL(key_scatter_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_whitelist,
-                         nw, pt, counts, p->d_bcodes[k], p->d_bindex[k]);
+                         nw, pt, counts, p->d_code[k], p->d_index[k]);
+    if (k == 0 && nw)
+      hipLaunchKernelGGL(mark_dups_kernel, dim3((unsigned)sct::ceil_div(nbuckets, WG)), dim3(WG), 0, s,
+                         p->d_range[0], nbuckets, p->d_code[0], p->d_index[0]);
     SCT_LAUNCH_CHECK();
   }
-  e = hipMalloc(&p->d_off_tab, sizeof(void*) * MAX_PARTS);
-  if (e == hipSuccess) e = hipMalloc(&p->d_code_tab, sizeof(void*) * MAX_PARTS);
-  if (e == hipSuccess) e = hipMalloc(&p->d_idx_tab, sizeof(void*) * MAX_PARTS);
-  if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "tables: %s", hipGetErrorString(e)));
-  SCT_HIP(hipMemcpyAsync(p->d_off_tab, p->d_offsets, sizeof(void*) * MAX_PARTS, hipMemcpyHostToDevice, s));
-  SCT_HIP(hipMemcpyAsync(p->d_code_tab, p->d_bcodes, sizeof(void*) * MAX_PARTS, hipMemcpyHostToDevice, s));
-  SCT_HIP(hipMemcpyAsync(p->d_idx_tab, p->d_bindex, sizeof(void*) * MAX_PARTS, hipMemcpyHostToDevice, s));
   SCT_HIP(hipStreamSynchronize(s));  // the scratch buffers die with this call
   *out = p;
   return SCT_OK;
@@ -219,14 +272,19 @@ extern "C" int sct_nearest_query(sct_nearest_plan* p, const uint64_t* d_queries,
   if (nq == 0) return SCT_OK;
   SCT_CHECK(d_queries && d_index && d_dist, "NULL pointer");
   hipStream_t s = sct::as_stream(stream);
+  const unsigned blocks = (unsigned)sct::ceil_div(nq, WG);  // one query per thread
+  SCT_CHECK(sct::ceil_div(nq, WG) < (1LL << 31), "too many queries for one launch");
+  Tables tb{};
+  for (int k = 0; k < p->nparts; ++k) {
+    tb.part[k] = p->parts.p[k];
+    tb.range[k] = p->d_range[k];
+    tb.code[k] = p->d_code[k];
+    tb.index[k] = p->d_index[k];
+  }
   if (p->kind == 2)
-    hipLaunchKernelGGL(nearest_query_kernel<2>, dim3(grid_for(nq)), dim3(WG), 0, s, d_queries, nq,
-                       p->nparts, p->parts, p->d_off_tab, p->d_code_tab, p->d_idx_tab, p->max_d,
-                       d_index, d_dist);
+    launch_query<2>(p->nparts, blocks, s, d_queries, nq, tb, p->max_d, d_index, d_dist);
   else
-    hipLaunchKernelGGL(nearest_query_kernel<3>, dim3(grid_for(nq)), dim3(WG), 0, s, d_queries, nq,
-                       p->nparts, p->parts, p->d_off_tab, p->d_code_tab, p->d_idx_tab, p->max_d,
-                       d_index, d_dist);
+    launch_query<3>(p->nparts, blocks, s, d_queries, nq, tb, p->max_d, d_index, d_dist);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
