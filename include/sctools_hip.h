@@ -210,6 +210,44 @@ int sct_nearest_query(sct_nearest_plan* plan, const uint64_t* d_queries, int64_t
 int sct_nearest_host(int kind, const uint64_t* whitelist, int64_t nw, const uint64_t* queries,
                      int64_t nq, int code_bits, int max_d, int32_t* index, uint8_t* dist);
 
+/* ---------------------------------------------------------------- FASTQ barcode extraction
+ * Replaces the per-record path reader.Reader.__iter__ (src/sctools/reader.py:56-85) ->
+ * fastq.Reader.record_grouper (src/sctools/fastq.py:143-150) -> Record name check
+ * (fastq.py:31-38) -> EmbeddedBarcodeGenerator / extract_barcode (fastq.py:181-200):
+ * record.sequence[start:end] and record.quality[start:end] of every record.
+ * The input is the files' bytes concatenated (file_ends = cumulative end offsets, the last
+ * == nbytes; a record may span files, an incomplete trailing record is dropped).  Lines
+ * keep their newline, so slices of short reads include '\n' exactly as in Python.
+ * text_mode = 0 is open(..., 'rb'): lines end at '\n'; 1 is 'r': '\n', "\r\n" and a lone
+ * '\r' each end a line and read back as '\n' (ASCII input only, else SCT_E_RANGE).
+ * first_bad_name = the first record whose name line does not start with '@' (the
+ * reference raises ValueError('fastq name must start with @') there), or -1.
+ */
+typedef struct sct_fastq_index sct_fastq_index;
+/* Pass 1: count every 4 KiB tile's lines (-> nrecords = lines / 4); keeps only per-tile
+ * line offsets.  The buffer must stay alive and unchanged until the index is destroyed. */
+int sct_fastq_index_create(const uint8_t* d_buf, int64_t nbytes, const int64_t* file_ends, int nfiles,
+                           int text_mode, void* stream, sct_fastq_index** index);
+int sct_fastq_index_destroy(sct_fastq_index* index);
+/* first_bad_name: from the last sct_fastq_extract_spans (-2 before any). */
+int sct_fastq_index_info(const sct_fastq_index* index, int64_t* nrecords, int64_t* nlines,
+                         int64_t* first_bad_name);
+/* Pass 2, synchronous: every record's sequence-line and quality-line slices for all spans
+ * (nspans <= 8 host (start, end) pairs, end <= 4096) and the '@' check of every name line.
+ * Span k's rows start at d_seq / d_qual + nrecords * sum_{i<k} width_i (zero padded rows of
+ * width_k), lengths at d_seq_len / d_qual_len + k * nrecords; every output is nullable. */
+int sct_fastq_extract_spans(sct_fastq_index* index, const uint8_t* d_buf, const int32_t* spans,
+                            int nspans, uint8_t* d_seq, uint8_t* d_qual, int32_t* d_seq_len,
+                            int32_t* d_qual_len, int64_t* first_bad_name, void* stream);
+/* Host convenience: spans = nspans (start, end) pairs.  Call with max_records < the record
+ * count to learn nrecords (outputs untouched); then with room for nrecords:
+ * seq_out/qual_out (nullable) = span k's rows at offset sum_{i<k} nrecords*width_i,
+ * seq_len/qual_len (nullable) = nspans x nrecords lengths. */
+int sct_fastq_extract_host(const uint8_t* buf, int64_t nbytes, const int64_t* file_ends, int nfiles,
+                           int text_mode, const int32_t* spans, int nspans, uint8_t* seq_out,
+                           uint8_t* qual_out, int32_t* seq_len, int32_t* qual_len,
+                           int64_t max_records, int64_t* nrecords, int64_t* first_bad_name);
+
 /* ---------------------------------------------------------------- summary
  * Replaces barcode.py:44-46 (np.percentile(distances,[0,25,50,75,100]) with numpy's
  * default 'linear' method, then np.mean) computed from the histogram alone,

@@ -68,6 +68,12 @@ SIGNATURES = {
     "sct_nearest_query": [_vp, _vp, _i64, _vp, _vp, _vp],
     "sct_nearest_host": [_i32, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _vp],
     "sct_base_frequency": [_vp, _i64, _i32, _vp, _vp],
+    "sct_fastq_index_create": [_vp, _i64, _vp, _i32, _i32, _vp, ctypes.POINTER(_vp)],
+    "sct_fastq_index_destroy": [_vp],
+    "sct_fastq_index_info": [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)],
+    "sct_fastq_extract_spans": [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, ctypes.POINTER(_i64), _vp],
+    "sct_fastq_extract_host": [_vp, _i64, _vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _i64,
+                               ctypes.POINTER(_i64), ctypes.POINTER(_i64)],
     "sct_base_frequency_host": [_vp, _i64, _i32, _vp],
 }
 _RESTYPES = {"sct_last_error": ctypes.c_char_p}
@@ -272,6 +278,70 @@ def base_frequency(codes, L):
     out = np.zeros((L, 4), dtype=np.uint64)
     check(lib().sct_base_frequency_host(_ptr(codes), codes.size, L, _ptr(out)))
     return out
+
+
+def fastq_extract(buf, file_ends, spans, text_mode, qualities=True):
+    """Device FASTQ slicing.  buf: bytes of the concatenated files; file_ends: cumulative
+    ends; spans: [(start, end)].  Returns (nrecords, first_bad_name, [(seq (n, w) uint8,
+    seq_len int32[n], qual (n, w) uint8 | None, qual_len | None) per span])."""
+    data = np.frombuffer(buf, dtype=np.uint8) if len(buf) else np.zeros(1, np.uint8)
+    ends = np.ascontiguousarray(file_ends, dtype=np.int64)
+    sp = np.ascontiguousarray(np.array(spans, dtype=np.int32).reshape(-1, 2))
+    nrec, bad = _i64(0), _i64(0)
+    f = lib().sct_fastq_extract_host
+    check(f(_ptr(data), len(buf), _ptr(ends), ends.size, int(text_mode), _ptr(sp), sp.shape[0],
+            None, None, None, None, -1, ctypes.byref(nrec), ctypes.byref(bad)))
+    n = nrec.value
+    widths = [int(e - s) for s, e in sp]
+    seq = np.zeros(max(1, n * sum(widths)), dtype=np.uint8)
+    qual = np.zeros_like(seq) if qualities else None
+    slen = np.zeros(max(1, n * len(widths)), dtype=np.int32)
+    qlen = np.zeros_like(slen) if qualities else None
+    check(f(_ptr(data), len(buf), _ptr(ends), ends.size, int(text_mode), _ptr(sp), sp.shape[0],
+            _ptr(seq), _ptr(qual), _ptr(slen), _ptr(qlen), n, ctypes.byref(nrec), ctypes.byref(bad)))
+    out, off = [], 0
+    for k, w in enumerate(widths):
+        rows = seq[off:off + n * w].reshape(n, w)
+        q = qual[off:off + n * w].reshape(n, w) if qualities else None
+        out.append((rows, slen[k * n:(k + 1) * n], q, qlen[k * n:(k + 1) * n] if qualities else None))
+        off += n * w
+    return n, bad.value, out
+
+
+class FastqIndex:
+    """Device FASTQ line/record index over a device buffer (sct_fastq_index)."""
+
+    def __init__(self, d_buf_ptr, nbytes, file_ends, text_mode=False, stream=0):
+        self._lib = lib()
+        self._h = _vp()
+        ends = np.ascontiguousarray(file_ends, dtype=np.int64)
+        check(self._lib.sct_fastq_index_create(_vp(d_buf_ptr), nbytes, _ptr(ends), ends.size,
+                                               int(text_mode), _vp(stream), ctypes.byref(self._h)))
+        nr, nl, bad = _i64(0), _i64(0), _i64(0)
+        check(self._lib.sct_fastq_index_info(self._h, ctypes.byref(nr), ctypes.byref(nl), ctypes.byref(bad)))
+        self.nrecords, self.nlines, self.first_bad_name = nr.value, nl.value, bad.value
+
+    def extract_spans(self, d_buf_ptr, spans, d_seq_ptr, d_qual_ptr=0, d_seq_len_ptr=0,
+                      d_qual_len_ptr=0, stream=0):
+        """All spans of every record in one pass; returns the first bad-name record or -1."""
+        sp = np.ascontiguousarray(np.array(spans, dtype=np.int32).reshape(-1, 2))
+        bad = _i64(0)
+        check(self._lib.sct_fastq_extract_spans(self._h, _vp(d_buf_ptr), _ptr(sp), sp.shape[0],
+                                                _vp(d_seq_ptr), _vp(d_qual_ptr), _vp(d_seq_len_ptr),
+                                                _vp(d_qual_len_ptr), ctypes.byref(bad), _vp(stream)))
+        self.first_bad_name = bad.value
+        return bad.value
+
+    def close(self):
+        if self._h:
+            self._lib.sct_fastq_index_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def allpairs_geometry(n, code_bits):

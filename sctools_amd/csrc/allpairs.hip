@@ -403,7 +403,11 @@ __global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __re
         __syncthreads();  // previous chunk no longer read
         const uint4* src = table + c * Gm::TILE;
 #pragma unroll
-        for (int k = tid; k < Gm::TILE; k += RB) tile[k] = src[k];
+        for (int k = 0; k < Gm::TILE / RB; ++k) tile[k * RB + tid] = src[k * RB + tid];
+        if constexpr (Gm::TILE % RB != 0) {
+          const int k = Gm::TILE / RB * RB + tid;
+          if (k < Gm::TILE) tile[k] = src[k];
+        }
         __syncthreads();
         loaded = c;
       }

@@ -1,0 +1,507 @@
+// FASTQ embedded-barcode extraction on gfx950.
+//
+// Replaces the per-record Python path that feeds barcodes into the hot path:
+//   reader.Reader.__iter__            (src/sctools/reader.py:56-85)   lines of each file, in order
+//   fastq.Reader.record_grouper       (src/sctools/fastq.py:143-150)  4 consecutive lines = 1 record
+//   fastq.Record.name setter          (src/sctools/fastq.py:31-38)    name must start with '@'
+//   EmbeddedBarcodeGenerator.__iter__ / extract_barcode (src/sctools/fastq.py:181-200):
+//       record.sequence[start:end], record.quality[start:end]
+// with the TenXV2 spans of platform.py:36-38 as the typical use.
+//
+// Semantics kept exactly: a line includes its newline, so a slice past the end of a short
+// read includes the '\n'; a file's last line may lack one; files are concatenated line
+// streams (a record may span two files) and an incomplete trailing record is dropped.
+// Mode 'rb' splits lines at '\n' only; mode 'r' (text) at '\n', "\r\n" and a lone '\r',
+// each read back as '\n' (Python's universal newlines), and only ASCII input is accepted.
+//
+// Device layout: the files' bytes concatenated in one buffer, read in 4 KiB tiles (16 bytes
+// per thread, SWAR byte compares).  Two passes: count_kernel counts each tile's line
+// terminators and an exclusive scan gives every tile its first line number (the index);
+// extract_kernel finds the terminators again, numbers them, and for each one that starts a
+// record's name / sequence / quality line checks the '@' or copies that line's slices.
+// No per-line array is ever stored.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <vector>
+
+#include "sct_common.h"
+
+namespace {
+
+constexpr int WG = 256;
+constexpr int TILE = 4096;  // bytes per counting thread-block tile (16 per thread)
+
+struct Files {
+  const int64_t* ends;  // cumulative end offsets, nfiles entries
+  int nfiles;
+};
+
+// file f ends at e (> its start) without a terminator on its last byte -> virtual terminator
+__device__ __forceinline__ bool virtual_end(const uint8_t* __restrict__ buf, int64_t n, Files fs, int f,
+                                            int text) {
+  const int64_t e = fs.ends[f], s = f ? fs.ends[f - 1] : 0;
+  if (e <= s) return false;
+  // a "\r\n" split across the file boundary is two files' bytes: only bytes of this file count
+  const uint8_t c = buf[e - 1];
+  return !(c == '\n' || (text && c == '\r'));
+}
+
+// Each thread owns 16 contiguous bytes (one 16-byte load); a tile = 256 threads = 4 KiB.
+// Terminators of the thread's bytes as a 16-bit mask (bit j = byte p0 + j), found with
+// SWAR byte compares on the four 32-bit words; text mode also needs the byte before and
+// after the span (a '\r' before '\n' is part of "\r\n", a lone '\r' is a terminator).
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t pat) {
+  // bit 7 of each byte set iff that byte equals the pattern byte (exact, no carries)
+  const uint32_t x = w ^ pat;
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}
+__device__ __forceinline__ uint32_t byte_mask4(uint32_t hi_bits) {  // bit 7 of byte k -> bit k
+  return ((hi_bits >> 7) & 1u) | ((hi_bits >> 14) & 2u) | ((hi_bits >> 21) & 4u) | ((hi_bits >> 28) & 8u);
+}
+
+__device__ __forceinline__ uint32_t load_mask(const uint8_t* __restrict__ buf, int64_t n, int64_t p0,
+                                              int text, uint32_t* kinds_crlf, uint32_t* nonascii) {
+  uint32_t w[4];
+  if (p0 + 16 <= n) {
+    const uint4 v = *reinterpret_cast<const uint4*>(buf + p0);
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t x = 0;
+      for (int b = 0; b < 4; ++b)
+        if (p0 + 4 * k + b < n) x |= (uint32_t)buf[p0 + 4 * k + b] << (8 * b);
+      w[k] = x;
+    }
+  }
+  const uint32_t valid = p0 + 16 <= n ? 0xFFFFu : (uint32_t)((1u << (n - p0)) - 1u);
+  uint32_t lf = 0, cr = 0, na = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    lf |= byte_mask4(eq_bytes(w[k], 0x0A0A0A0Au)) << (4 * k);
+    if (text) cr |= byte_mask4(eq_bytes(w[k], 0x0D0D0D0Du)) << (4 * k);
+    na |= w[k] & 0x80808080u;
+  }
+  lf &= valid;
+  cr &= valid;
+  uint32_t m = lf, crlf = 0;
+  if (text) {
+    const uint32_t cr_prev = (p0 > 0 && buf[p0 - 1] == '\r') ? 1u : 0u;  // byte before the span
+    const uint32_t lf_next = (p0 + 16 < n && buf[p0 + 16] == '\n') ? 1u : 0u;
+    crlf = lf & ((cr << 1) | cr_prev);                    // '\n' preceded by '\r'
+    const uint32_t lone_cr = cr & ~((lf >> 1) | (lf_next << 15));  // '\r' not followed by '\n'
+    m = lf | lone_cr;
+  }
+  *kinds_crlf = crlf;
+  *nonascii = na;
+  return m;
+}
+
+// file f's end e lies in (p0, p0 + 16] and its last byte is not a terminator -> virtual
+// terminator at e; returns the in-span offset e - p0 - 1 of its last byte, or -1
+__device__ __forceinline__ int virtual_in(const uint8_t* __restrict__ buf, int64_t n, Files fs,
+                                          int64_t p0, int text) {
+  int lo = 0, hi = fs.nfiles;  // first file with end > p0
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (fs.ends[mid] <= p0) lo = mid + 1; else hi = mid;
+  }
+  for (int f = lo; f < fs.nfiles && fs.ends[f] <= p0 + 16; ++f)
+    if (virtual_end(buf, n, fs, f, text)) return (int)(fs.ends[f] - p0 - 1);
+  return -1;
+}
+
+// Per tile: its terminator count, and its first terminator (in-tile offset << 2 | 1 if
+// virtual | 2 if "\r\n"; ~0 if none) -- the end of the previous tile's last line.
+__global__ __launch_bounds__(WG) void count_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs,
+                                                   int text, unsigned long long* __restrict__ counts,
+                                                   uint32_t* __restrict__ first,
+                                                   unsigned* __restrict__ flags) {
+  const int64_t p0 = (int64_t)blockIdx.x * TILE + (int64_t)threadIdx.x * 16;
+  uint32_t c = 0, na = 0, crlf = 0, m = 0, f = ~0u;
+  if (p0 < n) {
+    m = load_mask(buf, n, p0, text, &crlf, &na);
+    const int vj = virtual_in(buf, n, fs, p0, text);
+    c = __popc(m) + (vj >= 0);
+    if (m) {
+      const int j = __ffs(m) - 1;
+      f = ((uint32_t)(threadIdx.x * 16 + j) << 2) | ((crlf >> j & 1u) ? 2u : 0u);
+    } else if (vj >= 0) {
+      f = ((uint32_t)(threadIdx.x * 16 + vj + 1) << 2) | 1u;
+    }
+  }
+  using BR = hipcub::BlockReduce<uint32_t, WG>;
+  __shared__ typename BR::TempStorage tmp;
+  const uint32_t tot = BR(tmp).Sum(c);
+  __syncthreads();
+  const uint32_t fmin = BR(tmp).Reduce(f, hipcub::Min());
+  if (na) atomicOr(flags, 1u);
+  if (threadIdx.x == 0) {
+    counts[blockIdx.x] = tot;
+    first[blockIdx.x] = fmin;
+  }
+}
+
+// A line as the reference sees it: content [start, content_end), then '\n' when nl.  From a
+// line start, scan at most `need` bytes for its terminator ('\n'; in text mode also '\r',
+// whether of "\r\n" or lone) without crossing the end of the file that holds `start`.
+struct Line {
+  int64_t start, content_end;
+  int nl;
+};
+
+__device__ __forceinline__ Line scan_line(const uint8_t* __restrict__ buf, int64_t n, Files fs,
+                                          int64_t start, int need, int text) {
+  int lo = 0, hi = fs.nfiles;  // the file holding `start`: first end > start
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (fs.ends[mid] <= start) lo = mid + 1; else hi = mid;
+  }
+  const int64_t fe = lo < fs.nfiles ? fs.ends[lo] : n;
+  const int64_t lim = start + need < fe ? start + need : fe;
+  Line L{start, lim, 1};
+  for (int64_t i = start; i < lim; ++i) {
+    const uint8_t c = buf[i];
+    if (c == '\n' || (text && c == '\r')) {
+      L.content_end = i;
+      return L;
+    }
+  }
+  // no terminator in the window: the line is longer than needed (content_end = lim is
+  // enough), or it is the file's unterminated last line
+  if (lim == fe) L.nl = 0;
+  return L;
+}
+
+// One pass over the buffer, a tile per workgroup:
+//  1. each thread finds its 16 bytes' terminators (as count_kernel) and the block scan
+//     numbers them; their in-tile offsets go to LDS in byte order (bit 13 = virtual file
+//     end: the next line starts at the end and the line has no '\n'; bit 14 = "\r\n");
+//  2. the line after terminator t (global number g+1) belongs to record (g+1)/4: a name
+//     line (0) must start with '@' (fastq.py:35-36); a sequence (1) or quality (3) line
+//     becomes an "action" {start, content end, nl, record, which}: its end is the next
+//     terminator of the tile, or, for the tile's last line, found by a short scan;
+//  3. the block copies every action's slices for all spans cooperatively (one thread per
+//     output byte, re-reading the line bytes from L1/L2).
+// Record 0's name line starts at byte 0, checked by thread 0 of tile 0.
+constexpr int MAX_SPANS = 8;
+struct Spans {
+  int n, max_end, width;  // width = sum of the spans' widths
+  int start[MAX_SPANS], end[MAX_SPANS];
+  int64_t prefix[MAX_SPANS];  // sum of the widths of the spans before k
+};
+
+constexpr int MAX_TERM = TILE + 16;  // terminators a tile can hold (+ virtual file ends)
+constexpr uint32_t T_OFF = 0x1FFFu, T_VIRT = 1u << 13, T_CRLF = 1u << 14;
+
+// a sequence/quality line of the tile (8 bytes in LDS): its terminator's tile index t (the
+// line is number g0 + t + 1), its start offset in the tile, its content end relative to the
+// tile start with bit 31 = no '\n'
+struct Action {
+  uint16_t t, start;
+  int32_t cend;
+};
+
+__global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs,
+                                                     int text, const unsigned long long* __restrict__ offsets,
+                                                     const uint32_t* __restrict__ first, int64_t ntiles,
+                                                     int64_t nrec, Spans sp, uint8_t* __restrict__ seq_out,
+                                                     uint8_t* __restrict__ qual_out,
+                                                     int32_t* __restrict__ seq_len,
+                                                     int32_t* __restrict__ qual_len,
+                                                     unsigned long long* __restrict__ first_bad) {
+  __shared__ uint32_t term[MAX_TERM];
+  __shared__ Action act[MAX_TERM / 2 + 2];  // 33 KiB with term[]: 4 workgroups per CU
+  const int64_t t0 = (int64_t)blockIdx.x * TILE;
+  const int64_t p0 = t0 + (int64_t)threadIdx.x * 16;
+  uint32_t m = 0, crlf = 0, na;
+  int vj = -1;
+  if (p0 < n) {
+    m = load_mask(buf, n, p0, text, &crlf, &na);
+    vj = virtual_in(buf, n, fs, p0, text);
+  }
+  const uint32_t c = __popc(m) + (vj >= 0);
+  using BS = hipcub::BlockScan<uint32_t, WG>;
+  __shared__ typename BS::TempStorage tmp;
+  uint32_t pre, ntile;
+  BS(tmp).ExclusiveSum(c, pre, ntile);
+  {
+    uint32_t bits = m | (vj >= 0 ? (1u << vj) : 0u);
+    uint32_t at = pre;
+    while (bits) {
+      const int j = __ffs(bits) - 1;
+      bits &= bits - 1;
+      const uint32_t off = (uint32_t)(threadIdx.x * 16 + j);
+      if (m >> j & 1u) term[at++] = off | ((crlf >> j & 1u) ? T_CRLF : 0u);
+      if (j == vj) term[at++] = (off + 1) | T_VIRT;  // the file ends after byte off
+    }
+  }
+  __syncthreads();
+  const int64_t g0 = (int64_t)offsets[blockIdx.x];  // global number of the tile's first terminator
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nrec > 0 && buf[0] != '@') atomicMin(first_bad, 0ull);
+  for (uint32_t t = threadIdx.x; t < ntile; t += WG) {
+    const int64_t line = g0 + t + 1, r = line >> 2;
+    if (r >= nrec) continue;
+    const uint32_t e = term[t];
+    const int64_t next = t0 + (e & T_OFF) + ((e & T_VIRT) ? 0 : 1);  // the line's start
+    const int which = (int)(line & 3);
+    if (which == 0) {
+      if (buf[next] != '@') atomicMin(first_bad, (unsigned long long)r);
+    } else if (which == 1 || which == 3) {
+      int64_t cend;
+      int nl;
+      const uint32_t nf = blockIdx.x + 1 < ntiles ? first[blockIdx.x + 1] : ~0u;
+      if (t + 1 < ntile) {  // the line ends at the tile's next terminator
+        const uint32_t f = term[t + 1];
+        cend = t0 + (f & T_OFF) - ((f & T_CRLF) ? 1 : 0);
+        nl = (f & T_VIRT) ? 0 : 1;
+      } else if (nf != ~0u) {  // the tile's last line ends at the next tile's first terminator
+        cend = t0 + TILE + (nf >> 2) - ((nf & 2u) ? 1 : 0);
+        nl = (nf & 1u) ? 0 : 1;
+      } else {  // no terminator in the next tile either: scan (max_end bytes, within its file)
+        int lo = 0, hi = fs.nfiles;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (fs.ends[mid] <= next) lo = mid + 1; else hi = mid;
+        }
+        const int64_t fe = lo < fs.nfiles ? fs.ends[lo] : n;
+        const int64_t lim = next + sp.max_end < fe ? next + sp.max_end : fe;
+        cend = lim;
+        nl = lim == fe ? 0 : 1;  // longer than the window: its end is irrelevant
+        for (int64_t i = next; i < lim; ++i) {
+          const uint8_t ch = buf[i];
+          if (ch == '\n' || (text && ch == '\r')) {
+            cend = i;
+            nl = 1;
+            break;
+          }
+        }
+      }
+      Action A;
+      A.t = (uint16_t)t;
+      A.start = (uint16_t)(next - t0);  // <= TILE
+      A.cend = (int32_t)(cend - t0) | (nl ? 0 : (int32_t)0x80000000);
+      // sequence/quality lines follow the even-numbered terminators: slot = their rank
+      act[(g0 + t) / 2 - (g0 + 1) / 2] = A;
+    }
+  }
+  __syncthreads();
+  // actions of the tile = its even-numbered terminators (those of records < nrec)
+  int64_t lastg = g0 + ntile;  // one past the tile's last terminator number
+  if (lastg > 4 * nrec - 1) lastg = 4 * nrec - 1;  // terminators beyond the last record's line 3
+  const int na_ = lastg > g0 ? (int)((lastg + 1) / 2 - (g0 + 1) / 2) : 0;
+  // one thread per (action, span): length, then the slice's bytes (independent loads)
+  for (int q = threadIdx.x; q < na_ * sp.n; q += WG) {
+    const Action A = act[q / sp.n];
+    const int k = q - (q / sp.n) * sp.n;
+    const int64_t line = g0 + A.t + 1, rec = line >> 2;
+    const bool is_seq = (line & 3) == 1;
+    int32_t* len = is_seq ? seq_len : qual_len;
+    uint8_t* out = is_seq ? seq_out : qual_out;
+    const int64_t clen = (int64_t)(A.cend & 0x7FFFFFFF) - A.start, llen = clen + (A.cend < 0 ? 0 : 1);
+    const int64_t a = sp.start[k] < llen ? sp.start[k] : llen, b = sp.end[k] < llen ? sp.end[k] : llen;
+    if (len) len[k * nrec + rec] = (int32_t)(b - a);
+    if (!out) continue;
+    const int w = sp.end[k] - sp.start[k];
+    uint8_t* o = out + sp.prefix[k] * nrec + rec * w;
+    const uint8_t* src = buf + t0 + A.start;
+    // fast path: a whole-width slice inside the line's content, a row of whole dwords:
+    // aligned dword loads + byte-align funnel shifts, dword stores
+    const int64_t s0 = t0 + A.start + a;
+    const int64_t base = s0 & ~3LL;
+    const int nd = w / 4;
+    if (b - a == w && b <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
+        ((uintptr_t)o & 3) == 0) {
+      const uint32_t* d = reinterpret_cast<const uint32_t*>(buf + base);
+      const uint32_t sh = (uint32_t)(s0 & 3);
+      uint32_t* od = reinterpret_cast<uint32_t*>(o);
+      uint32_t lo = d[0];
+      for (int q2 = 0; q2 < nd; ++q2) {
+        const uint32_t hi = d[q2 + 1];
+        od[q2] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        lo = hi;
+      }
+      continue;
+    }
+#pragma unroll 8
+    for (int j = 0; j < w; ++j) {
+      const int64_t i = a + j;
+      o[j] = i < b ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
+    }
+  }
+}
+
+}  // namespace
+
+struct sct_fastq_index {
+  int64_t nbytes = 0, nlines = 0, nrec = 0, first_bad = -2;
+  int text = 0, nfiles = 0;
+  int64_t ntiles = 0;
+  void* d_mem = nullptr;                    // one allocation holding the arrays below
+  int64_t* d_ends = nullptr;                // file ends
+  unsigned long long* d_offsets = nullptr;  // ntiles + 1 line offsets (exclusive scan of tile counts)
+  uint32_t* d_first = nullptr;              // per tile: first terminator (see count_kernel)
+  unsigned long long* d_bad = nullptr;      // first bad-name record of the last extraction
+};
+
+extern "C" int sct_fastq_index_destroy(sct_fastq_index* ix) {
+  if (!ix) return SCT_OK;
+  if (ix->d_mem) (void)hipFree(ix->d_mem);
+  delete ix;
+  return SCT_OK;
+}
+
+extern "C" int sct_fastq_index_create(const uint8_t* d_buf, int64_t nbytes, const int64_t* file_ends,
+                                      int nfiles, int text_mode, void* stream, sct_fastq_index** out) {
+  SCT_CHECK(out != nullptr, "index is NULL");
+  *out = nullptr;
+  SCT_CHECK(nbytes >= 0 && (nbytes == 0 || d_buf != nullptr), "bad buffer");
+  SCT_CHECK(nfiles >= 1 && file_ends != nullptr, "need at least one file end");
+  for (int f = 0; f < nfiles; ++f)
+    SCT_CHECK(file_ends[f] >= (f ? file_ends[f - 1] : 0) && file_ends[f] <= nbytes,
+              "file_ends must be non-decreasing and <= nbytes");
+  SCT_CHECK(file_ends[nfiles - 1] == nbytes, "the last file must end at nbytes");
+  hipStream_t s = sct::as_stream(stream);
+  auto* ix = new sct_fastq_index();
+  auto fail_with = [&](int rc) {
+    sct_fastq_index_destroy(ix);
+    return rc;
+  };
+  ix->nbytes = nbytes;
+  ix->text = text_mode ? 1 : 0;
+  ix->nfiles = nfiles;
+  ix->ntiles = std::max<int64_t>(1, sct::ceil_div(nbytes, TILE));
+  SCT_CHECK(ix->ntiles < (1LL << 31), "buffer too large");
+  // one allocation: ends | offsets | counts | first | flags, bad | scan scratch
+  size_t tb = 0;
+  SCT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr,
+                                           (unsigned long long*)nullptr, (int)(ix->ntiles + 1), s));
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_ends = 0, o_off = up((size_t)nfiles * 8), o_cnt = o_off + up((ix->ntiles + 1) * 8),
+               o_first = o_cnt + up((ix->ntiles + 1) * 8), o_flags = o_first + up(ix->ntiles * 4),
+               o_tmp = o_flags + 256, total_bytes = o_tmp + up(tb);
+  hipError_t e = hipMalloc(&ix->d_mem, total_bytes);
+  if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "fastq index: %s", hipGetErrorString(e)));
+  char* base = (char*)ix->d_mem;
+  ix->d_ends = (int64_t*)(base + o_ends);
+  ix->d_offsets = (unsigned long long*)(base + o_off);
+  ix->d_first = (uint32_t*)(base + o_first);
+  unsigned long long* d_counts = (unsigned long long*)(base + o_cnt);
+  unsigned* d_flags = (unsigned*)(base + o_flags);
+  ix->d_bad = (unsigned long long*)(base + o_flags + 8);
+  void* d_tmp = base + o_tmp;
+  SCT_HIP(hipMemcpyAsync(ix->d_ends, file_ends, (size_t)nfiles * 8, hipMemcpyHostToDevice, s));
+  SCT_HIP(hipMemsetAsync(d_flags, 0, 8, s));
+  SCT_HIP(hipMemsetAsync(d_counts, 0, (size_t)(ix->ntiles + 1) * 8, s));
+  const Files fs{ix->d_ends, nfiles};
+  if (nbytes > 0)
+    hipLaunchKernelGGL(count_kernel, dim3((unsigned)ix->ntiles), dim3(WG), 0, s, d_buf, nbytes, fs,
+                       ix->text, d_counts, ix->d_first, d_flags);
+  SCT_LAUNCH_CHECK();
+  SCT_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb, d_counts, ix->d_offsets, (int)(ix->ntiles + 1), s));
+  unsigned long long total = 0;
+  unsigned flags = 0;
+  SCT_HIP(hipMemcpyAsync(&total, ix->d_offsets + ix->ntiles, 8, hipMemcpyDeviceToHost, s));
+  SCT_HIP(hipMemcpyAsync(&flags, d_flags, 4, hipMemcpyDeviceToHost, s));
+  SCT_HIP(hipStreamSynchronize(s));
+  if (ix->text && (flags & 1u))
+    return fail_with(sct::fail(SCT_E_RANGE, "text-mode FASTQ must be ASCII on the device path "
+                                            "(read it in 'rb' mode)"));
+  ix->nlines = (int64_t)total;
+  ix->nrec = (int64_t)total / 4;
+  *out = ix;
+  return SCT_OK;
+}
+
+extern "C" int sct_fastq_index_info(const sct_fastq_index* ix, int64_t* nrecords, int64_t* nlines,
+                                    int64_t* first_bad_name) {
+  SCT_CHECK(ix != nullptr, "index is NULL");
+  if (nrecords) *nrecords = ix->nrec;
+  if (nlines) *nlines = ix->nlines;
+  if (first_bad_name) *first_bad_name = ix->first_bad;
+  return SCT_OK;
+}
+
+extern "C" int sct_fastq_extract_spans(sct_fastq_index* ix, const uint8_t* d_buf, const int32_t* spans,
+                                       int nspans, uint8_t* d_seq, uint8_t* d_qual, int32_t* d_seq_len,
+                                       int32_t* d_qual_len, int64_t* first_bad_name, void* stream) {
+  SCT_CHECK(ix != nullptr, "index is NULL");
+  SCT_CHECK(nspans >= 0 && nspans <= MAX_SPANS && (nspans == 0 || spans), "0..%d spans", MAX_SPANS);
+  Spans sp{};
+  sp.n = nspans;
+  int64_t pre = 0;
+  for (int k = 0; k < nspans; ++k) {
+    SCT_CHECK(0 <= spans[2 * k] && spans[2 * k] <= spans[2 * k + 1] && spans[2 * k + 1] <= 4096,
+              "span %d = [%d, %d) unsupported", k, spans[2 * k], spans[2 * k + 1]);
+    sp.start[k] = spans[2 * k];
+    sp.end[k] = spans[2 * k + 1];
+    sp.prefix[k] = pre;
+    sp.max_end = std::max(sp.max_end, sp.end[k]);
+    pre += sp.end[k] - sp.start[k];
+  }
+  sp.width = (int)pre;
+  hipStream_t s = sct::as_stream(stream);
+  SCT_HIP(hipMemsetAsync(ix->d_bad, 0xFF, 8, s));
+  if (ix->nbytes > 0) {
+    SCT_CHECK(d_buf != nullptr, "buffer is NULL");
+    const Files fs{ix->d_ends, ix->nfiles};
+    hipLaunchKernelGGL(extract_kernel, dim3((unsigned)ix->ntiles), dim3(WG), 0, s, d_buf, ix->nbytes, fs,
+                       ix->text, ix->d_offsets, ix->d_first, ix->ntiles, ix->nrec, sp, d_seq, d_qual,
+                       d_seq_len, d_qual_len, ix->d_bad);
+    SCT_LAUNCH_CHECK();
+  }
+  unsigned long long bad = ~0ull;
+  SCT_HIP(hipMemcpyAsync(&bad, ix->d_bad, 8, hipMemcpyDeviceToHost, s));
+  SCT_HIP(hipStreamSynchronize(s));
+  ix->first_bad = bad == ~0ull ? -1 : (int64_t)bad;
+  if (first_bad_name) *first_bad_name = ix->first_bad;
+  return SCT_OK;
+}
+
+namespace {
+#define SCT_TRY(x)                 \
+  do {                             \
+    int rc_ = (x);                 \
+    if (rc_ != SCT_OK) return rc_; \
+  } while (0)
+}  // namespace
+
+extern "C" int sct_fastq_extract_host(const uint8_t* buf, int64_t nbytes, const int64_t* file_ends,
+                                      int nfiles, int text_mode, const int32_t* spans, int nspans,
+                                      uint8_t* seq_out, uint8_t* qual_out, int32_t* seq_len,
+                                      int32_t* qual_len, int64_t max_records, int64_t* nrecords,
+                                      int64_t* first_bad_name) {
+  SCT_CHECK(nrecords != nullptr, "nrecords is NULL");
+  SCT_CHECK(nspans >= 0 && (nspans == 0 || spans != nullptr), "bad spans");
+  sct::DevBuf d_buf;
+  SCT_HIP(d_buf.alloc((size_t)nbytes));
+  if (nbytes) SCT_HIP(hipMemcpy(d_buf.p, buf, (size_t)nbytes, hipMemcpyHostToDevice));
+  sct_fastq_index* ix = nullptr;
+  SCT_TRY(sct_fastq_index_create((const uint8_t*)d_buf.p, nbytes, file_ends, nfiles, text_mode, nullptr, &ix));
+  struct Guard {
+    sct_fastq_index* p;
+    ~Guard() { sct_fastq_index_destroy(p); }
+  } g{ix};
+  *nrecords = ix->nrec;
+  if (max_records < ix->nrec) return SCT_OK;  // sizing call: outputs untouched
+  // spans laid out back to back: row r of span k at out + nrec * off_k + r * width_k
+  int64_t width = 0;
+  for (int k = 0; k < nspans; ++k) width += (int64_t)spans[2 * k + 1] - spans[2 * k];
+  const int64_t bytes = width * ix->nrec;
+  const size_t lbytes = (size_t)ix->nrec * nspans * 4;
+  sct::DevBuf d_s, d_q, d_sl, d_ql;
+  SCT_HIP(d_s.alloc((size_t)bytes));
+  SCT_HIP(d_q.alloc((size_t)bytes));
+  SCT_HIP(d_sl.alloc(lbytes));
+  SCT_HIP(d_ql.alloc(lbytes));
+  SCT_TRY(sct_fastq_extract_spans(ix, (const uint8_t*)d_buf.p, spans, nspans,
+                                  seq_out ? (uint8_t*)d_s.p : nullptr, qual_out ? (uint8_t*)d_q.p : nullptr,
+                                  seq_len ? (int32_t*)d_sl.p : nullptr, qual_len ? (int32_t*)d_ql.p : nullptr,
+                                  first_bad_name, nullptr));
+  if (seq_out && bytes) SCT_HIP(hipMemcpy(seq_out, d_s.p, (size_t)bytes, hipMemcpyDeviceToHost));
+  if (qual_out && bytes) SCT_HIP(hipMemcpy(qual_out, d_q.p, (size_t)bytes, hipMemcpyDeviceToHost));
+  if (seq_len && lbytes) SCT_HIP(hipMemcpy(seq_len, d_sl.p, lbytes, hipMemcpyDeviceToHost));
+  if (qual_len && lbytes) SCT_HIP(hipMemcpy(qual_len, d_ql.p, lbytes, hipMemcpyDeviceToHost));
+  return SCT_OK;
+}
