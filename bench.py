@@ -124,7 +124,7 @@ def main():
 
     def step(record):
         counts.zero_()
-        plan.build(sptr)
+        plan.build(sptr, b, e)  # sort + the selection-table chunks this rank's items read
         if record:
             evm.record(stream)
         plan.moments(counts.data_ptr(), rank, world, sptr)  # MOMENTS scheme: this rank's share

@@ -152,6 +152,11 @@ int sct_allpairs_plan_scheme(const sct_allpairs_plan* plan, int* scheme, int* nc
                              int* code_bits);
 /* (Re)build the selection table from the codes the plan was created on. */
 int sct_allpairs_build(sct_allpairs_plan* plan, void* stream);
+/* Build only what counting items [item_begin, item_end) reads (its column chunks; the
+ * MOMENTS scheme also re-sorts the codes): a rank of a sharded job calls this with its
+ * own item range. */
+int sct_allpairs_build_items(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
+                             void* stream);
 /* Count work items [item_begin, item_end).  grid = 0 picks the persistent grid size. */
 int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
                        uint64_t* d_counts, int grid, void* stream);

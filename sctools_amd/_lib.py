@@ -55,6 +55,7 @@ SIGNATURES = {
     "sct_allpairs_plan_destroy": [_vp],
     "sct_allpairs_plan_info": [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i64), ctypes.POINTER(_i64)],
     "sct_allpairs_build": [_vp, _vp],
+    "sct_allpairs_build_items": [_vp, _i64, _i64, _vp],
     "sct_allpairs_count": [_vp, _i64, _i64, _vp, _i32, _vp],
     "sct_allpairs_range_pairs": [_vp, _i64, _i64, ctypes.POINTER(_i64)],
     "sct_allpairs_geometry": [_i64, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i64),
@@ -416,8 +417,14 @@ class AllPairsPlan:
         check(self._lib.sct_allpairs_plan_scheme(self._h, ctypes.byref(sc), ctypes.byref(nc), ctypes.byref(cb)))
         self.scheme, self.ncounts, self.code_bits = sc.value, nc.value, cb.value
 
-    def build(self, stream=0):
-        check(self._lib.sct_allpairs_build(self._h, _vp(stream)))
+    def build(self, stream=0, begin=None, end=None):
+        """Selection table for items [begin, end) (default: all of them)."""
+        if begin is None and end is None:
+            check(self._lib.sct_allpairs_build(self._h, _vp(stream)))
+        else:
+            begin = 0 if begin is None else begin
+            end = self.items if end is None else end
+            check(self._lib.sct_allpairs_build_items(self._h, begin, end, _vp(stream)))
 
     def moments(self, d_counts_ptr, part=0, nparts=1, stream=0):
         """MOMENTS scheme: add moment share `part` of `nparts` (no-op for SUBSETS)."""

@@ -438,9 +438,9 @@ __global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __re
 // table[h][pp][c] = bit-sliced 2-bit mismatch counts of nibble pp of the 64 codes of
 // group pair h against combo c (see file header).  One thread per entry.
 __global__ void allpairs_build_kernel(const uint64_t* __restrict__ codes, int64_t n, int npp,
-                                      int64_t entries, uint4* __restrict__ table) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= entries) return;
+                                      int64_t e_begin, int64_t e_end, uint4* __restrict__ table) {
+  const int64_t idx = e_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= e_end) return;
   const int c = (int)(idx & 15);
   const int pp = (int)((idx >> 4) % npp);
   const int64_t h = (idx >> 4) / npp;
@@ -470,11 +470,12 @@ __global__ void allpairs_build_kernel(const uint64_t* __restrict__ codes, int64_
 // then every thread forms entries from the planes held in LDS: per base, mismatch =
 // (lo ^ c_lo) | (hi ^ c_hi), and the 2-3 mismatch planes are summed by a half/full adder.
 __global__ __launch_bounds__(256) void allpairs_build_tri_kernel(const uint64_t* __restrict__ codes,
-                                                                 int64_t n, int64_t ngp,
+                                                                 int64_t n, int64_t gp_begin,
+                                                                 int64_t gp_end,
                                                                  uint4* __restrict__ table) {
   __shared__ uint64_t planes[4][32];  // [wave][2 * base + bit], group a = low 32 bits
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t h0 = (int64_t)blockIdx.x * 4;
+  const int64_t h0 = gp_begin + (int64_t)blockIdx.x * 4;
   {
     const int64_t j = (h0 + wave) * 64 + lane;
     const uint32_t code = j < n ? (uint32_t)codes[j] : 0u;
@@ -485,7 +486,7 @@ __global__ __launch_bounds__(256) void allpairs_build_tri_kernel(const uint64_t*
     }
   }
   __syncthreads();
-  const int64_t nh = ngp - h0 < 4 ? ngp - h0 : 4;
+  const int64_t nh = gp_end - h0 < 4 ? gp_end - h0 : 4;
   for (int t = threadIdx.x; t < nh * kTriRow; t += 256) {
     const int w = t / kTriRow, e = t - w * kTriRow;
     const int g = e < 32 ? (e >> 4) : 2 + ((e - 32) >> 6);
@@ -1073,21 +1074,52 @@ extern "C" int sct_allpairs_moments(sct_allpairs_plan* plan, int part, int npart
   return SCT_OK;
 }
 
+namespace {
+// column chunk holding work item t (items are chunk-major, chunk c has rows_of_chunk(c))
+int64_t chunk_of_item(const sct_allpairs_plan* p, int64_t t) {
+  int64_t c = 0, base = 0;
+  while (c < p->nchunks - 1 && base + rows_of_chunk(p, c) <= t) base += rows_of_chunk(p, c++);
+  return c;
+}
+}  // namespace
+
 extern "C" int sct_allpairs_build(sct_allpairs_plan* plan, void* stream) {
   SCT_CHECK(plan != nullptr, "plan is NULL");
+  return sct_allpairs_build_items(plan, 0, plan->items, stream);
+}
+
+extern "C" int sct_allpairs_build_items(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
+                                        void* stream) {
+  SCT_CHECK(plan != nullptr, "plan is NULL");
+  SCT_CHECK(0 <= item_begin && item_begin <= item_end && item_end <= plan->items,
+            "item range [%lld, %lld) outside [0, %lld)", (long long)item_begin, (long long)item_end,
+            (long long)plan->items);
   if (plan->table_entries == 0) return SCT_OK;
   hipStream_t s = sct::as_stream(stream);
-  const int64_t blocks = sct::ceil_div(plan->table_entries, 256);
+  // only the column chunks the items read (a rank of a sharded job builds its own slice)
+  int64_t c0 = 0, c1 = plan->nchunks;
+  if (item_end > item_begin) {
+    c0 = chunk_of_item(plan, item_begin);
+    c1 = chunk_of_item(plan, item_end - 1) + 1;
+  } else {
+    c1 = 0;
+  }
+  const int64_t gp_per_chunk = plan->ct / 2;
   if (plan->scheme == SCT_ALLPAIRS_MOMENTS) {
+    // every row block may be read: the whole (sorted) code list is needed
     size_t bytes = plan->sort_tmp_bytes;
     SCT_HIP(hipcub::DeviceRadixSort::SortKeys(plan->d_sort_tmp, bytes, (const uint64_t*)plan->d_codes,
                                               plan->d_sorted, (int)plan->n, 0, 32, s));
-    const int64_t ngp = plan->table_entries / kTriRow;
-    hipLaunchKernelGGL(allpairs_build_tri_kernel, dim3((unsigned)sct::ceil_div(ngp, 4)), dim3(256), 0,
-                       s, plan->d_sorted, plan->n, ngp, plan->d_table);
+    const int64_t gp0 = c0 * gp_per_chunk, ngp = (c1 - c0) * gp_per_chunk;
+    if (ngp > 0)
+      hipLaunchKernelGGL(allpairs_build_tri_kernel, dim3((unsigned)sct::ceil_div(ngp, 4)), dim3(256), 0,
+                         s, plan->d_sorted, plan->n, gp0, gp0 + ngp, plan->d_table);
   } else {
-    hipLaunchKernelGGL(allpairs_build_kernel, dim3((unsigned)blocks), dim3(256), 0, s, plan->d_codes,
-                       plan->n, plan->npp, plan->table_entries, plan->d_table);
+    const int64_t row = (int64_t)plan->npp * 16;
+    const int64_t e0 = c0 * gp_per_chunk * row, e1 = c1 * gp_per_chunk * row;
+    if (e1 > e0)
+      hipLaunchKernelGGL(allpairs_build_kernel, dim3((unsigned)sct::ceil_div(e1 - e0, 256)), dim3(256), 0,
+                         s, plan->d_codes, plan->n, plan->npp, e0, e1, plan->d_table);
   }
   SCT_LAUNCH_CHECK();
   return SCT_OK;

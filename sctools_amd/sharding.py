@@ -59,7 +59,7 @@ def allpairs_histogram_sharded(codes, code_bits=None, group=None, device=None, s
         s = (stream or torch.cuda.current_stream(device)).cuda_stream
         b, e = item_range(plan.items, rank, world)
         counts = torch.zeros(plan.ncounts, dtype=torch.int64, device=device)
-        plan.build(s)
+        plan.build(s, b, e)  # only the column chunks of this rank's items
         plan.moments(counts.data_ptr(), rank, world, s)
         plan.count(counts.data_ptr(), b, e, 0, s)
         return combine_counts(counts, group, plan.scheme, plan.nbins)

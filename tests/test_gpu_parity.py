@@ -9,7 +9,7 @@ import pytest
 
 from conftest import fromhex
 from oracle import oracle as O
-from sctools_amd import _lib, barcode, encodings, synthetic
+from sctools_amd import sharding, _lib, barcode, encodings, synthetic
 
 pytestmark = pytest.mark.gpu
 
@@ -277,6 +277,29 @@ def test_allpairs_shards_sum_to_whole():
     assert torch.equal(full, parts)
     assert total_pairs == plan.pairs == codes.size * (codes.size - 1) // 2
     plan.close()
+
+
+@pytest.mark.parametrize("scheme", [0, 1])
+def test_allpairs_partial_builds_per_rank(scheme):
+    """Each 'rank' builds only the table chunks of its item range (build_items), counts that
+    range and its moment share; the summed counts invert to the oracle histogram."""
+    torch = pytest.importorskip("torch")
+    codes = synthetic.whitelist_codes(30_000, 16, seed=21)
+    d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
+    world = 3
+    total = None
+    for rank in range(world):
+        plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=scheme)
+        b, e = sharding.item_range(plan.items, rank, world)
+        c = torch.zeros(plan.ncounts, dtype=torch.int64, device="cuda")
+        plan.build(0, b, e)
+        plan.moments(c.data_ptr(), rank, world)
+        plan.count(c.data_ptr(), b, e)
+        total = c if total is None else total + c
+        sch, nb = plan.scheme, plan.nbins
+        plan.close()
+    hist = _lib.counts_to_hist(total.cpu().numpy().view(np.uint64), sch, nb)
+    assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
 def test_allpairs_737k_properties():
