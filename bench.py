@@ -38,9 +38,9 @@ ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-b
 # VALU issue slots the bit-sliced count kernel spends per pair at 16 bp, from its unmasked
 # loop (v_bcnt_u32_b32 counts 2: half rate on gfx950), per count scheme:
 #   SUBSETS (nibble tables, full unroll): 33 v_bitop3 + 16 v_bcnt + 6 v_xor/v_and per 32 pairs;
-#   MOMENTS (triple tables, unroll 2): 24 v_bitop3 + 13 v_bcnt + 4 v_xor/v_and + 1.5 v_add.
+#   MOMENTS (triple tables, unroll 1): 24 v_bitop3 + 13 v_bcnt + 4 v_xor/v_and + 3 v_add.
 ISSUE_SLOTS_PER_PAIR = {_lib.SCHEME_SUBSETS: (33 + 2 * 16 + 6) / 32.0,
-                        _lib.SCHEME_MOMENTS: (24 + 2 * 13 + 4 + 1.5) / 32.0}
+                        _lib.SCHEME_MOMENTS: (24 + 2 * 13 + 4 + 3) / 32.0}
 
 
 def parse():

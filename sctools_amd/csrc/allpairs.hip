@@ -313,13 +313,16 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
 // unrolled 1, 2, fully (3: LDS offsets become immediates) or 4 times.  A software-
 // pipelined form (next group pair's reads issued before this one's counting) and forced
 // occupancy (amdgpu_waves_per_eu) measured no faster and were dropped.
-template <int V> struct Variant { static constexpr int UNROLL = V, ABL = 0; };
-template <> struct Variant<3> { static constexpr int UNROLL = 16, ABL = 0; };
+// WAVES > 1 asks the compiler for that many waves per SIMD (amdgpu_waves_per_eu: VGPRs
+// capped at 512 / WAVES): variant 5 = unroll 2 held to 128 VGPRs (4 waves per SIMD).
+template <int V> struct Variant { static constexpr int UNROLL = V, ABL = 0, WAVES = 1; };
+template <> struct Variant<3> { static constexpr int UNROLL = 16, ABL = 0, WAVES = 1; };
+template <> struct Variant<5> { static constexpr int UNROLL = 2, ABL = 0, WAVES = 4; };
 #ifdef SCT_ABLATION
 // ablation builds (wrong results, timing only): 11 no counting, 12 no tree, 13 no LDS reads
-template <> struct Variant<11> { static constexpr int UNROLL = 4, ABL = 1; };
-template <> struct Variant<12> { static constexpr int UNROLL = 4, ABL = 2; };
-template <> struct Variant<13> { static constexpr int UNROLL = 4, ABL = 3; };
+template <> struct Variant<11> { static constexpr int UNROLL = 4, ABL = 1, WAVES = 1; };
+template <> struct Variant<12> { static constexpr int UNROLL = 4, ABL = 2, WAVES = 1; };
+template <> struct Variant<13> { static constexpr int UNROLL = 4, ABL = 3, WAVES = 1; };
 #endif
 
 // Workgroup reduction of the per-lane counters: 64-lane butterfly (shfl_xor, lowered to
@@ -352,7 +355,8 @@ __device__ __forceinline__ void flush_counts(uint32_t (&cnt)[G], uint32_t& cnt0,
 }
 
 template <int NPP, int V, bool MOM>
-__global__ __launch_bounds__(RB) void allpairs_count_kernel(const uint64_t* __restrict__ codes,
+__global__ __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(Variant<V>::WAVES)))
+void allpairs_count_kernel(const uint64_t* __restrict__ codes,
                                                             const uint4* __restrict__ table,
                                                             int64_t n, int64_t nchunks,
                                                             int64_t item_begin, int64_t item_end,
@@ -755,6 +759,7 @@ struct CountKernels {
           case 1: return allpairs_count_kernel<NPP, 1, true>;
           case 3: return allpairs_count_kernel<NPP, 3, true>;
           case 4: return allpairs_count_kernel<NPP, 4, true>;
+          case 5: return allpairs_count_kernel<NPP, 5, true>;
 #ifdef SCT_ABLATION
           case 11: return allpairs_count_kernel<NPP, 11, true>;
           case 12: return allpairs_count_kernel<NPP, 12, true>;
@@ -986,13 +991,14 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess ||
       cus <= 0)
     cus = 256;
-  // defaults measured on MI355X: MOMENTS unroll 2, SUBSETS@16 bases full unroll
-  p->variant = p->scheme == SCT_ALLPAIRS_MOMENTS ? 2 : (p->npp == 8 ? 3 : 2);
+  // defaults measured on MI355X: MOMENTS unroll 1, SUBSETS@16 bases full unroll
+  p->variant = p->scheme == SCT_ALLPAIRS_MOMENTS ? 1 : (p->npp == 8 ? 3 : 2);
   // MOMENTS: 32 items per pull halves the chunk re-staging (L2 -> LDS) at no cost in time
   if (p->scheme == SCT_ALLPAIRS_MOMENTS) p->grab = 32;
   if (const char* v = getenv("SCT_ALLPAIRS_VARIANT")) {
     const int vv = atoi(v);
-    if ((vv >= 1 && vv <= 3) || (vv == 4 && p->scheme == SCT_ALLPAIRS_MOMENTS) || (vv >= 11 && vv <= 13))
+    if ((vv >= 1 && vv <= 3) || ((vv == 4 || vv == 5) && p->scheme == SCT_ALLPAIRS_MOMENTS) ||
+        (vv >= 11 && vv <= 13))
       p->variant = vv;
   }
   p->grid = grid_for(p->npp, cus, p->variant, p->scheme);
