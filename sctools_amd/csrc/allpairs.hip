@@ -246,6 +246,11 @@ __device__ __forceinline__ void one_group(const uint32_t (&s0)[Geom<NPP, MOM>::N
   constexpr int NL = Geom<NPP, MOM>::NL;
   constexpr int B = Geom<NPP, MOM>::B;  // MOMENTS: the carry into plane 4 is dropped (d mod 16)
   uint32_t d[B];
+  if constexpr (ABL == 4) {  // ablation: no tree and no counting (loads kept live, 1 op each)
+#pragma unroll
+    for (int b = 0; b < B; ++b) cnt[b] ^= s0[b % NL] ^ s1[(b + 1) % NL];
+    return;
+  }
   if constexpr (ABL == 2) {  // ablation: no adder tree (planes straight into counting)
 #pragma unroll
     for (int b = 0; b < B; ++b) d[b] = s0[b % NL] ^ s1[(b + 1) % NL];
@@ -319,10 +324,12 @@ template <int V> struct Variant { static constexpr int UNROLL = V, ABL = 0, WAVE
 template <> struct Variant<3> { static constexpr int UNROLL = 16, ABL = 0, WAVES = 1; };
 template <> struct Variant<5> { static constexpr int UNROLL = 2, ABL = 0, WAVES = 4; };
 #ifdef SCT_ABLATION
-// ablation builds (wrong results, timing only): 11 no counting, 12 no tree, 13 no LDS reads
+// ablation builds (wrong results, timing only): 11 no counting, 12 no tree, 13 no LDS reads,
+// 14 neither tree nor counting (the loop's fixed costs)
 template <> struct Variant<11> { static constexpr int UNROLL = 4, ABL = 1, WAVES = 1; };
 template <> struct Variant<12> { static constexpr int UNROLL = 4, ABL = 2, WAVES = 1; };
 template <> struct Variant<13> { static constexpr int UNROLL = 4, ABL = 3, WAVES = 1; };
+template <> struct Variant<14> { static constexpr int UNROLL = 4, ABL = 4, WAVES = 1; };
 #endif
 
 // Workgroup reduction of the per-lane counters: 64-lane butterfly (shfl_xor, lowered to
@@ -764,6 +771,7 @@ struct CountKernels {
           case 11: return allpairs_count_kernel<NPP, 11, true>;
           case 12: return allpairs_count_kernel<NPP, 12, true>;
           case 13: return allpairs_count_kernel<NPP, 13, true>;
+          case 14: return allpairs_count_kernel<NPP, 14, true>;
 #endif
           default: return allpairs_count_kernel<NPP, 2, true>;
         }
@@ -998,7 +1006,7 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
   if (const char* v = getenv("SCT_ALLPAIRS_VARIANT")) {
     const int vv = atoi(v);
     if ((vv >= 1 && vv <= 3) || ((vv == 4 || vv == 5) && p->scheme == SCT_ALLPAIRS_MOMENTS) ||
-        (vv >= 11 && vv <= 13))
+        (vv >= 11 && vv <= 14))
       p->variant = vv;
   }
   p->grid = grid_for(p->npp, cus, p->variant, p->scheme);
