@@ -129,14 +129,23 @@ int sct_hamming_pairs_host(int kind, const uint64_t* a, const uint64_t* b, int64
  *   counted once, every moment part added once) invert.  13 products instead of 16
  *   cut the count kernel's VALU work per pair.
  *
+ * SCT_ALLPAIRS_SPECTRAL (the same 16-base codes): no pair is enumerated.  The histogram
+ *   comes from the Walsh-Hadamard transform F of the codes' multiplicity over Z_2^32:
+ *   d_counts[1+w] += S_w = sum of F(z)^2 over the z with w non-zero 2-bit digits,
+ *   w = 0..16, and d_counts[0] += n once (by the range holding item 0).  ncounts = 18.
+ *   The items are the 4096 transform slices (z >> 20); the cost of a slice does not
+ *   depend on n, so AUTO picks this scheme for large whitelists.  Only
+ *   the counts of the whole job invert (host: Krawtchouk transform, checked exact).
+ *
  * The counts are linear, so they may be summed across devices (RCCL all-reduce)
  * before sct_counts_to_hist_ex.
  */
 typedef struct sct_allpairs_plan sct_allpairs_plan;
 
-#define SCT_ALLPAIRS_AUTO (-1)    /* MOMENTS where supported, else SUBSETS */
+#define SCT_ALLPAIRS_AUTO (-1)    /* 16 bases: SPECTRAL for large n, else MOMENTS; else SUBSETS */
 #define SCT_ALLPAIRS_SUBSETS 0
 #define SCT_ALLPAIRS_MOMENTS 1
+#define SCT_ALLPAIRS_SPECTRAL 2
 
 /* = sct_allpairs_plan_create_ex(..., SCT_ALLPAIRS_AUTO, plan) */
 int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int code_bits,
@@ -170,14 +179,16 @@ int sct_allpairs_moments(sct_allpairs_plan* plan, int part, int nparts, uint64_t
  * chunk.  Lets shard drivers partition [0, items) before touching a GPU. */
 int sct_allpairs_geometry(int64_t n, int code_bits, int* nbins, int64_t* items, int* rows_per_item,
                           int* cols_per_item);
-/* Pairs contained in work items [item_begin, item_end) (host arithmetic). */
+/* Pairs contained in work items [item_begin, item_end) (host arithmetic; SPECTRAL: the
+ * range's share floor(P*end/items) - floor(P*begin/items) of all P pairs). */
 int sct_allpairs_range_pairs(const sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
                              int64_t* pairs);
 
 /* Host: SUBSETS counts -> histogram (exact Moebius inversion), hist[d] for d < nbins. */
 int sct_counts_to_hist(const uint64_t* counts, int nbins, uint64_t* hist);
-/* Host: counts of either scheme -> histogram (MOMENTS: exact rational solve of the
- * 17 x 17 system, checked integral and non-negative).  nbins must be the plan's. */
+/* Host: counts of any scheme -> histogram (MOMENTS: exact rational solve of the
+ * 17 x 17 system; SPECTRAL: Krawtchouk transform; both checked integral and
+ * non-negative).  nbins must be the plan's. */
 int sct_counts_to_hist_ex(int scheme, const uint64_t* counts, int ncounts, uint64_t* hist,
                           int nbins);
 

@@ -26,6 +26,7 @@ SCT_E_RANGE = -4
 SCHEME_AUTO = -1
 SCHEME_SUBSETS = 0
 SCHEME_MOMENTS = 1
+SCHEME_SPECTRAL = 2
 
 _i32, _i64, _dbl = ctypes.c_int, ctypes.c_int64, ctypes.c_double
 _vp = ctypes.c_void_p
@@ -254,9 +255,10 @@ def hamming_hist_allpairs(codes, code_bits=None):
 
 
 def counts_to_hist(counts, scheme=SCHEME_SUBSETS, nbins=None):
-    """Counts of an all-pairs plan (either scheme) -> exact histogram (uint64[nbins])."""
+    """Counts of an all-pairs plan (any scheme) -> exact histogram (uint64[nbins])."""
     counts = np.ascontiguousarray(counts, dtype=np.uint64).reshape(-1)
-    nbins = counts.size if nbins is None else nbins
+    if nbins is None:  # SPECTRAL counts carry n ahead of the 17 weight sums
+        nbins = counts.size - 1 if scheme == SCHEME_SPECTRAL else counts.size
     hist = np.zeros(nbins, dtype=np.uint64)
     check(lib().sct_counts_to_hist_ex(scheme, _ptr(counts), counts.size, _ptr(hist), nbins))
     return hist

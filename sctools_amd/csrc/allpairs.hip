@@ -41,6 +41,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "sct_common.h"
+#include "spectral.h"
 
 namespace {
 
@@ -704,11 +705,26 @@ __global__ __launch_bounds__(256) void moments_finalize_kernel(const unsigned* _
 // groups per column chunk: nibble layout 32 (16 above 8 nibbles), triple layout 16
 int ct_for(int npp, bool tri) { return tri ? 16 : (npp <= 8 ? 32 : 16); }
 bool mom_supported(int npp, int64_t n) { return npp * 2 == sct::kMomG && n <= 100000000LL; }
-// what SCT_ALLPAIRS_AUTO resolves to (SCT_ALLPAIRS_SCHEME=0 in the environment forces SUBSETS)
-bool auto_moments(int npp, int64_t n) {
-  const char* v = getenv("SCT_ALLPAIRS_SCHEME");
-  return mom_supported(npp, n) && !(v && atoi(v) == 0);
+// SPECTRAL: the same 16-base codes; its cost does not depend on n
+bool spectral_supported(int npp, int64_t n) { return mom_supported(npp, n); }
+// smallest n for which AUTO picks SPECTRAL over MOMENTS (measured crossover)
+int64_t spectral_min_n() {
+  const char* v = getenv("SCT_SPECTRAL_MIN_N");
+  return v ? atoll(v) : 1500000;
 }
+// what SCT_ALLPAIRS_AUTO resolves to; SCT_ALLPAIRS_SCHEME=0/1/2 in the environment forces
+// SUBSETS / MOMENTS / SPECTRAL where the codes allow it
+int auto_scheme(int npp, int64_t n) {
+  if (const char* v = getenv("SCT_ALLPAIRS_SCHEME")) {
+    const int f = atoi(v);
+    if (f == SCT_ALLPAIRS_SUBSETS) return f;
+    if (f == SCT_ALLPAIRS_MOMENTS && mom_supported(npp, n)) return f;
+    if (f == SCT_ALLPAIRS_SPECTRAL && spectral_supported(npp, n)) return f;
+  }
+  if (spectral_supported(npp, n) && n >= spectral_min_n()) return SCT_ALLPAIRS_SPECTRAL;
+  return mom_supported(npp, n) ? SCT_ALLPAIRS_MOMENTS : SCT_ALLPAIRS_SUBSETS;
+}
+bool auto_moments(int npp, int64_t n) { return auto_scheme(npp, n) == SCT_ALLPAIRS_MOMENTS; }
 
 }  // namespace
 
@@ -743,6 +759,7 @@ struct sct_allpairs_plan {
   uint32_t* d_mpartial = nullptr;  // [nranges][560 * 64] partial bins
   int64_t mom_nwords = 0;
   int mom_nranges = 0;
+  sct_spectral::State spec;  // SPECTRAL scheme (spectral.hip)
 };
 
 namespace {
@@ -900,7 +917,7 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
                                            int scheme, sct_allpairs_plan** plan) {
   SCT_CHECK(plan != nullptr, "plan is NULL");
   SCT_CHECK(scheme == SCT_ALLPAIRS_AUTO || scheme == SCT_ALLPAIRS_SUBSETS ||
-                scheme == SCT_ALLPAIRS_MOMENTS,
+                scheme == SCT_ALLPAIRS_MOMENTS || scheme == SCT_ALLPAIRS_SPECTRAL,
             "unknown scheme %d", scheme);
   *plan = nullptr;
   SCT_CHECK(n >= 0, "n must be >= 0");
@@ -946,10 +963,24 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
   if (scheme == SCT_ALLPAIRS_MOMENTS && !mom_ok)
     return cleanup(sct::fail(SCT_E_INVALID, "MOMENTS scheme needs code_bits in 29..32 (got %d) "
                              "and n <= 1e8", code_bits));
-  p->scheme = (scheme == SCT_ALLPAIRS_MOMENTS ||
-               (scheme == SCT_ALLPAIRS_AUTO && auto_moments(p->npp, n)))
-                  ? SCT_ALLPAIRS_MOMENTS
-                  : SCT_ALLPAIRS_SUBSETS;
+  if (scheme == SCT_ALLPAIRS_SPECTRAL && !spectral_supported(p->npp, n))
+    return cleanup(sct::fail(SCT_E_INVALID, "SPECTRAL scheme needs code_bits in 29..32 (got %d) "
+                             "and n <= 1e8", code_bits));
+  p->scheme = scheme == SCT_ALLPAIRS_AUTO ? auto_scheme(p->npp, n) : scheme;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  if (p->scheme == SCT_ALLPAIRS_SPECTRAL) {
+    // items = the 4096 transform slices; no selection table
+    p->ncounts = sct_spectral::kNCounts;
+    p->items = n >= 2 ? sct_spectral::kSlices : 0;
+    const char* c = getenv("SCT_SPECTRAL_CHUNK");
+    const int rc = sct_spectral::create(p->spec, n, c ? atoll(c) : 1024, cus);
+    if (rc != SCT_OK) return cleanup(rc);
+    *plan = p;
+    return SCT_OK;
+  }
   p->ncounts = p->scheme == SCT_ALLPAIRS_MOMENTS ? sct::kMomNCounts : p->nbins;
   const bool tri = p->scheme == SCT_ALLPAIRS_MOMENTS;
   p->ct = ct_for(p->npp, tri);
@@ -995,10 +1026,6 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
       e = hipMemcpy(p->d_msrc, src.data(), src.size() * sizeof(MomSource), hipMemcpyHostToDevice);
     if (e != hipSuccess) return cleanup(sct::fail(SCT_E_HIP, "copy moments layout: %s", hipGetErrorString(e)));
   }
-  int cus = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess ||
-      cus <= 0)
-    cus = 256;
   // defaults measured on MI355X: MOMENTS unroll 1, SUBSETS@16 bases full unroll
   p->variant = p->scheme == SCT_ALLPAIRS_MOMENTS ? 1 : (p->npp == 8 ? 3 : 2);
   // MOMENTS: 32 items per pull halves the chunk re-staging (L2 -> LDS) at no cost in time
@@ -1035,6 +1062,7 @@ extern "C" int sct_allpairs_plan_destroy(sct_allpairs_plan* plan) {
   if (plan->d_mhist) (void)hipFree(plan->d_mhist);
   if (plan->d_mmasks) (void)hipFree(plan->d_mmasks);
   if (plan->d_mpartial) (void)hipFree(plan->d_mpartial);
+  sct_spectral::destroy(plan->spec);
   delete plan;
   return SCT_OK;
 }
@@ -1108,8 +1136,9 @@ extern "C" int sct_allpairs_build_items(sct_allpairs_plan* plan, int64_t item_be
   SCT_CHECK(0 <= item_begin && item_begin <= item_end && item_end <= plan->items,
             "item range [%lld, %lld) outside [0, %lld)", (long long)item_begin, (long long)item_end,
             (long long)plan->items);
-  if (plan->table_entries == 0) return SCT_OK;
   hipStream_t s = sct::as_stream(stream);
+  if (plan->scheme == SCT_ALLPAIRS_SPECTRAL) return sct_spectral::build(plan->spec, plan->d_codes, s);
+  if (plan->table_entries == 0) return SCT_OK;
   // only the column chunks the items read (a rank of a sharded job builds its own slice)
   int64_t c0 = 0, c1 = plan->nchunks;
   if (item_end > item_begin) {
@@ -1147,6 +1176,9 @@ extern "C" int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, i
             "item range [%lld, %lld) outside [0, %lld)", (long long)item_begin,
             (long long)item_end, (long long)plan->items);
   if (item_begin == item_end) return SCT_OK;
+  if (plan->scheme == SCT_ALLPAIRS_SPECTRAL)
+    return sct_spectral::count(plan->spec, item_begin, item_end,
+                               reinterpret_cast<unsigned long long*>(d_counts), sct::as_stream(stream));
   return dispatch_count(plan, item_begin, item_end, d_counts, grid, sct::as_stream(stream));
 }
 
@@ -1155,6 +1187,13 @@ extern "C" int sct_allpairs_geometry(int64_t n, int code_bits, int* nbins, int64
   SCT_CHECK(n >= 0, "n must be >= 0");
   SCT_CHECK(code_bits >= 1 && code_bits <= 64, "code_bits %d outside [1, 64]", code_bits);
   const int npp = (code_bits + 3) / 4;
+  if (auto_scheme(npp, n) == SCT_ALLPAIRS_SPECTRAL) {  // items = transform slices
+    if (nbins) *nbins = 2 * npp + 1;
+    if (items) *items = n >= 2 ? sct_spectral::kSlices : 0;
+    if (rows_per_item) *rows_per_item = 0;
+    if (cols_per_item) *cols_per_item = 0;
+    return SCT_OK;
+  }
   const int64_t cb = 32LL * ct_for(npp, auto_moments(npp, n));
   const int64_t nchunks = n > 0 ? sct::ceil_div(n, cb) : 0;
   int64_t it = 0;
@@ -1176,6 +1215,13 @@ extern "C" int sct_allpairs_range_pairs(const sct_allpairs_plan* plan, int64_t i
   SCT_CHECK(0 <= item_begin && item_begin <= item_end && item_end <= plan->items,
             "item range outside the plan");
   const int64_t n = plan->n;
+  if (plan->scheme == SCT_ALLPAIRS_SPECTRAL) {
+    // pairs are not split by slice: a slice range is credited its share of all pairs,
+    // floor(P * end / items) - floor(P * begin / items), which sums to P over a partition
+    const __int128 P = (__int128)n * (n - 1) / 2;
+    *pairs = plan->items ? (int64_t)(P * item_end / plan->items - P * item_begin / plan->items) : 0;
+    return SCT_OK;
+  }
   int64_t total = 0, c = 0, base = 0;
   while (c < plan->nchunks && base + rows_of_chunk(plan, c) <= item_begin) base += rows_of_chunk(plan, c++);
   int64_t r = item_begin - base;
@@ -1223,7 +1269,8 @@ extern "C" int sct_hamming_hist_allpairs_host(const uint64_t* codes, int64_t n, 
   if (rc != SCT_OK) return rc;
   uint64_t counts[129];
   SCT_HIP(hipMemcpy(counts, dcounts.p, (size_t)nc * 8, hipMemcpyDeviceToHost));
-  const int64_t expect = n * (n - 1) / 2;
+  // counts[0]: pairs counted (SUBSETS, MOMENTS) or the code count (SPECTRAL)
+  const int64_t expect = plan->scheme == SCT_ALLPAIRS_SPECTRAL ? n : n * (n - 1) / 2;
   if ((int64_t)counts[0] != (n >= 2 ? expect : 0))
     return sct::fail(SCT_E_HIP, "pair count mismatch: counted %llu, expected %lld",
                      (unsigned long long)counts[0], (long long)expect);

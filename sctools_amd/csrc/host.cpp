@@ -147,6 +147,50 @@ const MomInverse& mom_inverse() {
 
 }  // namespace
 
+// SPECTRAL counts [n, S_0..S_16] -> hist.  Ordered pairs (self pairs included) at
+// distance d: N(d) = 2^-32 sum_w S_w K_d(w), K_d(w) = [t^d] (1 + 3t)^(16-w) (1 - t)^w
+// (per 2-bit digit: 3 non-zero XOR values, characters sum to 3 if z's digit is 0, else
+// -1); hist[d] = (N(d) - n [d = 0]) / 2.  Every step is checked exact.
+static int spectral_to_hist(const uint64_t* counts, int ncounts, uint64_t* hist, int nbins) {
+  constexpr int G = 16;
+  SCT_CHECK(ncounts == G + 2 && nbins == G + 1, "SPECTRAL counts/hist hold %d/%d values (got %d, %d)",
+            G + 2, G + 1, ncounts, nbins);
+  struct Kraw {
+    __int128 k[G + 1][G + 1];  // k[d][w]
+    Kraw() {
+      for (int w = 0; w <= G; ++w) {
+        __int128 poly[G + 1] = {1};
+        for (int f = 0; f < G; ++f) {  // multiply by (1 + 3t) or (1 - t)
+          const int c = f < G - w ? 3 : -1;
+          for (int d = G; d >= 1; --d) poly[d] += c * poly[d - 1];
+        }
+        for (int d = 0; d <= G; ++d) k[d][w] = poly[d];
+      }
+    }
+  };
+  static const Kraw kraw;
+  const auto& K = kraw.k;
+  const __int128 n = counts[0];
+  __int128 total = 0;
+  for (int d = 0; d <= G; ++d) {
+    __int128 s = 0;
+    for (int w = 0; w <= G; ++w) s += K[d][w] * (__int128)counts[1 + w];
+    if (s % ((__int128)1 << 32) != 0)
+      return sct::fail(SCT_E_RANGE, "inconsistent SPECTRAL counts (bin %d not integral)", d);
+    __int128 h = s >> 32;
+    if (d == 0) h -= n;
+    if (h < 0 || (h & 1))
+      return sct::fail(SCT_E_RANGE, "inconsistent SPECTRAL counts (bin %d)", d);
+    h >>= 1;
+    if (h > (__int128)UINT64_MAX) return sct::fail(SCT_E_RANGE, "SPECTRAL bin %d out of range", d);
+    hist[d] = (uint64_t)h;
+    total += h;
+  }
+  if (total != n * (n - 1) / 2)
+    return sct::fail(SCT_E_RANGE, "inconsistent SPECTRAL counts (pair total)");
+  return SCT_OK;
+}
+
 extern "C" int sct_counts_to_hist_ex(int scheme, const uint64_t* counts, int ncounts,
                                      uint64_t* hist, int nbins) {
   SCT_CHECK(counts && hist, "NULL pointer");
@@ -154,6 +198,7 @@ extern "C" int sct_counts_to_hist_ex(int scheme, const uint64_t* counts, int nco
     SCT_CHECK(ncounts == nbins, "SUBSETS counts hold nbins values (%d != %d)", ncounts, nbins);
     return sct_counts_to_hist(counts, nbins, hist);
   }
+  if (scheme == SCT_ALLPAIRS_SPECTRAL) return spectral_to_hist(counts, ncounts, hist, nbins);
   SCT_CHECK(scheme == SCT_ALLPAIRS_MOMENTS, "unknown scheme %d", scheme);
   SCT_CHECK(ncounts == kN && nbins == kN, "MOMENTS counts/hist hold %d values (got %d, %d)", kN,
             ncounts, nbins);

@@ -303,14 +303,14 @@ def test_allpairs_partial_builds_per_rank(scheme):
 
 
 def test_allpairs_737k_properties():
-    """Full config-2 size: size-independent checks, the two count schemes agree, and
+    """Full config-2 size: size-independent checks, the three count schemes agree, and
     exact parity on a 60k-code prefix."""
     torch = pytest.importorskip("torch")
     n, L, seed = synthetic.CONFIGS[2]
     codes = synthetic.whitelist_codes(n, L, seed)
     d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
     hists = {}
-    for scheme in (_lib.SCHEME_MOMENTS, _lib.SCHEME_SUBSETS):
+    for scheme in (_lib.SCHEME_MOMENTS, _lib.SCHEME_SUBSETS, _lib.SCHEME_SPECTRAL):
         plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 32, scheme=scheme)
         assert plan.scheme == scheme
         plan.build()
@@ -318,7 +318,7 @@ def test_allpairs_737k_properties():
         plan.moments(counts.data_ptr())
         plan.count(counts.data_ptr())
         c = counts.cpu().numpy().view(np.uint64)
-        assert int(c[0]) == n * (n - 1) // 2
+        assert int(c[0]) == (n if scheme == _lib.SCHEME_SPECTRAL else n * (n - 1) // 2)
         hist = plan.counts_to_hist(c)
         assert int(hist.sum()) == n * (n - 1) // 2
         # twice gives the same (integer atomics are order independent)
@@ -328,7 +328,7 @@ def test_allpairs_737k_properties():
         assert torch.equal(counts, counts2)
         hists[scheme] = hist.tolist()
         plan.close()
-    assert hists[_lib.SCHEME_MOMENTS] == hists[_lib.SCHEME_SUBSETS]
+    assert hists[_lib.SCHEME_MOMENTS] == hists[_lib.SCHEME_SUBSETS] == hists[_lib.SCHEME_SPECTRAL]
     # the mean distance is fixed by the per-position base counts alone (first moment)
     bases = (codes[:, None] >> (2 * np.arange(16, dtype=np.uint64))) & np.uint64(3)
     agree = sum(int(np.bincount(bases[:, p].astype(np.int64), minlength=4).astype(object).dot(
@@ -367,6 +367,78 @@ def test_allpairs_moments_scheme_matches_oracle(n):
     # the one-shot host entry point picks MOMENTS for 16-base codes
     assert _lib.hamming_hist_allpairs(codes, 32).astype(np.int64).tolist() == ref.tolist()
     plan.close()
+
+
+def _spectral_hist(codes, ranges=None, chunk=None, monkeypatch=None):
+    torch = pytest.importorskip("torch")
+    if chunk is not None:
+        monkeypatch.setenv("SCT_SPECTRAL_CHUNK", str(chunk))
+    d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=_lib.SCHEME_SPECTRAL)
+    try:
+        assert plan.scheme == _lib.SCHEME_SPECTRAL and plan.ncounts == 18
+        assert plan.items == (4096 if codes.size >= 2 else 0)
+        counts = torch.zeros(plan.ncounts, dtype=torch.int64, device="cuda")
+        items = plan.items
+        if ranges is None:
+            ranges = [(0, items)]
+        credited = 0
+        for b, e in ranges:  # as separate ranks would: each builds, then counts its slices
+            plan.build(0, b, e)
+            plan.count(counts.data_ptr(), b, e)
+            credited += plan.range_pairs(b, e)
+        assert credited == codes.size * (codes.size - 1) // 2
+        c = counts.cpu().numpy().view(np.uint64)
+        assert int(c[0]) == (codes.size if codes.size >= 2 else 0)
+        return plan.counts_to_hist(c)
+    finally:
+        plan.close()
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 1025, 20_000])
+def test_allpairs_spectral_scheme_matches_oracle(n):
+    """SPECTRAL scheme (Walsh-Hadamard transform over Z_2^32, no pair enumerated) vs the
+    C oracle, with duplicates (d = 0) and complementary codes (d = 16), counted in three
+    slice ranges."""
+    codes = synthetic.whitelist_codes(max(2, n - n // 8), 16, seed=n + 7)
+    extra = []
+    if n >= 5:
+        extra = [codes[0], codes[0], codes[1] ^ np.uint64(0xAAAAAAAA), codes[1] ^ np.uint64(0xFFFFFFFF)]
+    codes = np.concatenate([codes, np.array(extra, dtype=np.uint64)])[:max(n, 2)]
+    hist = _spectral_hist(codes, [(0, 1000), (1000, 1001), (1001, 4096)])
+    assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
+
+
+def test_allpairs_spectral_crowded_low_bits(monkeypatch):
+    """3000 codes sharing their low 20 bits (one transform column holds them all: the seed's
+    per-lane register cache overflows to the global path), plus codes that differ only
+    there, with a 300-slice chunk (slices cut mid-range)."""
+    rng = np.random.default_rng(11)
+    hi = rng.integers(0, 1 << 12, 3000).astype(np.uint64)
+    codes = (hi << np.uint64(20)) | np.uint64(0x5A5A5)
+    codes = np.concatenate([codes, codes[:20] ^ np.uint64(0xFFFFF), rng.integers(0, 1 << 32, 50).astype(np.uint64)])
+    hist = _spectral_hist(codes, [(0, 4096)], chunk=300, monkeypatch=monkeypatch)
+    assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
+
+
+def test_allpairs_spectral_is_auto_for_large_whitelists():
+    """The one-shot host entry point resolves AUTO to SPECTRAL at config-5 scale and agrees
+    with the MOMENTS count kernel on a 1.6M-code whitelist."""
+    torch = pytest.importorskip("torch")
+    codes = synthetic.whitelist_codes(1_600_000, 16, 99)
+    d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
+    auto = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32)
+    assert auto.scheme == _lib.SCHEME_SPECTRAL
+    auto.close()
+    hs = _lib.hamming_hist_allpairs(codes, 32)
+    mom = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=_lib.SCHEME_MOMENTS)
+    mom.build()
+    counts = torch.zeros(mom.ncounts, dtype=torch.int64, device="cuda")
+    mom.moments(counts.data_ptr())
+    mom.count(counts.data_ptr())
+    hm = mom.counts_to_hist(counts.cpu().numpy().view(np.uint64))
+    mom.close()
+    assert hs.tolist() == hm.tolist()
 
 
 # ---------------------------------------------------------------- nearest whitelist

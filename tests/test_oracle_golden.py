@@ -162,3 +162,74 @@ def test_moments_solver_rejects_inconsistent_counts():
     c[14] += 1  # M_1 off by one: no integral histogram
     with pytest.raises(ValueError):
         _lib.counts_to_hist(c, _lib.SCHEME_MOMENTS, 17)
+
+
+# ---------------------------------------------------------------- SPECTRAL scheme identities
+def _pair_hist_digits(codes, G):
+    h = [0] * (G + 1)
+    for a, b in itertools.combinations([int(c) for c in codes], 2):
+        x = a ^ b
+        h[sum(1 for i in range(G) if (x >> (2 * i)) & 3)] += 1
+    return h
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_spectral_identity_small_space(seed):
+    """The SPECTRAL scheme's algebra, checked with an explicit Walsh-Hadamard transform in a
+    space small enough for numpy (G = 5 bases, 2^10 points): S_w = sum over z with w
+    non-zero digits of F(z)^2, then N(d) = 2^-2G sum_w S_w K_d(w) and (N(d) - n[d=0]) / 2
+    equal the brute-force pair histogram (duplicates included)."""
+    G = 5
+    rng = np.random.default_rng(seed)
+    codes = rng.integers(0, 1 << (2 * G), 60 + 20 * seed)
+    codes = np.concatenate([codes, codes[:7]])  # duplicates: d = 0 pairs
+    f = np.bincount(codes, minlength=1 << (2 * G)).astype(np.int64)
+    H = np.array([[1]])
+    for _ in range(2 * G):
+        H = np.block([[H, H], [H, -H]])
+    F = H @ f
+    z = np.arange(1 << (2 * G))
+    wt = np.array([sum(1 for i in range(G) if (int(v) >> (2 * i)) & 3) for v in z])
+    S = [int((F[wt == w] ** 2).sum()) for w in range(G + 1)]
+    K = O.krawtchouk4(G)
+    n = codes.size
+    got = []
+    for d in range(G + 1):
+        N = sum(S[w] * K[d][w] for w in range(G + 1))
+        assert N % (1 << (2 * G)) == 0
+        N //= 1 << (2 * G)
+        got.append((N - (n if d == 0 else 0)) // 2)
+    assert got == _pair_hist_digits(codes, G)
+    # and the forward map the tests use gives the same S
+    assert O.spectral_counts_from_hist(got, n).tolist() == [n] + S
+
+
+def test_spectral_counts_invert_on_reference_histograms(golden, golden_10k):
+    """The 18 SPECTRAL counts of the reference's golden histograms invert exactly through
+    the library's host Krawtchouk transform (no GPU)."""
+    wl = golden["whitelist_1k"]
+    n1 = len(wl["codes"])
+    assert _lib.counts_to_hist(O.spectral_counts_from_hist(wl["hist"], n1),
+                               _lib.SCHEME_SPECTRAL).tolist() == wl["hist"]
+    h10 = golden_10k["hist"]
+    assert _lib.counts_to_hist(O.spectral_counts_from_hist(h10, golden_10k["n"]),
+                               _lib.SCHEME_SPECTRAL, 17).tolist() == list(h10)
+
+
+def test_spectral_rejects_inconsistent_counts():
+    hist = [0, 0, 0, 1, 0, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0]  # 3 codes
+    c = O.spectral_counts_from_hist(hist, 3)
+    assert _lib.counts_to_hist(c, _lib.SCHEME_SPECTRAL).tolist() == hist
+    for i, delta in ((4, 1), (0, 1), (17, 1 << 32)):
+        bad = c.copy()
+        bad[i] += np.uint64(delta)
+        with pytest.raises(ValueError):
+            _lib.counts_to_hist(bad, _lib.SCHEME_SPECTRAL)
+
+
+def test_geometry_picks_spectral_for_large_whitelists():
+    """Host-only: AUTO resolves to SPECTRAL at 16 bases from SCT_SPECTRAL_MIN_N codes
+    (default 1.5M): 4096 transform slices are the work items."""
+    assert _lib.allpairs_geometry(3_700_000, 32)["items"] == 4096
+    assert _lib.allpairs_geometry(737_280, 32)["items"] != 4096
+    assert _lib.allpairs_geometry(3_700_000, 40)["items"] != 4096  # 20 bases: SUBSETS
