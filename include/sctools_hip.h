@@ -133,7 +133,7 @@ int sct_hamming_pairs_host(int kind, const uint64_t* a, const uint64_t* b, int64
  *   comes from the Walsh-Hadamard transform F of the codes' multiplicity over Z_2^32:
  *   d_counts[1+w] += S_w = sum of F(z)^2 over the z with w non-zero 2-bit digits,
  *   w = 0..16, and d_counts[0] += n once (by the range holding item 0).  ncounts = 18.
- *   The items are the 4096 transform slices (z >> 20); the cost of a slice does not
+ *   The items are the 2^18 transform slices (z >> 14); the cost of a slice does not
  *   depend on n, so AUTO picks this scheme for large whitelists.  Only
  *   the counts of the whole job invert (host: Krawtchouk transform, checked exact).
  *

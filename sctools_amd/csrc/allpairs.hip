@@ -976,7 +976,7 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
     p->ncounts = sct_spectral::kNCounts;
     p->items = n >= 2 ? sct_spectral::kSlices : 0;
     const char* c = getenv("SCT_SPECTRAL_CHUNK");
-    const int rc = sct_spectral::create(p->spec, n, c ? atoll(c) : 1024, cus);
+    const int rc = sct_spectral::create(p->spec, p->d_codes, n, c ? atoll(c) : 65536, cus);
     if (rc != SCT_OK) return cleanup(rc);
     *plan = p;
     return SCT_OK;

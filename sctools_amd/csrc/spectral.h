@@ -8,25 +8,29 @@
 namespace sct_spectral {
 
 constexpr int kSpaceBits = 32;                 // 16 bases: codes are points of Z_2^32
-constexpr int kLoBits = 20;                    // element index inside a slice
-constexpr int kSlices = 1 << (kSpaceBits - kLoBits);  // work items: z >> 20
+constexpr int kLoBits = 14;                    // element index inside a slice (one LDS tile)
+constexpr int kSlices = 1 << (kSpaceBits - kLoBits);  // work items: z >> 14
 constexpr int kNCounts = 1 + 17;               // [n, S_0..S_16]
 
 // Device state of a SPECTRAL plan (owned by sct_allpairs_plan).
 struct State {
   int64_t n = 0;
-  uint64_t* d_sorted = nullptr;  // codes sorted by their low 20 bits
-  uint16_t* d_hi = nullptr;      // code >> 20, in that order
-  uint32_t* d_off = nullptr;     // [2^20 + 1] first code of each low-20-bit value
-  int32_t* d_buf = nullptr;      // chunk slices x 2^20 transform values
+  uint64_t* d_sorted = nullptr;  // codes sorted by their low 14 bits
+  uint32_t* d_off = nullptr;     // [2^14 + 1] first code of each low-14-bit column
+  uint32_t* d_gofs = nullptr;    // [2^14 + 1] first 32-code group of each column
+  uint32_t* d_planes = nullptr;  // [groups][18] bit planes of the groups' code >> 14
+  int64_t max_groups = 0;
+  int elem_bytes = 1;            // seed -> tile intermediate: int8 / int16 / int32
+  void* d_buf = nullptr;         // chunk slices x 2^14 seed values
   int64_t chunk = 0;             // slices per pass
   void* d_sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
-  int grid = 0;                  // persistent grid of the square/reduce pass
+  int grid = 0;                  // persistent grid of the tile kernel
 };
 
-// allocate (chunk = slices held in HBM at once); returns an SCT_* code
-int create(State& st, int64_t n, int64_t chunk, int cus);
+// allocate (chunk = slices held in HBM at once) and size the intermediate from the
+// codes' densest column; returns an SCT_* code
+int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus);
 void destroy(State& st);
 // sort + split the codes (any slice range needs all of them)
 int build(State& st, const uint64_t* d_codes, hipStream_t s);

@@ -7,14 +7,17 @@
 //   polynomial.  The device computes S_w = sum_{wt(z) = w} F(z)^2 (17 uint64); the host
 //   (sct_counts_to_hist_ex) applies K and halves: hist[d] = (N(d) - n [d = 0]) / 2.
 //
-// Work does not depend on n: 2^32 int32 transform values, 64 GB of HBM traffic per
-// job, cut into 4096 slices of 2^20 values (z >> 20), the plan's work items.  Per slice:
-//   seed      z's high 12 bits, straight from the codes (F's inner sums are short:
-//             ~n / 2^20 codes share each low-20-bit value) -> write 4 MB
-//   tile      butterflies over bits 0..13 in LDS (64 KB contiguous tiles) -> r+w 8 MB
-//   square    butterflies over bits 14..19 in registers, F^2 binned by digit weight
-//             -> read 4 MB, no write
-// Exact: |F| <= n < 2^31 in int32, F^2 and S_w in uint64 (S_w <= 2^32 sum f^2).
+// z = (slice z >> 14, column z & 0x3FFF); the 2^18 slices are the plan's work items.
+//   seed   F's partial sums over the high 18 bits, per column, from bit planes of the
+//          column's codes: a Gray-code walk over 64 slices costs one XOR and one
+//          popcount per 32 codes per value.  |seed| <= codes in the column, so the
+//          values go to HBM as int8 (int16 / int32 for denser columns): 16 KB per slice
+//   tile   reads a slice back, butterflies over the 14 column bits (registers + LDS),
+//          F^2 binned by digit weight; writes nothing
+// 8 GB of HBM traffic per job at int8, whatever n is.  Exact: |F| <= n < 2^31 in int32,
+// F^2 and S_w in uint64 (S_w <= 2^32 sum f^2).
+#include <algorithm>
+
 #include <hipcub/hipcub.hpp>
 
 #include "sct_common.h"
@@ -23,12 +26,10 @@
 namespace sct_spectral {
 namespace {
 
-constexpr int kLo = 1 << kLoBits;
-constexpr int kTileBits = 14;  // tile pass: lo bits 0..13
-constexpr int kTile = 1 << kTileBits;
-constexpr int kTilesPerSlice = kLo / kTile;  // 64 = the square pass's register transform
-constexpr int kSeedZ = 64;     // slices per seed workgroup (16 per wave)
-constexpr int kRegCodes = 8;   // per-lane codes held in registers by the seed
+constexpr int kLo = 1 << kLoBits;         // columns (= tile values)
+constexpr int kHiBits = kSpaceBits - kLoBits;  // 18 bit planes
+constexpr int kWalk = 64;                 // slices per wave in the seed's Gray walk
+constexpr int kWalkBits = 6;
 
 // non-zero 2-bit digits of z
 __device__ __forceinline__ int digit_weight(uint32_t z) {
@@ -38,6 +39,15 @@ constexpr int digit_weight_c(uint32_t z) {
   int w = 0;
   for (; z; z >>= 2) w += (z & 3) != 0;
   return w;
+}
+constexpr int gray(int i) { return i ^ (i >> 1); }
+constexpr int ctz_c(int i) {
+  int k = 0;
+  while (!(i & 1)) {
+    i >>= 1;
+    ++k;
+  }
+  return k;
 }
 
 // in-register WHT of N values
@@ -54,119 +64,215 @@ __device__ __forceinline__ void wht(int32_t* x) {
       }
 }
 
-// off[k] = first index whose low 20 bits are >= k (k = 0..2^20), hi[i] = sorted[i] >> 20
-__global__ void split_kernel(const uint64_t* __restrict__ sorted, int64_t n, uint16_t* __restrict__ hi,
-                             uint32_t* __restrict__ off) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t < n) hi[t] = (uint16_t)(sorted[t] >> kLoBits);
-  if (t <= kLo) {
-    int64_t a = 0, b = n;
-    while (a < b) {
-      const int64_t m = (a + b) >> 1;
-      if ((int64_t)(sorted[m] & (kLo - 1)) < t) a = m + 1;
-      else b = m;
-    }
-    off[t] = (uint32_t)a;
+// off[c] = first sorted index whose column (low 14 bits) is >= c, c = 0..2^14
+__global__ void offsets_kernel(const uint64_t* __restrict__ sorted, int64_t n, uint32_t* __restrict__ off) {
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (c > kLo) return;
+  int64_t a = 0, b = n;
+  while (a < b) {
+    const int64_t m = (a + b) >> 1;
+    if ((int64_t)(sorted[m] & (kLo - 1)) < c) a = m + 1;
+    else b = m;
   }
+  off[c] = (uint32_t)a;
 }
 
-// buf[(z - z0) 2^20 + lo] = sum over codes c with c & (2^20-1) = lo of (-1)^popc((c >> 20) & z)
-// A wave holds 64 consecutive lo (256 B rows) and loops over 16 slices.
-__global__ __launch_bounds__(256) void seed_kernel(const uint16_t* __restrict__ hi,
-                                                   const uint32_t* __restrict__ off, int z0, int z1,
-                                                   int32_t* __restrict__ buf) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int lo = blockIdx.x * 64 + lane;
-  const uint32_t b = off[lo];
-  const int cnt = (int)(off[lo + 1] - b);
-  int wmax = cnt;
-#pragma unroll
-  for (int s = 32; s; s >>= 1) wmax = max(wmax, __shfl_xor(wmax, s));
-  uint32_t h[kRegCodes];
-#pragma unroll
-  for (int j = 0; j < kRegCodes; ++j) h[j] = j < cnt ? hi[b + j] : 0u;  // 0: parity 0
-  const int zb = z0 + (int)blockIdx.y * kSeedZ;
-  const int ze = min(zb + kSeedZ, z1);
-  for (int z = zb + wave; z < ze; z += 4) {
-    int par = 0;
-#pragma unroll
-    for (int j = 0; j < kRegCodes; ++j)
-      if (j < wmax) par += __popc(h[j] & (uint32_t)z) & 1;
-    for (int j = kRegCodes; j < wmax; ++j)  // crowded low-bit values only
-      if (j < cnt) par += __popc((uint32_t)hi[b + j] & (uint32_t)z) & 1;
-    buf[(int64_t)(z - z0) * kLo + lo] = cnt - 2 * par;
+// gofs[c] = sum over columns c' < c of ceil(m(c') / 32); one workgroup of 256
+__global__ __launch_bounds__(256) void group_offsets_kernel(const uint32_t* __restrict__ off,
+                                                            uint32_t* __restrict__ gofs) {
+  __shared__ uint32_t part[256];
+  constexpr int per = kLo / 256;
+  const int t = threadIdx.x;
+  uint32_t s = 0;
+  for (int k = 0; k < per; ++k) {
+    const int c = t * per + k;
+    s += (off[c + 1] - off[c] + 31) / 32;
   }
+  part[t] = s;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {  // inclusive Hillis-Steele scan
+    const uint32_t v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - s;
+  for (int k = 0; k < per; ++k) {
+    const int c = t * per + k;
+    gofs[c] = run;
+    run += (off[c + 1] - off[c] + 31) / 32;
+  }
+  if (t == 255) gofs[kLo] = run;
 }
 
-// LDS word of tile element i: 4-word groups of a 64-word row XOR-swizzled by the row,
-// so row-parallel (phase 2) b128 reads take the minimum 4 passes and every
-// column-parallel access is conflict-free.
-__device__ __forceinline__ int swz(int i) { return i ^ (((i >> 6) & 15) << 2); }
+// planes[k * max_groups + g] bit j = bit k of (code >> 14) of the j-th code of group g
+__global__ void planes_kernel(const uint64_t* __restrict__ sorted, const uint32_t* __restrict__ off,
+                              const uint32_t* __restrict__ gofs, int64_t max_groups,
+                              uint32_t* __restrict__ planes) {
+  const int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (g >= (int64_t)gofs[kLo]) return;
+  int a = 0, b = kLo;  // column c: gofs[c] <= g < gofs[c + 1]
+  while (b - a > 1) {
+    const int m = (a + b) >> 1;
+    if (gofs[m] <= (uint32_t)g) a = m;
+    else b = m;
+  }
+  const uint32_t first = off[a] + 32u * ((uint32_t)g - gofs[a]);
+  const uint32_t last = min(first + 32u, off[a + 1]);
+  uint32_t p[kHiBits];
+#pragma unroll
+  for (int k = 0; k < kHiBits; ++k) p[k] = 0;
+  for (uint32_t i = first; i < last; ++i) {
+    const uint32_t h = (uint32_t)(sorted[i] >> kLoBits), bit = 1u << (i - first);
+#pragma unroll
+    for (int k = 0; k < kHiBits; ++k) p[k] |= (h >> k) & 1u ? bit : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kHiBits; ++k) planes[k * max_groups + g] = p[k];
+}
 
-// WHT over bits 0..13 of each 2^14-value tile, in place.
-__global__ __launch_bounds__(256) void tile_kernel(int32_t* __restrict__ buf) {
-  __shared__ int32_t lds[kTile];
-  int32_t* t = buf + (int64_t)blockIdx.x * kTile;
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// Value type of the seed -> tile intermediate: |seed| <= codes in the column, so the
+// densest column decides (int8 for whitelists up to ~1.2M random barcodes).
+template <typename T>
+struct Chunk {
+  static constexpr int kVals = 16 / sizeof(T);                  // columns per 16-B chunk
+  static constexpr int kLog = sizeof(T) == 1 ? 4 : (sizeof(T) == 2 ? 3 : 2);
+  static constexpr int kPerThread = 64 / kVals;                 // chunks per tile thread
+};
+
+// Position of column c inside a slice row of the intermediate.  Chosen so that the tile
+// kernel's thread t, reading 16-B chunks at t*kVals + j*2^(kLog+8), receives the columns
+// with bits 4..11 = t and registers q = column bits 0..3 + 16 * bits 12, 13, whatever T is.
+template <typename T>
+__device__ __forceinline__ int column_pos(int c) {
+  constexpr int L = Chunk<T>::kLog;
+  return (c & ((1 << L) - 1)) | (((c >> 4) & 255) << L) | (((c >> L) & ((16 >> L) - 1)) << (L + 8)) |
+         ((c >> 12) << 12);
+}
+
+// buf[(z - z0) 2^14 + pos(c)] = sum over codes x of column c of (-1)^popc((x >> 14) & z)
+//                             = m(c) - 2 sum over groups of popc(XOR of the planes of z's bits).
+// A workgroup owns 256 columns and one 64-slice walk: each lane walks its column in Gray
+// order (one XOR per step from registers), the 64 x 256 values are staged in LDS and
+// written as 16-B chunks of slice rows.
+template <typename T>
+__global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ planes,
+                                                   const uint32_t* __restrict__ gofs,
+                                                   const uint32_t* __restrict__ off, int64_t max_groups,
+                                                   int z0, int z1, T* __restrict__ buf) {
+  __shared__ T stage[kWalk * 256];
   const int tid = threadIdx.x;
-  int32_t x[64];
-  // phase 1: bits 8..13 (thread = bits 0..7)
+  const int zblk = (z0 & ~(kWalk - 1)) + (int)blockIdx.y * kWalk;
+  const int c0 = blockIdx.x * 256, c = c0 + tid;
+  const int m = (int)(off[c + 1] - off[c]);
+  const uint32_t g0 = gofs[c];
+  const int ng = (int)(gofs[c + 1] - g0);
+  int wng = ng;
 #pragma unroll
-  for (int k = 0; k < 64; ++k) x[k] = __builtin_nontemporal_load(t + k * 256 + tid);
-  wht<64>(x);
+  for (int s = 32; s; s >>= 1) wng = max(wng, __shfl_xor(wng, s));
+  int acc[kWalk];
 #pragma unroll
-  for (int k = 0; k < 64; ++k) lds[swz(k * 256 + tid)] = x[k];
-  __syncthreads();
-  // phase 2: bits 0..5 (thread = bits 6..13)
+  for (int i = 0; i < kWalk; ++i) acc[i] = 0;
+  for (int g = 0; g < wng; ++g) {
+    uint32_t p[kHiBits];
 #pragma unroll
-  for (int j = 0; j < 64; j += 4) {
-    const int4 v = *reinterpret_cast<const int4*>(lds + swz(tid * 64 + j));
-    x[j] = v.x;
-    x[j + 1] = v.y;
-    x[j + 2] = v.z;
-    x[j + 3] = v.w;
+    for (int k = 0; k < kHiBits; ++k) p[k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = kWalkBits; k < kHiBits; ++k)
+      if ((zblk >> k) & 1) x ^= p[k];
+    acc[0] += __popc(x);
+#pragma unroll
+    for (int i = 1; i < kWalk; ++i) {
+      x ^= p[ctz_c(i)];
+      acc[gray(i)] += __popc(x);
+    }
   }
-  wht<64>(x);
 #pragma unroll
-  for (int j = 0; j < 64; j += 4)
-    *reinterpret_cast<int4*>(lds + swz(tid * 64 + j)) = make_int4(x[j], x[j + 1], x[j + 2], x[j + 3]);
+  for (int i = 0; i < kWalk; ++i) stage[i * 256 + tid] = (T)(m - 2 * acc[i]);
   __syncthreads();
-  // phase 3: bits 6, 7 (thread = bits 0..5 and 8, 9; loop over bits 10..13)
-  const int l = tid & 63, w = tid >> 6;
+  constexpr int V = Chunk<T>::kVals, per_row = 256 / V;
 #pragma unroll
-  for (int c = 0; c < 16; ++c)
-#pragma unroll
-    for (int a = 0; a < 4; ++a) x[c * 4 + a] = lds[swz(c * 1024 + w * 256 + a * 64 + l)];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) wht<4>(x + c * 4);
-#pragma unroll
-  for (int c = 0; c < 16; ++c)
-#pragma unroll
-    for (int a = 0; a < 4; ++a) t[c * 1024 + w * 256 + a * 64 + l] = x[c * 4 + a];
+  for (int r = 0; r < kWalk * per_row / 256; ++r) {
+    const int k = tid + 256 * r, i = k / per_row, ch = k % per_row;
+    const int z = zblk + i;
+    if (z < z0 || z >= z1) continue;
+    const uint4 v = *reinterpret_cast<const uint4*>(stage + i * 256 + ch * V);
+    *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + ch * V)) = v;
+  }
 }
 
-// WHT over bits 14..19, then S_w += F^2 by digit weight w; slices [z0, z0 + nslices).
-// Persistent: workgroups stride over (slice, 256-column) units; 17 global atomics each.
-__global__ __launch_bounds__(256) void square_kernel(const int32_t* __restrict__ buf, int z0,
-                                                     int nslices,
-                                                     unsigned long long* __restrict__ counts) {
+// LDS word of column e in the tile kernel: bits 2..5 XORed with bits 6, 7, 10, 11, so that
+// phase 1 (b128, lanes = e bits 4..9) and phase 3 (b128, same lanes) take the minimum 4
+// passes and phase 2 (b32, lanes = e bits 0..3, 10, 11) is conflict-free.
+__device__ __forceinline__ int swz(int e) { return e ^ (((e >> 6) & 3) << 2) ^ (((e >> 10) & 3) << 4); }
+
+// Per slice: WHT over the 14 column bits, then S_w += F^2 by digit weight.  Persistent:
+// workgroups stride over the chunk's slices; 17 global atomics per workgroup.
+//   phase 1  registers q = e bits 0..3 + 16 * (12, 13); thread = e bits 4..11
+//   phase 2  registers = e bits 4..9;                 thread = e bits 0..3, 10..13
+//   phase 3  registers = e bits 0..3 + 16 * (10, 11); thread = e bits 4..9, 12, 13
+// Phase 3's register and thread bits are whole 2-bit digits: the digit weight of an
+// element is a thread constant plus a compile-time one.
+template <typename T>
+__global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, int z0, int nslices,
+                                                   unsigned long long* __restrict__ counts) {
+  __shared__ int32_t lds[kLo];
   __shared__ unsigned long long bins[17];
+  constexpr int V = Chunk<T>::kVals, L = Chunk<T>::kLog;
   const int tid = threadIdx.x;
   if (tid < 17) bins[tid] = 0;
-  __syncthreads();
-  const int64_t units = (int64_t)nslices * (kTile / 256);
-  for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
-    const int s = (int)(u / (kTile / 256));
-    const int col = (int)(u % (kTile / 256)) * 256 + tid;  // lo bits 0..13
-    const int32_t* p = buf + (int64_t)s * kLo + col;
-    int32_t x[kTilesPerSlice];
+  const int t2 = (tid & 15) | ((tid >> 4) << 10);                   // phase-2 e base
+  const int t3 = ((tid & 63) << 4) | ((tid >> 6) << 12);            // phase-3 e base
+  const int wt3 = digit_weight((uint32_t)t3);
+  for (int s = blockIdx.x; s < nslices; s += gridDim.x) {
+    const T* row = buf + (int64_t)s * kLo;
+    int32_t x[64];
 #pragma unroll
-    for (int m = 0; m < kTilesPerSlice; ++m) x[m] = __builtin_nontemporal_load(p + m * kTile);
-    wht<kTilesPerSlice>(x);
+    for (int j = 0; j < Chunk<T>::kPerThread; ++j) {
+      const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(row + tid * V + (j << (L + 8))));
+      const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+      for (int r = 0; r < V; ++r) x[j * V + r] = e[r];
+    }
+    wht<64>(x);
+    __syncthreads();  // the previous slice's phase-3 reads are done
+#pragma unroll
+    for (int q = 0; q < 64; q += 4)
+      *reinterpret_cast<int4*>(lds + swz((q & 15) | (tid << 4) | ((q >> 4) << 12))) =
+          make_int4(x[q], x[q + 1], x[q + 2], x[q + 3]);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 64; ++q) x[q] = lds[swz(t2 | (q << 4))];
+    wht<64>(x);
+#pragma unroll
+    for (int q = 0; q < 64; ++q) lds[swz(t2 | (q << 4))] = x[q];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 64; q += 4) {
+      const int4 v = *reinterpret_cast<const int4*>(lds + swz(t3 | (q & 15) | ((q >> 4) << 10)));
+      x[q] = v.x;
+      x[q + 1] = v.y;
+      x[q + 2] = v.z;
+      x[q + 3] = v.w;
+    }
+#pragma unroll
+    for (int lo = 0; lo < 16; ++lo) {  // butterflies over e bits 10, 11 (q bits 4, 5)
+      int32_t y[4] = {x[lo], x[lo + 16], x[lo + 32], x[lo + 48]};
+      wht<4>(y);
+      x[lo] = y[0];
+      x[lo + 16] = y[1];
+      x[lo + 32] = y[2];
+      x[lo + 48] = y[3];
+    }
     unsigned long long acc[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int m = 0; m < kTilesPerSlice; ++m)
-      acc[digit_weight_c(m)] += (unsigned long long)((int64_t)x[m] * x[m]);
-    const int w0 = digit_weight(((uint32_t)(z0 + s) << kLoBits) | (uint32_t)col);
+    for (int q = 0; q < 64; ++q)
+      acc[digit_weight_c((uint32_t)(q & 15)) + digit_weight_c((uint32_t)(q >> 4))] +=
+          (unsigned long long)((int64_t)x[q] * x[q]);
+    const int w0 = digit_weight((uint32_t)(z0 + s)) + wt3;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (acc[k]) atomicAdd(&bins[w0 + k], acc[k]);
@@ -175,27 +281,67 @@ __global__ __launch_bounds__(256) void square_kernel(const int32_t* __restrict__
   if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
 }
 
+__global__ void max_column_kernel(const uint32_t* __restrict__ off, unsigned* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < kLo) atomicMax(out, off[c + 1] - off[c]);
+}
+
 __global__ void add_kernel(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
+
+template <typename T>
+int launch_chunk(const State& st, int z0, int z1, unsigned long long* counts, hipStream_t s) {
+  T* buf = reinterpret_cast<T*>(st.d_buf);
+  const int walks = (z1 - (z0 & ~(kWalk - 1)) + kWalk - 1) / kWalk;
+  hipLaunchKernelGGL(seed_kernel<T>, dim3(kLo / 256, (unsigned)walks), dim3(256), 0, s, st.d_planes, st.d_gofs,
+                     st.d_off, st.max_groups, z0, z1, buf);
+  SCT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(tile_kernel<T>, dim3((unsigned)std::min(st.grid, z1 - z0)), dim3(256), 0, s, buf, z0,
+                     z1 - z0, counts);
+  SCT_LAUNCH_CHECK();
+  return SCT_OK;
+}
 
 }  // namespace
 
-int create(State& st, int64_t n, int64_t chunk, int cus) {
+int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus) {
   st.n = n;
-  st.chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, kSlices));
-  st.grid = std::max(1, cus) * 8;
+  st.chunk = std::max<int64_t>(kWalk, std::min<int64_t>(chunk, kSlices));
+  st.grid = std::max(1, cus) * 2;  // 64 KB of LDS per tile workgroup: two per CU
   if (n < 2) return SCT_OK;
   SCT_HIP(hipMalloc(&st.d_sorted, (size_t)n * 8));
-  SCT_HIP(hipMalloc(&st.d_hi, (size_t)n * 2));
   SCT_HIP(hipMalloc(&st.d_off, (size_t)(kLo + 1) * 4));
-  SCT_HIP(hipMalloc(&st.d_buf, (size_t)st.chunk * kLo * 4));
   SCT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, st.sort_tmp_bytes, (const uint64_t*)nullptr,
                                             (uint64_t*)nullptr, (int)n, 0, kLoBits));
   SCT_HIP(hipMalloc(&st.d_sort_tmp, std::max<size_t>(st.sort_tmp_bytes, 16)));
+  // the densest column bounds |seed| and so the intermediate's width (the codes are
+  // fixed for the plan's life)
+  size_t bytes = st.sort_tmp_bytes;
+  SCT_HIP(hipcub::DeviceRadixSort::SortKeys(st.d_sort_tmp, bytes, d_codes, st.d_sorted, (int)n, 0, kLoBits));
+  hipLaunchKernelGGL(offsets_kernel, dim3((unsigned)sct::ceil_div(kLo + 1, 256)), dim3(256), 0, 0,
+                     st.d_sorted, n, st.d_off);
+  SCT_LAUNCH_CHECK();
+  sct::DevBuf dmax;
+  SCT_HIP(dmax.alloc(4));
+  SCT_HIP(hipMemset(dmax.p, 0, 4));
+  hipLaunchKernelGGL(max_column_kernel, dim3(kLo / 256), dim3(256), 0, 0, st.d_off, (unsigned*)dmax.p);
+  SCT_LAUNCH_CHECK();
+  unsigned maxm = 0;
+  SCT_HIP(hipMemcpy(&maxm, dmax.p, 4, hipMemcpyDeviceToHost));
+  st.elem_bytes = maxm <= 127 ? 1 : (maxm <= 32767 ? 2 : 4);
+  if (const char* w = getenv("SCT_SPECTRAL_BYTES")) {  // test hook: wider than needed
+    const int b = atoi(w);
+    if ((b == 2 || b == 4) && b > st.elem_bytes) st.elem_bytes = b;
+  }
+  st.max_groups = sct::ceil_div(n, 32) + kLo;
+  SCT_HIP(hipMalloc(&st.d_gofs, (size_t)(kLo + 1) * 4));
+  SCT_HIP(hipMalloc(&st.d_planes, (size_t)st.max_groups * kHiBits * 4));
+  SCT_HIP(hipMalloc(&st.d_buf, (size_t)st.chunk * kLo * st.elem_bytes));
   return SCT_OK;
 }
 
 void destroy(State& st) {
-  for (void* p : {(void*)st.d_sorted, (void*)st.d_hi, (void*)st.d_off, (void*)st.d_buf, st.d_sort_tmp})
+  for (void* p : {(void*)st.d_sorted, (void*)st.d_off, (void*)st.d_gofs, (void*)st.d_planes, st.d_buf,
+                  st.d_sort_tmp})
     if (p) (void)hipFree(p);
   st = State();
 }
@@ -205,9 +351,13 @@ int build(State& st, const uint64_t* d_codes, hipStream_t s) {
   size_t bytes = st.sort_tmp_bytes;
   SCT_HIP(hipcub::DeviceRadixSort::SortKeys(st.d_sort_tmp, bytes, d_codes, st.d_sorted, (int)st.n, 0,
                                             kLoBits, s));
-  const int64_t threads = std::max<int64_t>(st.n, kLo + 1);
-  hipLaunchKernelGGL(split_kernel, dim3((unsigned)sct::ceil_div(threads, 256)), dim3(256), 0, s,
-                     st.d_sorted, st.n, st.d_hi, st.d_off);
+  hipLaunchKernelGGL(offsets_kernel, dim3((unsigned)sct::ceil_div(kLo + 1, 256)), dim3(256), 0, s,
+                     st.d_sorted, st.n, st.d_off);
+  SCT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(group_offsets_kernel, dim3(1), dim3(256), 0, s, st.d_off, st.d_gofs);
+  SCT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(planes_kernel, dim3((unsigned)sct::ceil_div(st.max_groups, 256)), dim3(256), 0, s,
+                     st.d_sorted, st.d_off, st.d_gofs, st.max_groups, st.d_planes);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
@@ -218,15 +368,10 @@ int count(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_count
   if (st.n < 2 || z_begin == z_end) return SCT_OK;
   for (int64_t z0 = z_begin; z0 < z_end; z0 += st.chunk) {
     const int z1 = (int)std::min<int64_t>(z_end, z0 + st.chunk);
-    const int ns = z1 - (int)z0;
-    hipLaunchKernelGGL(seed_kernel, dim3(kLo / 64, (unsigned)sct::ceil_div(ns, kSeedZ)), dim3(256), 0, s,
-                       st.d_hi, st.d_off, (int)z0, z1, st.d_buf);
-    SCT_LAUNCH_CHECK();
-    hipLaunchKernelGGL(tile_kernel, dim3((unsigned)(ns * kTilesPerSlice)), dim3(256), 0, s, st.d_buf);
-    SCT_LAUNCH_CHECK();
-    const int grid = (int)std::min<int64_t>(st.grid, (int64_t)ns * (kTile / 256));
-    hipLaunchKernelGGL(square_kernel, dim3(grid), dim3(256), 0, s, st.d_buf, (int)z0, ns, d_counts);
-    SCT_LAUNCH_CHECK();
+    const int rc = st.elem_bytes == 1   ? launch_chunk<int8_t>(st, (int)z0, z1, d_counts, s)
+                   : st.elem_bytes == 2 ? launch_chunk<int16_t>(st, (int)z0, z1, d_counts, s)
+                                        : launch_chunk<int32_t>(st, (int)z0, z1, d_counts, s);
+    if (rc != SCT_OK) return rc;
   }
   if (z_begin == 0) {
     hipLaunchKernelGGL(add_kernel, dim3(1), dim3(1), 0, s, d_counts, (unsigned long long)st.n);

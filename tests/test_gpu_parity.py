@@ -377,7 +377,7 @@ def _spectral_hist(codes, ranges=None, chunk=None, monkeypatch=None):
     plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=_lib.SCHEME_SPECTRAL)
     try:
         assert plan.scheme == _lib.SCHEME_SPECTRAL and plan.ncounts == 18
-        assert plan.items == (4096 if codes.size >= 2 else 0)
+        assert plan.items == (1 << 18 if codes.size >= 2 else 0)
         counts = torch.zeros(plan.ncounts, dtype=torch.int64, device="cuda")
         items = plan.items
         if ranges is None:
@@ -395,29 +395,31 @@ def _spectral_hist(codes, ranges=None, chunk=None, monkeypatch=None):
         plan.close()
 
 
+@pytest.mark.parametrize("width", ["1", "2", "4"])
 @pytest.mark.parametrize("n", [2, 3, 5, 1025, 20_000])
-def test_allpairs_spectral_scheme_matches_oracle(n):
+def test_allpairs_spectral_scheme_matches_oracle(n, width, monkeypatch):
     """SPECTRAL scheme (Walsh-Hadamard transform over Z_2^32, no pair enumerated) vs the
     C oracle, with duplicates (d = 0) and complementary codes (d = 16), counted in three
-    slice ranges."""
+    slice ranges; int8 / int16 / int32 seed intermediate."""
+    monkeypatch.setenv("SCT_SPECTRAL_BYTES", width)
     codes = synthetic.whitelist_codes(max(2, n - n // 8), 16, seed=n + 7)
     extra = []
     if n >= 5:
         extra = [codes[0], codes[0], codes[1] ^ np.uint64(0xAAAAAAAA), codes[1] ^ np.uint64(0xFFFFFFFF)]
     codes = np.concatenate([codes, np.array(extra, dtype=np.uint64)])[:max(n, 2)]
-    hist = _spectral_hist(codes, [(0, 1000), (1000, 1001), (1001, 4096)])
+    hist = _spectral_hist(codes, [(0, 1000), (1000, 1001), (1001, 1 << 18)])
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
 def test_allpairs_spectral_crowded_low_bits(monkeypatch):
-    """3000 codes sharing their low 20 bits (one transform column holds them all: the seed's
-    per-lane register cache overflows to the global path), plus codes that differ only
-    there, with a 300-slice chunk (slices cut mid-range)."""
+    """3000 codes sharing their low 14 bits (one transform column holds them all: 94
+    32-code groups of bit planes, an int16 intermediate), plus codes that differ only
+    there, with a 300-slice chunk (Gray walks cut by chunk seams)."""
     rng = np.random.default_rng(11)
     hi = rng.integers(0, 1 << 12, 3000).astype(np.uint64)
     codes = (hi << np.uint64(20)) | np.uint64(0x5A5A5)
     codes = np.concatenate([codes, codes[:20] ^ np.uint64(0xFFFFF), rng.integers(0, 1 << 32, 50).astype(np.uint64)])
-    hist = _spectral_hist(codes, [(0, 4096)], chunk=300, monkeypatch=monkeypatch)
+    hist = _spectral_hist(codes, [(0, 1 << 18)], chunk=300, monkeypatch=monkeypatch)
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 

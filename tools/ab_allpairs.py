@@ -1,7 +1,7 @@
 """Interleaved A/B timing of all-pairs count-kernel variants in ONE process.
 
 Variants are selected at plan creation through SCT_ALLPAIRS_VARIANT / _GRID / _GRAB and
-the count scheme (s=0 SUBSETS, s=1 MOMENTS); each round times every variant once (HIP
+the count scheme (s=0 SUBSETS, s=1 MOMENTS, s=2 SPECTRAL with chunk=slices per pass); each round times every variant once (HIP
 events on the launch stream: the count kernel, and the moments pass separately); prints
 the median and min per variant and checks that all variants give identical histograms.
 
@@ -34,8 +34,8 @@ def main():
     for v in a.variants:
         kv = dict(x.split("=") for x in v.split(","))
         os.environ["SCT_ALLPAIRS_VARIANT"] = kv.get("v", "2")
-        for key in ("grid", "grab"):
-            env = "SCT_ALLPAIRS_" + key.upper()
+        for key, env in (("grid", "SCT_ALLPAIRS_GRID"), ("grab", "SCT_ALLPAIRS_GRAB"),
+                         ("chunk", "SCT_SPECTRAL_CHUNK")):
             if key in kv:
                 os.environ[env] = kv[key]
             else:
