@@ -204,29 +204,45 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
   }
 }
 
-// LDS word of column e in the tile kernel: bits 2..5 XORed with bits 6, 7, 10, 11, so that
-// phase 1 (b128, lanes = e bits 4..9) and phase 3 (b128, same lanes) take the minimum 4
-// passes and phase 2 (b32, lanes = e bits 0..3, 10, 11) is conflict-free.
-__device__ __forceinline__ int swz(int e) { return e ^ (((e >> 6) & 3) << 2) ^ (((e >> 10) & 3) << 4); }
+// LDS word of column e in the tile kernel: bits 2, 3, 4 XORed with bits 6, 5, 10, so the
+// phase-1 b128 stores (8-lane groups: e bits 4..6 vary) and the phase-2 b32 loads (32-lane
+// groups: e bits 0..3, 10 vary) are both conflict-free.
+__device__ __forceinline__ int swz(int e) {
+  return e ^ (((e >> 6) & 1) << 2) ^ (((e >> 5) & 1) << 3) ^ (((e >> 10) & 1) << 4);
+}
+
+// Butterfly over a lane bit without LDS: v_permlane{32,16}_swap brings the partner lane's
+// value of register a into this lane's b (and b's into the partner), so the pair is
+// combined in-lane.  Afterwards the lane bit and the register bit that told a from b have
+// traded places.
+__device__ __forceinline__ void lane_butterfly32(int32_t& a, int32_t& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap((unsigned)a, (unsigned)b, false, false);
+  a = (int32_t)(r[0] + r[1]);
+  b = (int32_t)(r[0] - r[1]);
+}
+__device__ __forceinline__ void lane_butterfly16(int32_t& a, int32_t& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap((unsigned)a, (unsigned)b, false, false);
+  a = (int32_t)(r[0] + r[1]);
+  b = (int32_t)(r[0] - r[1]);
+}
 
 // Per slice: WHT over the 14 column bits, then S_w += F^2 by digit weight.  Persistent:
 // workgroups stride over the chunk's slices; 17 global atomics per workgroup.
 //   phase 1  registers q = e bits 0..3 + 16 * (12, 13); thread = e bits 4..11
-//   phase 2  registers = e bits 4..9;                 thread = e bits 0..3, 10..13
-//   phase 3  registers = e bits 0..3 + 16 * (10, 11); thread = e bits 4..9, 12, 13
-// Phase 3's register and thread bits are whole 2-bit digits: the digit weight of an
-// element is a thread constant plus a compile-time one.
+//   phase 2  registers q = e bits 4..9;  lane = e bits 0..3, 10, 11; wave = e bits 12, 13
+//   phase 3  lane bits 5, 4 (e 11, 10) by permlane swaps against q bits 1, 0 (e 5, 4):
+//            then q = (e 10, 11, 6..9), lane = e bits 0..5, wave = e bits 12, 13 -- whole
+//            2-bit digits, so an element's digit weight is thread constant + compile time.
 template <typename T>
 __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, int z0, int nslices,
                                                    unsigned long long* __restrict__ counts) {
   __shared__ int32_t lds[kLo];
   __shared__ unsigned long long bins[17];
   constexpr int V = Chunk<T>::kVals, L = Chunk<T>::kLog;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < 17) bins[tid] = 0;
-  const int t2 = (tid & 15) | ((tid >> 4) << 10);                   // phase-2 e base
-  const int t3 = ((tid & 63) << 4) | ((tid >> 6) << 12);            // phase-3 e base
-  const int wt3 = digit_weight((uint32_t)t3);
+  const int t2 = (lane & 15) | ((lane >> 4) << 10) | (wave << 12);  // phase-2 e base
+  const int wt_thread = digit_weight((uint32_t)lane | ((uint32_t)wave << 12));
   for (int s = blockIdx.x; s < nslices; s += gridDim.x) {
     const T* row = buf + (int64_t)s * kLo;
     int32_t x[64];
@@ -238,7 +254,7 @@ __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, in
       for (int r = 0; r < V; ++r) x[j * V + r] = e[r];
     }
     wht<64>(x);
-    __syncthreads();  // the previous slice's phase-3 reads are done
+    __syncthreads();  // the previous slice's phase-2 reads are done
 #pragma unroll
     for (int q = 0; q < 64; q += 4)
       *reinterpret_cast<int4*>(lds + swz((q & 15) | (tid << 4) | ((q >> 4) << 12))) =
@@ -248,31 +264,17 @@ __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, in
     for (int q = 0; q < 64; ++q) x[q] = lds[swz(t2 | (q << 4))];
     wht<64>(x);
 #pragma unroll
-    for (int q = 0; q < 64; ++q) lds[swz(t2 | (q << 4))] = x[q];
-    __syncthreads();
+    for (int q = 0; q < 64; ++q)
+      if (!(q & 2)) lane_butterfly32(x[q], x[q | 2]);  // e bit 11 <-> q bit 1 (e bit 5)
 #pragma unroll
-    for (int q = 0; q < 64; q += 4) {
-      const int4 v = *reinterpret_cast<const int4*>(lds + swz(t3 | (q & 15) | ((q >> 4) << 10)));
-      x[q] = v.x;
-      x[q + 1] = v.y;
-      x[q + 2] = v.z;
-      x[q + 3] = v.w;
-    }
-#pragma unroll
-    for (int lo = 0; lo < 16; ++lo) {  // butterflies over e bits 10, 11 (q bits 4, 5)
-      int32_t y[4] = {x[lo], x[lo + 16], x[lo + 32], x[lo + 48]};
-      wht<4>(y);
-      x[lo] = y[0];
-      x[lo + 16] = y[1];
-      x[lo + 32] = y[2];
-      x[lo + 48] = y[3];
-    }
+    for (int q = 0; q < 64; ++q)
+      if (!(q & 1)) lane_butterfly16(x[q], x[q | 1]);  // e bit 10 <-> q bit 0 (e bit 4)
     unsigned long long acc[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < 64; ++q)
-      acc[digit_weight_c((uint32_t)(q & 15)) + digit_weight_c((uint32_t)(q >> 4))] +=
+      acc[digit_weight_c((uint32_t)(q & 3)) + digit_weight_c((uint32_t)(q >> 2))] +=
           (unsigned long long)((int64_t)x[q] * x[q]);
-    const int w0 = digit_weight((uint32_t)(z0 + s)) + wt3;
+    const int w0 = digit_weight((uint32_t)(z0 + s)) + wt_thread;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (acc[k]) atomicAdd(&bins[w0 + k], acc[k]);
