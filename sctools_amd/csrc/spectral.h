@@ -25,7 +25,7 @@ struct State {
   int64_t chunk = 0;             // slices per pass
   void* d_sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
-  int grid = 0;                  // persistent grid of the tile kernel
+  int grid = 0;                  // compute units (the tile kernel's persistent grid)
 };
 
 // allocate (chunk = slices held in HBM at once) and size the intermediate from the

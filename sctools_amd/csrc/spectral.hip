@@ -17,6 +17,7 @@
 // 8 GB of HBM traffic per job at int8, whatever n is.  Exact: |F| <= n < 2^31 in int32,
 // F^2 and S_w in uint64 (S_w <= 2^32 sum f^2).
 #include <algorithm>
+#include <type_traits>
 
 #include <hipcub/hipcub.hpp>
 
@@ -152,19 +153,35 @@ __device__ __forceinline__ int column_pos(int c) {
          ((c >> 12) << 12);
 }
 
+// Byte (int8) / half (int16) transposes for the seed's store-out: p dwords hold P values of
+// consecutive slices for one column each; out[j] = the j-th values of all of them, packed.
+__device__ __forceinline__ void transpose4x4_bytes(const uint32_t* d, uint32_t* out) {
+  // d[0..3] bytes (slice 0..3) of columns 0..3  ->  out[j] = (d0.j, d1.j, d2.j, d3.j)
+  const uint32_t ab_lo = __builtin_amdgcn_perm(d[1], d[0], 0x05010400u);  // a0 b0 a1 b1
+  const uint32_t ab_hi = __builtin_amdgcn_perm(d[1], d[0], 0x07030602u);  // a2 b2 a3 b3
+  const uint32_t cd_lo = __builtin_amdgcn_perm(d[3], d[2], 0x05010400u);
+  const uint32_t cd_hi = __builtin_amdgcn_perm(d[3], d[2], 0x07030602u);
+  out[0] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u);  // a0 b0 c0 d0
+  out[1] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u);  // a1 b1 c1 d1
+  out[2] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u);
+  out[3] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
+}
+
 // buf[(z - z0) 2^14 + pos(c)] = sum over codes x of column c of (-1)^popc((x >> 14) & z)
 //                             = m(c) - 2 sum over groups of popc(XOR of the planes of z's bits).
 // A workgroup owns 256 columns and one 64-slice walk: each lane walks its column in Gray
-// order (one XOR per step from registers), the 64 x 256 values are staged in LDS and
-// written as 16-B chunks of slice rows.
+// order (one XOR per step from registers); the 64 x 256 values are staged in LDS as dwords
+// of 4 / sizeof(T) consecutive slices per column, transposed in registers and written as
+// 16-B chunks of slice rows.
 template <typename T>
 __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ planes,
                                                    const uint32_t* __restrict__ gofs,
                                                    const uint32_t* __restrict__ off, int64_t max_groups,
                                                    int z0, int z1, T* __restrict__ buf) {
-  __shared__ T stage[kWalk * 256];
+  constexpr int P = 4 / sizeof(T);          // slices per staged dword
+  constexpr int V = Chunk<T>::kVals;        // columns per 16-B output chunk
+  __shared__ uint32_t stage[(kWalk / P) * 256];
   const int tid = threadIdx.x;
-  const int zblk = (z0 & ~(kWalk - 1)) + (int)blockIdx.y * kWalk;
   const int c0 = blockIdx.x * 256, c = c0 + tid;
   const int m = (int)(off[c + 1] - off[c]);
   const uint32_t g0 = gofs[c];
@@ -172,10 +189,9 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
   int wng = ng;
 #pragma unroll
   for (int s = 32; s; s >>= 1) wng = max(wng, __shfl_xor(wng, s));
+  const int zblk = (z0 & ~(kWalk - 1)) + (int)blockIdx.y * kWalk;
   int acc[kWalk];
-#pragma unroll
-  for (int i = 0; i < kWalk; ++i) acc[i] = 0;
-  for (int g = 0; g < wng; ++g) {
+  auto walk = [&](int g, auto first) {
     uint32_t p[kHiBits];
 #pragma unroll
     for (int k = 0; k < kHiBits; ++k) p[k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
@@ -183,24 +199,69 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
 #pragma unroll
     for (int k = kWalkBits; k < kHiBits; ++k)
       if ((zblk >> k) & 1) x ^= p[k];
-    acc[0] += __popc(x);
+    if constexpr (decltype(first)::value) acc[0] = __popc(x);
+    else acc[0] += __popc(x);
 #pragma unroll
     for (int i = 1; i < kWalk; ++i) {
       x ^= p[ctz_c(i)];
-      acc[gray(i)] += __popc(x);
+      if constexpr (decltype(first)::value) acc[gray(i)] = __popc(x);
+      else acc[gray(i)] += __popc(x);
     }
+  };
+  walk(0, std::true_type());  // columns without codes: planes 0, popc 0
+  for (int g = 1; g < wng; ++g) walk(g, std::false_type());
+  // 4-dword groups of a 16-dword column block XOR-swizzled by the block, so the
+  // store-out's b128 reads of 16 consecutive columns are conflict-free
+  auto sidx = [](int row, int col) { return row * 256 + (col ^ (((col >> 6) & 3) << 2)); };
+#pragma unroll
+  for (int r = 0; r < kWalk / P; ++r) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < P; ++j)
+      w |= ((uint32_t)(m - 2 * acc[r * P + j]) & (0xFFFFFFFFu >> (32 - 8 * sizeof(T)))) << (8 * sizeof(T) * j);
+    stage[sidx(r, tid)] = w;
   }
-#pragma unroll
-  for (int i = 0; i < kWalk; ++i) stage[i * 256 + tid] = (T)(m - 2 * acc[i]);
   __syncthreads();
-  constexpr int V = Chunk<T>::kVals, per_row = 256 / V;
+  // blocks of V columns x P slices: V dwords in, P chunks out
+  constexpr int kBlocks = (kWalk / P) * (256 / V);
 #pragma unroll
-  for (int r = 0; r < kWalk * per_row / 256; ++r) {
-    const int k = tid + 256 * r, i = k / per_row, ch = k % per_row;
-    const int z = zblk + i;
-    if (z < z0 || z >= z1) continue;
-    const uint4 v = *reinterpret_cast<const uint4*>(stage + i * 256 + ch * V);
-    *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + ch * V)) = v;
+  for (int r = 0; r < kBlocks / 256; ++r) {
+    const int b = tid + 256 * r, row = b / (256 / V), cb = (b % (256 / V)) * V;
+    uint32_t d[V];
+#pragma unroll
+    for (int k = 0; k < V; k += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(stage + sidx(row, cb + k));
+      d[k] = v.x;
+      d[k + 1] = v.y;
+      d[k + 2] = v.z;
+      d[k + 3] = v.w;
+    }
+    uint32_t out[P][4];
+    if constexpr (P == 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t t[4];
+        transpose4x4_bytes(d + 4 * k, t);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) out[j][k] = t[j];
+      }
+    } else if constexpr (P == 2) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        out[0][k] = __builtin_amdgcn_perm(d[2 * k + 1], d[2 * k], 0x05040100u);
+        out[1][k] = __builtin_amdgcn_perm(d[2 * k + 1], d[2 * k], 0x07060302u);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) out[0][k] = d[k];
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int z = zblk + row * P + j;
+      if (z < z0 || z >= z1) continue;
+      *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + cb)) =
+          make_uint4(out[j][0], out[j][1], out[j][2], out[j][3]);
+    }
   }
 }
 
@@ -209,6 +270,14 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
 // groups: e bits 0..3, 10 vary) are both conflict-free.
 __device__ __forceinline__ int swz(int e) {
   return e ^ (((e >> 6) & 1) << 2) ^ (((e >> 5) & 1) << 3) ^ (((e >> 10) & 1) << 4);
+}
+
+// int16 exchange (int8 seeds): dword of the element pair e >> 1, bits 1, 2, 3 XORed with
+// e bits 6, 7, 10: the phase-1 b64 stores (16-lane groups: e bits 4..7 vary) and the
+// phase-2 u16 loads (32-lane groups: e bits 0..3, 10 vary; pairs share a dword) are
+// conflict-free.
+__device__ __forceinline__ int swz16(int e) {
+  return (e >> 1) ^ (((e >> 6) & 1) << 1) ^ (((e >> 7) & 1) << 2) ^ (((e >> 10) & 1) << 3);
 }
 
 // Butterfly over a lane bit without LDS: v_permlane{32,16}_swap brings the partner lane's
@@ -233,10 +302,15 @@ __device__ __forceinline__ void lane_butterfly16(int32_t& a, int32_t& b) {
 //   phase 3  lane bits 5, 4 (e 11, 10) by permlane swaps against q bits 1, 0 (e 5, 4):
 //            then q = (e 10, 11, 6..9), lane = e bits 0..5, wave = e bits 12, 13 -- whole
 //            2-bit digits, so an element's digit weight is thread constant + compile time.
-template <typename T>
+// ABL (ablation builds only, wrong results by design): 1 = no global loads, 2 = no LDS
+// exchange, 3 = no squares/bins, 4 = loads only.
+template <typename T, int ABL = 0>
 __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, int z0, int nslices,
                                                    unsigned long long* __restrict__ counts) {
-  __shared__ int32_t lds[kLo];
+  // int8 seeds: after phase 1 |x| <= 64 * 127 fits int16, so the exchange takes 32 KB
+  // and three workgroups share a CU
+  constexpr bool kNarrow = sizeof(T) == 1;
+  __shared__ std::conditional_t<kNarrow, int16_t, int32_t> lds[kLo];
   __shared__ unsigned long long bins[17];
   constexpr int V = Chunk<T>::kVals, L = Chunk<T>::kLog;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -246,22 +320,49 @@ __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, in
   for (int s = blockIdx.x; s < nslices; s += gridDim.x) {
     const T* row = buf + (int64_t)s * kLo;
     int32_t x[64];
+    if constexpr (ABL == 1) {
 #pragma unroll
-    for (int j = 0; j < Chunk<T>::kPerThread; ++j) {
-      const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(row + tid * V + (j << (L + 8))));
-      const T* e = reinterpret_cast<const T*>(&v);
+      for (int q = 0; q < 64; ++q) x[q] = (s * 7 + q * 3 + tid) & 127;
+    } else {
 #pragma unroll
-      for (int r = 0; r < V; ++r) x[j * V + r] = e[r];
+      for (int j = 0; j < Chunk<T>::kPerThread; ++j) {
+        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(row + tid * V + (j << (L + 8))));
+        const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+        for (int r = 0; r < V; ++r) x[j * V + r] = e[r];
+      }
+    }
+    if constexpr (ABL == 4) {
+      int32_t a = 0;
+#pragma unroll
+      for (int q = 0; q < 64; ++q) a += x[q];
+      if (a == 0x7fffffff) counts[0] = 1;
+      continue;
     }
     wht<64>(x);
-    __syncthreads();  // the previous slice's phase-2 reads are done
+    if constexpr (ABL != 2) {
+      __syncthreads();  // the previous slice's phase-2 reads are done
+      if constexpr (kNarrow) {
 #pragma unroll
-    for (int q = 0; q < 64; q += 4)
-      *reinterpret_cast<int4*>(lds + swz((q & 15) | (tid << 4) | ((q >> 4) << 12))) =
-          make_int4(x[q], x[q + 1], x[q + 2], x[q + 3]);
-    __syncthreads();
+        for (int q = 0; q < 64; q += 4)
+          *reinterpret_cast<uint2*>(lds + 2 * swz16((q & 15) | (tid << 4) | ((q >> 4) << 12))) =
+              make_uint2(((uint32_t)x[q] & 0xFFFFu) | ((uint32_t)x[q + 1] << 16),
+                         ((uint32_t)x[q + 2] & 0xFFFFu) | ((uint32_t)x[q + 3] << 16));
+        __syncthreads();
+        const int a2 = 2 * swz16(t2) + (t2 & 1);  // the map is XOR-linear in e
 #pragma unroll
-    for (int q = 0; q < 64; ++q) x[q] = lds[swz(t2 | (q << 4))];
+        for (int q = 0; q < 64; ++q) x[q] = lds[a2 ^ (2 * swz16(q << 4))];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 64; q += 4)
+          *reinterpret_cast<int4*>(lds + swz((q & 15) | (tid << 4) | ((q >> 4) << 12))) =
+              make_int4(x[q], x[q + 1], x[q + 2], x[q + 3]);
+        __syncthreads();
+        const int a2 = swz(t2);
+#pragma unroll
+        for (int q = 0; q < 64; ++q) x[q] = lds[a2 ^ swz(q << 4)];
+      }
+    }
     wht<64>(x);
 #pragma unroll
     for (int q = 0; q < 64; ++q)
@@ -269,6 +370,13 @@ __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, in
 #pragma unroll
     for (int q = 0; q < 64; ++q)
       if (!(q & 1)) lane_butterfly16(x[q], x[q | 1]);  // e bit 10 <-> q bit 0 (e bit 4)
+    if constexpr (ABL == 3) {
+      int32_t a = 0;
+#pragma unroll
+      for (int q = 0; q < 64; ++q) a ^= x[q];
+      if (a == 0x7fffffff) counts[0] = 1;
+      continue;
+    }
     unsigned long long acc[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < 64; ++q)
@@ -297,8 +405,19 @@ int launch_chunk(const State& st, int z0, int z1, unsigned long long* counts, hi
   hipLaunchKernelGGL(seed_kernel<T>, dim3(kLo / 256, (unsigned)walks), dim3(256), 0, s, st.d_planes, st.d_gofs,
                      st.d_off, st.max_groups, z0, z1, buf);
   SCT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(tile_kernel<T>, dim3((unsigned)std::min(st.grid, z1 - z0)), dim3(256), 0, s, buf, z0,
-                     z1 - z0, counts);
+  const dim3 grid((unsigned)std::min(st.grid * (sizeof(T) == 1 ? 3 : 2), z1 - z0));
+#ifdef SCT_ABLATION
+  static const int abl = getenv("SCT_SPECTRAL_ABL") ? atoi(getenv("SCT_SPECTRAL_ABL")) : 0;
+  if (abl == 1) hipLaunchKernelGGL((tile_kernel<T, 1>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
+  if (abl == 2) hipLaunchKernelGGL((tile_kernel<T, 2>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
+  if (abl == 3) hipLaunchKernelGGL((tile_kernel<T, 3>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
+  if (abl == 4) hipLaunchKernelGGL((tile_kernel<T, 4>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
+  if (abl >= 1 && abl <= 4) {
+    SCT_LAUNCH_CHECK();
+    return SCT_OK;
+  }
+#endif
+  hipLaunchKernelGGL(tile_kernel<T>, grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
@@ -308,7 +427,7 @@ int launch_chunk(const State& st, int z0, int z1, unsigned long long* counts, hi
 int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus) {
   st.n = n;
   st.chunk = std::max<int64_t>(kWalk, std::min<int64_t>(chunk, kSlices));
-  st.grid = std::max(1, cus) * 2;  // 64 KB of LDS per tile workgroup: two per CU
+  st.grid = std::max(1, cus);  // CUs; the tile kernel runs 3 workgroups per CU (int8), else 2
   if (n < 2) return SCT_OK;
   SCT_HIP(hipMalloc(&st.d_sorted, (size_t)n * 8));
   SCT_HIP(hipMalloc(&st.d_off, (size_t)(kLo + 1) * 4));
