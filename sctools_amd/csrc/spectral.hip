@@ -173,7 +173,9 @@ __device__ __forceinline__ void transpose4x4_bytes(const uint32_t* d, uint32_t* 
 // order (one XOR per step from registers); the 64 x 256 values are staged in LDS as dwords
 // of 4 / sizeof(T) consecutive slices per column, transposed in registers and written as
 // 16-B chunks of slice rows.
-template <typename T>
+// ABL (ablation builds only, wrong results by design): 1 = no global stores, 2 = no
+// Gray walk (one group, no planes), 3 = no LDS staging/transposes.
+template <typename T, int ABL = 0>
 __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ planes,
                                                    const uint32_t* __restrict__ gofs,
                                                    const uint32_t* __restrict__ off, int64_t max_groups,
@@ -208,8 +210,22 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
       else acc[gray(i)] += __popc(x);
     }
   };
-  walk(0, std::true_type());  // columns without codes: planes 0, popc 0
-  for (int g = 1; g < wng; ++g) walk(g, std::false_type());
+  if constexpr (ABL == 2) {
+#pragma unroll
+    for (int i = 0; i < kWalk; ++i) acc[i] = (i * 5 + tid) & 31;
+  } else {
+    walk(0, std::true_type());  // columns without codes: planes 0, popc 0
+    for (int g = 1; g < wng; ++g) walk(g, std::false_type());
+  }
+  if constexpr (ABL == 3) {
+    const int z = zblk + (tid & 63);
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < kWalk; ++i) w += (uint32_t)acc[i] << (i & 7);
+    if (z >= z0 && z < z1)
+      reinterpret_cast<uint32_t*>(buf + (int64_t)(z - z0) * kLo + c0)[tid >> 6] = w;
+    return;
+  }
   // 4-dword groups of a 16-dword column block XOR-swizzled by the block, so the
   // store-out's b128 reads of 16 consecutive columns are conflict-free
   auto sidx = [](int row, int col) { return row * 256 + (col ^ (((col >> 6) & 3) << 2)); };
@@ -259,6 +275,9 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
     for (int j = 0; j < P; ++j) {
       const int z = zblk + row * P + j;
       if (z < z0 || z >= z1) continue;
+      if constexpr (ABL == 1) {
+        if ((out[j][0] ^ out[j][1] ^ out[j][2] ^ out[j][3]) != 0x12345678u) continue;
+      }
       *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + cb)) =
           make_uint4(out[j][0], out[j][1], out[j][2], out[j][3]);
     }
@@ -402,8 +421,22 @@ template <typename T>
 int launch_chunk(const State& st, int z0, int z1, unsigned long long* counts, hipStream_t s) {
   T* buf = reinterpret_cast<T*>(st.d_buf);
   const int walks = (z1 - (z0 & ~(kWalk - 1)) + kWalk - 1) / kWalk;
-  hipLaunchKernelGGL(seed_kernel<T>, dim3(kLo / 256, (unsigned)walks), dim3(256), 0, s, st.d_planes, st.d_gofs,
-                     st.d_off, st.max_groups, z0, z1, buf);
+  const dim3 sgrid(kLo / 256, (unsigned)walks);
+#ifdef SCT_ABLATION
+  static const int sabl = getenv("SCT_SEED_ABL") ? atoi(getenv("SCT_SEED_ABL")) : 0;
+  if (sabl == 1)
+    hipLaunchKernelGGL((seed_kernel<T, 1>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                       st.max_groups, z0, z1, buf);
+  if (sabl == 2)
+    hipLaunchKernelGGL((seed_kernel<T, 2>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                       st.max_groups, z0, z1, buf);
+  if (sabl == 3)
+    hipLaunchKernelGGL((seed_kernel<T, 3>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                       st.max_groups, z0, z1, buf);
+  if (sabl < 1 || sabl > 3)
+#endif
+    hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, st.max_groups,
+                       z0, z1, buf);
   SCT_LAUNCH_CHECK();
   const dim3 grid((unsigned)std::min(st.grid * (sizeof(T) == 1 ? 3 : 2), z1 - z0));
 #ifdef SCT_ABLATION
