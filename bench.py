@@ -1,18 +1,21 @@
 """Benchmark: Hamming pair-comparisons/s, 737,280-barcode all-pairs histogram (BASELINE.json).
 
 One step = the whole hot path of Barcodes.summarize_hamming_distances on device-
-resident codes: build the bit-sliced selection table, count this rank's share of the
-all-pairs work items, all-reduce the subset counts over RCCL (N > 1), copy them to
-the host, invert them to the exact histogram and compute the numpy-exact summary.
+resident codes, with the count scheme the library picks (AUTO; --scheme forces one):
+build the plan's tables, count this rank's share of the work items, all-reduce the
+counts over RCCL (N > 1), copy them to the host, invert them to the exact histogram
+and compute the numpy-exact summary.  At 737K 16-bp codes AUTO is SPECTRAL (the
+Walsh-Hadamard route, DESIGN.md §3.8: no pair is enumerated, the histogram is the same
+bit for bit); the pair-enumerating MOMENTS kernel is timed beside it as `pair_kernel`.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
 Rank 0 prints one JSON line.  `value` = all pairs of the whole job / max-over-ranks
-wall time of the K timed steps.  `roofline` prices the dominant kernel
-(allpairs_count) with the algorithmic op count of SURVEY.md §8(d) (4 int32 ops per
-16-bp pair) over its average duration, measured with HIP events on the stream the
-kernel runs on.  `cpu_baseline` times the C oracle restatement (test infrastructure,
+wall time of the K timed steps.  `roofline` prices the dominant kernel over its average
+duration, measured with HIP events on the stream it runs on: SPECTRAL's tile kernel
+with its algorithmic int32 ops (14 butterfly add/subs + 1 square-accumulate per
+transform value), or the pair count kernel with SURVEY.md §8(d)'s 4 ops per 16-bp pair.  `cpu_baseline` times the C oracle restatement (test infrastructure,
 never the product) on a bounded row sample of the same workload, rank 0 only.
 """
 
@@ -41,6 +44,12 @@ ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-b
 #   MOMENTS (triple tables, unroll 1): 24 v_bitop3 + 13 v_bcnt + 4 v_xor/v_and + 3 v_add.
 ISSUE_SLOTS_PER_PAIR = {_lib.SCHEME_SUBSETS: (33 + 2 * 16 + 6) / 32.0,
                         _lib.SCHEME_MOMENTS: (24 + 2 * 13 + 4 + 3) / 32.0}
+# SPECTRAL tile kernel: per slice of 2^14 transform values, 14 butterfly levels (one add
+# or sub per value per level) and one square-accumulate per value
+SPECTRAL_OPS_PER_SLICE = (1 << 14) * (14 + 1)
+SCHEMES = {"auto": _lib.SCHEME_AUTO, "subsets": _lib.SCHEME_SUBSETS, "moments": _lib.SCHEME_MOMENTS,
+           "spectral": _lib.SCHEME_SPECTRAL}
+SCHEME_NAMES = {v: k for k, v in SCHEMES.items()}
 
 
 def parse():
@@ -52,6 +61,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--scheme", default="auto", choices=sorted(SCHEMES))
+    ap.add_argument("--pair-steps", type=int, default=5,
+                    help="steps of the pair-enumerating MOMENTS kernel timed beside SPECTRAL (N=1)")
     return ap.parse_args()
 
 
@@ -89,6 +101,83 @@ def cpu_baseline(codes, target_s):
             "python_reference_1core_pairs_per_s": 752540.0}
 
 
+def _traffic(name):
+    """HBM bytes per launch of the kernel from the committed PMC summary (FETCH_SIZE +
+    WRITE_SIZE, gfx950-corrected; tools/summarize_profile.py), or None."""
+    pmc = os.path.join(ROOT, "profiles", name)
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    return None
+
+
+def spectral_roofline(spectral_ms, step_kernel_ms):
+    """Dominant kernel of SPECTRAL: the tile kernel (14-bit WHT per slice + F^2 binning)."""
+    tile = float(np.mean([t["tile_ms"] for t in spectral_ms]))
+    seed = float(np.mean([t["seed_ms"] for t in spectral_ms]))
+    launches = spectral_ms[-1]["launches"]
+    slices = spectral_ms[-1]["slices"]
+    achieved = slices * SPECTRAL_OPS_PER_SLICE / (tile * 1e-3)
+    return {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12, "unit": "Tops/s",
+            "frac": achieved / VALU_PEAK_OPS, "traffic": _traffic("pmc_spectral_latest.json"),
+            "kernel": "sct_spectral::tile_kernel<int8>", "kernel_ms": tile / max(1, launches),
+            "launches_per_step": launches, "slices_per_launch": slices / max(1, launches),
+            "algo_ops_per_slice": SPECTRAL_OPS_PER_SLICE, "seed_kernel_ms_per_step": seed,
+            "tile_kernel_ms_per_step": tile, "count_ms_per_step": step_kernel_ms,
+            "algo_bytes_per_launch": slices / max(1, launches) * (1 << 14),
+            "note": "traffic = tile-kernel HBM bytes per launch from PMC; its algorithmic bytes are "
+                    "the int8 seed values it reads (16 KB per slice)"}
+
+
+def pair_roofline(plan, my_pairs, kms, L, moments_ms):
+    achieved = my_pairs * ALGO_OPS_PER_PAIR / (kms * 1e-3)
+    slots_per_pair = ISSUE_SLOTS_PER_PAIR[plan.scheme] if L == 16 else float("nan")
+    slots = my_pairs * slots_per_pair / (kms * 1e-3)
+    return {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
+            "unit": "Tops/s", "frac": achieved / VALU_PEAK_OPS, "traffic": _traffic("pmc_allpairs_latest.json"),
+            "kernel": "allpairs_count_kernel<8>", "kernel_ms": kms,
+            "algo_ops_per_pair": ALGO_OPS_PER_PAIR,
+            "issue_slots_per_pair": slots_per_pair,
+            "scheme": SCHEME_NAMES[plan.scheme],
+            "moments_ms": moments_ms,
+            "issue_slot_frac": slots / VALU_PEAK_OPS,
+            "note": "frac > 1: the bit-sliced kernel needs %.2f VALU issue slots per "
+                    "pair where SURVEY 8(d)'s formulation needs 4 ops (5 slots: "
+                    "v_bcnt is half rate); issue_slot_frac is the VALU utilisation" % slots_per_pair}
+
+
+def time_pair_kernel(d_codes, n, L, pairs_total, steps):
+    """The pair-enumerating MOMENTS kernel on the same codes (whole step: build, moments,
+    count, inversion), for comparison with SPECTRAL."""
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 2 * L, scheme=_lib.SCHEME_MOMENTS)
+    dev = d_codes.device
+    counts = torch.zeros(plan.ncounts, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    kms, hist = [], None
+    for i in range(steps + 1):
+        if i == 1:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        counts.zero_()
+        plan.build(s.cuda_stream)
+        plan.moments(counts.data_ptr(), 0, 1, s.cuda_stream)
+        ev0.record(s)
+        plan.count(counts.data_ptr(), 0, plan.items, 0, s.cuda_stream)
+        ev1.record(s)
+        hist = sharding.combine_counts(counts, None, plan.scheme, plan.nbins)
+        if i:
+            kms.append(ev0.elapsed_time(ev1))
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    plan.close()
+    assert int(hist.sum()) == pairs_total
+    km = float(np.mean(kms))
+    return {"scheme": "moments", "value": pairs_total / dt, "unit": "pairs/s", "ms_per_step": dt * 1e3,
+            "steps": steps, "kernel_ms": km,
+            "kernel_frac": pairs_total * ALGO_OPS_PER_PAIR / (km * 1e-3) / VALU_PEAK_OPS}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,7 +199,10 @@ def main():
     n, L, seed = synthetic.CONFIGS[args.config]
     codes = synthetic.whitelist_codes(n, L, seed)
     d_codes = torch.from_numpy(codes.view(np.int64)).to(dev)
-    plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 2 * L)
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 2 * L, scheme=SCHEMES[args.scheme])
+    spectral = plan.scheme == _lib.SCHEME_SPECTRAL
+    if spectral:
+        plan.profile(True)  # HIP events around every seed / tile launch
     b, e = sharding.item_range(plan.items, rank, world)
     counts = torch.zeros(plan.ncounts, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -124,6 +216,7 @@ def main():
     ev_zero, ev_mom = torch.cuda.Event(), torch.cuda.Event()
     evm0, evm1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     moments_ms = []
+    spectral_ms = []
 
     def step(record):
         counts.zero_()
@@ -147,6 +240,8 @@ def main():
         if record:
             kernel_ms.append(ev0.elapsed_time(ev1))
             moments_ms.append(evm0.elapsed_time(evm1))
+            if spectral:
+                spectral_ms.append(plan.kernel_ms())
         return hist, _lib.summary_from_hist(hist)
 
     for _ in range(args.warmup):
@@ -170,14 +265,13 @@ def main():
     assert int(hist.sum()) == pairs_total, "histogram does not cover every pair"
     my_pairs = plan.range_pairs(b, e)
     kms = float(np.mean(kernel_ms))
-    achieved = my_pairs * ALGO_OPS_PER_PAIR / (kms * 1e-3)
-    slots_per_pair = ISSUE_SLOTS_PER_PAIR[plan.scheme] if L == 16 else float("nan")
-    slots = my_pairs * slots_per_pair / (kms * 1e-3)
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_allpairs_latest.json")  # tools/summarize_profile.py
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    if spectral:
+        roofline = spectral_roofline(spectral_ms, kms)
+    else:
+        roofline = pair_roofline(plan, my_pairs, kms, L, float(np.mean(moments_ms)))
+    pair_kernel = None
+    if spectral and world == 1 and args.pair_steps > 0:
+        pair_kernel = time_pair_kernel(d_codes, n, L, pairs_total, args.pair_steps)
 
     if rank == 0:
         out = {
@@ -191,28 +285,20 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "u32",
+            "dtype": "i32" if spectral else "u32",
             "data": "synthetic (seeded uniform random unique 16-bp codes, sctools_amd/synthetic.py)",
             "config": {"workload": "config %d: %d-barcode all-pairs TwoBit Hamming histogram + summary"
                                    % (args.config, n),
                        "barcodes": n, "barcode_length": L, "pairs": pairs_total,
-                       "parallelism": "item-range + moment shards, RCCL all-reduce of %d counts" % plan.ncounts
-                       if world > 1 else "single GPU"},
-            "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
-                         "unit": "Tops/s", "frac": achieved / VALU_PEAK_OPS, "traffic": traffic,
-                         "kernel": "allpairs_count_kernel<8>", "kernel_ms": kms,
-                         "algo_ops_per_pair": ALGO_OPS_PER_PAIR,
-                         "issue_slots_per_pair": slots_per_pair,
-                         "scheme": {0: "subsets", 1: "moments"}[plan.scheme],
-                         "moments_ms": float(np.mean(moments_ms)),
-                         "issue_slot_frac": slots / VALU_PEAK_OPS,
-                         "note": "frac > 1: the bit-sliced kernel needs %.2f VALU issue slots per "
-                                 "pair where SURVEY 8(d)'s formulation needs 4 ops (5 slots: "
-                                 "v_bcnt is half rate); issue_slot_frac is the VALU utilisation"
-                                 % slots_per_pair},
+                       "scheme": SCHEME_NAMES[plan.scheme],
+                       "parallelism": ("transform-slice shards" if spectral else "item-range + moment shards")
+                       + ", RCCL all-reduce of %d counts" % plan.ncounts if world > 1 else "single GPU"},
+            "roofline": roofline,
             "summary": dict(zip(("minimum", "p25", "median", "p75", "maximum", "average"),
                                 [float(x) for x in summ])),
         }
+        if pair_kernel is not None:
+            out["pair_kernel"] = pair_kernel
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(codes, args.cpu_seconds)
         print(json.dumps(out), flush=True)

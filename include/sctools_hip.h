@@ -142,7 +142,7 @@ int sct_hamming_pairs_host(int kind, const uint64_t* a, const uint64_t* b, int64
  */
 typedef struct sct_allpairs_plan sct_allpairs_plan;
 
-#define SCT_ALLPAIRS_AUTO (-1)    /* 16 bases: SPECTRAL for large n, else MOMENTS; else SUBSETS */
+#define SCT_ALLPAIRS_AUTO (-1)    /* 16 bases: SPECTRAL from 500K codes, else MOMENTS; else SUBSETS */
 #define SCT_ALLPAIRS_SUBSETS 0
 #define SCT_ALLPAIRS_MOMENTS 1
 #define SCT_ALLPAIRS_SPECTRAL 2
@@ -183,6 +183,14 @@ int sct_allpairs_geometry(int64_t n, int code_bits, int* nbins, int64_t* items, 
  * range's share floor(P*end/items) - floor(P*begin/items) of all P pairs). */
 int sct_allpairs_range_pairs(const sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
                              int64_t* pairs);
+
+/* SPECTRAL plans: record HIP events around every kernel of later sct_allpairs_count
+ * calls (enable = 1); sct_allpairs_kernel_ms then reports the last call's
+ * out[0] = tile-kernel ms, out[1] = seed-kernel ms (summed over launches), out[2] =
+ * launches of each, out[3] = slices counted (waits on the events).  Other schemes report
+ * zeros (time their single count kernel on the caller's stream). */
+int sct_allpairs_profile(sct_allpairs_plan* plan, int enable);
+int sct_allpairs_kernel_ms(sct_allpairs_plan* plan, double* out, int nout);
 
 /* Host: SUBSETS counts -> histogram (exact Moebius inversion), hist[d] for d < nbins. */
 int sct_counts_to_hist(const uint64_t* counts, int nbins, uint64_t* hist);

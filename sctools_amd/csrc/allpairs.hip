@@ -710,7 +710,7 @@ bool spectral_supported(int npp, int64_t n) { return mom_supported(npp, n); }
 // smallest n for which AUTO picks SPECTRAL over MOMENTS (measured crossover)
 int64_t spectral_min_n() {
   const char* v = getenv("SCT_SPECTRAL_MIN_N");
-  return v ? atoll(v) : 1500000;
+  return v ? atoll(v) : 500000;
 }
 // what SCT_ALLPAIRS_AUTO resolves to; SCT_ALLPAIRS_SCHEME=0/1/2 in the environment forces
 // SUBSETS / MOMENTS / SPECTRAL where the codes allow it
@@ -1180,6 +1180,26 @@ extern "C" int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, i
     return sct_spectral::count(plan->spec, item_begin, item_end,
                                reinterpret_cast<unsigned long long*>(d_counts), sct::as_stream(stream));
   return dispatch_count(plan, item_begin, item_end, d_counts, grid, sct::as_stream(stream));
+}
+
+extern "C" int sct_allpairs_profile(sct_allpairs_plan* plan, int enable) {
+  SCT_CHECK(plan != nullptr, "plan is NULL");
+  plan->spec.timing = enable != 0;
+  return SCT_OK;
+}
+
+extern "C" int sct_allpairs_kernel_ms(sct_allpairs_plan* plan, double* out, int nout) {
+  SCT_CHECK(plan != nullptr && (out != nullptr || nout == 0), "NULL pointer");
+  double v[4] = {0, 0, 0, 0};
+  if (plan->scheme == SCT_ALLPAIRS_SPECTRAL) {
+    int launches = 0;
+    const int rc = sct_spectral::kernel_ms(plan->spec, &v[0], &v[1], &launches);
+    if (rc != SCT_OK) return rc;
+    v[2] = launches;
+    v[3] = (double)plan->spec.slices_timed;
+  }
+  for (int i = 0; i < nout && i < 4; ++i) out[i] = v[i];
+  return SCT_OK;
 }
 
 extern "C" int sct_allpairs_geometry(int64_t n, int code_bits, int* nbins, int64_t* items,

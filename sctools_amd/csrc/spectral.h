@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace sct_spectral {
 
 constexpr int kSpaceBits = 32;                 // 16 bases: codes are points of Z_2^32
@@ -26,6 +28,10 @@ struct State {
   void* d_sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   int grid = 0;                  // compute units (the tile kernel's persistent grid)
+  bool timing = false;           // record HIP events around every seed / tile launch
+  std::vector<hipEvent_t> events;
+  int nev = 0;
+  int64_t slices_timed = 0;
 };
 
 // allocate (chunk = slices held in HBM at once) and size the intermediate from the
@@ -37,5 +43,8 @@ int build(State& st, const uint64_t* d_codes, hipStream_t s);
 // add the counts of slices [z_begin, z_end): d_counts[1 + w] += S_w over those slices,
 // d_counts[0] += n when z_begin == 0
 int count(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_counts, hipStream_t s);
+
+// HIP-event times of the last count call's launches (timing on): summed seed and tile ms
+int kernel_ms(State& st, double* seed_ms, double* tile_ms, int* launches);
 
 }  // namespace sct_spectral

@@ -418,10 +418,21 @@ __global__ void max_column_kernel(const uint32_t* __restrict__ off, unsigned* __
 __global__ void add_kernel(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
 
 template <typename T>
-int launch_chunk(const State& st, int z0, int z1, unsigned long long* counts, hipStream_t s) {
+int launch_chunk(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s) {
   T* buf = reinterpret_cast<T*>(st.d_buf);
   const int walks = (z1 - (z0 & ~(kWalk - 1)) + kWalk - 1) / kWalk;
   const dim3 sgrid(kLo / 256, (unsigned)walks);
+  hipEvent_t* ev = nullptr;  // [seed start, seed end = tile start, tile end]
+  if (st.timing) {
+    if (st.nev + 3 > (int)st.events.size()) {
+      const size_t old = st.events.size();
+      st.events.resize(old + 48);
+      for (size_t i = old; i < st.events.size(); ++i) SCT_HIP(hipEventCreate(&st.events[i]));
+    }
+    ev = st.events.data() + st.nev;
+    st.nev += 3;
+    SCT_HIP(hipEventRecord(ev[0], s));
+  }
 #ifdef SCT_ABLATION
   static const int sabl = getenv("SCT_SEED_ABL") ? atoi(getenv("SCT_SEED_ABL")) : 0;
   if (sabl == 1)
@@ -438,6 +449,7 @@ int launch_chunk(const State& st, int z0, int z1, unsigned long long* counts, hi
     hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, st.max_groups,
                        z0, z1, buf);
   SCT_LAUNCH_CHECK();
+  if (ev) SCT_HIP(hipEventRecord(ev[1], s));
   const dim3 grid((unsigned)std::min(st.grid * (sizeof(T) == 1 ? 3 : 2), z1 - z0));
 #ifdef SCT_ABLATION
   static const int abl = getenv("SCT_SPECTRAL_ABL") ? atoi(getenv("SCT_SPECTRAL_ABL")) : 0;
@@ -452,6 +464,7 @@ int launch_chunk(const State& st, int z0, int z1, unsigned long long* counts, hi
 #endif
   hipLaunchKernelGGL(tile_kernel<T>, grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
   SCT_LAUNCH_CHECK();
+  if (ev) SCT_HIP(hipEventRecord(ev[2], s));
   return SCT_OK;
 }
 
@@ -493,7 +506,24 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   return SCT_OK;
 }
 
+int kernel_ms(State& st, double* seed_ms, double* tile_ms, int* launches) {
+  double a = 0, b = 0;
+  for (int i = 0; i + 3 <= st.nev; i += 3) {
+    float x = 0, y = 0;
+    SCT_HIP(hipEventSynchronize(st.events[i + 2]));
+    SCT_HIP(hipEventElapsedTime(&x, st.events[i], st.events[i + 1]));
+    SCT_HIP(hipEventElapsedTime(&y, st.events[i + 1], st.events[i + 2]));
+    a += x;
+    b += y;
+  }
+  if (seed_ms) *seed_ms = a;
+  if (tile_ms) *tile_ms = b;
+  if (launches) *launches = st.nev / 3;
+  return SCT_OK;
+}
+
 void destroy(State& st) {
+  for (hipEvent_t e : st.events) (void)hipEventDestroy(e);
   for (void* p : {(void*)st.d_sorted, (void*)st.d_off, (void*)st.d_gofs, (void*)st.d_planes, st.d_buf,
                   st.d_sort_tmp})
     if (p) (void)hipFree(p);
@@ -519,7 +549,10 @@ int build(State& st, const uint64_t* d_codes, hipStream_t s) {
 int count(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_counts, hipStream_t s) {
   SCT_CHECK(0 <= z_begin && z_begin <= z_end && z_end <= kSlices, "slice range [%lld, %lld)",
             (long long)z_begin, (long long)z_end);
+  st.nev = 0;
+  st.slices_timed = 0;
   if (st.n < 2 || z_begin == z_end) return SCT_OK;
+  st.slices_timed = z_end - z_begin;
   for (int64_t z0 = z_begin; z0 < z_end; z0 += st.chunk) {
     const int z1 = (int)std::min<int64_t>(z_end, z0 + st.chunk);
     const int rc = st.elem_bytes == 1   ? launch_chunk<int8_t>(st, (int)z0, z1, d_counts, s)

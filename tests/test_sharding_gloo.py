@@ -109,7 +109,10 @@ def test_item_range_partitions():
             assert max(sizes) - min(sizes) <= 1
 
 
-def test_geometry_item_count_matches_oracle_enumeration():
+def test_geometry_item_count_matches_oracle_enumeration(monkeypatch):
+    # 737K codes resolve to SPECTRAL (2^18 slice items); the pair-item geometry is MOMENTS'
+    assert _lib.allpairs_geometry(737_280, 32)["items"] == 1 << 18
+    monkeypatch.setenv("SCT_ALLPAIRS_SCHEME", "1")
     for n in (2, 100, 1024, 1025, 5000, 737_280):
         geo = _lib.allpairs_geometry(n, 32)
         rb, cb = geo["rows_per_item"], geo["cols_per_item"]

@@ -4,7 +4,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu --pair-steps 2"
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/trace -o run --output-format csv -- $B > gpurun_out/prof/trace.log 2>&1 || exit 3
 i=0
 for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \

@@ -2,9 +2,9 @@
 
   python tools/summarize_profile.py --round r01 [--src gpurun_out/prof]
 
-Writes profiles/<round>_kernel_stats.csv (rocprofv3 --kernel-trace --stats) and
-profiles/pmc_allpairs_<round>.json: per-launch PMC averages of the all-pairs count
-kernel plus derived figures (clock from GRBM_GUI_ACTIVE / 8 XCDs / duration, VALU
+Writes profiles/<round>_kernel_stats.csv (rocprofv3 --kernel-trace --stats) and, for
+the SPECTRAL tile kernel and the pair count kernel, profiles/pmc_{spectral,allpairs}_
+<round>.json: per-launch PMC averages plus derived figures (clock from GRBM_GUI_ACTIVE / 8 XCDs / duration, VALU
 lane-ops, HBM bytes from FETCH_SIZE/WRITE_SIZE in KiB with the gfx950 correction of
 MI355X_MICROARCH.md §HBM: FETCH_SIZE counts half the bytes of wide streaming reads).
 """
@@ -38,36 +38,47 @@ def kernel_avg_ns(stats_csv, kernel_substr):
     return None, 0
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--round", default="r01")
-    ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out", "prof"))
-    ap.add_argument("--kernel", default="allpairs_count_kernel<8")
-    ap.add_argument("--pairs", type=float, default=737280 * 737279 / 2)
-    a = ap.parse_args()
-    dst = os.path.join(ROOT, "profiles")
-    os.makedirs(dst, exist_ok=True)
-    stats = os.path.join(a.src, "trace", "run_kernel_stats.csv")
-    shutil.copy(stats, os.path.join(dst, "%s_kernel_stats.csv" % a.round))
-    avg_ns, calls = kernel_avg_ns(stats, a.kernel)
-    m = pmc_means(a.src, a.kernel)
-    out = {"kernel": a.kernel, "trace_avg_ns": avg_ns, "trace_calls": calls, "pmc": m}
+KERNELS = (("allpairs", "allpairs_count_kernel<8"), ("spectral", "tile_kernel<signed char"))
+
+
+def summarize(src, dst, rnd, name, kernel, pairs):
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+    avg_ns, calls = kernel_avg_ns(stats, kernel)
+    if not calls:
+        return None
+    m = pmc_means(src, kernel)
+    out = {"kernel": kernel, "trace_avg_ns": avg_ns, "trace_calls": calls, "pmc": m}
     if "GRBM_GUI_ACTIVE" in m and avg_ns:
         out["clock_ghz_estimate"] = m["GRBM_GUI_ACTIVE"] / 8 / avg_ns
     if "SQ_INSTS_VALU" in m:
         out["valu_wave_instructions"] = m["SQ_INSTS_VALU"]
-        out["valu_lane_ops_per_pair"] = m["SQ_INSTS_VALU"] * 64 / a.pairs
+        if name == "allpairs":
+            out["valu_lane_ops_per_pair"] = m["SQ_INSTS_VALU"] * 64 / pairs
     if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
         fetch = m["FETCH_SIZE"] * 1024
         write = m["WRITE_SIZE"] * 1024
         out["hbm_bytes_per_launch_raw"] = fetch + write
         out["hbm_bytes_per_launch"] = 2 * fetch + write  # gfx950 FETCH_SIZE half-count correction
         out["note"] = ("FETCH_SIZE/WRITE_SIZE are KiB per dispatch; reads doubled per the gfx950 "
-                       "correction (an upper bound here: only the table staging is 16 B/lane).")
-    for name in ("pmc_allpairs_%s.json" % a.round, "pmc_allpairs_latest.json"):
-        with open(os.path.join(dst, name), "w") as f:
-            json.dump(dict(out, round=a.round), f, indent=1)
-    print(json.dumps(out, indent=1))
+                       "correction (16-B-per-lane streaming reads).")
+    for fn in ("pmc_%s_%s.json" % (name, rnd), "pmc_%s_latest.json" % name):
+        with open(os.path.join(dst, fn), "w") as f:
+            json.dump(dict(out, round=rnd), f, indent=1)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--round", default="r01")
+    ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out", "prof"))
+    ap.add_argument("--pairs", type=float, default=737280 * 737279 / 2)
+    a = ap.parse_args()
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(a.src, "trace", "run_kernel_stats.csv"),
+                os.path.join(dst, "%s_kernel_stats.csv" % a.round))
+    for name, kernel in KERNELS:
+        print(name, json.dumps(summarize(a.src, dst, a.round, name, kernel, a.pairs), indent=1))
 
 
 if __name__ == "__main__":
