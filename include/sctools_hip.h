@@ -184,13 +184,13 @@ int sct_allpairs_geometry(int64_t n, int code_bits, int* nbins, int64_t* items, 
 int sct_allpairs_range_pairs(const sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
                              int64_t* pairs);
 
-/* SPECTRAL plans: record HIP events around every kernel of later sct_allpairs_count
- * calls (enable = 1); sct_allpairs_kernel_ms then reports the last call's
- * out[0] = tile-kernel ms, out[1] = seed-kernel ms (summed over launches), out[2] =
- * launches of each, out[3] = slices counted (waits on the events).  Other schemes report
- * zeros (time their single count kernel on the caller's stream). */
-int sct_allpairs_profile(sct_allpairs_plan* plan, int enable);
-int sct_allpairs_kernel_ms(sct_allpairs_plan* plan, double* out, int nout);
+/* Bench aid (d_counts receives garbage): the dominant kernel's ms per launch, timed as
+ * `repeats` back-to-back launches bracketed by HIP events on `stream`.  SPECTRAL: out[0] =
+ * tile kernel, out[1] = seed kernel, both on the first chunk of the range (out[2] = its
+ * slices); other schemes: out[0] = count kernel over the range, out[1] = 0, out[2] = items.
+ * Needs a built plan. */
+int sct_allpairs_time_kernels(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
+                              uint64_t* d_counts, int repeats, double* out, void* stream);
 
 /* Host: SUBSETS counts -> histogram (exact Moebius inversion), hist[d] for d < nbins. */
 int sct_counts_to_hist(const uint64_t* counts, int nbins, uint64_t* hist);

@@ -59,8 +59,7 @@ SIGNATURES = {
     "sct_allpairs_build_items": [_vp, _i64, _i64, _vp],
     "sct_allpairs_count": [_vp, _i64, _i64, _vp, _i32, _vp],
     "sct_allpairs_range_pairs": [_vp, _i64, _i64, ctypes.POINTER(_i64)],
-    "sct_allpairs_profile": [_vp, _i32],
-    "sct_allpairs_kernel_ms": [_vp, ctypes.POINTER(ctypes.c_double), _i32],
+    "sct_allpairs_time_kernels": [_vp, _i64, _i64, _vp, _i32, ctypes.POINTER(ctypes.c_double), _vp],
     "sct_allpairs_geometry": [_i64, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i64),
                               ctypes.POINTER(_i32), ctypes.POINTER(_i32)],
     "sct_counts_to_hist": [_vp, _i32, _vp],
@@ -441,15 +440,14 @@ class AllPairsPlan:
     def counts_to_hist(self, counts):
         return counts_to_hist(counts, self.scheme, self.nbins)
 
-    def profile(self, enable=True):
-        """SPECTRAL: time every kernel of later count calls with HIP events."""
-        check(self._lib.sct_allpairs_profile(self._h, int(bool(enable))))
-
-    def kernel_ms(self):
-        """Last count call (profile on): dict(tile_ms, seed_ms, launches, slices)."""
-        out = (ctypes.c_double * 4)()
-        check(self._lib.sct_allpairs_kernel_ms(self._h, out, 4))
-        return {"tile_ms": out[0], "seed_ms": out[1], "launches": int(out[2]), "slices": int(out[3])}
+    def time_kernels(self, d_scratch_ptr, begin=0, end=None, repeats=5, stream=0):
+        """Bench aid: dict(kernel_ms, seed_ms, units) -- the dominant kernel's ms per launch
+        (SPECTRAL: tile kernel on one chunk of `units` slices; else the count kernel)."""
+        end = self.items if end is None else end
+        out = (ctypes.c_double * 3)()
+        check(self._lib.sct_allpairs_time_kernels(self._h, begin, end, _vp(d_scratch_ptr), repeats, out,
+                                                  _vp(stream)))
+        return {"kernel_ms": out[0], "seed_ms": out[1], "units": int(out[2])}
 
     def range_pairs(self, begin, end):
         p = _i64(0)

@@ -1182,24 +1182,36 @@ extern "C" int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, i
   return dispatch_count(plan, item_begin, item_end, d_counts, grid, sct::as_stream(stream));
 }
 
-extern "C" int sct_allpairs_profile(sct_allpairs_plan* plan, int enable) {
-  SCT_CHECK(plan != nullptr, "plan is NULL");
-  plan->spec.timing = enable != 0;
-  return SCT_OK;
-}
-
-extern "C" int sct_allpairs_kernel_ms(sct_allpairs_plan* plan, double* out, int nout) {
-  SCT_CHECK(plan != nullptr && (out != nullptr || nout == 0), "NULL pointer");
-  double v[4] = {0, 0, 0, 0};
+extern "C" int sct_allpairs_time_kernels(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
+                                         uint64_t* d_counts, int repeats, double* out, void* stream) {
+  SCT_CHECK(plan != nullptr && d_counts != nullptr && out != nullptr, "NULL pointer");
+  SCT_CHECK(0 <= item_begin && item_begin < item_end && item_end <= plan->items && repeats > 0,
+            "item range [%lld, %lld) outside [0, %lld) or repeats < 1", (long long)item_begin,
+            (long long)item_end, (long long)plan->items);
+  hipStream_t s = sct::as_stream(stream);
   if (plan->scheme == SCT_ALLPAIRS_SPECTRAL) {
-    int launches = 0;
-    const int rc = sct_spectral::kernel_ms(plan->spec, &v[0], &v[1], &launches);
-    if (rc != SCT_OK) return rc;
-    v[2] = launches;
-    v[3] = (double)plan->spec.slices_timed;
+    int64_t slices = 0;
+    const int rc = sct_spectral::time_kernels(plan->spec, item_begin, item_end,
+                                              reinterpret_cast<unsigned long long*>(d_counts), repeats, s,
+                                              &out[1], &out[0], &slices);
+    out[2] = (double)slices;
+    return rc;
   }
-  for (int i = 0; i < nout && i < 4; ++i) out[i] = v[i];
-  return SCT_OK;
+  hipEvent_t e[2];
+  SCT_HIP(hipEventCreate(&e[0]));
+  SCT_HIP(hipEventCreate(&e[1]));
+  int rc = SCT_OK;
+  (void)hipEventRecord(e[0], s);
+  for (int r = 0; rc == SCT_OK && r < repeats; ++r) rc = dispatch_count(plan, item_begin, item_end, d_counts, 0, s);
+  (void)hipEventRecord(e[1], s);
+  float ms = 0;
+  if (rc == SCT_OK && hipEventSynchronize(e[1]) == hipSuccess) (void)hipEventElapsedTime(&ms, e[0], e[1]);
+  (void)hipEventDestroy(e[0]);
+  (void)hipEventDestroy(e[1]);
+  out[0] = ms / repeats;
+  out[1] = 0;
+  out[2] = (double)(item_end - item_begin);
+  return rc;
 }
 
 extern "C" int sct_allpairs_geometry(int64_t n, int code_bits, int* nbins, int64_t* items,

@@ -5,8 +5,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <vector>
-
 namespace sct_spectral {
 
 constexpr int kSpaceBits = 32;                 // 16 bases: codes are points of Z_2^32
@@ -28,10 +26,6 @@ struct State {
   void* d_sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   int grid = 0;                  // compute units (the tile kernel's persistent grid)
-  bool timing = false;           // record HIP events around every seed / tile launch
-  std::vector<hipEvent_t> events;
-  int nev = 0;
-  int64_t slices_timed = 0;
 };
 
 // allocate (chunk = slices held in HBM at once) and size the intermediate from the
@@ -44,7 +38,9 @@ int build(State& st, const uint64_t* d_codes, hipStream_t s);
 // d_counts[0] += n when z_begin == 0
 int count(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_counts, hipStream_t s);
 
-// HIP-event times of the last count call's launches (timing on): summed seed and tile ms
-int kernel_ms(State& st, double* seed_ms, double* tile_ms, int* launches);
+// bench aid: ms per launch of the seed and tile kernels over the first chunk of
+// [z_begin, z_end) (`slices` of them), each timed as `repeats` back-to-back launches
+int time_kernels(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_counts, int repeats,
+                 hipStream_t s, double* seed_ms, double* tile_ms, int64_t* slices);
 
 }  // namespace sct_spectral

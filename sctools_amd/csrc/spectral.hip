@@ -418,21 +418,10 @@ __global__ void max_column_kernel(const uint32_t* __restrict__ off, unsigned* __
 __global__ void add_kernel(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
 
 template <typename T>
-int launch_chunk(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s) {
+int launch_seed(State& st, int z0, int z1, hipStream_t s) {
   T* buf = reinterpret_cast<T*>(st.d_buf);
   const int walks = (z1 - (z0 & ~(kWalk - 1)) + kWalk - 1) / kWalk;
   const dim3 sgrid(kLo / 256, (unsigned)walks);
-  hipEvent_t* ev = nullptr;  // [seed start, seed end = tile start, tile end]
-  if (st.timing) {
-    if (st.nev + 3 > (int)st.events.size()) {
-      const size_t old = st.events.size();
-      st.events.resize(old + 48);
-      for (size_t i = old; i < st.events.size(); ++i) SCT_HIP(hipEventCreate(&st.events[i]));
-    }
-    ev = st.events.data() + st.nev;
-    st.nev += 3;
-    SCT_HIP(hipEventRecord(ev[0], s));
-  }
 #ifdef SCT_ABLATION
   static const int sabl = getenv("SCT_SEED_ABL") ? atoi(getenv("SCT_SEED_ABL")) : 0;
   if (sabl == 1)
@@ -449,7 +438,12 @@ int launch_chunk(State& st, int z0, int z1, unsigned long long* counts, hipStrea
     hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, st.max_groups,
                        z0, z1, buf);
   SCT_LAUNCH_CHECK();
-  if (ev) SCT_HIP(hipEventRecord(ev[1], s));
+  return SCT_OK;
+}
+
+template <typename T>
+int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s) {
+  T* buf = reinterpret_cast<T*>(st.d_buf);
   const dim3 grid((unsigned)std::min(st.grid * (sizeof(T) == 1 ? 3 : 2), z1 - z0));
 #ifdef SCT_ABLATION
   static const int abl = getenv("SCT_SPECTRAL_ABL") ? atoi(getenv("SCT_SPECTRAL_ABL")) : 0;
@@ -464,7 +458,43 @@ int launch_chunk(State& st, int z0, int z1, unsigned long long* counts, hipStrea
 #endif
   hipLaunchKernelGGL(tile_kernel<T>, grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
   SCT_LAUNCH_CHECK();
-  if (ev) SCT_HIP(hipEventRecord(ev[2], s));
+  return SCT_OK;
+}
+
+template <typename T>
+int launch_chunk(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s) {
+  const int rc = launch_seed<T>(st, z0, z1, s);
+  return rc != SCT_OK ? rc : launch_tile<T>(st, z0, z1, counts, s);
+}
+
+// Bench aid: seed and tile kernels timed apart, each as `repeats` back-to-back launches on
+// one chunk bracketed by HIP events (the timestamps of events between dependent kernels of
+// one stream do not split the kernels reliably).  counts receives garbage.
+template <typename T>
+int time_chunk(State& st, int z0, int z1, unsigned long long* counts, int repeats, hipStream_t s,
+               double* seed_ms, double* tile_ms) {
+  hipEvent_t e[3];
+  for (auto& x : e) SCT_HIP(hipEventCreate(&x));
+  struct Free {
+    hipEvent_t* e;
+    ~Free() {
+      for (int i = 0; i < 3; ++i) (void)hipEventDestroy(e[i]);
+    }
+  } guard{e};
+  int rc = launch_seed<T>(st, z0, z1, s);  // warm
+  if (rc == SCT_OK) rc = launch_tile<T>(st, z0, z1, counts, s);
+  SCT_HIP(hipEventRecord(e[0], s));
+  for (int r = 0; rc == SCT_OK && r < repeats; ++r) rc = launch_seed<T>(st, z0, z1, s);
+  SCT_HIP(hipEventRecord(e[1], s));
+  for (int r = 0; rc == SCT_OK && r < repeats; ++r) rc = launch_tile<T>(st, z0, z1, counts, s);
+  SCT_HIP(hipEventRecord(e[2], s));
+  if (rc != SCT_OK) return rc;
+  SCT_HIP(hipEventSynchronize(e[2]));
+  float a = 0, b = 0;
+  SCT_HIP(hipEventElapsedTime(&a, e[0], e[1]));
+  SCT_HIP(hipEventElapsedTime(&b, e[1], e[2]));
+  *seed_ms = a / repeats;
+  *tile_ms = b / repeats;
   return SCT_OK;
 }
 
@@ -506,24 +536,7 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   return SCT_OK;
 }
 
-int kernel_ms(State& st, double* seed_ms, double* tile_ms, int* launches) {
-  double a = 0, b = 0;
-  for (int i = 0; i + 3 <= st.nev; i += 3) {
-    float x = 0, y = 0;
-    SCT_HIP(hipEventSynchronize(st.events[i + 2]));
-    SCT_HIP(hipEventElapsedTime(&x, st.events[i], st.events[i + 1]));
-    SCT_HIP(hipEventElapsedTime(&y, st.events[i + 1], st.events[i + 2]));
-    a += x;
-    b += y;
-  }
-  if (seed_ms) *seed_ms = a;
-  if (tile_ms) *tile_ms = b;
-  if (launches) *launches = st.nev / 3;
-  return SCT_OK;
-}
-
 void destroy(State& st) {
-  for (hipEvent_t e : st.events) (void)hipEventDestroy(e);
   for (void* p : {(void*)st.d_sorted, (void*)st.d_off, (void*)st.d_gofs, (void*)st.d_planes, st.d_buf,
                   st.d_sort_tmp})
     if (p) (void)hipFree(p);
@@ -549,10 +562,7 @@ int build(State& st, const uint64_t* d_codes, hipStream_t s) {
 int count(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_counts, hipStream_t s) {
   SCT_CHECK(0 <= z_begin && z_begin <= z_end && z_end <= kSlices, "slice range [%lld, %lld)",
             (long long)z_begin, (long long)z_end);
-  st.nev = 0;
-  st.slices_timed = 0;
   if (st.n < 2 || z_begin == z_end) return SCT_OK;
-  st.slices_timed = z_end - z_begin;
   for (int64_t z0 = z_begin; z0 < z_end; z0 += st.chunk) {
     const int z1 = (int)std::min<int64_t>(z_end, z0 + st.chunk);
     const int rc = st.elem_bytes == 1   ? launch_chunk<int8_t>(st, (int)z0, z1, d_counts, s)
@@ -565,6 +575,17 @@ int count(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_count
     SCT_LAUNCH_CHECK();
   }
   return SCT_OK;
+}
+
+int time_kernels(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_counts, int repeats,
+                 hipStream_t s, double* seed_ms, double* tile_ms, int64_t* slices) {
+  SCT_CHECK(0 <= z_begin && z_begin < z_end && z_end <= kSlices && repeats > 0 && st.n >= 2,
+            "time_kernels: empty range or plan");
+  const int z1 = (int)std::min<int64_t>(z_end, z_begin + st.chunk);
+  *slices = z1 - z_begin;
+  return st.elem_bytes == 1   ? time_chunk<int8_t>(st, (int)z_begin, z1, d_counts, repeats, s, seed_ms, tile_ms)
+         : st.elem_bytes == 2 ? time_chunk<int16_t>(st, (int)z_begin, z1, d_counts, repeats, s, seed_ms, tile_ms)
+                              : time_chunk<int32_t>(st, (int)z_begin, z1, d_counts, repeats, s, seed_ms, tile_ms);
 }
 
 }  // namespace sct_spectral
