@@ -119,3 +119,30 @@ def test_geometry_item_count_matches_oracle_enumeration(monkeypatch):
         nch = -(-n // cb)
         items = sum(max(0, -(-(min((c + 1) * cb, n) - 1) // rb)) for c in range(nch))
         assert geo["items"] == items
+
+
+def _worker_spectral(rank, world, port, n, seed, out_path):
+    """SPECTRAL counts of one rank: its share of every S_w (the slices it would count;
+    here an arbitrary integer split of the oracle's S), n on the rank holding item 0."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        codes = synthetic.whitelist_codes(n, 16, seed)
+        full = O.spectral_counts_from_hist(O.c_hist_rows(codes)[:17], n).astype(object)
+        share = [int(x) * (rank + 1) // world - int(x) * rank // world for x in full[1:]]
+        b, _ = sharding.item_range(1 << 18, rank, world)
+        counts = torch.tensor([n if b == 0 else 0] + share, dtype=torch.int64)
+        hist = sharding.combine_counts(counts, None, _lib.SCHEME_SPECTRAL, 17)
+        np.save(out_path % rank, hist.astype(np.int64))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 1500), (3, 700)])
+def test_sharded_spectral_histogram_matches_oracle(tmp_path, world, n):
+    port = _free_port()
+    out = str(tmp_path / "shist_%d.npy")
+    mp.spawn(_worker_spectral, args=(world, port, n, 29, out), nprocs=world, join=True)
+    ref = O.c_hist_rows(synthetic.whitelist_codes(n, 16, 29))[:17]
+    for r in range(world):
+        assert np.load(out % r).tolist() == ref.tolist()
