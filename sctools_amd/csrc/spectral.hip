@@ -17,6 +17,7 @@
 // 8 GB of HBM traffic per job at int8, whatever n is.  Exact: |F| <= n < 2^31 in int32,
 // F^2 and S_w in uint64 (S_w <= 2^32 sum f^2).
 #include <algorithm>
+#include <vector>
 #include <type_traits>
 
 #include <hipcub/hipcub.hpp>
@@ -31,6 +32,8 @@ constexpr int kLo = 1 << kLoBits;         // columns (= tile values)
 constexpr int kHiBits = kSpaceBits - kLoBits;  // 18 bit planes
 constexpr int kWalk = 64;                 // slices per wave in the seed's Gray walk
 constexpr int kWalkBits = 6;
+constexpr int kRegGroups = 2;             // seed: 32-code groups whose planes stay in registers
+constexpr int kSeedWalks = 8;             // seed: walks per workgroup
 
 // non-zero 2-bit digits of z
 __device__ __forceinline__ int digit_weight(uint32_t z) {
@@ -191,12 +194,18 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
   int wng = ng;
 #pragma unroll
   for (int s = 32; s; s >>= 1) wng = max(wng, __shfl_xor(wng, s));
-  const int zblk = (z0 & ~(kWalk - 1)) + (int)blockIdx.y * kWalk;
-  int acc[kWalk];
-  auto walk = [&](int g, auto first) {
-    uint32_t p[kHiBits];
+  // the first kRegGroups groups' planes stay in registers for all of this workgroup's walks
+  uint32_t pr[kRegGroups][kHiBits];
 #pragma unroll
-    for (int k = 0; k < kHiBits; ++k) p[k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
+  for (int g = 0; g < kRegGroups; ++g)
+#pragma unroll
+    for (int k = 0; k < kHiBits; ++k) pr[g][k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
+  const int za = z0 & ~(kWalk - 1);
+  const int nwalks = (z1 - za + kWalk - 1) / kWalk;
+  for (int wk = blockIdx.y; wk < nwalks; wk += gridDim.y) {
+  const int zblk = za + wk * kWalk;
+  int acc[kWalk];
+  auto walk = [&](const uint32_t* p, auto first) {
     uint32_t x = 0;
 #pragma unroll
     for (int k = kWalkBits; k < kHiBits; ++k)
@@ -214,8 +223,16 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
 #pragma unroll
     for (int i = 0; i < kWalk; ++i) acc[i] = (i * 5 + tid) & 31;
   } else {
-    walk(0, std::true_type());  // columns without codes: planes 0, popc 0
-    for (int g = 1; g < wng; ++g) walk(g, std::false_type());
+    walk(pr[0], std::true_type());  // columns without codes: planes 0, popc 0
+#pragma unroll
+    for (int g = 1; g < kRegGroups; ++g)
+      if (g < wng) walk(pr[g], std::false_type());
+    for (int g = kRegGroups; g < wng; ++g) {  // dense columns: the rest from L2
+      uint32_t p[kHiBits];
+#pragma unroll
+      for (int k = 0; k < kHiBits; ++k) p[k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
+      walk(p, std::false_type());
+    }
   }
   if constexpr (ABL == 3) {
     const int z = zblk + (tid & 63);
@@ -224,8 +241,9 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
     for (int i = 0; i < kWalk; ++i) w += (uint32_t)acc[i] << (i & 7);
     if (z >= z0 && z < z1)
       reinterpret_cast<uint32_t*>(buf + (int64_t)(z - z0) * kLo + c0)[tid >> 6] = w;
-    return;
+    continue;
   }
+  __syncthreads();  // the previous walk's store-out reads of `stage` are done
   // 4-dword groups of a 16-dword column block XOR-swizzled by the block, so the
   // store-out's b128 reads of 16 consecutive columns are conflict-free
   auto sidx = [](int row, int col) { return row * 256 + (col ^ (((col >> 6) & 3) << 2)); };
@@ -281,6 +299,7 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
       *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + cb)) =
           make_uint4(out[j][0], out[j][1], out[j][2], out[j][3]);
     }
+  }
   }
 }
 
@@ -410,6 +429,137 @@ __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, in
   if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
 }
 
+// ---------------------------------------------------------------- MFMA tile (int8 seeds)
+// The first six butterfly levels are a 64-point Hadamard product on the matrix cores:
+// v_mfma_i32_16x16x64_i8 with A = 16 rows of H_64 (+-1 int8) and B = the int8 seed values
+// exactly as a 16-B load leaves them (lane l holds B[k = 16 (l >> 4) + j][n = l & 15],
+// verified by tools/mfma_i8_probe.hip), so the bytes go from HBM into the MFMA with no
+// unpacking.  Per slice, thread t's 16-B chunks j = 0..3 hold columns 16 t + r + 4096 j:
+// k = column bits 0..3 (r) and 8, 9 (lane bits 4, 5), n = column bits 4..7 (lane bits
+// 0..3).  Outputs C[row 4 (l >> 4) + i][col l & 15] of quarter q: transformed column bits
+// 0, 1 = i, 2, 3 = lane bits 4, 5, 8, 9 = q.  Then 2 register levels over j (bits 12, 13),
+// one int16 LDS exchange, 6 register levels over bits 4..7, 10, 11 -- whose register and
+// thread bits are whole 2-bit digits -- and the F^2 binning.
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef long v2l_t __attribute__((ext_vector_type(2)));
+
+// dword of the int16 pair holding column e: bits 0..4 = e1^e4, e2, e3^e5, e8^e6, e7, then
+// e4, e5, e6, e9..e13.  Conflict-free for the packed b32 stores (32-lane groups: e bits 2,
+// 4..7 vary) and the u16 loads (e bits 0..3, 8 vary; pairs share a dword).
+__device__ __forceinline__ int dmf(int e) {
+  return (((e >> 1) ^ (e >> 4)) & 1) | (((e >> 2) & 1) << 1) | ((((e >> 3) ^ (e >> 5)) & 1) << 2) |
+         ((((e >> 8) ^ (e >> 6)) & 1) << 3) | (((e >> 7) & 1) << 4) | (((e >> 4) & 7) << 5) | ((e >> 9) << 8);
+}
+
+// Slices: workgroup b takes a contiguous block of positions u; position u is slice
+// z0 + order[u] (order = a whole aligned chunk's offsets sorted by digit weight, so a
+// workgroup's slices share their weight for long runs and F^2 is binned in registers,
+// flushed to LDS only when it changes), or z0 + u (order = nullptr).
+__global__ __launch_bounds__(256) void tile_mfma_kernel(const int8_t* __restrict__ buf,
+                                                        const uint16_t* __restrict__ order, int z0,
+                                                        int nslices, unsigned long long* __restrict__ counts) {
+  __shared__ uint32_t lds32[kLo / 2];
+  __shared__ unsigned long long bins[17];
+  const int16_t* lds16 = reinterpret_cast<const int16_t*>(lds32);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 17) bins[tid] = 0;
+  v2l_t A[4];  // H_64 rows 16 q + (l & 15), columns 16 (l >> 4) + j
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * q + (lane & 15), col = 16 * (lane >> 4) + 4 * d + r;
+        v |= ((__popc(row & col) & 1) ? 0xFFu : 0x01u) << (8 * r);
+      }
+      w[d] = v;
+    }
+    A[q] = v2l_t{(long)(((uint64_t)w[1] << 32) | w[0]), (long)(((uint64_t)w[3] << 32) | w[2])};
+  }
+  const int wt_thread = digit_weight((uint32_t)(lane & 15) | ((uint32_t)(lane >> 4) << 8) | ((uint32_t)wave << 12));
+  const int ew = ((lane >> 4) << 2) | ((lane & 15) << 4) | (wave << 10);       // store-side e bits
+  const int er = (lane & 15) | ((lane >> 4) << 8) | (wave << 12);              // load-side e bits
+  // the next slice's chunks are loaded while this one is transformed (HBM latency is
+  // otherwise exposed once per slice at 2 workgroups per CU)
+  v2l_t B[4], Bn[4];
+  auto slice_of = [&](int u) { return order ? (int)order[u] : u; };
+  auto load = [&](int s, v2l_t* dst) {
+    const int8_t* row = buf + (int64_t)s * kLo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      dst[j] = __builtin_nontemporal_load(reinterpret_cast<const v2l_t*>(row + 16 * tid + 4096 * j));
+  };
+  const int ub = (int)((int64_t)nslices * blockIdx.x / gridDim.x);
+  const int ue = (int)((int64_t)nslices * (blockIdx.x + 1) / gridDim.x);
+  unsigned long long tot[4] = {0, 0, 0, 0};
+  int cur_w = -1;
+  auto flush = [&]() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tot[k]) atomicAdd(&bins[cur_w + wt_thread + k], tot[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tot[k] = 0;
+  };
+  if (ub < ue) load(slice_of(ub), Bn);
+  for (int u = ub; u < ue; ++u) {
+    const int s = slice_of(u);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) B[j] = Bn[j];
+    if (u + 1 < ue) load(slice_of(u + 1), Bn);
+    int32_t x[64];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const v4i_t c = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[q], B[j], v4i_t{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[j * 16 + q * 4 + i] = c[i];
+      }
+#pragma unroll
+    for (int qi = 0; qi < 16; ++qi) {  // column bits 12, 13 (registers j)
+      int32_t y[4] = {x[qi], x[16 + qi], x[32 + qi], x[48 + qi]};
+      wht<4>(y);
+      x[qi] = y[0];
+      x[16 + qi] = y[1];
+      x[32 + qi] = y[2];
+      x[48 + qi] = y[3];
+    }
+    __syncthreads();  // the previous slice's loads from LDS are done
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int ip = 0; ip < 2; ++ip) {
+          const int e = ew | (2 * ip) | (q << 8) | (j << 12);
+          const int k = j * 16 + q * 4 + 2 * ip;
+          lds32[dmf(e)] = ((uint32_t)x[k] & 0xFFFFu) | ((uint32_t)x[k + 1] << 16);
+        }
+    __syncthreads();
+#pragma unroll
+    for (int q2 = 0; q2 < 64; ++q2) {  // registers = column bits 4..7, 10, 11
+      const int e = er | ((q2 & 15) << 4) | ((q2 >> 4) << 10);
+      x[q2] = lds16[2 * dmf(e) + (e & 1)];
+    }
+    wht<64>(x);
+    const int wz = digit_weight((uint32_t)(z0 + s));  // workgroup-uniform
+    if (wz != cur_w) {
+      if (cur_w >= 0) flush();
+      cur_w = wz;
+    }
+#pragma unroll
+    for (int q2 = 0; q2 < 64; ++q2)
+      tot[digit_weight_c((uint32_t)(q2 & 15)) + digit_weight_c((uint32_t)(q2 >> 4))] +=
+          (unsigned long long)((int64_t)x[q2] * x[q2]);
+  }
+  if (cur_w >= 0) flush();
+  __syncthreads();
+  if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
+}
+
 __global__ void max_column_kernel(const uint32_t* __restrict__ off, unsigned* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < kLo) atomicMax(out, off[c + 1] - off[c]);
@@ -421,7 +571,7 @@ template <typename T>
 int launch_seed(State& st, int z0, int z1, hipStream_t s) {
   T* buf = reinterpret_cast<T*>(st.d_buf);
   const int walks = (z1 - (z0 & ~(kWalk - 1)) + kWalk - 1) / kWalk;
-  const dim3 sgrid(kLo / 256, (unsigned)walks);
+  const dim3 sgrid(kLo / 256, (unsigned)((walks + kSeedWalks - 1) / kSeedWalks));
 #ifdef SCT_ABLATION
   static const int sabl = getenv("SCT_SEED_ABL") ? atoi(getenv("SCT_SEED_ABL")) : 0;
   if (sabl == 1)
@@ -456,6 +606,16 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
     return SCT_OK;
   }
 #endif
+  if constexpr (sizeof(T) == 1) {
+    if (st.mfma) {
+      // whole aligned chunks go in digit-weight order (one table serves every chunk)
+      const uint16_t* order = (z0 % 65536 == 0 && z1 - z0 == 65536) ? st.d_order : nullptr;
+      hipLaunchKernelGGL(tile_mfma_kernel, dim3((unsigned)std::min(st.grid * 2, z1 - z0)), dim3(256), 0, s, buf,
+                         order, z0, z1 - z0, counts);
+      SCT_LAUNCH_CHECK();
+      return SCT_OK;
+    }
+  }
   hipLaunchKernelGGL(tile_kernel<T>, grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
@@ -525,6 +685,16 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   unsigned maxm = 0;
   SCT_HIP(hipMemcpy(&maxm, dmax.p, 4, hipMemcpyDeviceToHost));
   st.elem_bytes = maxm <= 127 ? 1 : (maxm <= 32767 ? 2 : 4);
+  const char* mf = getenv("SCT_SPECTRAL_MFMA");  // 0: VALU tile kernel for int8 seeds too
+  st.mfma = !(mf && atoi(mf) == 0);
+  {
+    std::vector<uint16_t> order(65536);
+    for (int u = 0; u < 65536; ++u) order[u] = (uint16_t)u;
+    std::stable_sort(order.begin(), order.end(),
+                     [](uint16_t a, uint16_t b) { return digit_weight_c(a) < digit_weight_c(b); });
+    SCT_HIP(hipMalloc(&st.d_order, order.size() * 2));
+    SCT_HIP(hipMemcpy(st.d_order, order.data(), order.size() * 2, hipMemcpyHostToDevice));
+  }
   if (const char* w = getenv("SCT_SPECTRAL_BYTES")) {  // test hook: wider than needed
     const int b = atoi(w);
     if ((b == 2 || b == 4) && b > st.elem_bytes) st.elem_bytes = b;
@@ -538,7 +708,7 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
 
 void destroy(State& st) {
   for (void* p : {(void*)st.d_sorted, (void*)st.d_off, (void*)st.d_gofs, (void*)st.d_planes, st.d_buf,
-                  st.d_sort_tmp})
+                  st.d_sort_tmp, (void*)st.d_order})
     if (p) (void)hipFree(p);
   st = State();
 }

@@ -1,0 +1,13 @@
+# PMC passes over the SPECTRAL kernels (tools/spectral_time.py, config ${SP_CONFIG:-2}).
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/proft
+B="python3 tools/spectral_time.py ${SP_CONFIG:-2} 2"
+i=0
+for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS" \
+           "SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE GRBM_COUNT" \
+           "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_MISC SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_INST_LEVEL_LDS SQ_INSTS_VMEM_RD SQ_CYCLES"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $pmc -d gpurun_out/proft/pmc$i -o run --output-format csv -- $B > gpurun_out/proft/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; }
+done
