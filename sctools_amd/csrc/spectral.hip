@@ -34,6 +34,9 @@ constexpr int kWalk = 64;                 // slices per wave in the seed's Gray 
 constexpr int kWalkBits = 6;
 constexpr int kRegGroups = 2;             // seed: 32-code groups whose planes stay in registers
 constexpr int kSeedWalks = 8;             // seed: walks per workgroup
+// MFMA tile: load the next slice while transforming this one.  Measured no faster (the
+// kernel is not waiting on HBM) and it costs 16 VGPRs: off.
+constexpr bool kTilePrefetch = false;
 
 // non-zero 2-bit digits of z
 __device__ __forceinline__ int digit_weight(uint32_t z) {
@@ -455,7 +458,7 @@ __device__ __forceinline__ int dmf(int e) {
 // z0 + order[u] (order = a whole aligned chunk's offsets sorted by digit weight, so a
 // workgroup's slices share their weight for long runs and F^2 is binned in registers,
 // flushed to LDS only when it changes), or z0 + u (order = nullptr).
-__global__ __launch_bounds__(256) void tile_mfma_kernel(const int8_t* __restrict__ buf,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_mfma_kernel(const int8_t* __restrict__ buf,
                                                         const uint16_t* __restrict__ order, int z0,
                                                         int nslices, unsigned long long* __restrict__ counts) {
   __shared__ uint32_t lds32[kLo / 2];
@@ -482,8 +485,6 @@ __global__ __launch_bounds__(256) void tile_mfma_kernel(const int8_t* __restrict
   const int wt_thread = digit_weight((uint32_t)(lane & 15) | ((uint32_t)(lane >> 4) << 8) | ((uint32_t)wave << 12));
   const int ew = ((lane >> 4) << 2) | ((lane & 15) << 4) | (wave << 10);       // store-side e bits
   const int er = (lane & 15) | ((lane >> 4) << 8) | (wave << 12);              // load-side e bits
-  // the next slice's chunks are loaded while this one is transformed (HBM latency is
-  // otherwise exposed once per slice at 2 workgroups per CU)
   v2l_t B[4], Bn[4];
   auto slice_of = [&](int u) { return order ? (int)order[u] : u; };
   auto load = [&](int s, v2l_t* dst) {
@@ -503,12 +504,16 @@ __global__ __launch_bounds__(256) void tile_mfma_kernel(const int8_t* __restrict
 #pragma unroll
     for (int k = 0; k < 4; ++k) tot[k] = 0;
   };
-  if (ub < ue) load(slice_of(ub), Bn);
   for (int u = ub; u < ue; ++u) {
     const int s = slice_of(u);
+    if constexpr (kTilePrefetch) {
+      if (u == ub) load(s, Bn);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) B[j] = Bn[j];
-    if (u + 1 < ue) load(slice_of(u + 1), Bn);
+      for (int j = 0; j < 4; ++j) B[j] = Bn[j];
+      if (u + 1 < ue) load(slice_of(u + 1), Bn);
+    } else {
+      load(s, B);
+    }
     int32_t x[64];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -610,7 +615,7 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
     if (st.mfma) {
       // whole aligned chunks go in digit-weight order (one table serves every chunk)
       const uint16_t* order = (z0 % 65536 == 0 && z1 - z0 == 65536) ? st.d_order : nullptr;
-      hipLaunchKernelGGL(tile_mfma_kernel, dim3((unsigned)std::min(st.grid * 2, z1 - z0)), dim3(256), 0, s, buf,
+      hipLaunchKernelGGL(tile_mfma_kernel, dim3((unsigned)std::min(st.grid * st.tile_wgs, z1 - z0)), dim3(256), 0, s, buf,
                          order, z0, z1 - z0, counts);
       SCT_LAUNCH_CHECK();
       return SCT_OK;
@@ -687,6 +692,13 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   st.elem_bytes = maxm <= 127 ? 1 : (maxm <= 32767 ? 2 : 4);
   const char* mf = getenv("SCT_SPECTRAL_MFMA");  // 0: VALU tile kernel for int8 seeds too
   st.mfma = !(mf && atoi(mf) == 0);
+  {
+    int per_cu = 0;  // resident MFMA-tile workgroups per CU (VGPR / LDS bound)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma_kernel, 256, 0) != hipSuccess ||
+        per_cu <= 0)
+      per_cu = 2;
+    st.tile_wgs = per_cu;
+  }
   {
     std::vector<uint16_t> order(65536);
     for (int u = 0; u < 65536; ++u) order[u] = (uint16_t)u;
