@@ -118,7 +118,7 @@ def spectral_roofline(tk, step_count_ms, my_slices):
     launches = -(-my_slices // per_launch)
     return {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12, "unit": "Tops/s",
             "frac": achieved / VALU_PEAK_OPS, "traffic": _traffic("pmc_spectral_latest.json"),
-            "kernel": "sct_spectral::tile_kernel<int8>", "kernel_ms": tk["kernel_ms"],
+            "kernel": "sct_spectral::tile_mfma_kernel (int8 seeds)", "kernel_ms": tk["kernel_ms"],
             "slices_per_launch": per_launch, "launches_per_step": launches,
             "algo_ops_per_slice": SPECTRAL_OPS_PER_SLICE, "seed_kernel_ms": tk["seed_ms"],
             "count_ms_per_step": step_count_ms,

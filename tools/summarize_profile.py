@@ -38,7 +38,7 @@ def kernel_avg_ns(stats_csv, kernel_substr):
     return None, 0
 
 
-KERNELS = (("allpairs", "allpairs_count_kernel<8"), ("spectral", "tile_kernel<signed char"))
+KERNELS = (("allpairs", "allpairs_count_kernel<8"), ("spectral", "tile_mfma_kernel"))
 
 
 def summarize(src, dst, rnd, name, kernel, pairs):
