@@ -614,7 +614,10 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
   if constexpr (sizeof(T) == 1) {
     if (st.mfma) {
       // whole aligned chunks go in digit-weight order (one table serves every chunk)
-      const uint16_t* order = (z0 % 65536 == 0 && z1 - z0 == 65536) ? st.d_order : nullptr;
+      const uint16_t* order =
+          ((st.chunk & (st.chunk - 1)) == 0 && st.chunk <= 65536 && z0 % st.chunk == 0 && z1 - z0 == st.chunk)
+              ? st.d_order
+              : nullptr;
       hipLaunchKernelGGL(tile_mfma_kernel, dim3((unsigned)std::min(st.grid * st.tile_wgs, z1 - z0)), dim3(256), 0, s, buf,
                          order, z0, z1 - z0, counts);
       SCT_LAUNCH_CHECK();
@@ -700,8 +703,10 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
     st.tile_wgs = per_cu;
   }
   {
-    std::vector<uint16_t> order(65536);
-    for (int u = 0; u < 65536; ++u) order[u] = (uint16_t)u;
+    // offsets of an aligned chunk (a power of two <= 65536) sorted by digit weight
+    const int len = (st.chunk & (st.chunk - 1)) == 0 && st.chunk <= 65536 ? (int)st.chunk : 0;
+    std::vector<uint16_t> order(std::max(len, 1));
+    for (int u = 0; u < len; ++u) order[u] = (uint16_t)u;
     std::stable_sort(order.begin(), order.end(),
                      [](uint16_t a, uint16_t b) { return digit_weight_c(a) < digit_weight_c(b); });
     SCT_HIP(hipMalloc(&st.d_order, order.size() * 2));
