@@ -523,14 +523,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
 #pragma unroll
         for (int i = 0; i < 4; ++i) x[j * 16 + q * 4 + i] = c[i];
       }
+    // pack column pairs (bit 0) into int16x2 -- |x| <= 64 * 127 here and <= 256 * 127
+    // after the next two levels -- and do those levels packed (v_pk_add/sub_u16; the
+    // arithmetic wraps mod 2^16 and the results are in range, so it is exact)
+    typedef short s2_t __attribute__((ext_vector_type(2)));
+    s2_t pk[32];  // pk[j * 8 + q * 2 + ip] = (x[k], x[k + 1]), k = j * 16 + q * 4 + 2 ip
 #pragma unroll
-    for (int qi = 0; qi < 16; ++qi) {  // column bits 12, 13 (registers j)
-      int32_t y[4] = {x[qi], x[16 + qi], x[32 + qi], x[48 + qi]};
-      wht<4>(y);
-      x[qi] = y[0];
-      x[16 + qi] = y[1];
-      x[32 + qi] = y[2];
-      x[48 + qi] = y[3];
+    for (int k = 0; k < 64; k += 2)
+      pk[k / 2] = __builtin_bit_cast(s2_t, __builtin_amdgcn_perm((uint32_t)x[k + 1], (uint32_t)x[k], 0x05040100u));
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {  // column bits 12, 13 (registers j)
+      const s2_t a = pk[r], b = pk[8 + r], c = pk[16 + r], d = pk[24 + r];
+      const s2_t ab0 = a + b, ab1 = a - b, cd0 = c + d, cd1 = c - d;
+      pk[r] = ab0 + cd0;
+      pk[8 + r] = ab1 + cd1;
+      pk[16 + r] = ab0 - cd0;
+      pk[24 + r] = ab1 - cd1;
     }
     __syncthreads();  // the previous slice's loads from LDS are done
 #pragma unroll
@@ -540,8 +548,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
 #pragma unroll
         for (int ip = 0; ip < 2; ++ip) {
           const int e = ew | (2 * ip) | (q << 8) | (j << 12);
-          const int k = j * 16 + q * 4 + 2 * ip;
-          lds32[dmf(e)] = ((uint32_t)x[k] & 0xFFFFu) | ((uint32_t)x[k + 1] << 16);
+          lds32[dmf(e)] = __builtin_bit_cast(uint32_t, pk[j * 8 + q * 2 + ip]);
         }
     __syncthreads();
 #pragma unroll
