@@ -15,8 +15,9 @@ constexpr int kNCounts = 1 + 17;               // [n, S_0..S_16]
 // Device state of a SPECTRAL plan (owned by sct_allpairs_plan).
 struct State {
   int64_t n = 0;
-  uint64_t* d_sorted = nullptr;  // codes sorted by their low 14 bits
+  uint32_t* d_hi = nullptr;      // code >> 14 of every code, grouped by column (low 14 bits)
   uint32_t* d_off = nullptr;     // [2^14 + 1] first code of each low-14-bit column
+  uint32_t* d_cnt = nullptr;     // [2][2^14] column counts, scatter cursors
   uint32_t* d_gofs = nullptr;    // [2^14 + 1] first 32-code group of each column
   uint32_t* d_planes = nullptr;  // [groups][18] bit planes of the groups' code >> 14
   int64_t max_groups = 0;
@@ -26,8 +27,6 @@ struct State {
   int tile_wgs = 2;              // resident MFMA-tile workgroups per CU
   void* d_buf = nullptr;         // chunk slices x 2^14 seed values
   int64_t chunk = 0;             // slices per pass
-  void* d_sort_tmp = nullptr;
-  size_t sort_tmp_bytes = 0;
   int grid = 0;                  // compute units (the tile kernel's persistent grid)
 };
 
@@ -35,7 +34,7 @@ struct State {
 // codes' densest column; returns an SCT_* code
 int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus);
 void destroy(State& st);
-// sort + split the codes (any slice range needs all of them)
+// group the codes by column + bit planes (any slice range needs all of them)
 int build(State& st, const uint64_t* d_codes, hipStream_t s);
 // add the counts of slices [z_begin, z_end): d_counts[1 + w] += S_w over those slices,
 // d_counts[0] += n when z_begin == 0

@@ -20,7 +20,6 @@
 #include <vector>
 #include <type_traits>
 
-#include <hipcub/hipcub.hpp>
 
 #include "sct_common.h"
 #include "spectral.h"
@@ -71,49 +70,65 @@ __device__ __forceinline__ void wht(int32_t* x) {
       }
 }
 
-// off[c] = first sorted index whose column (low 14 bits) is >= c, c = 0..2^14
-__global__ void offsets_kernel(const uint64_t* __restrict__ sorted, int64_t n, uint32_t* __restrict__ off) {
-  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (c > kLo) return;
-  int64_t a = 0, b = n;
-  while (a < b) {
-    const int64_t m = (a + b) >> 1;
-    if ((int64_t)(sorted[m] & (kLo - 1)) < c) a = m + 1;
-    else b = m;
-  }
-  off[c] = (uint32_t)a;
+// Counting sort of the codes by column (low 14 bits): only code >> 14 is kept, in column
+// order (the order inside a column is whatever the atomics give: every use of a column's
+// codes is an order-independent sum).
+__global__ void column_hist_kernel(const uint64_t* __restrict__ codes, int64_t n, uint32_t* __restrict__ cnt) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&cnt[codes[i] & (kLo - 1)], 1u);
 }
 
-// gofs[c] = sum over columns c' < c of ceil(m(c') / 32); one workgroup of 256
-__global__ __launch_bounds__(256) void group_offsets_kernel(const uint32_t* __restrict__ off,
-                                                            uint32_t* __restrict__ gofs) {
-  __shared__ uint32_t part[256];
+// One workgroup of 256: off = exclusive prefix of the column counts, gofs = of their
+// 32-code group counts (both with the total at [2^14]); cursor = off (scatter positions).
+__global__ __launch_bounds__(256) void column_scan_kernel(const uint32_t* __restrict__ cnt,
+                                                          uint32_t* __restrict__ off,
+                                                          uint32_t* __restrict__ gofs,
+                                                          uint32_t* __restrict__ cursor) {
+  __shared__ uint32_t part[2][256];
   constexpr int per = kLo / 256;
   const int t = threadIdx.x;
-  uint32_t s = 0;
+  uint32_t s = 0, sg = 0;
   for (int k = 0; k < per; ++k) {
-    const int c = t * per + k;
-    s += (off[c + 1] - off[c] + 31) / 32;
+    const uint32_t m = cnt[t * per + k];
+    s += m;
+    sg += (m + 31) / 32;
   }
-  part[t] = s;
+  part[0][t] = s;
+  part[1][t] = sg;
   __syncthreads();
-  for (int d = 1; d < 256; d <<= 1) {  // inclusive Hillis-Steele scan
-    const uint32_t v = t >= d ? part[t - d] : 0;
+  for (int d = 1; d < 256; d <<= 1) {  // inclusive Hillis-Steele scans
+    const uint32_t v = t >= d ? part[0][t - d] : 0, vg = t >= d ? part[1][t - d] : 0;
     __syncthreads();
-    part[t] += v;
+    part[0][t] += v;
+    part[1][t] += vg;
     __syncthreads();
   }
-  uint32_t run = part[t] - s;
+  uint32_t run = part[0][t] - s, rung = part[1][t] - sg;
   for (int k = 0; k < per; ++k) {
     const int c = t * per + k;
-    gofs[c] = run;
-    run += (off[c + 1] - off[c] + 31) / 32;
+    const uint32_t m = cnt[c];
+    off[c] = run;
+    cursor[c] = run;
+    gofs[c] = rung;
+    run += m;
+    rung += (m + 31) / 32;
   }
-  if (t == 255) gofs[kLo] = run;
+  if (t == 255) {
+    off[kLo] = run;
+    gofs[kLo] = rung;
+  }
+}
+
+__global__ void column_scatter_kernel(const uint64_t* __restrict__ codes, int64_t n, uint32_t* __restrict__ cursor,
+                                      uint32_t* __restrict__ hi) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t x = codes[i];
+    hi[atomicAdd(&cursor[x & (kLo - 1)], 1u)] = (uint32_t)(x >> kLoBits);
+  }
 }
 
 // planes[k * max_groups + g] bit j = bit k of (code >> 14) of the j-th code of group g
-__global__ void planes_kernel(const uint64_t* __restrict__ sorted, const uint32_t* __restrict__ off,
+__global__ void planes_kernel(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ off,
                               const uint32_t* __restrict__ gofs, int64_t max_groups,
                               uint32_t* __restrict__ planes) {
   const int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -130,7 +145,7 @@ __global__ void planes_kernel(const uint64_t* __restrict__ sorted, const uint32_
 #pragma unroll
   for (int k = 0; k < kHiBits; ++k) p[k] = 0;
   for (uint32_t i = first; i < last; ++i) {
-    const uint32_t h = (uint32_t)(sorted[i] >> kLoBits), bit = 1u << (i - first);
+    const uint32_t h = hi[i], bit = 1u << (i - first);
 #pragma unroll
     for (int k = 0; k < kHiBits; ++k) p[k] |= (h >> k) & 1u ? bit : 0u;
   }
@@ -572,9 +587,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
 }
 
-__global__ void max_column_kernel(const uint32_t* __restrict__ off, unsigned* __restrict__ out) {
+__global__ void max_column_kernel(const uint32_t* __restrict__ cnt, unsigned* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < kLo) atomicMax(out, off[c + 1] - off[c]);
+  if (c < kLo) atomicMax(out, cnt[c]);
 }
 
 __global__ void add_kernel(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
@@ -680,22 +695,18 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   st.chunk = std::max<int64_t>(kWalk, std::min<int64_t>(chunk, kSlices));
   st.grid = std::max(1, cus);  // CUs; the tile kernel runs 3 workgroups per CU (int8), else 2
   if (n < 2) return SCT_OK;
-  SCT_HIP(hipMalloc(&st.d_sorted, (size_t)n * 8));
+  SCT_HIP(hipMalloc(&st.d_hi, (size_t)n * 4));
   SCT_HIP(hipMalloc(&st.d_off, (size_t)(kLo + 1) * 4));
-  SCT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, st.sort_tmp_bytes, (const uint64_t*)nullptr,
-                                            (uint64_t*)nullptr, (int)n, 0, kLoBits));
-  SCT_HIP(hipMalloc(&st.d_sort_tmp, std::max<size_t>(st.sort_tmp_bytes, 16)));
+  SCT_HIP(hipMalloc(&st.d_cnt, (size_t)2 * kLo * 4));  // counts, then scatter cursors
   // the densest column bounds |seed| and so the intermediate's width (the codes are
   // fixed for the plan's life)
-  size_t bytes = st.sort_tmp_bytes;
-  SCT_HIP(hipcub::DeviceRadixSort::SortKeys(st.d_sort_tmp, bytes, d_codes, st.d_sorted, (int)n, 0, kLoBits));
-  hipLaunchKernelGGL(offsets_kernel, dim3((unsigned)sct::ceil_div(kLo + 1, 256)), dim3(256), 0, 0,
-                     st.d_sorted, n, st.d_off);
+  SCT_HIP(hipMemset(st.d_cnt, 0, (size_t)kLo * 4));
+  hipLaunchKernelGGL(column_hist_kernel, dim3(1024), dim3(256), 0, 0, d_codes, n, st.d_cnt);
   SCT_LAUNCH_CHECK();
   sct::DevBuf dmax;
   SCT_HIP(dmax.alloc(4));
   SCT_HIP(hipMemset(dmax.p, 0, 4));
-  hipLaunchKernelGGL(max_column_kernel, dim3(kLo / 256), dim3(256), 0, 0, st.d_off, (unsigned*)dmax.p);
+  hipLaunchKernelGGL(max_column_kernel, dim3(kLo / 256), dim3(256), 0, 0, st.d_cnt, (unsigned*)dmax.p);
   SCT_LAUNCH_CHECK();
   unsigned maxm = 0;
   SCT_HIP(hipMemcpy(&maxm, dmax.p, 4, hipMemcpyDeviceToHost));
@@ -731,24 +742,24 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
 }
 
 void destroy(State& st) {
-  for (void* p : {(void*)st.d_sorted, (void*)st.d_off, (void*)st.d_gofs, (void*)st.d_planes, st.d_buf,
-                  st.d_sort_tmp, (void*)st.d_order})
+  for (void* p : {(void*)st.d_hi, (void*)st.d_off, (void*)st.d_cnt, (void*)st.d_gofs, (void*)st.d_planes,
+                  st.d_buf, (void*)st.d_order})
     if (p) (void)hipFree(p);
   st = State();
 }
 
 int build(State& st, const uint64_t* d_codes, hipStream_t s) {
   if (st.n < 2) return SCT_OK;
-  size_t bytes = st.sort_tmp_bytes;
-  SCT_HIP(hipcub::DeviceRadixSort::SortKeys(st.d_sort_tmp, bytes, d_codes, st.d_sorted, (int)st.n, 0,
-                                            kLoBits, s));
-  hipLaunchKernelGGL(offsets_kernel, dim3((unsigned)sct::ceil_div(kLo + 1, 256)), dim3(256), 0, s,
-                     st.d_sorted, st.n, st.d_off);
+  SCT_HIP(hipMemsetAsync(st.d_cnt, 0, (size_t)kLo * 4, s));
+  const unsigned g = (unsigned)std::min<int64_t>(1024, sct::ceil_div(st.n, 256));
+  hipLaunchKernelGGL(column_hist_kernel, dim3(g), dim3(256), 0, s, d_codes, st.n, st.d_cnt);
   SCT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(group_offsets_kernel, dim3(1), dim3(256), 0, s, st.d_off, st.d_gofs);
+  hipLaunchKernelGGL(column_scan_kernel, dim3(1), dim3(256), 0, s, st.d_cnt, st.d_off, st.d_gofs, st.d_cnt + kLo);
+  SCT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(column_scatter_kernel, dim3(g), dim3(256), 0, s, d_codes, st.n, st.d_cnt + kLo, st.d_hi);
   SCT_LAUNCH_CHECK();
   hipLaunchKernelGGL(planes_kernel, dim3((unsigned)sct::ceil_div(st.max_groups, 256)), dim3(256), 0, s,
-                     st.d_sorted, st.d_off, st.d_gofs, st.max_groups, st.d_planes);
+                     st.d_hi, st.d_off, st.d_gofs, st.max_groups, st.d_planes);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
