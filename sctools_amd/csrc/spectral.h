@@ -23,7 +23,7 @@ struct State {
   int64_t max_groups = 0;
   int elem_bytes = 1;            // seed -> tile intermediate: int8 / int16 / int32
   bool mfma = true;              // int8 seeds: first 6 butterfly levels on the matrix cores
-  uint16_t* d_order = nullptr;   // [65536] slice offsets of a chunk sorted by digit weight
+  uint16_t* d_order = nullptr;   // [2^17]: at [L, 2L) the offsets [0, L) sorted by digit weight
   int tile_wgs = 2;              // resident MFMA-tile workgroups per CU
   void* d_buf = nullptr;         // chunk slices x 2^14 seed values
   int64_t chunk = 0;             // slices per pass

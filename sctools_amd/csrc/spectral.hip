@@ -33,6 +33,7 @@ constexpr int kWalk = 64;                 // slices per wave in the seed's Gray 
 constexpr int kWalkBits = 6;
 constexpr int kRegGroups = 2;             // seed: 32-code groups whose planes stay in registers
 constexpr int kSeedWalks = 8;             // seed: walks per workgroup
+constexpr int kMaxOrder = 1 << 16;        // largest slice range with a digit-weight order table
 // MFMA tile: load the next slice while transforming this one.  Measured no faster (the
 // kernel is not waiting on HBM) and it costs 16 VGPRs: off.
 constexpr bool kTilePrefetch = false;
@@ -635,11 +636,10 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
 #endif
   if constexpr (sizeof(T) == 1) {
     if (st.mfma) {
-      // whole aligned chunks go in digit-weight order (one table serves every chunk)
+      // an aligned power-of-two range goes in digit-weight order (table 2^b at offset 2^b)
+      const int ns = z1 - z0;
       const uint16_t* order =
-          ((st.chunk & (st.chunk - 1)) == 0 && st.chunk <= 65536 && z0 % st.chunk == 0 && z1 - z0 == st.chunk)
-              ? st.d_order
-              : nullptr;
+          ((ns & (ns - 1)) == 0 && ns <= kMaxOrder && z0 % ns == 0) ? st.d_order + ns : nullptr;
       hipLaunchKernelGGL(tile_mfma_kernel, dim3((unsigned)std::min(st.grid * st.tile_wgs, z1 - z0)), dim3(256), 0, s, buf,
                          order, z0, z1 - z0, counts);
       SCT_LAUNCH_CHECK();
@@ -721,12 +721,14 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
     st.tile_wgs = per_cu;
   }
   {
-    // offsets of an aligned chunk (a power of two <= 65536) sorted by digit weight
-    const int len = (st.chunk & (st.chunk - 1)) == 0 && st.chunk <= 65536 ? (int)st.chunk : 0;
-    std::vector<uint16_t> order(std::max(len, 1));
-    for (int u = 0; u < len; ++u) order[u] = (uint16_t)u;
-    std::stable_sort(order.begin(), order.end(),
-                     [](uint16_t a, uint16_t b) { return digit_weight_c(a) < digit_weight_c(b); });
+    // for every power of two L <= 2^16: the offsets [0, L) sorted by digit weight, stored
+    // at [L, 2L) (an aligned range of L slices adds a constant weight to all of them)
+    std::vector<uint16_t> order(2 * kMaxOrder);
+    for (int len = 1; len <= kMaxOrder; len *= 2) {
+      uint16_t* o = order.data() + len;
+      for (int u = 0; u < len; ++u) o[u] = (uint16_t)u;
+      std::stable_sort(o, o + len, [](uint16_t a, uint16_t b) { return digit_weight_c(a) < digit_weight_c(b); });
+    }
     SCT_HIP(hipMalloc(&st.d_order, order.size() * 2));
     SCT_HIP(hipMemcpy(st.d_order, order.data(), order.size() * 2, hipMemcpyHostToDevice));
   }
