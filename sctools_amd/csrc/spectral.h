@@ -17,7 +17,9 @@ struct State {
   int64_t n = 0;
   uint32_t* d_hi = nullptr;      // code >> 14 of every code, grouped by column (low 14 bits)
   uint32_t* d_off = nullptr;     // [2^14 + 1] first code of each low-14-bit column
-  uint32_t* d_cnt = nullptr;     // [2][2^14] column counts, scatter cursors
+  uint32_t* d_cnt = nullptr;     // [2][2^14] column counts
+  uint32_t* d_hist = nullptr;    // [128][2^14] per-workgroup column counts -> prefixes (build)
+  unsigned max_m = 0;            // codes in the densest column
   uint32_t* d_gofs = nullptr;    // [2^14 + 1] first 32-code group of each column
   uint32_t* d_planes = nullptr;  // [groups][18] bit planes of the groups' code >> 14
   int64_t max_groups = 0;

@@ -79,53 +79,145 @@ __global__ void column_hist_kernel(const uint64_t* __restrict__ codes, int64_t n
     atomicAdd(&cnt[codes[i] & (kLo - 1)], 1u);
 }
 
-// One workgroup of 256: off = exclusive prefix of the column counts, gofs = of their
-// 32-code group counts (both with the total at [2^14]); cursor = off (scatter positions).
-__global__ __launch_bounds__(256) void column_scan_kernel(const uint32_t* __restrict__ cnt,
-                                                          uint32_t* __restrict__ off,
-                                                          uint32_t* __restrict__ gofs,
-                                                          uint32_t* __restrict__ cursor) {
-  __shared__ uint32_t part[2][256];
-  constexpr int per = kLo / 256;
-  const int t = threadIdx.x;
-  uint32_t s = 0, sg = 0;
-  for (int k = 0; k < per; ++k) {
-    const uint32_t m = cnt[t * per + k];
-    s += m;
-    sg += (m + 31) / 32;
-  }
-  part[0][t] = s;
-  part[1][t] = sg;
+// Privatised counting sort (the build of every step; no global atomics):
+//   hist_wg   workgroup g counts its contiguous share of the codes per column in LDS and
+//             writes the 2^14 counts to H[g][.]
+//   prefix    per column: H[g][c] <- sum of H[g' < g][c] (in place), m(c) = the total
+//   scan      one workgroup: off / gofs = exclusive scans of m(c) and ceil(m(c) / 32)
+//   scatter   workgroup g: LDS cursors off[c] + H[g][c], one LDS atomic per code
+constexpr int kSortWGs = 128;
+constexpr int kSortThreads = 1024;
+
+__device__ __forceinline__ void wg_range(int64_t n, int64_t& b, int64_t& e) {
+  b = n * blockIdx.x / gridDim.x;
+  e = n * (blockIdx.x + 1) / gridDim.x;
+}
+
+__global__ __launch_bounds__(kSortThreads) void column_hist_wg_kernel(const uint64_t* __restrict__ codes, int64_t n,
+                                                                      uint32_t* __restrict__ H) {
+  __shared__ uint32_t h[kLo];
+  for (int c = threadIdx.x; c < kLo; c += kSortThreads) h[c] = 0;
   __syncthreads();
-  for (int d = 1; d < 256; d <<= 1) {  // inclusive Hillis-Steele scans
-    const uint32_t v = t >= d ? part[0][t - d] : 0, vg = t >= d ? part[1][t - d] : 0;
-    __syncthreads();
-    part[0][t] += v;
-    part[1][t] += vg;
-    __syncthreads();
+  int64_t b, e;
+  wg_range(n, b, e);
+  for (int64_t i = b + threadIdx.x; i < e; i += kSortThreads) atomicAdd(&h[codes[i] & (kLo - 1)], 1u);
+  __syncthreads();
+  uint32_t* out = H + (int64_t)blockIdx.x * kLo;
+  for (int c = threadIdx.x; c < kLo; c += kSortThreads) out[c] = h[c];
+}
+
+__global__ __launch_bounds__(256) void column_prefix_kernel(uint32_t* __restrict__ H, int wgs,
+                                                            uint32_t* __restrict__ m) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  uint32_t run = 0;
+#pragma unroll 8
+  for (int g = 0; g < wgs; ++g) {
+    const uint32_t v = H[(int64_t)g * kLo + c];
+    H[(int64_t)g * kLo + c] = run;
+    run += v;
   }
-  uint32_t run = part[0][t] - s, rung = part[1][t] - sg;
-  for (int k = 0; k < per; ++k) {
-    const int c = t * per + k;
-    const uint32_t m = cnt[c];
-    off[c] = run;
-    cursor[c] = run;
-    gofs[c] = rung;
-    run += m;
-    rung += (m + 31) / 32;
+  m[c] = run;
+}
+
+// one workgroup of 1024: 16 columns per thread, wave scans + one LDS pass over the waves
+__global__ __launch_bounds__(1024) void column_scan16_kernel(const uint32_t* __restrict__ m,
+                                                             uint32_t* __restrict__ off,
+                                                             uint32_t* __restrict__ gofs) {
+  __shared__ uint32_t wsum[2][16];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t v[16];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 q = reinterpret_cast<const uint4*>(m)[t * 4 + k];
+    v[4 * k] = q.x;
+    v[4 * k + 1] = q.y;
+    v[4 * k + 2] = q.z;
+    v[4 * k + 3] = q.w;
   }
-  if (t == 255) {
+  uint32_t s = 0, sg = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    s += v[k];
+    sg += (v[k] + 31) / 32;
+  }
+  uint32_t is = s, isg = sg;  // inclusive scans over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t a = __shfl_up(is, d), ag = __shfl_up(isg, d);
+    if (lane >= d) {
+      is += a;
+      isg += ag;
+    }
+  }
+  if (lane == 63) {
+    wsum[0][wave] = is;
+    wsum[1][wave] = isg;
+  }
+  __syncthreads();
+  uint32_t base = 0, baseg = 0;
+  for (int w = 0; w < wave; ++w) {
+    base += wsum[0][w];
+    baseg += wsum[1][w];
+  }
+  uint32_t run = base + is - s, rung = baseg + isg - sg;
+  uint32_t o[16], og[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    o[k] = run;
+    og[k] = rung;
+    run += v[k];
+    rung += (v[k] + 31) / 32;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    reinterpret_cast<uint4*>(off)[t * 4 + k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+    reinterpret_cast<uint4*>(gofs)[t * 4 + k] = make_uint4(og[4 * k], og[4 * k + 1], og[4 * k + 2], og[4 * k + 3]);
+  }
+  if (t == 1023) {
     off[kLo] = run;
     gofs[kLo] = rung;
   }
 }
 
-__global__ void column_scatter_kernel(const uint64_t* __restrict__ codes, int64_t n, uint32_t* __restrict__ cursor,
-                                      uint32_t* __restrict__ hi) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+__global__ __launch_bounds__(kSortThreads) void column_scatter_wg_kernel(const uint64_t* __restrict__ codes,
+                                                                         int64_t n,
+                                                                         const uint32_t* __restrict__ H,
+                                                                         const uint32_t* __restrict__ off,
+                                                                         uint32_t* __restrict__ hi) {
+  __shared__ uint32_t cur[kLo];
+  const uint32_t* pre = H + (int64_t)blockIdx.x * kLo;
+  for (int c = threadIdx.x; c < kLo; c += kSortThreads) cur[c] = off[c] + pre[c];
+  __syncthreads();
+  int64_t b, e;
+  wg_range(n, b, e);
+  for (int64_t i = b + threadIdx.x; i < e; i += kSortThreads) {
     const uint64_t x = codes[i];
-    hi[atomicAdd(&cursor[x & (kLo - 1)], 1u)] = (uint32_t)(x >> kLoBits);
+    hi[atomicAdd(&cur[x & (kLo - 1)], 1u)] = (uint32_t)(x >> kLoBits);
   }
+}
+
+// planes of group slot k of column c (thread (c, k); columns of <= 32 * kSlots codes)
+template <int kSlots>
+__global__ __launch_bounds__(256) void planes_slot_kernel(const uint32_t* __restrict__ hi,
+                                                          const uint32_t* __restrict__ off,
+                                                          const uint32_t* __restrict__ gofs, int64_t max_groups,
+                                                          uint32_t* __restrict__ planes) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int c = t / kSlots, k = t % kSlots;
+  const uint32_t g0 = gofs[c];
+  if (k >= (int)(gofs[c + 1] - g0)) return;
+  const uint32_t first = off[c] + 32u * k, last = min(first + 32u, off[c + 1]);
+  uint32_t p[kHiBits];
+#pragma unroll
+  for (int b = 0; b < kHiBits; ++b) p[b] = 0;
+  for (uint32_t i = first; i < last; ++i) {
+    const uint32_t h = hi[i], bit = 1u << (i - first);
+#pragma unroll
+    for (int b = 0; b < kHiBits; ++b) p[b] |= (h >> b) & 1u ? bit : 0u;
+  }
+  const int64_t g = g0 + k;
+#pragma unroll
+  for (int b = 0; b < kHiBits; ++b) planes[b * max_groups + g] = p[b];
 }
 
 // planes[k * max_groups + g] bit j = bit k of (code >> 14) of the j-th code of group g
@@ -219,6 +311,24 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
   for (int g = 0; g < kRegGroups; ++g)
 #pragma unroll
     for (int k = 0; k < kHiBits; ++k) pr[g][k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
+  // int8 byte store-out: this thread writes columns c0 + mcb .. + 15; mx = their m | 0x80
+  // as bytes (ABL 4 = the same path, for A/B against the ablations)
+  constexpr bool kByteStage = sizeof(T) == 1 && (ABL == 0 || ABL == 4);
+  const int mcb = (tid & 15) * 16;
+  uint4 mx = make_uint4(0, 0, 0, 0);
+  if constexpr (kByteStage) {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      w[k] = 0x80808080u;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int cc = c0 + mcb + 4 * k + b;
+        w[k] |= (off[cc + 1] - off[cc]) << (8 * b);
+      }
+    }
+    mx = make_uint4(w[0], w[1], w[2], w[3]);
+  }
   const int za = z0 & ~(kWalk - 1);
   const int nwalks = (z1 - za + kWalk - 1) / kWalk;
   for (int wk = blockIdx.y; wk < nwalks; wk += gridDim.y) {
@@ -260,6 +370,28 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
     for (int i = 0; i < kWalk; ++i) w += (uint32_t)acc[i] << (i & 7);
     if (z >= z0 && z < z1)
       reinterpret_cast<uint32_t*>(buf + (int64_t)(z - z0) * kLo + c0)[tid >> 6] = w;
+    continue;
+  }
+  if constexpr (kByteStage) {
+    // int8: the raw popcount sums go to LDS as bytes (row = slice, byte = column; no
+    // packing), and the store-out forms m - 2 acc for 16 columns at once:
+    //   ((m | 0x80) - 2 acc) ^ 0x80 per byte -- acc <= m <= 127, so 2 acc fits a byte
+    //   and m + 128 - 2 acc lies in [1, 255]: no carry or borrow crosses a byte.
+    uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
+    __syncthreads();  // the previous walk's store-out reads of `stage` are done
+#pragma unroll
+    for (int i = 0; i < kWalk; ++i) st8[i * 256 + tid] = (uint8_t)acc[i];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kWalk / 16; ++r) {
+      const int row = (tid >> 4) + 16 * r;
+      const uint4 v = *reinterpret_cast<const uint4*>(st8 + row * 256 + mcb);
+      const uint4 o = make_uint4((mx.x - (v.x + v.x)) ^ 0x80808080u, (mx.y - (v.y + v.y)) ^ 0x80808080u,
+                                 (mx.z - (v.z + v.z)) ^ 0x80808080u, (mx.w - (v.w + v.w)) ^ 0x80808080u);
+      const int z = zblk + row;
+      if (z >= z0 && z < z1)
+        *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + mcb)) = o;
+    }
     continue;
   }
   __syncthreads();  // the previous walk's store-out reads of `stage` are done
@@ -474,6 +606,9 @@ __device__ __forceinline__ int dmf(int e) {
 // z0 + order[u] (order = a whole aligned chunk's offsets sorted by digit weight, so a
 // workgroup's slices share their weight for long runs and F^2 is binned in registers,
 // flushed to LDS only when it changes), or z0 + u (order = nullptr).
+// ABL (ablation builds only, wrong results by design): 1 = no global loads, 2 = no
+// phase-2 butterflies, 3 = no squares/bins, 4 = no LDS exchange, 5 = prefetch the next slice.
+template <int ABL = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_mfma_kernel(const int8_t* __restrict__ buf,
                                                         const uint16_t* __restrict__ order, int z0,
                                                         int nslices, unsigned long long* __restrict__ counts) {
@@ -522,7 +657,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   };
   for (int u = ub; u < ue; ++u) {
     const int s = slice_of(u);
-    if constexpr (kTilePrefetch) {
+    if constexpr (ABL == 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) B[j] = v2l_t{(long)(s * 0x9E3779B97F4A7C15ull + j), (long)tid};
+    } else if constexpr (kTilePrefetch || ABL == 5) {
       if (u == ub) load(s, Bn);
 #pragma unroll
       for (int j = 0; j < 4; ++j) B[j] = Bn[j];
@@ -556,6 +694,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
       pk[16 + r] = ab0 - cd0;
       pk[24 + r] = ab1 - cd1;
     }
+    if constexpr (ABL == 4) {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        const uint32_t w = __builtin_bit_cast(uint32_t, pk[k]);
+        x[2 * k] = (int16_t)w;
+        x[2 * k + 1] = (int32_t)w >> 16;
+      }
+    } else {
     __syncthreads();  // the previous slice's loads from LDS are done
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -572,11 +718,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
       const int e = er | ((q2 & 15) << 4) | ((q2 >> 4) << 10);
       x[q2] = lds16[2 * dmf(e) + (e & 1)];
     }
-    wht<64>(x);
+    }
+    if constexpr (ABL != 2) wht<64>(x);
     const int wz = digit_weight((uint32_t)(z0 + s));  // workgroup-uniform
     if (wz != cur_w) {
       if (cur_w >= 0) flush();
       cur_w = wz;
+    }
+    if constexpr (ABL == 3) {
+      int32_t a = 0;
+#pragma unroll
+      for (int q2 = 0; q2 < 64; ++q2) a ^= x[q2];
+      tot[0] += (unsigned)a;
+      continue;
     }
 #pragma unroll
     for (int q2 = 0; q2 < 64; ++q2)
@@ -611,7 +765,10 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
   if (sabl == 3)
     hipLaunchKernelGGL((seed_kernel<T, 3>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
                        st.max_groups, z0, z1, buf);
-  if (sabl < 1 || sabl > 3)
+  if (sabl == 4)
+    hipLaunchKernelGGL((seed_kernel<T, 4>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                       st.max_groups, z0, z1, buf);
+  if (sabl < 1 || sabl > 4)
 #endif
     hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, st.max_groups,
                        z0, z1, buf);
@@ -640,8 +797,20 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
       const int ns = z1 - z0;
       const uint16_t* order =
           ((ns & (ns - 1)) == 0 && ns <= kMaxOrder && z0 % ns == 0) ? st.d_order + ns : nullptr;
-      hipLaunchKernelGGL(tile_mfma_kernel, dim3((unsigned)std::min(st.grid * st.tile_wgs, z1 - z0)), dim3(256), 0, s, buf,
-                         order, z0, z1 - z0, counts);
+      const dim3 mgrid((unsigned)std::min(st.grid * st.tile_wgs, z1 - z0));
+#ifdef SCT_ABLATION
+      static const int mabl = getenv("SCT_SPECTRAL_ABL") ? atoi(getenv("SCT_SPECTRAL_ABL")) : 0;
+      if (mabl >= 11 && mabl <= 15) {
+        if (mabl == 11) hipLaunchKernelGGL(tile_mfma_kernel<1>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+        if (mabl == 12) hipLaunchKernelGGL(tile_mfma_kernel<2>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+        if (mabl == 13) hipLaunchKernelGGL(tile_mfma_kernel<3>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+        if (mabl == 14) hipLaunchKernelGGL(tile_mfma_kernel<4>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+        if (mabl == 15) hipLaunchKernelGGL(tile_mfma_kernel<5>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+        SCT_LAUNCH_CHECK();
+        return SCT_OK;
+      }
+#endif
+      hipLaunchKernelGGL(tile_mfma_kernel<0>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
       SCT_LAUNCH_CHECK();
       return SCT_OK;
     }
@@ -710,12 +879,13 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   SCT_LAUNCH_CHECK();
   unsigned maxm = 0;
   SCT_HIP(hipMemcpy(&maxm, dmax.p, 4, hipMemcpyDeviceToHost));
+  st.max_m = maxm;
   st.elem_bytes = maxm <= 127 ? 1 : (maxm <= 32767 ? 2 : 4);
   const char* mf = getenv("SCT_SPECTRAL_MFMA");  // 0: VALU tile kernel for int8 seeds too
   st.mfma = !(mf && atoi(mf) == 0);
   {
     int per_cu = 0;  // resident MFMA-tile workgroups per CU (VGPR / LDS bound)
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma_kernel, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma_kernel<0>, 256, 0) != hipSuccess ||
         per_cu <= 0)
       per_cu = 2;
     st.tile_wgs = per_cu;
@@ -738,13 +908,14 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   }
   st.max_groups = sct::ceil_div(n, 32) + kLo;
   SCT_HIP(hipMalloc(&st.d_gofs, (size_t)(kLo + 1) * 4));
+  SCT_HIP(hipMalloc(&st.d_hist, (size_t)kSortWGs * kLo * 4));
   SCT_HIP(hipMalloc(&st.d_planes, (size_t)st.max_groups * kHiBits * 4));
   SCT_HIP(hipMalloc(&st.d_buf, (size_t)st.chunk * kLo * st.elem_bytes));
   return SCT_OK;
 }
 
 void destroy(State& st) {
-  for (void* p : {(void*)st.d_hi, (void*)st.d_off, (void*)st.d_cnt, (void*)st.d_gofs, (void*)st.d_planes,
+  for (void* p : {(void*)st.d_hi, (void*)st.d_off, (void*)st.d_cnt, (void*)st.d_gofs, (void*)st.d_planes, (void*)st.d_hist,
                   st.d_buf, (void*)st.d_order})
     if (p) (void)hipFree(p);
   st = State();
@@ -752,16 +923,22 @@ void destroy(State& st) {
 
 int build(State& st, const uint64_t* d_codes, hipStream_t s) {
   if (st.n < 2) return SCT_OK;
-  SCT_HIP(hipMemsetAsync(st.d_cnt, 0, (size_t)kLo * 4, s));
-  const unsigned g = (unsigned)std::min<int64_t>(1024, sct::ceil_div(st.n, 256));
-  hipLaunchKernelGGL(column_hist_kernel, dim3(g), dim3(256), 0, s, d_codes, st.n, st.d_cnt);
+  hipLaunchKernelGGL(column_hist_wg_kernel, dim3(kSortWGs), dim3(kSortThreads), 0, s, d_codes, st.n, st.d_hist);
   SCT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(column_scan_kernel, dim3(1), dim3(256), 0, s, st.d_cnt, st.d_off, st.d_gofs, st.d_cnt + kLo);
+  hipLaunchKernelGGL(column_prefix_kernel, dim3(kLo / 256), dim3(256), 0, s, st.d_hist, kSortWGs, st.d_cnt);
   SCT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(column_scatter_kernel, dim3(g), dim3(256), 0, s, d_codes, st.n, st.d_cnt + kLo, st.d_hi);
+  hipLaunchKernelGGL(column_scan16_kernel, dim3(1), dim3(1024), 0, s, st.d_cnt, st.d_off, st.d_gofs);
   SCT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(planes_kernel, dim3((unsigned)sct::ceil_div(st.max_groups, 256)), dim3(256), 0, s,
-                     st.d_hi, st.d_off, st.d_gofs, st.max_groups, st.d_planes);
+  hipLaunchKernelGGL(column_scatter_wg_kernel, dim3(kSortWGs), dim3(kSortThreads), 0, s, d_codes, st.n, st.d_hist,
+                     st.d_off, st.d_hi);
+  SCT_LAUNCH_CHECK();
+  if (st.max_m <= 128) {
+    hipLaunchKernelGGL(planes_slot_kernel<4>, dim3(kLo * 4 / 256), dim3(256), 0, s, st.d_hi, st.d_off, st.d_gofs,
+                       st.max_groups, st.d_planes);
+  } else {
+    hipLaunchKernelGGL(planes_kernel, dim3((unsigned)sct::ceil_div(st.max_groups, 256)), dim3(256), 0, s,
+                       st.d_hi, st.d_off, st.d_gofs, st.max_groups, st.d_planes);
+  }
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }

@@ -41,6 +41,18 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint64_t* clk, uint32_t 
       }
       if constexpr (OP == 8) asm volatile("v_add_u32 %0, %1, %0" : "+v"(x[c]) : "v"(y));
       if constexpr (OP == 9) asm volatile("v_and_b32 %0, %1, %0" : "+v"(x[c]) : "v"(y));
+      if constexpr (OP == 10) {  // 64-bit accumulate of a square: v_mad_i64_i32
+        uint64_t a64 = ((uint64_t)x[c] << 32) | y;
+        asm volatile("v_mad_i64_i32 %0, vcc, %1, %1, %0" : "+v"(a64) : "v"(z) : "vcc");
+        x[c] = (uint32_t)a64 ^ (uint32_t)(a64 >> 32);
+      }
+      if constexpr (OP == 11) asm volatile("v_mul_i32_i24 %0, %1, %0" : "+v"(x[c]) : "v"(y));
+      if constexpr (OP == 12) asm volatile("v_mul_hi_i32_i24 %0, %1, %0" : "+v"(x[c]) : "v"(y));
+      if constexpr (OP == 13) asm volatile("v_lshl_add_u32 %0, %1, 8, %0" : "+v"(x[c]) : "v"(y));
+      if constexpr (OP == 14) asm volatile("v_perm_b32 %0, %1, %0, %2" : "+v"(x[c]) : "v"(y), "v"(z));
+      if constexpr (OP == 15) asm volatile("v_pk_add_u16 %0, %1, %0" : "+v"(x[c]) : "v"(y));
+      if constexpr (OP == 16) asm volatile("v_mad_u32_u24 %0, %1, %2, %0" : "+v"(x[c]) : "v"(y), "v"(z));
+      if constexpr (OP == 17) asm volatile("v_mul_lo_u32 %0, %1, %0" : "+v"(x[c]) : "v"(y));
       if constexpr (OP == 3) {  // the kernel's mix: 2 bitop3 : 1 bcnt
         x[c] = __builtin_amdgcn_bitop3_b32(x[c], y, z, 0xE8);
         x[c] = __builtin_amdgcn_bitop3_b32(x[c], y, z, 0x96);
@@ -107,6 +119,14 @@ int main() {
   run<7>("bcnt+xor_e32", 2, blocks);
   run<8>("v_add_u32_e32", 1, blocks);
   run<9>("v_and_b32_e32", 1, blocks);
+  run<10>("v_mad_i64_i32(+2 xor/shift)", 1, blocks);
+  run<11>("v_mul_i32_i24", 1, blocks);
+  run<12>("v_mul_hi_i32_i24", 1, blocks);
+  run<13>("v_lshl_add_u32", 1, blocks);
+  run<14>("v_perm_b32", 1, blocks);
+  run<15>("v_pk_add_u16", 1, blocks);
+  run<16>("v_mad_u32_u24", 1, blocks);
+  run<17>("v_mul_lo_u32", 1, blocks);
   run<2>("v_xor_b32@1wps", 1, 256);
   run<2>("v_xor_b32@2wps", 1, 512);
   run<2>("v_xor_b32@4wps", 1, 1024);
