@@ -37,6 +37,7 @@ from sctools_amd import _lib, sharding, synthetic  # noqa: E402
 # Full-rate VALU issue: 256 CU x 4 SIMD32 x 32 lanes/clk x 2.4 GHz = 78.6 Tops/s (2-source
 # int32 ops; measured 121 lane-ops/clk/CU for v_xor_b32 by tools/valu_peak.hip / valu_banks.hip).
 VALU_PEAK_OPS = 256 * 128 * 2.4e9
+HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E (MI355X_MICROARCH.md)
 ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-bit code word
 # VALU issue slots the bit-sliced count kernel spends per pair at 16 bp, from its unmasked
 # loop (v_bcnt_u32_b32 counts 2: half rate on gfx950), per count scheme:
@@ -112,20 +113,38 @@ def _traffic(name):
 
 
 def spectral_roofline(tk, step_count_ms, my_slices):
-    """Dominant kernel of SPECTRAL: the tile kernel (14-bit WHT per slice + F^2 binning)."""
+    """SPECTRAL's two kernels per chunk: seed (writes 2^14 int8 values per slice) and tile
+    (reads them back: 14-bit WHT on the matrix cores + F^2 binning).  Both move 16 KiB per
+    slice through HBM, so the roofline is HBM bandwidth; the dominant (slower) kernel is the
+    one reported, the other beside it."""
     per_launch = tk["units"]
-    achieved = per_launch * SPECTRAL_OPS_PER_SLICE / (tk["kernel_ms"] * 1e-3)
     launches = -(-my_slices // per_launch)
-    return {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12, "unit": "Tops/s",
-            "frac": achieved / VALU_PEAK_OPS, "traffic": _traffic("pmc_spectral_latest.json"),
-            "kernel": "sct_spectral::tile_mfma_kernel (int8 seeds)", "kernel_ms": tk["kernel_ms"],
+    algo_bytes = per_launch * (1 << 14)  # int8 seed values per launch (seed writes, tile reads)
+    kern = {"tile": {"kernel": "sct_spectral::tile_mfma2_pf_kernel (int8 seeds)", "ms": tk["kernel_ms"],
+                     "traffic": _traffic("pmc_spectral_latest.json")},
+            "seed": {"kernel": "sct_spectral::seed_kernel<int8_t>", "ms": tk["seed_ms"],
+                     "traffic": _traffic("pmc_spectral_seed_latest.json")}}
+    for k in kern.values():
+        k["achieved_gbs"] = algo_bytes / (k["ms"] * 1e-3) / 1e9
+        k["frac"] = k["achieved_gbs"] * 1e9 / HBM_PEAK_BPS
+    dom, other = ("seed", "tile") if tk["seed_ms"] >= tk["kernel_ms"] else ("tile", "seed")
+    d = kern[dom]
+    tile_ops = per_launch * SPECTRAL_OPS_PER_SLICE / (tk["kernel_ms"] * 1e-3)
+    return {"bound": "hbm", "achieved": d["achieved_gbs"], "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
+            "frac": d["frac"], "traffic": d["traffic"], "kernel": d["kernel"], "kernel_ms": d["ms"],
+            "other_kernel": dict(kern[other], name=other),
             "slices_per_launch": per_launch, "launches_per_step": launches,
-            "algo_ops_per_slice": SPECTRAL_OPS_PER_SLICE, "seed_kernel_ms": tk["seed_ms"],
+            "algo_bytes_per_launch": algo_bytes,
             "count_ms_per_step": step_count_ms,
-            "algo_bytes_per_launch": per_launch * (1 << 14),
-            "note": "kernel_ms: HIP events around 5 back-to-back launches on the bench stream; "
-                    "traffic: tile-kernel HBM bytes per launch from PMC, against the int8 seed "
-                    "values it must read (algo_bytes_per_launch)"}
+            "chunk_frac": 2 * algo_bytes / ((tk["seed_ms"] + tk["kernel_ms"]) * 1e-3) / HBM_PEAK_BPS,
+            "tile_valu_equivalent": {"algo_ops_per_slice": SPECTRAL_OPS_PER_SLICE, "achieved_tops": tile_ops / 1e12,
+                                     "peak_tops": VALU_PEAK_OPS / 1e12, "frac": tile_ops / VALU_PEAK_OPS,
+                                     "note": "14 butterfly add/subs + 1 square-accumulate per value as int32 "
+                                             "VALU ops; 12 of the 14 levels run on the matrix cores"},
+            "note": "kernel_ms: HIP events around 5 back-to-back launches of each kernel on the bench "
+                    "stream; algo bytes = the int8 seed values of one launch (the seed kernel writes them, "
+                    "the tile kernel reads them); traffic: HBM bytes per launch from PMC "
+                    "(tools/summarize_profile.py); chunk_frac = both kernels' bytes over their summed time"}
 
 
 def pair_roofline(plan, my_pairs, kms, L, moments_ms):

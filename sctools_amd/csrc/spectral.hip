@@ -608,10 +608,9 @@ __device__ __forceinline__ int dmf(int e) {
 // flushed to LDS only when it changes), or z0 + u (order = nullptr).
 // ABL (ablation builds only, wrong results by design): 1 = no global loads, 2 = no
 // phase-2 butterflies, 3 = no squares/bins, 4 = no LDS exchange, 5 = prefetch the next slice.
-template <int ABL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_mfma_kernel(const int8_t* __restrict__ buf,
-                                                        const uint16_t* __restrict__ order, int z0,
-                                                        int nslices, unsigned long long* __restrict__ counts) {
+template <int ABL>
+__device__ __forceinline__ void tile_mfma_body(const int8_t* __restrict__ buf, const uint16_t* __restrict__ order,
+                                               int z0, int nslices, unsigned long long* __restrict__ counts) {
   __shared__ uint32_t lds32[kLo / 2];
   __shared__ unsigned long long bins[17];
   const int16_t* lds16 = reinterpret_cast<const int16_t*>(lds32);
@@ -742,6 +741,176 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
 }
 
+template <int ABL = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_mfma_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts) {
+  tile_mfma_body<ABL>(buf, order, z0, nslices, counts);
+}
+
+// ---------------------------------------------------------------- two-stage MFMA tile
+// Both 64-point stages on the matrix cores.  Stage 1 as tile_mfma_kernel (column bits 0..3,
+// 8, 9) plus the 4-point transform over the load registers j (bits 12, 13) in int32; the
+// j = 0 MFMAs start from an accumulator of 128, which that transform spreads to every
+// output (H_4 (128, 0, 0, 0) = (128, 128, 128, 128)), so y = x + 128 leaves the stage.
+// One int16 LDS exchange (ds_write_b16), then stage 2 over bits 4..7, 10, 11 with
+// k = bits 4..7 (the 16 bytes a lane holds) + bits 10, 11 (lane bits 4, 5) and n = bits
+// 0..3: y = 256 h + l with h = the high byte of y and l - 128 = the low byte of y ^ 0x80
+// (both signed bytes), so x = 256 h + (l - 128) and H x = (H h << 8) + H (l - 128): two
+// i8 MFMAs per output tile, the first one's result shifted into the second's accumulator.
+// Stage-2 outputs: bits 0..3 = lane bits 0..3, 4, 5 = i, 6, 7 = lane bits 4, 5, 8, 9 =
+// the register group g, 10, 11 = the A quarter q, 12, 13 = the wave -- whole digits.
+// LDS element of column e: bits 4..7 in the low 4 bits (bit 7 ^= bit 3, so each 16-lane
+// group of the stage-2 b128 reads covers all 64 banks), bits 0..3 above them (bit 0 ^=
+// bit 2: the stage-1 b16 stores of lane bits 4 = 0 / 1 land on different banks), then 8..13.
+__device__ __forceinline__ int lds_e2(int e) {
+  const int lo4 = ((e >> 4) & 15) ^ (((e >> 3) & 1) << 3);
+  const int mid4 = (e & 15) ^ ((e >> 2) & 1);
+  return lo4 | (mid4 << 4) | ((e >> 8) << 8);
+}
+
+template <bool PF>
+__device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, const uint16_t* __restrict__ order,
+                                                int z0, int nslices, unsigned long long* __restrict__ counts) {
+  __shared__ __attribute__((aligned(16))) int16_t lds[kLo];
+  __shared__ unsigned long long bins[17];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 17) bins[tid] = 0;
+  v2l_t A[4];  // H_64 rows 16 q + (l & 15), columns 16 (l >> 4) + j (both stages)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * q + (lane & 15), col = 16 * (lane >> 4) + 4 * d + r;
+        v |= ((__popc(row & col) & 1) ? 0xFFu : 0x01u) << (8 * r);
+      }
+      w[d] = v;
+    }
+    A[q] = v2l_t{(long)(((uint64_t)w[1] << 32) | w[0]), (long)(((uint64_t)w[3] << 32) | w[2])};
+  }
+  // stage-2 output bits 0..3 (two digits), 6, 7 and 12, 13 are thread constants
+  const int wt_thread = digit_weight((uint32_t)(lane & 15) | ((uint32_t)(lane >> 4) << 6) | ((uint32_t)wave << 12));
+  // stage-1 store base: e = i | (l >> 4) << 2 | (l & 15) << 4 | q << 8 | wave << 10 | j << 12
+  const int wbase = lds_e2(((lane >> 4) << 2) | ((lane & 15) << 4) | (wave << 10));
+  // stage-2 read base: e = (l & 15) | (l >> 4) << 10 | g << 8 | wave << 12, bits 4..7 = 0..15
+  const int rbase = lds_e2((lane & 15) | ((lane >> 4) << 10) | (wave << 12));
+  auto slice_of = [&](int u) { return order ? (int)order[u] : u; };
+  const int ub = (int)((int64_t)nslices * blockIdx.x / gridDim.x);
+  const int ue = (int)((int64_t)nslices * (blockIdx.x + 1) / gridDim.x);
+  unsigned long long tot[4] = {0, 0, 0, 0};
+  int cur_w = -1;
+  auto flush = [&]() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tot[k]) atomicAdd(&bins[cur_w + wt_thread + k], tot[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tot[k] = 0;
+  };
+  auto load = [&](int u, v2l_t* dst) {
+    const int8_t* row = buf + (int64_t)slice_of(u) * kLo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      dst[j] = __builtin_nontemporal_load(reinterpret_cast<const v2l_t*>(row + 16 * tid + 4096 * j));
+  };
+  v2l_t Bn[4];
+  if constexpr (PF) {
+    if (ub < ue) load(ub, Bn);
+  }
+  for (int u = ub; u < ue; ++u) {
+    const int s = slice_of(u);
+    v2l_t B[4];
+    if constexpr (PF) {  // the next slice's loads fly while this one is transformed
+#pragma unroll
+      for (int j = 0; j < 4; ++j) B[j] = Bn[j];
+      if (u + 1 < ue) load(u + 1, Bn);
+    } else {
+      load(u, B);
+    }
+    int32_t x[64];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int b0 = j == 0 ? 128 : 0;
+        const v4i_t c = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[q], B[j], v4i_t{b0, b0, b0, b0}, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[j * 16 + q * 4 + i] = c[i];
+      }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {  // column bits 12, 13 (registers j)
+      const int32_t a = x[r], b = x[16 + r], c = x[32 + r], d = x[48 + r];
+      const int32_t ab0 = a + b, ab1 = a - b, cd0 = c + d, cd1 = c - d;
+      x[r] = ab0 + cd0;
+      x[16 + r] = ab1 + cd1;
+      x[32 + r] = ab0 - cd0;
+      x[48 + r] = ab1 - cd1;
+    }
+    __syncthreads();  // the previous slice's stage-2 reads are done
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // the offset is XOR-linear in e: wbase ^ lds_e2(i | q << 8 | j << 12)
+          lds[wbase ^ lds_e2(i | (q << 8) | (j << 12))] = (int16_t)x[j * 16 + q * 4 + i];
+    __syncthreads();
+    const int wz = digit_weight((uint32_t)(z0 + s));  // workgroup-uniform
+    if (wz != cur_w) {
+      if (cur_w >= 0) flush();
+      cur_w = wz;
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int base = rbase ^ lds_e2(g << 8);
+      // base already carries the bit-7 swizzle (lds_e2 of e with bits 4..7 = 0)
+      const uint4 h0 = *reinterpret_cast<const uint4*>(lds + base);        // bits 4..6, bit 7 = 0
+      const uint4 h1 = *reinterpret_cast<const uint4*>(lds + (base ^ 8));  // bit 7 = 1
+      const uint32_t d[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+      uint32_t lo[4], hi[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        lo[m] = __builtin_amdgcn_perm(d[2 * m + 1], d[2 * m], 0x06040200u) ^ 0x80808080u;
+        hi[m] = __builtin_amdgcn_perm(d[2 * m + 1], d[2 * m], 0x07050301u);
+      }
+      const v2l_t Bl = v2l_t{(long)(((uint64_t)lo[1] << 32) | lo[0]), (long)(((uint64_t)lo[3] << 32) | lo[2])};
+      const v2l_t Bh = v2l_t{(long)(((uint64_t)hi[1] << 32) | hi[0]), (long)(((uint64_t)hi[3] << 32) | hi[2])};
+      v4i_t c[4];  // the four quarters' high-byte products first: independent MFMAs
+#pragma unroll
+      for (int q = 0; q < 4; ++q) c[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[q], Bh, v4i_t{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) c[q][i] <<= 8;
+        c[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[q], Bl, c[q], 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          tot[digit_weight_c((uint32_t)i) + digit_weight_c((uint32_t)g) + digit_weight_c((uint32_t)q)] +=
+              (unsigned long long)((int64_t)c[q][i] * c[q][i]);
+    }
+  }
+  if (cur_w >= 0) flush();
+  __syncthreads();
+  if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_mfma2_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts) {
+  tile_mfma2_body<false>(buf, order, z0, nslices, counts);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_mfma2_pf_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts) {
+  tile_mfma2_body<true>(buf, order, z0, nslices, counts);
+}
+
 __global__ void max_column_kernel(const uint32_t* __restrict__ cnt, unsigned* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < kLo) atomicMax(out, cnt[c]);
@@ -800,17 +969,25 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
       const dim3 mgrid((unsigned)std::min(st.grid * st.tile_wgs, z1 - z0));
 #ifdef SCT_ABLATION
       static const int mabl = getenv("SCT_SPECTRAL_ABL") ? atoi(getenv("SCT_SPECTRAL_ABL")) : 0;
-      if (mabl >= 11 && mabl <= 15) {
+      if (mabl >= 11 && mabl <= 19) {
         if (mabl == 11) hipLaunchKernelGGL(tile_mfma_kernel<1>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 12) hipLaunchKernelGGL(tile_mfma_kernel<2>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 13) hipLaunchKernelGGL(tile_mfma_kernel<3>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 14) hipLaunchKernelGGL(tile_mfma_kernel<4>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 15) hipLaunchKernelGGL(tile_mfma_kernel<5>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+        if (mabl == 17 || mabl == 19) {  // two-stage without prefetch / the one-stage kernel
+          int per_cu = 0;
+          if (mabl == 17) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma2_kernel, 256, 0);
+          else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma_kernel<0>, 256, 0);
+          const dim3 g2((unsigned)std::min(st.grid * std::max(per_cu, 1), z1 - z0));
+          if (mabl == 17) hipLaunchKernelGGL(tile_mfma2_kernel, g2, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+          else hipLaunchKernelGGL(tile_mfma_kernel<0>, g2, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+        }
         SCT_LAUNCH_CHECK();
         return SCT_OK;
       }
 #endif
-      hipLaunchKernelGGL(tile_mfma_kernel<0>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+      hipLaunchKernelGGL(tile_mfma2_pf_kernel, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
       SCT_LAUNCH_CHECK();
       return SCT_OK;
     }
@@ -885,7 +1062,7 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   st.mfma = !(mf && atoi(mf) == 0);
   {
     int per_cu = 0;  // resident MFMA-tile workgroups per CU (VGPR / LDS bound)
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma_kernel<0>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma2_pf_kernel, 256, 0) != hipSuccess ||
         per_cu <= 0)
       per_cu = 2;
     st.tile_wgs = per_cu;
