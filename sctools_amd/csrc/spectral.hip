@@ -289,32 +289,33 @@ __device__ __forceinline__ void transpose4x4_bytes(const uint32_t* d, uint32_t* 
 // 16-B chunks of slice rows.
 // ABL (ablation builds only, wrong results by design): 1 = no global stores, 2 = no
 // Gray walk (one group, no planes), 3 = no LDS staging/transposes.
-template <typename T, int ABL = 0>
-__global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ planes,
+template <typename T, int ABL, int kRegG, int NT = 256>
+__device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
                                                    const uint32_t* __restrict__ gofs,
                                                    const uint32_t* __restrict__ off, int64_t max_groups,
                                                    int z0, int z1, T* __restrict__ buf) {
   constexpr int P = 4 / sizeof(T);          // slices per staged dword
   constexpr int V = Chunk<T>::kVals;        // columns per 16-B output chunk
-  __shared__ uint32_t stage[(kWalk / P) * 256];
+  __shared__ uint32_t stage[(kWalk / P) * NT];
   const int tid = threadIdx.x;
-  const int c0 = blockIdx.x * 256, c = c0 + tid;
+  const int c0 = blockIdx.x * NT, c = c0 + tid;
   const int m = (int)(off[c + 1] - off[c]);
   const uint32_t g0 = gofs[c];
   const int ng = (int)(gofs[c + 1] - g0);
   int wng = ng;
 #pragma unroll
   for (int s = 32; s; s >>= 1) wng = max(wng, __shfl_xor(wng, s));
-  // the first kRegGroups groups' planes stay in registers for all of this workgroup's walks
-  uint32_t pr[kRegGroups][kHiBits];
+  // the first kRegG groups' planes stay in registers for all of this workgroup's walks
+  uint32_t pr[kRegG][kHiBits];
 #pragma unroll
-  for (int g = 0; g < kRegGroups; ++g)
+  for (int g = 0; g < kRegG; ++g)
 #pragma unroll
     for (int k = 0; k < kHiBits; ++k) pr[g][k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
   // int8 byte store-out: this thread writes columns c0 + mcb .. + 15; mx = their m | 0x80
   // as bytes (ABL 4 = the same path, for A/B against the ablations)
-  constexpr bool kByteStage = sizeof(T) == 1 && (ABL == 0 || ABL == 4);
-  const int mcb = (tid & 15) * 16;
+  constexpr bool kByteStage = sizeof(T) == 1 && (ABL == 0 || ABL == 4 || ABL == 6 || ABL == 7);
+  // ABL 6: each wave stages and stores its own 64 columns (no workgroup barrier)
+  const int mcb = ABL == 6 ? 64 * (tid >> 6) + 16 * (tid & 3) : (tid % (NT / 16)) * 16;
   uint4 mx = make_uint4(0, 0, 0, 0);
   if constexpr (kByteStage) {
     uint32_t w[4];
@@ -354,9 +355,9 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
   } else {
     walk(pr[0], std::true_type());  // columns without codes: planes 0, popc 0
 #pragma unroll
-    for (int g = 1; g < kRegGroups; ++g)
+    for (int g = 1; g < kRegG; ++g)
       if (g < wng) walk(pr[g], std::false_type());
-    for (int g = kRegGroups; g < wng; ++g) {  // dense columns: the rest from L2
+    for (int g = kRegG; g < wng; ++g) {  // dense columns: the rest from L2
       uint32_t p[kHiBits];
 #pragma unroll
       for (int k = 0; k < kHiBits; ++k) p[k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
@@ -378,14 +379,37 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
     //   ((m | 0x80) - 2 acc) ^ 0x80 per byte -- acc <= m <= 127, so 2 acc fits a byte
     //   and m + 128 - 2 acc lies in [1, 255]: no carry or borrow crosses a byte.
     uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
+    if constexpr (ABL == 6) {
+      uint8_t* w8 = st8 + 4096 * (tid >> 6);  // this wave's 64 slices x 64 columns
+      const int lane = tid & 63;
+      // the previous walk's reads of w8 are this wave's own, issued earlier: LDS keeps order
+#pragma unroll
+      for (int i = 0; i < kWalk; ++i) w8[i * 64 + lane] = (uint8_t)acc[i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int r = 0; r < kWalk / 16; ++r) {
+        const int row = (lane >> 2) + 16 * r;
+        const uint4 v = *reinterpret_cast<const uint4*>(w8 + row * 64 + 16 * (lane & 3));
+        const uint4 o = make_uint4((mx.x - (v.x + v.x)) ^ 0x80808080u, (mx.y - (v.y + v.y)) ^ 0x80808080u,
+                                   (mx.z - (v.z + v.z)) ^ 0x80808080u, (mx.w - (v.w + v.w)) ^ 0x80808080u);
+        const int z = zblk + row;
+        if (z >= z0 && z < z1)
+          *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + mcb)) = o;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
     __syncthreads();  // the previous walk's store-out reads of `stage` are done
 #pragma unroll
-    for (int i = 0; i < kWalk; ++i) st8[i * 256 + tid] = (uint8_t)acc[i];
+    for (int i = 0; i < kWalk; ++i) st8[i * NT + tid] = (uint8_t)acc[i];
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kWalk / 16; ++r) {
-      const int row = (tid >> 4) + 16 * r;
-      const uint4 v = *reinterpret_cast<const uint4*>(st8 + row * 256 + mcb);
+      const int row = tid / (NT / 16) + 16 * r;
+      const uint4 v = *reinterpret_cast<const uint4*>(st8 + row * NT + mcb);
       const uint4 o = make_uint4((mx.x - (v.x + v.x)) ^ 0x80808080u, (mx.y - (v.y + v.y)) ^ 0x80808080u,
                                  (mx.z - (v.z + v.z)) ^ 0x80808080u, (mx.w - (v.w + v.w)) ^ 0x80808080u);
       const int z = zblk + row;
@@ -452,6 +476,29 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
     }
   }
   }
+}
+
+template <typename T, int ABL = 0>
+__global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ planes,
+                                                   const uint32_t* __restrict__ gofs,
+                                                   const uint32_t* __restrict__ off, int64_t max_groups,
+                                                   int z0, int z1, T* __restrict__ buf) {
+  seed_body<T, ABL, kRegGroups>(planes, gofs, off, max_groups, z0, z1, buf);
+}
+// store-width variant (A/B): 512 columns per workgroup (512-B slice-row segments)
+template <typename T>
+__global__ __launch_bounds__(512) void seed_wide_kernel(const uint32_t* __restrict__ planes,
+                                                        const uint32_t* __restrict__ gofs,
+                                                        const uint32_t* __restrict__ off, int64_t max_groups,
+                                                        int z0, int z1, T* __restrict__ buf) {
+  seed_body<T, 7, kRegGroups, 512>(planes, gofs, off, max_groups, z0, z1, buf);
+}
+// occupancy variant (A/B): one register-resident group, 4 waves per SIMD
+template <typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void seed_r1_kernel(
+    const uint32_t* __restrict__ planes, const uint32_t* __restrict__ gofs, const uint32_t* __restrict__ off,
+    int64_t max_groups, int z0, int z1, T* __restrict__ buf) {
+  seed_body<T, 0, 1>(planes, gofs, off, max_groups, z0, z1, buf);
 }
 
 // LDS word of column e in the tile kernel: bits 2, 3, 4 XORed with bits 6, 5, 10, so the
@@ -810,25 +857,36 @@ __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, 
 #pragma unroll
     for (int k = 0; k < 4; ++k) tot[k] = 0;
   };
-  auto load = [&](int u, v2l_t* dst) {
-    const int8_t* row = buf + (int64_t)slice_of(u) * kLo;
+  auto load = [&](int sl, v2l_t* dst) {
+    const int8_t* row = buf + (int64_t)sl * kLo;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       dst[j] = __builtin_nontemporal_load(reinterpret_cast<const v2l_t*>(row + 16 * tid + 4096 * j));
   };
   v2l_t Bn[4];
+  // PF: slice indices run two ahead (their table loads wait a whole slice) and the values
+  // one ahead (the next slice's loads fly while this one is transformed)
+  int s_cur = 0, s_nxt = 0;
   if constexpr (PF) {
-    if (ub < ue) load(ub, Bn);
+    if (ub < ue) {
+      s_cur = slice_of(ub);
+      load(s_cur, Bn);
+    }
+    if (ub + 1 < ue) s_nxt = slice_of(ub + 1);
   }
   for (int u = ub; u < ue; ++u) {
-    const int s = slice_of(u);
     v2l_t B[4];
-    if constexpr (PF) {  // the next slice's loads fly while this one is transformed
+    int s;
+    if constexpr (PF) {
+      s = s_cur;
 #pragma unroll
       for (int j = 0; j < 4; ++j) B[j] = Bn[j];
-      if (u + 1 < ue) load(u + 1, Bn);
+      if (u + 1 < ue) load(s_nxt, Bn);
+      s_cur = s_nxt;
+      if (u + 2 < ue) s_nxt = slice_of(u + 2);
     } else {
-      load(u, B);
+      s = slice_of(u);
+      load(s, B);
     }
     int32_t x[64];
 #pragma unroll
@@ -937,7 +995,16 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
   if (sabl == 4)
     hipLaunchKernelGGL((seed_kernel<T, 4>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
                        st.max_groups, z0, z1, buf);
-  if (sabl < 1 || sabl > 4)
+  if (sabl == 7 && sizeof(T) == 1)
+    hipLaunchKernelGGL(seed_wide_kernel<T>, dim3(kLo / 512, sgrid.y), dim3(512), 0, s, st.d_planes, st.d_gofs,
+                       st.d_off, st.max_groups, z0, z1, buf);
+  if (sabl == 6)
+    hipLaunchKernelGGL((seed_kernel<T, 6>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                       st.max_groups, z0, z1, buf);
+  if (sabl == 5)
+    hipLaunchKernelGGL(seed_r1_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                       st.max_groups, z0, z1, buf);
+  if (sabl < 1 || sabl > 7)
 #endif
     hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, st.max_groups,
                        z0, z1, buf);
