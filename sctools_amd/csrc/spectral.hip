@@ -313,7 +313,7 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
     for (int k = 0; k < kHiBits; ++k) pr[g][k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
   // int8 byte store-out: this thread writes columns c0 + mcb .. + 15; mx = their m | 0x80
   // as bytes (ABL 4 = the same path, for A/B against the ablations)
-  constexpr bool kByteStage = sizeof(T) == 1 && (ABL == 0 || ABL == 4 || ABL == 6 || ABL == 7);
+  constexpr bool kByteStage = sizeof(T) == 1 && (ABL == 0 || ABL == 4 || ABL == 6 || ABL == 7 || (ABL >= 8 && ABL <= 10));
   // ABL 6: each wave stages and stores its own 64 columns (no workgroup barrier)
   const int mcb = ABL == 6 ? 64 * (tid >> 6) + 16 * (tid & 3) : (tid % (NT / 16)) * 16;
   uint4 mx = make_uint4(0, 0, 0, 0);
@@ -329,6 +329,17 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
       }
     }
     mx = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  // Co-resident workgroups start together and run identical walks, so they stay in
+  // lockstep: all 12 waves of a CU walk (VALU-bound) and then all store (HBM-bound).
+  // Starting them 0 / 1,536 / 3,072 cycles apart (about 1/6 and 1/3 of a walk) lets one
+  // workgroup's stores drain under another's walk: 0.35 -> 0.32-0.33 ms per launch
+  // (ABL 9 / 10: 2x / 4x the offset, smaller gains).
+  if constexpr (ABL == 0 || (ABL >= 8 && ABL <= 10)) {
+    constexpr int kS = ABL == 9 ? 48 : (ABL == 10 ? 96 : 24);
+    const int ph = (blockIdx.x + blockIdx.y) % 3;
+    if (ph >= 1) __builtin_amdgcn_s_sleep(kS);
+    if (ph == 2) __builtin_amdgcn_s_sleep(kS);
   }
   const int za = z0 & ~(kWalk - 1);
   const int nwalks = (z1 - za + kWalk - 1) / kWalk;
@@ -406,6 +417,20 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
 #pragma unroll
     for (int i = 0; i < kWalk; ++i) st8[i * NT + tid] = (uint8_t)acc[i];
     __syncthreads();
+    if (zblk >= z0 && zblk + kWalk <= z1) {  // the whole walk is in range: all loads, then all stores
+      uint4 v[kWalk / 16];
+#pragma unroll
+      for (int r = 0; r < kWalk / 16; ++r)
+        v[r] = *reinterpret_cast<const uint4*>(st8 + (tid / (NT / 16) + 16 * r) * NT + mcb);
+#pragma unroll
+      for (int r = 0; r < kWalk / 16; ++r) {
+        const uint4 o = make_uint4((mx.x - (v[r].x + v[r].x)) ^ 0x80808080u, (mx.y - (v[r].y + v[r].y)) ^ 0x80808080u,
+                                   (mx.z - (v[r].z + v[r].z)) ^ 0x80808080u, (mx.w - (v[r].w + v[r].w)) ^ 0x80808080u);
+        const int z = zblk + tid / (NT / 16) + 16 * r;
+        *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + mcb)) = o;
+      }
+      continue;
+    }
 #pragma unroll
     for (int r = 0; r < kWalk / 16; ++r) {
       const int row = tid / (NT / 16) + 16 * r;
@@ -816,7 +841,7 @@ __device__ __forceinline__ int lds_e2(int e) {
   return lo4 | (mid4 << 4) | ((e >> 8) << 8);
 }
 
-template <bool PF>
+template <bool PF, int STAGGER = 0>
 __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, const uint16_t* __restrict__ order,
                                                 int z0, int nslices, unsigned long long* __restrict__ counts) {
   __shared__ __attribute__((aligned(16))) int16_t lds[kLo];
@@ -857,6 +882,10 @@ __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, 
 #pragma unroll
     for (int k = 0; k < 4; ++k) tot[k] = 0;
   };
+  if constexpr (STAGGER > 0) {  // A/B: phase-offset co-resident workgroups
+    const int ph = blockIdx.x & 3;
+    for (int k = 0; k < ph; ++k) __builtin_amdgcn_s_sleep(STAGGER);
+  }
   auto load = [&](int sl, v2l_t* dst) {
     const int8_t* row = buf + (int64_t)sl * kLo;
 #pragma unroll
@@ -963,6 +992,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
     unsigned long long* __restrict__ counts) {
   tile_mfma2_body<false>(buf, order, z0, nslices, counts);
 }
+template <int STAGGER>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_mfma2_pf_st_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts) {
+  tile_mfma2_body<true, STAGGER>(buf, order, z0, nslices, counts);
+}
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_mfma2_pf_kernel(
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
     unsigned long long* __restrict__ counts) {
@@ -998,13 +1033,22 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
   if (sabl == 7 && sizeof(T) == 1)
     hipLaunchKernelGGL(seed_wide_kernel<T>, dim3(kLo / 512, sgrid.y), dim3(512), 0, s, st.d_planes, st.d_gofs,
                        st.d_off, st.max_groups, z0, z1, buf);
+  if (sabl == 8)
+    hipLaunchKernelGGL((seed_kernel<T, 8>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                       st.max_groups, z0, z1, buf);
+  if (sabl == 9)
+    hipLaunchKernelGGL((seed_kernel<T, 9>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                       st.max_groups, z0, z1, buf);
+  if (sabl == 10)
+    hipLaunchKernelGGL((seed_kernel<T, 10>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                       st.max_groups, z0, z1, buf);
   if (sabl == 6)
     hipLaunchKernelGGL((seed_kernel<T, 6>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
                        st.max_groups, z0, z1, buf);
   if (sabl == 5)
     hipLaunchKernelGGL(seed_r1_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
                        st.max_groups, z0, z1, buf);
-  if (sabl < 1 || sabl > 7)
+  if (sabl < 1 || sabl > 10)
 #endif
     hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, st.max_groups,
                        z0, z1, buf);
@@ -1036,12 +1080,14 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
       const dim3 mgrid((unsigned)std::min(st.grid * st.tile_wgs, z1 - z0));
 #ifdef SCT_ABLATION
       static const int mabl = getenv("SCT_SPECTRAL_ABL") ? atoi(getenv("SCT_SPECTRAL_ABL")) : 0;
-      if (mabl >= 11 && mabl <= 19) {
+      if (mabl >= 11 && mabl <= 21) {
         if (mabl == 11) hipLaunchKernelGGL(tile_mfma_kernel<1>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 12) hipLaunchKernelGGL(tile_mfma_kernel<2>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 13) hipLaunchKernelGGL(tile_mfma_kernel<3>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 14) hipLaunchKernelGGL(tile_mfma_kernel<4>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 15) hipLaunchKernelGGL(tile_mfma_kernel<5>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+        if (mabl == 20) hipLaunchKernelGGL(tile_mfma2_pf_st_kernel<20>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+        if (mabl == 21) hipLaunchKernelGGL(tile_mfma2_pf_st_kernel<40>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 17 || mabl == 19) {  // two-stage without prefetch / the one-stage kernel
           int per_cu = 0;
           if (mabl == 17) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma2_kernel, 256, 0);
