@@ -146,3 +146,53 @@ def test_sharded_spectral_histogram_matches_oracle(tmp_path, world, n):
     ref = O.c_hist_rows(synthetic.whitelist_codes(n, 16, 29))[:17]
     for r in range(world):
         assert np.load(out % r).tolist() == ref.tolist()
+
+
+def _oracle_nearest(kind, whitelist, queries, max_d, code_bits):
+    """Test-only stand-in for the GPU nearest path on this rank's slice."""
+    idx, dist_ = O.nearest_bruteforce(kind, [int(x) for x in whitelist], [int(x) for x in queries], max_d)
+    return np.asarray(idx, dtype=np.int32), np.asarray(dist_, dtype=np.uint8)
+
+
+def _oracle_encode(kind, seqs, L):
+    enc = O.two_bit_encode if kind == 2 else O.three_bit_encode
+    gcf = O.two_bit_gc if kind == 2 else O.three_bit_gc
+    codes = np.array([[enc(bytes(r))] for r in seqs], dtype=np.uint64).reshape(-1, 1)
+    gc = np.array([gcf(int(c[0]), L) if kind == 2 else gcf(int(c[0])) for c in codes], dtype=np.uint8)
+    return codes, gc, np.zeros(len(seqs), dtype=np.uint8)
+
+
+def _worker_ranges(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(5)
+        wl = np.unique(rng.integers(0, 1 << 48, 300, dtype=np.uint64))[:250]
+        q = np.concatenate([wl[:40], wl[40:80] ^ np.uint64(1 << 7), rng.integers(0, 1 << 48, 37, dtype=np.uint64)])
+        idx, d = sharding.nearest_sharded(3, wl, q, 1, 48, fn=_oracle_nearest)
+        seqs = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=(101, 16))
+        codes, gc, flags = sharding.encode_sharded(2, seqs, 16, fn=_oracle_encode)
+        np.savez(out_path % rank, idx=idx, d=d, codes=codes, gc=gc, flags=flags)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_contiguous_range_sharding_gathers_whole_result(tmp_path, world):
+    """Config 4 / encoder sharding: contiguous record ranges per rank, whole
+    result all-gathered on every rank, identical to the unsharded computation."""
+    port = _free_port()
+    out = str(tmp_path / "ranges_%d.npz")
+    mp.spawn(_worker_ranges, args=(world, port, out), nprocs=world, join=True)
+    rng = np.random.default_rng(5)
+    wl = np.unique(rng.integers(0, 1 << 48, 300, dtype=np.uint64))[:250]
+    q = np.concatenate([wl[:40], wl[40:80] ^ np.uint64(1 << 7), rng.integers(0, 1 << 48, 37, dtype=np.uint64)])
+    ridx, rd = _oracle_nearest(3, wl, q, 1, 48)
+    seqs = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=(101, 16))
+    rcodes, rgc, _ = _oracle_encode(2, seqs, 16)
+    assert (ridx[:40] == np.arange(40)).all() and (ridx[40:80] == np.arange(40, 80)).all()
+    for r in range(world):
+        z = np.load(out % r)
+        assert z["idx"].tolist() == ridx.tolist() and z["d"].tolist() == rd.tolist()
+        assert z["codes"].shape == (101, 1) and z["codes"].tolist() == rcodes.tolist()
+        assert z["gc"].tolist() == rgc.tolist() and z["flags"].shape == (101,)
