@@ -567,7 +567,8 @@ __device__ __forceinline__ void lane_butterfly16(int32_t& a, int32_t& b) {
 // exchange, 3 = no squares/bins, 4 = loads only.
 template <typename T, int ABL = 0>
 __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, int z0, int nslices,
-                                                   unsigned long long* __restrict__ counts) {
+                                                   unsigned long long* __restrict__ counts,
+                                                   unsigned long long add_n = 0) {
   // int8 seeds: after phase 1 |x| <= 64 * 127 fits int16, so the exchange takes 32 KB
   // and three workgroups share a CU
   constexpr bool kNarrow = sizeof(T) == 1;
@@ -650,6 +651,7 @@ __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, in
   }
   __syncthreads();
   if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
+  if (add_n && blockIdx.x == 0 && tid == 0) atomicAdd(counts, add_n);  // n, once per job
 }
 
 // ---------------------------------------------------------------- MFMA tile (int8 seeds)
@@ -843,7 +845,8 @@ __device__ __forceinline__ int lds_e2(int e) {
 
 template <bool PF, int STAGGER = 0>
 __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, const uint16_t* __restrict__ order,
-                                                int z0, int nslices, unsigned long long* __restrict__ counts) {
+                                                int z0, int nslices, unsigned long long* __restrict__ counts,
+                                                unsigned long long add_n) {
   __shared__ __attribute__((aligned(16))) int16_t lds[kLo];
   __shared__ unsigned long long bins[17];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -985,23 +988,24 @@ __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, 
   if (cur_w >= 0) flush();
   __syncthreads();
   if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
+  if (add_n && blockIdx.x == 0 && tid == 0) atomicAdd(counts, add_n);  // n, once per job
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_mfma2_kernel(
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts) {
-  tile_mfma2_body<false>(buf, order, z0, nslices, counts);
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_mfma2_body<false>(buf, order, z0, nslices, counts, add_n);
 }
 template <int STAGGER>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_mfma2_pf_st_kernel(
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts) {
-  tile_mfma2_body<true, STAGGER>(buf, order, z0, nslices, counts);
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_mfma2_body<true, STAGGER>(buf, order, z0, nslices, counts, add_n);
 }
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_mfma2_pf_kernel(
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts) {
-  tile_mfma2_body<true>(buf, order, z0, nslices, counts);
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_mfma2_body<true>(buf, order, z0, nslices, counts, add_n);
 }
 
 __global__ void max_column_kernel(const uint32_t* __restrict__ cnt, unsigned* __restrict__ out) {
@@ -1057,16 +1061,17 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
 }
 
 template <typename T>
-int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s) {
+int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s, unsigned long long add_n = 0) {
   T* buf = reinterpret_cast<T*>(st.d_buf);
   const dim3 grid((unsigned)std::min(st.grid * (sizeof(T) == 1 ? 3 : 2), z1 - z0));
 #ifdef SCT_ABLATION
   static const int abl = getenv("SCT_SPECTRAL_ABL") ? atoi(getenv("SCT_SPECTRAL_ABL")) : 0;
-  if (abl == 1) hipLaunchKernelGGL((tile_kernel<T, 1>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
-  if (abl == 2) hipLaunchKernelGGL((tile_kernel<T, 2>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
-  if (abl == 3) hipLaunchKernelGGL((tile_kernel<T, 3>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
-  if (abl == 4) hipLaunchKernelGGL((tile_kernel<T, 4>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
+  if (abl == 1) hipLaunchKernelGGL((tile_kernel<T, 1>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, 0ull);
+  if (abl == 2) hipLaunchKernelGGL((tile_kernel<T, 2>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, 0ull);
+  if (abl == 3) hipLaunchKernelGGL((tile_kernel<T, 3>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, 0ull);
+  if (abl == 4) hipLaunchKernelGGL((tile_kernel<T, 4>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, 0ull);
   if (abl >= 1 && abl <= 4) {
+    if (add_n) hipLaunchKernelGGL(add_kernel, dim3(1), dim3(1), 0, s, counts, add_n);
     SCT_LAUNCH_CHECK();
     return SCT_OK;
   }
@@ -1086,34 +1091,35 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
         if (mabl == 13) hipLaunchKernelGGL(tile_mfma_kernel<3>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 14) hipLaunchKernelGGL(tile_mfma_kernel<4>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 15) hipLaunchKernelGGL(tile_mfma_kernel<5>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
-        if (mabl == 20) hipLaunchKernelGGL(tile_mfma2_pf_st_kernel<20>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
-        if (mabl == 21) hipLaunchKernelGGL(tile_mfma2_pf_st_kernel<40>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+        if (mabl == 20) hipLaunchKernelGGL(tile_mfma2_pf_st_kernel<20>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
+        if (mabl == 21) hipLaunchKernelGGL(tile_mfma2_pf_st_kernel<40>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
         if (mabl == 17 || mabl == 19) {  // two-stage without prefetch / the one-stage kernel
           int per_cu = 0;
           if (mabl == 17) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma2_kernel, 256, 0);
           else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma_kernel<0>, 256, 0);
           const dim3 g2((unsigned)std::min(st.grid * std::max(per_cu, 1), z1 - z0));
-          if (mabl == 17) hipLaunchKernelGGL(tile_mfma2_kernel, g2, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+          if (mabl == 17) hipLaunchKernelGGL(tile_mfma2_kernel, g2, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
           else hipLaunchKernelGGL(tile_mfma_kernel<0>, g2, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         }
+        if (add_n) hipLaunchKernelGGL(add_kernel, dim3(1), dim3(1), 0, s, counts, add_n);
         SCT_LAUNCH_CHECK();
         return SCT_OK;
       }
 #endif
-      hipLaunchKernelGGL(tile_mfma2_pf_kernel, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
+      hipLaunchKernelGGL(tile_mfma2_pf_kernel, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
       SCT_LAUNCH_CHECK();
       return SCT_OK;
     }
   }
-  hipLaunchKernelGGL(tile_kernel<T>, grid, dim3(256), 0, s, buf, z0, z1 - z0, counts);
+  hipLaunchKernelGGL(tile_kernel<T>, grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, add_n);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
 
 template <typename T>
-int launch_chunk(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s) {
+int launch_chunk(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s, unsigned long long add_n) {
   const int rc = launch_seed<T>(st, z0, z1, s);
-  return rc != SCT_OK ? rc : launch_tile<T>(st, z0, z1, counts, s);
+  return rc != SCT_OK ? rc : launch_tile<T>(st, z0, z1, counts, s, add_n);
 }
 
 // Bench aid: seed and tile kernels timed apart, each as `repeats` back-to-back launches on
@@ -1239,14 +1245,12 @@ int count(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_count
   if (st.n < 2 || z_begin == z_end) return SCT_OK;
   for (int64_t z0 = z_begin; z0 < z_end; z0 += st.chunk) {
     const int z1 = (int)std::min<int64_t>(z_end, z0 + st.chunk);
-    const int rc = st.elem_bytes == 1   ? launch_chunk<int8_t>(st, (int)z0, z1, d_counts, s)
-                   : st.elem_bytes == 2 ? launch_chunk<int16_t>(st, (int)z0, z1, d_counts, s)
-                                        : launch_chunk<int32_t>(st, (int)z0, z1, d_counts, s);
+    // d_counts[0] += n by the job's first tile launch (the range holding slice 0)
+    const unsigned long long add_n = z0 == 0 ? (unsigned long long)st.n : 0ull;
+    const int rc = st.elem_bytes == 1   ? launch_chunk<int8_t>(st, (int)z0, z1, d_counts, s, add_n)
+                   : st.elem_bytes == 2 ? launch_chunk<int16_t>(st, (int)z0, z1, d_counts, s, add_n)
+                                        : launch_chunk<int32_t>(st, (int)z0, z1, d_counts, s, add_n);
     if (rc != SCT_OK) return rc;
-  }
-  if (z_begin == 0) {
-    hipLaunchKernelGGL(add_kernel, dim3(1), dim3(1), 0, s, d_counts, (unsigned long long)st.n);
-    SCT_LAUNCH_CHECK();
   }
   return SCT_OK;
 }
