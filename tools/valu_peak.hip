@@ -24,6 +24,10 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint64_t* clk, uint32_t 
 #pragma unroll
   for (int c = 0; c < CH; ++c) x[c] = seed * (threadIdx.x + 1) + c * 0x9E3779B9u;
   const uint32_t y = seed ^ threadIdx.x, z = seed + blockIdx.x;
+  double dacc[CH];  // OPs 18-20: fp64 accumulate of a square
+#pragma unroll
+  for (int c = 0; c < CH; ++c) dacc[c] = (double)x[c];
+  const double dz = (double)(int)z;
   uint64_t t0 = __builtin_amdgcn_s_memtime();
   uint64_t r0 = __builtin_amdgcn_s_memrealtime();
   for (int i = 0; i < ITERS; ++i) {
@@ -53,6 +57,17 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint64_t* clk, uint32_t 
       if constexpr (OP == 15) asm volatile("v_pk_add_u16 %0, %1, %0" : "+v"(x[c]) : "v"(y));
       if constexpr (OP == 16) asm volatile("v_mad_u32_u24 %0, %1, %2, %0" : "+v"(x[c]) : "v"(y), "v"(z));
       if constexpr (OP == 17) asm volatile("v_mul_lo_u32 %0, %1, %0" : "+v"(x[c]) : "v"(y));
+      if constexpr (OP == 18) asm volatile("v_fma_f64 %0, %1, %1, %0" : "+v"(dacc[c]) : "v"(dz));
+      if constexpr (OP == 19) {  // int32 -> f64, then acc += v * v
+        double t;
+        asm volatile("v_cvt_f64_i32 %0, %1" : "=v"(t) : "v"(x[c]));
+        asm volatile("v_fma_f64 %0, %1, %1, %0" : "+v"(dacc[c]) : "v"(t));
+      }
+      if constexpr (OP == 20) {
+        double t;
+        asm volatile("v_cvt_f64_i32 %0, %1" : "=v"(t) : "v"(x[c]));
+        x[c] ^= (uint32_t)__builtin_bit_cast(uint64_t, t);
+      }
       if constexpr (OP == 3) {  // the kernel's mix: 2 bitop3 : 1 bcnt
         x[c] = __builtin_amdgcn_bitop3_b32(x[c], y, z, 0xE8);
         x[c] = __builtin_amdgcn_bitop3_b32(x[c], y, z, 0x96);
@@ -64,7 +79,7 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint64_t* clk, uint32_t 
   uint64_t r1 = __builtin_amdgcn_s_memrealtime();
   uint32_t acc = 0;
 #pragma unroll
-  for (int c = 0; c < CH; ++c) acc ^= x[c];
+  for (int c = 0; c < CH; ++c) acc ^= x[c] ^ (uint32_t)__builtin_bit_cast(uint64_t, dacc[c]);
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
   if (threadIdx.x == 0) {
     clk[2 * blockIdx.x] = t1 - t0;
@@ -127,6 +142,9 @@ int main() {
   run<15>("v_pk_add_u16", 1, blocks);
   run<16>("v_mad_u32_u24", 1, blocks);
   run<17>("v_mul_lo_u32", 1, blocks);
+  run<18>("v_fma_f64", 1, blocks);
+  run<19>("v_cvt_f64_i32+v_fma_f64", 2, blocks);
+  run<20>("v_cvt_f64_i32(+xor)", 1, blocks);
   run<2>("v_xor_b32@1wps", 1, 256);
   run<2>("v_xor_b32@2wps", 1, 512);
   run<2>("v_xor_b32@4wps", 1, 1024);
