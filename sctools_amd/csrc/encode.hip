@@ -140,13 +140,39 @@ __global__ __launch_bounds__(WG) void encode_tiled_kernel(const uint8_t* __restr
   const int tid = threadIdx.x;
   constexpr int TILE = R * WG;  // records per workgroup iteration: R in flight per lane
   const int64_t ntiles = (n + TILE - 1) / TILE;
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  // a thread's 16-B loads of a tile are all issued before any of them is stored to LDS (8
+  // per batch: 7 at L = 28).  When one batch holds a whole tile (L * R <= 128) the next
+  // tile's loads are issued right after this tile's LDS stores, so they fly while this
+  // tile is packed.
+  const bool pipe = L * R <= 128;
+  v4u t[8];
+  auto fetch = [&](int64_t tl, int64_t k0) {
+    const int64_t rb = tl * TILE, nr = n - rb < TILE ? n - rb : TILE;
+    const int64_t m16 = (nr * L) >> 4;
+    const v4u* s4 = reinterpret_cast<const v4u*>(seqs + rb * L);  // 16-B aligned: TILE * L % 16 == 0
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t k = k0 + u * WG + tid;
+      if (k < m16) t[u] = __builtin_nontemporal_load(s4 + k);
+    }
+  };
+  if (pipe && (int64_t)blockIdx.x < ntiles) fetch(blockIdx.x, 0);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t r0 = tile * TILE;
     const int64_t nrec = n - r0 < TILE ? n - r0 : TILE;
     const int64_t nbytes = nrec * L;
-    const uint8_t* src = seqs + r0 * L;  // 16-byte aligned: TILE * L is a multiple of 16
+    const uint8_t* src = seqs + r0 * L;
     const int64_t n16 = nbytes >> 4;
-    for (int64_t k = tid; k < n16; k += WG) stage4[k] = reinterpret_cast<const uint4*>(src)[k];
+    for (int64_t k0 = 0; k0 < n16; k0 += 8 * WG) {
+      if (!pipe) fetch(tile, k0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t k = k0 + u * WG + tid;
+        if (k < n16) stage4[k] = make_uint4(t[u].x, t[u].y, t[u].z, t[u].w);
+      }
+    }
+    if (pipe && tile + gridDim.x < ntiles) fetch(tile + gridDim.x, 0);
     for (int64_t k = (n16 << 4) + tid; k < nbytes; k += WG)
       reinterpret_cast<uint8_t*>(stage4)[k] = src[k];
     __syncthreads();
@@ -157,7 +183,27 @@ __global__ __launch_bounds__(WG) void encode_tiled_kernel(const uint8_t* __restr
         const uint8_t* rec = stage + (int64_t)lr * L;
         uint64_t code = 0;
         uint32_t fl = 0;
-        if ((L & 3) == 0) {
+        bool done = false;
+        if (BITS == 2 && (L & 3) == 0) {
+          // TwoBit, 4 bases per dword without the LUT: u = the bytes upper-cased; their low 3
+          // bits (A 1, C 3, T 4, G 7) index a v_perm byte table of the expected letters, so
+          // u == table[u & 7] in every byte iff all four are ACGTacgt.  The values are
+          // (u >> 1) & 3 per byte (A 0, C 1, T 2, G 3), gathered MSB-first into one byte by
+          // one multiply: v * (1 + 2^10 + 2^20 + 2^30) puts byte j's value at bits 30 - 2j,
+          // every other partial product in a disjoint 2-bit slot below 24 (no carries).
+          // A record with any other byte takes the LUT loop below (flags, N draws).
+          const uint32_t* rw = reinterpret_cast<const uint32_t*>(rec);
+          uint32_t bad = 0;
+          for (int k = 0; k < (L >> 2); ++k) {
+            const uint32_t u = rw[k] & 0xDFDFDFDFu;
+            bad |= u ^ __builtin_amdgcn_perm(0x47010154u, 0x43014101u, u & 0x07070707u);
+            code = (code << 8) | (((u >> 1) & 0x03030303u) * 0x40100401u >> 24);
+          }
+          done = bad == 0;
+          if (!done) code = 0;
+        }
+        if (done) {
+        } else if ((L & 3) == 0) {
           const uint32_t* rw = reinterpret_cast<const uint32_t*>(rec);
           for (int k = 0; k < (L >> 2); ++k) {
             const uint32_t w = rw[k];
@@ -345,7 +391,17 @@ extern "C" int sct_encode(int kind, const uint8_t* seqs, int64_t n, int64_t stri
   if (stride == L && words == 1 && L > 0 && L <= 64 && (uintptr_t)seqs % 16 == 0) {
     constexpr int R = 4;  // 4 x 256 records staged per iteration (28 KiB at L = 28)
     const size_t lds = (size_t)R * WG * L;
-    const unsigned grid = (unsigned)std::min<int64_t>(sct::ceil_div(n, R * WG), 4096);
+    // persistent: exactly the resident workgroups (a 4096 grid at 5 per CU left a partial
+    // last round of workgroups, each looping over many tiles)
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    if (kind == 2)
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_tiled_kernel<2, R>, WG, lds);
+    else
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_tiled_kernel<3, R>, WG, lds);
+    const int64_t resident = (int64_t)std::max(cus, 1) * std::max(per_cu, 1);
+    const unsigned grid = (unsigned)std::min<int64_t>(sct::ceil_div(n, R * WG), resident);
     if (kind == 2)
       hipLaunchKernelGGL((encode_tiled_kernel<2, R>), dim3(grid), dim3(WG), lds,
                          sct::as_stream(stream), seqs, n, L, codes, gc, flags);
