@@ -61,7 +61,8 @@ __device__ __forceinline__ uint32_t byte_mask4(uint32_t hi_bits) {  // bit 7 of 
 }
 
 __device__ __forceinline__ uint32_t load_mask(const uint8_t* __restrict__ buf, int64_t n, int64_t p0,
-                                              int text, uint32_t* kinds_crlf, uint32_t* nonascii) {
+                                              int text, uint32_t* kinds_crlf, uint32_t* nonascii,
+                                              uint4* bytes_out = nullptr) {
   uint32_t w[4];
   if (p0 + 16 <= n) {
     const uint4 v = *reinterpret_cast<const uint4*>(buf + p0);
@@ -75,6 +76,7 @@ __device__ __forceinline__ uint32_t load_mask(const uint8_t* __restrict__ buf, i
       w[k] = x;
     }
   }
+  if (bytes_out) *bytes_out = make_uint4(w[0], w[1], w[2], w[3]);
   const uint32_t valid = p0 + 16 <= n ? 0xFFFFu : (uint32_t)((1u << (n - p0)) - 1u);
   uint32_t lf = 0, cr = 0, na = 0;
 #pragma unroll
@@ -213,14 +215,18 @@ __global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__
                                                      unsigned long long* __restrict__ first_bad) {
   __shared__ uint32_t term[MAX_TERM];
   __shared__ Action act[MAX_TERM / 2 + 2];  // 33 KiB with term[]: 4 workgroups per CU
+  __shared__ uint4 tile_bytes[TILE / 16];    // the tile itself: slices inside it copy from LDS
   const int64_t t0 = (int64_t)blockIdx.x * TILE;
   const int64_t p0 = t0 + (int64_t)threadIdx.x * 16;
   uint32_t m = 0, crlf = 0, na;
   int vj = -1;
+  uint4 mine = make_uint4(0, 0, 0, 0);
   if (p0 < n) {
-    m = load_mask(buf, n, p0, text, &crlf, &na);
+    m = load_mask(buf, n, p0, text, &crlf, &na, &mine);
     vj = virtual_in(buf, n, fs, p0, text);
   }
+  tile_bytes[threadIdx.x] = mine;
+  const uint32_t* tile32 = reinterpret_cast<const uint32_t*>(tile_bytes);
   const uint32_t c = __popc(m) + (vj >= 0);
   using BS = hipcub::BlockScan<uint32_t, WG>;
   __shared__ typename BS::TempStorage tmp;
@@ -313,9 +319,25 @@ __global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__
     const int nd = w / 4;
     if (b - a == w && b <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
         ((uintptr_t)o & 3) == 0) {
-      const uint32_t* d = reinterpret_cast<const uint32_t*>(buf + base);
+      // rows inside the tile read its LDS copy; the rest (lines running past it) read L2
+      const uint32_t* d = base + 4 * (nd + 1) <= t0 + TILE ? tile32 + ((base - t0) >> 2)
+                                                           : reinterpret_cast<const uint32_t*>(buf + base);
       const uint32_t sh = (uint32_t)(s0 & 3);
       uint32_t* od = reinterpret_cast<uint32_t*>(o);
+      // the common widths as one vector store (16-B CB / 8-B UMI rows of aligned outputs)
+      if (nd == 4 && ((uintptr_t)o & 15) == 0) {
+        const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3], x4 = d[4];
+        *reinterpret_cast<uint4*>(o) =
+            make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                       __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+        continue;
+      }
+      if (nd == 2 && ((uintptr_t)o & 7) == 0) {
+        const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
+        *reinterpret_cast<uint2*>(o) =
+            make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
+        continue;
+      }
       uint32_t lo = d[0];
       for (int q2 = 0; q2 < nd; ++q2) {
         const uint32_t hi = d[q2 + 1];
