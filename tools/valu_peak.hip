@@ -68,6 +68,10 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint64_t* clk, uint32_t 
         asm volatile("v_cvt_f64_i32 %0, %1" : "=v"(t) : "v"(x[c]));
         x[c] ^= (uint32_t)__builtin_bit_cast(uint64_t, t);
       }
+      if constexpr (OP == 21) {  // packed int16 dot: acc += a.lo * b.lo + a.hi * b.hi
+        typedef short s2 __attribute__((ext_vector_type(2)));
+        x[c] = (uint32_t)__builtin_amdgcn_sdot2(__builtin_bit_cast(s2, y), __builtin_bit_cast(s2, z), (int)x[c], false);
+      }
       if constexpr (OP == 3) {  // the kernel's mix: 2 bitop3 : 1 bcnt
         x[c] = __builtin_amdgcn_bitop3_b32(x[c], y, z, 0xE8);
         x[c] = __builtin_amdgcn_bitop3_b32(x[c], y, z, 0x96);
@@ -145,6 +149,7 @@ int main() {
   run<18>("v_fma_f64", 1, blocks);
   run<19>("v_cvt_f64_i32+v_fma_f64", 2, blocks);
   run<20>("v_cvt_f64_i32(+xor)", 1, blocks);
+  run<21>("v_dot2_i32_i16", 1, blocks);
   run<2>("v_xor_b32@1wps", 1, 256);
   run<2>("v_xor_b32@2wps", 1, 512);
   run<2>("v_xor_b32@4wps", 1, 1024);
