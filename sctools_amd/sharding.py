@@ -21,7 +21,7 @@ import numpy as np
 
 from . import _lib
 
-__all__ = ["item_range", "combine_counts", "allpairs_histogram_sharded", "gather_ranges", "nearest_sharded",
+__all__ = ["item_range", "combine_counts", "ShardedAllPairs", "allpairs_histogram_sharded", "gather_ranges", "nearest_sharded",
            "encode_sharded"]
 
 
@@ -42,34 +42,112 @@ def combine_counts(counts, group=None, scheme=_lib.SCHEME_SUBSETS, nbins=None):
     return _lib.counts_to_hist(host, scheme, nbins)
 
 
-def allpairs_histogram_sharded(codes, code_bits=None, group=None, device=None, stream=None):
+class ShardedAllPairs:
+    """One rank's share of ``Barcodes.summarize_hamming_distances`` (barcode.py:39-46) on
+    its own GPU: a plan over this rank's replica of the codes, the rank's item range
+    ``item_range(items, rank, W)`` (SPECTRAL: transform slices; pair schemes: row block x
+    column chunk items plus moment share r of W), and the one all-reduce of the counts.
+
+    ``step()`` is the whole per-rank hot path -- build, count, all-reduce (W > 1), D2H,
+    exact inversion -- and returns the histogram (np.uint64) on every rank.  The MOMENTS
+    scheme's moment pass runs on a side stream beside the build.  With ``timing=True``
+    every step records HIP events (on the streams the work runs on) around the build, the
+    count and the all-reduce; ``timings()`` averages them.  bench.py times this object."""
+
+    def __init__(self, codes, code_bits=None, scheme=_lib.SCHEME_AUTO, group=None, device=None):
+        import torch
+        self.group = group
+        self.world, self.rank = _group_info(group)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        if isinstance(codes, np.ndarray):
+            host = np.ascontiguousarray(codes, dtype=np.uint64).reshape(-1)
+            self.d_codes = torch.from_numpy(host.view(np.int64)).to(self.device)
+        else:
+            self.d_codes = codes.to(device=self.device, dtype=torch.int64).contiguous().reshape(-1)
+            host = None
+        n = int(self.d_codes.numel())
+        if code_bits is None:
+            if host is None:
+                host = self.d_codes.cpu().numpy().view(np.uint64)
+            code_bits = max(1, int(np.bitwise_or.reduce(host)).bit_length()) if n else 1
+        self.n = n
+        self.plan = _lib.AllPairsPlan(self.d_codes.data_ptr(), n, code_bits, scheme=scheme)
+        self.begin, self.end = item_range(self.plan.items, self.rank, self.world)
+        self.counts = torch.zeros(self.plan.ncounts, dtype=torch.int64, device=self.device)
+        self.stream = torch.cuda.current_stream(self.device)
+        self.side = torch.cuda.Stream(self.device)
+        self._ev = {k: torch.cuda.Event(enable_timing=True) for k in
+                    ("b0", "b1", "c1", "a1", "m0", "m1")}
+        self._ev_zero, self._ev_mom = torch.cuda.Event(), torch.cuda.Event()
+        self._t = {"build_ms": [], "count_ms": [], "allreduce_us": [], "moments_ms": []}
+
+    @property
+    def scheme(self):
+        return self.plan.scheme
+
+    def my_pairs(self):
+        return self.plan.range_pairs(self.begin, self.end)
+
+    def step(self, timing=False):
+        import torch.distributed as dist
+        ev, s, side, sptr = self._ev, self.stream, self.side, self.stream.cuda_stream
+        self.counts.zero_()
+        moments = self.plan.scheme == _lib.SCHEME_MOMENTS
+        if moments:  # independent of the table: beside the build
+            self._ev_zero.record(s)
+            side.wait_event(self._ev_zero)
+            if timing:
+                ev["m0"].record(side)
+            self.plan.moments(self.counts.data_ptr(), self.rank, self.world, side.cuda_stream)
+            if timing:
+                ev["m1"].record(side)
+            self._ev_mom.record(side)
+        if timing:
+            ev["b0"].record(s)
+        self.plan.build(sptr, self.begin, self.end)  # only what this rank's items read
+        if moments:
+            s.wait_event(self._ev_mom)
+        if timing:
+            ev["b1"].record(s)
+        self.plan.count(self.counts.data_ptr(), self.begin, self.end, 0, sptr)
+        if timing:
+            ev["c1"].record(s)
+        if self.world > 1:
+            dist.all_reduce(self.counts, op=dist.ReduceOp.SUM, group=self.group)
+        if timing:
+            ev["a1"].record(s)
+        host = self.counts.cpu().numpy().astype(np.int64).view(np.uint64)  # syncs the stream
+        hist = _lib.counts_to_hist(host, self.plan.scheme, self.plan.nbins)
+        if timing:
+            self._t["build_ms"].append(ev["b0"].elapsed_time(ev["b1"]))
+            self._t["count_ms"].append(ev["b1"].elapsed_time(ev["c1"]))
+            self._t["allreduce_us"].append(1e3 * ev["c1"].elapsed_time(ev["a1"]))
+            if moments:
+                self._t["moments_ms"].append(ev["m0"].elapsed_time(ev["m1"]))
+        return hist
+
+    def reset_timings(self):
+        self._t = {k: [] for k in self._t}
+
+    def timings(self):
+        return {k: (float(np.mean(v)) if v else None) for k, v in self._t.items()}
+
+    def close(self):
+        self.plan.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def allpairs_histogram_sharded(codes, code_bits=None, group=None, device=None, scheme=_lib.SCHEME_AUTO):
     """Histogram of TwoBit distances over all unordered pairs of `codes` (np.uint64 or a
     torch tensor), sharded over the ranks of `group` (one GPU each).  Call on every rank
-    with the same codes."""
-    import torch
-    import torch.distributed as dist
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    device = device or torch.device("cuda", torch.cuda.current_device())
-    if isinstance(codes, np.ndarray):
-        d_codes = torch.from_numpy(np.ascontiguousarray(codes, dtype=np.uint64).view(np.int64)).to(device)
-    else:
-        d_codes = codes.to(device=device, dtype=torch.int64).contiguous()
-    n = int(d_codes.numel())
-    if code_bits is None:
-        orv = int(np.bitwise_or.reduce(d_codes.cpu().numpy().view(np.uint64))) if n else 0
-        code_bits = max(1, orv.bit_length())
-    plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, code_bits)
-    try:
-        s = (stream or torch.cuda.current_stream(device)).cuda_stream
-        b, e = item_range(plan.items, rank, world)
-        counts = torch.zeros(plan.ncounts, dtype=torch.int64, device=device)
-        plan.build(s, b, e)  # only the column chunks of this rank's items
-        plan.moments(counts.data_ptr(), rank, world, s)
-        plan.count(counts.data_ptr(), b, e, 0, s)
-        return combine_counts(counts, group, plan.scheme, plan.nbins)
-    finally:
-        plan.close()
+    with the same codes; every rank gets the whole histogram."""
+    with ShardedAllPairs(codes, code_bits, scheme, group, device) as job:
+        return job.step()
 
 
 def _group_info(group):
@@ -113,6 +191,10 @@ def nearest_sharded(kind, whitelist, queries, max_d=1, code_bits=None, group=Non
     world, rank = _group_info(group)
     q = np.ascontiguousarray(queries, dtype=np.uint64).reshape(-1)
     b, e = item_range(q.size, rank, world)
+    if code_bits is None:  # the block split's width, as barcode.nearest_whitelist picks it
+        wl = np.ascontiguousarray(whitelist, dtype=np.uint64).reshape(-1)
+        orv = int(np.bitwise_or.reduce(wl)) if wl.size else 0
+        code_bits = min(64, max(orv.bit_length(), kind * (max_d + 1), 1))
     idx, dist_ = (fn or _lib.nearest)(kind, whitelist, q[b:e], max_d, code_bits)
     return gather_ranges(np.asarray(idx, dtype=np.int32), q.size, group), \
         gather_ranges(np.asarray(dist_, dtype=np.uint8), q.size, group)

@@ -1,0 +1,55 @@
+"""GPU, 2 ranks sharing the one GPU of the test box over gloo: the product's per-rank
+path (sharding.ShardedAllPairs: plan, build of the rank's items, count of its slice /
+item range, all-reduce, inversion) with real kernels on every rank, against the oracle.
+The 8-GPU RCCL run itself is the driver's; this proves the per-rank split is exact."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+from sctools_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n, seed, scheme, out_path):
+    import torch
+    import torch.distributed as dist
+    from sctools_amd import _lib, sharding
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    _lib.check(_lib.lib().sct_set_device(0))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        codes = synthetic.whitelist_codes(n, 16, seed)
+        with sharding.ShardedAllPairs(codes, 32, scheme) as job:
+            assert job.scheme == scheme
+            assert (job.begin, job.end) == sharding.item_range(job.plan.items, rank, world)
+            hist = job.step(timing=True)
+            mine = job.my_pairs()
+        np.savez(out_path % rank, hist=hist.astype(np.int64), mine=mine)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("scheme,world,n", [(2, 2, 20_000), (1, 2, 20_000), (0, 3, 6_000)])
+def test_ranks_on_gpu_match_oracle(tmp_path, scheme, world, n):
+    out = str(tmp_path / "r%d.npz")
+    mp.spawn(_worker, args=(world, _free_port(), n, 41 + scheme, scheme, out), nprocs=world, join=True)
+    ref = O.c_hist16(synthetic.whitelist_codes(n, 16, 41 + scheme))[0][:17]
+    shares = 0
+    for r in range(world):
+        z = np.load(out % r)
+        assert z["hist"].tolist() == ref.tolist()
+        shares += int(z["mine"])
+    assert shares == n * (n - 1) // 2

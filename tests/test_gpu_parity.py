@@ -574,3 +574,61 @@ def test_encode_stream_pipeline():
     random.seed(3)
     b = [TwoBit.encode(seqs[r].tobytes()) for r in range(0, 1000)]
     assert a[:1000].tolist() == b
+
+
+# ---------------------------------------------------------------- headline sizes vs the oracle
+def test_allpairs_737k_spectral_bin_for_bin():
+    """Config 2 at full size: AUTO (= SPECTRAL) histogram of all 271,790,530,560 pairs,
+    bin for bin against the C oracle's AVX-512 popcount loop over every pair."""
+    n, L, seed = synthetic.CONFIGS[2]
+    codes = synthetic.whitelist_codes(n, L, seed)
+    torch = pytest.importorskip("torch")
+    d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 32)
+    assert plan.scheme == _lib.SCHEME_SPECTRAL
+    plan.close()
+    hist = sharding.allpairs_histogram_sharded(codes, 32)
+    ref, simd = O.c_hist16(codes)
+    assert hist.astype(np.int64).tolist() == ref[:17].tolist()
+    assert int(hist.sum()) == n * (n - 1) // 2
+    # the drop-in on the same set
+    s = barcode.Barcodes.from_iterable_encoded(codes.tolist(), 16)
+    assert s.summarize_hamming_distances() == O.summary_from_hist_numpy(ref[:17])
+
+
+@pytest.mark.parametrize("m", [126, 127, 128, 129])
+def test_allpairs_spectral_column_width_edges(m):
+    """A transform column (low 14 bits) holding exactly m codes: 127 is the last int8
+    intermediate, 128 the first int16; 128 / 129 are the last 4-group / first 5-group
+    column of the plane build.  SPECTRAL vs the oracle."""
+    rng = np.random.default_rng(m)
+    hi = np.unique(rng.integers(0, 1 << 18, 4 * m).astype(np.uint64))[:m]
+    col = (hi << np.uint64(14)) | np.uint64(0x1ABC)
+    rest = synthetic.whitelist_codes(5000, 16, seed=m)
+    rest = rest[(rest & np.uint64(0x3FFF)) != np.uint64(0x1ABC)]
+    codes = np.concatenate([col, rest])
+    rng.shuffle(codes)
+    assert np.bincount((codes & np.uint64(0x3FFF)).astype(np.int64)).max() == m
+    hist = _spectral_hist(codes, [(0, 1 << 17), (1 << 17, 1 << 18)])
+    assert hist.astype(np.int64).tolist() == O.c_hist16(codes)[0][:17].tolist()
+
+
+def test_allpairs_config5_spectral_vs_moments():
+    """Config 5's 3,686,400 codes (int16 intermediate, ~225 codes per column): SPECTRAL vs
+    the MOMENTS pair kernel over all 6.79e12 pairs, the pair count, and the mean distance
+    the per-position base counts imply."""
+    torch = pytest.importorskip("torch")
+    n, L, seed = synthetic.CONFIGS[5]
+    codes = synthetic.whitelist_codes(n, L, seed)
+    d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
+    hs = sharding.allpairs_histogram_sharded(d_codes, 32, scheme=_lib.SCHEME_SPECTRAL)
+    hm = sharding.allpairs_histogram_sharded(d_codes, 32, scheme=_lib.SCHEME_MOMENTS)
+    assert hs.tolist() == hm.tolist()
+    P = n * (n - 1) // 2
+    assert int(hs.sum()) == P
+    bases = (codes[:, None] >> (2 * np.arange(16, dtype=np.uint64))) & np.uint64(3)
+    agree = 0
+    for p in range(16):
+        cnt = np.bincount(bases[:, p].astype(np.int64), minlength=4).astype(object)
+        agree += int(cnt.dot(cnt - 1)) // 2
+    assert sum(d * int(x) for d, x in enumerate(hs)) == 16 * P - agree
