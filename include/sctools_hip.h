@@ -205,6 +205,21 @@ int sct_counts_to_hist_ex(int scheme, const uint64_t* counts, int ncounts, uint6
 int sct_hamming_hist_allpairs_host(const uint64_t* codes, int64_t n, int code_bits,
                                    uint64_t* hist, int nbins);
 
+/* ---------------------------------------------------------------- all-pairs, wide codes
+ * The same pair loop (barcode.py:42-43) for keys of any width up to 256 limbs: codes are
+ * n x `words` little-endian uint64 limbs (Python ints >= 2^64: ThreeBit-encoded 22..28-bp
+ * barcodes, TwoBit > 32 bp).  TwoBit.hamming_distance (encodings.py:113-121) of multi-limb
+ * codes = the sum of the per-limb counts (no 2-bit group straddles a limb).  Work items
+ * are pairs of 256-code tiles (a <= b, row-major), so contiguous item ranges shard across
+ * devices; sct_allpairs_wide ACCUMULATES hist[d] (nbins = 32 * words + 1 uint64) with
+ * the pairs i < j of items [item_begin, item_end). */
+int sct_allpairs_wide_geometry(int64_t n, int words, int64_t* items, int* nbins);
+int sct_allpairs_wide_range_pairs(int64_t n, int64_t item_begin, int64_t item_end, int64_t* pairs);
+int sct_allpairs_wide(const uint64_t* d_codes, int64_t n, int words, int64_t item_begin, int64_t item_end,
+                      uint64_t* d_hist, int nbins, void* stream);
+int sct_hamming_hist_allpairs_wide_host(const uint64_t* codes, int64_t n, int words, uint64_t* hist,
+                                        int nbins);
+
 /* ---------------------------------------------------------------- base frequency
  * Replaces Barcodes.base_frequency (src/sctools/barcode.py:48-70): out[p*4 + v] =
  * number of codes whose base p (0 = first, MSB-first TwoBit packing) has 2-bit value

@@ -66,6 +66,10 @@ SIGNATURES = {
     "sct_counts_to_hist_ex": [_i32, _vp, _i32, _vp, _i32],
     "sct_hamming_hist_allpairs_host": [_vp, _i64, _i32, _vp, _i32],
     "sct_summary_from_hist": [_vp, _i32, _vp],
+    "sct_allpairs_wide_geometry": [_i64, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_i32)],
+    "sct_allpairs_wide_range_pairs": [_i64, _i64, _i64, ctypes.POINTER(_i64)],
+    "sct_allpairs_wide": [_vp, _i64, _i32, _i64, _i64, _vp, _i32, _vp],
+    "sct_hamming_hist_allpairs_wide_host": [_vp, _i64, _i32, _vp, _i32],
     "sct_nearest_plan_create": [_i32, _vp, _i64, _i32, _i32, _vp, ctypes.POINTER(_vp)],
     "sct_nearest_plan_destroy": [_vp],
     "sct_nearest_query": [_vp, _vp, _i64, _vp, _vp, _vp],
@@ -253,6 +257,30 @@ def hamming_hist_allpairs(codes, code_bits=None):
     hist = np.zeros(nbins, dtype=np.uint64)
     check(lib().sct_hamming_hist_allpairs_host(_ptr(codes), codes.size, code_bits, _ptr(hist), nbins))
     return hist
+
+
+def hamming_hist_allpairs_wide(limbs):
+    """Histogram (uint64[32*words+1]) of TwoBit distances over all unordered pairs of
+    multi-limb codes ((n, words) little-endian uint64: Python ints of any size)."""
+    limbs = np.ascontiguousarray(limbs, dtype=np.uint64)
+    limbs = limbs.reshape(limbs.shape[0], -1) if limbs.ndim else limbs.reshape(0, 1)
+    n, words = limbs.shape
+    hist = np.zeros(32 * words + 1, dtype=np.uint64)
+    check(lib().sct_hamming_hist_allpairs_wide_host(_ptr(limbs), n, words, _ptr(hist), hist.size))
+    return hist
+
+
+def wide_geometry(n, words):
+    """(items, nbins) of the wide all-pairs kernel (host arithmetic)."""
+    it, nb = _i64(0), _i32(0)
+    check(lib().sct_allpairs_wide_geometry(n, words, ctypes.byref(it), ctypes.byref(nb)))
+    return it.value, nb.value
+
+
+def wide_range_pairs(n, begin, end):
+    p = _i64(0)
+    check(lib().sct_allpairs_wide_range_pairs(n, begin, end, ctypes.byref(p)))
+    return p.value
 
 
 def counts_to_hist(counts, scheme=SCHEME_SUBSETS, nbins=None):

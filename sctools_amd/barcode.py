@@ -9,7 +9,7 @@ The README's ``ObservedBarcodeSet`` / ``PriorBarcodeSet`` names (README.md:33) a
 provided as subclasses.
 """
 
-import itertools  # noqa: F401  (kept for API parity with the reference module namespace)
+import itertools
 from collections import Counter
 from collections.abc import Mapping
 
@@ -55,19 +55,34 @@ class Barcodes:
 
     # ------------------------------------------------------------ device input
     def codes_array(self):
-        """Unique codes as np.uint64 in iteration order (the kernel's input)."""
-        if self._codes is None or self._codes.size != len(self._data):
-            try:
-                self._codes = np.fromiter(self._data.keys(), dtype=np.uint64, count=len(self._data))
-            except (OverflowError, ValueError, TypeError) as e:
-                raise ValueError('summarize_hamming_distances on MI355X needs non-negative integer '
-                                 'codes below 2**64 (%s)' % e) from None
-        return self._codes
+        """The unique keys in iteration order, as the kernels take them: np.uint64 (n,)
+        when every key fits 64 bits, else (n, words) little-endian uint64 limbs.  Built from
+        the mapping on every call (the reference re-reads ``self`` each time, barcode.py:42),
+        so a mapping changed in place is never served stale."""
+        keys = self._data.keys()
+        n = len(self._data)
+        if not all(issubclass(t, (int, np.integer)) for t in set(map(type, keys))):
+            # the reference's pair loop dies at its first ``a ^ b`` on a non-integer key
+            # (encodings.py:117 via barcode.py:42-43): raise exactly that TypeError
+            for a, b in itertools.combinations(self._data, 2):
+                a ^ b
+            return np.zeros(n, dtype=np.uint64)  # < 2 keys: no pair, nothing to compare
+        try:
+            return np.fromiter(keys, dtype=np.uint64, count=n)
+        except OverflowError:
+            ints = [int(k) for k in keys]
+        if any(v < 0 for v in ints):
+            # the reference's `while difference:` never ends on a negative XOR (encodings.py:118)
+            raise ValueError('barcode codes must be non-negative integers')
+        return _lib.ints_to_limbs(ints)
 
     def hamming_histogram(self):
         """np.uint64 histogram H[d] of TwoBit distances over all unordered pairs."""
         codes = self.codes_array()
-        hist = _lib.hamming_hist_allpairs(codes)
+        if codes.ndim == 2:  # keys >= 2^64: the multi-limb pair kernel
+            hist = _lib.hamming_hist_allpairs_wide(codes)
+        else:
+            hist = _lib.hamming_hist_allpairs(codes)
         want = (self._barcode_length + 1) if isinstance(self._barcode_length, int) else 0
         if want > hist.size:  # bins up to the barcode length, as np.bincount(minlength=L+1)
             hist = np.concatenate([hist, np.zeros(want - hist.size, dtype=hist.dtype)])
@@ -84,14 +99,16 @@ class Barcodes:
         """For each TwoBit-encoded query, the index (in iteration order) of the unique
         closest barcode of this set within ``max_distance`` (TwoBit.hamming_distance),
         -2 for a tie, -1 for none; and that distance (255 for none)."""
-        return nearest_whitelist(queries, self.codes_array(), max_distance=max_distance,
-                                 encoding='TwoBit')
+        codes = self.codes_array()
+        if codes.ndim != 1:
+            raise ValueError('nearest needs barcode codes below 2**64')
+        return nearest_whitelist(queries, codes, max_distance=max_distance, encoding='TwoBit')
 
     def base_frequency(self, weighted=False):
         """(barcode_length, 4) uint64 base counts by position, columns A, C, T, G
         (barcode.py:48-70)."""
-        codes = np.fromiter(self._data.keys(), dtype=np.uint64)
-        if weighted:  # the reference raises here too (barcode.py:66-67)
+        codes = np.fromiter(self._data.keys(), dtype=np.uint64)  # OverflowError >= 2^64, as there
+        if weighted and self._barcode_length > 0:  # raised inside the position loop there (:66-67)
             raise NotImplementedError
         return _lib.base_frequency(codes, self._barcode_length)
 

@@ -31,5 +31,11 @@ def golden_10k():
         return json.load(f)
 
 
+@pytest.fixture(scope="session")
+def golden_wide():
+    with open(os.path.join(GOLDEN_DIR, "wide_sets.json")) as f:
+        return json.load(f)
+
+
 def fromhex(d):
     return {k: float.fromhex(v) for k, v in d.items()}

@@ -632,3 +632,54 @@ def test_allpairs_config5_spectral_vs_moments():
         cnt = np.bincount(bases[:, p].astype(np.int64), minlength=4).astype(object)
         agree += int(cnt.dot(cnt - 1)) // 2
     assert sum(d * int(x) for d, x in enumerate(hs)) == 16 * P - agree
+
+
+# ---------------------------------------------------------------- keys >= 2^64 (multi-limb)
+def test_wide_sets_golden(golden_wide):
+    """ThreeBit-encoded 22..28-bp whitelists, TwoBit > 32 bp and mixed-width key sets
+    through the drop-in: the reference's own summaries and histograms."""
+    for rec in golden_wide:
+        s = barcode.Barcodes.from_iterable_encoded([int(c) for c in rec["codes"]], rec["L"])
+        if "error" in rec:
+            with pytest.raises(IndexError):
+                s.summarize_hamming_distances()
+            continue
+        assert s.summarize_hamming_distances() == fromhex(rec["summary"]), (rec["kind"], rec["L"])
+        h = s.hamming_histogram()
+        nz = len(rec["hist"])
+        assert h[:nz].astype(np.int64).tolist() == rec["hist"] and not h[nz:].any()
+
+
+@pytest.mark.parametrize("words,n", [(1, 3000), (2, 20_000), (2, 257), (3, 4097), (4, 3000), (5, 1000), (9, 600)])
+def test_wide_kernel_vs_oracle(words, n):
+    """Every limb count the wide kernel specialises (1-4 private-counter columns, 5+ the
+    shared-histogram path) against the C oracle, with duplicates and near neighbours."""
+    rng = np.random.default_rng(words * 1000 + n)
+    limbs = rng.integers(0, 2 ** 63, size=(n, words), dtype=np.uint64) * np.uint64(2) + \
+        rng.integers(0, 2, size=(n, words), dtype=np.uint64)
+    limbs[n // 2:n // 2 + 10] = limbs[:10]  # duplicates (d = 0)
+    limbs[n // 3, -1] ^= np.uint64(1 << 40)  # a near neighbour of row n/3 + 1
+    limbs[n // 3 + 1] = limbs[n // 3]
+    limbs[n // 3 + 1, -1] ^= np.uint64(3 << 20)
+    hist = _lib.hamming_hist_allpairs_wide(limbs)
+    ref = O.c_hist_wide(limbs)
+    assert hist.astype(np.int64).tolist() == ref.tolist()
+    assert int(hist.sum()) == n * (n - 1) // 2
+
+
+def test_wide_kernel_item_ranges_sum_to_whole():
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(8)
+    n, words = 5000, 2
+    limbs = rng.integers(0, 2 ** 62, size=(n, words), dtype=np.uint64)
+    items, nb = _lib.wide_geometry(n, words)
+    d = torch.from_numpy(limbs.view(np.int64)).cuda()
+    total = torch.zeros(nb, dtype=torch.int64, device="cuda")
+    cuts = [0, 1, items // 5, items // 2 + 3, items - 1, items]
+    pairs = 0
+    for b, e in zip(cuts[:-1], cuts[1:]):
+        _lib.check(_lib.lib().sct_allpairs_wide(d.data_ptr(), n, words, b, e, total.data_ptr(), nb, None))
+        pairs += _lib.wide_range_pairs(n, b, e)
+    torch.cuda.synchronize()
+    assert pairs == n * (n - 1) // 2
+    assert total.cpu().numpy().tolist() == O.c_hist_wide(limbs).tolist()

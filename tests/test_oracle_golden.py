@@ -234,3 +234,18 @@ def test_geometry_picks_spectral_for_large_whitelists():
     assert _lib.allpairs_geometry(737_280, 32)["items"] == 1 << 18
     assert _lib.allpairs_geometry(400_000, 32)["items"] != 1 << 18
     assert _lib.allpairs_geometry(3_700_000, 40)["items"] != 1 << 18  # 20 bases: SUBSETS
+
+
+def test_wide_sets_oracle(golden_wide):
+    """Keys >= 2^64 (ThreeBit 22..28 bp, TwoBit > 32 bp, mixed widths): the multi-limb C
+    oracle and the histogram summary against the reference's own numbers."""
+    for rec in golden_wide:
+        codes = list(dict.fromkeys(int(c) for c in rec["codes"]))  # Counter keys, insertion order
+        words = _lib.words_for_bits(max(c.bit_length() for c in codes))
+        hist = O.c_hist_wide(_lib.ints_to_limbs(codes, words))
+        nz = len(rec["hist"])
+        assert hist[:nz].tolist() == rec["hist"] and not hist[nz:].any()
+        if "summary" in rec:
+            assert O.summary_from_hist_numpy(rec["hist"]) == fromhex(rec["summary"])
+        else:
+            assert len(codes) < 2
