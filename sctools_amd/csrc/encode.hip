@@ -16,6 +16,7 @@
 //   ThreeBit.gc     :182-192 bit 0 of every triplet
 //   ThreeBit.hamming:194-202 non-zero 3-bit groups of a^b
 #include <algorithm>
+#include <string.h>
 
 #include "sct_common.h"
 
@@ -388,8 +389,9 @@ extern "C" int sct_encode(int kind, const uint8_t* seqs, int64_t n, int64_t stri
   if (n == 0) return SCT_OK;
   SCT_CHECK(codes != nullptr && (L == 0 || seqs != nullptr), "NULL pointer");
   const int words = words_for(kind, L);
-  if (stride == L && words == 1 && L > 0 && L <= 64 && (uintptr_t)seqs % 16 == 0) {
-    constexpr int R = 4;  // 4 x 256 records staged per iteration (28 KiB at L = 28)
+  constexpr int R = 4;  // tiled encoder: 4 x 256 records staged per iteration (28 KiB at L = 28)
+  // (fewer records than one tile -- the drop-in's scalar calls -- skip the occupancy query)
+  if (n >= R * WG && stride == L && words == 1 && L > 0 && L <= 64 && (uintptr_t)seqs % 16 == 0) {
     const size_t lds = (size_t)R * WG * L;
     // persistent: exactly the resident workgroups (a 4096 grid at 5 per CU left a partial
     // last round of workgroups, each looping over many tiles)
@@ -480,23 +482,99 @@ extern "C" int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint6
 }
 
 // ---------------------------------------------------------------- host-pointer wrappers
+// Every *_host call runs on the thread's host stage (sct::HostStage): small calls (the
+// drop-in's scalar methods are batches of one) read their inputs from and write their
+// outputs to the page-locked buffer directly (zero-copy: one launch and one stream sync,
+// no allocation), larger ones pack inputs / outputs into one H2D and one D2H copy through
+// the stage's device buffer, and only calls above kStageBytes allocate per call.
 namespace {
-template <typename T>
-int to_dev(sct::DevBuf& d, const T* h, size_t count) {
-  SCT_HIP(d.alloc(count * sizeof(T)));
-  if (count) SCT_HIP(hipMemcpy(d.p, h, count * sizeof(T), hipMemcpyHostToDevice));
-  return SCT_OK;
-}
-template <typename T>
-int from_dev(T* h, const sct::DevBuf& d, size_t count) {
-  if (count) SCT_HIP(hipMemcpy(h, d.p, count * sizeof(T), hipMemcpyDeviceToHost));
-  return SCT_OK;
-}
 #define SCT_TRY(x)              \
   do {                          \
     int rc_ = (x);              \
     if (rc_ != SCT_OK) return rc_; \
   } while (0)
+
+struct In {
+  const void* p;
+  size_t bytes;
+};
+struct Out {
+  void* p;
+  size_t bytes;
+};
+
+// launch(ptrs, stream): ptrs = device-visible inputs then outputs (nullptr for a null host
+// pointer).  zero_copy = false for kernels that update outputs atomically (PCIe atomics on
+// host memory are not assumed).
+template <int NI, int NO, class F>
+int host_call(const In (&ins)[NI], const Out (&outs)[NO], bool zero_copy, F&& launch) {
+  constexpr int N = NI + NO;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t off[N], total = 0;
+  for (int k = 0; k < NI; ++k) {
+    off[k] = total;
+    total += al(ins[k].p ? ins[k].bytes : 0);
+  }
+  const size_t in_total = total;
+  for (int k = 0; k < NO; ++k) {
+    off[NI + k] = total;
+    total += al(outs[k].p ? outs[k].bytes : 0);
+  }
+  sct::HostStage* st = sct::host_stage();
+  if (!st) return SCT_E_HIP;
+  void* ptr[N];
+  if (zero_copy && total <= sct::kZeroCopyBytes) {
+    SCT_TRY(sct::stage_reserve(st, total, 0));
+    for (int k = 0; k < NI; ++k) {
+      if (ins[k].p && ins[k].bytes) memcpy(st->pinned + off[k], ins[k].p, ins[k].bytes);
+      ptr[k] = ins[k].p ? st->pinned_dev + off[k] : nullptr;
+    }
+    for (int k = 0; k < NO; ++k) ptr[NI + k] = outs[k].p ? st->pinned_dev + off[NI + k] : nullptr;
+    SCT_TRY(launch(ptr, st->stream));
+    SCT_HIP(hipStreamSynchronize(st->stream));
+    for (int k = 0; k < NO; ++k)
+      if (outs[k].p && outs[k].bytes) memcpy(outs[k].p, st->pinned + off[NI + k], outs[k].bytes);
+    return SCT_OK;
+  }
+  if (total <= sct::kStageBytes) {
+    SCT_TRY(sct::stage_reserve(st, total, total));
+    for (int k = 0; k < NI; ++k) {
+      if (ins[k].p && ins[k].bytes) memcpy(st->pinned + off[k], ins[k].p, ins[k].bytes);
+      ptr[k] = ins[k].p ? st->dev + off[k] : nullptr;
+    }
+    for (int k = 0; k < NO; ++k) ptr[NI + k] = outs[k].p ? st->dev + off[NI + k] : nullptr;
+    if (in_total) SCT_HIP(hipMemcpyAsync(st->dev, st->pinned, in_total, hipMemcpyHostToDevice, st->stream));
+    SCT_TRY(launch(ptr, st->stream));
+    if (total > in_total)
+      SCT_HIP(hipMemcpyAsync(st->pinned + in_total, st->dev + in_total, total - in_total, hipMemcpyDeviceToHost,
+                             st->stream));
+    SCT_HIP(hipStreamSynchronize(st->stream));
+    for (int k = 0; k < NO; ++k)
+      if (outs[k].p && outs[k].bytes) memcpy(outs[k].p, st->pinned + off[NI + k], outs[k].bytes);
+    return SCT_OK;
+  }
+  sct::DevBuf buf[N];
+  for (int k = 0; k < NI; ++k) {
+    ptr[k] = nullptr;
+    if (!ins[k].p) continue;
+    SCT_HIP(buf[k].alloc(ins[k].bytes));
+    if (ins[k].bytes)
+      SCT_HIP(hipMemcpyAsync(buf[k].p, ins[k].p, ins[k].bytes, hipMemcpyHostToDevice, st->stream));
+    ptr[k] = buf[k].p;
+  }
+  for (int k = 0; k < NO; ++k) {
+    ptr[NI + k] = nullptr;
+    if (!outs[k].p) continue;
+    SCT_HIP(buf[NI + k].alloc(outs[k].bytes));
+    ptr[NI + k] = buf[NI + k].p;
+  }
+  SCT_TRY(launch(ptr, st->stream));
+  for (int k = 0; k < NO; ++k)
+    if (outs[k].p && outs[k].bytes)
+      SCT_HIP(hipMemcpyAsync(outs[k].p, buf[NI + k].p, outs[k].bytes, hipMemcpyDeviceToHost, st->stream));
+  SCT_HIP(hipStreamSynchronize(st->stream));
+  return SCT_OK;
+}
 }  // namespace
 
 extern "C" int sct_encode_host(int kind, const uint8_t* seqs, int64_t n, int64_t stride, int L,
@@ -505,28 +583,20 @@ extern "C" int sct_encode_host(int kind, const uint8_t* seqs, int64_t n, int64_t
   SCT_CHECK(n >= 0 && L >= 0 && stride >= L, "bad n/L/stride");
   if (n == 0) return SCT_OK;
   const int words = words_for(kind, L);
-  sct::DevBuf ds, dc, dg, df;
   const size_t in_bytes = (size_t)((n - 1) * stride + L);
-  SCT_TRY(to_dev(ds, seqs, in_bytes));
-  SCT_HIP(dc.alloc((size_t)n * words * 8));
-  if (gc) SCT_HIP(dg.alloc((size_t)n));
-  if (flags) SCT_HIP(df.alloc((size_t)n));
-  SCT_TRY(sct_encode(kind, (const uint8_t*)ds.p, n, stride, L, (uint64_t*)dc.p,
-                     gc ? (uint8_t*)dg.p : nullptr, flags ? (uint8_t*)df.p : nullptr, nullptr));
-  SCT_TRY(from_dev(codes, dc, (size_t)n * words));
-  if (gc) SCT_TRY(from_dev(gc, dg, (size_t)n));
-  if (flags) SCT_TRY(from_dev(flags, df, (size_t)n));
-  return SCT_OK;
+  return host_call<1, 3>({{seqs, in_bytes}}, {{codes, (size_t)n * words * 8}, {gc, (size_t)n}, {flags, (size_t)n}},
+                         true, [&](void** p, hipStream_t s) {
+                           return sct_encode(kind, (const uint8_t*)p[0], n, stride, L, (uint64_t*)p[1], (uint8_t*)p[2],
+                                             (uint8_t*)p[3], s);
+                         });
 }
 
 extern "C" int sct_base_frequency_host(const uint64_t* codes, int64_t n, int L, uint64_t* out) {
   SCT_CHECK(n >= 0 && L >= 0 && L <= 1024, "bad n/L");
   if (L == 0) return SCT_OK;
-  sct::DevBuf dc, dout;
-  SCT_TRY(to_dev(dc, codes, (size_t)n));
-  SCT_HIP(dout.alloc((size_t)L * 4 * 8));
-  SCT_TRY(sct_base_frequency((const uint64_t*)dc.p, n, L, (uint64_t*)dout.p, nullptr));
-  return from_dev(out, dout, (size_t)L * 4);
+  return host_call<1, 1>({{codes, (size_t)n * 8}}, {{out, (size_t)L * 4 * 8}}, false, [&](void** p, hipStream_t s) {
+    return sct_base_frequency((const uint64_t*)p[0], n, L, (uint64_t*)p[1], s);
+  });
 }
 
 // Host-resident stream (config 5): records live in host memory; chunks flow through
@@ -598,49 +668,41 @@ extern "C" int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, 
 extern "C" int sct_decode2_host(const uint64_t* codes, int64_t n, int words, int L, uint8_t* out) {
   SCT_CHECK(n >= 0 && words >= 1 && L >= 0, "bad n/words/L");
   if (n == 0 || L == 0) return SCT_OK;
-  sct::DevBuf dc, dout;
-  SCT_TRY(to_dev(dc, codes, (size_t)n * words));
-  SCT_HIP(dout.alloc((size_t)n * L));
-  SCT_TRY(sct_decode2((const uint64_t*)dc.p, n, words, L, (uint8_t*)dout.p, nullptr));
-  return from_dev(out, dout, (size_t)n * L);
+  return host_call<1, 1>({{codes, (size_t)n * words * 8}}, {{out, (size_t)n * L}}, true,
+                         [&](void** p, hipStream_t s) {
+                           return sct_decode2((const uint64_t*)p[0], n, words, L, (uint8_t*)p[1], s);
+                         });
 }
 
 extern "C" int sct_decode3_host(const uint64_t* codes, int64_t n, int words, int maxlen,
                                 uint8_t* out, int32_t* lengths, int32_t* bad) {
   SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
   if (n == 0) return SCT_OK;
-  sct::DevBuf dc, dout, dl, db;
-  SCT_TRY(to_dev(dc, codes, (size_t)n * words));
-  SCT_HIP(dout.alloc((size_t)n * maxlen));
-  SCT_HIP(dl.alloc((size_t)n * 4));
-  SCT_HIP(db.alloc((size_t)n * 4));
-  SCT_TRY(sct_decode3((const uint64_t*)dc.p, n, words, maxlen, (uint8_t*)dout.p, (int32_t*)dl.p,
-                      (int32_t*)db.p, nullptr));
-  SCT_TRY(from_dev(out, dout, (size_t)n * maxlen));
-  SCT_TRY(from_dev(lengths, dl, (size_t)n));
-  return from_dev(bad, db, (size_t)n);
+  return host_call<1, 3>({{codes, (size_t)n * words * 8}},
+                         {{out, (size_t)n * maxlen}, {lengths, (size_t)n * 4}, {bad, (size_t)n * 4}}, true,
+                         [&](void** p, hipStream_t s) {
+                           return sct_decode3((const uint64_t*)p[0], n, words, maxlen, (uint8_t*)p[1],
+                                              (int32_t*)p[2], (int32_t*)p[3], s);
+                         });
 }
 
 extern "C" int sct_gc_content_host(int kind, const uint64_t* codes, int64_t n, int words, int L,
                                    int32_t* out) {
   SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
   if (n == 0) return SCT_OK;
-  sct::DevBuf dc, dout;
-  SCT_TRY(to_dev(dc, codes, (size_t)n * words));
-  SCT_HIP(dout.alloc((size_t)n * 4));
-  SCT_TRY(sct_gc_content(kind, (const uint64_t*)dc.p, n, words, L, (int32_t*)dout.p, nullptr));
-  return from_dev(out, dout, (size_t)n);
+  return host_call<1, 1>({{codes, (size_t)n * words * 8}}, {{out, (size_t)n * 4}}, true,
+                         [&](void** p, hipStream_t s) {
+                           return sct_gc_content(kind, (const uint64_t*)p[0], n, words, L, (int32_t*)p[1], s);
+                         });
 }
 
 extern "C" int sct_hamming_pairs_host(int kind, const uint64_t* a, const uint64_t* b, int64_t n,
                                       int words, int32_t* out) {
   SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
   if (n == 0) return SCT_OK;
-  sct::DevBuf da, db, dout;
-  SCT_TRY(to_dev(da, a, (size_t)n * words));
-  SCT_TRY(to_dev(db, b, (size_t)n * words));
-  SCT_HIP(dout.alloc((size_t)n * 4));
-  SCT_TRY(sct_hamming_pairs(kind, (const uint64_t*)da.p, (const uint64_t*)db.p, n, words,
-                            (int32_t*)dout.p, nullptr));
-  return from_dev(out, dout, (size_t)n);
+  return host_call<2, 1>({{a, (size_t)n * words * 8}, {b, (size_t)n * words * 8}}, {{out, (size_t)n * 4}}, true,
+                         [&](void** p, hipStream_t s) {
+                           return sct_hamming_pairs(kind, (const uint64_t*)p[0], (const uint64_t*)p[1], n, words,
+                                                    (int32_t*)p[2], s);
+                         });
 }

@@ -20,6 +20,52 @@ void set_error(const char* fmt, ...) {
 
 const char* last_error() { return g_err; }
 
+HostStage* host_stage() {
+  static thread_local HostStage* stages[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    fail(SCT_E_HIP, "host stage: no current device");
+    return nullptr;
+  }
+  if (!stages[dev]) {
+    auto* st = new HostStage();
+    st->device = dev;
+    if (hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess) {
+      fail(SCT_E_HIP, "host stage: hipStreamCreate failed");
+      delete st;
+      return nullptr;
+    }
+    stages[dev] = st;
+  }
+  return stages[dev];
+}
+
+int stage_reserve(HostStage* st, size_t pinned_bytes, size_t dev_bytes) {
+  auto grow = [](size_t have, size_t need) {
+    size_t c = have ? have : (size_t)1 << 16;
+    while (c < need) c *= 2;
+    return c;
+  };
+  if (pinned_bytes > st->pinned_cap) {
+    if (st->pinned) (void)hipHostFree(st->pinned);
+    st->pinned = nullptr;
+    st->pinned_cap = 0;
+    const size_t c = grow(0, pinned_bytes);
+    SCT_HIP(hipHostMalloc((void**)&st->pinned, c, hipHostMallocCoherent | hipHostMallocMapped));
+    SCT_HIP(hipHostGetDevicePointer((void**)&st->pinned_dev, st->pinned, 0));
+    st->pinned_cap = c;
+  }
+  if (dev_bytes > st->dev_cap) {
+    if (st->dev) (void)hipFree(st->dev);
+    st->dev = nullptr;
+    st->dev_cap = 0;
+    const size_t c = grow(0, dev_bytes);
+    SCT_HIP(hipMalloc((void**)&st->dev, c));
+    st->dev_cap = c;
+  }
+  return SCT_OK;
+}
+
 }  // namespace sct
 
 extern "C" int sct_version(void) { return 1; }

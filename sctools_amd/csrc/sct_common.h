@@ -37,6 +37,28 @@ struct DevBuf {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Per-thread, per-device staging of the *_host entry points (host.cpp): one non-blocking
+// stream, one page-locked host-coherent buffer and one device buffer, created on first use
+// and grown on demand (never freed: process exit reclaims them), so a drop-in scalar call
+// costs a launch and a stream sync instead of hipMalloc / hipFree per argument.
+struct HostStage {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  uint8_t* pinned = nullptr;  // hipHostMallocCoherent: kernels may read / write it directly
+  uint8_t* pinned_dev = nullptr;  // the same buffer as the device sees it
+  size_t pinned_cap = 0;
+  uint8_t* dev = nullptr;
+  size_t dev_cap = 0;
+};
+// nullptr (with the error set) if the stage cannot be created.
+HostStage* host_stage();
+int stage_reserve(HostStage* st, size_t pinned_bytes, size_t dev_bytes);
+// Calls of at most this many bytes (inputs + outputs) run zero-copy on the pinned buffer.
+constexpr size_t kZeroCopyBytes = 64 << 10;
+// Larger calls up to this size go through the pinned + device buffers (two copies); beyond
+// it the caller's arrays are copied through per-call device allocations.
+constexpr size_t kStageBytes = 256ull << 20;
+
 // Moment-assisted all-pairs scheme (SCT_ALLPAIRS_MOMENTS, 16-base TwoBit codes):
 // the count kernel accumulates only these 13 subset products of the distance bits
 // d0..d3 (d mod 16), and the agreement moments M_k = sum over pairs of C(16 - d, k),
