@@ -178,6 +178,56 @@ def limbs_to_ints(limbs):
     return [int.from_bytes(row.astype("<u8").tobytes(), "little") for row in limbs]
 
 
+# ------------------------------------------------------------------ scalar calls
+# The drop-in's scalar methods (TwoBit.encode(bytes) -> int, ...) are batches of one; these
+# helpers pass one-limb values through per-thread ctypes buffers (no numpy arrays per call)
+# into the library's zero-copy host stage.
+_tls = threading.local()
+
+
+def _scalar_bufs():
+    b = getattr(_tls, "bufs", None)
+    if b is None:
+        b = _tls.bufs = {"a": (ctypes.c_uint64 * 1)(), "b": (ctypes.c_uint64 * 1)(), "i": (ctypes.c_int32 * 1)(),
+                         "gc": (ctypes.c_uint8 * 1)(), "fl": (ctypes.c_uint8 * 1)(), "out": ctypes.create_string_buffer(64)}
+    return b
+
+
+def hamming1(kind, a, b):
+    """One pair of one-limb codes (< 2^64) -> distance."""
+    bufs = _scalar_bufs()
+    bufs["a"][0] = a
+    bufs["b"][0] = b
+    check(lib().sct_hamming_pairs_host(kind, ctypes.addressof(bufs["a"]), ctypes.addressof(bufs["b"]), 1, 1,
+                                       ctypes.addressof(bufs["i"])))
+    return bufs["i"][0]
+
+
+def gc1(kind, code, L=0):
+    bufs = _scalar_bufs()
+    bufs["a"][0] = code
+    check(lib().sct_gc_content_host(kind, ctypes.addressof(bufs["a"]), 1, 1, L, ctypes.addressof(bufs["i"])))
+    return bufs["i"][0]
+
+
+def encode1(kind, seq):
+    """One record of L <= 64 / kind bytes -> (code, flags): a one-limb code."""
+    bufs = _scalar_bufs()
+    L = len(seq)
+    check(lib().sct_encode_host(kind, seq, 1, L, L, ctypes.addressof(bufs["a"]), None,
+                                ctypes.addressof(bufs["fl"])))
+    return bufs["a"][0], bufs["fl"][0]
+
+
+def decode2_1(code, L):
+    """One one-limb TwoBit code -> L bytes (L <= 64)."""
+    bufs = _scalar_bufs()
+    bufs["a"][0] = code
+    out = bufs["out"]
+    check(lib().sct_decode2_host(ctypes.addressof(bufs["a"]), 1, 1, L, ctypes.addressof(out)))
+    return out.raw[:L]
+
+
 # ------------------------------------------------------------------ entry points
 def encode(kind, seqs, L):
     """(n, L) uint8 array -> (codes (n, words) uint64, gc uint8|None, flags uint8)."""

@@ -531,7 +531,11 @@ int host_call(const In (&ins)[NI], const Out (&outs)[NO], bool zero_copy, F&& la
     }
     for (int k = 0; k < NO; ++k) ptr[NI + k] = outs[k].p ? st->pinned_dev + off[NI + k] : nullptr;
     SCT_TRY(launch(ptr, st->stream));
-    SCT_HIP(hipStreamSynchronize(st->stream));
+    // a few-microsecond kernel: poll instead of a blocking sync (saves the wake-up)
+    hipError_t q;
+    while ((q = hipStreamQuery(st->stream)) == hipErrorNotReady) {
+    }
+    SCT_HIP(q);
     for (int k = 0; k < NO; ++k)
       if (outs[k].p && outs[k].bytes) memcpy(outs[k].p, st->pinned + off[NI + k], outs[k].bytes);
     return SCT_OK;

@@ -12,10 +12,11 @@
 // Algorithm (exact pigeonhole index): split the G base positions into P = max_d + 1
 // contiguous blocks; any w with dist(q, w) <= max_d agrees with q exactly on at least
 // one block.  For each block the whitelist is bucketed by a multiplicative hash of that
-// block's bits into ~nw/2 buckets (CSR: offsets[b] .. offsets[b+1] into 16-byte
-// {code, index} entries, built by a histogram / exclusive-scan / scatter on the GPU).
-// A query issues all P bucket-offset loads before it reads any entry (one dependent
-// random access per probe, the offset tables are a few MB and L2/MALL-resident), then
+// block's bits into ~4x as many buckets as the block has distinct values (CSR: u32
+// offsets[b] .. offsets[b+1] into 8-byte code entries + a 4-byte index array read only for
+// candidates; built by a histogram / exclusive-scan / scatter on the GPU).  A query issues
+// all P bucket-offset loads before it reads any entry (one dependent random access per
+// probe; the offset tables are sized to stay in each XCD's L2), then
 // verifies every entry of its P buckets with the full distance, so hash collisions never
 // change the result.  A code found through several blocks has one index, so it is never
 // counted as a tie with itself.
@@ -65,43 +66,48 @@ __global__ void key_hist_kernel(const uint64_t* __restrict__ wl, int64_t nw, Par
 }
 
 // entries: codes[pos] (8 B, what a probe scans) and index[pos] (read only for a new best);
-// index bit 31 = the code occurs more than once in the whitelist (mark_dups_kernel)
+// index bit 31 = the code occurs more than once in the whitelist (flag_dups_kernel)
 __global__ void key_scatter_kernel(const uint64_t* __restrict__ wl, int64_t nw, Part part,
-                                   uint32_t* __restrict__ cursor, uint64_t* __restrict__ codes,
-                                   uint32_t* __restrict__ index) {
+                                   uint32_t* __restrict__ cursor, const uint8_t* __restrict__ dup,
+                                   uint64_t* __restrict__ codes, uint32_t* __restrict__ index) {
   for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j < nw; j += (int64_t)gridDim.x * WG) {
     const uint64_t w = wl[j];
     const uint32_t pos = atomicAdd(&cursor[part_bucket(w, part)], 1u);
     codes[pos] = w;
-    index[pos] = (uint32_t)j;
+    index[pos] = (uint32_t)j | (dup[j] ? 0x80000000u : 0u);
   }
 }
 
-// bucket b's entries are [range[b].x, range[b].y): one 8-byte load per probe
-__global__ void ranges_kernel(const uint32_t* __restrict__ offsets, int64_t nbuckets,
-                              uint2* __restrict__ range) {
-  const int64_t b = (int64_t)blockIdx.x * WG + threadIdx.x;
-  if (b < nbuckets) range[b] = make_uint2(offsets[b], offsets[b + 1]);
+// occupied buckets of a provisional table (~ the distinct block values)
+__global__ void count_nonzero_kernel(const uint32_t* __restrict__ counts, int64_t nbuckets,
+                                     unsigned long long* __restrict__ out) {
+  uint32_t c = 0;
+  for (int64_t b = (int64_t)blockIdx.x * WG + threadIdx.x; b < nbuckets; b += (int64_t)gridDim.x * WG)
+    c += counts[b] != 0;
+  for (int o = 32; o; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, (unsigned long long)c);
 }
 
-// one thread per bucket of part 0 (identical codes share every bucket): flag duplicates
-__global__ void mark_dups_kernel(const uint2* __restrict__ range, int64_t nbuckets,
-                                 const uint64_t* __restrict__ codes, uint32_t* __restrict__ index) {
-  const int64_t b = (int64_t)blockIdx.x * WG + threadIdx.x;
-  if (b >= nbuckets) return;
-  const uint2 r = range[b];
-  for (uint32_t t = r.x; t < r.y; ++t)
-    for (uint32_t u = r.x; u < r.y; ++u)
-      if (u != t && codes[u] == codes[t]) {
-        index[t] |= 0x80000000u;
-        break;
-      }
+// Duplicate whitelist codes (the same code at two indices always ties): the codes sorted
+// with their indices, equal neighbours flag both indices.  No per-bucket pair scan, so a
+// block value shared by many codes costs nothing extra.
+__global__ void flag_dups_kernel(const uint64_t* __restrict__ sorted, const uint32_t* __restrict__ idx, int64_t nw,
+                                 uint8_t* __restrict__ dup) {
+  for (int64_t k = (int64_t)blockIdx.x * WG + threadIdx.x; k < nw; k += (int64_t)gridDim.x * WG) {
+    const uint64_t c = sorted[k];
+    const bool d = (k > 0 && sorted[k - 1] == c) || (k + 1 < nw && sorted[k + 1] == c);
+    dup[idx[k]] = d ? 1 : 0;
+  }
+}
+
+__global__ void iota_kernel(uint32_t* __restrict__ v, int64_t n) {
+  for (int64_t k = (int64_t)blockIdx.x * WG + threadIdx.x; k < n; k += (int64_t)gridDim.x * WG) v[k] = (uint32_t)k;
 }
 
 // Per-probe tables, passed by value (kernarg -> SGPRs) so every load is a global load.
 struct Tables {
   Part part[MAX_PARTS];
-  const uint2* range[MAX_PARTS];
+  const uint32_t* off[MAX_PARTS];  // bucket b's entries are [off[b], off[b + 1])
   const uint64_t* code[MAX_PARTS];
   const uint32_t* index[MAX_PARTS];
 };
@@ -116,7 +122,10 @@ __global__ __launch_bounds__(WG) void nearest_query_kernel(const uint64_t* __res
   const uint64_t q = queries[i];
   uint2 r[NP];
 #pragma unroll
-  for (int p = 0; p < NP; ++p) r[p] = tb.range[p][part_bucket(q, tb.part[p])];  // all in flight
+  for (int p = 0; p < NP; ++p) {  // all in flight
+    const uint32_t* o = tb.off[p] + part_bucket(q, tb.part[p]);
+    r[p] = make_uint2(o[0], o[1]);
+  }
   int best_d = max_d + 1, best_j = -1;
   bool tie = false, exact_unique = false;
 #pragma unroll
@@ -171,7 +180,8 @@ struct sct_nearest_plan {
   int kind = 2, max_d = 0, nparts = 0, code_bits = 0;
   int64_t nw = 0;
   Parts parts{};
-  uint2* d_range[MAX_PARTS] = {};
+  int64_t nbuckets[MAX_PARTS] = {};
+  uint32_t* d_off[MAX_PARTS] = {};
   uint64_t* d_code[MAX_PARTS] = {};
   uint32_t* d_index[MAX_PARTS] = {};
 };
@@ -179,7 +189,7 @@ struct sct_nearest_plan {
 extern "C" int sct_nearest_plan_destroy(sct_nearest_plan* p) {
   if (!p) return SCT_OK;
   for (int k = 0; k < MAX_PARTS; ++k) {
-    if (p->d_range[k]) (void)hipFree(p->d_range[k]);
+    if (p->d_off[k]) (void)hipFree(p->d_off[k]);
     if (p->d_code[k]) (void)hipFree(p->d_code[k]);
     if (p->d_index[k]) (void)hipFree(p->d_index[k]);
   }
@@ -210,54 +220,94 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
   p->nw = nw;
   p->code_bits = code_bits;
   p->nparts = max_d + 1;
-  // ~PER entries per bucket (8-byte codes: 8 per 64-byte line); fewer, fuller buckets keep
-  // the range table L2-resident (SCT_NEAREST_PER overrides, for A/B)
-  int per = 2;
-  if (const char* v = getenv("SCT_NEAREST_PER")) per = std::max(1, atoi(v));
-  int lg = 0;
-  while (lg < 28 && (1LL << lg) * per < nw) ++lg;
-  const int64_t nbuckets = 1LL << lg;
+  // Bucket count per part: a provisional table of ~nw/2 buckets counts the occupied ones
+  // (~ the distinct block values: 4^8 = 65,536 for an 8-base ThreeBit block of a 737K
+  // whitelist, nw itself for max_d = 0), then the part gets ~SCT_NEAREST_LOAD (4) buckets per
+  // distinct value, never more than the provisional count: the offset tables stay small
+  // enough to live in each XCD's L2 while colliding block values add few extra entries.
+  int lg0 = 0;
+  while (lg0 < 28 && (1LL << lg0) * 2 < nw) ++lg0;
+  int load = 4;
+  if (const char* v = getenv("SCT_NEAREST_LOAD")) load = std::max(1, atoi(v));
   for (int k = 0; k < p->nparts; ++k) {
     const int pos_lo = G * k / p->nparts, pos_hi = G * (k + 1) / p->nparts;
     Part& pt = p->parts.p[k];
     pt.lo_bit = pos_lo * kind;
     pt.nbits = std::min(64, pos_hi * kind) - pt.lo_bit;
     pt.mask = (pt.nbits >= 64 ? ~0ull : ((1ull << pt.nbits) - 1ull)) << pt.lo_bit;
-    pt.mul = lg == 0 ? 0ull : 0x9E3779B97F4A7C15ull;
-    pt.shift = lg == 0 ? 63 : 64 - lg;
+    pt.mul = lg0 == 0 ? 0ull : 0x9E3779B97F4A7C15ull;
+    pt.shift = lg0 == 0 ? 63 : 64 - lg0;
   }
-  size_t scan_bytes = 0;
+  const int64_t nb0 = 1LL << lg0;
+  size_t scan_bytes = 0, sort_bytes = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                         (int)(nbuckets + 1), s);
-  sct::DevBuf scan_tmp, cursor, offsets;
-  hipError_t e = scan_tmp.alloc(scan_bytes);
-  if (e == hipSuccess) e = cursor.alloc((size_t)(nbuckets + 1) * 4);
-  if (e == hipSuccess) e = offsets.alloc((size_t)(nbuckets + 1) * 4);
+                                         (int)(nb0 + 1), s);
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)std::max<int64_t>(nw, 1),
+                                           0, 64, s);
+  sct::DevBuf scan_tmp, cursor, occ, skeys, sidx, iota, dup;
+  hipError_t e = scan_tmp.alloc(std::max(scan_bytes, sort_bytes));
+  if (e == hipSuccess) e = cursor.alloc((size_t)(nb0 + 1) * 4);
+  if (e == hipSuccess) e = occ.alloc(8 * MAX_PARTS);
+  if (e == hipSuccess) e = skeys.alloc((size_t)std::max<int64_t>(nw, 1) * 8);
+  if (e == hipSuccess) e = sidx.alloc((size_t)std::max<int64_t>(nw, 1) * 4);
+  if (e == hipSuccess) e = iota.alloc((size_t)std::max<int64_t>(nw, 1) * 4);
+  if (e == hipSuccess) e = dup.alloc((size_t)std::max<int64_t>(nw, 1));
   if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "scratch: %s", hipGetErrorString(e)));
+  uint32_t* counts = (uint32_t*)cursor.p;
+  auto* d_occ = (unsigned long long*)occ.p;
+  SCT_HIP(hipMemsetAsync(d_occ, 0, 8 * MAX_PARTS, s));
+  SCT_HIP(hipMemsetAsync(dup.p, 0, (size_t)std::max<int64_t>(nw, 1), s));
+  if (nw > 1) {
+    // duplicate codes: sort (code, index), flag equal neighbours
+    hipLaunchKernelGGL(iota_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, (uint32_t*)iota.p, nw);
+    size_t tb = sort_bytes;
+    e = hipcub::DeviceRadixSort::SortPairs(scan_tmp.p, tb, d_whitelist, (uint64_t*)skeys.p, (const uint32_t*)iota.p,
+                                           (uint32_t*)sidx.p, (int)nw, 0, 64, s);
+    if (e != hipSuccess) return fail_with(sct::fail(SCT_E_HIP, "sort: %s", hipGetErrorString(e)));
+    hipLaunchKernelGGL(flag_dups_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, (const uint64_t*)skeys.p,
+                       (const uint32_t*)sidx.p, nw, (uint8_t*)dup.p);
+  }
+  if (nw && lg0 > 0) {  // occupied provisional buckets per part
+    for (int k = 0; k < p->nparts; ++k) {
+      SCT_HIP(hipMemsetAsync(counts, 0, (size_t)(nb0 + 1) * 4, s));
+      hipLaunchKernelGGL(key_hist_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_whitelist, nw,
+                         p->parts.p[k], counts);
+      hipLaunchKernelGGL(count_nonzero_kernel, dim3(grid_for(nb0, 1024)), dim3(WG), 0, s, counts, nb0, d_occ + k);
+    }
+    SCT_LAUNCH_CHECK();
+    unsigned long long h_occ[MAX_PARTS] = {};
+    SCT_HIP(hipMemcpyAsync(h_occ, d_occ, 8 * MAX_PARTS, hipMemcpyDeviceToHost, s));
+    SCT_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < p->nparts; ++k) {
+      int lg = 0;
+      while (lg < lg0 && (1ULL << lg) < (unsigned long long)load * std::max(1ULL, h_occ[k])) ++lg;
+      Part& pt = p->parts.p[k];
+      pt.mul = lg == 0 ? 0ull : 0x9E3779B97F4A7C15ull;
+      pt.shift = lg == 0 ? 63 : 64 - lg;
+      p->nbuckets[k] = 1LL << lg;
+    }
+  } else {
+    for (int k = 0; k < p->nparts; ++k) p->nbuckets[k] = nb0;
+  }
   for (int k = 0; k < p->nparts; ++k) {
     const Part pt = p->parts.p[k];
-    e = hipMalloc(&p->d_range[k], (size_t)nbuckets * 8);
+    const int64_t nbuckets = p->nbuckets[k];
+    e = hipMalloc(&p->d_off[k], (size_t)(nbuckets + 1) * 4);
     if (e == hipSuccess) e = hipMalloc(&p->d_code[k], (size_t)std::max<int64_t>(nw, 1) * 8);
     if (e == hipSuccess) e = hipMalloc(&p->d_index[k], (size_t)std::max<int64_t>(nw, 1) * 4);
     if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "bucket arrays: %s", hipGetErrorString(e)));
-    uint32_t* counts = (uint32_t*)cursor.p;
-    uint32_t* off = (uint32_t*)offsets.p;
     SCT_HIP(hipMemsetAsync(counts, 0, (size_t)(nbuckets + 1) * 4, s));
     if (nw)
       hipLaunchKernelGGL(key_hist_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_whitelist, nw,
                          pt, counts);
     size_t b = scan_bytes;
-    e = hipcub::DeviceScan::ExclusiveSum(scan_tmp.p, b, counts, off, (int)(nbuckets + 1), s);
+    e = hipcub::DeviceScan::ExclusiveSum(scan_tmp.p, b, counts, p->d_off[k], (int)(nbuckets + 1), s);
     if (e != hipSuccess) return fail_with(sct::fail(SCT_E_HIP, "scan: %s", hipGetErrorString(e)));
-    hipLaunchKernelGGL(ranges_kernel, dim3((unsigned)sct::ceil_div(nbuckets, WG)), dim3(WG), 0, s, off,
-                       nbuckets, p->d_range[k]);
-    SCT_HIP(hipMemcpyAsync(counts, off, (size_t)nbuckets * 4, hipMemcpyDeviceToDevice, s));
+    SCT_HIP(hipMemcpyAsync(counts, p->d_off[k], (size_t)nbuckets * 4, hipMemcpyDeviceToDevice, s));
     if (nw)
       hipLaunchKernelGGL(key_scatter_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_whitelist,
-                         nw, pt, counts, p->d_code[k], p->d_index[k]);
-    if (k == 0 && nw)
-      hipLaunchKernelGGL(mark_dups_kernel, dim3((unsigned)sct::ceil_div(nbuckets, WG)), dim3(WG), 0, s,
-                         p->d_range[0], nbuckets, p->d_code[0], p->d_index[0]);
+                         nw, pt, counts, (const uint8_t*)dup.p, p->d_code[k], p->d_index[k]);
     SCT_LAUNCH_CHECK();
   }
   SCT_HIP(hipStreamSynchronize(s));  // the scratch buffers die with this call
@@ -277,7 +327,7 @@ extern "C" int sct_nearest_query(sct_nearest_plan* p, const uint64_t* d_queries,
   Tables tb{};
   for (int k = 0; k < p->nparts; ++k) {
     tb.part[k] = p->parts.p[k];
-    tb.range[k] = p->d_range[k];
+    tb.off[k] = p->d_off[k];
     tb.code[k] = p->d_code[k];
     tb.index[k] = p->d_index[k];
   }

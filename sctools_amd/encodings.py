@@ -54,6 +54,7 @@ def _records(seqs):
 
 
 _STREAM_MIN_RECORDS = 1 << 20
+_U64 = 1 << 64
 
 
 def _encode_records(kind, recs):
@@ -193,6 +194,10 @@ class TwoBit(Encoding):
             # the reference indexes its byte map with a str and then calls chr() on it
             raise TypeError("'str' object cannot be interpreted as an integer")
         seq = _as_bytes(bytes_encoded)
+        if 0 < len(seq) <= 32:  # one limb: the lean scalar call
+            code, flags = _lib.encode1(2, seq)
+            if not flags:
+                return code
         recs = np.frombuffer(seq, dtype=np.uint8).reshape(1, len(seq))
         codes, gc, flags = _lib.encode(2, recs, len(seq))
         _fill_ambiguous(recs, codes, gc, flags)
@@ -200,11 +205,17 @@ class TwoBit(Encoding):
 
     def decode(self, integer_encoded):
         """encodings.py:90-100 (batch of one)."""
+        x = int(integer_encoded)
+        if 0 <= x < _U64 and 0 < self.sequence_length <= 64:
+            return _lib.decode2_1(x, self.sequence_length)
         limbs = _limbs_of([integer_encoded])
         return _lib.decode2(limbs, self.sequence_length)[0].tobytes()
 
     def gc_content(self, integer_encoded):
         """encodings.py:102-111 (batch of one)."""
+        x = int(integer_encoded)
+        if 0 <= x < _U64:
+            return _lib.gc1(2, x, self.sequence_length)
         return int(_lib.gc_content(2, _limbs_of([integer_encoded]), self.sequence_length)[0])
 
     @staticmethod
@@ -274,6 +285,8 @@ class ThreeBit(Encoding):
             seq = b"N" * len(bytes_encoded)
         else:
             seq = _as_bytes(bytes_encoded)
+        if 0 < len(seq) <= 21:  # one limb: the lean scalar call
+            return _lib.encode1(3, seq)[0]
         recs = np.frombuffer(seq, dtype=np.uint8).reshape(1, len(seq))
         codes, _, _ = _lib.encode(3, recs, len(seq))
         return _lib.limbs_to_ints(codes)[0]
@@ -286,6 +299,9 @@ class ThreeBit(Encoding):
     @classmethod
     def gc_content(cls, integer_encoded):
         """encodings.py:182-192 (batch of one)."""
+        x = int(integer_encoded)
+        if 0 <= x < _U64:
+            return _lib.gc1(3, x)
         return int(_lib.gc_content(3, _limbs_of([integer_encoded]))[0])
 
     @staticmethod
@@ -304,6 +320,8 @@ def _pad(limbs, words):
 
 def _hamming1(kind, a, b):
     a, b = int(a), int(b)
+    if 0 <= a < _U64 and 0 <= b < _U64:
+        return _lib.hamming1(kind, a, b)
     if a < 0 or b < 0:
         raise ValueError("encoded values must be non-negative")
     words = _lib.words_for_bits(max(a.bit_length(), b.bit_length()))

@@ -45,3 +45,45 @@ def decode_ascii(codes, barcode_length):
     shifts = np.arange(barcode_length - 1, -1, -1, dtype=np.uint64) * np.uint64(2)
     idx = (codes[:, None] >> shifts[None, :]) & np.uint64(3)
     return lut[idx.astype(np.intp)]
+
+
+def two_to_three(codes2, barcode_length=16):
+    """TwoBit codes -> ThreeBit codes of the same sequence (A0 C1 T2 G3 -> A2 C1 T4 G3;
+    encodings.py:58-59 vs :142-143)."""
+    m = np.array([2, 1, 4, 3], dtype=np.uint64)
+    codes2 = np.asarray(codes2, dtype=np.uint64)
+    out = np.zeros(codes2.size, dtype=np.uint64)
+    for p in range(barcode_length):
+        v = (codes2 >> np.uint64(2 * p)) & np.uint64(3)
+        out |= m[v.astype(np.intp)] << np.uint64(3 * p)
+    return out
+
+
+def config4_queries(wl3, nq, seed=4, barcode_length=16, device=None):
+    """Config 4's observed barcodes as ThreeBit codes, built on `device` (a torch device):
+    50 % exact whitelist draws, 25 % one substitution (A/C/G/T), 15 % one N, 10 % uniformly
+    random ACGT.  Returns (queries int64 tensor, picked whitelist index, class tensor: 0
+    exact, 1 substitution, 2 N, 3 random)."""
+    import torch
+    L = barcode_length
+    dev = device or torch.device("cuda")
+    d_wl = torch.as_tensor(np.ascontiguousarray(wl3, dtype=np.uint64).view(np.int64), device=dev)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    n = d_wl.numel()
+    pick = torch.randint(0, n, (nq,), device=dev, generator=g)
+    q = d_wl[pick].clone()
+    u = torch.rand(nq, device=dev, generator=g)
+    pos = torch.randint(0, L, (nq,), device=dev, generator=g) * 3
+    base = torch.randint(1, 5, (nq,), device=dev, generator=g)
+    clear = ~(torch.full_like(q, 7) << pos)
+    sub = (u >= 0.5) & (u < 0.75)
+    q = torch.where(sub, (q & clear) | (base << pos), q)
+    nmask = (u >= 0.75) & (u < 0.9)
+    q = torch.where(nmask, (q & clear) | (torch.full_like(q, 6) << pos), q)
+    rnd = u >= 0.9
+    r = torch.zeros_like(q)
+    for p in range(L):
+        r |= torch.randint(1, 5, (nq,), device=dev, generator=g) << (3 * p)
+    q = torch.where(rnd, r, q)
+    cls = sub.to(torch.int8) + 2 * nmask.to(torch.int8) + 3 * rnd.to(torch.int8)
+    return q, pick, cls

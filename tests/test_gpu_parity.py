@@ -683,3 +683,50 @@ def test_wide_kernel_item_ranges_sum_to_whole():
     torch.cuda.synchronize()
     assert pairs == n * (n - 1) // 2
     assert total.cpu().numpy().tolist() == O.c_hist_wide(limbs).tolist()
+
+
+# ---------------------------------------------------------------- config 4 at full size
+def test_nearest_config4_full_size():
+    """Config 4 as specified: the 737,280-code ThreeBit whitelist and 100M observed
+    barcodes (50 % exact, 25 % substitution, 15 % N, 10 % random) at max_d = 1.  Every
+    exact draw must come back as its own index at distance 0, every one-edit query within
+    distance 1; 20,000 sampled queries of every class bit-exact against the OpenMP brute
+    force over the whole whitelist."""
+    torch = pytest.importorskip("torch")
+    n, L, seed = synthetic.CONFIGS[2]
+    wl = synthetic.two_to_three(synthetic.whitelist_codes(n, L, seed), L)
+    nq = 100_000_000
+    q, pick, cls = synthetic.config4_queries(wl, nq, seed=4)
+    d_wl = torch.from_numpy(wl.view(np.int64)).cuda()
+    idx = torch.empty(nq, dtype=torch.int32, device="cuda")
+    dist = torch.empty(nq, dtype=torch.uint8, device="cuda")
+    plan = _lib.NearestPlan(3, d_wl.data_ptr(), n, 3 * L, 1)
+    plan.query(q.data_ptr(), nq, idx.data_ptr(), dist.data_ptr())
+    torch.cuda.synchronize()
+    plan.close()
+    exact = cls == 0
+    assert torch.equal(idx[exact].long(), pick[exact]) and bool((dist[exact] == 0).all())
+    one = (cls == 1) | (cls == 2)
+    assert bool((dist[one] <= 1).all()) and bool((idx[one] != -1).all())
+    g = torch.Generator(device="cuda").manual_seed(44)
+    samp = torch.randint(0, nq, (20_000,), device="cuda", generator=g)
+    ridx, rdist = O.c_nearest(3, wl, q[samp].cpu().numpy().view(np.uint64), 1)
+    assert np.array_equal(idx[samp].cpu().numpy(), ridx)
+    assert np.array_equal(dist[samp].cpu().numpy(), rdist)
+    # the drop-in entry point on the sampled queries
+    i2, d2 = barcode.nearest_whitelist(q[samp].cpu().numpy().view(np.uint64), wl, 1)
+    assert np.array_equal(i2, ridx) and np.array_equal(d2, rdist)
+
+
+@pytest.mark.parametrize("kind,max_d", [(2, 7), (3, 7), (2, 5)])
+def test_nearest_max_d_near_limit(kind, max_d):
+    """max_d + 1 = 8 / 6 blocks of 2-3 bases: block values shared by thousands of codes
+    (buckets of ~nw / 16 entries) -- the duplicate flagging sorts instead of scanning pairs."""
+    rng = np.random.default_rng(70 + kind + max_d)
+    wl2 = synthetic.whitelist_codes(20_000, 16, seed=kind + max_d)
+    wl = wl2 if kind == 2 else synthetic.two_to_three(wl2)
+    wl = np.concatenate([wl, wl[:25]])  # duplicates -> ties
+    q = np.concatenate([wl[:500], rng.permutation(wl)[:500] ^ np.uint64(1 << 5)])
+    idx, dist = barcode.nearest_whitelist(q, wl, max_distance=max_d, encoding=kind)
+    ridx, rdist = O.c_nearest(kind, wl, q, max_d)
+    assert np.array_equal(idx, ridx) and np.array_equal(dist, rdist)

@@ -119,38 +119,14 @@ def bench_encode_stream(n_reads, L=28):
             "note": "H2D L bytes + D2H 10 bytes per read over PCIe Gen5 x16 (63 GB/s spec per direction)"}
 
 
-def two_to_three(codes2, L=16):
-    """TwoBit codes -> ThreeBit codes of the same sequence (A0 C1 T2 G3 -> A2 C1 T4 G3)."""
-    m = np.array([2, 1, 4, 3], dtype=np.uint64)
-    out = np.zeros(codes2.size, dtype=np.uint64)
-    for p in range(L):
-        v = (codes2 >> np.uint64(2 * p)) & np.uint64(3)
-        out |= m[v.astype(np.intp)] << np.uint64(3 * p)
-    return out
-
-
 def bench_nearest(nq, max_d=1):
     dev = torch.device("cuda")
     s = torch.cuda.current_stream()
     n, L, seed = synthetic.CONFIGS[2]
-    wl = two_to_three(synthetic.whitelist_codes(n, L, seed), L)
+    wl = synthetic.two_to_three(synthetic.whitelist_codes(n, L, seed), L)
     d_wl = torch.from_numpy(wl.view(np.int64)).to(dev)
+    q, _, _ = synthetic.config4_queries(wl, nq, seed=4, device=dev)
     g = torch.Generator(device=dev).manual_seed(4)
-    pick = torch.randint(0, n, (nq,), device=dev, generator=g)
-    q = d_wl[pick].clone()
-    kind = torch.rand(nq, device=dev, generator=g)
-    pos = torch.randint(0, L, (nq,), device=dev, generator=g) * 3
-    base = torch.randint(1, 5, (nq,), device=dev, generator=g)
-    clear = ~(torch.full_like(q, 7) << pos)
-    sub = (kind >= 0.5) & (kind < 0.75)
-    q = torch.where(sub, (q & clear) | (base << pos), q)
-    nmask = (kind >= 0.75) & (kind < 0.9)
-    q = torch.where(nmask, (q & clear) | (torch.full_like(q, 6) << pos), q)
-    rnd = kind >= 0.9
-    r = torch.zeros_like(q)
-    for p in range(L):
-        r |= torch.randint(1, 5, (nq,), device=dev, generator=g) << (3 * p)
-    q = torch.where(rnd, r, q)
     idx = torch.empty(nq, dtype=torch.int32, device=dev)
     dist = torch.empty(nq, dtype=torch.uint8, device=dev)
     t0 = time.perf_counter()
@@ -170,7 +146,7 @@ def bench_nearest(nq, max_d=1):
     # parity spot check against the oracle brute force on a sample
     from oracle import oracle as O
     samp = torch.randint(0, nq, (2000,), device=dev, generator=g)
-    ridx, rdist = O.nearest_bruteforce(3, wl, q[samp].cpu().numpy().view(np.uint64), max_d)
+    ridx, rdist = O.c_nearest(3, wl, q[samp].cpu().numpy().view(np.uint64), max_d)
     assert np.array_equal(idx[samp].cpu().numpy(), ridx) and np.array_equal(dist[samp].cpu().numpy(), rdist)
     hist = torch.bincount(idx.clamp(min=-2).add(2).clamp(max=2).long(), minlength=3).tolist()
     plan.close()
