@@ -22,7 +22,9 @@
 // counted as a tie with itself.
 #include <hipcub/hipcub.hpp>
 
+#include <math.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 
@@ -154,6 +156,128 @@ __global__ __launch_bounds__(WG) void nearest_query_kernel(const uint64_t* __res
   out_dist[i] = best_j < 0 ? (uint8_t)255 : (uint8_t)best_d;
 }
 
+// ---------------------------------------------------------------- open-addressing multi-index
+// When the whitelist's keys are (nearly) unique -- max_d = 0 (key = the whole code), or
+// max_d = 1..2 with P = max_d + 2 blocks and keys = PAIRS of blocks (a code within max_d
+// agrees exactly on >= 2 of the P blocks, so on at least one pair): config 4 has three
+// 10-11-base pair keys for 737K codes -- every key gets a hash table of 16-byte slots
+// {code, index} in 64-byte groups of 4 (linear probing from the key's group, load <= 1/2).
+// A query reads one group per table, all tables' groups in flight at once: one dependent
+// round trip per query instead of an offset load followed by a scan of ~11 entries per
+// probe; a group without a free slot continues in the next (rare).
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+constexpr int kGroup = 4;  // slots per group (64 B)
+constexpr int MAX_KEYS = 6;  // C(4, 2): max_d = 2
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+struct OTable {
+  uint64_t keymask;  // OR of the key's block masks
+  uint64_t gmask;    // groups - 1
+  uint4* slots;      // {code lo, code hi, index | kEmpty, 0}
+};
+struct OTables {
+  OTable t[MAX_KEYS];
+};
+
+__global__ void oa_clear_kernel(uint4* __restrict__ slots, int64_t nslots) {
+  for (int64_t k = (int64_t)blockIdx.x * WG + threadIdx.x; k < nslots; k += (int64_t)gridDim.x * WG)
+    slots[k] = make_uint4(0u, 0u, kEmpty, 0u);
+}
+
+__global__ void oa_insert_kernel(const uint64_t* __restrict__ wl, int64_t nw, OTable tb) {
+  const int64_t nslots = (int64_t)(tb.gmask + 1) * kGroup;
+  for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j < nw; j += (int64_t)gridDim.x * WG) {
+    const uint64_t w = wl[j];
+    int64_t sidx = (int64_t)(mix64(w & tb.keymask) & tb.gmask) * kGroup;
+    for (int64_t step = 0; step < nslots; ++step, sidx = (sidx + 1) & (nslots - 1)) {
+      uint32_t* ix = reinterpret_cast<uint32_t*>(tb.slots + sidx) + 2;
+      if (atomicCAS(ix, kEmpty, (uint32_t)j) == kEmpty) {
+        uint32_t* c = reinterpret_cast<uint32_t*>(tb.slots + sidx);
+        c[0] = (uint32_t)w;
+        c[1] = (uint32_t)(w >> 32);
+        break;
+      }
+    }
+  }
+}
+
+template <int KIND, int T>
+__global__ __launch_bounds__(WG) void oa_query_kernel(const uint64_t* __restrict__ queries, int64_t nq, OTables tb,
+                                                      int max_d, int32_t* __restrict__ out_index,
+                                                      uint8_t* __restrict__ out_dist) {
+  const int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (i >= nq) return;
+  const uint64_t q = queries[i];
+  int best_d = max_d + 1, best_j = -1;
+  bool tie = false;
+  uint64_t grp[T];
+  uint4 v[T][kGroup];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {  // every table's group in flight before any is read
+    grp[t] = mix64(q & tb.t[t].keymask) & tb.t[t].gmask;
+    const uint4* g = tb.t[t].slots + grp[t] * kGroup;
+#pragma unroll
+    for (int k = 0; k < kGroup; ++k) v[t][k] = g[k];
+  }
+  auto visit = [&](const uint4 e) {
+    const uint64_t w = ((uint64_t)e.y << 32) | e.x;
+    const int d = KIND == 2 ? dist2(q, w) : dist3(q, w);
+    if (d <= best_d && d <= max_d) {
+      const int j = (int)e.z;
+      if (d < best_d) {
+        best_d = d;
+        best_j = j;
+        tie = false;
+      } else if (j != best_j) {
+        tie = true;
+      }
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    bool open = false;  // a free slot ends the key's probe sequence
+#pragma unroll
+    for (int k = 0; k < kGroup; ++k) {
+      if (v[t][k].z == kEmpty) open = true;
+      else if (!open) visit(v[t][k]);
+    }
+    for (uint64_t g = grp[t]; !open;) {  // the group was full: the next one (rare)
+      g = (g + 1) & tb.t[t].gmask;
+      const uint4* gp = tb.t[t].slots + g * kGroup;
+      for (int k = 0; k < kGroup && !open; ++k) {
+        const uint4 e = gp[k];
+        if (e.z == kEmpty) open = true;
+        else visit(e);
+      }
+    }
+  }
+  out_index[i] = best_j < 0 ? -1 : (tie ? -2 : best_j);
+  out_dist[i] = best_j < 0 ? (uint8_t)255 : (uint8_t)best_d;
+}
+
+template <int KIND>
+void launch_oa_query(int nt, unsigned blocks, hipStream_t s, const uint64_t* q, int64_t nq, const OTables& tb,
+                     int max_d, int32_t* idx, uint8_t* dist) {
+#define SCT_OQ(T)                                                                                       \
+  case T:                                                                                               \
+    hipLaunchKernelGGL((oa_query_kernel<KIND, T>), dim3(blocks), dim3(WG), 0, s, q, nq, tb, max_d, idx, \
+                       dist);                                                                           \
+    break;
+  switch (nt) {
+    SCT_OQ(1) SCT_OQ(3) SCT_OQ(6)
+    default: break;
+  }
+#undef SCT_OQ
+}
+
 template <int KIND>
 void launch_query(int np, unsigned blocks, hipStream_t s, const uint64_t* q, int64_t nq,
                   const Tables& tb, int max_d, int32_t* idx, uint8_t* dist) {
@@ -179,6 +303,8 @@ unsigned grid_for(int64_t n, int64_t cap = 16384) {
 struct sct_nearest_plan {
   int kind = 2, max_d = 0, nparts = 0, code_bits = 0;
   int64_t nw = 0;
+  int nkeys = 0;  // > 0: open-addressing multi-index (OTables); 0: CSR per block (Parts)
+  OTables ot{};
   Parts parts{};
   int64_t nbuckets[MAX_PARTS] = {};
   uint32_t* d_off[MAX_PARTS] = {};
@@ -188,6 +314,8 @@ struct sct_nearest_plan {
 
 extern "C" int sct_nearest_plan_destroy(sct_nearest_plan* p) {
   if (!p) return SCT_OK;
+  for (int k = 0; k < MAX_KEYS; ++k)
+    if (p->ot.t[k].slots) (void)hipFree(p->ot.t[k].slots);
   for (int k = 0; k < MAX_PARTS; ++k) {
     if (p->d_off[k]) (void)hipFree(p->d_off[k]);
     if (p->d_code[k]) (void)hipFree(p->d_code[k]);
@@ -220,6 +348,48 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
   p->nw = nw;
   p->code_bits = code_bits;
   p->nparts = max_d + 1;
+  // Open addressing when the multi-index keys are nearly unique for random codes: s = 1 block
+  // per key for max_d = 0 (the whole code), s = 2 (pairs of P = max_d + 2 blocks) for max_d 1..2,
+  // if every key spans enough bases that 4^bases >= nw / 2, i.e. at most ~2 random codes share
+  // a key (SCT_NEAREST_SCHEME=csr / oa forces one).
+  {
+    const int P = max_d == 0 ? 1 : max_d + 2;
+    const int sz = max_d == 0 ? 1 : 2;
+    const int nkeys = sz == 1 ? 1 : P * (P - 1) / 2;
+    int min_bases = G;  // the smallest key: two smallest blocks of a floor split
+    if (sz == 2) min_bases = 2 * (G / P);
+    bool oa = P <= G && nkeys <= MAX_KEYS && 2.0 * min_bases >= std::log2(0.5 * std::max<int64_t>(nw, 2));
+    if (const char* v = getenv("SCT_NEAREST_SCHEME")) {
+      if (!strcmp(v, "csr")) oa = false;
+      if (!strcmp(v, "oa")) oa = P <= G && nkeys <= MAX_KEYS;
+    }
+    if (oa) {
+      uint64_t bmask[MAX_KEYS + 2] = {};
+      for (int b = 0; b < P; ++b) {
+        const int lo = G * b / P * kind, hi = std::min(64, G * (b + 1) / P * kind);
+        bmask[b] = (hi - lo >= 64 ? ~0ull : ((1ull << (hi - lo)) - 1ull)) << lo;
+      }
+      int64_t nslots = kGroup;
+      while (nslots < 2 * nw) nslots *= 2;  // load <= 1/2
+      int t = 0;
+      for (int a = 0; a < P; ++a)
+        for (int b = sz == 1 ? a : a + 1; b < P; ++b) {
+          if (sz == 1 && b != a) continue;
+          OTable& ot = p->ot.t[t++];
+          ot.keymask = bmask[a] | bmask[b];
+          ot.gmask = (uint64_t)(nslots / kGroup - 1);
+          hipError_t e = hipMalloc(&ot.slots, (size_t)nslots * 16);
+          if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "slots: %s", hipGetErrorString(e)));
+          hipLaunchKernelGGL(oa_clear_kernel, dim3(grid_for(nslots, 8192)), dim3(WG), 0, s, ot.slots, nslots);
+          if (nw) hipLaunchKernelGGL(oa_insert_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_whitelist, nw, ot);
+          SCT_LAUNCH_CHECK();
+        }
+      p->nkeys = t;
+      SCT_HIP(hipStreamSynchronize(s));
+      *out = p;
+      return SCT_OK;
+    }
+  }
   // Bucket count per part: a provisional table of ~nw/2 buckets counts the occupied ones
   // (~ the distinct block values: 4^8 = 65,536 for an 8-base ThreeBit block of a 737K
   // whitelist, nw itself for max_d = 0), then the part gets ~SCT_NEAREST_LOAD (4) buckets per
@@ -324,6 +494,14 @@ extern "C" int sct_nearest_query(sct_nearest_plan* p, const uint64_t* d_queries,
   hipStream_t s = sct::as_stream(stream);
   const unsigned blocks = (unsigned)sct::ceil_div(nq, WG);  // one query per thread
   SCT_CHECK(sct::ceil_div(nq, WG) < (1LL << 31), "too many queries for one launch");
+  if (p->nkeys > 0) {
+    if (p->kind == 2)
+      launch_oa_query<2>(p->nkeys, blocks, s, d_queries, nq, p->ot, p->max_d, d_index, d_dist);
+    else
+      launch_oa_query<3>(p->nkeys, blocks, s, d_queries, nq, p->ot, p->max_d, d_index, d_dist);
+    SCT_LAUNCH_CHECK();
+    return SCT_OK;
+  }
   Tables tb{};
   for (int k = 0; k < p->nparts; ++k) {
     tb.part[k] = p->parts.p[k];

@@ -470,8 +470,13 @@ def _config4_queries(wl_seqs, nq, rng, alphabet=b"ACGT"):
     return picks
 
 
+@pytest.mark.parametrize("scheme", ["auto", "csr", "oa"])
 @pytest.mark.parametrize("kind,max_d", [(3, 0), (3, 1), (3, 2), (3, 3), (2, 0), (2, 1), (2, 2)])
-def test_nearest_vs_bruteforce(kind, max_d):
+def test_nearest_vs_bruteforce(kind, max_d, scheme, monkeypatch):
+    """Both index schemes (CSR buckets per block; open-addressing tables of block-pair
+    keys) against the brute force on config-4-shaped sets."""
+    if scheme != "auto":
+        monkeypatch.setenv("SCT_NEAREST_SCHEME", scheme)
     rng = np.random.default_rng(100 + 10 * kind + max_d)
     wl_codes2 = synthetic.whitelist_codes(3000, 16, seed=kind * 7 + max_d)
     wl_seqs = synthetic.decode_ascii(wl_codes2, 16)
@@ -686,13 +691,17 @@ def test_wide_kernel_item_ranges_sum_to_whole():
 
 
 # ---------------------------------------------------------------- config 4 at full size
-def test_nearest_config4_full_size():
+@pytest.mark.parametrize("scheme", ["auto", "csr"])
+def test_nearest_config4_full_size(scheme, monkeypatch):
     """Config 4 as specified: the 737,280-code ThreeBit whitelist and 100M observed
     barcodes (50 % exact, 25 % substitution, 15 % N, 10 % random) at max_d = 1.  Every
     exact draw must come back as its own index at distance 0, every one-edit query within
     distance 1; 20,000 sampled queries of every class bit-exact against the OpenMP brute
-    force over the whole whitelist."""
+    force over the whole whitelist.  AUTO = the open-addressing pair-key tables; CSR = the
+    per-block buckets."""
     torch = pytest.importorskip("torch")
+    if scheme != "auto":
+        monkeypatch.setenv("SCT_NEAREST_SCHEME", scheme)
     n, L, seed = synthetic.CONFIGS[2]
     wl = synthetic.two_to_three(synthetic.whitelist_codes(n, L, seed), L)
     nq = 100_000_000

@@ -1,14 +1,17 @@
 # rocprofv3 kernel trace + PMC passes over the config-4 nearest-whitelist query (100M
-# ThreeBit queries, 737K whitelist, max_d 1), for the shipped table sizing and, with
-# SCT_NEAREST_LOAD=1000000 (every part keeps ~nw/2 buckets: the round-1 sizing), for A/B.
+# ThreeBit queries, 737K whitelist, max_d 1): the shipped open-addressing pair-key tables
+# ("after"), the CSR per-block buckets sized by distinct block values ("csr"), and with
+# SCT_NEAREST_LOAD=1000000 the CSR buckets at the round-1 sizing of ~nw/2 ("before").
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 B="python3 tools/bench_paths.py --reads 0 --stream-reads 0 --fastq-records 0 --skip-allpairs5 --queries 100000000"
-for variant in after before; do
+for variant in after csr before; do
   D=gpurun_out/profn_$variant
   mkdir -p $D
-  if [ $variant = before ]; then export SCT_NEAREST_LOAD=1000000; else unset SCT_NEAREST_LOAD; fi
+  unset SCT_NEAREST_LOAD SCT_NEAREST_SCHEME
+  if [ $variant = before ]; then export SCT_NEAREST_LOAD=1000000 SCT_NEAREST_SCHEME=csr; fi
+  if [ $variant = csr ]; then export SCT_NEAREST_SCHEME=csr; fi
   timeout -k 10 240 $B > $D/bench.json 2> $D/bench.err || exit 3
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $D/trace -o run --output-format csv -- $B > $D/trace.log 2>&1 || exit 3
   i=0

@@ -20,12 +20,12 @@ def main():
     ap.add_argument("--round", default="r02")
     ap.add_argument("--queries", type=float, default=1e8)
     a = ap.parse_args()
-    for variant in ("after", "before"):
+    for variant in ("after", "csr", "before"):
         src = os.path.join(ROOT, "gpurun_out", "profn_" + variant)
         stats = os.path.join(src, "trace", "run_kernel_stats.csv")
         if not os.path.exists(stats):
             continue
-        k = "nearest_query_kernel"
+        k = "oa_query_kernel" if variant == "after" else "nearest_query_kernel"
         avg_ns, calls = kernel_avg_ns(stats, k)
         m = pmc_means(src, k)
         per_q = {c: v / a.queries for c, v in m.items() if c.startswith(("TCC", "TCP", "SQ_INSTS"))}
