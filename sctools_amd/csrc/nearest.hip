@@ -181,7 +181,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 struct OTable {
   uint64_t keymask;  // OR of the key's block masks
   uint64_t gmask;    // groups - 1
-  uint4* slots;      // {code lo, code hi, index | kEmpty, 0}
+  uint4* slots;      // {code lo, code hi, index | kEmpty, 1 if the code occurs twice}
 };
 struct OTables {
   OTable t[MAX_KEYS];
@@ -192,7 +192,8 @@ __global__ void oa_clear_kernel(uint4* __restrict__ slots, int64_t nslots) {
     slots[k] = make_uint4(0u, 0u, kEmpty, 0u);
 }
 
-__global__ void oa_insert_kernel(const uint64_t* __restrict__ wl, int64_t nw, OTable tb) {
+__global__ void oa_insert_kernel(const uint64_t* __restrict__ wl, int64_t nw, const uint8_t* __restrict__ dup,
+                                 OTable tb) {
   const int64_t nslots = (int64_t)(tb.gmask + 1) * kGroup;
   for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j < nw; j += (int64_t)gridDim.x * WG) {
     const uint64_t w = wl[j];
@@ -203,6 +204,7 @@ __global__ void oa_insert_kernel(const uint64_t* __restrict__ wl, int64_t nw, OT
         uint32_t* c = reinterpret_cast<uint32_t*>(tb.slots + sidx);
         c[0] = (uint32_t)w;
         c[1] = (uint32_t)(w >> 32);
+        c[3] = dup[j];
         break;
       }
     }
@@ -220,13 +222,33 @@ __global__ __launch_bounds__(WG) void oa_query_kernel(const uint64_t* __restrict
   bool tie = false;
   uint64_t grp[T];
   uint4 v[T][kGroup];
-#pragma unroll
-  for (int t = 0; t < T; ++t) {  // every table's group in flight before any is read
+  auto load_group = [&](int t) {
     grp[t] = mix64(q & tb.t[t].keymask) & tb.t[t].gmask;
     const uint4* g = tb.t[t].slots + grp[t] * kGroup;
 #pragma unroll
     for (int k = 0; k < kGroup; ++k) v[t][k] = g[k];
+  };
+  // Table 0 first: an exact hit on a code that occurs once is the answer (every other code
+  // is >= 1 away) and the other tables are never read -- half of config 4's queries.  Any
+  // exact match shares every key, so it is always in table 0's probe sequence.
+  load_group(0);
+  bool exact_unique = false;
+#pragma unroll
+  for (int k = 0; k < kGroup; ++k) {
+    const uint4 e = v[0][k];
+    if (e.z != kEmpty && ((uint64_t)e.y << 32 | e.x) == q && !e.w) {
+      exact_unique = true;
+      best_d = 0;
+      best_j = (int)e.z;
+    }
   }
+  if (exact_unique) {
+    out_index[i] = best_j;
+    out_dist[i] = 0;
+    return;
+  }
+#pragma unroll
+  for (int t = 1; t < T; ++t) load_group(t);  // the other tables' groups in flight together
   auto visit = [&](const uint4 e) {
     const uint64_t w = ((uint64_t)e.y << 32) | e.x;
     const int d = KIND == 2 ? dist2(q, w) : dist3(q, w);
@@ -300,6 +322,29 @@ unsigned grid_for(int64_t n, int64_t cap = 16384) {
 
 }  // namespace
 
+// dup[j] = 1 if whitelist code j occurs more than once (sorted (code, index), equal
+// neighbours); a device buffer of nw bytes, ready on `s` when this returns.
+static int compute_dups(const uint64_t* d_whitelist, int64_t nw, uint8_t* dup, hipStream_t s) {
+  SCT_HIP(hipMemsetAsync(dup, 0, (size_t)std::max<int64_t>(nw, 1), s));
+  if (nw < 2) return SCT_OK;
+  size_t sort_bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)nw, 0, 64, s);
+  sct::DevBuf tmp, skeys, sidx, iota;
+  SCT_HIP(tmp.alloc(sort_bytes));
+  SCT_HIP(skeys.alloc((size_t)nw * 8));
+  SCT_HIP(sidx.alloc((size_t)nw * 4));
+  SCT_HIP(iota.alloc((size_t)nw * 4));
+  hipLaunchKernelGGL(iota_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, (uint32_t*)iota.p, nw);
+  SCT_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, sort_bytes, d_whitelist, (uint64_t*)skeys.p,
+                                             (const uint32_t*)iota.p, (uint32_t*)sidx.p, (int)nw, 0, 64, s));
+  hipLaunchKernelGGL(flag_dups_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, (const uint64_t*)skeys.p,
+                     (const uint32_t*)sidx.p, nw, dup);
+  SCT_LAUNCH_CHECK();
+  SCT_HIP(hipStreamSynchronize(s));  // the scratch dies here
+  return SCT_OK;
+}
+
 struct sct_nearest_plan {
   int kind = 2, max_d = 0, nparts = 0, code_bits = 0;
   int64_t nw = 0;
@@ -348,6 +393,10 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
   p->nw = nw;
   p->code_bits = code_bits;
   p->nparts = max_d + 1;
+  sct::DevBuf dup;
+  if (dup.alloc((size_t)std::max<int64_t>(nw, 1)) != hipSuccess)
+    return fail_with(sct::fail(SCT_E_NOMEM, "dup flags"));
+  if (int rc = compute_dups(d_whitelist, nw, (uint8_t*)dup.p, s); rc != SCT_OK) return fail_with(rc);
   // Open addressing when the multi-index keys are nearly unique for random codes: s = 1 block
   // per key for max_d = 0 (the whole code), s = 2 (pairs of P = max_d + 2 blocks) for max_d 1..2,
   // if every key spans enough bases that 4^bases >= nw / 2, i.e. at most ~2 random codes share
@@ -381,7 +430,9 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
           hipError_t e = hipMalloc(&ot.slots, (size_t)nslots * 16);
           if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "slots: %s", hipGetErrorString(e)));
           hipLaunchKernelGGL(oa_clear_kernel, dim3(grid_for(nslots, 8192)), dim3(WG), 0, s, ot.slots, nslots);
-          if (nw) hipLaunchKernelGGL(oa_insert_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_whitelist, nw, ot);
+          if (nw)
+            hipLaunchKernelGGL(oa_insert_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_whitelist, nw,
+                               (const uint8_t*)dup.p, ot);
           SCT_LAUNCH_CHECK();
         }
       p->nkeys = t;
@@ -409,35 +460,17 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
     pt.shift = lg0 == 0 ? 63 : 64 - lg0;
   }
   const int64_t nb0 = 1LL << lg0;
-  size_t scan_bytes = 0, sort_bytes = 0;
+  size_t scan_bytes = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                          (int)(nb0 + 1), s);
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)std::max<int64_t>(nw, 1),
-                                           0, 64, s);
-  sct::DevBuf scan_tmp, cursor, occ, skeys, sidx, iota, dup;
-  hipError_t e = scan_tmp.alloc(std::max(scan_bytes, sort_bytes));
+  sct::DevBuf scan_tmp, cursor, occ;
+  hipError_t e = scan_tmp.alloc(scan_bytes);
   if (e == hipSuccess) e = cursor.alloc((size_t)(nb0 + 1) * 4);
   if (e == hipSuccess) e = occ.alloc(8 * MAX_PARTS);
-  if (e == hipSuccess) e = skeys.alloc((size_t)std::max<int64_t>(nw, 1) * 8);
-  if (e == hipSuccess) e = sidx.alloc((size_t)std::max<int64_t>(nw, 1) * 4);
-  if (e == hipSuccess) e = iota.alloc((size_t)std::max<int64_t>(nw, 1) * 4);
-  if (e == hipSuccess) e = dup.alloc((size_t)std::max<int64_t>(nw, 1));
   if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "scratch: %s", hipGetErrorString(e)));
   uint32_t* counts = (uint32_t*)cursor.p;
   auto* d_occ = (unsigned long long*)occ.p;
   SCT_HIP(hipMemsetAsync(d_occ, 0, 8 * MAX_PARTS, s));
-  SCT_HIP(hipMemsetAsync(dup.p, 0, (size_t)std::max<int64_t>(nw, 1), s));
-  if (nw > 1) {
-    // duplicate codes: sort (code, index), flag equal neighbours
-    hipLaunchKernelGGL(iota_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, (uint32_t*)iota.p, nw);
-    size_t tb = sort_bytes;
-    e = hipcub::DeviceRadixSort::SortPairs(scan_tmp.p, tb, d_whitelist, (uint64_t*)skeys.p, (const uint32_t*)iota.p,
-                                           (uint32_t*)sidx.p, (int)nw, 0, 64, s);
-    if (e != hipSuccess) return fail_with(sct::fail(SCT_E_HIP, "sort: %s", hipGetErrorString(e)));
-    hipLaunchKernelGGL(flag_dups_kernel, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, (const uint64_t*)skeys.p,
-                       (const uint32_t*)sidx.p, nw, (uint8_t*)dup.p);
-  }
   if (nw && lg0 > 0) {  // occupied provisional buckets per part
     for (int k = 0; k < p->nparts; ++k) {
       SCT_HIP(hipMemsetAsync(counts, 0, (size_t)(nb0 + 1) * 4, s));
