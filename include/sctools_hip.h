@@ -65,6 +65,26 @@ int sct_encode_host(int kind, const uint8_t* seqs, int64_t n, int64_t stride, in
 int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, int L, uint64_t* codes,
                            uint8_t* gc, uint8_t* flags, int64_t chunk);
 
+/* Variable-length records (device): record r = starts[r] .. starts[r] + lens[r] of buf,
+ * encoded as encodings.py:75-88 / :155-167 do into `words` limbs (words >= ceil(kind*len/64)
+ * for every record); gc (nullable, saturating at 255) and flags as sct_encode. */
+int sct_encode_var(int kind, const uint8_t* buf, const int64_t* starts, const int32_t* lens, int64_t n,
+                   int words, uint64_t* codes, uint8_t* gc, uint8_t* flags, void* stream);
+
+/* ---------------------------------------------------------------- whitelist ingest
+ * Replaces the line loop of Barcodes.from_whitelist (src/sctools/barcode.py:95-97): the
+ * file opened 'rb', every line (ending at '\n'; a final line may lack it) chopped by
+ * `line[:-1]` (its last byte, whatever it is) and TwoBit-encoded.
+ * sct_lines (device, synchronous): starts / lens (the chopped length) of every line; a
+ * call with max_lines < the line count only reports *nlines (and *max_len = 0).
+ * sct_whitelist_encode_host: the same plus sct_encode_var on the lines, host pointers;
+ * call with max_lines = 0 to learn nlines and max_len, then with room for nlines. */
+int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines, int64_t* d_starts, int32_t* d_lens,
+              int64_t* nlines, int32_t* max_len, void* stream);
+int sct_whitelist_encode_host(const uint8_t* buf, int64_t nbytes, int kind, int words, int64_t max_lines,
+                              int64_t* nlines, int32_t* max_len, uint64_t* codes, int64_t* starts,
+                              int32_t* lens, uint8_t* flags);
+
 /* ---------------------------------------------------------------- decoders
  * TwoBit(L).decode (encodings.py:90-100): exactly L bytes from the LSB upward,
  * bits above 2L ignored.  out: n*L bytes.
@@ -286,6 +306,22 @@ int sct_fastq_extract_host(const uint8_t* buf, int64_t nbytes, const int64_t* fi
                            int text_mode, const int32_t* spans, int nspans, uint8_t* seq_out,
                            uint8_t* qual_out, int32_t* seq_len, int32_t* qual_len,
                            int64_t max_records, int64_t* nrecords, int64_t* first_bad_name);
+
+/* Streaming form (reader.Reader reads its files lazily, reader.py:56-85): a stream keeps
+ * its device buffers across pieces of the concatenated files.  Each piece must end on a
+ * '\n' unless final; file_ends are the files' ends inside the piece (the last == nbytes).
+ * chunk: extracts every complete record of the piece on the device; consumed = the byte
+ * just past the last complete record (final = 1: nbytes, the incomplete tail dropped);
+ * the caller starts the next piece there.  fetch: that piece's outputs, laid out as
+ * sct_fastq_extract_host's (each nullable; qualities only if the stream keeps them). */
+typedef struct sct_fastq_stream sct_fastq_stream;
+int sct_fastq_stream_create(int text_mode, const int32_t* spans, int nspans, int qualities,
+                            sct_fastq_stream** stream);
+int sct_fastq_stream_destroy(sct_fastq_stream* stream);
+int sct_fastq_stream_chunk(sct_fastq_stream* stream, const uint8_t* buf, int64_t nbytes, const int64_t* file_ends,
+                           int nfiles, int final, int64_t* nrecords, int64_t* consumed, int64_t* first_bad_name);
+int sct_fastq_stream_fetch(sct_fastq_stream* stream, uint8_t* seq_out, uint8_t* qual_out, int32_t* seq_len,
+                           int32_t* qual_len);
 
 /* ---------------------------------------------------------------- summary
  * Replaces barcode.py:44-46 (np.percentile(distances,[0,25,50,75,100]) with numpy's

@@ -41,6 +41,10 @@ SIGNATURES = {
     "sct_encode": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
     "sct_encode_host": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp],
     "sct_encode_stream_host": [_i32, _vp, _i64, _i32, _vp, _vp, _vp, _i64],
+    "sct_encode_var": [_i32, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp],
+    "sct_lines": [_vp, _i64, _i64, _vp, _vp, ctypes.POINTER(_i64), ctypes.POINTER(_i32), _vp],
+    "sct_whitelist_encode_host": [_vp, _i64, _i32, _i32, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i32), _vp,
+                                  _vp, _vp, _vp],
     "sct_decode2": [_vp, _i64, _i32, _i32, _vp, _vp],
     "sct_decode2_host": [_vp, _i64, _i32, _i32, _vp],
     "sct_decode3": [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp],
@@ -82,6 +86,11 @@ SIGNATURES = {
     "sct_fastq_extract_host": [_vp, _i64, _vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _i64,
                                ctypes.POINTER(_i64), ctypes.POINTER(_i64)],
     "sct_base_frequency_host": [_vp, _i64, _i32, _vp],
+    "sct_fastq_stream_create": [_i32, _vp, _i32, _i32, ctypes.POINTER(_vp)],
+    "sct_fastq_stream_destroy": [_vp],
+    "sct_fastq_stream_chunk": [_vp, _vp, _i64, _vp, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
+                               ctypes.POINTER(_i64)],
+    "sct_fastq_stream_fetch": [_vp, _vp, _vp, _vp, _vp],
 }
 _RESTYPES = {"sct_last_error": ctypes.c_char_p}
 
@@ -253,6 +262,25 @@ def encode_stream(kind, seqs, chunk=0):
     return codes, gc, flags
 
 
+def whitelist_encode(data, kind=2):
+    """Whitelist file bytes -> every line's [:-1] encoded on the device (barcode.py:95-97):
+    (codes (n, words) uint64, starts int64[n], chopped lengths int32[n], flags uint8[n])."""
+    buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    n, mx = _i64(0), _i32(0)
+    f = lib().sct_whitelist_encode_host
+    check(f(_ptr(buf), len(data), kind, 1, 0, ctypes.byref(n), ctypes.byref(mx), None, None, None, None))
+    nl = n.value
+    words = words_for_bits(kind * mx.value)
+    codes = np.zeros((nl, words), dtype=np.uint64)
+    starts = np.zeros(nl, dtype=np.int64)
+    lens = np.zeros(nl, dtype=np.int32)
+    flags = np.zeros(nl, dtype=np.uint8)
+    if nl:
+        check(f(_ptr(buf), len(data), kind, words, nl, ctypes.byref(n), ctypes.byref(mx), _ptr(codes),
+                _ptr(starts), _ptr(lens), _ptr(flags)))
+    return codes, starts, lens, flags
+
+
 def decode2(codes, L):
     codes = np.ascontiguousarray(codes, dtype=np.uint64)
     codes2 = codes.reshape(codes.shape[0], -1)
@@ -388,6 +416,54 @@ def fastq_extract(buf, file_ends, spans, text_mode, qualities=True):
         out.append((rows, slen[k * n:(k + 1) * n], q, qlen[k * n:(k + 1) * n] if qualities else None))
         off += n * w
     return n, bad.value, out
+
+
+class FastqStream:
+    """Chunked FASTQ extraction (sct_fastq_stream): device buffers kept across pieces."""
+
+    def __init__(self, spans, text_mode, qualities=True):
+        self._lib = lib()
+        self._h = _vp()
+        self.spans = [(int(a), int(b)) for a, b in spans]
+        self.qualities = bool(qualities)
+        sp = np.ascontiguousarray(np.array(self.spans, dtype=np.int32).reshape(-1, 2))
+        check(self._lib.sct_fastq_stream_create(int(text_mode), _ptr(sp), sp.shape[0], int(qualities),
+                                                ctypes.byref(self._h)))
+
+    def chunk(self, buf, nbytes, file_ends, final):
+        """Extract the complete records of buf[:nbytes] (a writable or read-only buffer);
+        returns (nrecords, consumed, first_bad, [(seq, seq_len, qual, qual_len) per span])."""
+        data = np.frombuffer(buf, dtype=np.uint8, count=nbytes) if nbytes else np.zeros(1, np.uint8)
+        ends = np.ascontiguousarray(file_ends, dtype=np.int64)
+        n, used, bad = _i64(0), _i64(0), _i64(0)
+        check(self._lib.sct_fastq_stream_chunk(self._h, _ptr(data), nbytes, _ptr(ends), ends.size, int(final),
+                                               ctypes.byref(n), ctypes.byref(used), ctypes.byref(bad)))
+        del data
+        nr = n.value
+        widths = [b - a for a, b in self.spans]
+        seq = np.zeros(max(1, nr * sum(widths)), dtype=np.uint8)
+        qual = np.zeros_like(seq) if self.qualities else None
+        slen = np.zeros(max(1, nr * len(widths)), dtype=np.int32)
+        qlen = np.zeros_like(slen) if self.qualities else None
+        check(self._lib.sct_fastq_stream_fetch(self._h, _ptr(seq), _ptr(qual), _ptr(slen), _ptr(qlen)))
+        out, off = [], 0
+        for k, w in enumerate(widths):
+            rows = seq[off:off + nr * w].reshape(nr, w)
+            q = qual[off:off + nr * w].reshape(nr, w) if self.qualities else None
+            out.append((rows, slen[k * nr:(k + 1) * nr], q, qlen[k * nr:(k + 1) * nr] if self.qualities else None))
+            off += nr * w
+        return nr, used.value, bad.value, out
+
+    def close(self):
+        if self._h:
+            self._lib.sct_fastq_stream_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class FastqIndex:

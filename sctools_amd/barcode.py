@@ -122,10 +122,19 @@ class Barcodes:
         """Barcode set from a whitelist file (barcode.py:84-97).
 
         As in the reference each line loses exactly its LAST byte (``barcode[:-1]``),
-        every line is TwoBit-encoded, and duplicates collapse through Counter."""
+        every line is TwoBit-encoded, and duplicates collapse through Counter.  The file's
+        bytes go to the GPU whole: the line split, the chop and the encode run there
+        (sctools_amd/csrc/lines.hip); lines with ambiguous or invalid bytes are then redone
+        in file order through TwoBit.encode, so the random draws and the KeyError of
+        encodings.py:63-69 happen exactly as the reference's loop makes them."""
         with open(file_, 'rb') as f:
-            lines = list(f)
-        return cls(Counter(_encode_lines([ln[:-1] for ln in lines])), barcode_length)
+            data = f.read()
+        codes, starts, lens, flags = _lib.whitelist_encode(data, 2)
+        vals = codes[:, 0].tolist() if codes.shape[1] == 1 else _lib.limbs_to_ints(codes)
+        for i in np.flatnonzero(flags).tolist():
+            s = int(starts[i])
+            vals[i] = TwoBit.encode(data[s:s + int(lens[i])])
+        return cls(Counter(vals), barcode_length)
 
     @classmethod
     def from_iterable_encoded(cls, iterable, barcode_length):

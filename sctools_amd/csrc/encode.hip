@@ -73,16 +73,21 @@ struct RecordReader {
   }
 };
 
+// Records at seqs + r * stride of L bytes, or (starts != nullptr) at seqs + starts[r] of
+// lens[r] bytes each (variable-length lines: the whitelist ingest, sctools_amd/csrc/lines.hip).
 __global__ __launch_bounds__(WG) void encode_kernel(int kind, const uint8_t* __restrict__ seqs,
-                                                    int64_t n, int64_t stride, int L, int words,
+                                                    int64_t n, int64_t stride, int L_all, int words,
                                                     bool dword_path, uint64_t* __restrict__ codes,
                                                     uint8_t* __restrict__ gc,
-                                                    uint8_t* __restrict__ flags) {
+                                                    uint8_t* __restrict__ flags,
+                                                    const int64_t* __restrict__ starts = nullptr,
+                                                    const int32_t* __restrict__ lens = nullptr) {
   __shared__ uint8_t lut[256];
   fill_lut(lut, kind);
   const int bits = kind;
   for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
-    RecordReader rd{seqs + r * stride, dword_path, 0u, -1};
+    const int L = starts ? lens[r] : L_all;
+    RecordReader rd{seqs + (starts ? starts[r] : r * stride), dword_path, 0u, -1};
     uint32_t fl = 0;
     uint64_t* out = codes + r * words;
     uint32_t g = 0;
@@ -119,7 +124,7 @@ __global__ __launch_bounds__(WG) void encode_kernel(int kind, const uint8_t* __r
       if (wcur < words) out[wcur++] = nxt;
       while (wcur < words) out[wcur++] = 0;
     }
-    if (gc) gc[r] = (uint8_t)g;
+    if (gc) gc[r] = (uint8_t)(g > 255 ? 255 : g);
     if (flags) flags[r] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
   }
 }
@@ -415,7 +420,20 @@ extern "C" int sct_encode(int kind, const uint8_t* seqs, int64_t n, int64_t stri
   }
   const bool dw = (L % 4 == 0) && (stride % 4 == 0) && ((uintptr_t)seqs % 4 == 0);
   hipLaunchKernelGGL(encode_kernel, dim3(grid_for(n)), dim3(WG), 0, sct::as_stream(stream), kind,
-                     seqs, n, stride, L, words, dw, codes, gc, flags);
+                     seqs, n, stride, L, words, dw, codes, gc, flags, (const int64_t*)nullptr,
+                     (const int32_t*)nullptr);
+  SCT_LAUNCH_CHECK();
+  return SCT_OK;
+}
+
+extern "C" int sct_encode_var(int kind, const uint8_t* buf, const int64_t* starts, const int32_t* lens,
+                              int64_t n, int words, uint64_t* codes, uint8_t* gc, uint8_t* flags, void* stream) {
+  SCT_CHECK(kind == 2 || kind == 3, "kind must be 2 or 3");
+  SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
+  if (n == 0) return SCT_OK;
+  SCT_CHECK(buf && starts && lens && codes, "NULL pointer");
+  hipLaunchKernelGGL(encode_kernel, dim3(grid_for(n)), dim3(WG), 0, sct::as_stream(stream), kind, buf, n,
+                     (int64_t)0, 0, words, false, codes, gc, flags, starts, lens);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }

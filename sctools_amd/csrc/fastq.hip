@@ -22,6 +22,8 @@
 // No per-line array is ever stored.
 #include <hipcub/hipcub.hpp>
 
+#include <string.h>
+
 #include <algorithm>
 #include <vector>
 
@@ -354,6 +356,39 @@ __global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__
   }
 }
 
+// The byte just past line `target` (0-based line number; its terminator is terminator
+// number `target` of the buffer): one workgroup finds the tile holding it (binary search of
+// the tile offsets) and recounts that tile's terminators as extract_kernel does.
+__global__ __launch_bounds__(WG) void line_end_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs, int text,
+                                                      const unsigned long long* __restrict__ offsets, int64_t ntiles,
+                                                      unsigned long long target, long long* __restrict__ out) {
+  int64_t lo = 0, hi = ntiles - 1;  // last tile k with offsets[k] <= target
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (offsets[mid] <= target) lo = mid; else hi = mid - 1;
+  }
+  const int64_t t0 = lo * TILE, p0 = t0 + (int64_t)threadIdx.x * 16;
+  uint32_t m = 0, crlf = 0, na;
+  int vj = -1;
+  if (p0 < n) {
+    m = load_mask(buf, n, p0, text, &crlf, &na);
+    vj = virtual_in(buf, n, fs, p0, text);
+  }
+  uint32_t bits = m | (vj >= 0 ? (1u << vj) : 0u);
+  using BS = hipcub::BlockScan<uint32_t, WG>;
+  __shared__ typename BS::TempStorage tmp;
+  uint32_t pre;
+  BS(tmp).ExclusiveSum((uint32_t)__popc(bits), pre);
+  const unsigned long long want = target - offsets[lo];
+  uint32_t at = pre;
+  while (bits) {
+    const int j = __ffs(bits) - 1;
+    bits &= bits - 1;
+    if (at == want) *out = p0 + j + 1;  // a real terminator ends at its byte; a virtual one at the file end
+    ++at;
+  }
+}
+
 }  // namespace
 
 struct sct_fastq_index {
@@ -525,5 +560,156 @@ extern "C" int sct_fastq_extract_host(const uint8_t* buf, int64_t nbytes, const 
   if (qual_out && bytes) SCT_HIP(hipMemcpy(qual_out, d_q.p, (size_t)bytes, hipMemcpyDeviceToHost));
   if (seq_len && lbytes) SCT_HIP(hipMemcpy(seq_len, d_sl.p, lbytes, hipMemcpyDeviceToHost));
   if (qual_len && lbytes) SCT_HIP(hipMemcpy(qual_len, d_ql.p, lbytes, hipMemcpyDeviceToHost));
+  return SCT_OK;
+}
+
+// ---------------------------------------------------------------- streaming (chunked) ingest
+// reader.Reader iterates its files lazily (src/sctools/reader.py:56-85); a FASTQ stream of
+// a billion reads never sits in host memory whole.  A stream object keeps its device
+// buffers across chunks: the caller passes consecutive pieces of the concatenated files
+// (each ending on a '\n' unless it is the last), every complete record of a piece is
+// extracted, and `consumed` says where the next piece must start (the lines of a record
+// cut by the piece end are carried over by the caller).
+struct sct_fastq_stream {
+  int text = 0, nspans = 0, qualities = 1;
+  int32_t spans[2 * MAX_SPANS] = {};
+  int64_t width = 0;  // sum of span widths
+  sct::HostStage* st = nullptr;
+  void* d_buf = nullptr;
+  int64_t buf_cap = 0;
+  void* d_out = nullptr;  // seq | qual | seq_len | qual_len for rec_cap records
+  int64_t rec_cap = 0;
+  long long* d_end = nullptr;
+  int64_t nrec = 0, first_bad = -1, consumed = 0;
+};
+
+extern "C" int sct_fastq_stream_destroy(sct_fastq_stream* s) {
+  if (!s) return SCT_OK;
+  if (s->d_buf) (void)hipFree(s->d_buf);
+  if (s->d_out) (void)hipFree(s->d_out);
+  if (s->d_end) (void)hipFree(s->d_end);
+  delete s;
+  return SCT_OK;
+}
+
+extern "C" int sct_fastq_stream_create(int text_mode, const int32_t* spans, int nspans, int qualities,
+                                       sct_fastq_stream** out) {
+  SCT_CHECK(out != nullptr, "stream is NULL");
+  *out = nullptr;
+  SCT_CHECK(nspans >= 0 && nspans <= MAX_SPANS && (nspans == 0 || spans), "0..%d spans", MAX_SPANS);
+  auto* s = new sct_fastq_stream();
+  s->text = text_mode ? 1 : 0;
+  s->nspans = nspans;
+  s->qualities = qualities ? 1 : 0;
+  for (int k = 0; k < nspans; ++k) {
+    if (!(0 <= spans[2 * k] && spans[2 * k] <= spans[2 * k + 1] && spans[2 * k + 1] <= 4096)) {
+      delete s;
+      return sct::fail(SCT_E_INVALID, "span %d = [%d, %d) unsupported", k, spans[2 * k], spans[2 * k + 1]);
+    }
+    s->spans[2 * k] = spans[2 * k];
+    s->spans[2 * k + 1] = spans[2 * k + 1];
+    s->width += spans[2 * k + 1] - spans[2 * k];
+  }
+  s->st = sct::host_stage();
+  if (!s->st || hipMalloc((void**)&s->d_end, 8) != hipSuccess) {
+    sct_fastq_stream_destroy(s);
+    return sct::fail(SCT_E_HIP, "fastq stream: device setup failed");
+  }
+  *out = s;
+  return SCT_OK;
+}
+
+// One piece: extract its complete records on the device.  final = 0: `consumed` = the byte
+// just past the last complete record; final = 1: the whole piece is consumed (a trailing
+// incomplete record is dropped, as the reference's grouper drops it).
+extern "C" int sct_fastq_stream_chunk(sct_fastq_stream* s, const uint8_t* buf, int64_t nbytes,
+                                      const int64_t* file_ends, int nfiles, int final, int64_t* nrecords,
+                                      int64_t* consumed, int64_t* first_bad_name) {
+  SCT_CHECK(s && nrecords && consumed && first_bad_name, "NULL pointer");
+  SCT_CHECK(nbytes >= 0 && (nbytes == 0 || buf), "bad buffer");
+  hipStream_t hs = s->st->stream;
+  if (nbytes > s->buf_cap) {
+    if (s->d_buf) (void)hipFree(s->d_buf);
+    s->d_buf = nullptr;
+    s->buf_cap = 0;
+    SCT_HIP(hipMalloc(&s->d_buf, (size_t)nbytes));
+    s->buf_cap = nbytes;
+  }
+  // through the stage's pinned buffer in 64 MB pieces: page-locked copies, no per-call pinning
+  constexpr size_t kPiece = 64ull << 20;
+  SCT_TRY(sct::stage_reserve(s->st, std::min<size_t>((size_t)nbytes, kPiece), 0));
+  for (int64_t o = 0; o < nbytes; o += (int64_t)kPiece) {
+    const size_t len = (size_t)std::min<int64_t>((int64_t)kPiece, nbytes - o);
+    SCT_HIP(hipStreamSynchronize(hs));  // the previous piece's copy has left the pinned buffer
+    memcpy(s->st->pinned, buf + o, len);
+    SCT_HIP(hipMemcpyAsync((uint8_t*)s->d_buf + o, s->st->pinned, len, hipMemcpyHostToDevice, hs));
+  }
+  sct_fastq_index* ix = nullptr;
+  SCT_TRY(sct_fastq_index_create((const uint8_t*)s->d_buf, nbytes, file_ends, nfiles, s->text, hs, &ix));
+  struct Guard {
+    sct_fastq_index* p;
+    ~Guard() { sct_fastq_index_destroy(p); }
+  } g{ix};
+  const int64_t nrec = ix->nrec;
+  if (nrec > s->rec_cap) {
+    if (s->d_out) (void)hipFree(s->d_out);
+    s->d_out = nullptr;
+    s->rec_cap = 0;
+    const int64_t cap = nrec + nrec / 4 + 1024;
+    SCT_HIP(hipMalloc(&s->d_out, (size_t)cap * (2 * s->width + 8 * s->nspans) + 256));
+    s->rec_cap = cap;
+  }
+  uint8_t* d_seq = (uint8_t*)s->d_out;
+  uint8_t* d_qual = d_seq + s->rec_cap * s->width;
+  int32_t* d_sl = (int32_t*)(d_qual + s->rec_cap * s->width);
+  int32_t* d_ql = d_sl + s->rec_cap * s->nspans;
+  int64_t bad = -1;
+  SCT_TRY(sct_fastq_extract_spans(ix, (const uint8_t*)s->d_buf, s->spans, s->nspans, d_seq,
+                                  s->qualities ? d_qual : nullptr, d_sl, s->qualities ? d_ql : nullptr, &bad, hs));
+  int64_t used = nbytes;
+  if (!final) {
+    used = 0;
+    if (nrec > 0) {
+      hipLaunchKernelGGL(line_end_kernel, dim3(1), dim3(WG), 0, hs, (const uint8_t*)s->d_buf, nbytes,
+                         Files{ix->d_ends, ix->nfiles}, s->text, ix->d_offsets, ix->ntiles,
+                         (unsigned long long)(4 * nrec - 1), s->d_end);
+      SCT_LAUNCH_CHECK();
+      long long e = -1;
+      SCT_HIP(hipMemcpyAsync(&e, s->d_end, 8, hipMemcpyDeviceToHost, hs));
+      SCT_HIP(hipStreamSynchronize(hs));
+      SCT_CHECK(e > 0 && e <= nbytes, "record end not found");
+      used = e;
+    }
+  }
+  s->nrec = nrec;
+  s->first_bad = bad;
+  s->consumed = used;
+  *nrecords = nrec;
+  *consumed = used;
+  *first_bad_name = bad;
+  return SCT_OK;
+}
+
+// The last piece's outputs, laid out as sct_fastq_extract_host's (nullable each).
+extern "C" int sct_fastq_stream_fetch(sct_fastq_stream* s, uint8_t* seq_out, uint8_t* qual_out, int32_t* seq_len,
+                                      int32_t* qual_len) {
+  SCT_CHECK(s != nullptr, "stream is NULL");
+  SCT_CHECK(s->qualities || (!qual_out && !qual_len), "stream created without qualities");
+  hipStream_t hs = s->st->stream;
+  const int64_t n = s->nrec;
+  if (n == 0) return SCT_OK;
+  const uint8_t* d_seq = (const uint8_t*)s->d_out;
+  const uint8_t* d_qual = d_seq + s->rec_cap * s->width;
+  const int32_t* d_sl = (const int32_t*)(d_qual + s->rec_cap * s->width);
+  const int32_t* d_ql = d_sl + s->rec_cap * s->nspans;
+  // the extraction lays span k's rows out at n * prefix_k and its lengths at n * k, as here
+  if (seq_out && s->width) SCT_HIP(hipMemcpyAsync(seq_out, d_seq, (size_t)(n * s->width), hipMemcpyDeviceToHost, hs));
+  if (qual_out && s->width)
+    SCT_HIP(hipMemcpyAsync(qual_out, d_qual, (size_t)(n * s->width), hipMemcpyDeviceToHost, hs));
+  if (seq_len && s->nspans)
+    SCT_HIP(hipMemcpyAsync(seq_len, d_sl, (size_t)n * s->nspans * 4, hipMemcpyDeviceToHost, hs));
+  if (qual_len && s->nspans)
+    SCT_HIP(hipMemcpyAsync(qual_len, d_ql, (size_t)n * s->nspans * 4, hipMemcpyDeviceToHost, hs));
+  SCT_HIP(hipStreamSynchronize(hs));
   return SCT_OK;
 }

@@ -6,7 +6,11 @@
 record happen in one pass on the GPU (sctools_amd/csrc/fastq.hip); Python objects are made
 only for the records actually iterated.  ``extract_arrays()`` is the batch form that feeds
 the hot path without per-record objects: fixed-width numpy rows plus lengths, ready for
-``encodings.TwoBit.encode_array`` / ``ThreeBit.encode_array``.
+``encodings.TwoBit.encode_array`` / ``ThreeBit.encode_array``; ``iter_arrays()`` yields the
+same per piece of the files, which are read lazily in pieces of ``CHUNK_BYTES`` (a record
+cut by a piece end is carried into the next piece, also across a file boundary), so a
+billion-read stream never sits in host memory whole.  Text mode accepts ASCII only (the
+device slices bytes; a non-ASCII text file raises ValueError: read it in 'rb' mode).
 
 File handling follows reader.Reader (src/sctools/reader.py:15-85): a str or a list of str
 filenames, modes 'r' (text: universal newlines, str fields) and 'rb' (bytes fields), and
@@ -40,17 +44,18 @@ def _filenames(files):
     raise TypeError('files must be a string filename or a list of such names.')
 
 
-def _read_bytes(name):
-    """reader.py:64-71: .gz / .bz2 by suffix, else a plain file (bytes; the device applies
-    the text-mode newline rules)."""
+def _open_binary(name):
+    """reader.py:64-71: .gz / .bz2 by suffix, else a plain file, always as bytes (the device
+    applies the text-mode newline rules)."""
     if name.endswith('.gz'):
-        with gzip.open(name, 'rb') as f:
-            return f.read()
+        return gzip.open(name, 'rb')
     if name.endswith('.bz2'):
-        with bz2.open(name, 'rb') as f:
-            return f.read()
-    with open(name, 'rb') as f:
-        return f.read()
+        return bz2.open(name, 'rb')
+    return open(name, 'rb')
+
+
+#: bytes per piece handed to the device (the files are read lazily, piece by piece)
+CHUNK_BYTES = 256 << 20
 
 
 class EmbeddedBarcodeGenerator:
@@ -72,11 +77,73 @@ class EmbeddedBarcodeGenerator:
     def filenames(self):
         return self._files
 
+    def _pieces(self, qualities=True, chunk_bytes=None):
+        """Read the files lazily (reader.py:56-85) in pieces of about `chunk_bytes`, cut after
+        their last '\\n'; the device extracts each piece's complete records and says where
+        the next piece starts (a record cut by the piece end is carried over, also across a
+        file boundary).  Yields (first record number, nrecords, first bad-name record of the
+        piece or -1, per-span arrays)."""
+        chunk_bytes = int(chunk_bytes or CHUNK_BYTES)
+        st = _lib.FastqStream([(eb.start, eb.end) for eb in self.embedded_barcodes], self._mode == 'r', qualities)
+        pending = bytearray()
+        ends = []  # file ends inside `pending`
+        done = 0
+        try:
+            for name in self._files:
+                with _open_binary(name) as f:
+                    while True:
+                        data = f.read(chunk_bytes)
+                        if not data:
+                            break
+                        pending += data
+                        while len(pending) >= chunk_bytes:
+                            cut = pending.rfind(b'\n') + 1
+                            if cut <= 0:
+                                break  # no line ends yet: read on
+                            n, used, bad, parts = st.chunk(pending, cut, [e for e in ends if e < cut] + [cut],
+                                                           final=False)
+                            yield done, n, bad, parts
+                            if bad >= 0:
+                                return
+                            done += n
+                            del pending[:used]
+                            ends = [e - used for e in ends if e > used]
+                            if used == 0:
+                                break  # no complete record in the piece: read on
+                ends.append(len(pending))
+            n, _, bad, parts = st.chunk(pending, len(pending), ends or [0], final=True)
+            yield done, n, bad, parts
+        finally:
+            st.close()
+
     def _run(self, qualities=True):
-        blobs = [_read_bytes(f) for f in self._files]
-        ends = np.cumsum([len(b) for b in blobs], dtype=np.int64)
-        spans = [(eb.start, eb.end) for eb in self.embedded_barcodes]
-        return _lib.fastq_extract(b''.join(blobs), ends, spans, self._mode == 'r', qualities)
+        """All records at once (the batch form): (nrecords, first bad record or -1, per-span
+        arrays concatenated over the pieces)."""
+        total, first_bad, acc = 0, -1, None
+        for base, n, bad, parts in self._pieces(qualities):
+            if acc is None:
+                acc = [[[] for _ in range(4)] for _ in parts]
+            for k, tup in enumerate(parts):
+                for i, a in enumerate(tup):
+                    if a is not None:
+                        acc[k][i].append(a[: (bad if bad >= 0 else n)])
+            if bad >= 0:
+                return base + bad, base + bad, self._join(acc, qualities)
+            total = base + n
+        return total, first_bad, self._join(acc, qualities)
+
+    def _join(self, acc, qualities):
+        out = []
+        for k, eb in enumerate(self.embedded_barcodes):
+            w = eb.end - eb.start
+            lists = acc[k] if acc is not None else [[] for _ in range(4)]
+            cat = [np.concatenate(x) if x else None for x in lists]
+            seq = cat[0] if cat[0] is not None else np.zeros((0, w), np.uint8)
+            slen = cat[1] if cat[1] is not None else np.zeros(0, np.int32)
+            qual = (cat[2] if cat[2] is not None else np.zeros((0, w), np.uint8)) if qualities else None
+            qlen = (cat[3] if cat[3] is not None else np.zeros(0, np.int32)) if qualities else None
+            out.append((seq, slen, qual, qlen))
+        return out
 
     def extract_arrays(self, qualities=True):
         """Batch form: {sequence_tag: (rows 'S{w}', lengths), quality_tag: (...)} over every
@@ -96,21 +163,44 @@ class EmbeddedBarcodeGenerator:
         return out
 
     def __len__(self):
-        """reader.py:47-54 counts lines; fastq records = lines // 4 (the grouper's zip)."""
-        return self._run(False)[0]
+        """reader.py:47-54 iterates every record, so a bad name line raises there too
+        (fastq.py:35-36)."""
+        total = 0
+        for base, n, bad, _ in self._pieces(False):
+            if bad >= 0:
+                raise ValueError('fastq name must start with @')
+            total = base + n
+        return total
+
+    def iter_arrays(self, qualities=True, chunk_bytes=None):
+        """Streaming batch form: per piece of the files, the extract_arrays dict of that
+        piece's records (a billion-read stream never sits in host memory whole)."""
+        for base, n, bad, parts in self._pieces(qualities, chunk_bytes):
+            stop = n if bad < 0 else bad
+            out = {}
+            for eb, (seq, slen, qual, qlen) in zip(self.embedded_barcodes, parts):
+                w = eb.end - eb.start
+                out[eb.sequence_tag] = (np.ascontiguousarray(seq[:stop]).view('S%d' % w).reshape(stop) if w else
+                                        np.zeros(stop, dtype='S1'), slen[:stop].copy())
+                if qualities:
+                    out[eb.quality_tag] = (np.ascontiguousarray(qual[:stop]).view('S%d' % w).reshape(stop) if w else
+                                           np.zeros(stop, dtype='S1'), qlen[:stop].copy())
+            yield out
+            if bad >= 0:
+                raise ValueError('fastq name must start with @')
 
     def __iter__(self):
-        n, bad, parts = self._run(True)
         text = self._mode == 'r'
-        stop = n if bad < 0 else bad
-        for r in range(stop):
-            rec = []
-            for eb, (seq, slen, qual, qlen) in zip(self.embedded_barcodes, parts):
-                s = bytes(seq[r, :slen[r]])
-                q = bytes(qual[r, :qlen[r]])
-                if text:
-                    s, q = s.decode('ascii'), q.decode('ascii')
-                rec.extend(((eb.sequence_tag, s, 'Z'), (eb.quality_tag, q, 'Z')))
-            yield rec
-        if bad >= 0:                                                  # fastq.py:35-36
-            raise ValueError('fastq name must start with @')
+        for base, n, bad, parts in self._pieces(True):
+            stop = n if bad < 0 else bad
+            for r in range(stop):
+                rec = []
+                for eb, (seq, slen, qual, qlen) in zip(self.embedded_barcodes, parts):
+                    s = bytes(seq[r, :slen[r]])
+                    q = bytes(qual[r, :qlen[r]])
+                    if text:
+                        s, q = s.decode('ascii'), q.decode('ascii')
+                    rec.extend(((eb.sequence_tag, s, 'Z'), (eb.quality_tag, q, 'Z')))
+                yield rec
+            if bad >= 0:                                                  # fastq.py:35-36
+                raise ValueError('fastq name must start with @')

@@ -125,3 +125,97 @@ def test_fastq_synthetic_large_text_vs_python(tmp_path):
             rows, lens = arr[tag]
             assert lens.tolist() == [len(w) for w in want]
             assert [bytes(x) for x in rows] == want, (mode, tag)  # 'S' rows: NUL padding dropped
+
+
+# ---------------------------------------------------------------- streaming (pieces)
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [7, 64, 333])
+def test_fastq_golden_cases_in_small_pieces(fq_golden, tmp_path, monkeypatch, chunk):
+    """The files read lazily in tiny pieces (records and CRLF lines cut by piece ends, pieces
+    spanning file boundaries): the same records and errors as the reference."""
+    monkeypatch.setattr(fastq, "CHUNK_BYTES", chunk)
+    test_fastq_golden_cases(fq_golden, tmp_path)
+
+
+@pytest.mark.gpu
+def test_fastq_len_raises_on_bad_name(fq_golden, tmp_path):
+    case = next(c for c in fq_golden["cases"] if "error" in c)
+    gen = fastq.EmbeddedBarcodeGenerator(_ebs(fq_golden, case["tags"]), _paths(case, tmp_path), case["mode"])
+    with pytest.raises(ValueError) as ei:
+        len(gen)
+    assert str(ei.value) == "fastq name must start with @"
+
+
+@pytest.mark.gpu
+def test_fastq_multifile_stream_vs_python(tmp_path):
+    """Three files (records spanning the file boundaries, the last file unterminated), read
+    in 1 MB pieces and as one piece: identical arrays, equal to a plain Python reading of
+    the concatenated lines; iter_arrays' pieces concatenate to the same."""
+    rng = np.random.default_rng(9)
+    lines = []
+    for r in range(60_000):
+        L = int(rng.integers(10, 60))
+        seq = bytes(rng.choice(list(b"ACGTN"), size=L).tolist())
+        lines += [b"@q%d\n" % r, seq + b"\n", b"+\n", bytes([65 + r % 20] * L) + b"\n"]
+    blob = b"".join(lines)
+    cuts = [len(blob) // 3 + 5, 2 * len(blob) // 3 + 11]
+    parts = [blob[:cuts[0]], blob[cuts[0]:cuts[1]], blob[cuts[1]:-1]]  # the last without '\n'
+    paths = []
+    for k, part in enumerate(parts):
+        p = tmp_path / ("s%d.fastq" % k)
+        p.write_bytes(part)
+        paths.append(str(p))
+    eb = [platform.TenXV2.cell_barcode, platform.TenXV2.molecule_barcode]
+    py_lines = []
+    for p in paths:
+        with open(p, "rb") as f:
+            py_lines += f.readlines()
+    seqs, quals = py_lines[1::4], py_lines[3::4]
+    n = len(py_lines) // 4
+    gen = fastq.EmbeddedBarcodeGenerator(eb, paths, "rb")
+    whole = gen.extract_arrays()
+    fastq_chunk = fastq.CHUNK_BYTES
+    try:
+        fastq.CHUNK_BYTES = 1 << 20
+        small = gen.extract_arrays()
+        assert len(gen) == n
+        pieces = list(gen.iter_arrays())
+    finally:
+        fastq.CHUNK_BYTES = fastq_chunk
+    assert len(pieces) > 3
+    for tag, (s, e), src in (("CR", (0, 16), seqs), ("UY", (16, 24), quals)):
+        want = [x[s:e] for x in src[:n]]
+        for arr in (whole, small):
+            rows, lens = arr[tag]
+            assert rows.shape[0] == n and lens.tolist() == [len(w) for w in want]
+            assert [bytes(x) for x in rows] == want
+        cat = np.concatenate([p[tag][0] for p in pieces])
+        assert cat.tolist() == whole[tag][0].tolist()
+
+
+# ---------------------------------------------------------------- whitelist ingest
+@pytest.mark.gpu
+def test_whitelist_lines_on_device_vs_python(tmp_path):
+    """from_whitelist's device line split + [:-1] chop + encode against Python's own line
+    iteration of the same file (barcode.py:96-97), with ragged and empty lines and no final
+    newline; a 737,280-line whitelist file as well."""
+    from oracle import oracle as O
+    from sctools_amd import barcode, synthetic
+    rng = np.random.default_rng(12)
+    lines = [bytes(rng.choice(list(b"ACGTacgt"), size=int(rng.integers(1, 40))).tolist()) + b"\n"
+             for _ in range(5000)]
+    lines[10] = b"\n"
+    lines[4999] = lines[4999][:-1]
+    p = tmp_path / "wl.txt"
+    p.write_bytes(b"".join(lines))
+    b = barcode.Barcodes.from_whitelist(str(p), 16)
+    with open(p, "rb") as f:
+        want = [O.two_bit_encode(ln[:-1]) for ln in f]
+    from collections import Counter
+    assert list(b) == list(Counter(want)) and [b[k] for k in b] == list(Counter(want).values())
+    n, L, seed = synthetic.CONFIGS[2]
+    codes = synthetic.whitelist_codes(n, L, seed)
+    p2 = tmp_path / "737k.txt"
+    p2.write_bytes(b"".join(r.tobytes() + b"\n" for r in synthetic.decode_ascii(codes, L)))
+    big = barcode.PriorBarcodeSet.from_whitelist(str(p2), L)
+    assert np.array_equal(big.codes_array(), codes)
