@@ -157,9 +157,9 @@ def test_fastq_multifile_stream_vs_python(tmp_path):
         L = int(rng.integers(10, 60))
         seq = bytes(rng.choice(list(b"ACGTN"), size=L).tolist())
         lines += [b"@q%d\n" % r, seq + b"\n", b"+\n", bytes([65 + r % 20] * L) + b"\n"]
-    blob = b"".join(lines)
-    cuts = [len(blob) // 3 + 5, 2 * len(blob) // 3 + 11]
-    parts = [blob[:cuts[0]], blob[cuts[0]:cuts[1]], blob[cuts[1]:-1]]  # the last without '\n'
+    # files cut between lines 2 and 3 / 1 and 2 of a record: records span the file ends
+    c0, c1 = 4 * 20_000 + 2, 4 * 41_000 + 1
+    parts = [b"".join(lines[:c0]), b"".join(lines[c0:c1]), b"".join(lines[c1:])[:-1]]  # last: no '\n'
     paths = []
     for k, part in enumerate(parts):
         p = tmp_path / ("s%d.fastq" % k)
