@@ -27,6 +27,8 @@ struct State {
   bool mfma = true;              // int8 seeds: first 6 butterfly levels on the matrix cores
   uint16_t* d_order = nullptr;   // [2^17]: at [L, 2L) the offsets [0, L) sorted by digit weight
   int tile_wgs = 2;              // resident MFMA-tile workgroups per CU
+  int tile_reg = 0;              // int8 seeds: the register-resident tile (one wave per slice), variant
+  int tile_reg_wgs = 2;          // its resident workgroups per CU
   void* d_buf = nullptr;         // chunk slices x 2^14 seed values
   int64_t chunk = 0;             // slices per pass
   int grid = 0;                  // compute units (the tile kernel's persistent grid)

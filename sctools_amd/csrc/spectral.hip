@@ -16,6 +16,8 @@
 //          F^2 binned by digit weight; writes nothing
 // 8 GB of HBM traffic per job at int8, whatever n is.  Exact: |F| <= n < 2^31 in int32,
 // F^2 and S_w in uint64 (S_w <= 2^32 sum f^2).
+#include <string.h>
+
 #include <algorithm>
 #include <vector>
 #include <type_traits>
@@ -843,7 +845,9 @@ __device__ __forceinline__ int lds_e2(int e) {
   return lo4 | (mid4 << 4) | ((e >> 8) << 8);
 }
 
-template <bool PF, int STAGGER = 0>
+// ABL (ablation builds only, wrong results by design): 1 = no global loads, 2 = no squares,
+// 3 = no LDS exchange, 4 = no stage-2 MFMAs, 5 = no barriers
+template <bool PF, int STAGGER = 0, int ABL = 0>
 __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, const uint16_t* __restrict__ order,
                                                 int z0, int nslices, unsigned long long* __restrict__ counts,
                                                 unsigned long long add_n) {
@@ -890,6 +894,11 @@ __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, 
     for (int k = 0; k < ph; ++k) __builtin_amdgcn_s_sleep(STAGGER);
   }
   auto load = [&](int sl, v2l_t* dst) {
+    if constexpr (ABL == 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = v2l_t{(long)(sl * 0x9E3779B97F4A7C15ull + j), (long)tid};
+      return;
+    }
     const int8_t* row = buf + (int64_t)sl * kLo;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -939,7 +948,8 @@ __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, 
       x[32 + r] = ab0 - cd0;
       x[48 + r] = ab1 - cd1;
     }
-    __syncthreads();  // the previous slice's stage-2 reads are done
+    if constexpr (ABL != 3) {
+    if constexpr (ABL != 5) __syncthreads();  // the previous slice's stage-2 reads are done
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -947,7 +957,8 @@ __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, 
 #pragma unroll
         for (int i = 0; i < 4; ++i)  // the offset is XOR-linear in e: wbase ^ lds_e2(i | q << 8 | j << 12)
           lds[wbase ^ lds_e2(i | (q << 8) | (j << 12))] = (int16_t)x[j * 16 + q * 4 + i];
-    __syncthreads();
+    if constexpr (ABL != 5) __syncthreads();
+    }
     const int wz = digit_weight((uint32_t)(z0 + s));  // workgroup-uniform
     if (wz != cur_w) {
       if (cur_w >= 0) flush();
@@ -957,8 +968,14 @@ __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, 
     for (int g = 0; g < 4; ++g) {
       const int base = rbase ^ lds_e2(g << 8);
       // base already carries the bit-7 swizzle (lds_e2 of e with bits 4..7 = 0)
-      const uint4 h0 = *reinterpret_cast<const uint4*>(lds + base);        // bits 4..6, bit 7 = 0
-      const uint4 h1 = *reinterpret_cast<const uint4*>(lds + (base ^ 8));  // bit 7 = 1
+      uint4 h0, h1;
+      if constexpr (ABL == 3) {
+        h0 = make_uint4(x[16 * g], x[16 * g + 1], x[16 * g + 2], x[16 * g + 3]);
+        h1 = make_uint4(x[16 * g + 4], x[16 * g + 5], x[16 * g + 6], x[16 * g + 7]);
+      } else {
+        h0 = *reinterpret_cast<const uint4*>(lds + base);        // bits 4..6, bit 7 = 0
+        h1 = *reinterpret_cast<const uint4*>(lds + (base ^ 8));  // bit 7 = 1
+      }
       const uint32_t d[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
       uint32_t lo[4], hi[4];
 #pragma unroll
@@ -969,6 +986,11 @@ __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, 
       const v2l_t Bl = v2l_t{(long)(((uint64_t)lo[1] << 32) | lo[0]), (long)(((uint64_t)lo[3] << 32) | lo[2])};
       const v2l_t Bh = v2l_t{(long)(((uint64_t)hi[1] << 32) | hi[0]), (long)(((uint64_t)hi[3] << 32) | hi[2])};
       v4i_t c[4];  // the four quarters' high-byte products first: independent MFMAs
+      if constexpr (ABL == 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          c[q] = v4i_t{(int)lo[q], (int)hi[q], (int)(lo[q] ^ hi[(q + 1) & 3]), (int)(hi[q] + lo[(q + 2) & 3])};
+      } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q) c[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[q], Bh, v4i_t{0, 0, 0, 0}, 0, 0, 0);
 #pragma unroll
@@ -977,12 +999,20 @@ __device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, 
         for (int i = 0; i < 4; ++i) c[q][i] <<= 8;
         c[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[q], Bl, c[q], 0, 0, 0);
       }
+      }
+      if constexpr (ABL == 2) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) tot[i] ^= (unsigned)c[q][i];
+      } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           tot[digit_weight_c((uint32_t)i) + digit_weight_c((uint32_t)g) + digit_weight_c((uint32_t)q)] +=
               (unsigned long long)((int64_t)c[q][i] * c[q][i]);
+      }
     }
   }
   if (cur_w >= 0) flush();
@@ -1002,10 +1032,189 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
     unsigned long long* __restrict__ counts, unsigned long long add_n) {
   tile_mfma2_body<true, STAGGER>(buf, order, z0, nslices, counts, add_n);
 }
+template <int ABL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_mfma2_pf_abl_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_mfma2_body<true, 0, ABL>(buf, order, z0, nslices, counts, add_n);
+}
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_mfma2_pf_kernel(
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
     unsigned long long* __restrict__ counts, unsigned long long add_n) {
   tile_mfma2_body<true>(buf, order, z0, nslices, counts, add_n);
+}
+
+// ---------------------------------------------------------------- register-resident tile
+// One WAVE transforms one whole slice with no LDS exchange and no barrier.  Column bits:
+// P = 0..5 (digits 0-2), Q = 6..11 (digits 3-5), R = 12, 13 (digit 6).  Lane l's 16-B load
+// (plane R, load mt) holds columns 16 (l >> 4) + 64 (l & 15) + 1024 mt + 4096 R + j: a wave
+// reads each kilobyte of the slice whole.
+//   stage 1 (per plane R): the bytes are the A operand of v_mfma_i32_16x16x64_i8 as loaded
+//     (A[m = Q bits 0..3 = l & 15][k = P = 16 (l >> 4) + j]) against B = a quarter qn of H_64:
+//     C1[m][n] = sum_P D * H -> transformed P' (n = P' bits 0..3 = l & 15, qn = bits 4, 5),
+//     output rows m = 4 (l >> 4) + i.  So lane l holds Q bits 0, 1 = i, 2, 3 = l >> 4 and,
+//     over the 4 loads, Q bits 4, 5 = mt: 16 values that ARE stage 2's B operand (k = 16 (l >> 4)
+//     + 4 mt + i, a relabeling of whole Q digits), packed into bytes in registers.
+//   stage 2: H_64 over Q (A = the same H quarters) as the two-byte split of tile_mfma2
+//     (y = v + 128 = 256 h + l', v = 256 h + (l' - 128), two i8 MFMAs, the first shifted into
+//     the second's accumulator); outputs Q' rows 16 q2 + 4 (l >> 4) + i2: whole digits.
+//   R (one base digit) by Parseval instead of a butterfly: with G_R = the 12-bit transform of
+//     plane R and F(R') = sum_R (-1)^<R, R'> G_R,  F(0) = transform of sum_R D_R = sum_R C1_R
+//     (added after stage 1) and sum_{R' != 0} F(R')^2 = 4 sum_R G_R^2 - F(0)^2.  So every
+//     (P', Q') adds F(0)^2 to weight w and 4 sum G_R^2 - F(0)^2 to weight w + 1: five stage-2
+//     transforms per slice (4 planes + the sum), no exchange between planes.
+// Weight of (P', Q', R'): digits of l & 3, (l >> 2) & 3, l >> 4 (thread constant) + qn + q2
+// + i2 (compile time) + the slice's + [R' != 0].
+template <bool PF, int ABL = 0>
+__device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, const uint16_t* __restrict__ order,
+                                              int z0, int nslices, unsigned long long* __restrict__ counts,
+                                              unsigned long long add_n) {
+  __shared__ unsigned long long bins[17];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 17) bins[tid] = 0;
+  __syncthreads();
+  v2l_t H[4];  // H_64 rows 16 q + (l & 15), columns 16 (l >> 4) + j: stage 1's B and stage 2's A
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * q + (lane & 15), col = 16 * (lane >> 4) + 4 * d + r;
+        v |= ((__popc(row & col) & 1) ? 0xFFu : 0x01u) << (8 * r);
+      }
+      w[d] = v;
+    }
+    H[q] = v2l_t{(long)(((uint64_t)w[1] << 32) | w[0]), (long)(((uint64_t)w[3] << 32) | w[2])};
+  }
+  const int wt_thread = digit_weight((uint32_t)(lane & 15)) + digit_weight((uint32_t)(lane >> 4));
+  const int lane_off = 16 * (lane >> 4) + 64 * (lane & 15);
+  // each wave of the grid takes a contiguous run of slice positions
+  const int gw = blockIdx.x * 4 + wave, GW = gridDim.x * 4;
+  const int ub = (int)((int64_t)nslices * gw / GW), ue = (int)((int64_t)nslices * (gw + 1) / GW);
+  unsigned long long accA[4] = {0, 0, 0, 0}, accB[4] = {0, 0, 0, 0};
+  int cur_w = -1;
+  auto flush = [&]() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (accA[k]) atomicAdd(&bins[cur_w + wt_thread + k], accA[k]);
+      const unsigned long long b = 4 * accB[k] - accA[k];
+      if (b) atomicAdd(&bins[cur_w + wt_thread + k + 1], b);
+      accA[k] = 0;
+      accB[k] = 0;
+    }
+  };
+  auto load_plane = [&](int sl, int R, v2l_t* dst) {
+    const int8_t* p = buf + (int64_t)sl * kLo + lane_off + 4096 * R;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) dst[mt] = __builtin_nontemporal_load(reinterpret_cast<const v2l_t*>(p + 1024 * mt));
+  };
+  // stage 2 of 16 values per lane (c1[mt][i] = v + 128 of stage 1, one quarter qn) -> squares
+  auto stage2 = [&](const v4i_t* c1, auto qn_c, unsigned long long* acc) {
+    constexpr int qn = decltype(qn_c)::value;
+    uint32_t lo[4], hi[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const uint32_t t1 = __builtin_amdgcn_perm((uint32_t)c1[mt][1], (uint32_t)c1[mt][0], 0x05010400u);
+      const uint32_t t2 = __builtin_amdgcn_perm((uint32_t)c1[mt][3], (uint32_t)c1[mt][2], 0x05010400u);
+      lo[mt] = __builtin_amdgcn_perm(t2, t1, 0x05040100u) ^ 0x80808080u;
+      hi[mt] = __builtin_amdgcn_perm(t2, t1, 0x07060302u);
+    }
+    const v2l_t Bl = v2l_t{(long)(((uint64_t)lo[1] << 32) | lo[0]), (long)(((uint64_t)lo[3] << 32) | lo[2])};
+    const v2l_t Bh = v2l_t{(long)(((uint64_t)hi[1] << 32) | hi[0]), (long)(((uint64_t)hi[3] << 32) | hi[2])};
+    v4i_t c[4];
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2) c[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bh, v4i_t{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) c[q2][i] <<= 8;
+      c[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bl, c[q2], 0, 0, 0);
+    }
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        constexpr int dummy = 0;
+        (void)dummy;
+        if constexpr (ABL == 2)
+          acc[0] ^= (unsigned)c[q2][i];
+        else
+          acc[digit_weight_c((uint32_t)qn) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
+              (unsigned long long)((int64_t)c[q2][i] * c[q2][i]);
+      }
+  };
+  // planes in turn (a runtime loop: one plane's 16 VGPRs of bytes live at a time, PF: the
+  // next plane's loads in flight), the per-plane sums of all four quarters carried across
+  for (int u = ub; u < ue; ++u) {
+    const int s = order ? (int)order[u] : u;
+    const int wz = digit_weight((uint32_t)(z0 + s));  // wave-uniform
+    if (wz != cur_w) {
+      if (cur_w >= 0) flush();
+      cur_w = wz;
+    }
+    v4i_t cs[4][4];  // [qn][mt]: sum over the planes of v + 128, from -384 (-> sum v + 128)
+#pragma unroll
+    for (int qn = 0; qn < 4; ++qn)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) cs[qn][mt] = v4i_t{-384, -384, -384, -384};
+    v2l_t dn[4];
+    if constexpr (PF) load_plane(s, 0, dn);
+#pragma unroll 1
+    for (int R = 0; R < 4; ++R) {
+      v2l_t d[4];
+      if constexpr (PF) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) d[mt] = dn[mt];
+        if (R < 3) load_plane(s, R + 1, dn);
+      } else {
+        load_plane(s, R, d);
+      }
+      auto quarter = [&](auto qn_c) {
+        constexpr int qn = decltype(qn_c)::value;
+        v4i_t c1[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          c1[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qn], v4i_t{128, 128, 128, 128}, 0, 0, 0);
+          cs[qn][mt] += c1[mt];
+        }
+        stage2(c1, qn_c, accB);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      quarter(std::integral_constant<int, 0>());
+      quarter(std::integral_constant<int, 1>());
+      quarter(std::integral_constant<int, 2>());
+      quarter(std::integral_constant<int, 3>());
+    }
+    stage2(cs[0], std::integral_constant<int, 0>(), accA);
+    stage2(cs[1], std::integral_constant<int, 1>(), accA);
+    stage2(cs[2], std::integral_constant<int, 2>(), accA);
+    stage2(cs[3], std::integral_constant<int, 3>(), accA);
+  }
+  if (cur_w >= 0) flush();
+  __syncthreads();
+  if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
+  if (add_n && blockIdx.x == 0 && tid == 0) atomicAdd(counts, add_n);  // n, once per job
+}
+
+// 2 waves per SIMD, the next plane prefetched (195 VGPRs, no spill)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<true>(buf, order, z0, nslices, counts, add_n);
+}
+// A/B: 2 waves per SIMD without the prefetch; 3 waves per SIMD (a few registers spilled)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_np_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<false>(buf, order, z0, nslices, counts, add_n);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_reg_w3_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<false>(buf, order, z0, nslices, counts, add_n);
 }
 
 __global__ void max_column_kernel(const uint32_t* __restrict__ cnt, unsigned* __restrict__ out) {
@@ -1019,7 +1228,9 @@ template <typename T>
 int launch_seed(State& st, int z0, int z1, hipStream_t s) {
   T* buf = reinterpret_cast<T*>(st.d_buf);
   const int walks = (z1 - (z0 & ~(kWalk - 1)) + kWalk - 1) / kWalk;
-  int per_wg = kSeedWalks;
+  // 16 walks per workgroup for a full chunk (measured best at 65,536 slices); smaller chunks
+  // keep >= 64 workgroup rows so the grid still fills the chip
+  int per_wg = std::max(1, std::min(kSeedWalks, walks / 64));
 #ifdef SCT_ABLATION
   if (const char* e = getenv("SCT_SEED_WALKS")) per_wg = std::max(1, atoi(e));
 #endif
@@ -1089,13 +1300,18 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
       const dim3 mgrid((unsigned)std::min(st.grid * st.tile_wgs, z1 - z0));
 #ifdef SCT_ABLATION
       static const int mabl = getenv("SCT_SPECTRAL_ABL") ? atoi(getenv("SCT_SPECTRAL_ABL")) : 0;
-      if (mabl >= 11 && mabl <= 21) {
+      if ((mabl >= 11 && mabl <= 21) || (mabl >= 31 && mabl <= 35)) {
         if (mabl == 11) hipLaunchKernelGGL(tile_mfma_kernel<1>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 12) hipLaunchKernelGGL(tile_mfma_kernel<2>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 13) hipLaunchKernelGGL(tile_mfma_kernel<3>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 14) hipLaunchKernelGGL(tile_mfma_kernel<4>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 15) hipLaunchKernelGGL(tile_mfma_kernel<5>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
         if (mabl == 20) hipLaunchKernelGGL(tile_mfma2_pf_st_kernel<20>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
+        if (mabl == 31) hipLaunchKernelGGL(tile_mfma2_pf_abl_kernel<1>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
+        if (mabl == 32) hipLaunchKernelGGL(tile_mfma2_pf_abl_kernel<2>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
+        if (mabl == 33) hipLaunchKernelGGL(tile_mfma2_pf_abl_kernel<3>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
+        if (mabl == 34) hipLaunchKernelGGL(tile_mfma2_pf_abl_kernel<4>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
+        if (mabl == 35) hipLaunchKernelGGL(tile_mfma2_pf_abl_kernel<5>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
         if (mabl == 21) hipLaunchKernelGGL(tile_mfma2_pf_st_kernel<40>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
         if (mabl == 17 || mabl == 19) {  // two-stage without prefetch / the one-stage kernel
           int per_cu = 0;
@@ -1110,7 +1326,17 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
         return SCT_OK;
       }
 #endif
-      hipLaunchKernelGGL(tile_mfma2_pf_kernel, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+      if (st.tile_reg) {
+        const dim3 rgrid((unsigned)std::max(1, std::min(st.grid * st.tile_reg_wgs, (z1 - z0 + 3) / 4)));
+        if (st.tile_reg == 2)
+          hipLaunchKernelGGL(tile_reg_np_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+        else if (st.tile_reg == 3)
+          hipLaunchKernelGGL(tile_reg_w3_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+        else
+          hipLaunchKernelGGL(tile_reg_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+      } else {
+        hipLaunchKernelGGL(tile_mfma2_pf_kernel, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+      }
       SCT_LAUNCH_CHECK();
       return SCT_OK;
     }
@@ -1189,6 +1415,14 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
         per_cu <= 0)
       per_cu = 2;
     st.tile_wgs = per_cu;
+    const char* tv = getenv("SCT_SPECTRAL_TILE");  // A/B: reg / reg_np / reg_w3 = the register-resident tile
+    st.tile_reg = !tv ? 0 : !strcmp(tv, "reg") ? 1 : !strcmp(tv, "reg_np") ? 2 : !strcmp(tv, "reg_w3") ? 3 : 0;
+    int per_cu_reg = 0;  // its resident workgroups per CU
+    const void* kf = st.tile_reg == 2 ? (const void*)tile_reg_np_kernel
+                     : st.tile_reg == 3 ? (const void*)tile_reg_w3_kernel : (const void*)tile_reg_kernel;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_reg, kf, 256, 0) != hipSuccess || per_cu_reg <= 0)
+      per_cu_reg = 2;
+    st.tile_reg_wgs = per_cu_reg;
   }
   {
     // for every power of two L <= 2^16: the offsets [0, L) sorted by digit weight, stored
