@@ -29,6 +29,7 @@ struct State {
   int tile_wgs = 2;              // resident MFMA-tile workgroups per CU
   int tile_reg = 0;              // int8 seeds: the register-resident tile (one wave per slice), variant
   int tile_reg_wgs = 2;          // its resident workgroups per CU
+  bool seed_spread = false;      // int8 seeds: stores spread over the walk (16-slice blocks)
   void* d_buf = nullptr;         // chunk slices x 2^14 seed values
   int64_t chunk = 0;             // slices per pass
   int grid = 0;                  // compute units (the tile kernel's persistent grid)

@@ -505,6 +505,118 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
   }
 }
 
+// int8 seeds, stores spread over the walk: the 64-slice Gray walk is cut into four 16-slice
+// blocks (the Gray order keeps each block's slices contiguous: steps 16 b .. 16 b + 15 visit
+// slices 16 gray(b) + 0..15), and each block is staged through one of two 4-KiB LDS buffers
+// (row = slice, byte = column) and stored at once, so a workgroup's HBM writes are spread
+// over its walk instead of bunched after it, and 16 running sums (not 64) stay in registers.
+// One barrier per block (double buffer).  The walk itself is seed_body's.
+template <int kRegG>
+__device__ __forceinline__ void seed_spread_body(const uint32_t* __restrict__ planes, const uint32_t* __restrict__ gofs,
+                                                 const uint32_t* __restrict__ off, int64_t max_groups, int z0, int z1,
+                                                 int8_t* __restrict__ buf) {
+  constexpr int NT = 256, kB = 16;  // threads (= columns), slices per block
+  __shared__ uint32_t stage[2][kB * NT / 4];
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.x * NT, c = c0 + tid;
+  const uint32_t g0 = gofs[c];
+  const int ng = (int)(gofs[c + 1] - g0);
+  int wng = ng;
+#pragma unroll
+  for (int s = 32; s; s >>= 1) wng = max(wng, __shfl_xor(wng, s));
+  uint32_t pr[kRegG][kHiBits];
+#pragma unroll
+  for (int g = 0; g < kRegG; ++g)
+#pragma unroll
+    for (int k = 0; k < kHiBits; ++k) pr[g][k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
+  // store-out: this thread writes row tid / 16 of a block, columns c0 + mcb .. + 15
+  const int mcb = (tid % (NT / 16)) * 16, srow = tid / (NT / 16);
+  uint4 mx;
+  {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      w[k] = 0x80808080u;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int cc = c0 + mcb + 4 * k + b;
+        w[k] |= (off[cc + 1] - off[cc]) << (8 * b);
+      }
+    }
+    mx = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  const int za = z0 & ~(kWalk - 1);
+  const int nwalks = (z1 - za + kWalk - 1) / kWalk;
+  for (int wk = blockIdx.y; wk < nwalks; wk += gridDim.y) {
+    const int zblk = za + wk * kWalk;
+    uint32_t x[kRegG];  // each register group's XOR state, carried from block to block
+#pragma unroll
+    for (int g = 0; g < kRegG; ++g) {
+      x[g] = 0;
+#pragma unroll
+      for (int k = kWalkBits; k < kHiBits; ++k)
+        if ((zblk >> k) & 1) x[g] ^= pr[g][k];
+    }
+    auto block = [&](auto b_c) {
+      constexpr int b = decltype(b_c)::value;
+      constexpr int base = kB * gray(b);  // this block's first slice in the walk
+      int acc[kB];
+      // group 0 (every column; a column without codes has planes 0)
+#pragma unroll
+      for (int i = kB * b; i < kB * (b + 1); ++i) {
+        if (i > 0) x[0] ^= pr[0][ctz_c(i)];
+        acc[gray(i) - base] = __popc(x[0]);
+      }
+#pragma unroll
+      for (int g = 1; g < kRegG; ++g) {
+        if (g < wng) {
+#pragma unroll
+          for (int i = kB * b; i < kB * (b + 1); ++i) {
+            if (i > 0) x[g] ^= pr[g][ctz_c(i)];
+            acc[gray(i) - base] += __popc(x[g]);
+          }
+        }
+      }
+      for (int g = kRegG; g < wng; ++g) {  // dense columns: the rest from L2, state rebuilt
+        uint32_t p[kHiBits];
+#pragma unroll
+        for (int k = 0; k < kHiBits; ++k) p[k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
+        uint32_t y = 0;
+        const int zs = zblk + gray(kB * b);  // the slice of the block's first step
+#pragma unroll
+        for (int k = 0; k < kHiBits; ++k)
+          if ((zs >> k) & 1) y ^= p[k];
+#pragma unroll
+        for (int i = kB * b; i < kB * (b + 1); ++i) {
+          if (i > kB * b) y ^= p[ctz_c(i)];
+          acc[gray(i) - base] += __popc(y);
+        }
+      }
+      uint8_t* st8 = reinterpret_cast<uint8_t*>(stage[b & 1]);
+#pragma unroll
+      for (int j = 0; j < kB; ++j) st8[j * NT + tid] = (uint8_t)acc[j];
+      __syncthreads();  // (buffer b & 1 was last read two blocks ago, before the previous barrier)
+      const uint4 v = *reinterpret_cast<const uint4*>(st8 + srow * NT + mcb);
+      // m - 2 acc per byte as ((m | 0x80) - 2 acc) ^ 0x80 (acc <= m <= 127: no carries)
+      const uint4 o = make_uint4((mx.x - (v.x + v.x)) ^ 0x80808080u, (mx.y - (v.y + v.y)) ^ 0x80808080u,
+                                 (mx.z - (v.z + v.z)) ^ 0x80808080u, (mx.w - (v.w + v.w)) ^ 0x80808080u);
+      const int z = zblk + base + srow;
+      if (z >= z0 && z < z1) *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + c0 + mcb) = o;
+    };
+    block(std::integral_constant<int, 0>());
+    block(std::integral_constant<int, 1>());
+    block(std::integral_constant<int, 2>());
+    block(std::integral_constant<int, 3>());
+  }
+}
+
+__global__ __launch_bounds__(256) void seed_spread_kernel(const uint32_t* __restrict__ planes,
+                                                          const uint32_t* __restrict__ gofs,
+                                                          const uint32_t* __restrict__ off, int64_t max_groups,
+                                                          int z0, int z1, int8_t* __restrict__ buf) {
+  seed_spread_body<kRegGroups>(planes, gofs, off, max_groups, z0, z1, buf);
+}
+
 template <typename T, int ABL = 0>
 __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ planes,
                                                    const uint32_t* __restrict__ gofs,
@@ -1269,8 +1381,14 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
                        st.max_groups, z0, z1, buf);
   if (sabl < 1 || sabl > 10)
 #endif
-    hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, st.max_groups,
-                       z0, z1, buf);
+  {
+    if (sizeof(T) == 1 && st.seed_spread)
+      hipLaunchKernelGGL(seed_spread_kernel, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                         st.max_groups, z0, z1, reinterpret_cast<int8_t*>(buf));
+    else
+      hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, st.max_groups,
+                         z0, z1, buf);
+  }
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
@@ -1415,6 +1533,8 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
         per_cu <= 0)
       per_cu = 2;
     st.tile_wgs = per_cu;
+    const char* sv = getenv("SCT_SPECTRAL_SEED");  // A/B: "spread" = stores spread over the walk
+    st.seed_spread = sv && !strcmp(sv, "spread");
     const char* tv = getenv("SCT_SPECTRAL_TILE");  // A/B: reg / reg_np / reg_w3 = the register-resident tile
     st.tile_reg = !tv ? 0 : !strcmp(tv, "reg") ? 1 : !strcmp(tv, "reg_np") ? 2 : !strcmp(tv, "reg_w3") ? 3 : 0;
     int per_cu_reg = 0;  // its resident workgroups per CU
