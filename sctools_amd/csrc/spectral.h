@@ -30,6 +30,12 @@ struct State {
   int tile_reg = 0;              // int8 seeds: the register-resident tile (one wave per slice), variant
   int tile_reg_wgs = 2;          // its resident workgroups per CU
   bool seed_spread = false;      // int8 seeds: stores spread over the walk (16-slice blocks)
+  void* d_mx = nullptr;          // int8 seeds: the MFMA seed's operand tables (null: the walk seed)
+  // seed / tile overlap: chunk j+1's seed (side stream, second buffer) runs beside chunk j's tile
+  bool overlap = false;
+  void* d_buf2 = nullptr;
+  hipStream_t side = nullptr;
+  hipEvent_t ev[5] = {};         // [0, 1] tile done with buffer 0 / 1, [2, 3] seed done, [4] start
   void* d_buf = nullptr;         // chunk slices x 2^14 seed values
   int64_t chunk = 0;             // slices per pass
   int grid = 0;                  // compute units (the tile kernel's persistent grid)

@@ -1329,12 +1329,215 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   tile_reg_body<false>(buf, order, z0, nslices, counts, add_n);
 }
 
+// ---------------------------------------------------------------- MFMA seed (int8 seeds)
+// The seed as a product of two +-1 matrices.  Split the slice z = (r: bits 8..17, zm: bits
+// 4..7, zn: bits 0..3) and each code's hi_k = code >> 14 the same way (r_k, x_k, y_k):
+//   D_z(c) = sum_k (-1)^(r.r_k) (-1)^(zm.x_k) (-1)^(zn.y_k) = sum_k A_r[zm][k] B[k][zn],
+//   A_r[zm][k] = s_k(r) (-1)^(zm.x_k),  B[k][zn] = (-1)^(zn.y_k),  s_k(r) = (-1)^(r.r_k),
+// so one v_mfma_i32_16x16x64_i8 gives a column's 256 slices (zm, zn) of one r from 64
+// codes.  A wave owns 16 consecutive columns; lane l's results are always the slices
+// (zm = 4 (l >> 4) + i, zn = l & 15), i = 0..3, whatever the column, so after the 16
+// columns' products each lane packs 4 slices x 16 columns into four 16-B chunks -- no
+// cross-lane transpose.  The chunks go through a 64-KB LDS stage so that the stores cover
+// whole 128-column lines (stored straight, 64 lanes hit 64 slices: 2x slower).  r runs a Gray walk: one bit b flips per step, and
+// A_r ^= PM_b (0xFE in the bytes of the codes with bit b of r_k set: +1 <-> -1 in int8).
+// The operands (A_0, B, PM per 64-code block) are built once per plan by seed_ops_kernel.
+// A column with 65..127 codes adds a second product for its codes 64.., whose A is rebuilt
+// from the table at every step (rare: a handful of columns at the headline sizes).
+// Per step and wave: 16 MFMAs for 4,096 values, 64 XORs, 48 byte packs, 4 LDS writes, 4 LDS
+// reads, 4 stores; one barrier per step.
+constexpr int kMxRBits = kHiBits - 8;  // r: the walked slice bits
+constexpr int kMxKB = 2;               // 64-code blocks per column (int8: <= 127 codes)
+constexpr int kMxCols = 16;            // columns per wave (one 16-B chunk per slice)
+constexpr int kMxSegBits = 5;          // r values per walk segment = 32
+
+// table layouts: a 16-column block's entries side by side (one base address, immediate offsets)
+__device__ __forceinline__ size_t mx_op(int c, int kb, int lane) {
+  return ((((size_t)(c >> 4) * kMxKB + kb) * 64 + lane) << 4) + (c & 15);
+}
+__device__ __forceinline__ size_t mx_pm(int c, int kb, int b, int g) {
+  return (((((size_t)(c >> 4) * kMxKB + kb) * kMxRBits + b) * 4 + g) << 4) + (c & 15);
+}
+
+__device__ __forceinline__ v2l_t pack_v2l(const uint32_t* w) {
+  return v2l_t{(long)(((uint64_t)w[1] << 32) | w[0]), (long)(((uint64_t)w[3] << 32) | w[2])};
+}
+
+// One thread per (column, 64-code block, lane): the lane's 16 bytes of A_0 and B in the
+// MFMA operand layout (byte j = code 64 kb + 16 (l >> 4) + j; rows / columns zm = zn =
+// l & 15; 0 past the column's codes), and for lanes 0, 16, 32, 48 the sign planes PM_b of
+// their 16 codes.
+__global__ __launch_bounds__(256) void seed_ops_kernel(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ off,
+                                                       v2l_t* __restrict__ opa, v2l_t* __restrict__ opb,
+                                                       v2l_t* __restrict__ opm) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int lane = t & 63, kb = (t >> 6) & (kMxKB - 1), c = t / (64 * kMxKB);
+  if (c >= kLo) return;
+  const int m = (int)(off[c + 1] - off[c]);
+  const uint32_t* h = hi + off[c];
+  const int g = lane >> 4, row = lane & 15;
+  uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, pm[kMxRBits][4] = {};
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = 64 * kb + 16 * g + j;
+    if (k < m) {
+      const uint32_t x = h[k];
+      a[j >> 2] |= ((__popc(row & (x >> 4) & 15) & 1) ? 0xFFu : 0x01u) << (8 * (j & 3));
+      b[j >> 2] |= ((__popc(row & x & 15) & 1) ? 0xFFu : 0x01u) << (8 * (j & 3));
+#pragma unroll
+      for (int bb = 0; bb < kMxRBits; ++bb)
+        if ((x >> (8 + bb)) & 1) pm[bb][j >> 2] |= 0xFEu << (8 * (j & 3));
+    }
+  }
+  opa[mx_op(c, kb, lane)] = pack_v2l(a);
+  opb[mx_op(c, kb, lane)] = pack_v2l(b);
+  if (row == 0)
+#pragma unroll
+    for (int bb = 0; bb < kMxRBits; ++bb) opm[mx_pm(c, kb, bb, g)] = pack_v2l(pm[bb]);
+}
+
+// codes 64.. of column c for slice bits 8..17 = r: A_r rebuilt from block 1 of the table
+__device__ __forceinline__ v4i_t seed_mx_block1(const v2l_t* __restrict__ opa, const v2l_t* __restrict__ opb,
+                                                          const v2l_t* __restrict__ opm, int c, int r, int lane,
+                                                          v4i_t acc) {
+  v2l_t a1 = opa[mx_op(c, 1, lane)];
+  for (int bb = 0; bb < kMxRBits; ++bb)
+    if ((r >> bb) & 1) a1 ^= opm[mx_pm(c, 1, bb, lane >> 4)];
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, opb[mx_op(c, 1, lane)], acc, 0, 0, 0);
+}
+
+// buf[(z - z0) 2^14 + c] = D_z(c) for z in [z0, z1); workgroup = 128 columns (128 / C waves
+// of C = 16 or 8 columns) x one walk segment of 2^kMxSegBits r values (blockIdx.y).
+// ABL (ablation builds only, wrong results by design): 1 = stores to one contiguous region
+// per workgroup (sequential writes), 2 = no global stores, 3 = no sign updates (A fixed),
+// 4 = no MFMAs, 5 = no LDS stage / barrier and no global stores.
+template <int C, int ABL = 0>
+__global__ __launch_bounds__(64 * (128 / C)) __attribute__((amdgpu_waves_per_eu(C == 16 ? 2 : 4))) void seed_mx_kernel(
+    const v2l_t* __restrict__ opa, const v2l_t* __restrict__ opb, const v2l_t* __restrict__ opm,
+    const uint32_t* __restrict__ off, int z0, int z1, int8_t* __restrict__ buf) {
+  constexpr int W = 128 / C, S = 1 << kMxSegBits, K4 = C / 4;
+  __shared__ v2l_t pm_s[W][kMxSegBits][C][4];  // the walk's planes (block 0)
+  __shared__ uint4 stage[2][256 * 8];          // double-buffered store-out: 256 slices x 128 B
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4;
+  const int cw = blockIdx.x * 128, c0 = cw + wv * C;
+  for (int e = lane; e < C * kMxSegBits * 4; e += 64) {
+    const int cc = e % C, gg = (e / C) & 3, bb = e / (4 * C);
+    pm_s[wv][bb][cc][gg] = opm[mx_pm(c0 + cc, 0, bb, gg)];
+  }
+  unsigned ovf = 0;  // columns with more than 64 codes
+#pragma unroll
+  for (int cc = 0; cc < C; ++cc) ovf |= (unsigned)(off[c0 + cc + 1] - off[c0 + cc] > 64) << cc;
+  ovf = __builtin_amdgcn_readfirstlane(ovf);
+  v2l_t B[C];
+#pragma unroll
+  for (int cc = 0; cc < C; ++cc) B[cc] = opb[mx_op(c0 + cc, 0, lane)];
+  __syncthreads();
+  const int rs = ((z0 >> 8) & ~(S - 1)) + (int)blockIdx.y * S;  // the launch sizes grid.y to the range
+  v2l_t A[C];
+#pragma unroll
+  for (int cc = 0; cc < C; ++cc) A[cc] = opa[mx_op(c0 + cc, 0, lane)];
+  for (int bb = kMxSegBits; bb < kMxRBits; ++bb)
+    if ((rs >> bb) & 1)
+#pragma unroll
+      for (int cc = 0; cc < C; ++cc) A[cc] ^= opm[mx_pm(c0 + cc, 0, bb, g)];
+#pragma unroll 1
+  for (int i = 0; i < S; ++i) {
+    if (i) {
+      const int bb = __builtin_ctz(i);
+#pragma unroll
+      for (int cc = 0; cc < C; ++cc)
+        if constexpr (ABL != 3) A[cc] ^= pm_s[wv][bb][cc][g];
+    }
+    const int r = rs ^ (i ^ (i >> 1));
+    if (r * 256 + 255 < z0 || r * 256 >= z1) continue;
+    uint32_t w[4][K4];  // [slice row 4 g + q][columns 4 k .. 4 k + 3]: low bytes of the products
+#pragma unroll
+    for (int k = 0; k < K4; ++k) {
+      v4i_t acc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int cc = 4 * k + u;
+        if constexpr (ABL == 4)
+          acc[u] = v4i_t{(int)A[cc][0], (int)(A[cc][0] >> 32), (int)B[cc][1], (int)(B[cc][1] >> 32)};
+        else
+          acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[cc], B[cc], v4i_t{0, 0, 0, 0}, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        w[q][k] = __builtin_amdgcn_perm((uint32_t)acc[1][q], (uint32_t)acc[0][q], 0x0c0c0400u) |
+                  __builtin_amdgcn_perm((uint32_t)acc[3][q], (uint32_t)acc[2][q], 0x04000c0cu);
+    }
+    for (unsigned ov = ovf; ov; ov &= ov - 1) {  // columns with codes 64..: add their products
+      const int cc = __builtin_ctz(ov);
+      const v4i_t a1 = seed_mx_block1(opa, opb, opm, c0 + cc, r, lane, v4i_t{0, 0, 0, 0});
+      const int sh = 8 * (cc & 3);
+#pragma unroll
+      for (int k = 0; k < K4; ++k)
+        if (k == (cc >> 2))
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // byte add mod 256: |D| <= 127, so the int8 sum is exact
+            const uint32_t t = ((w[q][k] >> sh) + (uint32_t)a1[q]) & 0xFFu;
+            w[q][k] = (w[q][k] & ~(0xFFu << sh)) | (t << sh);
+          }
+    }
+    if constexpr (ABL == 5) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < K4; ++k) x ^= w[q][k];
+      if (x == 0x12345678u) *reinterpret_cast<uint32_t*>(buf) = x;
+      continue;
+    }
+    // through LDS: each store instruction then covers 8 slices x 128 columns (whole lines)
+    // instead of 64 slices x C columns.  A slice's 128 B hold the waves' C-byte pieces at
+    // XOR-swizzled positions (conflict-free writes); 16-B position p of slice `row` holds
+    // columns 16 (p ^ swz(row)) .. + 15 in order.
+    uint4* stg = stage[i & 1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (4 * g + q) * 16 + (lane & 15);
+      if constexpr (C == 16)
+        stg[row * 8 + (wv ^ (row & 7))] = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
+      else
+        reinterpret_cast<uint2*>(stg)[row * 16 + (wv ^ (row & 14))] = make_uint2(w[q][0], w[q][1]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 2048 / (64 * W); ++t) {
+      const int e = t * 64 * W + (int)threadIdx.x, row = e >> 3;
+      const int swz = C == 16 ? (row & 7) : ((row >> 1) & 7);
+      const int z = r * 256 + row;
+      if constexpr (ABL == 1) {
+        *reinterpret_cast<uint4*>(buf + ((int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * S + i) * 32768 + 16 * e) = stg[e];
+      } else if constexpr (ABL == 2) {
+        const uint4 v = stg[e];
+        if ((v.x ^ v.y ^ v.z ^ v.w) == 0x12345678u) *reinterpret_cast<uint4*>(buf) = v;
+      } else if (z >= z0 && z < z1) {
+        *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + cw + 16 * ((e & 7) ^ swz)) = stg[e];
+      }
+    }
+  }
+}
+
 __global__ void max_column_kernel(const uint32_t* __restrict__ cnt, unsigned* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < kLo) atomicMax(out, cnt[c]);
 }
 
 __global__ void add_kernel(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
+
+// the MFMA seed's tables inside st.d_mx: A_0 and B [column][block][lane], PM [column][block][bit][lane group]
+struct MxTables {
+  v2l_t *a, *b, *m;
+};
+constexpr size_t kMxOpBytes = (size_t)kLo * kMxKB * 64 * sizeof(v2l_t);
+constexpr size_t kMxBytes = 2 * kMxOpBytes + (size_t)kLo * kMxKB * kMxRBits * 4 * sizeof(v2l_t);
+MxTables mx_tables(const State& st) {
+  char* p = static_cast<char*>(st.d_mx);
+  return MxTables{reinterpret_cast<v2l_t*>(p), reinterpret_cast<v2l_t*>(p + kMxOpBytes),
+                  reinterpret_cast<v2l_t*>(p + 2 * kMxOpBytes)};
+}
 
 template <typename T>
 int launch_seed(State& st, int z0, int z1, hipStream_t s) {
@@ -1382,7 +1585,37 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
   if (sabl < 1 || sabl > 10)
 #endif
   {
-    if (sizeof(T) == 1 && st.seed_spread)
+    if (sizeof(T) == 1 && st.d_mx) {
+      const MxTables mx = mx_tables(st);
+      const int ra = (z0 >> 8) & ~((1 << kMxSegBits) - 1), rend = ((z1 - 1) >> 8) + 1;
+      const int nseg = (rend - ra + (1 << kMxSegBits) - 1) >> kMxSegBits;
+      const dim3 mgrid(kLo / 128, (unsigned)nseg);
+#ifdef SCT_ABLATION
+      // SCT_MX_ABL = ablation variant v (10 + v: 8-column waves)
+      if (const char* e = getenv("SCT_MX_ABL")) {
+        const int v = atoi(e);
+        int8_t* b8 = reinterpret_cast<int8_t*>(buf);
+#define SCT_MX_L(C_, A_) \
+  hipLaunchKernelGGL((seed_mx_kernel<C_, A_>), mgrid, dim3(64 * (128 / C_)), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1, b8)
+        switch (v) {
+          case 1: SCT_MX_L(16, 1); break;
+          case 2: SCT_MX_L(16, 2); break;
+          case 3: SCT_MX_L(16, 3); break;
+          case 4: SCT_MX_L(16, 4); break;
+          case 5: SCT_MX_L(16, 5); break;
+          case 10: SCT_MX_L(8, 0); break;
+          case 12: SCT_MX_L(8, 2); break;
+          case 15: SCT_MX_L(8, 5); break;
+          default: SCT_MX_L(16, 0); break;
+        }
+#undef SCT_MX_L
+        SCT_LAUNCH_CHECK();
+        return SCT_OK;
+      }
+#endif
+      hipLaunchKernelGGL((seed_mx_kernel<kMxCols, 0>), mgrid, dim3(64 * (128 / kMxCols)), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1,
+                         reinterpret_cast<int8_t*>(buf));
+    } else if (sizeof(T) == 1 && st.seed_spread)
       hipLaunchKernelGGL(seed_spread_kernel, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
                          st.max_groups, z0, z1, reinterpret_cast<int8_t*>(buf));
     else
@@ -1527,16 +1760,23 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   st.elem_bytes = maxm <= 127 ? 1 : (maxm <= 32767 ? 2 : 4);
   const char* mf = getenv("SCT_SPECTRAL_MFMA");  // 0: VALU tile kernel for int8 seeds too
   st.mfma = !(mf && atoi(mf) == 0);
+  bool seed_mx = true;
   {
     int per_cu = 0;  // resident MFMA-tile workgroups per CU (VGPR / LDS bound)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma2_pf_kernel, 256, 0) != hipSuccess ||
         per_cu <= 0)
       per_cu = 2;
     st.tile_wgs = per_cu;
-    const char* sv = getenv("SCT_SPECTRAL_SEED");  // A/B: "spread" = stores spread over the walk
+    // seed variant (int8): the Gray-walk popcount seed by default; "mx" = the MFMA seed,
+    // "spread" = the walk with its stores spread over the walk
+    const char* sv = getenv("SCT_SPECTRAL_SEED");
     st.seed_spread = sv && !strcmp(sv, "spread");
-    const char* tv = getenv("SCT_SPECTRAL_TILE");  // A/B: reg / reg_np / reg_w3 = the register-resident tile
-    st.tile_reg = !tv ? 0 : !strcmp(tv, "reg") ? 1 : !strcmp(tv, "reg_np") ? 2 : !strcmp(tv, "reg_w3") ? 3 : 0;
+    seed_mx = sv && !strcmp(sv, "mx");
+    // tile variant: the register-resident tile by default (r02 A/B on the 737K headline: 0.304 vs
+    // 0.320 ms per 65536 slices, count 2.39 vs 2.47 ms); "mfma2" = the LDS-exchange tile,
+    // reg_np / reg_w3 = register-tile ablations
+    const char* tv = getenv("SCT_SPECTRAL_TILE");
+    st.tile_reg = !tv ? 1 : !strcmp(tv, "mfma2") ? 0 : !strcmp(tv, "reg_np") ? 2 : !strcmp(tv, "reg_w3") ? 3 : 1;
     int per_cu_reg = 0;  // its resident workgroups per CU
     const void* kf = st.tile_reg == 2 ? (const void*)tile_reg_np_kernel
                      : st.tile_reg == 3 ? (const void*)tile_reg_w3_kernel : (const void*)tile_reg_kernel;
@@ -1565,13 +1805,23 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   SCT_HIP(hipMalloc(&st.d_hist, (size_t)kSortWGs * kLo * 4));
   SCT_HIP(hipMalloc(&st.d_planes, (size_t)st.max_groups * kHiBits * 4));
   SCT_HIP(hipMalloc(&st.d_buf, (size_t)st.chunk * kLo * st.elem_bytes));
+  if (seed_mx && st.elem_bytes == 1) SCT_HIP(hipMalloc(&st.d_mx, kMxBytes));  // 84 MB
+  if (const char* ov = getenv("SCT_SPECTRAL_OVERLAP")) st.overlap = atoi(ov) != 0;
+  if (st.overlap) {
+    SCT_HIP(hipMalloc(&st.d_buf2, (size_t)st.chunk * kLo * st.elem_bytes));
+    SCT_HIP(hipStreamCreateWithFlags(&st.side, hipStreamNonBlocking));
+    for (auto& e : st.ev) SCT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   return SCT_OK;
 }
 
 void destroy(State& st) {
   for (void* p : {(void*)st.d_hi, (void*)st.d_off, (void*)st.d_cnt, (void*)st.d_gofs, (void*)st.d_planes, (void*)st.d_hist,
-                  st.d_buf, (void*)st.d_order})
+                  st.d_buf, (void*)st.d_order, st.d_mx, st.d_buf2})
     if (p) (void)hipFree(p);
+  for (auto e : st.ev)
+    if (e) (void)hipEventDestroy(e);
+  if (st.side) (void)hipStreamDestroy(st.side);
   st = State();
 }
 
@@ -1594,6 +1844,12 @@ int build(State& st, const uint64_t* d_codes, hipStream_t s) {
                        st.d_hi, st.d_off, st.d_gofs, st.max_groups, st.d_planes);
   }
   SCT_LAUNCH_CHECK();
+  if (st.d_mx) {
+    const MxTables mx = mx_tables(st);
+    hipLaunchKernelGGL(seed_ops_kernel, dim3(kLo * kMxKB * 64 / 256), dim3(256), 0, s, st.d_hi, st.d_off, mx.a, mx.b,
+                       mx.m);
+    SCT_LAUNCH_CHECK();
+  }
   return SCT_OK;
 }
 
@@ -1601,6 +1857,34 @@ int count(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_count
   SCT_CHECK(0 <= z_begin && z_begin <= z_end && z_end <= kSlices, "slice range [%lld, %lld)",
             (long long)z_begin, (long long)z_end);
   if (st.n < 2 || z_begin == z_end) return SCT_OK;
+  if (st.overlap && z_end - z_begin > st.chunk) {
+    // chunk j's seed runs on the side stream into buffer j % 2 once chunk j-2's tile has
+    // released it; chunk j's tile runs on s after that seed.  Launch order alternates so
+    // that seed j+1 is queued before tile j.
+    void* bufs[2] = {st.d_buf, st.d_buf2};
+    SCT_HIP(hipEventRecord(st.ev[4], s));
+    SCT_HIP(hipStreamWaitEvent(st.side, st.ev[4], 0));
+    int j = 0;
+    for (int64_t z0 = z_begin; z0 < z_end; z0 += st.chunk, ++j) {
+      const int z1 = (int)std::min<int64_t>(z_end, z0 + st.chunk);
+      if (j >= 2) SCT_HIP(hipStreamWaitEvent(st.side, st.ev[j & 1], 0));
+      st.d_buf = bufs[j & 1];
+      int rc = st.elem_bytes == 1   ? launch_seed<int8_t>(st, (int)z0, z1, st.side)
+               : st.elem_bytes == 2 ? launch_seed<int16_t>(st, (int)z0, z1, st.side)
+                                    : launch_seed<int32_t>(st, (int)z0, z1, st.side);
+      if (rc == SCT_OK) rc = hipEventRecord(st.ev[2 + (j & 1)], st.side) == hipSuccess ? SCT_OK : SCT_E_HIP;
+      if (rc == SCT_OK) rc = hipStreamWaitEvent(s, st.ev[2 + (j & 1)], 0) == hipSuccess ? SCT_OK : SCT_E_HIP;
+      const unsigned long long add_n = z0 == 0 ? (unsigned long long)st.n : 0ull;
+      if (rc == SCT_OK)
+        rc = st.elem_bytes == 1   ? launch_tile<int8_t>(st, (int)z0, z1, d_counts, s, add_n)
+             : st.elem_bytes == 2 ? launch_tile<int16_t>(st, (int)z0, z1, d_counts, s, add_n)
+                                  : launch_tile<int32_t>(st, (int)z0, z1, d_counts, s, add_n);
+      if (rc == SCT_OK) rc = hipEventRecord(st.ev[j & 1], s) == hipSuccess ? SCT_OK : SCT_E_HIP;
+      st.d_buf = bufs[0];
+      if (rc != SCT_OK) return rc;
+    }
+    return SCT_OK;
+  }
   for (int64_t z0 = z_begin; z0 < z_end; z0 += st.chunk) {
     const int z1 = (int)std::min<int64_t>(z_end, z0 + st.chunk);
     // d_counts[0] += n by the job's first tile launch (the range holding slice 0)

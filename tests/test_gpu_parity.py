@@ -411,6 +411,40 @@ def test_allpairs_spectral_scheme_matches_oracle(n, width, monkeypatch):
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
+@pytest.mark.parametrize("tile,seed,overlap", [("reg", "", "0"), ("mfma2", "", "0"), ("reg_np", "", "0"),
+                                               ("reg_w3", "", "0"), ("reg", "walk", "0"), ("reg", "mx", "0"),
+                                               ("reg", "spread", "0"), ("reg", "walk", "1"), ("reg", "mx", "1")])
+def test_allpairs_spectral_kernel_variants(tile, seed, overlap, monkeypatch):
+    """Every tile / seed kernel variant, with and without the seed / tile overlap over two
+    streams, gives the oracle's histogram, with 1000-slice chunks (seams inside the range)."""
+    monkeypatch.setenv("SCT_SPECTRAL_TILE", tile)
+    monkeypatch.setenv("SCT_SPECTRAL_SEED", seed)
+    monkeypatch.setenv("SCT_SPECTRAL_OVERLAP", overlap)
+    codes = synthetic.whitelist_codes(30_000, 16, seed=5)
+    codes = np.concatenate([codes, codes[:3], codes[3:5] ^ np.uint64(0xFFFFFFFF)])
+    hist = _spectral_hist(codes, [(0, 777), (777, 1 << 18)], chunk=1000, monkeypatch=monkeypatch)
+    assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
+
+
+@pytest.mark.parametrize("seed", ["mx", "walk"])
+def test_allpairs_spectral_column_sizes(seed, monkeypatch):
+    """Columns (low 14 bits) holding 63, 64, 65, 100 and 127 codes -- the MFMA seed's one- and
+    two-block columns and the int8 limit -- next to sparse ones, duplicates included; slice
+    ranges cut inside 256-slice tiles and walk segments."""
+    monkeypatch.setenv("SCT_SPECTRAL_SEED", seed)
+    rng = np.random.default_rng(21)
+    bg = synthetic.whitelist_codes(5000, 16, seed=3)
+    cols = (5, 6, 7, 20, 16383)
+    parts = [bg[~np.isin(bg & np.uint64(0x3FFF), np.array(cols, dtype=np.uint64))]]
+    for col, m in zip(cols, (63, 64, 65, 100, 127)):
+        hi = rng.integers(0, 1 << 18, m).astype(np.uint64)
+        hi[-1] = hi[0]  # a duplicate code inside the column
+        parts.append((hi << np.uint64(14)) | np.uint64(col))
+    codes = np.concatenate(parts)
+    hist = _spectral_hist(codes, [(0, 300), (300, 8191), (8191, 1 << 18)])
+    assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
+
+
 def test_allpairs_spectral_crowded_low_bits(monkeypatch):
     """3000 codes sharing their low 14 bits (one transform column holds them all: 94
     32-code groups of bit planes, an int16 intermediate), plus codes that differ only
