@@ -37,3 +37,12 @@ def test_wide_and_negative_keys():
         barcode.Barcodes({-1: 1, 2 ** 65: 1}, 4).codes_array()
     with pytest.raises(OverflowError):  # as the reference's np.fromiter (barcode.py:59)
         b.base_frequency()
+
+
+def test_base4_entropy_golden(golden):
+    """stats.base4_entropy on the reference's own base counts reproduces the
+    effective_diversity the reference computed from them, bit for bit."""
+    from sctools_amd.stats import base4_entropy
+    wl = golden["whitelist_1k"]
+    got = base4_entropy(np.array(wl["base_frequency"]))
+    assert [float(v) for v in got] == [float.fromhex(v) for v in wl["effective_diversity"]]

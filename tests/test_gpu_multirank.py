@@ -53,3 +53,46 @@ def test_ranks_on_gpu_match_oracle(tmp_path, scheme, world, n):
         assert z["hist"].tolist() == ref.tolist()
         shares += int(z["mine"])
     assert shares == n * (n - 1) // 2
+
+
+def _records():
+    """5,003 random 28-bp ACGT records, (n, 28) uint8."""
+    rng = np.random.default_rng(3)
+    return np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, (5_003, 28))]
+
+
+def _worker_records(rank, world, port, out_path):
+    """config 4 / config 5 shapes, small: nearest with the queries split over the ranks,
+    and the batch encoder with the records split, both through the GPU path on every rank."""
+    import torch
+    import torch.distributed as dist
+    from sctools_amd import _lib, sharding
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    _lib.check(_lib.lib().sct_set_device(0))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        wl3 = synthetic.two_to_three(synthetic.whitelist_codes(20_000, 16, 5), 16)
+        q = synthetic.config4_queries(wl3, 30_001, seed=9)[0].cpu().numpy().view(np.uint64)
+        idx, dist_ = sharding.nearest_sharded(3, wl3, q, 1)
+        codes, gc, flags = sharding.encode_sharded(2, _records(), 28)
+        np.savez(out_path % rank, idx=idx, dist=dist_, codes=codes, gc=gc, q=q, wl=wl3)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_record_sharding_on_gpu(tmp_path):
+    """Contiguous record ranges per rank (no reduction, one all-gather): every rank ends with
+    the oracle's whole nearest result and the single-process encoder's whole output."""
+    out = str(tmp_path / "q%d.npz")
+    mp.spawn(_worker_records, args=(2, _free_port(), out), nprocs=2, join=True)
+    z0 = np.load(out % 0)
+    ref_idx, ref_dist = O.c_nearest(3, z0["wl"], z0["q"], 1)
+    seqs = [bytes(r) for r in _records()]
+    ref_codes = [O.two_bit_encode(s) for s in seqs]
+    for r in range(2):
+        z = np.load(out % r)
+        assert z["idx"].tolist() == ref_idx.tolist()
+        assert z["dist"].tolist() == ref_dist.tolist()
+        assert z["codes"].reshape(-1).astype(np.uint64).tolist() == ref_codes
+        assert z["gc"].tolist() == [s.count(b"C") + s.count(b"G") for s in seqs]
