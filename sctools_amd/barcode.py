@@ -39,7 +39,6 @@ class Barcodes:
         if not isinstance(barcode_length, int) and barcode_length > 0:
             raise ValueError('barcode length must be a positive integer')
         self._barcode_length = barcode_length
-        self._codes = None
 
     def __contains__(self, item):
         return item in self._data
@@ -67,10 +66,19 @@ class Barcodes:
             for a, b in itertools.combinations(self._data, 2):
                 a ^ b
             return np.zeros(n, dtype=np.uint64)  # < 2 keys: no pair, nothing to compare
-        try:
-            return np.fromiter(keys, dtype=np.uint64, count=n)
+        try:  # the common case (every key < 2^63) on numpy's fastest conversion
+            arr = np.fromiter(keys, dtype=np.int64, count=n)
+            if n and int(arr.min()) < 0:
+                raise ValueError('barcode codes must be non-negative integers')
+            return arr.view(np.uint64)
         except OverflowError:
-            ints = [int(k) for k in keys]
+            pass
+        if not any(isinstance(k, np.signedinteger) and k < 0 for k in keys):  # (numpy would wrap those)
+            try:
+                return np.fromiter(keys, dtype=np.uint64, count=n)
+            except OverflowError:
+                pass
+        ints = [int(k) for k in keys]
         if any(v < 0 for v in ints):
             # the reference's `while difference:` never ends on a negative XOR (encodings.py:118)
             raise ValueError('barcode codes must be non-negative integers')

@@ -22,6 +22,16 @@ constexpr int kT = 256;  // codes per tile = threads per workgroup
 
 __device__ __forceinline__ int dist2(uint64_t x) { return __popcll((x | (x >> 1)) & 0x5555555555555555ull); }
 
+// the even bits of x packed into 32 bits (bit 2g -> bit g)
+__device__ __forceinline__ uint32_t even_bits(uint64_t x) {
+  x &= 0x5555555555555555ull;
+  x = (x | (x >> 1)) & 0x3333333333333333ull;
+  x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+  return (uint32_t)(x | (x >> 16));
+}
+
 // item t -> tile pair (a, b), items of row a: b = a .. nb-1, row a starts at a nb - a(a-1)/2
 __device__ __forceinline__ void item_to_tiles(int64_t t, int64_t nb, int64_t& a, int64_t& b) {
   const double B = 2.0 * (double)nb + 1.0;
@@ -40,7 +50,10 @@ __global__ __launch_bounds__(kT) void wide_private_kernel(const uint64_t* __rest
                                                           unsigned long long* __restrict__ hist) {
   constexpr int NB = 32 * W + 1;
   __shared__ uint32_t cnt[NB * kT];
-  __shared__ uint64_t col[W * kT];
+  // the column tile as 2-bit-group planes: per code and limb {low bits, high bits} of the
+  // 32 groups, so a pair's limb distance is popcount((lo ^ lo') | (hi ^ hi')): 2 ops + a
+  // v_bcnt instead of the 64-bit XOR / shift / OR / AND / 2 popcounts
+  __shared__ uint2 col[W * kT];
   const int t = threadIdx.x;
   for (int k = t; k < NB * kT; k += kT) cnt[k] = 0;
   const int64_t nb = (n + kT - 1) / kT;
@@ -49,20 +62,25 @@ __global__ __launch_bounds__(kT) void wide_private_kernel(const uint64_t* __rest
   const int64_t ie = item_begin + span * (blockIdx.x + 1) / gridDim.x;
   int64_t a = 0, b = 0;
   if (ib < ie) item_to_tiles(ib, nb, a, b);
-  uint64_t q[W];
+  uint32_t qlo[W], qhi[W];
   int64_t qa = -1;
   for (int64_t it = ib; it < ie; ++it) {
     if (a != qa) {  // a new row tile: this thread's code
       const int64_t i = a * kT + t;
 #pragma unroll
-      for (int w = 0; w < W; ++w) q[w] = i < n ? codes[i * W + w] : 0;
+      for (int w = 0; w < W; ++w) {
+        const uint64_t x = i < n ? codes[i * W + w] : 0;
+        qlo[w] = even_bits(x);
+        qhi[w] = even_bits(x >> 1);
+      }
       qa = a;
     }
     __syncthreads();  // the previous item's reads of col are done
     const int64_t j0 = b * kT;
     for (int k = t; k < W * kT; k += kT) {
       const int64_t j = j0 + k / W;
-      col[k] = j < n ? codes[j0 * W + k] : 0;
+      const uint64_t x = j < n ? codes[j0 * W + k] : 0;
+      col[k] = make_uint2(even_bits(x), even_bits(x >> 1));
     }
     __syncthreads();
     const int64_t i = a * kT + t;
@@ -71,9 +89,12 @@ __global__ __launch_bounds__(kT) void wide_private_kernel(const uint64_t* __rest
     const int jlast = (int)min<int64_t>(kT, n - j0);
     if (i < n) {
       for (int jj = jfirst; jj < jlast; ++jj) {
-        int d = 0;
+        uint32_t d = 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w) d += dist2(q[w] ^ col[jj * W + w]);
+        for (int w = 0; w < W; ++w) {
+          const uint2 c = col[jj * W + w];
+          d += __popc((qlo[w] ^ c.x) | (qhi[w] ^ c.y));
+        }
         atomicAdd(&cnt[d * kT + t], 1u);  // private column: ds_add_u32, never contended
       }
     }
