@@ -150,6 +150,28 @@ def allpairs_histogram_sharded(codes, code_bits=None, group=None, device=None, s
         return job.step()
 
 
+def allpairs_wide_sharded(limbs, group=None, device=None):
+    """The multi-limb histogram (keys >= 2^64: (n, words) little-endian uint64 limbs, the
+    32 * words + 1 bins of ``_lib.hamming_hist_allpairs_wide``) with the tile-pair items
+    split into contiguous ranges over the ranks of `group` and one all-reduce of the bins."""
+    import torch
+    import torch.distributed as dist
+    world, rank = _group_info(group)
+    limbs = np.ascontiguousarray(limbs, dtype=np.uint64)
+    limbs = limbs.reshape(limbs.shape[0], -1) if limbs.ndim else limbs.reshape(0, 1)
+    n, words = limbs.shape
+    items, nbins = _lib.wide_geometry(n, words)
+    b, e = item_range(items, rank, world)
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    d = torch.from_numpy(limbs.view(np.int64)).to(dev)
+    hist = torch.zeros(nbins, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(_lib.lib().sct_allpairs_wide(d.data_ptr(), n, words, b, e, hist.data_ptr(), nbins, stream))
+    if world > 1:
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+    return hist.cpu().numpy().view(np.uint64)
+
+
 def _group_info(group):
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():

@@ -61,6 +61,13 @@ def _records():
     return np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, (5_003, 28))]
 
 
+def _wide_limbs():
+    """3,001 random 90-bit keys as (n, 2) limbs (the multi-limb path)."""
+    rng = np.random.default_rng(8)
+    return np.stack([rng.integers(0, 2**63, 3_001, dtype=np.uint64) * np.uint64(2) + np.uint64(1),
+                     rng.integers(0, 2**26, 3_001, dtype=np.uint64)], axis=1)
+
+
 def _worker_records(rank, world, port, out_path):
     """config 4 / config 5 shapes, small: nearest with the queries split over the ranks,
     and the batch encoder with the records split, both through the GPU path on every rank."""
@@ -76,14 +83,16 @@ def _worker_records(rank, world, port, out_path):
         q = synthetic.config4_queries(wl3, 30_001, seed=9)[0].cpu().numpy().view(np.uint64)
         idx, dist_ = sharding.nearest_sharded(3, wl3, q, 1)
         codes, gc, flags = sharding.encode_sharded(2, _records(), 28)
-        np.savez(out_path % rank, idx=idx, dist=dist_, codes=codes, gc=gc, q=q, wl=wl3)
+        wide = sharding.allpairs_wide_sharded(_wide_limbs())
+        np.savez(out_path % rank, idx=idx, dist=dist_, codes=codes, gc=gc, q=q, wl=wl3, wide=wide)
     finally:
         dist.destroy_process_group()
 
 
 def test_record_sharding_on_gpu(tmp_path):
     """Contiguous record ranges per rank (no reduction, one all-gather): every rank ends with
-    the oracle's whole nearest result and the single-process encoder's whole output."""
+    the oracle's whole nearest result and the oracle's encodings; the multi-limb all-pairs
+    histogram with its tile-pair items split over the ranks equals the oracle's."""
     out = str(tmp_path / "q%d.npz")
     mp.spawn(_worker_records, args=(2, _free_port(), out), nprocs=2, join=True)
     z0 = np.load(out % 0)
@@ -96,3 +105,4 @@ def test_record_sharding_on_gpu(tmp_path):
         assert z["dist"].tolist() == ref_dist.tolist()
         assert z["codes"].reshape(-1).astype(np.uint64).tolist() == ref_codes
         assert z["gc"].tolist() == [s.count(b"C") + s.count(b"G") for s in seqs]
+        assert z["wide"].tolist() == O.c_hist_wide(_wide_limbs()).tolist()
