@@ -31,6 +31,7 @@ struct State {
   int tile_reg_wgs = 2;          // its resident workgroups per CU
   bool seed_spread = false;      // int8 seeds: stores spread over the walk (16-slice blocks)
   void* d_mx = nullptr;          // int8 seeds: the MFMA seed's operand tables (null: the walk seed)
+  int mx_form = 2;               // the MFMA seed's workgroup shape (A/B)
   // seed / tile overlap: chunk j+1's seed (side stream, second buffer) runs beside chunk j's tile
   bool overlap = false;
   void* d_buf2 = nullptr;

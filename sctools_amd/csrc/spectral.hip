@@ -1411,15 +1411,26 @@ __device__ __forceinline__ v4i_t seed_mx_block1(const v2l_t* __restrict__ opa, c
 // ABL (ablation builds only, wrong results by design): 1 = stores to one contiguous region
 // per workgroup (sequential writes), 2 = no global stores, 3 = no sign updates (A fixed),
 // 4 = no MFMAs, 5 = no LDS stage / barrier and no global stores.
-template <int C, int ABL = 0>
-__global__ __launch_bounds__(64 * (128 / C)) __attribute__((amdgpu_waves_per_eu(C == 16 ? 2 : 4))) void seed_mx_kernel(
+//
+// W waves of C columns: C x W = 128 columns per workgroup (whole 128-B lines per slice), or
+// C = 8, W = 8: 64 columns (half lines) with two co-resident workgroups per CU and the two
+// halves of every line given to workgroups 8 apart in dispatch order, which the dispatcher
+// places on the same XCD (round robin), so its L2 merges the halves.
+template <int C, int W, int ABL = 0>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(C == 16 ? 2 : 4))) void seed_mx_kernel(
     const v2l_t* __restrict__ opa, const v2l_t* __restrict__ opb, const v2l_t* __restrict__ opm,
     const uint32_t* __restrict__ off, int z0, int z1, int8_t* __restrict__ buf) {
-  constexpr int W = 128 / C, S = 1 << kMxSegBits, K4 = C / 4;
+  constexpr int S = 1 << kMxSegBits, K4 = C / 4, RB = C * W, P = RB / 16;  // row bytes, 16-B positions
   __shared__ v2l_t pm_s[W][kMxSegBits][C][4];  // the walk's planes (block 0)
-  __shared__ uint4 stage[2][256 * 8];          // double-buffered store-out: 256 slices x 128 B
+  __shared__ uint4 stage[2][256 * P];          // double-buffered store-out: 256 slices x RB bytes
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4;
-  const int cw = blockIdx.x * 128, c0 = cw + wv * C;
+  int cblk = blockIdx.x, seg = blockIdx.y;
+  if constexpr (RB == 64) {  // 1-D grid: L = 16 u + 8 h + x (x = XCD slot), unit u * 8 + x = (pair, segment)
+    const int L = blockIdx.x, unit = (L >> 4) * 8 + (L & 7), npairs = kLo / 128;
+    cblk = 2 * (unit % npairs) + ((L >> 3) & 1);
+    seg = unit / npairs;
+  }
+  const int cw = cblk * RB, c0 = cw + wv * C;
   for (int e = lane; e < C * kMxSegBits * 4; e += 64) {
     const int cc = e % C, gg = (e / C) & 3, bb = e / (4 * C);
     pm_s[wv][bb][cc][gg] = opm[mx_pm(c0 + cc, 0, bb, gg)];
@@ -1432,7 +1443,7 @@ __global__ __launch_bounds__(64 * (128 / C)) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
   for (int cc = 0; cc < C; ++cc) B[cc] = opb[mx_op(c0 + cc, 0, lane)];
   __syncthreads();
-  const int rs = ((z0 >> 8) & ~(S - 1)) + (int)blockIdx.y * S;  // the launch sizes grid.y to the range
+  const int rs = ((z0 >> 8) & ~(S - 1)) + seg * S;  // the launch sizes the grid to the range
   v2l_t A[C];
 #pragma unroll
   for (int cc = 0; cc < C; ++cc) A[cc] = opa[mx_op(c0 + cc, 0, lane)];
@@ -1493,28 +1504,32 @@ __global__ __launch_bounds__(64 * (128 / C)) __attribute__((amdgpu_waves_per_eu(
     // instead of 64 slices x C columns.  A slice's 128 B hold the waves' C-byte pieces at
     // XOR-swizzled positions (conflict-free writes); 16-B position p of slice `row` holds
     // columns 16 (p ^ swz(row)) .. + 15 in order.
+    // swizzle: a slice's C-byte pieces sit at XOR-permuted positions that keep every pair
+    // of 8-B pieces (one 16-B position) in column order; writes are bank-conflict-free
+    auto swz = [](int row) {  // in 16-B positions
+      return C == 16 ? (row & 7) : (RB == 128 ? ((row >> 1) & 7) : ((row >> 2) & 3));
+    };
     uint4* stg = stage[i & 1];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int row = (4 * g + q) * 16 + (lane & 15);
       if constexpr (C == 16)
-        stg[row * 8 + (wv ^ (row & 7))] = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
+        stg[row * P + (wv ^ swz(row))] = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
       else
-        reinterpret_cast<uint2*>(stg)[row * 16 + (wv ^ (row & 14))] = make_uint2(w[q][0], w[q][1]);
+        reinterpret_cast<uint2*>(stg)[row * 2 * P + (wv ^ (2 * swz(row)))] = make_uint2(w[q][0], w[q][1]);
     }
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < 2048 / (64 * W); ++t) {
-      const int e = t * 64 * W + (int)threadIdx.x, row = e >> 3;
-      const int swz = C == 16 ? (row & 7) : ((row >> 1) & 7);
+    for (int t = 0; t < 256 * P / (64 * W); ++t) {
+      const int e = t * 64 * W + (int)threadIdx.x, row = e / P;
       const int z = r * 256 + row;
       if constexpr (ABL == 1) {
-        *reinterpret_cast<uint4*>(buf + ((int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * S + i) * 32768 + 16 * e) = stg[e];
+        *reinterpret_cast<uint4*>(buf + ((int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * S + i) * (256 * RB) + 16 * e) = stg[e];
       } else if constexpr (ABL == 2) {
         const uint4 v = stg[e];
         if ((v.x ^ v.y ^ v.z ^ v.w) == 0x12345678u) *reinterpret_cast<uint4*>(buf) = v;
       } else if (z >= z0 && z < z1) {
-        *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + cw + 16 * ((e & 7) ^ swz)) = stg[e];
+        *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + cw + 16 * ((e % P) ^ swz(row))) = stg[e];
       }
     }
   }
@@ -1590,31 +1605,34 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
       const int ra = (z0 >> 8) & ~((1 << kMxSegBits) - 1), rend = ((z1 - 1) >> 8) + 1;
       const int nseg = (rend - ra + (1 << kMxSegBits) - 1) >> kMxSegBits;
       const dim3 mgrid(kLo / 128, (unsigned)nseg);
+      const dim3 hgrid((unsigned)(2 * (kLo / 128) * nseg));  // the 64-column form: paired, 1-D
+      int8_t* b8 = reinterpret_cast<int8_t*>(buf);
+#define SCT_MX_L(C_, W_, A_, G_) \
+  hipLaunchKernelGGL((seed_mx_kernel<C_, W_, A_>), G_, dim3(64 * W_), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1, b8)
 #ifdef SCT_ABLATION
-      // SCT_MX_ABL = ablation variant v (10 + v: 8-column waves)
+      // SCT_MX_ABL = ablation variant v on the shipped form (see seed_mx_kernel's ABL list)
       if (const char* e = getenv("SCT_MX_ABL")) {
-        const int v = atoi(e);
-        int8_t* b8 = reinterpret_cast<int8_t*>(buf);
-#define SCT_MX_L(C_, A_) \
-  hipLaunchKernelGGL((seed_mx_kernel<C_, A_>), mgrid, dim3(64 * (128 / C_)), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1, b8)
-        switch (v) {
-          case 1: SCT_MX_L(16, 1); break;
-          case 2: SCT_MX_L(16, 2); break;
-          case 3: SCT_MX_L(16, 3); break;
-          case 4: SCT_MX_L(16, 4); break;
-          case 5: SCT_MX_L(16, 5); break;
-          case 10: SCT_MX_L(8, 0); break;
-          case 12: SCT_MX_L(8, 2); break;
-          case 15: SCT_MX_L(8, 5); break;
-          default: SCT_MX_L(16, 0); break;
+        switch (atoi(e)) {
+          case 1: SCT_MX_L(8, 8, 1, hgrid); break;
+          case 2: SCT_MX_L(8, 8, 2, hgrid); break;
+          case 5: SCT_MX_L(8, 8, 5, hgrid); break;
+          default: SCT_MX_L(8, 8, 0, hgrid); break;
         }
-#undef SCT_MX_L
         SCT_LAUNCH_CHECK();
         return SCT_OK;
       }
 #endif
-      hipLaunchKernelGGL((seed_mx_kernel<kMxCols, 0>), mgrid, dim3(64 * (128 / kMxCols)), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1,
-                         reinterpret_cast<int8_t*>(buf));
+      // SCT_SPECTRAL_MX_FORM: 2 = 8-column waves x 16 (128-column workgroups, default: 0.354-
+      // 0.360 ms per launch), 1 = 16-column waves x 8 (0.383), 0 = 8-column waves x 8 with
+      // XCD-paired 64-column workgroups, two per CU (0.419: the half-line writes cost more
+      // than the second workgroup hides)
+      if (st.mx_form == 1)
+        SCT_MX_L(16, 8, 0, mgrid);
+      else if (st.mx_form == 0)
+        SCT_MX_L(8, 8, 0, hgrid);
+      else
+        SCT_MX_L(8, 16, 0, mgrid);
+#undef SCT_MX_L
     } else if (sizeof(T) == 1 && st.seed_spread)
       hipLaunchKernelGGL(seed_spread_kernel, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
                          st.max_groups, z0, z1, reinterpret_cast<int8_t*>(buf));
@@ -1772,6 +1790,7 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
     const char* sv = getenv("SCT_SPECTRAL_SEED");
     st.seed_spread = sv && !strcmp(sv, "spread");
     seed_mx = sv && !strcmp(sv, "mx");
+    if (const char* f = getenv("SCT_SPECTRAL_MX_FORM")) st.mx_form = atoi(f);
     // tile variant: the register-resident tile by default (r02 A/B on the 737K headline: 0.304 vs
     // 0.320 ms per 65536 slices, count 2.39 vs 2.47 ms); "mfma2" = the LDS-exchange tile,
     // reg_np / reg_w3 = register-tile ablations
