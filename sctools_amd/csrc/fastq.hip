@@ -62,23 +62,24 @@ __device__ __forceinline__ uint32_t byte_mask4(uint32_t hi_bits) {  // bit 7 of 
   return ((hi_bits >> 7) & 1u) | ((hi_bits >> 14) & 2u) | ((hi_bits >> 21) & 4u) | ((hi_bits >> 28) & 8u);
 }
 
-__device__ __forceinline__ uint32_t load_mask(const uint8_t* __restrict__ buf, int64_t n, int64_t p0,
-                                              int text, uint32_t* kinds_crlf, uint32_t* nonascii,
-                                              uint4* bytes_out = nullptr) {
+// the 16 bytes at p0 (zero past n)
+__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ buf, int64_t n, int64_t p0) {
+  if (p0 + 16 <= n) return *reinterpret_cast<const uint4*>(buf + p0);
   uint32_t w[4];
-  if (p0 + 16 <= n) {
-    const uint4 v = *reinterpret_cast<const uint4*>(buf + p0);
-    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-  } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint32_t x = 0;
-      for (int b = 0; b < 4; ++b)
-        if (p0 + 4 * k + b < n) x |= (uint32_t)buf[p0 + 4 * k + b] << (8 * b);
-      w[k] = x;
-    }
+  for (int k = 0; k < 4; ++k) {
+    uint32_t x = 0;
+    for (int b = 0; b < 4; ++b)
+      if (p0 + 4 * k + b < n) x |= (uint32_t)buf[p0 + 4 * k + b] << (8 * b);
+    w[k] = x;
   }
-  if (bytes_out) *bytes_out = make_uint4(w[0], w[1], w[2], w[3]);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// terminator mask of the 16 bytes v loaded from p0
+__device__ __forceinline__ uint32_t load_mask(const uint8_t* __restrict__ buf, int64_t n, int64_t p0,
+                                              int text, uint32_t* kinds_crlf, uint32_t* nonascii, uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   const uint32_t valid = p0 + 16 <= n ? 0xFFFFu : (uint32_t)((1u << (n - p0)) - 1u);
   uint32_t lf = 0, cr = 0, na = 0;
 #pragma unroll
@@ -118,32 +119,43 @@ __device__ __forceinline__ int virtual_in(const uint8_t* __restrict__ buf, int64
 
 // Per tile: its terminator count, and its first terminator (in-tile offset << 2 | 1 if
 // virtual | 2 if "\r\n"; ~0 if none) -- the end of the previous tile's last line.
+// Persistent: a workgroup walks tiles blockIdx.x, + gridDim.x, ... with the next tile's
+// 16 bytes per thread loaded before this tile is reduced (one load in flight per thread
+// while it works: a tile per workgroup left the loads latency-bound).
 __global__ __launch_bounds__(WG) void count_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs,
                                                    int text, unsigned long long* __restrict__ counts,
                                                    uint32_t* __restrict__ first,
-                                                   unsigned* __restrict__ flags) {
-  const int64_t p0 = (int64_t)blockIdx.x * TILE + (int64_t)threadIdx.x * 16;
-  uint32_t c = 0, na = 0, crlf = 0, m = 0, f = ~0u;
-  if (p0 < n) {
-    m = load_mask(buf, n, p0, text, &crlf, &na);
-    const int vj = virtual_in(buf, n, fs, p0, text);
-    c = __popc(m) + (vj >= 0);
-    if (m) {
-      const int j = __ffs(m) - 1;
-      f = ((uint32_t)(threadIdx.x * 16 + j) << 2) | ((crlf >> j & 1u) ? 2u : 0u);
-    } else if (vj >= 0) {
-      f = ((uint32_t)(threadIdx.x * 16 + vj + 1) << 2) | 1u;
-    }
-  }
+                                                   unsigned* __restrict__ flags, int64_t ntiles) {
   using BR = hipcub::BlockReduce<uint32_t, WG>;
   __shared__ typename BR::TempStorage tmp;
-  const uint32_t tot = BR(tmp).Sum(c);
-  __syncthreads();
-  const uint32_t fmin = BR(tmp).Reduce(f, hipcub::Min());
-  if (na) atomicOr(flags, 1u);
-  if (threadIdx.x == 0) {
-    counts[blockIdx.x] = tot;
-    first[blockIdx.x] = fmin;
+  int64_t tile = blockIdx.x;
+  uint4 cur = tile < ntiles ? load16(buf, n, tile * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int64_t nt = tile + gridDim.x;
+    const uint4 nxt = nt < ntiles ? load16(buf, n, nt * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
+    const int64_t p0 = tile * TILE + (int64_t)threadIdx.x * 16;
+    uint32_t c = 0, na = 0, crlf = 0, m = 0, f = ~0u;
+    if (p0 < n) {
+      m = load_mask(buf, n, p0, text, &crlf, &na, cur);
+      const int vj = virtual_in(buf, n, fs, p0, text);
+      c = __popc(m) + (vj >= 0);
+      if (m) {
+        const int j = __ffs(m) - 1;
+        f = ((uint32_t)(threadIdx.x * 16 + j) << 2) | ((crlf >> j & 1u) ? 2u : 0u);
+      } else if (vj >= 0) {
+        f = ((uint32_t)(threadIdx.x * 16 + vj + 1) << 2) | 1u;
+      }
+    }
+    __syncthreads();  // the previous tile's reductions are done with tmp
+    const uint32_t tot = BR(tmp).Sum(c);
+    __syncthreads();
+    const uint32_t fmin = BR(tmp).Reduce(f, hipcub::Min());
+    if (na) atomicOr(flags, 1u);
+    if (threadIdx.x == 0) {
+      counts[tile] = tot;
+      first[tile] = fmin;
+    }
+    cur = nxt;
   }
 }
 
@@ -218,20 +230,29 @@ __global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__
   __shared__ uint32_t term[MAX_TERM];
   __shared__ Action act[MAX_TERM / 2 + 2];  // 33 KiB with term[]: 4 workgroups per CU
   __shared__ uint4 tile_bytes[TILE / 16];    // the tile itself: slices inside it copy from LDS
-  const int64_t t0 = (int64_t)blockIdx.x * TILE;
+  using BS = hipcub::BlockScan<uint32_t, WG>;
+  __shared__ typename BS::TempStorage tmp;
+  // persistent, as count_kernel: the next tile's bytes load while this one is extracted
+  int64_t tile = blockIdx.x;
+  uint4 cur = tile < ntiles ? load16(buf, n, tile * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
+  for (; tile < ntiles; tile += gridDim.x) {
+  const int64_t ntl = tile + gridDim.x;
+  const uint4 nxt = ntl < ntiles ? load16(buf, n, ntl * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
+  const int64_t t0 = tile * TILE;
   const int64_t p0 = t0 + (int64_t)threadIdx.x * 16;
   uint32_t m = 0, crlf = 0, na;
   int vj = -1;
   uint4 mine = make_uint4(0, 0, 0, 0);
   if (p0 < n) {
-    m = load_mask(buf, n, p0, text, &crlf, &na, &mine);
+    mine = cur;
+    m = load_mask(buf, n, p0, text, &crlf, &na, cur);
     vj = virtual_in(buf, n, fs, p0, text);
   }
+  cur = nxt;
+  __syncthreads();  // the previous tile's readers of tile_bytes / term / act / tmp are done
   tile_bytes[threadIdx.x] = mine;
   const uint32_t* tile32 = reinterpret_cast<const uint32_t*>(tile_bytes);
   const uint32_t c = __popc(m) + (vj >= 0);
-  using BS = hipcub::BlockScan<uint32_t, WG>;
-  __shared__ typename BS::TempStorage tmp;
   uint32_t pre, ntile;
   BS(tmp).ExclusiveSum(c, pre, ntile);
   {
@@ -246,20 +267,22 @@ __global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__
     }
   }
   __syncthreads();
-  const int64_t g0 = (int64_t)offsets[blockIdx.x];  // global number of the tile's first terminator
-  if (blockIdx.x == 0 && threadIdx.x == 0 && nrec > 0 && buf[0] != '@') atomicMin(first_bad, 0ull);
+  const int64_t g0 = (int64_t)offsets[tile];  // global number of the tile's first terminator
+  if (tile == 0 && threadIdx.x == 0 && nrec > 0 && buf[0] != '@') atomicMin(first_bad, 0ull);
   for (uint32_t t = threadIdx.x; t < ntile; t += WG) {
     const int64_t line = g0 + t + 1, r = line >> 2;
     if (r >= nrec) continue;
     const uint32_t e = term[t];
     const int64_t next = t0 + (e & T_OFF) + ((e & T_VIRT) ? 0 : 1);  // the line's start
     const int which = (int)(line & 3);
-    if (which == 0) {
-      if (buf[next] != '@') atomicMin(first_bad, (unsigned long long)r);
+    if (which == 0) {  // the '@' from the tile's LDS copy unless the line starts past the tile
+      const int64_t o = next - t0;
+      const uint8_t ch = o < TILE ? reinterpret_cast<const uint8_t*>(tile_bytes)[o] : buf[next];
+      if (ch != '@') atomicMin(first_bad, (unsigned long long)r);
     } else if (which == 1 || which == 3) {
       int64_t cend;
       int nl;
-      const uint32_t nf = blockIdx.x + 1 < ntiles ? first[blockIdx.x + 1] : ~0u;
+      const uint32_t nf = tile + 1 < ntiles ? first[tile + 1] : ~0u;
       if (t + 1 < ntile) {  // the line ends at the tile's next terminator
         const uint32_t f = term[t + 1];
         cend = t0 + (f & T_OFF) - ((f & T_CRLF) ? 1 : 0);
@@ -354,6 +377,15 @@ __global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__
       o[j] = i < b ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
     }
   }
+  }
+}
+
+// grid of the persistent tile kernels: every resident workgroup slot once (at most ntiles)
+unsigned resident_grid(const void* kernel, int64_t ntiles) {
+  int dev = 0, cus = 256, per_cu = 0;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, WG, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)cus * per_cu));
 }
 
 // The byte just past line `target` (0-based line number; its terminator is terminator
@@ -371,7 +403,7 @@ __global__ __launch_bounds__(WG) void line_end_kernel(const uint8_t* __restrict_
   uint32_t m = 0, crlf = 0, na;
   int vj = -1;
   if (p0 < n) {
-    m = load_mask(buf, n, p0, text, &crlf, &na);
+    m = load_mask(buf, n, p0, text, &crlf, &na, load16(buf, n, p0));
     vj = virtual_in(buf, n, fs, p0, text);
   }
   uint32_t bits = m | (vj >= 0 ? (1u << vj) : 0u);
@@ -453,8 +485,8 @@ extern "C" int sct_fastq_index_create(const uint8_t* d_buf, int64_t nbytes, cons
   SCT_HIP(hipMemsetAsync(d_counts, 0, (size_t)(ix->ntiles + 1) * 8, s));
   const Files fs{ix->d_ends, nfiles};
   if (nbytes > 0)
-    hipLaunchKernelGGL(count_kernel, dim3((unsigned)ix->ntiles), dim3(WG), 0, s, d_buf, nbytes, fs,
-                       ix->text, d_counts, ix->d_first, d_flags);
+    hipLaunchKernelGGL(count_kernel, dim3(resident_grid((const void*)count_kernel, ix->ntiles)), dim3(WG), 0, s,
+                       d_buf, nbytes, fs, ix->text, d_counts, ix->d_first, d_flags, ix->ntiles);
   SCT_LAUNCH_CHECK();
   SCT_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb, d_counts, ix->d_offsets, (int)(ix->ntiles + 1), s));
   unsigned long long total = 0;
@@ -503,7 +535,8 @@ extern "C" int sct_fastq_extract_spans(sct_fastq_index* ix, const uint8_t* d_buf
   if (ix->nbytes > 0) {
     SCT_CHECK(d_buf != nullptr, "buffer is NULL");
     const Files fs{ix->d_ends, ix->nfiles};
-    hipLaunchKernelGGL(extract_kernel, dim3((unsigned)ix->ntiles), dim3(WG), 0, s, d_buf, ix->nbytes, fs,
+    hipLaunchKernelGGL(extract_kernel, dim3(resident_grid((const void*)extract_kernel, ix->ntiles)), dim3(WG), 0, s,
+                       d_buf, ix->nbytes, fs,
                        ix->text, ix->d_offsets, ix->d_first, ix->ntiles, ix->nrec, sp, d_seq, d_qual,
                        d_seq_len, d_qual_len, ix->d_bad);
     SCT_LAUNCH_CHECK();
