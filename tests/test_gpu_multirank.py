@@ -106,3 +106,41 @@ def test_record_sharding_on_gpu(tmp_path):
         assert z["codes"].reshape(-1).astype(np.uint64).tolist() == ref_codes
         assert z["gc"].tolist() == [s.count(b"C") + s.count(b"G") for s in seqs]
         assert z["wide"].tolist() == O.c_hist_wide(_wide_limbs()).tolist()
+
+
+def _worker_rccl(rank, world, port, out_path):
+    """the RCCL stack as bench.py's ranks use it: nccl group bound to the device, an
+    all-reduce / all-gather / barrier of CUDA tensors, and ShardedAllPairs inside the group."""
+    import torch
+    import torch.distributed as dist
+    from sctools_amd import _lib, sharding
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    try:
+        _lib.check(_lib.lib().sct_set_device(0))
+        t = torch.arange(18, dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        rows = [torch.zeros(3, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(rows, torch.tensor([rank, 1.5, 2.5], dtype=torch.float64, device=dev))
+        dist.barrier()
+        codes = synthetic.whitelist_codes(5_000, 16, 3)
+        with sharding.ShardedAllPairs(codes, 32, _lib.SCHEME_SPECTRAL) as job:
+            hist = job.step(timing=True)
+        np.savez(out_path % rank, t=t.cpu().numpy(), rows=torch.stack(rows).cpu().numpy(), hist=hist.astype(np.int64),
+                 backend=np.array([dist.get_backend()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_group_on_gpu(tmp_path):
+    """One rank (a box has one GPU; RCCL refuses two ranks on one device): the nccl (= RCCL)
+    backend initialises bound to the device and its collectives run, as in bench.py."""
+    out = str(tmp_path / "n%d.npz")
+    mp.spawn(_worker_rccl, args=(1, _free_port(), out), nprocs=1, join=True)
+    z = np.load(out % 0)
+    assert z["t"].tolist() == list(range(18))
+    assert z["rows"].tolist() == [[0.0, 1.5, 2.5]]
+    assert str(z["backend"][0]) == "nccl"
+    assert z["hist"].tolist() == O.c_hist16(synthetic.whitelist_codes(5_000, 16, 3))[0][:17].tolist()
