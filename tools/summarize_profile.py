@@ -31,6 +31,17 @@ def pmc_means(path, kernel_substr):
     return {k: agg[k] / cnt[k] for k in agg}
 
 
+def last_calls_avg_ns(trace_csv, kernel_substr, k=5):
+    """Mean duration of the kernel's last k dispatches in the trace: for bench.py these are
+    the back-to-back launches of sct_allpairs_time_kernels, the same launches the bench
+    line's kernel_ms times with HIP events."""
+    if not os.path.exists(trace_csv):
+        return None
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace_csv))
+         if kernel_substr in r["Kernel_Name"]]
+    return sum(d[-k:]) / len(d[-k:]) if d else None
+
+
 def kernel_avg_ns(stats_csv, kernel_substr):
     for r in csv.DictReader(open(stats_csv)):
         if kernel_substr in r["Name"]:
@@ -49,6 +60,12 @@ def summarize(src, dst, rnd, name, kernel, pairs):
         return None
     m = pmc_means(src, kernel)
     out = {"kernel": kernel, "trace_avg_ns": avg_ns, "trace_calls": calls, "pmc": m}
+    if name.startswith("spectral"):
+        out["trace_time_kernels_avg_ns"] = last_calls_avg_ns(os.path.join(src, "trace", "run_kernel_trace.csv"),
+                                                             kernel)
+        out["trace_note"] = ("trace_avg_ns averages every dispatch of the profiled bench run (warm-up and "
+                             "timed steps included); trace_time_kernels_avg_ns the last 5, i.e. the "
+                             "back-to-back launches the bench line's kernel_ms times with HIP events")
     if "GRBM_GUI_ACTIVE" in m and avg_ns:
         out["clock_ghz_estimate"] = m["GRBM_GUI_ACTIVE"] / 8 / avg_ns
     if "SQ_INSTS_VALU" in m:
