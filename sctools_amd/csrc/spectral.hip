@@ -1177,7 +1177,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
 //     transforms per slice (4 planes + the sum), no exchange between planes.
 // Weight of (P', Q', R'): digits of l & 3, (l >> 2) & 3, l >> 4 (thread constant) + qn + q2
 // + i2 (compile time) + the slice's + [R' != 0].
-template <bool PF, int ABL = 0>
+// QP: two quarters' chains interleaved in one wave (stage 1 of both, then both splits, then
+// both high-byte and both low-byte stage-2 MFMA groups), for MFMA/VALU overlap inside a wave.
+template <bool PF, int ABL = 0, int QP = 0>
 __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, const uint16_t* __restrict__ order,
                                               int z0, int nslices, unsigned long long* __restrict__ counts,
                                               unsigned long long add_n) {
@@ -1258,6 +1260,52 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
               (unsigned long long)((int64_t)c[q2][i] * c[q2][i]);
       }
   };
+  auto split = [&](const v4i_t* c1, v2l_t& Bl, v2l_t& Bh) {
+    uint32_t lo[4], hi[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const uint32_t t1 = __builtin_amdgcn_perm((uint32_t)c1[mt][1], (uint32_t)c1[mt][0], 0x05010400u);
+      const uint32_t t2 = __builtin_amdgcn_perm((uint32_t)c1[mt][3], (uint32_t)c1[mt][2], 0x05010400u);
+      lo[mt] = __builtin_amdgcn_perm(t2, t1, 0x05040100u) ^ 0x80808080u;
+      hi[mt] = __builtin_amdgcn_perm(t2, t1, 0x07060302u);
+    }
+    Bl = v2l_t{(long)(((uint64_t)lo[1] << 32) | lo[0]), (long)(((uint64_t)lo[3] << 32) | lo[2])};
+    Bh = v2l_t{(long)(((uint64_t)hi[1] << 32) | hi[0]), (long)(((uint64_t)hi[3] << 32) | hi[2])};
+  };
+  // two quarters qa, qb at once (QP); `between` runs after the last MFMAs are issued and
+  // before the squares (QP 2: the next pair's stage 1)
+  auto stage2x2 = [&](const v4i_t* c1a, const v4i_t* c1b, auto qa_c, auto qb_c, unsigned long long* acc,
+                      auto&& between) {
+    constexpr int qa = decltype(qa_c)::value, qb = decltype(qb_c)::value;
+    v2l_t Bla, Bha, Blb, Bhb;
+    split(c1a, Bla, Bha);
+    split(c1b, Blb, Bhb);
+    v4i_t ca[4], cb[4];
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2) {
+      ca[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bha, v4i_t{0, 0, 0, 0}, 0, 0, 0);
+      cb[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bhb, v4i_t{0, 0, 0, 0}, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ca[q2][i] <<= 8;
+      ca[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bla, ca[q2], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cb[q2][i] <<= 8;
+      cb[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Blb, cb[q2], 0, 0, 0);
+    }
+    between();
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[digit_weight_c((uint32_t)qa) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
+            (unsigned long long)((int64_t)ca[q2][i] * ca[q2][i]);
+        acc[digit_weight_c((uint32_t)qb) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
+            (unsigned long long)((int64_t)cb[q2][i] * cb[q2][i]);
+      }
+  };
   // planes in turn (a runtime loop: one plane's 16 VGPRs of bytes live at a time, PF: the
   // next plane's loads in flight), the per-plane sums of all four quarters carried across
   for (int u = ub; u < ue; ++u) {
@@ -1295,15 +1343,67 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
         stage2(c1, qn_c, accB);
         __builtin_amdgcn_sched_barrier(0);
       };
-      quarter(std::integral_constant<int, 0>());
-      quarter(std::integral_constant<int, 1>());
-      quarter(std::integral_constant<int, 2>());
-      quarter(std::integral_constant<int, 3>());
+      auto quarters = [&](auto qa_c, auto qb_c) {
+        constexpr int qa = decltype(qa_c)::value, qb = decltype(qb_c)::value;
+        v4i_t c1a[4], c1b[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          c1a[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qa], v4i_t{128, 128, 128, 128}, 0, 0, 0);
+          c1b[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qb], v4i_t{128, 128, 128, 128}, 0, 0, 0);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          cs[qa][mt] += c1a[mt];
+          cs[qb][mt] += c1b[mt];
+        }
+        stage2x2(c1a, c1b, qa_c, qb_c, accB, [] {});
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      if constexpr (QP == 2) {
+        v4i_t c1[4][4];
+        auto s1 = [&](int q) {
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            c1[q][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[q], v4i_t{128, 128, 128, 128}, 0, 0, 0);
+          }
+        };
+        s1(0);
+        s1(1);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          cs[0][mt] += c1[0][mt];
+          cs[1][mt] += c1[1][mt];
+        }
+        stage2x2(c1[0], c1[1], std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), accB, [&] {
+          s1(2);
+          s1(3);
+        });
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          cs[2][mt] += c1[2][mt];
+          cs[3][mt] += c1[3][mt];
+        }
+        stage2x2(c1[2], c1[3], std::integral_constant<int, 2>(), std::integral_constant<int, 3>(), accB, [] {});
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (QP) {
+        quarters(std::integral_constant<int, 0>(), std::integral_constant<int, 1>());
+        quarters(std::integral_constant<int, 2>(), std::integral_constant<int, 3>());
+      } else {
+        quarter(std::integral_constant<int, 0>());
+        quarter(std::integral_constant<int, 1>());
+        quarter(std::integral_constant<int, 2>());
+        quarter(std::integral_constant<int, 3>());
+      }
     }
-    stage2(cs[0], std::integral_constant<int, 0>(), accA);
-    stage2(cs[1], std::integral_constant<int, 1>(), accA);
-    stage2(cs[2], std::integral_constant<int, 2>(), accA);
-    stage2(cs[3], std::integral_constant<int, 3>(), accA);
+    if constexpr (QP) {
+      stage2x2(cs[0], cs[1], std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), accA, [] {});
+      stage2x2(cs[2], cs[3], std::integral_constant<int, 2>(), std::integral_constant<int, 3>(), accA, [] {});
+    } else {
+      stage2(cs[0], std::integral_constant<int, 0>(), accA);
+      stage2(cs[1], std::integral_constant<int, 1>(), accA);
+      stage2(cs[2], std::integral_constant<int, 2>(), accA);
+      stage2(cs[3], std::integral_constant<int, 3>(), accA);
+    }
   }
   if (cur_w >= 0) flush();
   __syncthreads();
@@ -1316,6 +1416,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
     unsigned long long* __restrict__ counts, unsigned long long add_n) {
   tile_reg_body<true>(buf, order, z0, nslices, counts, add_n);
+}
+// two quarters per MFMA chain group (QP above)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_qp_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<true, 0, 1>(buf, order, z0, nslices, counts, add_n);
+}
+// the same with the second pair's stage 1 issued before the first pair's squares
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_qp2_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<true, 0, 2>(buf, order, z0, nslices, counts, add_n);
 }
 // A/B: 2 waves per SIMD without the prefetch; 3 waves per SIMD (a few registers spilled)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_np_kernel(
@@ -1701,6 +1813,10 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
           hipLaunchKernelGGL(tile_reg_np_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
         else if (st.tile_reg == 3)
           hipLaunchKernelGGL(tile_reg_w3_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+        else if (st.tile_reg == 4)
+          hipLaunchKernelGGL(tile_reg_qp_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+        else if (st.tile_reg == 5)
+          hipLaunchKernelGGL(tile_reg_qp2_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
         else
           hipLaunchKernelGGL(tile_reg_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
       } else {
@@ -1795,10 +1911,15 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
     // 0.320 ms per 65536 slices, count 2.39 vs 2.47 ms); "mfma2" = the LDS-exchange tile,
     // reg_np / reg_w3 = register-tile ablations
     const char* tv = getenv("SCT_SPECTRAL_TILE");
-    st.tile_reg = !tv ? 1 : !strcmp(tv, "mfma2") ? 0 : !strcmp(tv, "reg_np") ? 2 : !strcmp(tv, "reg_w3") ? 3 : 1;
+    // (round 2, later: "reg_qp", two quarters' MFMA chains interleaved, is the default: 0.286-0.296
+    // vs 0.291-0.306 ms on two boxes; "reg" = one quarter at a time)
+    st.tile_reg = !tv ? 4 : !strcmp(tv, "mfma2") ? 0 : !strcmp(tv, "reg_np") ? 2 : !strcmp(tv, "reg_w3") ? 3
+                : !strcmp(tv, "reg") ? 1 : !strcmp(tv, "reg_qp2") ? 5 : 4;
     int per_cu_reg = 0;  // its resident workgroups per CU
     const void* kf = st.tile_reg == 2 ? (const void*)tile_reg_np_kernel
-                     : st.tile_reg == 3 ? (const void*)tile_reg_w3_kernel : (const void*)tile_reg_kernel;
+                     : st.tile_reg == 3 ? (const void*)tile_reg_w3_kernel
+                     : st.tile_reg == 4 ? (const void*)tile_reg_qp_kernel
+                     : st.tile_reg == 5 ? (const void*)tile_reg_qp2_kernel : (const void*)tile_reg_kernel;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_reg, kf, 256, 0) != hipSuccess || per_cu_reg <= 0)
       per_cu_reg = 2;
     st.tile_reg_wgs = per_cu_reg;

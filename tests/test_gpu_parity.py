@@ -411,7 +411,7 @@ def test_allpairs_spectral_scheme_matches_oracle(n, width, monkeypatch):
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
-@pytest.mark.parametrize("tile,seed,overlap", [("reg", "", "0"), ("mfma2", "", "0"), ("reg_np", "", "0"),
+@pytest.mark.parametrize("tile,seed,overlap", [("reg", "", "0"), ("reg_qp", "", "0"), ("reg_qp2", "", "0"), ("mfma2", "", "0"), ("reg_np", "", "0"),
                                                ("reg_w3", "", "0"), ("reg", "walk", "0"), ("reg", "mx", "0"),
                                                ("reg", "spread", "0"), ("reg", "walk", "1"), ("reg", "mx", "1")])
 def test_allpairs_spectral_kernel_variants(tile, seed, overlap, monkeypatch):
@@ -442,6 +442,27 @@ def test_allpairs_spectral_column_sizes(seed, monkeypatch):
         parts.append((hi << np.uint64(14)) | np.uint64(col))
     codes = np.concatenate(parts)
     hist = _spectral_hist(codes, [(0, 300), (300, 8191), (8191, 1 << 18)])
+    assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
+
+
+@pytest.mark.parametrize("tile", ["reg", "reg_qp", "reg_qp2"])
+def test_allpairs_spectral_high_energy_planes(tile, monkeypatch):
+    """Planes (column bits 12, 13) of large seeds in every slice -- 120 columns of 120 codes,
+    110 of them sharing their high bits, in planes 0 and 2 -- beside sparse ones (squares
+    above 2^32 per plane, |G| above 2^16)."""
+    monkeypatch.setenv("SCT_SPECTRAL_TILE", tile)
+    rng = np.random.default_rng(33)
+    bg = synthetic.whitelist_codes(5000, 16, seed=8)
+    parts = []
+    dense = np.concatenate([rng.choice(4096, 120, replace=False), 8192 + rng.choice(4096, 120, replace=False)])
+    bg = bg[~np.isin(bg & np.uint64(0x3FFF), dense.astype(np.uint64))]
+    parts.append(bg)
+    for col in dense:
+        hi = np.full(120, rng.integers(0, 1 << 18), dtype=np.uint64)
+        hi[110:] = rng.integers(0, 1 << 18, 10).astype(np.uint64)
+        parts.append((hi << np.uint64(14)) | np.uint64(col))
+    codes = np.concatenate(parts)
+    hist = _spectral_hist(codes, [(0, 5000), (5000, 1 << 18)])
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
