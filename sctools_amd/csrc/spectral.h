@@ -32,6 +32,7 @@ struct State {
   bool seed_spread = false;      // int8 seeds: stores spread over the walk (16-slice blocks)
   void* d_mx = nullptr;          // int8 seeds: the MFMA seed's operand tables (null: the walk seed)
   int mx_form = 2;               // the MFMA seed's workgroup shape (A/B)
+  int ilv = 0;                   // int8: the direct MFMA seed + G-slice interleaved intermediate (G)
   // seed / tile overlap: chunk j+1's seed (side stream, second buffer) runs beside chunk j's tile
   bool overlap = false;
   void* d_buf2 = nullptr;

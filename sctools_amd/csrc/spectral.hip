@@ -269,6 +269,14 @@ __device__ __forceinline__ int column_pos(int c) {
          ((c >> 12) << 12);
 }
 
+// The G-slice interleaved int8 layout (direct MFMA seed + ILV register tile), G = 4, 8, 16:
+// slice-relative index zr and 16-column block b; the 16-B chunks of G consecutive slices of one
+// block are contiguous (16 G bytes).  A group of G slices is G x 16 KB.
+template <int G>
+__device__ __forceinline__ size_t ilv_off(int zr, int b) {
+  return ((size_t)(zr / G) * (kLo / 16) + b) * (16 * G) + (zr % G) * 16;
+}
+
 // Byte (int8) / half (int16) transposes for the seed's store-out: p dwords hold P values of
 // consecutive slices for one column each; out[j] = the j-th values of all of them, packed.
 __device__ __forceinline__ void transpose4x4_bytes(const uint32_t* d, uint32_t* out) {
@@ -1179,7 +1187,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
 // + i2 (compile time) + the slice's + [R' != 0].
 // QP: two quarters' chains interleaved in one wave (stage 1 of both, then both splits, then
 // both high-byte and both low-byte stage-2 MFMA groups), for MFMA/VALU overlap inside a wave.
-template <bool PF, int ABL = 0, int QP = 0>
+// ILV = G > 0: the intermediate in the G-slice interleaved layout (ilv_off<G>, written by the
+// direct MFMA seed).  A team of G / 4 workgroups -- blocks b, b + 8, ..: the same XCD under the
+// round-robin dispatch -- takes the G slices of one group at a time (workgroup k of the team,
+// wave w: slice G g + 4 k + w), so every 16 G-byte piece a wave reads 16 B of is read whole by
+// its team while it sits in that XCD's L2.
+template <bool PF, int ABL = 0, int QP = 0, int ILV = 0>
 __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, const uint16_t* __restrict__ order,
                                               int z0, int nslices, unsigned long long* __restrict__ counts,
                                               unsigned long long add_n) {
@@ -1205,9 +1218,14 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
   }
   const int wt_thread = digit_weight((uint32_t)(lane & 15)) + digit_weight((uint32_t)(lane >> 4));
   const int lane_off = 16 * (lane >> 4) + 64 * (lane & 15);
-  // each wave of the grid takes a contiguous run of slice positions
-  const int gw = blockIdx.x * 4 + wave, GW = gridDim.x * 4;
-  const int ub = (int)((int64_t)nslices * gw / GW), ue = (int)((int64_t)nslices * (gw + 1) / GW);
+  // each wave of the grid takes a contiguous run of slice positions (ILV: each workgroup a
+  // contiguous run of 4-slice group positions)
+  constexpr int TS = ILV ? ILV / 4 : 1;  // workgroups per team
+  const int team_k = ILV ? (int)(blockIdx.x / 8) % TS : 0;
+  const int gw = ILV ? (int)(blockIdx.x / (8 * TS)) * 8 + (int)(blockIdx.x % 8) : blockIdx.x * 4 + wave;
+  const int GW = ILV ? (int)gridDim.x / TS : gridDim.x * 4;
+  const int nunits = ILV ? (nslices + ILV - 1) / ILV : nslices;
+  const int ub = (int)((int64_t)nunits * gw / GW), ue = (int)((int64_t)nunits * (gw + 1) / GW);
   unsigned long long accA[4] = {0, 0, 0, 0}, accB[4] = {0, 0, 0, 0};
   int cur_w = -1;
   auto flush = [&]() {
@@ -1221,9 +1239,16 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
     }
   };
   auto load_plane = [&](int sl, int R, v2l_t* dst) {
-    const int8_t* p = buf + (int64_t)sl * kLo + lane_off + 4096 * R;
+    if constexpr (ILV) {
+      const int8_t* p = buf + ilv_off<(ILV ? ILV : 4)>(sl, (lane >> 4) + 4 * (lane & 15) + 256 * R);
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) dst[mt] = __builtin_nontemporal_load(reinterpret_cast<const v2l_t*>(p + 1024 * mt));
+      for (int mt = 0; mt < 4; ++mt) dst[mt] = *reinterpret_cast<const v2l_t*>(p + 64 * 16 * ILV * mt);
+    } else {
+      const int8_t* p = buf + (int64_t)sl * kLo + lane_off + 4096 * R;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        dst[mt] = __builtin_nontemporal_load(reinterpret_cast<const v2l_t*>(p + 1024 * mt));
+    }
   };
   // stage 2 of 16 values per lane (c1[mt][i] = v + 128 of stage 1, one quarter qn) -> squares
   auto stage2 = [&](const v4i_t* c1, auto qn_c, unsigned long long* acc) {
@@ -1309,7 +1334,11 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
   // planes in turn (a runtime loop: one plane's 16 VGPRs of bytes live at a time, PF: the
   // next plane's loads in flight), the per-plane sums of all four quarters carried across
   for (int u = ub; u < ue; ++u) {
-    const int s = order ? (int)order[u] : u;
+    int s = order ? (int)order[u] : u;
+    if constexpr (ILV) {
+      s = ILV * s + 4 * team_k + wave;
+      if (s >= nslices) continue;
+    }
     const int wz = digit_weight((uint32_t)(z0 + s));  // wave-uniform
     if (wz != cur_w) {
       if (cur_w >= 0) flush();
@@ -1428,6 +1457,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
     unsigned long long* __restrict__ counts, unsigned long long add_n) {
   tile_reg_body<true, 0, 2>(buf, order, z0, nslices, counts, add_n);
+}
+// the same on the 4-slice interleaved intermediate (the direct MFMA seed's layout)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_ilv_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<true, 0, 1, 4>(buf, order, z0, nslices, counts, add_n);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_ilv8_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<true, 0, 1, 8>(buf, order, z0, nslices, counts, add_n);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_ilv16_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<true, 0, 1, 16>(buf, order, z0, nslices, counts, add_n);
 }
 // A/B: 2 waves per SIMD without the prefetch; 3 waves per SIMD (a few registers spilled)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_np_kernel(
@@ -1647,6 +1692,85 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(C == 16 
   }
 }
 
+// The MFMA seed storing straight into the 4-slice interleaved layout (ilv_off): no LDS stage
+// and no barrier.  Lane l's chunk for row q is slice r 256 + (4 (l >> 4) + q) 16 + (l & 15) of
+// the wave's 16-column block, so lanes 4k .. 4k + 3 write one contiguous 64-B piece and the
+// neighbouring wave (the next block) the other half of its 128-B line.  Workgroup = W waves
+// (16 W consecutive columns) x one walk segment of 2^kMxSegBits r values (blockIdx.y).
+template <int W, int G>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2))) void seed_mxd_kernel(
+    const v2l_t* __restrict__ opa, const v2l_t* __restrict__ opb, const v2l_t* __restrict__ opm,
+    const uint32_t* __restrict__ off, int z0, int z1, int8_t* __restrict__ buf) {
+  constexpr int C = 16, S = 1 << kMxSegBits;
+  __shared__ v2l_t pm_s[W][kMxSegBits][C][4];  // the walk's planes (block 0)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4;
+  const int c0 = (blockIdx.x * W + wv) * C, seg = blockIdx.y;
+  for (int e = lane; e < C * kMxSegBits * 4; e += 64) {
+    const int cc = e % C, gg = (e / C) & 3, bb = e / (4 * C);
+    pm_s[wv][bb][cc][gg] = opm[mx_pm(c0 + cc, 0, bb, gg)];
+  }
+  unsigned ovf = 0;  // columns with more than 64 codes
+#pragma unroll
+  for (int cc = 0; cc < C; ++cc) ovf |= (unsigned)(off[c0 + cc + 1] - off[c0 + cc] > 64) << cc;
+  ovf = __builtin_amdgcn_readfirstlane(ovf);
+  v2l_t B[C];
+#pragma unroll
+  for (int cc = 0; cc < C; ++cc) B[cc] = opb[mx_op(c0 + cc, 0, lane)];
+  const int rs = ((z0 >> 8) & ~(S - 1)) + seg * S;  // the launch sizes the grid to the range
+  v2l_t A[C];
+#pragma unroll
+  for (int cc = 0; cc < C; ++cc) A[cc] = opa[mx_op(c0 + cc, 0, lane)];
+  for (int bb = kMxSegBits; bb < kMxRBits; ++bb)
+    if ((rs >> bb) & 1)
+#pragma unroll
+      for (int cc = 0; cc < C; ++cc) A[cc] ^= opm[mx_pm(c0 + cc, 0, bb, g)];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // pm_s: this wave's own writes
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  int8_t* bw = buf + ilv_off<G>(0, c0 >> 4);
+#pragma unroll 1
+  for (int i = 0; i < S; ++i) {
+    if (i) {
+      const int bb = __builtin_ctz(i);
+#pragma unroll
+      for (int cc = 0; cc < C; ++cc) A[cc] ^= pm_s[wv][bb][cc][g];
+    }
+    const int r = rs ^ (i ^ (i >> 1));
+    if (r * 256 + 255 < z0 || r * 256 >= z1) continue;
+    uint32_t w[4][4];  // [slice row 4 g + q][columns 4 k .. 4 k + 3]: low bytes of the products
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v4i_t acc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[4 * k + u], B[4 * k + u], v4i_t{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        w[q][k] = __builtin_amdgcn_perm((uint32_t)acc[1][q], (uint32_t)acc[0][q], 0x0c0c0400u) |
+                  __builtin_amdgcn_perm((uint32_t)acc[3][q], (uint32_t)acc[2][q], 0x04000c0cu);
+    }
+    for (unsigned ov = ovf; ov; ov &= ov - 1) {  // columns with codes 64..: add their products
+      const int cc = __builtin_ctz(ov);
+      const v4i_t a1 = seed_mx_block1(opa, opb, opm, c0 + cc, r, lane, v4i_t{0, 0, 0, 0});
+      const int sh = 8 * (cc & 3);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k == (cc >> 2))
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // byte add mod 256: |D| <= 127, so the int8 sum is exact
+            const uint32_t t = ((w[q][k] >> sh) + (uint32_t)a1[q]) & 0xFFu;
+            w[q][k] = (w[q][k] & ~(0xFFu << sh)) | (t << sh);
+          }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int z = r * 256 + (4 * g + q) * 16 + (lane & 15);
+      if (z >= z0 && z < z1)
+        *reinterpret_cast<uint4*>(bw + ilv_off<G>(z - z0, 0)) = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
+    }
+  }
+}
+
 __global__ void max_column_kernel(const uint32_t* __restrict__ cnt, unsigned* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < kLo) atomicMax(out, cnt[c]);
@@ -1712,7 +1836,20 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
   if (sabl < 1 || sabl > 10)
 #endif
   {
-    if (sizeof(T) == 1 && st.d_mx) {
+    if (sizeof(T) == 1 && st.d_mx && st.ilv) {
+      const MxTables mx = mx_tables(st);
+      const int ra = (z0 >> 8) & ~((1 << kMxSegBits) - 1), rend = ((z1 - 1) >> 8) + 1;
+      const int nseg = (rend - ra + (1 << kMxSegBits) - 1) >> kMxSegBits;
+      constexpr int W = 4;
+      const dim3 xg(kLo / (16 * W), (unsigned)nseg);
+      int8_t* b8 = reinterpret_cast<int8_t*>(buf);
+      if (st.ilv == 16)
+        hipLaunchKernelGGL((seed_mxd_kernel<W, 16>), xg, dim3(64 * W), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1, b8);
+      else if (st.ilv == 8)
+        hipLaunchKernelGGL((seed_mxd_kernel<W, 8>), xg, dim3(64 * W), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1, b8);
+      else
+        hipLaunchKernelGGL((seed_mxd_kernel<W, 4>), xg, dim3(64 * W), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1, b8);
+    } else if (sizeof(T) == 1 && st.d_mx) {
       const MxTables mx = mx_tables(st);
       const int ra = (z0 >> 8) & ~((1 << kMxSegBits) - 1), rend = ((z1 - 1) >> 8) + 1;
       const int nseg = (rend - ra + (1 << kMxSegBits) - 1) >> kMxSegBits;
@@ -1807,7 +1944,21 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
         return SCT_OK;
       }
 #endif
-      if (st.tile_reg) {
+      if (st.ilv) {
+        const int G = st.ilv, ts = G / 4;  // G-slice groups, in digit-weight order when aligned
+        const int ng = (z1 - z0 + G - 1) / G;
+        const uint16_t* gorder = ((ng & (ng - 1)) == 0 && ng <= kMaxOrder && z0 % G == 0 && (z0 / G) % ng == 0)
+                                     ? st.d_order + ng : nullptr;
+        // teams of ts workgroups 8 apart in dispatch order; whole rounds of 8 teams
+        const int teams = std::max(1, std::min(st.grid * st.tile_reg_wgs / ts, ng));
+        const dim3 igrid((unsigned)(8 * ts * ((teams + 7) / 8)));
+        const void* kf = G == 16 ? (const void*)tile_reg_ilv16_kernel
+                         : G == 8 ? (const void*)tile_reg_ilv8_kernel : (const void*)tile_reg_ilv_kernel;
+        void* args[] = {(void*)&buf, (void*)&gorder, (void*)&z0, nullptr, (void*)&counts, (void*)&add_n};
+        int ns = z1 - z0;
+        args[3] = (void*)&ns;
+        SCT_HIP(hipLaunchKernel(kf, igrid, dim3(256), args, 0, s));
+      } else if (st.tile_reg) {
         const dim3 rgrid((unsigned)std::max(1, std::min(st.grid * st.tile_reg_wgs, (z1 - z0 + 3) / 4)));
         if (st.tile_reg == 2)
           hipLaunchKernelGGL(tile_reg_np_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
@@ -1905,7 +2056,10 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
     // "spread" = the walk with its stores spread over the walk
     const char* sv = getenv("SCT_SPECTRAL_SEED");
     st.seed_spread = sv && !strcmp(sv, "spread");
-    seed_mx = sv && !strcmp(sv, "mx");
+    seed_mx = sv && (!strcmp(sv, "mx") || !strcmp(sv, "mxd"));
+    st.ilv = sv && !strcmp(sv, "mxd") ? 4 : 0;
+    if (st.ilv)
+      if (const char* g = getenv("SCT_SPECTRAL_ILV")) st.ilv = atoi(g) == 16 ? 16 : atoi(g) == 8 ? 8 : 4;
     if (const char* f = getenv("SCT_SPECTRAL_MX_FORM")) st.mx_form = atoi(f);
     // tile variant: the register-resident tile by default (r02 A/B on the 737K headline: 0.304 vs
     // 0.320 ms per 65536 slices, count 2.39 vs 2.47 ms); "mfma2" = the LDS-exchange tile,
@@ -1944,11 +2098,13 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   SCT_HIP(hipMalloc(&st.d_gofs, (size_t)(kLo + 1) * 4));
   SCT_HIP(hipMalloc(&st.d_hist, (size_t)kSortWGs * kLo * 4));
   SCT_HIP(hipMalloc(&st.d_planes, (size_t)st.max_groups * kHiBits * 4));
-  SCT_HIP(hipMalloc(&st.d_buf, (size_t)st.chunk * kLo * st.elem_bytes));
+  if (st.elem_bytes != 1) st.ilv = 0;
+  const size_t buf_bytes = (size_t)((st.chunk + 15) & ~15ll) * kLo * st.elem_bytes;  // whole 16-slice groups
+  SCT_HIP(hipMalloc(&st.d_buf, buf_bytes));
   if (seed_mx && st.elem_bytes == 1) SCT_HIP(hipMalloc(&st.d_mx, kMxBytes));  // 84 MB
   if (const char* ov = getenv("SCT_SPECTRAL_OVERLAP")) st.overlap = atoi(ov) != 0;
   if (st.overlap) {
-    SCT_HIP(hipMalloc(&st.d_buf2, (size_t)st.chunk * kLo * st.elem_bytes));
+    SCT_HIP(hipMalloc(&st.d_buf2, buf_bytes));
     SCT_HIP(hipStreamCreateWithFlags(&st.side, hipStreamNonBlocking));
     for (auto& e : st.ev) SCT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }

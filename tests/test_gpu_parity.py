@@ -413,7 +413,8 @@ def test_allpairs_spectral_scheme_matches_oracle(n, width, monkeypatch):
 
 @pytest.mark.parametrize("tile,seed,overlap", [("reg", "", "0"), ("reg_qp", "", "0"), ("reg_qp2", "", "0"), ("mfma2", "", "0"), ("reg_np", "", "0"),
                                                ("reg_w3", "", "0"), ("reg", "walk", "0"), ("reg", "mx", "0"),
-                                               ("reg", "spread", "0"), ("reg", "walk", "1"), ("reg", "mx", "1")])
+                                               ("reg", "spread", "0"), ("reg", "walk", "1"), ("reg", "mx", "1"),
+                                               ("reg", "mxd", "0"), ("reg", "mxd", "1")])
 def test_allpairs_spectral_kernel_variants(tile, seed, overlap, monkeypatch):
     """Every tile / seed kernel variant, with and without the seed / tile overlap over two
     streams, gives the oracle's histogram, with 1000-slice chunks (seams inside the range)."""
@@ -426,7 +427,22 @@ def test_allpairs_spectral_kernel_variants(tile, seed, overlap, monkeypatch):
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
-@pytest.mark.parametrize("seed", ["mx", "walk"])
+@pytest.mark.parametrize("group", ["4", "8", "16"])
+def test_allpairs_spectral_interleaved_groups(group, monkeypatch):
+    """The direct MFMA seed into the G-slice interleaved intermediate and the team-of-
+    workgroups tile reading it, G = 4 / 8 / 16: unaligned slice ranges (partial groups at
+    both ends), 1000-slice chunks, duplicates and complements."""
+    monkeypatch.setenv("SCT_SPECTRAL_SEED", "mxd")
+    monkeypatch.setenv("SCT_SPECTRAL_ILV", group)
+    codes = synthetic.whitelist_codes(25_000, 16, seed=int(group))
+    codes = np.concatenate([codes, codes[:4], codes[4:6] ^ np.uint64(0xFFFFFFFF)])
+    hist = _spectral_hist(codes, [(0, 333), (333, 70_001), (70_001, 1 << 18)], chunk=1000, monkeypatch=monkeypatch)
+    assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
+    full = _spectral_hist(codes)
+    assert full.tolist() == hist.tolist()
+
+
+@pytest.mark.parametrize("seed", ["mx", "walk", "mxd"])
 def test_allpairs_spectral_column_sizes(seed, monkeypatch):
     """Columns (low 14 bits) holding 63, 64, 65, 100 and 127 codes -- the MFMA seed's one- and
     two-block columns and the int8 limit -- next to sparse ones, duplicates included; slice
