@@ -200,7 +200,7 @@ def spectral_roofline(tk, step_count_ms, my_slices):
     per_launch = tk["units"]
     launches = -(-my_slices // per_launch)
     algo_bytes = per_launch * (1 << 14)
-    kern = {"tile": {"kernel": "sct_spectral::tile_reg_qp_kernel (int8 seeds)", "ms": tk["kernel_ms"],
+    kern = {"tile": {"kernel": "sct_spectral::tile_reg_p16_kernel (int8 seeds)", "ms": tk["kernel_ms"],
                      "traffic": _traffic("pmc_spectral_latest.json")},
             "seed": {"kernel": "sct_spectral::seed_kernel<int8_t>", "ms": tk["seed_ms"],
                      "traffic": _traffic("pmc_spectral_seed_latest.json")}}

@@ -789,6 +789,11 @@ __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, in
 // thread bits are whole 2-bit digits -- and the F^2 binning.
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef long v2l_t __attribute__((ext_vector_type(2)));
+typedef short v2s_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2l_t pack_v2l(const uint32_t* w) {
+  return v2l_t{(long)(((uint64_t)w[1] << 32) | w[0]), (long)(((uint64_t)w[3] << 32) | w[2])};
+}
+
 
 // dword of the int16 pair holding column e: bits 0..4 = e1^e4, e2, e3^e5, e8^e6, e7, then
 // e4, e5, e6, e9..e13.  Conflict-free for the packed b32 stores (32-lane groups: e bits 2,
@@ -1299,12 +1304,9 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
   };
   // two quarters qa, qb at once (QP); `between` runs after the last MFMAs are issued and
   // before the squares (QP 2: the next pair's stage 1)
-  auto stage2x2 = [&](const v4i_t* c1a, const v4i_t* c1b, auto qa_c, auto qb_c, unsigned long long* acc,
-                      auto&& between) {
+  auto stage2x2B = [&](const v2l_t& Bla, const v2l_t& Bha, const v2l_t& Blb, const v2l_t& Bhb, auto qa_c,
+                       auto qb_c, unsigned long long* acc, auto&& between) {
     constexpr int qa = decltype(qa_c)::value, qb = decltype(qb_c)::value;
-    v2l_t Bla, Bha, Blb, Bhb;
-    split(c1a, Bla, Bha);
-    split(c1b, Blb, Bhb);
     v4i_t ca[4], cb[4];
 #pragma unroll
     for (int q2 = 0; q2 < 4; ++q2) {
@@ -1331,6 +1333,52 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
             (unsigned long long)((int64_t)cb[q2][i] * cb[q2][i]);
       }
   };
+  // one quarter from its split (QP 4)
+  auto stage2B = [&](const v2l_t& Bl, const v2l_t& Bh, auto qn_c, unsigned long long* acc) {
+    constexpr int qn = decltype(qn_c)::value;
+    v4i_t c[4];
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2) c[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bh, v4i_t{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) c[q2][i] <<= 8;
+      c[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bl, c[q2], 0, 0, 0);
+    }
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[digit_weight_c((uint32_t)qn) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
+            (unsigned long long)((int64_t)c[q2][i] * c[q2][i]);
+  };
+  auto stage2x2 = [&](const v4i_t* c1a, const v4i_t* c1b, auto qa_c, auto qb_c, unsigned long long* acc,
+                      auto&& between) {
+    v2l_t Bla, Bha, Blb, Bhb;
+    split(c1a, Bla, Bha);
+    split(c1b, Blb, Bhb);
+    stage2x2B(Bla, Bha, Blb, Bhb, qa_c, qb_c, acc, between);
+  };
+  // QP 3: the split through int16 pairs (|v + 128| < 2^15), which are also what the plane sums
+  // accumulate: cs as packed int16 (sum over the planes of v + 128 from -384 stays within
+  // +-32,640), 32 VGPRs instead of 64
+  auto split16 = [&](const uint32_t (*pr)[2], v2l_t& Bl, v2l_t& Bh) {
+    uint32_t lo[4], hi[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      lo[mt] = __builtin_amdgcn_perm(pr[mt][1], pr[mt][0], 0x06040200u) ^ 0x80808080u;
+      hi[mt] = __builtin_amdgcn_perm(pr[mt][1], pr[mt][0], 0x07050301u);
+    }
+    Bl = pack_v2l(lo);
+    Bh = pack_v2l(hi);
+  };
+  auto pairs16 = [&](const v4i_t* c1, uint32_t (*pr)[2]) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      pr[mt][0] = __builtin_amdgcn_perm((uint32_t)c1[mt][1], (uint32_t)c1[mt][0], 0x05040100u);
+      pr[mt][1] = __builtin_amdgcn_perm((uint32_t)c1[mt][3], (uint32_t)c1[mt][2], 0x05040100u);
+    }
+  };
   // planes in turn (a runtime loop: one plane's 16 VGPRs of bytes live at a time, PF: the
   // next plane's loads in flight), the per-plane sums of all four quarters carried across
   for (int u = ub; u < ue; ++u) {
@@ -1344,11 +1392,20 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
       if (cur_w >= 0) flush();
       cur_w = wz;
     }
-    v4i_t cs[4][4];  // [qn][mt]: sum over the planes of v + 128, from -384 (-> sum v + 128)
+    constexpr bool P16 = QP == 3 || QP == 4;
+    v4i_t cs[P16 ? 1 : 4][4];  // [qn][mt]: sum over the planes of v + 128, from -384 (-> sum v + 128)
+    uint32_t csp[P16 ? 4 : 1][4][2];  // QP 3, 4: the same as int16 pairs
+    if constexpr (P16) {
 #pragma unroll
-    for (int qn = 0; qn < 4; ++qn)
+      for (int qn = 0; qn < 4; ++qn)
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) cs[qn][mt] = v4i_t{-384, -384, -384, -384};
+        for (int mt = 0; mt < 4; ++mt) csp[qn][mt][0] = csp[qn][mt][1] = 0xFE80FE80u;
+    } else {
+#pragma unroll
+      for (int qn = 0; qn < (P16 ? 1 : 4); ++qn)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) cs[qn][mt] = v4i_t{-384, -384, -384, -384};
+    }
     v2l_t dn[4];
     if constexpr (PF) load_plane(s, 0, dn);
 #pragma unroll 1
@@ -1388,7 +1445,60 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
         stage2x2(c1a, c1b, qa_c, qb_c, accB, [] {});
         __builtin_amdgcn_sched_barrier(0);
       };
-      if constexpr (QP == 2) {
+      if constexpr (QP == 4) {
+        auto quarter16 = [&](auto qn_c) {
+          constexpr int qn = decltype(qn_c)::value;
+          v4i_t c1[4];
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+            c1[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qn], v4i_t{128, 128, 128, 128}, 0, 0, 0);
+          uint32_t pa[4][2];
+          pairs16(c1, pa);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+              csp[qn][mt][h] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s_t, csp[qn][mt][h]) +
+                                                                __builtin_bit_cast(v2s_t, pa[mt][h]));
+          v2l_t Bl, Bh;
+          split16(pa, Bl, Bh);
+          stage2B(Bl, Bh, qn_c, accB);
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        quarter16(std::integral_constant<int, 0>());
+        quarter16(std::integral_constant<int, 1>());
+        quarter16(std::integral_constant<int, 2>());
+        quarter16(std::integral_constant<int, 3>());
+      } else if constexpr (QP == 3) {
+        auto quarters16 = [&](auto qa_c, auto qb_c) {
+          constexpr int qa = decltype(qa_c)::value, qb = decltype(qb_c)::value;
+          v4i_t c1a[4], c1b[4];
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            c1a[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qa], v4i_t{128, 128, 128, 128}, 0, 0, 0);
+            c1b[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qb], v4i_t{128, 128, 128, 128}, 0, 0, 0);
+          }
+          uint32_t pa[4][2], pb[4][2];
+          pairs16(c1a, pa);
+          pairs16(c1b, pb);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              csp[qa][mt][h] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s_t, csp[qa][mt][h]) +
+                                                                __builtin_bit_cast(v2s_t, pa[mt][h]));
+              csp[qb][mt][h] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s_t, csp[qb][mt][h]) +
+                                                                __builtin_bit_cast(v2s_t, pb[mt][h]));
+            }
+          v2l_t Bla, Bha, Blb, Bhb;
+          split16(pa, Bla, Bha);
+          split16(pb, Blb, Bhb);
+          stage2x2B(Bla, Bha, Blb, Bhb, qa_c, qb_c, accB, [] {});
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        quarters16(std::integral_constant<int, 0>(), std::integral_constant<int, 1>());
+        quarters16(std::integral_constant<int, 2>(), std::integral_constant<int, 3>());
+      } else if constexpr (QP == 2) {
         v4i_t c1[4][4];
         auto s1 = [&](int q) {
 #pragma unroll
@@ -1424,7 +1534,25 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
         quarter(std::integral_constant<int, 3>());
       }
     }
-    if constexpr (QP) {
+    if constexpr (QP == 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v2l_t Bl, Bh;
+        split16(csp[q], Bl, Bh);
+        if (q == 0) stage2B(Bl, Bh, std::integral_constant<int, 0>(), accA);
+        if (q == 1) stage2B(Bl, Bh, std::integral_constant<int, 1>(), accA);
+        if (q == 2) stage2B(Bl, Bh, std::integral_constant<int, 2>(), accA);
+        if (q == 3) stage2B(Bl, Bh, std::integral_constant<int, 3>(), accA);
+      }
+    } else if constexpr (QP == 3) {
+      v2l_t Bla, Bha, Blb, Bhb;
+      split16(csp[0], Bla, Bha);
+      split16(csp[1], Blb, Bhb);
+      stage2x2B(Bla, Bha, Blb, Bhb, std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), accA, [] {});
+      split16(csp[2], Bla, Bha);
+      split16(csp[3], Blb, Bhb);
+      stage2x2B(Bla, Bha, Blb, Bhb, std::integral_constant<int, 2>(), std::integral_constant<int, 3>(), accA, [] {});
+    } else if constexpr (QP) {
       stage2x2(cs[0], cs[1], std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), accA, [] {});
       stage2x2(cs[2], cs[3], std::integral_constant<int, 2>(), std::integral_constant<int, 3>(), accA, [] {});
     } else {
@@ -1451,6 +1579,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
     unsigned long long* __restrict__ counts, unsigned long long add_n) {
   tile_reg_body<true, 0, 1>(buf, order, z0, nslices, counts, add_n);
+}
+// the same with the plane sums as packed int16 (QP 3); at 3 waves per SIMD, with / without the
+// next plane in flight
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_p16_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<true, 0, 3>(buf, order, z0, nslices, counts, add_n);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_reg_p16w3_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<true, 0, 3>(buf, order, z0, nslices, counts, add_n);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_reg_p16w3np_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<false, 0, 3>(buf, order, z0, nslices, counts, add_n);
+}
+// packed plane sums, one quarter at a time (QP 4): 3 waves per SIMD; 4 (spills), with / without prefetch
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_reg_q16w3_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<true, 0, 4>(buf, order, z0, nslices, counts, add_n);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_reg_q16w4np_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+  tile_reg_body<false, 0, 4>(buf, order, z0, nslices, counts, add_n);
 }
 // the same with the second pair's stage 1 issued before the first pair's squares
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_qp2_kernel(
@@ -1516,9 +1672,6 @@ __device__ __forceinline__ size_t mx_pm(int c, int kb, int b, int g) {
   return (((((size_t)(c >> 4) * kMxKB + kb) * kMxRBits + b) * 4 + g) << 4) + (c & 15);
 }
 
-__device__ __forceinline__ v2l_t pack_v2l(const uint32_t* w) {
-  return v2l_t{(long)(((uint64_t)w[1] << 32) | w[0]), (long)(((uint64_t)w[3] << 32) | w[2])};
-}
 
 // One thread per (column, 64-code block, lane): the lane's 16 bytes of A_0 and B in the
 // MFMA operand layout (byte j = code 64 kb + 16 (l >> 4) + j; rows / columns zm = zn =
@@ -1968,6 +2121,16 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
           hipLaunchKernelGGL(tile_reg_qp_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
         else if (st.tile_reg == 5)
           hipLaunchKernelGGL(tile_reg_qp2_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+        else if (st.tile_reg == 6)
+          hipLaunchKernelGGL(tile_reg_p16_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+        else if (st.tile_reg == 7)
+          hipLaunchKernelGGL(tile_reg_p16w3_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+        else if (st.tile_reg == 8)
+          hipLaunchKernelGGL(tile_reg_p16w3np_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+        else if (st.tile_reg == 9)
+          hipLaunchKernelGGL(tile_reg_q16w3_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+        else if (st.tile_reg == 10)
+          hipLaunchKernelGGL(tile_reg_q16w4np_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
         else
           hipLaunchKernelGGL(tile_reg_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
       } else {
@@ -2065,15 +2228,23 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
     // 0.320 ms per 65536 slices, count 2.39 vs 2.47 ms); "mfma2" = the LDS-exchange tile,
     // reg_np / reg_w3 = register-tile ablations
     const char* tv = getenv("SCT_SPECTRAL_TILE");
-    // (round 2, later: "reg_qp", two quarters' MFMA chains interleaved, is the default: 0.286-0.296
-    // vs 0.291-0.306 ms on two boxes; "reg" = one quarter at a time)
-    st.tile_reg = !tv ? 4 : !strcmp(tv, "mfma2") ? 0 : !strcmp(tv, "reg_np") ? 2 : !strcmp(tv, "reg_w3") ? 3
-                : !strcmp(tv, "reg") ? 1 : !strcmp(tv, "reg_qp2") ? 5 : 4;
+    // (round 2, later: "reg_p16" is the default -- two quarters' MFMA chains interleaved and the
+    // plane sums as packed int16, 167 VGPRs, 3 waves per SIMD: 0.267-0.281 ms against 0.287-0.293
+    // for "reg_qp" (pairs, int32 sums, 2 waves per SIMD) and 0.291-0.306 for "reg" on the same boxes)
+    st.tile_reg = !tv ? 6 : !strcmp(tv, "mfma2") ? 0 : !strcmp(tv, "reg_np") ? 2 : !strcmp(tv, "reg_w3") ? 3
+                : !strcmp(tv, "reg") ? 1 : !strcmp(tv, "reg_qp2") ? 5 : !strcmp(tv, "reg_p16") ? 6
+                : !strcmp(tv, "reg_p16w3") ? 7 : !strcmp(tv, "reg_p16w3np") ? 8 : !strcmp(tv, "reg_q16w3") ? 9
+                : !strcmp(tv, "reg_q16w4np") ? 10 : !strcmp(tv, "reg_qp") ? 4 : 6;
     int per_cu_reg = 0;  // its resident workgroups per CU
     const void* kf = st.tile_reg == 2 ? (const void*)tile_reg_np_kernel
                      : st.tile_reg == 3 ? (const void*)tile_reg_w3_kernel
                      : st.tile_reg == 4 ? (const void*)tile_reg_qp_kernel
-                     : st.tile_reg == 5 ? (const void*)tile_reg_qp2_kernel : (const void*)tile_reg_kernel;
+                     : st.tile_reg == 5 ? (const void*)tile_reg_qp2_kernel
+                     : st.tile_reg == 6 ? (const void*)tile_reg_p16_kernel
+                     : st.tile_reg == 7 ? (const void*)tile_reg_p16w3_kernel
+                     : st.tile_reg == 8 ? (const void*)tile_reg_p16w3np_kernel
+                     : st.tile_reg == 9 ? (const void*)tile_reg_q16w3_kernel
+                     : st.tile_reg == 10 ? (const void*)tile_reg_q16w4np_kernel : (const void*)tile_reg_kernel;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_reg, kf, 256, 0) != hipSuccess || per_cu_reg <= 0)
       per_cu_reg = 2;
     st.tile_reg_wgs = per_cu_reg;

@@ -411,7 +411,7 @@ def test_allpairs_spectral_scheme_matches_oracle(n, width, monkeypatch):
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
-@pytest.mark.parametrize("tile,seed,overlap", [("reg", "", "0"), ("reg_qp", "", "0"), ("reg_qp2", "", "0"), ("mfma2", "", "0"), ("reg_np", "", "0"),
+@pytest.mark.parametrize("tile,seed,overlap", [("reg", "", "0"), ("reg_qp", "", "0"), ("reg_qp2", "", "0"), ("reg_p16", "", "0"), ("reg_p16w3np", "", "0"), ("reg_q16w3", "", "0"), ("mfma2", "", "0"), ("reg_np", "", "0"),
                                                ("reg_w3", "", "0"), ("reg", "walk", "0"), ("reg", "mx", "0"),
                                                ("reg", "spread", "0"), ("reg", "walk", "1"), ("reg", "mx", "1"),
                                                ("reg", "mxd", "0"), ("reg", "mxd", "1")])
@@ -461,7 +461,7 @@ def test_allpairs_spectral_column_sizes(seed, monkeypatch):
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
-@pytest.mark.parametrize("tile", ["reg", "reg_qp", "reg_qp2"])
+@pytest.mark.parametrize("tile", ["reg", "reg_qp", "reg_qp2", "reg_p16"])
 def test_allpairs_spectral_high_energy_planes(tile, monkeypatch):
     """Planes (column bits 12, 13) of large seeds in every slice -- 120 columns of 120 codes,
     110 of them sharing their high bits, in planes 0 and 2 -- beside sparse ones (squares

@@ -49,7 +49,7 @@ def kernel_avg_ns(stats_csv, kernel_substr):
     return None, 0
 
 
-KERNELS = (("allpairs", "allpairs_count_kernel<8"), ("spectral", "tile_reg_qp_kernel"),
+KERNELS = (("allpairs", "allpairs_count_kernel<8"), ("spectral", "tile_reg_p16_kernel"),
            ("spectral_seed", "seed_kernel<signed char"))
 
 
