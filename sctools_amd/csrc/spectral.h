@@ -29,6 +29,7 @@ struct State {
   int tile_wgs = 2;              // resident MFMA-tile workgroups per CU
   int tile_reg = 0;              // int8 seeds: the register-resident tile (one wave per slice), variant
   int tile_reg_wgs = 2;          // its resident workgroups per CU
+  bool seed_db = false;          // int8 walk seed: double-buffered byte stage
   bool seed_spread = false;      // int8 seeds: stores spread over the walk (16-slice blocks)
   void* d_mx = nullptr;          // int8 seeds: the MFMA seed's operand tables (null: the walk seed)
   int mx_form = 2;               // the MFMA seed's workgroup shape (A/B)

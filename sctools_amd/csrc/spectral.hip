@@ -299,14 +299,17 @@ __device__ __forceinline__ void transpose4x4_bytes(const uint32_t* d, uint32_t* 
 // 16-B chunks of slice rows.
 // ABL (ablation builds only, wrong results by design): 1 = no global stores, 2 = no
 // Gray walk (one group, no planes), 3 = no LDS staging/transposes.
-template <typename T, int ABL, int kRegG, int NT = 256>
+// DB: the int8 byte stage double-buffered (walk i + 1 writes the other buffer while walk i's
+// store-out may still read this one): one workgroup barrier per walk instead of two.
+template <typename T, int ABL, int kRegG, int NT = 256, bool DB = false>
 __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
                                                    const uint32_t* __restrict__ gofs,
                                                    const uint32_t* __restrict__ off, int64_t max_groups,
                                                    int z0, int z1, T* __restrict__ buf) {
   constexpr int P = 4 / sizeof(T);          // slices per staged dword
   constexpr int V = Chunk<T>::kVals;        // columns per 16-B output chunk
-  __shared__ uint32_t stage[(kWalk / P) * NT];
+  __shared__ uint32_t stage[(DB ? 2 : 1) * (kWalk / P) * NT];
+  int it = 0;  // this workgroup's walk count (DB: which buffer)
   const int tid = threadIdx.x;
   const int c0 = blockIdx.x * NT, c = c0 + tid;
   const int m = (int)(off[c + 1] - off[c]);
@@ -399,7 +402,7 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
     // packing), and the store-out forms m - 2 acc for 16 columns at once:
     //   ((m | 0x80) - 2 acc) ^ 0x80 per byte -- acc <= m <= 127, so 2 acc fits a byte
     //   and m + 128 - 2 acc lies in [1, 255]: no carry or borrow crosses a byte.
-    uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
+    uint8_t* st8 = reinterpret_cast<uint8_t*>(stage) + (DB ? (it++ & 1) * (kWalk * NT) : 0);
     if constexpr (ABL == 6) {
       uint8_t* w8 = st8 + 4096 * (tid >> 6);  // this wave's 64 slices x 64 columns
       const int lane = tid & 63;
@@ -423,7 +426,9 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
       __builtin_amdgcn_wave_barrier();
       continue;
     }
-    __syncthreads();  // the previous walk's store-out reads of `stage` are done
+    // the previous walk's store-out reads of this buffer are done (DB: the barrier after the
+    // previous walk's writes already ordered the reads of two walks ago, the last ones of it)
+    if constexpr (!DB) __syncthreads();
 #pragma unroll
     for (int i = 0; i < kWalk; ++i) st8[i * NT + tid] = (uint8_t)acc[i];
     __syncthreads();
@@ -631,6 +636,14 @@ __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ off, int64_t max_groups,
                                                    int z0, int z1, T* __restrict__ buf) {
   seed_body<T, ABL, kRegGroups>(planes, gofs, off, max_groups, z0, z1, buf);
+}
+// the byte stage double-buffered (DB above)
+template <typename T>
+__global__ __launch_bounds__(256) void seed_db_kernel(const uint32_t* __restrict__ planes,
+                                                      const uint32_t* __restrict__ gofs,
+                                                      const uint32_t* __restrict__ off, int64_t max_groups,
+                                                      int z0, int z1, T* __restrict__ buf) {
+  seed_body<T, 0, kRegGroups, 256, true>(planes, gofs, off, max_groups, z0, z1, buf);
 }
 // store-width variant (A/B): 512 columns per workgroup (512-B slice-row segments)
 template <typename T>
@@ -2035,7 +2048,10 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
       else
         SCT_MX_L(8, 16, 0, mgrid);
 #undef SCT_MX_L
-    } else if (sizeof(T) == 1 && st.seed_spread)
+    } else if (sizeof(T) == 1 && st.seed_db)
+      hipLaunchKernelGGL(seed_db_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, st.max_groups,
+                         z0, z1, buf);
+    else if (sizeof(T) == 1 && st.seed_spread)
       hipLaunchKernelGGL(seed_spread_kernel, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
                          st.max_groups, z0, z1, reinterpret_cast<int8_t*>(buf));
     else
@@ -2219,6 +2235,7 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
     // "spread" = the walk with its stores spread over the walk
     const char* sv = getenv("SCT_SPECTRAL_SEED");
     st.seed_spread = sv && !strcmp(sv, "spread");
+    st.seed_db = sv && !strcmp(sv, "db");
     seed_mx = sv && (!strcmp(sv, "mx") || !strcmp(sv, "mxd"));
     st.ilv = sv && !strcmp(sv, "mxd") ? 4 : 0;
     if (st.ilv)

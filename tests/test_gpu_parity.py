@@ -414,7 +414,8 @@ def test_allpairs_spectral_scheme_matches_oracle(n, width, monkeypatch):
 @pytest.mark.parametrize("tile,seed,overlap", [("reg", "", "0"), ("reg_qp", "", "0"), ("reg_qp2", "", "0"), ("reg_p16", "", "0"), ("reg_p16w3np", "", "0"), ("reg_q16w3", "", "0"), ("mfma2", "", "0"), ("reg_np", "", "0"),
                                                ("reg_w3", "", "0"), ("reg", "walk", "0"), ("reg", "mx", "0"),
                                                ("reg", "spread", "0"), ("reg", "walk", "1"), ("reg", "mx", "1"),
-                                               ("reg", "mxd", "0"), ("reg", "mxd", "1")])
+                                               ("reg", "mxd", "0"), ("reg", "mxd", "1"),
+                                               ("reg", "db", "0")])
 def test_allpairs_spectral_kernel_variants(tile, seed, overlap, monkeypatch):
     """Every tile / seed kernel variant, with and without the seed / tile overlap over two
     streams, gives the oracle's histogram, with 1000-slice chunks (seams inside the range)."""
@@ -442,7 +443,7 @@ def test_allpairs_spectral_interleaved_groups(group, monkeypatch):
     assert full.tolist() == hist.tolist()
 
 
-@pytest.mark.parametrize("seed", ["mx", "walk", "mxd"])
+@pytest.mark.parametrize("seed", ["mx", "walk", "mxd", "db"])
 def test_allpairs_spectral_column_sizes(seed, monkeypatch):
     """Columns (low 14 bits) holding 63, 64, 65, 100 and 127 codes -- the MFMA seed's one- and
     two-block columns and the int8 limit -- next to sparse ones, duplicates included; slice
