@@ -22,9 +22,11 @@
 // No per-line array is ever stored.
 #include <hipcub/hipcub.hpp>
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "sct_common.h"
@@ -117,6 +119,17 @@ __device__ __forceinline__ int virtual_in(const uint8_t* __restrict__ buf, int64
   return -1;
 }
 
+// A workgroup's walk over increasing tile starts t0: f = the first file ending after t0 (loads
+// of uniform addresses: scalar), so a tile holding no file end (almost all of them) skips the
+// per-thread virtual-terminator search.
+struct FileCursor {
+  int f = 0;
+  __device__ __forceinline__ bool advance(Files fs, int64_t t0) {
+    while (f < fs.nfiles && fs.ends[f] <= t0) ++f;
+    return f < fs.nfiles && fs.ends[f] <= t0 + TILE + 16;
+  }
+};
+
 // Per tile: its terminator count, and its first terminator (in-tile offset << 2 | 1 if
 // virtual | 2 if "\r\n"; ~0 if none) -- the end of the previous tile's last line.
 // Persistent: a workgroup walks tiles blockIdx.x, + gridDim.x, ... with the next tile's
@@ -130,14 +143,16 @@ __global__ __launch_bounds__(WG) void count_kernel(const uint8_t* __restrict__ b
   __shared__ typename BR::TempStorage tmp;
   int64_t tile = blockIdx.x;
   uint4 cur = tile < ntiles ? load16(buf, n, tile * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
+  FileCursor fc;
   for (; tile < ntiles; tile += gridDim.x) {
     const int64_t nt = tile + gridDim.x;
     const uint4 nxt = nt < ntiles ? load16(buf, n, nt * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
     const int64_t p0 = tile * TILE + (int64_t)threadIdx.x * 16;
+    const bool ends_here = fc.advance(fs, tile * TILE);  // wave-uniform: a file end in this tile
     uint32_t c = 0, na = 0, crlf = 0, m = 0, f = ~0u;
     if (p0 < n) {
       m = load_mask(buf, n, p0, text, &crlf, &na, cur);
-      const int vj = virtual_in(buf, n, fs, p0, text);
+      const int vj = ends_here ? virtual_in(buf, n, fs, p0, text) : -1;
       c = __popc(m) + (vj >= 0);
       if (m) {
         const int j = __ffs(m) - 1;
@@ -204,6 +219,7 @@ __device__ __forceinline__ Line scan_line(const uint8_t* __restrict__ buf, int64
 constexpr int MAX_SPANS = 8;
 struct Spans {
   int n, max_end, width;  // width = sum of the spans' widths
+  uint32_t inv_n;         // ceil(2^32 / n) for n >= 2: q / n = umulhi(q, inv_n) for q < 2^29
   int start[MAX_SPANS], end[MAX_SPANS];
   int64_t prefix[MAX_SPANS];  // sum of the widths of the spans before k
 };
@@ -235,18 +251,26 @@ __global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__
   // persistent, as count_kernel: the next tile's bytes load while this one is extracted
   int64_t tile = blockIdx.x;
   uint4 cur = tile < ntiles ? load16(buf, n, tile * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
+  // the tile's first terminator number and the next tile's first terminator: uniform loads
+  // issued a tile ahead, with the bytes
+  unsigned long long g0_cur = tile < ntiles ? offsets[tile] : 0ull;
+  uint32_t nf_cur = tile + 1 < ntiles ? first[tile + 1] : ~0u;
+  FileCursor fc;
   for (; tile < ntiles; tile += gridDim.x) {
   const int64_t ntl = tile + gridDim.x;
   const uint4 nxt = ntl < ntiles ? load16(buf, n, ntl * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
+  const unsigned long long g0_nxt = ntl < ntiles ? offsets[ntl] : 0ull;
+  const uint32_t nf_nxt = ntl + 1 < ntiles ? first[ntl + 1] : ~0u;
   const int64_t t0 = tile * TILE;
   const int64_t p0 = t0 + (int64_t)threadIdx.x * 16;
+  const bool ends_here = fc.advance(fs, t0);
   uint32_t m = 0, crlf = 0, na;
   int vj = -1;
   uint4 mine = make_uint4(0, 0, 0, 0);
   if (p0 < n) {
     mine = cur;
     m = load_mask(buf, n, p0, text, &crlf, &na, cur);
-    vj = virtual_in(buf, n, fs, p0, text);
+    vj = ends_here ? virtual_in(buf, n, fs, p0, text) : -1;
   }
   cur = nxt;
   __syncthreads();  // the previous tile's readers of tile_bytes / term / act / tmp are done
@@ -267,7 +291,7 @@ __global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__
     }
   }
   __syncthreads();
-  const int64_t g0 = (int64_t)offsets[tile];  // global number of the tile's first terminator
+  const int64_t g0 = (int64_t)g0_cur;  // global number of the tile's first terminator
   if (tile == 0 && threadIdx.x == 0 && nrec > 0 && buf[0] != '@') atomicMin(first_bad, 0ull);
   for (uint32_t t = threadIdx.x; t < ntile; t += WG) {
     const int64_t line = g0 + t + 1, r = line >> 2;
@@ -282,7 +306,7 @@ __global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__
     } else if (which == 1 || which == 3) {
       int64_t cend;
       int nl;
-      const uint32_t nf = tile + 1 < ntiles ? first[tile + 1] : ~0u;
+      const uint32_t nf = nf_cur;
       if (t + 1 < ntile) {  // the line ends at the tile's next terminator
         const uint32_t f = term[t + 1];
         cend = t0 + (f & T_OFF) - ((f & T_CRLF) ? 1 : 0);
@@ -377,6 +401,174 @@ __global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__
       o[j] = i < b ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
     }
   }
+  g0_cur = g0_nxt;
+  nf_cur = nf_nxt;
+  }
+}
+
+// The same extraction with fewer LDS bytes and one barrier fewer per tile: terminators as
+// 16-bit tile offsets (bit 13 = virtual file end, bit 14 = "\r\n"; 8 KB), no action array --
+// a copy item (action a, span k) finds its line from the terminators around it (the line
+// after the tile's (te0 + 2a)-th terminator; te0 = 1 when the tile's first terminator number
+// is odd) -- so the name checks and the copies run in one phase after the terminators are
+// written.  13 KB of LDS: twice the resident workgroups of extract_kernel.
+constexpr uint16_t T16_OFF = 0x1FFF, T16_VIRT = 1u << 13, T16_CRLF = 1u << 14;
+
+__global__ __launch_bounds__(WG) void extract2_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs,
+                                                      int text, const unsigned long long* __restrict__ offsets,
+                                                      const uint32_t* __restrict__ first, int64_t ntiles,
+                                                      int64_t nrec, Spans sp, uint8_t* __restrict__ seq_out,
+                                                      uint8_t* __restrict__ qual_out,
+                                                      int32_t* __restrict__ seq_len,
+                                                      int32_t* __restrict__ qual_len,
+                                                      unsigned long long* __restrict__ first_bad) {
+  __shared__ uint16_t term[MAX_TERM];
+  __shared__ uint4 tile_bytes[TILE / 16];  // the tile itself: slices inside it copy from LDS
+  using BS = hipcub::BlockScan<uint32_t, WG>;
+  __shared__ typename BS::TempStorage tmp;
+  int64_t tile = blockIdx.x;
+  uint4 cur = tile < ntiles ? load16(buf, n, tile * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
+  unsigned long long g0_cur = tile < ntiles ? offsets[tile] : 0ull;
+  uint32_t nf_cur = tile + 1 < ntiles ? first[tile + 1] : ~0u;
+  FileCursor fc;
+  const uint8_t* tile8 = reinterpret_cast<const uint8_t*>(tile_bytes);
+  const uint32_t* tile32 = reinterpret_cast<const uint32_t*>(tile_bytes);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int64_t ntl = tile + gridDim.x;
+    const uint4 nxt = ntl < ntiles ? load16(buf, n, ntl * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
+    const unsigned long long g0_nxt = ntl < ntiles ? offsets[ntl] : 0ull;
+    const uint32_t nf_nxt = ntl + 1 < ntiles ? first[ntl + 1] : ~0u;
+    const int64_t t0 = tile * TILE;
+    const int64_t p0 = t0 + (int64_t)threadIdx.x * 16;
+    const bool ends_here = fc.advance(fs, t0);
+    uint32_t m = 0, crlf = 0, na;
+    int vj = -1;
+    uint4 mine = make_uint4(0, 0, 0, 0);
+    if (p0 < n) {
+      mine = cur;
+      m = load_mask(buf, n, p0, text, &crlf, &na, cur);
+      vj = ends_here ? virtual_in(buf, n, fs, p0, text) : -1;
+    }
+    cur = nxt;
+    __syncthreads();  // the previous tile's readers of tile_bytes / term / tmp are done
+    tile_bytes[threadIdx.x] = mine;
+    const uint32_t c = __popc(m) + (vj >= 0);
+    uint32_t pre, ntile;
+    BS(tmp).ExclusiveSum(c, pre, ntile);
+    {
+      uint32_t bits = m | (vj >= 0 ? (1u << vj) : 0u);
+      uint32_t at = pre;
+      while (bits) {
+        const int j = __ffs(bits) - 1;
+        bits &= bits - 1;
+        const uint32_t off = (uint32_t)(threadIdx.x * 16 + j);
+        if (m >> j & 1u) term[at++] = (uint16_t)(off | ((crlf >> j & 1u) ? T16_CRLF : 0u));
+        if (j == vj) term[at++] = (uint16_t)((off + 1) | T16_VIRT);  // the file ends after byte off
+      }
+    }
+    __syncthreads();
+    const int64_t g0 = (int64_t)g0_cur;  // global number of the tile's first terminator
+    const uint32_t nf = nf_cur;
+    if (tile == 0 && threadIdx.x == 0 && nrec > 0 && buf[0] != '@') atomicMin(first_bad, 0ull);
+    // terminators of the tile that belong to records < nrec: [0, tmax)
+    const int64_t lim_g = 4 * nrec - 1;  // terminators beyond the last record's line 3 end nothing
+    const int tmax = (int)(g0 + ntile <= lim_g ? ntile : (lim_g > g0 ? lim_g - g0 : 0));
+    // name lines: after terminators g = 3 (mod 4)
+    for (int t = (int)((3 - (g0 & 3)) & 3) + 4 * (int)threadIdx.x; t < tmax; t += 4 * WG) {
+      const uint32_t e = term[t];
+      const int64_t o = (int64_t)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // the line's start in the tile
+      const uint8_t ch = o < TILE ? tile8[o] : buf[t0 + o];
+      if (ch != '@') atomicMin(first_bad, (unsigned long long)((g0 + t + 1) >> 2));
+    }
+    // sequence / quality lines: after even terminators; one item per (line, span)
+    const int te0 = (int)(g0 & 1);
+    const int nact = tmax > te0 ? (tmax - te0 + 1) / 2 : 0;
+    for (int q = threadIdx.x; q < nact * sp.n; q += WG) {
+      const int a = sp.n == 1 ? q : (int)__umulhi((uint32_t)q, sp.inv_n), k = q - a * sp.n;  // q / n, q % n
+      const int t = te0 + 2 * a;
+      const int64_t line = g0 + t + 1, rec = line >> 2;
+      const bool is_seq = (line & 3) == 1;
+      const uint32_t e = term[t];
+      const int start = (int)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // <= TILE
+      int64_t cend;  // content end relative to the tile start
+      int nl;
+      if (t + 1 < (int)ntile) {  // the line ends at the tile's next terminator
+        const uint32_t f = term[t + 1];
+        cend = (int64_t)(f & T16_OFF) - ((f & T16_CRLF) ? 1 : 0);
+        nl = (f & T16_VIRT) ? 0 : 1;
+      } else if (nf != ~0u) {  // the tile's last line ends at the next tile's first terminator
+        cend = TILE + (int64_t)(nf >> 2) - ((nf & 2u) ? 1 : 0);
+        nl = (nf & 1u) ? 0 : 1;
+      } else {  // no terminator in the next tile either: scan (max_end bytes, within its file)
+        const int64_t next = t0 + start;
+        int lo = 0, hi = fs.nfiles;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (fs.ends[mid] <= next) lo = mid + 1; else hi = mid;
+        }
+        const int64_t fe = lo < fs.nfiles ? fs.ends[lo] : n;
+        const int64_t lim = next + sp.max_end < fe ? next + sp.max_end : fe;
+        cend = lim - t0;
+        nl = lim == fe ? 0 : 1;  // longer than the window: its end is irrelevant
+        for (int64_t i = next; i < lim; ++i) {
+          const uint8_t ch = buf[i];
+          if (ch == '\n' || (text && ch == '\r')) {
+            cend = i - t0;
+            nl = 1;
+            break;
+          }
+        }
+      }
+      int32_t* len = is_seq ? seq_len : qual_len;
+      uint8_t* out = is_seq ? seq_out : qual_out;
+      const int64_t clen = cend - start, llen = clen + nl;
+      const int64_t sa = sp.start[k] < llen ? sp.start[k] : llen, sb = sp.end[k] < llen ? sp.end[k] : llen;
+      if (len) len[k * nrec + rec] = (int32_t)(sb - sa);
+      if (!out) continue;
+      const int w = sp.end[k] - sp.start[k];
+      uint8_t* o = out + sp.prefix[k] * nrec + rec * w;
+      const uint8_t* src = buf + t0 + start;
+      // fast path: a whole-width slice inside the line's content, a row of whole dwords:
+      // aligned dword loads + byte-align funnel shifts, dword stores
+      const int64_t s0 = t0 + start + sa;
+      const int64_t base = s0 & ~3LL;
+      const int nd = w / 4;
+      if (sb - sa == w && sb <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
+          ((uintptr_t)o & 3) == 0) {
+        // rows inside the tile read its LDS copy; the rest (lines running past it) read L2
+        const uint32_t* d = base + 4 * (nd + 1) <= t0 + TILE ? tile32 + ((base - t0) >> 2)
+                                                             : reinterpret_cast<const uint32_t*>(buf + base);
+        const uint32_t sh = (uint32_t)(s0 & 3);
+        uint32_t* od = reinterpret_cast<uint32_t*>(o);
+        if (nd == 4 && ((uintptr_t)o & 15) == 0) {
+          const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3], x4 = d[4];
+          *reinterpret_cast<uint4*>(o) =
+              make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                         __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+          continue;
+        }
+        if (nd == 2 && ((uintptr_t)o & 7) == 0) {
+          const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
+          *reinterpret_cast<uint2*>(o) =
+              make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
+          continue;
+        }
+        uint32_t lo = d[0];
+        for (int q2 = 0; q2 < nd; ++q2) {
+          const uint32_t hi = d[q2 + 1];
+          od[q2] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+          lo = hi;
+        }
+        continue;
+      }
+#pragma unroll 8
+      for (int j = 0; j < w; ++j) {
+        const int64_t i = sa + j;
+        o[j] = i < sb ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
+      }
+    }
+    g0_cur = g0_nxt;
+    nf_cur = nf_nxt;
   }
 }
 
@@ -423,11 +615,58 @@ __global__ __launch_bounds__(WG) void line_end_kernel(const uint8_t* __restrict_
 
 }  // namespace
 
+namespace {
+// One spare index allocation per device, kept when an index is destroyed and taken by the
+// next create that fits: a stream of pieces (one index per piece) or repeated extractions pay
+// no hipMalloc / hipFree per call.  Every user of an index synchronises its stream before the
+// index is destroyed, so a cached block is idle.
+constexpr int kMaxDev = 16;
+std::mutex g_ix_mu;
+struct Spare {
+  void* p = nullptr;
+  size_t bytes = 0;
+} g_ix_spare[kMaxDev];
+
+hipError_t ix_alloc(void** p, size_t bytes, size_t* got) {
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDev) {
+    std::lock_guard<std::mutex> g(g_ix_mu);
+    Spare& sp = g_ix_spare[dev];
+    if (sp.p && sp.bytes >= bytes) {
+      *p = sp.p;
+      *got = sp.bytes;
+      sp.p = nullptr;
+      sp.bytes = 0;
+      return hipSuccess;
+    }
+  }
+  *got = bytes;
+  return hipMalloc(p, bytes);
+}
+
+void ix_release(void* p, size_t bytes) {
+  if (!p) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDev) {
+    std::lock_guard<std::mutex> g(g_ix_mu);
+    Spare& sp = g_ix_spare[dev];
+    if (bytes > sp.bytes) {  // keep the larger block
+      if (sp.p) (void)hipFree(sp.p);
+      sp.p = p;
+      sp.bytes = bytes;
+      return;
+    }
+  }
+  (void)hipFree(p);
+}
+}  // namespace
+
 struct sct_fastq_index {
   int64_t nbytes = 0, nlines = 0, nrec = 0, first_bad = -2;
   int text = 0, nfiles = 0;
   int64_t ntiles = 0;
   void* d_mem = nullptr;                    // one allocation holding the arrays below
+  size_t mem_bytes = 0;
   int64_t* d_ends = nullptr;                // file ends
   unsigned long long* d_offsets = nullptr;  // ntiles + 1 line offsets (exclusive scan of tile counts)
   uint32_t* d_first = nullptr;              // per tile: first terminator (see count_kernel)
@@ -436,7 +675,7 @@ struct sct_fastq_index {
 
 extern "C" int sct_fastq_index_destroy(sct_fastq_index* ix) {
   if (!ix) return SCT_OK;
-  if (ix->d_mem) (void)hipFree(ix->d_mem);
+  ix_release(ix->d_mem, ix->mem_bytes);
   delete ix;
   return SCT_OK;
 }
@@ -470,7 +709,7 @@ extern "C" int sct_fastq_index_create(const uint8_t* d_buf, int64_t nbytes, cons
   const size_t o_ends = 0, o_off = up((size_t)nfiles * 8), o_cnt = o_off + up((ix->ntiles + 1) * 8),
                o_first = o_cnt + up((ix->ntiles + 1) * 8), o_flags = o_first + up(ix->ntiles * 4),
                o_tmp = o_flags + 256, total_bytes = o_tmp + up(tb);
-  hipError_t e = hipMalloc(&ix->d_mem, total_bytes);
+  hipError_t e = ix_alloc(&ix->d_mem, total_bytes, &ix->mem_bytes);
   if (e != hipSuccess) return fail_with(sct::fail(SCT_E_NOMEM, "fastq index: %s", hipGetErrorString(e)));
   char* base = (char*)ix->d_mem;
   ix->d_ends = (int64_t*)(base + o_ends);
@@ -530,12 +769,15 @@ extern "C" int sct_fastq_extract_spans(sct_fastq_index* ix, const uint8_t* d_buf
     pre += sp.end[k] - sp.start[k];
   }
   sp.width = (int)pre;
+  sp.inv_n = nspans >= 2 ? (uint32_t)((0xFFFFFFFFull + nspans) / nspans) : 0u;
   hipStream_t s = sct::as_stream(stream);
   SCT_HIP(hipMemsetAsync(ix->d_bad, 0xFF, 8, s));
   if (ix->nbytes > 0) {
     SCT_CHECK(d_buf != nullptr, "buffer is NULL");
     const Files fs{ix->d_ends, ix->nfiles};
-    hipLaunchKernelGGL(extract_kernel, dim3(resident_grid((const void*)extract_kernel, ix->ntiles)), dim3(WG), 0, s,
+    static const bool v1 = getenv("SCT_FASTQ_EXTRACT") && atoi(getenv("SCT_FASTQ_EXTRACT")) == 1;  // A/B
+    const void* kf = v1 ? (const void*)extract_kernel : (const void*)extract2_kernel;
+    hipLaunchKernelGGL(v1 ? extract_kernel : extract2_kernel, dim3(resident_grid(kf, ix->ntiles)), dim3(WG), 0, s,
                        d_buf, ix->nbytes, fs,
                        ix->text, ix->d_offsets, ix->d_first, ix->ntiles, ix->nrec, sp, d_seq, d_qual,
                        d_seq_len, d_qual_len, ix->d_bad);
