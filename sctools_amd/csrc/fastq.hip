@@ -17,7 +17,7 @@
 // Device layout: the files' bytes concatenated in one buffer, read in 4 KiB tiles (16 bytes
 // per thread, SWAR byte compares).  Two passes: count_kernel counts each tile's line
 // terminators and an exclusive scan gives every tile its first line number (the index);
-// extract_kernel finds the terminators again, numbers them, and for each one that starts a
+// extract2_kernel finds the terminators again, numbers them, and for each one that starts a
 // record's name / sequence / quality line checks the '@' or copies that line's slices.
 // No per-line array is ever stored.
 #include <hipcub/hipcub.hpp>
@@ -210,11 +210,10 @@ __device__ __forceinline__ Line scan_line(const uint8_t* __restrict__ buf, int64
 //     numbers them; their in-tile offsets go to LDS in byte order (bit 13 = virtual file
 //     end: the next line starts at the end and the line has no '\n'; bit 14 = "\r\n");
 //  2. the line after terminator t (global number g+1) belongs to record (g+1)/4: a name
-//     line (0) must start with '@' (fastq.py:35-36); a sequence (1) or quality (3) line
-//     becomes an "action" {start, content end, nl, record, which}: its end is the next
-//     terminator of the tile, or, for the tile's last line, found by a short scan;
-//  3. the block copies every action's slices for all spans cooperatively (one thread per
-//     output byte, re-reading the line bytes from L1/L2).
+//     line (0) must start with '@' (fastq.py:35-36); for a sequence (1) or quality (3)
+//     line, one item per (line, span) finds the line's end at the tile's next terminator
+//     (for the tile's last line: the next tile's first, or a short scan) and copies its
+//     slice (rows inside the tile from the tile's LDS copy).
 // Record 0's name line starts at byte 0, checked by thread 0 of tile 0.
 constexpr int MAX_SPANS = 8;
 struct Spans {
@@ -225,193 +224,14 @@ struct Spans {
 };
 
 constexpr int MAX_TERM = TILE + 16;  // terminators a tile can hold (+ virtual file ends)
-constexpr uint32_t T_OFF = 0x1FFFu, T_VIRT = 1u << 13, T_CRLF = 1u << 14;
 
-// a sequence/quality line of the tile (8 bytes in LDS): its terminator's tile index t (the
-// line is number g0 + t + 1), its start offset in the tile, its content end relative to the
-// tile start with bit 31 = no '\n'
-struct Action {
-  uint16_t t, start;
-  int32_t cend;
-};
-
-__global__ __launch_bounds__(WG) void extract_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs,
-                                                     int text, const unsigned long long* __restrict__ offsets,
-                                                     const uint32_t* __restrict__ first, int64_t ntiles,
-                                                     int64_t nrec, Spans sp, uint8_t* __restrict__ seq_out,
-                                                     uint8_t* __restrict__ qual_out,
-                                                     int32_t* __restrict__ seq_len,
-                                                     int32_t* __restrict__ qual_len,
-                                                     unsigned long long* __restrict__ first_bad) {
-  __shared__ uint32_t term[MAX_TERM];
-  __shared__ Action act[MAX_TERM / 2 + 2];  // 33 KiB with term[]: 4 workgroups per CU
-  __shared__ uint4 tile_bytes[TILE / 16];    // the tile itself: slices inside it copy from LDS
-  using BS = hipcub::BlockScan<uint32_t, WG>;
-  __shared__ typename BS::TempStorage tmp;
-  // persistent, as count_kernel: the next tile's bytes load while this one is extracted
-  int64_t tile = blockIdx.x;
-  uint4 cur = tile < ntiles ? load16(buf, n, tile * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
-  // the tile's first terminator number and the next tile's first terminator: uniform loads
-  // issued a tile ahead, with the bytes
-  unsigned long long g0_cur = tile < ntiles ? offsets[tile] : 0ull;
-  uint32_t nf_cur = tile + 1 < ntiles ? first[tile + 1] : ~0u;
-  FileCursor fc;
-  for (; tile < ntiles; tile += gridDim.x) {
-  const int64_t ntl = tile + gridDim.x;
-  const uint4 nxt = ntl < ntiles ? load16(buf, n, ntl * TILE + (int64_t)threadIdx.x * 16) : make_uint4(0, 0, 0, 0);
-  const unsigned long long g0_nxt = ntl < ntiles ? offsets[ntl] : 0ull;
-  const uint32_t nf_nxt = ntl + 1 < ntiles ? first[ntl + 1] : ~0u;
-  const int64_t t0 = tile * TILE;
-  const int64_t p0 = t0 + (int64_t)threadIdx.x * 16;
-  const bool ends_here = fc.advance(fs, t0);
-  uint32_t m = 0, crlf = 0, na;
-  int vj = -1;
-  uint4 mine = make_uint4(0, 0, 0, 0);
-  if (p0 < n) {
-    mine = cur;
-    m = load_mask(buf, n, p0, text, &crlf, &na, cur);
-    vj = ends_here ? virtual_in(buf, n, fs, p0, text) : -1;
-  }
-  cur = nxt;
-  __syncthreads();  // the previous tile's readers of tile_bytes / term / act / tmp are done
-  tile_bytes[threadIdx.x] = mine;
-  const uint32_t* tile32 = reinterpret_cast<const uint32_t*>(tile_bytes);
-  const uint32_t c = __popc(m) + (vj >= 0);
-  uint32_t pre, ntile;
-  BS(tmp).ExclusiveSum(c, pre, ntile);
-  {
-    uint32_t bits = m | (vj >= 0 ? (1u << vj) : 0u);
-    uint32_t at = pre;
-    while (bits) {
-      const int j = __ffs(bits) - 1;
-      bits &= bits - 1;
-      const uint32_t off = (uint32_t)(threadIdx.x * 16 + j);
-      if (m >> j & 1u) term[at++] = off | ((crlf >> j & 1u) ? T_CRLF : 0u);
-      if (j == vj) term[at++] = (off + 1) | T_VIRT;  // the file ends after byte off
-    }
-  }
-  __syncthreads();
-  const int64_t g0 = (int64_t)g0_cur;  // global number of the tile's first terminator
-  if (tile == 0 && threadIdx.x == 0 && nrec > 0 && buf[0] != '@') atomicMin(first_bad, 0ull);
-  for (uint32_t t = threadIdx.x; t < ntile; t += WG) {
-    const int64_t line = g0 + t + 1, r = line >> 2;
-    if (r >= nrec) continue;
-    const uint32_t e = term[t];
-    const int64_t next = t0 + (e & T_OFF) + ((e & T_VIRT) ? 0 : 1);  // the line's start
-    const int which = (int)(line & 3);
-    if (which == 0) {  // the '@' from the tile's LDS copy unless the line starts past the tile
-      const int64_t o = next - t0;
-      const uint8_t ch = o < TILE ? reinterpret_cast<const uint8_t*>(tile_bytes)[o] : buf[next];
-      if (ch != '@') atomicMin(first_bad, (unsigned long long)r);
-    } else if (which == 1 || which == 3) {
-      int64_t cend;
-      int nl;
-      const uint32_t nf = nf_cur;
-      if (t + 1 < ntile) {  // the line ends at the tile's next terminator
-        const uint32_t f = term[t + 1];
-        cend = t0 + (f & T_OFF) - ((f & T_CRLF) ? 1 : 0);
-        nl = (f & T_VIRT) ? 0 : 1;
-      } else if (nf != ~0u) {  // the tile's last line ends at the next tile's first terminator
-        cend = t0 + TILE + (nf >> 2) - ((nf & 2u) ? 1 : 0);
-        nl = (nf & 1u) ? 0 : 1;
-      } else {  // no terminator in the next tile either: scan (max_end bytes, within its file)
-        int lo = 0, hi = fs.nfiles;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (fs.ends[mid] <= next) lo = mid + 1; else hi = mid;
-        }
-        const int64_t fe = lo < fs.nfiles ? fs.ends[lo] : n;
-        const int64_t lim = next + sp.max_end < fe ? next + sp.max_end : fe;
-        cend = lim;
-        nl = lim == fe ? 0 : 1;  // longer than the window: its end is irrelevant
-        for (int64_t i = next; i < lim; ++i) {
-          const uint8_t ch = buf[i];
-          if (ch == '\n' || (text && ch == '\r')) {
-            cend = i;
-            nl = 1;
-            break;
-          }
-        }
-      }
-      Action A;
-      A.t = (uint16_t)t;
-      A.start = (uint16_t)(next - t0);  // <= TILE
-      A.cend = (int32_t)(cend - t0) | (nl ? 0 : (int32_t)0x80000000);
-      // sequence/quality lines follow the even-numbered terminators: slot = their rank
-      act[(g0 + t) / 2 - (g0 + 1) / 2] = A;
-    }
-  }
-  __syncthreads();
-  // actions of the tile = its even-numbered terminators (those of records < nrec)
-  int64_t lastg = g0 + ntile;  // one past the tile's last terminator number
-  if (lastg > 4 * nrec - 1) lastg = 4 * nrec - 1;  // terminators beyond the last record's line 3
-  const int na_ = lastg > g0 ? (int)((lastg + 1) / 2 - (g0 + 1) / 2) : 0;
-  // one thread per (action, span): length, then the slice's bytes (independent loads)
-  for (int q = threadIdx.x; q < na_ * sp.n; q += WG) {
-    const Action A = act[q / sp.n];
-    const int k = q - (q / sp.n) * sp.n;
-    const int64_t line = g0 + A.t + 1, rec = line >> 2;
-    const bool is_seq = (line & 3) == 1;
-    int32_t* len = is_seq ? seq_len : qual_len;
-    uint8_t* out = is_seq ? seq_out : qual_out;
-    const int64_t clen = (int64_t)(A.cend & 0x7FFFFFFF) - A.start, llen = clen + (A.cend < 0 ? 0 : 1);
-    const int64_t a = sp.start[k] < llen ? sp.start[k] : llen, b = sp.end[k] < llen ? sp.end[k] : llen;
-    if (len) len[k * nrec + rec] = (int32_t)(b - a);
-    if (!out) continue;
-    const int w = sp.end[k] - sp.start[k];
-    uint8_t* o = out + sp.prefix[k] * nrec + rec * w;
-    const uint8_t* src = buf + t0 + A.start;
-    // fast path: a whole-width slice inside the line's content, a row of whole dwords:
-    // aligned dword loads + byte-align funnel shifts, dword stores
-    const int64_t s0 = t0 + A.start + a;
-    const int64_t base = s0 & ~3LL;
-    const int nd = w / 4;
-    if (b - a == w && b <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
-        ((uintptr_t)o & 3) == 0) {
-      // rows inside the tile read its LDS copy; the rest (lines running past it) read L2
-      const uint32_t* d = base + 4 * (nd + 1) <= t0 + TILE ? tile32 + ((base - t0) >> 2)
-                                                           : reinterpret_cast<const uint32_t*>(buf + base);
-      const uint32_t sh = (uint32_t)(s0 & 3);
-      uint32_t* od = reinterpret_cast<uint32_t*>(o);
-      // the common widths as one vector store (16-B CB / 8-B UMI rows of aligned outputs)
-      if (nd == 4 && ((uintptr_t)o & 15) == 0) {
-        const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3], x4 = d[4];
-        *reinterpret_cast<uint4*>(o) =
-            make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                       __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
-        continue;
-      }
-      if (nd == 2 && ((uintptr_t)o & 7) == 0) {
-        const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
-        *reinterpret_cast<uint2*>(o) =
-            make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
-        continue;
-      }
-      uint32_t lo = d[0];
-      for (int q2 = 0; q2 < nd; ++q2) {
-        const uint32_t hi = d[q2 + 1];
-        od[q2] = __builtin_amdgcn_alignbyte(hi, lo, sh);
-        lo = hi;
-      }
-      continue;
-    }
-#pragma unroll 8
-    for (int j = 0; j < w; ++j) {
-      const int64_t i = a + j;
-      o[j] = i < b ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
-    }
-  }
-  g0_cur = g0_nxt;
-  nf_cur = nf_nxt;
-  }
-}
-
-// The same extraction with fewer LDS bytes and one barrier fewer per tile: terminators as
+// The extraction (round 2: fewer LDS bytes and one barrier fewer per tile than the first
+// version, which kept 32-bit terminators and an action array): terminators as
 // 16-bit tile offsets (bit 13 = virtual file end, bit 14 = "\r\n"; 8 KB), no action array --
 // a copy item (action a, span k) finds its line from the terminators around it (the line
 // after the tile's (te0 + 2a)-th terminator; te0 = 1 when the tile's first terminator number
 // is odd) -- so the name checks and the copies run in one phase after the terminators are
-// written.  13 KB of LDS: twice the resident workgroups of extract_kernel.
+// written.  13 KB of LDS: 7 resident workgroups per CU (4 for the first version).
 constexpr uint16_t T16_OFF = 0x1FFF, T16_VIRT = 1u << 13, T16_CRLF = 1u << 14;
 
 __global__ __launch_bounds__(WG) void extract2_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs,
@@ -582,7 +402,7 @@ unsigned resident_grid(const void* kernel, int64_t ntiles) {
 
 // The byte just past line `target` (0-based line number; its terminator is terminator
 // number `target` of the buffer): one workgroup finds the tile holding it (binary search of
-// the tile offsets) and recounts that tile's terminators as extract_kernel does.
+// the tile offsets) and recounts that tile's terminators as extract2_kernel does.
 __global__ __launch_bounds__(WG) void line_end_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs, int text,
                                                       const unsigned long long* __restrict__ offsets, int64_t ntiles,
                                                       unsigned long long target, long long* __restrict__ out) {
@@ -775,9 +595,7 @@ extern "C" int sct_fastq_extract_spans(sct_fastq_index* ix, const uint8_t* d_buf
   if (ix->nbytes > 0) {
     SCT_CHECK(d_buf != nullptr, "buffer is NULL");
     const Files fs{ix->d_ends, ix->nfiles};
-    static const bool v1 = getenv("SCT_FASTQ_EXTRACT") && atoi(getenv("SCT_FASTQ_EXTRACT")) == 1;  // A/B
-    const void* kf = v1 ? (const void*)extract_kernel : (const void*)extract2_kernel;
-    hipLaunchKernelGGL(v1 ? extract_kernel : extract2_kernel, dim3(resident_grid(kf, ix->ntiles)), dim3(WG), 0, s,
+    hipLaunchKernelGGL(extract2_kernel, dim3(resident_grid((const void*)extract2_kernel, ix->ntiles)), dim3(WG), 0, s,
                        d_buf, ix->nbytes, fs,
                        ix->text, ix->d_offsets, ix->d_first, ix->ntiles, ix->nrec, sp, d_seq, d_qual,
                        d_seq_len, d_qual_len, ix->d_bad);
