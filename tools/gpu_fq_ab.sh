@@ -9,7 +9,7 @@ timeout -k 10 300 python -u -m pytest tests -x -q --timeout 120 --timeout-method
 rc=$?; echo "pytest rc=$rc"; [ $rc -gt 1 ] && exit $rc
 for i in 1 2 3; do
   echo "{\"lib\": \"new\", \"t\": $(timeout -k 10 120 python -u tools/fq_experiment.py)}" >> gpurun_out/fq_ab.jsonl || exit $?
-  echo "{\"lib\": \"new_v1\", \"t\": $(SCT_FASTQ_EXTRACT=1 timeout -k 10 120 python -u tools/fq_experiment.py)}" >> gpurun_out/fq_ab.jsonl || exit $?
+
   echo "{\"lib\": \"old\", \"t\": $(SCTOOLS_HIP_LIB=$PWD/${OLD_LIB:-sctools_amd/libsctools_hip_old.so} timeout -k 10 120 python -u tools/fq_experiment.py)}" >> gpurun_out/fq_ab.jsonl || exit $?
 done
 exit 0
