@@ -1593,14 +1593,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     unsigned long long* __restrict__ counts, unsigned long long add_n) {
   tile_reg_body<true, 0, 1>(buf, order, z0, nslices, counts, add_n);
 }
-// the same with the plane sums as packed int16 (QP 3); at 3 waves per SIMD, with / without the
-// next plane in flight
+// the same with the plane sums as packed int16 (QP 3): 167 VGPRs, 3 waves per SIMD; at 3 waves
+// per SIMD without the next plane in flight
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_p16_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<true, 0, 3>(buf, order, z0, nslices, counts, add_n);
-}
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_reg_p16w3_kernel(
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
     unsigned long long* __restrict__ counts, unsigned long long add_n) {
   tile_reg_body<true, 0, 3>(buf, order, z0, nslices, counts, add_n);
@@ -1610,16 +1605,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
     unsigned long long* __restrict__ counts, unsigned long long add_n) {
   tile_reg_body<false, 0, 3>(buf, order, z0, nslices, counts, add_n);
 }
-// packed plane sums, one quarter at a time (QP 4): 3 waves per SIMD; 4 (spills), with / without prefetch
+// packed plane sums, one quarter at a time (QP 4), 3 waves per SIMD (at 4 the compiler spills)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_reg_q16w3_kernel(
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
     unsigned long long* __restrict__ counts, unsigned long long add_n) {
   tile_reg_body<true, 0, 4>(buf, order, z0, nslices, counts, add_n);
-}
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_reg_q16w4np_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<false, 0, 4>(buf, order, z0, nslices, counts, add_n);
 }
 // the same with the second pair's stage 1 issued before the first pair's squares
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_qp2_kernel(
@@ -2139,14 +2129,11 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
           hipLaunchKernelGGL(tile_reg_qp2_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
         else if (st.tile_reg == 6)
           hipLaunchKernelGGL(tile_reg_p16_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
-        else if (st.tile_reg == 7)
-          hipLaunchKernelGGL(tile_reg_p16w3_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
         else if (st.tile_reg == 8)
           hipLaunchKernelGGL(tile_reg_p16w3np_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
         else if (st.tile_reg == 9)
           hipLaunchKernelGGL(tile_reg_q16w3_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
-        else if (st.tile_reg == 10)
-          hipLaunchKernelGGL(tile_reg_q16w4np_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+
         else
           hipLaunchKernelGGL(tile_reg_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
       } else {
@@ -2250,18 +2237,15 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
     // for "reg_qp" (pairs, int32 sums, 2 waves per SIMD) and 0.291-0.306 for "reg" on the same boxes)
     st.tile_reg = !tv ? 6 : !strcmp(tv, "mfma2") ? 0 : !strcmp(tv, "reg_np") ? 2 : !strcmp(tv, "reg_w3") ? 3
                 : !strcmp(tv, "reg") ? 1 : !strcmp(tv, "reg_qp2") ? 5 : !strcmp(tv, "reg_p16") ? 6
-                : !strcmp(tv, "reg_p16w3") ? 7 : !strcmp(tv, "reg_p16w3np") ? 8 : !strcmp(tv, "reg_q16w3") ? 9
-                : !strcmp(tv, "reg_q16w4np") ? 10 : !strcmp(tv, "reg_qp") ? 4 : 6;
+                : !strcmp(tv, "reg_p16w3np") ? 8 : !strcmp(tv, "reg_q16w3") ? 9 : !strcmp(tv, "reg_qp") ? 4 : 6;
     int per_cu_reg = 0;  // its resident workgroups per CU
     const void* kf = st.tile_reg == 2 ? (const void*)tile_reg_np_kernel
                      : st.tile_reg == 3 ? (const void*)tile_reg_w3_kernel
                      : st.tile_reg == 4 ? (const void*)tile_reg_qp_kernel
                      : st.tile_reg == 5 ? (const void*)tile_reg_qp2_kernel
                      : st.tile_reg == 6 ? (const void*)tile_reg_p16_kernel
-                     : st.tile_reg == 7 ? (const void*)tile_reg_p16w3_kernel
                      : st.tile_reg == 8 ? (const void*)tile_reg_p16w3np_kernel
-                     : st.tile_reg == 9 ? (const void*)tile_reg_q16w3_kernel
-                     : st.tile_reg == 10 ? (const void*)tile_reg_q16w4np_kernel : (const void*)tile_reg_kernel;
+                     : st.tile_reg == 9 ? (const void*)tile_reg_q16w3_kernel : (const void*)tile_reg_kernel;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_reg, kf, 256, 0) != hipSuccess || per_cu_reg <= 0)
       per_cu_reg = 2;
     st.tile_reg_wgs = per_cu_reg;
