@@ -59,6 +59,32 @@ constexpr int ctz_c(int i) {
   return k;
 }
 
+// Bit planes of a 32-code group: planes + g * kPlaneWords holds its 18 planes (plane k bit j =
+// bit k of (code >> 14) of the group's j-th code) and 2 words of padding, so a group's planes
+// are five aligned 16-B words: one lane's group is 5 loads from 2 lines, not 18 from 18.
+constexpr int kPlaneWords = 20;
+__device__ __forceinline__ void load_planes(const uint32_t* __restrict__ planes, int64_t g, uint32_t* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(planes + g * kPlaneWords);
+  uint32_t w[kPlaneWords];
+#pragma unroll
+  for (int i = 0; i < kPlaneWords / 4; ++i) {
+    const uint4 v = q[i];
+    w[4 * i] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+#pragma unroll
+  for (int k = 0; k < 18; ++k) p[k] = w[k];
+}
+__device__ __forceinline__ void store_planes(uint32_t* __restrict__ planes, int64_t g, const uint32_t* p) {
+  uint4* q = reinterpret_cast<uint4*>(planes + g * kPlaneWords);
+#pragma unroll
+  for (int i = 0; i < kPlaneWords / 4; ++i)
+    q[i] = make_uint4(4 * i < 18 ? p[4 * i] : 0u, 4 * i + 1 < 18 ? p[4 * i + 1] : 0u,
+                      4 * i + 2 < 18 ? p[4 * i + 2] : 0u, 4 * i + 3 < 18 ? p[4 * i + 3] : 0u);
+}
+
 // in-register WHT of N values
 template <int N>
 __device__ __forceinline__ void wht(int32_t* x) {
@@ -218,11 +244,10 @@ __global__ __launch_bounds__(256) void planes_slot_kernel(const uint32_t* __rest
     for (int b = 0; b < kHiBits; ++b) p[b] |= (h >> b) & 1u ? bit : 0u;
   }
   const int64_t g = g0 + k;
-#pragma unroll
-  for (int b = 0; b < kHiBits; ++b) planes[b * max_groups + g] = p[b];
+  store_planes(planes, g, p);
 }
 
-// planes[k * max_groups + g] bit j = bit k of (code >> 14) of the j-th code of group g
+// group g's planes (load_planes layout)
 __global__ void planes_kernel(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ off,
                               const uint32_t* __restrict__ gofs, int64_t max_groups,
                               uint32_t* __restrict__ planes) {
@@ -244,8 +269,7 @@ __global__ void planes_kernel(const uint32_t* __restrict__ hi, const uint32_t* _
 #pragma unroll
     for (int k = 0; k < kHiBits; ++k) p[k] |= (h >> k) & 1u ? bit : 0u;
   }
-#pragma unroll
-  for (int k = 0; k < kHiBits; ++k) planes[k * max_groups + g] = p[k];
+  store_planes(planes, g, p);
 }
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -322,8 +346,12 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
   uint32_t pr[kRegG][kHiBits];
 #pragma unroll
   for (int g = 0; g < kRegG; ++g)
+    if (g < ng) {
+      load_planes(planes, (int64_t)g0 + g, pr[g]);
+    } else {
 #pragma unroll
-    for (int k = 0; k < kHiBits; ++k) pr[g][k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
+      for (int k = 0; k < kHiBits; ++k) pr[g][k] = 0u;
+    }
   // int8 byte store-out: this thread writes columns c0 + mcb .. + 15; mx = their m | 0x80
   // as bytes (ABL 4 = the same path, for A/B against the ablations)
   constexpr bool kByteStage = sizeof(T) == 1 && (ABL == 0 || ABL == 4 || ABL == 6 || ABL == 7 || (ABL >= 8 && ABL <= 10));
@@ -383,8 +411,12 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
       if (g < wng) walk(pr[g], std::false_type());
     for (int g = kRegG; g < wng; ++g) {  // dense columns: the rest from L2
       uint32_t p[kHiBits];
+      if (g < ng) {
+        load_planes(planes, (int64_t)g0 + g, p);
+      } else {
 #pragma unroll
-      for (int k = 0; k < kHiBits; ++k) p[k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
+        for (int k = 0; k < kHiBits; ++k) p[k] = 0u;
+      }
       walk(p, std::false_type());
     }
   }
@@ -540,8 +572,12 @@ __device__ __forceinline__ void seed_spread_body(const uint32_t* __restrict__ pl
   uint32_t pr[kRegG][kHiBits];
 #pragma unroll
   for (int g = 0; g < kRegG; ++g)
+    if (g < ng) {
+      load_planes(planes, (int64_t)g0 + g, pr[g]);
+    } else {
 #pragma unroll
-    for (int k = 0; k < kHiBits; ++k) pr[g][k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
+      for (int k = 0; k < kHiBits; ++k) pr[g][k] = 0u;
+    }
   // store-out: this thread writes row tid / 16 of a block, columns c0 + mcb .. + 15
   const int mcb = (tid % (NT / 16)) * 16, srow = tid / (NT / 16);
   uint4 mx;
@@ -592,8 +628,12 @@ __device__ __forceinline__ void seed_spread_body(const uint32_t* __restrict__ pl
       }
       for (int g = kRegG; g < wng; ++g) {  // dense columns: the rest from L2, state rebuilt
         uint32_t p[kHiBits];
+        if (g < ng) {
+          load_planes(planes, (int64_t)g0 + g, p);
+        } else {
 #pragma unroll
-        for (int k = 0; k < kHiBits; ++k) p[k] = g < ng ? planes[k * max_groups + g0 + g] : 0u;
+          for (int k = 0; k < kHiBits; ++k) p[k] = 0u;
+        }
         uint32_t y = 0;
         const int zs = zblk + gray(kB * b);  // the slice of the block's first step
 #pragma unroll
@@ -2269,7 +2309,7 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   st.max_groups = sct::ceil_div(n, 32) + kLo;
   SCT_HIP(hipMalloc(&st.d_gofs, (size_t)(kLo + 1) * 4));
   SCT_HIP(hipMalloc(&st.d_hist, (size_t)kSortWGs * kLo * 4));
-  SCT_HIP(hipMalloc(&st.d_planes, (size_t)st.max_groups * kHiBits * 4));
+  SCT_HIP(hipMalloc(&st.d_planes, (size_t)st.max_groups * kPlaneWords * 4));
   if (st.elem_bytes != 1) st.ilv = 0;
   const size_t buf_bytes = (size_t)((st.chunk + 15) & ~15ll) * kLo * st.elem_bytes;  // whole 16-slice groups
   SCT_HIP(hipMalloc(&st.d_buf, buf_bytes));
