@@ -1,0 +1,133 @@
+"""Property tests (hypothesis) of the drop-in encoders and summaries on the GPU against the
+oracle's restatement of the reference (oracle/oracle.py, pinned by the golden fixtures):
+random barcodes over the reference's alphabets -- upper / lower case, IUPAC ambiguity codes,
+N, bytes outside every map -- and random small barcode sets.
+
+Each example is one batch through the C ABI: codes, GC, decode and Hamming distances must be
+bit-exact, the global `random` state after a TwoBit batch must equal the state after the
+reference's per-record loop (encodings.py:63-69 draws `random.randint(0, 3)` per ambiguous
+base, left to right), and an invalid byte must raise the reference's KeyError after the same
+draws."""
+import random
+
+import numpy as np
+import pytest
+
+hypothesis = pytest.importorskip("hypothesis")
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+from oracle import oracle as O  # noqa: E402
+from sctools_amd import barcode, encodings  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+ACGT = b"ACGTacgt"
+IUPAC = b"MRWSYKVHDBNmrwsykvhdbn"
+OTHER = b"XZ-.0 \x00\xff"
+
+SETTINGS = settings(max_examples=60, deadline=None, derandomize=True)
+
+
+def _records(alphabet, min_len=1, max_len=40):
+    return st.integers(min_len, max_len).flatmap(
+        lambda L: st.lists(st.binary(min_size=L, max_size=L).map(lambda b: bytes(alphabet[x % len(alphabet)] for x in b)),
+                           min_size=1, max_size=40))
+
+
+def _oracle_two_bit_batch(seqs):
+    out = []
+    for s in seqs:
+        out.append(O.two_bit_encode(s))
+    return out
+
+
+@SETTINGS
+@given(seqs=_records(ACGT + IUPAC), seed=st.integers(0, 2**32 - 1))
+def test_two_bit_encode_batch_matches_reference_loop(seqs, seed):
+    """Codes and the RNG state after the batch (ambiguous bases drawn in reference order)."""
+    random.seed(seed)
+    want = _oracle_two_bit_batch(seqs)
+    want_state = random.getstate()
+    random.seed(seed)
+    got, gc = encodings.TwoBit.encode_array(seqs, return_gc=True)
+    L = len(seqs[0])
+    got_ints = [int(x) for x in got] if got.ndim == 1 else \
+        [sum(int(w) << (64 * k) for k, w in enumerate(row)) for row in got]
+    assert got_ints == want
+    assert random.getstate() == want_state
+    assert [int(g) for g in gc] == [O.two_bit_gc(c, L) for c in want]
+
+
+@SETTINGS
+@given(seqs=_records(ACGT + IUPAC + OTHER, max_len=24), seed=st.integers(0, 2**32 - 1))
+def test_two_bit_encode_invalid_bytes_raise_like_reference(seqs, seed):
+    """A batch holding bytes outside the IUPAC map raises the reference's KeyError for the
+    first one in record order, after exactly the draws the reference makes before it."""
+    random.seed(seed)
+    want_exc = None
+    try:
+        want = _oracle_two_bit_batch(seqs)
+    except KeyError as e:
+        want_exc = e.args
+    want_state = random.getstate()
+    random.seed(seed)
+    if want_exc is None:
+        got = encodings.TwoBit.encode_array(seqs)
+        assert [int(x) for x in np.atleast_1d(got)] == want
+    else:
+        with pytest.raises(KeyError) as ei:
+            encodings.TwoBit.encode_array(seqs)
+        assert ei.value.args == want_exc
+    assert random.getstate() == want_state
+
+
+@SETTINGS
+@given(seqs=_records(ACGT + IUPAC + OTHER, max_len=21))
+def test_three_bit_encode_decode_gc(seqs):
+    """ThreeBit: any byte outside the map is N (encodings.py:145-149); decode / GC of the
+    codes as the reference computes them (one-limb codes, L <= 21)."""
+    got, gc = encodings.ThreeBit.encode_array(seqs, return_gc=True)
+    want = [O.three_bit_encode(s) for s in seqs]
+    assert [int(x) for x in got] == want
+    assert [int(g) for g in gc] == [O.three_bit_gc(c) for c in want]
+    dec = encodings.ThreeBit.decode_array(np.asarray(want, dtype=np.uint64))
+    assert [bytes(d) for d in dec] == [O.three_bit_decode(c) for c in want]
+
+
+@SETTINGS
+@given(L=st.integers(1, 32), data=st.data())
+def test_two_bit_decode_gc_hamming(L, data):
+    n = data.draw(st.integers(1, 64))
+    a = np.array(data.draw(st.lists(st.integers(0, 4**L - 1), min_size=n, max_size=n)), dtype=np.uint64)
+    b = np.array(data.draw(st.lists(st.integers(0, 4**L - 1), min_size=n, max_size=n)), dtype=np.uint64)
+    tb = encodings.TwoBit(L)
+    assert [bytes(x) for x in tb.decode_array(a)] == [O.two_bit_decode(int(c), L) for c in a]
+    assert [int(g) for g in tb.gc_content_array(a)] == [O.two_bit_gc(int(c), L) for c in a]
+    assert [int(d) for d in encodings.TwoBit.hamming_distance_array(a, b)] == \
+        [O.two_bit_hamming(int(x), int(y)) for x, y in zip(a, b)]
+
+
+@SETTINGS
+@given(L=st.integers(1, 21), data=st.data())
+def test_three_bit_hamming(L, data):
+    n = data.draw(st.integers(1, 64))
+    a = np.array(data.draw(st.lists(st.integers(0, 8**L - 1), min_size=n, max_size=n)), dtype=np.uint64)
+    b = np.array(data.draw(st.lists(st.integers(0, 8**L - 1), min_size=n, max_size=n)), dtype=np.uint64)
+    assert [int(d) for d in encodings.ThreeBit.hamming_distance_array(a, b)] == \
+        [O.three_bit_hamming(int(x), int(y)) for x, y in zip(a, b)]
+
+
+@SETTINGS
+@given(L=st.integers(1, 16), data=st.data())
+def test_summarize_small_sets(L, data):
+    """summarize_hamming_distances on small random sets (close codes drawn from a small pool)
+    equals numpy's percentiles and mean over the reference's pair loop (barcode.py:39-46)."""
+    n = data.draw(st.integers(2, 60))
+    pool = data.draw(st.lists(st.integers(0, 4**L - 1), min_size=1, max_size=n))
+    codes = [pool[data.draw(st.integers(0, len(pool) - 1))] for _ in range(n)]
+    s = barcode.Barcodes({c: 1 for c in codes}, L) if len(set(codes)) >= 2 else None
+    if s is None:
+        return
+    keys = list(s.keys())
+    dists = [O.two_bit_hamming(a, b) for i, a in enumerate(keys) for b in keys[i + 1:]]
+    assert s.summarize_hamming_distances() == O.summary_numpy(np.array(dists, dtype=np.int64))
