@@ -128,6 +128,6 @@ def test_summarize_small_sets(L, data):
     s = barcode.Barcodes({c: 1 for c in codes}, L) if len(set(codes)) >= 2 else None
     if s is None:
         return
-    keys = list(s.keys())
+    keys = list(s)
     dists = [O.two_bit_hamming(a, b) for i, a in enumerate(keys) for b in keys[i + 1:]]
     assert s.summarize_hamming_distances() == O.summary_numpy(np.array(dists, dtype=np.int64))
