@@ -122,6 +122,20 @@ int sct_hamming_pairs(int kind, const uint64_t* a, const uint64_t* b, int64_t n,
 int sct_hamming_pairs_host(int kind, const uint64_t* a, const uint64_t* b, int64_t n, int words,
                            int32_t* out);
 
+/* ---------------------------------------------------------------- scalar server
+ * The *_host calls above with n <= 64 records (the drop-in's scalar methods, e.g.
+ * TwoBit.encode / hamming_distance, encodings.py:75-121) are served by a resident
+ * one-wave kernel per host thread and device that polls a page-locked mailbox, instead of
+ * one kernel launch per call; it exits by itself after SCT_SCALAR_IDLE_MS (default 5) idle
+ * milliseconds and before any kernel that sizes its grid to the resident workgroups.
+ * SCT_SCALAR_SERVER=0 turns it off (every call is then a launch).
+ * sct_scalar_server_stop: ask every server of the process to exit and wait for it.
+ * sct_scalar_server_status: server launches so far and servers running now (either may
+ * be NULL).
+ */
+int sct_scalar_server_stop(void);
+int sct_scalar_server_status(int64_t* launches, int* running);
+
 /* ---------------------------------------------------------------- all-pairs histogram
  * Replaces the pair loop of Barcodes.summarize_hamming_distances
  * (src/sctools/barcode.py:42-43: itertools.combinations + TwoBit.hamming_distance).

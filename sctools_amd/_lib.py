@@ -91,6 +91,8 @@ SIGNATURES = {
     "sct_fastq_stream_chunk": [_vp, _vp, _i64, _vp, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                                ctypes.POINTER(_i64)],
     "sct_fastq_stream_fetch": [_vp, _vp, _vp, _vp, _vp],
+    "sct_scalar_server_stop": [],
+    "sct_scalar_server_status": [ctypes.POINTER(_i64), ctypes.POINTER(_i32)],
 }
 _RESTYPES = {"sct_last_error": ctypes.c_char_p}
 

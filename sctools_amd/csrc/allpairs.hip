@@ -1171,6 +1171,7 @@ extern "C" int sct_allpairs_build_items(sct_allpairs_plan* plan, int64_t item_be
 extern "C" int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
                                   uint64_t* d_counts, int grid, void* stream) {
   SCT_CHECK(plan != nullptr, "plan is NULL");
+  sct::scalar_quiesce();  // persistent grids below size themselves to the resident slots
   SCT_CHECK(d_counts != nullptr, "counts is NULL");
   SCT_CHECK(0 <= item_begin && item_begin <= item_end && item_end <= plan->items,
             "item range [%lld, %lld) outside [0, %lld)", (long long)item_begin,
@@ -1184,6 +1185,7 @@ extern "C" int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, i
 
 extern "C" int sct_allpairs_time_kernels(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
                                          uint64_t* d_counts, int repeats, double* out, void* stream) {
+  sct::scalar_quiesce();
   SCT_CHECK(plan != nullptr && d_counts != nullptr && out != nullptr, "NULL pointer");
   SCT_CHECK(0 <= item_begin && item_begin < item_end && item_end <= plan->items && repeats > 0,
             "item range [%lld, %lld) outside [0, %lld) or repeats < 1", (long long)item_begin,

@@ -15,8 +15,15 @@
 //   ThreeBit.decode :169-180 triplets up to the top non-zero one; 0/5/7 -> KeyError
 //   ThreeBit.gc     :182-192 bit 0 of every triplet
 //   ThreeBit.hamming:194-202 non-zero 3-bit groups of a^b
-#include <algorithm>
+#include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <vector>
 
 #include "sct_common.h"
 
@@ -73,6 +80,48 @@ struct RecordReader {
   }
 };
 
+// One record of L bytes through the byte LUT into `words` limbs of out; returns the GC
+// count (capped at 255 by the callers) and the ambiguous / invalid flags (bits 0 / 1).
+__device__ __forceinline__ void encode_record(const uint8_t* lut, int bits, RecordReader& rd, int L, int words,
+                                              uint64_t* out, uint32_t& g, uint32_t& flag_bits) {
+  uint32_t fl = 0;
+  g = 0;
+  if (words == 1) {
+    uint64_t code = 0;
+    for (int p = 0; p < L; ++p) {
+      const uint32_t e = lut[rd.byte(p)];
+      code = (code << bits) | (e & 7u);
+      fl |= e;
+    }
+    out[0] = code;
+    const uint64_t m = bits == 2 ? 0x5555555555555555ull : 0x9249249249249249ull;
+    g = __popcll(code & m);
+  } else {
+    // LSB-first over positions so limbs complete in order; a triplet may straddle limbs.
+    uint64_t cur = 0, nxt = 0;
+    int wcur = 0;
+    for (int p = L - 1; p >= 0; --p) {
+      const uint32_t e = lut[rd.byte(p)];
+      fl |= e;
+      const uint64_t v = e & 7u;
+      g += (uint32_t)(v & 1u);
+      const int64_t pos = (int64_t)bits * (L - 1 - p);
+      const int w = (int)(pos >> 6), off = (int)(pos & 63);
+      while (w > wcur) {
+        out[wcur++] = cur;
+        cur = nxt;
+        nxt = 0;
+      }
+      cur |= v << off;
+      if (off + bits > 64) nxt |= v >> (64 - off);
+    }
+    out[wcur++] = cur;
+    if (wcur < words) out[wcur++] = nxt;
+    while (wcur < words) out[wcur++] = 0;
+  }
+  flag_bits = ((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u);
+}
+
 // Records at seqs + r * stride of L bytes, or (starts != nullptr) at seqs + starts[r] of
 // lens[r] bytes each (variable-length lines: the whitelist ingest, sctools_amd/csrc/lines.hip).
 __global__ __launch_bounds__(WG) void encode_kernel(int kind, const uint8_t* __restrict__ seqs,
@@ -84,48 +133,13 @@ __global__ __launch_bounds__(WG) void encode_kernel(int kind, const uint8_t* __r
                                                     const int32_t* __restrict__ lens = nullptr) {
   __shared__ uint8_t lut[256];
   fill_lut(lut, kind);
-  const int bits = kind;
   for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
     const int L = starts ? lens[r] : L_all;
     RecordReader rd{seqs + (starts ? starts[r] : r * stride), dword_path, 0u, -1};
-    uint32_t fl = 0;
-    uint64_t* out = codes + r * words;
-    uint32_t g = 0;
-    if (words == 1) {
-      uint64_t code = 0;
-      for (int p = 0; p < L; ++p) {
-        const uint32_t e = lut[rd.byte(p)];
-        code = (code << bits) | (e & 7u);
-        fl |= e;
-      }
-      out[0] = code;
-      const uint64_t m = bits == 2 ? 0x5555555555555555ull : 0x9249249249249249ull;
-      g = __popcll(code & m);
-    } else {
-      // LSB-first over positions so limbs complete in order; a triplet may straddle limbs.
-      uint64_t cur = 0, nxt = 0;
-      int wcur = 0;
-      for (int p = L - 1; p >= 0; --p) {
-        const uint32_t e = lut[rd.byte(p)];
-        fl |= e;
-        const uint64_t v = e & 7u;
-        g += (uint32_t)(v & 1u);
-        const int64_t pos = (int64_t)bits * (L - 1 - p);
-        const int w = (int)(pos >> 6), off = (int)(pos & 63);
-        while (w > wcur) {
-          out[wcur++] = cur;
-          cur = nxt;
-          nxt = 0;
-        }
-        cur |= v << off;
-        if (off + bits > 64) nxt |= v >> (64 - off);
-      }
-      out[wcur++] = cur;
-      if (wcur < words) out[wcur++] = nxt;
-      while (wcur < words) out[wcur++] = 0;
-    }
+    uint32_t g, fl;
+    encode_record(lut, kind, rd, L, words, codes + r * words, g, fl);
     if (gc) gc[r] = (uint8_t)(g > 255 ? 255 : g);
-    if (flags) flags[r] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
+    if (flags) flags[r] = (uint8_t)fl;
   }
 }
 
@@ -250,50 +264,57 @@ __device__ __forceinline__ uint32_t group_at(const uint64_t* w, int words, int64
   return (uint32_t)(v & ((1u << width) - 1u));
 }
 
+__device__ __forceinline__ void decode2_record(const uint64_t* w, int words, int L, uint8_t* o) {
+  for (int p = 0; p < L; ++p) {
+    const int64_t pos = 2LL * (L - 1 - p);
+    const uint32_t v = pos < 64LL * words ? group_at(w, words, pos, 2) : 0u;
+    o[p] = (uint8_t)("ACTG"[v]);
+  }
+}
+
 __global__ __launch_bounds__(WG) void decode2_kernel(const uint64_t* __restrict__ codes, int64_t n,
                                                      int words, int L, uint8_t* __restrict__ out) {
-  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
-    const uint64_t* w = codes + r * words;
-    uint8_t* o = out + r * L;
-    for (int p = 0; p < L; ++p) {
-      const int64_t pos = 2LL * (L - 1 - p);
-      const uint32_t v = pos < 64LL * words ? group_at(w, words, pos, 2) : 0u;
-      o[p] = (uint8_t)("ACTG"[v]);
+  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG)
+    decode2_record(codes + r * words, words, L, out + r * L);
+}
+
+// o[maxlen - 1 - t] = base of triplet t for t <= the top non-zero triplet; returns that
+// count, and in err the first invalid triplet value (0 / 5 / 7) or -1
+__device__ __forceinline__ int32_t decode3_record(const uint64_t* w, int words, int maxlen, uint8_t* o,
+                                                  int32_t& err) {
+  const int ntrip = (64 * words + 2) / 3;
+  int top = -1;
+  for (int t = ntrip - 1; t >= 0; --t)
+    if (group_at(w, words, 3LL * t, 3) != 0u) {
+      top = t;
+      break;
     }
+  err = -1;
+  for (int t = 0; t <= top; ++t) {
+    const uint32_t v = group_at(w, words, 3LL * t, 3);
+    uint8_t ch = 0;
+    switch (v) {
+      case 1: ch = 'C'; break;
+      case 2: ch = 'A'; break;
+      case 3: ch = 'G'; break;
+      case 4: ch = 'T'; break;
+      case 6: ch = 'N'; break;
+      default:
+        if (err < 0) err = (int32_t)v;
+        break;
+    }
+    o[maxlen - 1 - t] = ch;
   }
+  return top + 1;
 }
 
 __global__ __launch_bounds__(WG) void decode3_kernel(const uint64_t* __restrict__ codes, int64_t n,
                                                      int words, int maxlen, uint8_t* __restrict__ out,
                                                      int32_t* __restrict__ lengths,
                                                      int32_t* __restrict__ bad) {
-  const int ntrip = (64 * words + 2) / 3;
   for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
-    const uint64_t* w = codes + r * words;
-    int top = -1;
-    for (int t = ntrip - 1; t >= 0; --t)
-      if (group_at(w, words, 3LL * t, 3) != 0u) {
-        top = t;
-        break;
-      }
-    int32_t err = -1;
-    uint8_t* o = out + r * maxlen;
-    for (int t = 0; t <= top; ++t) {
-      const uint32_t v = group_at(w, words, 3LL * t, 3);
-      uint8_t ch = 0;
-      switch (v) {
-        case 1: ch = 'C'; break;
-        case 2: ch = 'A'; break;
-        case 3: ch = 'G'; break;
-        case 4: ch = 'T'; break;
-        case 6: ch = 'N'; break;
-        default:
-          if (err < 0) err = (int32_t)v;
-          break;
-      }
-      o[maxlen - 1 - t] = ch;
-    }
-    lengths[r] = top + 1;
+    int32_t err;
+    lengths[r] = decode3_record(codes + r * words, words, maxlen, out + r * maxlen, err);
     bad[r] = err;
   }
 }
@@ -307,51 +328,54 @@ __device__ __forceinline__ uint64_t m3(int i) {
   }
 }
 
+__device__ __forceinline__ int32_t gc_record(int kind, const uint64_t* w, int words, int L) {
+  int32_t g = 0;
+  for (int i = 0; i < words; ++i) {
+    uint64_t m;
+    if (kind == 2) {
+      const int64_t lo = 64LL * i, rem = 2LL * L - lo;  // bits of the L groups inside this limb
+      if (rem <= 0) break;
+      m = 0x5555555555555555ull;
+      if (rem < 64) m &= (1ull << rem) - 1ull;
+    } else {
+      m = m3(i);
+    }
+    g += __popcll(w[i] & m);
+  }
+  return g;
+}
+
 __global__ __launch_bounds__(WG) void gc_kernel(int kind, const uint64_t* __restrict__ codes,
                                                 int64_t n, int words, int L,
                                                 int32_t* __restrict__ out) {
-  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
-    const uint64_t* w = codes + r * words;
-    int32_t g = 0;
+  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG)
+    out[r] = gc_record(kind, codes + r * words, words, L);
+}
+
+__device__ __forceinline__ int32_t hamming_record(int kind, const uint64_t* x, const uint64_t* y, int words) {
+  int32_t d = 0;
+  if (kind == 2) {
     for (int i = 0; i < words; ++i) {
-      uint64_t m;
-      if (kind == 2) {
-        const int64_t lo = 64LL * i, rem = 2LL * L - lo;  // bits of the L groups inside this limb
-        if (rem <= 0) break;
-        m = 0x5555555555555555ull;
-        if (rem < 64) m &= (1ull << rem) - 1ull;
-      } else {
-        m = m3(i);
-      }
-      g += __popcll(w[i] & m);
+      const uint64_t v = x[i] ^ y[i];
+      d += __popcll((v | (v >> 1)) & 0x5555555555555555ull);
     }
-    out[r] = g;
+  } else {
+    uint64_t v = x[0] ^ y[0];
+    for (int i = 0; i < words; ++i) {
+      const uint64_t nx = i + 1 < words ? (x[i + 1] ^ y[i + 1]) : 0ull;
+      const uint64_t s = v | ((v >> 1) | (nx << 63)) | ((v >> 2) | (nx << 62));
+      d += __popcll(s & m3(i));
+      v = nx;
+    }
   }
+  return d;
 }
 
 __global__ __launch_bounds__(WG) void hamming_kernel(int kind, const uint64_t* __restrict__ a,
                                                      const uint64_t* __restrict__ b, int64_t n,
                                                      int words, int32_t* __restrict__ out) {
-  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
-    const uint64_t* x = a + r * words;
-    const uint64_t* y = b + r * words;
-    int32_t d = 0;
-    if (kind == 2) {
-      for (int i = 0; i < words; ++i) {
-        const uint64_t v = x[i] ^ y[i];
-        d += __popcll((v | (v >> 1)) & 0x5555555555555555ull);
-      }
-    } else {
-      uint64_t v = x[0] ^ y[0];
-      for (int i = 0; i < words; ++i) {
-        const uint64_t nx = i + 1 < words ? (x[i + 1] ^ y[i + 1]) : 0ull;
-        const uint64_t s = v | ((v >> 1) | (nx << 63)) | ((v >> 2) | (nx << 62));
-        d += __popcll(s & m3(i));
-        v = nx;
-      }
-    }
-    out[r] = d;
-  }
+  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG)
+    out[r] = hamming_record(kind, a + r * words, b + r * words, words);
 }
 
 // per-position base counts: LDS u32 tallies per workgroup, one u64 atomic per bin
@@ -398,6 +422,7 @@ extern "C" int sct_encode(int kind, const uint8_t* seqs, int64_t n, int64_t stri
   // (fewer records than one tile -- the drop-in's scalar calls -- skip the occupancy query)
   if (n >= R * WG && stride == L && words == 1 && L > 0 && L <= 64 && (uintptr_t)seqs % 16 == 0) {
     const size_t lds = (size_t)R * WG * L;
+    sct::scalar_quiesce();
     // persistent: exactly the resident workgroups (a 4096 grid at 5 per CU left a partial
     // last round of workgroups, each looping over many tiles)
     int dev = 0, cus = 0, per_cu = 0;
@@ -499,6 +524,316 @@ extern "C" int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint6
   return SCT_OK;
 }
 
+#define SCT_TRY(x)              \
+  do {                          \
+    int rc_ = (x);              \
+    if (rc_ != SCT_OK) return rc_; \
+  } while (0)
+// ---------------------------------------------------------------- resident scalar server
+// A scalar drop-in call (TwoBit.encode, hamming_distance, decode, gc_content: a batch of
+// one) costs a kernel launch and its completion signal, ~15 us, while the work is a few
+// hundred instructions.  Instead, the first such call of a host thread on a device launches
+// one 64-lane server kernel that polls a page-locked, host-coherent mailbox over PCIe:
+// the host writes the request (opcode, sizes, the packed inputs) and then its sequence
+// number; the wave sees the new number, pulls the payload into LDS with one round of
+// dword loads, runs the same per-record device functions as the batch kernels (one record
+// per lane, n <= 64), writes the outputs back with system-scope stores and publishes the
+// sequence number as done.  The wave exits after idle_ticks of its wall clock without a
+// request, on the mailbox's stop word, or never while a request is pending; it always
+// writes its launch id to exit_gen last, so the host tells "exited" from "slow" without a
+// HIP call, and relaunches (the pending request is served first) when it finds its
+// request unanswered and the server gone.
+namespace {
+enum : uint32_t { OP_ENCODE = 1, OP_DECODE2 = 2, OP_DECODE3 = 3, OP_GC = 4, OP_HAMMING = 5 };
+constexpr int kSrvIn = 1024, kSrvOut = 1024, kSrvMaxN = 64;
+
+constexpr int kSrvInline = 32;  // payload bytes that ride in the request line itself
+
+// One request line of 64 B: req[0] = seq (written last), req[1..7] = the packed fields,
+// req[8..15] = the first 32 payload bytes; the rest of the payload follows contiguously in
+// `more`.  The wave reads the whole line with one 64-B load per poll, so a scalar call
+// (payload <= 32 B: a pair of one-limb codes, a 32-base record) costs one PCIe read.
+struct SrvMailbox {
+  alignas(64) uint32_t req[16];
+  uint32_t more[(kSrvIn - kSrvInline) / 4];
+  // control (host)
+  alignas(64) uint32_t stop;
+  // response (device): the last served seq and its status; the launch id on exit
+  alignas(64) uint32_t done;
+  int32_t status;
+  uint32_t exit_gen;
+  alignas(64) uint32_t out[kSrvOut / 4];
+};
+static_assert(offsetof(SrvMailbox, more) == 64, "payload must continue the request line");
+
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ int32_t sys_load(const int32_t* p) {
+  return (int32_t)sys_load(reinterpret_cast<const uint32_t*>(p));
+}
+
+__global__ __launch_bounds__(64) void scalar_server_kernel(SrvMailbox* mb, uint32_t served, uint32_t gen,
+                                                           uint64_t idle_ticks) {
+  __shared__ uint8_t lut[2][256];
+  __shared__ uint32_t in_l[kSrvIn / 4], out_l[kSrvOut / 4];
+  const int lane = threadIdx.x;
+  for (int c = lane; c < 256; c += 64) {
+    lut[0][c] = lut_entry(2, c);
+    lut[1][c] = lut_entry(3, c);
+  }
+  __syncthreads();
+  uint64_t t_last = wall_clock64();
+  for (;;) {
+    const uint32_t line = lane < 16 ? sys_load(&mb->req[lane]) : 0u;
+    const uint32_t seq = __builtin_amdgcn_readlane(line, 0);
+    if (seq != served) {
+      const uint32_t h1 = __builtin_amdgcn_readlane(line, 1), h2 = __builtin_amdgcn_readlane(line, 2),
+                     h3 = __builtin_amdgcn_readlane(line, 3), h4 = __builtin_amdgcn_readlane(line, 4),
+                     h5 = __builtin_amdgcn_readlane(line, 5), h6 = __builtin_amdgcn_readlane(line, 6),
+                     h7 = __builtin_amdgcn_readlane(line, 7);
+      auto off16 = [](uint32_t v) { return v == 0xFFFFu ? -1 : (int)v; };
+      const uint32_t op = h1 & 0xFFu;
+      const int kind = (int)((h1 >> 8) & 0xFFu), words = (int)(h1 >> 16);
+      const int n = (int)(h2 & 0xFFFFu), L = (int)(h2 >> 16);
+      const int stride = (int)(h3 & 0xFFFFu), maxlen = (int)(h3 >> 16);
+      const int in_words = ((int)(h4 & 0xFFFFu) + 3) / 4, out_words = ((int)(h4 >> 16) + 3) / 4;
+      const int io[2] = {off16(h5 & 0xFFFFu), off16(h5 >> 16)};
+      const int oo[3] = {off16(h6 & 0xFFFFu), off16(h6 >> 16), off16(h7 & 0xFFFFu)};
+      // payload: the first 8 dwords came with the line; the rest (if any) in one more round trip
+      if (lane >= 8 && lane < 16 && lane - 8 < in_words) in_l[lane - 8] = line;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      for (int k = kSrvInline / 4 + lane; k < in_words; k += 64) in_l[k] = sys_load(&mb->more[k - kSrvInline / 4]);
+      for (int k = lane; k < out_words; k += 64) out_l[k] = 0u;
+      __syncthreads();
+      const uint8_t* in8 = reinterpret_cast<const uint8_t*>(in_l);
+      uint8_t* out8 = reinterpret_cast<uint8_t*>(out_l);
+      const int r = lane;
+      if (r < n) {
+        switch (op) {
+          case OP_ENCODE: {
+            RecordReader rd{in8 + io[0] + r * stride, false, 0u, -1};
+            uint32_t g, fl;
+            encode_record(lut[kind == 2 ? 0 : 1], kind, rd, L, words,
+                          reinterpret_cast<uint64_t*>(out8 + oo[0]) + r * words, g, fl);
+            if (oo[1] >= 0) out8[oo[1] + r] = (uint8_t)(g > 255 ? 255 : g);
+            if (oo[2] >= 0) out8[oo[2] + r] = (uint8_t)fl;
+            break;
+          }
+          case OP_DECODE2:
+            decode2_record(reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words, words, L, out8 + oo[0] + r * L);
+            break;
+          case OP_DECODE3: {
+            int32_t err;
+            const int32_t len = decode3_record(reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words, words, maxlen,
+                                               out8 + oo[0] + r * maxlen, err);
+            reinterpret_cast<int32_t*>(out8 + oo[1])[r] = len;
+            reinterpret_cast<int32_t*>(out8 + oo[2])[r] = err;
+            break;
+          }
+          case OP_GC:
+            reinterpret_cast<int32_t*>(out8 + oo[0])[r] =
+                gc_record(kind, reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words, words, L);
+            break;
+          case OP_HAMMING:
+            reinterpret_cast<int32_t*>(out8 + oo[0])[r] =
+                hamming_record(kind, reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words,
+                               reinterpret_cast<const uint64_t*>(in8 + io[1]) + r * words, words);
+            break;
+          default:
+            break;
+        }
+      }
+      __syncthreads();
+      for (int k = lane; k < out_words; k += 64)
+        __hip_atomic_store(&mb->out[k], out_l[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      if (lane == 0) {
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(&mb->status), (uint32_t)(op >= OP_ENCODE && op <= OP_HAMMING ? 0 : 1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      served = seq;
+      t_last = wall_clock64();
+      continue;
+    }
+    if (sys_load(&mb->stop) != 0u || wall_clock64() - t_last > idle_ticks) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (lane == 0) __hip_atomic_store(&mb->exit_gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+struct Server {
+  int device = -1;
+  SrvMailbox* mb = nullptr;      // host view
+  SrvMailbox* mb_dev = nullptr;  // device view
+  hipStream_t stream = nullptr;
+  uint32_t seq = 0;
+  std::atomic<uint32_t> gen{0};
+  uint64_t idle_ticks = 0;
+};
+
+std::mutex g_srv_mu;
+std::vector<Server*> g_servers;  // every server of the process (quiesce, exit)
+std::atomic<int64_t> g_srv_launches{0};
+
+template <class T>
+T host_load(const T* p) {
+  return __atomic_load_n(p, __ATOMIC_ACQUIRE);
+}
+
+bool server_running(const Server* sv) { return host_load(&sv->mb->exit_gen) != sv->gen.load(); }
+
+// ask one server to exit and wait (bounded) for its exit mark; no HIP calls (process exit)
+void server_stop(Server* sv, int64_t wait_us) {
+  if (!server_running(sv)) return;
+  __atomic_store_n(&sv->mb->stop, 1u, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (server_running(sv) &&
+         std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(wait_us)) {
+  }
+}
+
+void stop_all_at_exit() {
+  std::lock_guard<std::mutex> g(g_srv_mu);
+  for (Server* sv : g_servers) server_stop(sv, 200000);
+}
+
+bool server_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SCT_SCALAR_SERVER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// nullptr (error set) if the server cannot be created; callers then take the launch path
+Server* server() {
+  static thread_local Server* per_dev[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (per_dev[dev]) return per_dev[dev];
+  auto* sv = new Server();
+  sv->device = dev;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+  const char* e = getenv("SCT_SCALAR_IDLE_MS");
+  const double ms = e ? atof(e) : 5.0;
+  sv->idle_ticks = (uint64_t)(khz * (ms > 0 ? ms : 5.0));
+  if (hipStreamCreateWithFlags(&sv->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc((void**)&sv->mb, sizeof(SrvMailbox), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&sv->mb_dev, sv->mb, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;  // leaked on this rare path; the launch path still works
+  }
+  memset(sv->mb, 0, sizeof(SrvMailbox));  // exit_gen == gen == 0: "not running"
+  {
+    std::lock_guard<std::mutex> g(g_srv_mu);
+    if (g_servers.empty()) atexit(stop_all_at_exit);  // runs before HIP's own teardown
+    g_servers.push_back(sv);
+  }
+  per_dev[dev] = sv;
+  return sv;
+}
+
+int server_launch(Server* sv) {
+  SCT_HIP(hipStreamSynchronize(sv->stream));  // the previous server has returned
+  const uint32_t gen = sv->gen.load() + 1;
+  __atomic_store_n(&sv->mb->stop, 0u, __ATOMIC_RELEASE);
+  sv->gen.store(gen);
+  hipLaunchKernelGGL(scalar_server_kernel, dim3(1), dim3(64), 0, sv->stream, sv->mb_dev, host_load(&sv->mb->done), gen,
+                     sv->idle_ticks);
+  SCT_LAUNCH_CHECK();
+  g_srv_launches.fetch_add(1);
+  return SCT_OK;
+}
+
+struct SrvIn {
+  const void* p;
+  size_t bytes;
+};
+struct SrvOut {
+  void* p;
+  size_t bytes;
+};
+
+// Returns SCT_OK when served, 1 when the request does not fit the server (the caller takes
+// the launch path), or an error code.
+template <int NI, int NO>
+int srv_call(uint32_t op, int kind, int64_t n, int words, int L, int64_t stride, int maxlen, const SrvIn (&ins)[NI],
+             const SrvOut (&outs)[NO]) {
+  if (!server_enabled() || n > kSrvMaxN || stride > kSrvIn || L > kSrvOut || maxlen > kSrvOut || words > 255) return 1;
+  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  int32_t io[2] = {-1, -1}, oo[3] = {-1, -1, -1};
+  size_t tin = 0, tout = 0;
+  for (int k = 0; k < NI; ++k) {
+    io[k] = (int32_t)tin;
+    tin += al(ins[k].bytes);
+  }
+  for (int k = 0; k < NO; ++k) {
+    if (!outs[k].p) continue;
+    oo[k] = (int32_t)tout;
+    tout += al(outs[k].bytes);
+  }
+  if (tin > (size_t)kSrvIn || tout > (size_t)kSrvOut) return 1;
+  Server* sv = server();
+  if (!sv) return 1;
+  SrvMailbox* mb = sv->mb;
+  uint8_t* pay = reinterpret_cast<uint8_t*>(&mb->req[kSrvInline / 4]);
+  for (int k = 0; k < NI; ++k)
+    if (ins[k].bytes) memcpy(pay + io[k], ins[k].p, ins[k].bytes);
+  auto o16 = [](int32_t v) { return v < 0 ? 0xFFFFu : (uint32_t)v; };
+  mb->req[1] = op | (uint32_t)kind << 8 | (uint32_t)words << 16;
+  mb->req[2] = (uint32_t)n | (uint32_t)L << 16;
+  mb->req[3] = (uint32_t)stride | (uint32_t)maxlen << 16;
+  mb->req[4] = (uint32_t)tin | (uint32_t)tout << 16;
+  mb->req[5] = o16(io[0]) | o16(io[1]) << 16;
+  mb->req[6] = o16(oo[0]) | o16(oo[1]) << 16;
+  mb->req[7] = o16(oo[2]);
+  const uint32_t seq = ++sv->seq;
+  __atomic_store_n(&mb->req[0], seq, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 1;; ++spin) {
+    if (host_load(&mb->done) == seq) break;
+    if (!server_running(sv)) {
+      if (host_load(&mb->done) == seq) break;  // served just before it left
+      SCT_TRY(server_launch(sv));
+      continue;
+    }
+    if ((spin & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+      return sct::fail(SCT_E_HIP, "scalar server: no answer in 10 s");
+  }
+  if (host_load(&mb->status) != 0) return sct::fail(SCT_E_HIP, "scalar server: bad request");
+  for (int k = 0; k < NO; ++k)
+    if (outs[k].p && outs[k].bytes) memcpy(outs[k].p, reinterpret_cast<const uint8_t*>(mb->out) + oo[k], outs[k].bytes);
+  return SCT_OK;
+}
+}  // namespace
+
+namespace sct {
+void scalar_quiesce() {
+  std::lock_guard<std::mutex> g(g_srv_mu);
+  for (Server* sv : g_servers) server_stop(sv, 1000000);
+}
+}  // namespace sct
+
+extern "C" int sct_scalar_server_stop(void) {
+  sct::scalar_quiesce();
+  return SCT_OK;
+}
+
+extern "C" int sct_scalar_server_status(int64_t* launches, int* running) {
+  if (launches) *launches = g_srv_launches.load();
+  if (running) {
+    std::lock_guard<std::mutex> g(g_srv_mu);
+    int c = 0;
+    for (Server* sv : g_servers) c += server_running(sv) ? 1 : 0;
+    *running = c;
+  }
+  return SCT_OK;
+}
+
 // ---------------------------------------------------------------- host-pointer wrappers
 // Every *_host call runs on the thread's host stage (sct::HostStage): small calls (the
 // drop-in's scalar methods are batches of one) read their inputs from and write their
@@ -506,11 +841,6 @@ extern "C" int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint6
 // no allocation), larger ones pack inputs / outputs into one H2D and one D2H copy through
 // the stage's device buffer, and only calls above kStageBytes allocate per call.
 namespace {
-#define SCT_TRY(x)              \
-  do {                          \
-    int rc_ = (x);              \
-    if (rc_ != SCT_OK) return rc_; \
-  } while (0)
 
 struct In {
   const void* p;
@@ -606,6 +936,11 @@ extern "C" int sct_encode_host(int kind, const uint8_t* seqs, int64_t n, int64_t
   if (n == 0) return SCT_OK;
   const int words = words_for(kind, L);
   const size_t in_bytes = (size_t)((n - 1) * stride + L);
+  if (codes && (L == 0 || seqs) && (gc == nullptr || L <= 255)) {
+    const int rc = srv_call<1, 3>(OP_ENCODE, kind, n, words, L, stride, 0, {{seqs, in_bytes}},
+                                  {{codes, (size_t)n * words * 8}, {gc, (size_t)n}, {flags, (size_t)n}});
+    if (rc != 1) return rc;
+  }
   return host_call<1, 3>({{seqs, in_bytes}}, {{codes, (size_t)n * words * 8}, {gc, (size_t)n}, {flags, (size_t)n}},
                          true, [&](void** p, hipStream_t s) {
                            return sct_encode(kind, (const uint8_t*)p[0], n, stride, L, (uint64_t*)p[1], (uint8_t*)p[2],
@@ -690,6 +1025,10 @@ extern "C" int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, 
 extern "C" int sct_decode2_host(const uint64_t* codes, int64_t n, int words, int L, uint8_t* out) {
   SCT_CHECK(n >= 0 && words >= 1 && L >= 0, "bad n/words/L");
   if (n == 0 || L == 0) return SCT_OK;
+  if (codes && out) {
+    const int rc = srv_call<1, 1>(OP_DECODE2, 2, n, words, L, 0, 0, {{codes, (size_t)n * words * 8}}, {{out, (size_t)n * L}});
+    if (rc != 1) return rc;
+  }
   return host_call<1, 1>({{codes, (size_t)n * words * 8}}, {{out, (size_t)n * L}}, true,
                          [&](void** p, hipStream_t s) {
                            return sct_decode2((const uint64_t*)p[0], n, words, L, (uint8_t*)p[1], s);
@@ -700,6 +1039,11 @@ extern "C" int sct_decode3_host(const uint64_t* codes, int64_t n, int words, int
                                 uint8_t* out, int32_t* lengths, int32_t* bad) {
   SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
   if (n == 0) return SCT_OK;
+  if (codes && out && lengths && bad && maxlen >= (64 * words + 2) / 3) {
+    const int rc = srv_call<1, 3>(OP_DECODE3, 3, n, words, 0, 0, maxlen, {{codes, (size_t)n * words * 8}},
+                                  {{out, (size_t)n * maxlen}, {lengths, (size_t)n * 4}, {bad, (size_t)n * 4}});
+    if (rc != 1) return rc;
+  }
   return host_call<1, 3>({{codes, (size_t)n * words * 8}},
                          {{out, (size_t)n * maxlen}, {lengths, (size_t)n * 4}, {bad, (size_t)n * 4}}, true,
                          [&](void** p, hipStream_t s) {
@@ -712,6 +1056,10 @@ extern "C" int sct_gc_content_host(int kind, const uint64_t* codes, int64_t n, i
                                    int32_t* out) {
   SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
   if (n == 0) return SCT_OK;
+  if ((kind == 2 || kind == 3) && L >= 0 && codes && out) {
+    const int rc = srv_call<1, 1>(OP_GC, kind, n, words, L, 0, 0, {{codes, (size_t)n * words * 8}}, {{out, (size_t)n * 4}});
+    if (rc != 1) return rc;
+  }
   return host_call<1, 1>({{codes, (size_t)n * words * 8}}, {{out, (size_t)n * 4}}, true,
                          [&](void** p, hipStream_t s) {
                            return sct_gc_content(kind, (const uint64_t*)p[0], n, words, L, (int32_t*)p[1], s);
@@ -722,9 +1070,15 @@ extern "C" int sct_hamming_pairs_host(int kind, const uint64_t* a, const uint64_
                                       int words, int32_t* out) {
   SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
   if (n == 0) return SCT_OK;
+  if ((kind == 2 || kind == 3) && a && b && out) {
+    const int rc = srv_call<2, 1>(OP_HAMMING, kind, n, words, 0, 0, 0,
+                                  {{a, (size_t)n * words * 8}, {b, (size_t)n * words * 8}}, {{out, (size_t)n * 4}});
+    if (rc != 1) return rc;
+  }
   return host_call<2, 1>({{a, (size_t)n * words * 8}, {b, (size_t)n * words * 8}}, {{out, (size_t)n * 4}}, true,
                          [&](void** p, hipStream_t s) {
                            return sct_hamming_pairs(kind, (const uint64_t*)p[0], (const uint64_t*)p[1], n, words,
                                                     (int32_t*)p[2], s);
                          });
 }
+

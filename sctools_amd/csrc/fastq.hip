@@ -432,6 +432,7 @@ __global__ __launch_bounds__(WG) void extract2_kernel(const uint8_t* __restrict_
 
 // grid of the persistent tile kernels: every resident workgroup slot once (at most ntiles)
 unsigned resident_grid(const void* kernel, int64_t ntiles) {
+  sct::scalar_quiesce();
   int dev = 0, cus = 256, per_cu = 0;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, WG, 0) != hipSuccess || per_cu <= 0) per_cu = 4;

@@ -59,6 +59,11 @@ constexpr size_t kZeroCopyBytes = 64 << 10;
 // it the caller's arrays are copied through per-call device allocations.
 constexpr size_t kStageBytes = 256ull << 20;
 
+// Stop the resident scalar servers (encode.hip) before a launch whose grid is sized to the
+// resident workgroups, so none of its workgroups waits behind a server wave's registers.
+// Cheap when no server runs.
+void scalar_quiesce();
+
 // Moment-assisted all-pairs scheme (SCT_ALLPAIRS_MOMENTS, 16-base TwoBit codes):
 // the count kernel accumulates only these 13 subset products of the distance bits
 // d0..d3 (d mod 16), and the agreement moments M_k = sum over pairs of C(16 - d, k),
