@@ -1,5 +1,7 @@
 # Nearest-whitelist A/B: nearest parity tests under the variant, then config 4 (100M
 # queries) with the shipped kernel (SCT_NEAREST_SPEC=0) and the variant (=1), alternately.
+# (The all-tables-at-once variant behind SCT_NEAREST_SPEC was removed after this A/B,
+# profiles/ab_nearest_spec_r02.jsonl; re-add a switch before reusing the script.)
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
