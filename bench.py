@@ -330,15 +330,16 @@ def run_rank(args, rank, world, local):
               "spectral": _lib.SCHEME_SPECTRAL}[args.scheme]
     job = sharding.ShardedAllPairs(codes, 2 * L, scheme)
     spectral = job.scheme == _lib.SCHEME_SPECTRAL
-    for _ in range(args.warmup):
-        hist = job.step()
+    # steps run software-pipelined two deep (ShardedAllPairs.run): every step's zero, build,
+    # count, all-reduce, read-back and inversion happen inside the timed region; step k+1's
+    # kernels are queued before the host waits for step k's histogram
+    job.run(args.warmup)
     job.reset_timings()  # the timings cover the timed steps only
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        hist = job.step(timing=True)
+    hists = job.run(args.steps, timing=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -361,6 +362,8 @@ def run_rank(args, rank, world, local):
     for r in per_rank:
         r["rank"], r["items"] = int(r["rank"]), int(r["items"])
 
+    hist = hists[-1]
+    assert len(hists) == args.steps and all(np.array_equal(h, hist) for h in hists), "steps disagree"
     P = job.plan.pairs
     assert int(hist.sum()) == P, "histogram does not cover every pair"
     summ = _lib.summary_from_hist(hist)

@@ -126,6 +126,85 @@ class ShardedAllPairs:
                 self._t["moments_ms"].append(ev["m0"].elapsed_time(ev["m1"]))
         return hist
 
+    def run(self, steps, timing=False):
+        """``steps`` whole steps, software-pipelined two deep; returns their histograms.
+
+        Every step does all of ``step()``'s work -- zero, build, count, all-reduce, D2H,
+        exact inversion -- into one of two count buffers: step k + 1's build and count are
+        queued on the main stream before the host waits for step k, whose all-reduce and
+        read-back run on a tail stream, so they and the host's inversion overlap the next
+        step's kernels instead of leaving the GPU idle between steps."""
+        import torch
+        import torch.distributed as dist
+        if steps <= 0:
+            return []
+        if not hasattr(self, "_pipe"):
+            dev = self.device
+            self._pipe = {
+                "counts": [self.counts, torch.zeros_like(self.counts)],
+                "host": [torch.zeros(self.plan.ncounts, dtype=torch.int64).pin_memory() for _ in range(2)],
+                "tail": torch.cuda.Stream(dev),
+                "ev": [{k: torch.cuda.Event(enable_timing=True) for k in ("b0", "b1", "c1", "a1", "m0", "m1")}
+                       for _ in range(2)],
+                "done": [torch.cuda.Event() for _ in range(2)],
+                "zero": [torch.cuda.Event() for _ in range(2)],
+                "mom": [torch.cuda.Event() for _ in range(2)],
+            }
+        pp = self._pipe
+        s, side, tail, sptr = self.stream, self.side, pp["tail"], self.stream.cuda_stream
+        moments = self.plan.scheme == _lib.SCHEME_MOMENTS
+
+        def issue(b):
+            counts, ev = pp["counts"][b], pp["ev"][b]
+            s.wait_event(pp["done"][b])  # this buffer's read-back two steps ago has finished
+            counts.zero_()
+            if moments:
+                pp["zero"][b].record(s)
+                side.wait_event(pp["zero"][b])
+                if timing:
+                    ev["m0"].record(side)
+                self.plan.moments(counts.data_ptr(), self.rank, self.world, side.cuda_stream)
+                if timing:
+                    ev["m1"].record(side)
+                pp["mom"][b].record(side)
+            if timing:
+                ev["b0"].record(s)
+            self.plan.build(sptr, self.begin, self.end)
+            if moments:
+                s.wait_event(pp["mom"][b])
+            if timing:
+                ev["b1"].record(s)
+            self.plan.count(counts.data_ptr(), self.begin, self.end, 0, sptr)
+            ev["c1"].record(s)
+            tail.wait_event(ev["c1"])
+            with torch.cuda.stream(tail):
+                if self.world > 1:
+                    dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=self.group)
+                if timing:
+                    ev["a1"].record(tail)
+                pp["host"][b].copy_(counts, non_blocking=True)
+                pp["done"][b].record(tail)
+
+        def finish(b):
+            pp["done"][b].synchronize()
+            host = pp["host"][b].numpy().astype(np.int64).view(np.uint64)
+            if timing:
+                ev = pp["ev"][b]
+                self._t["build_ms"].append(ev["b0"].elapsed_time(ev["b1"]))
+                self._t["count_ms"].append(ev["b1"].elapsed_time(ev["c1"]))
+                self._t["allreduce_us"].append(1e3 * ev["c1"].elapsed_time(ev["a1"]))
+                if moments:
+                    self._t["moments_ms"].append(ev["m0"].elapsed_time(ev["m1"]))
+            return _lib.counts_to_hist(host, self.plan.scheme, self.plan.nbins)
+
+        hists = []
+        for k in range(steps):
+            issue(k & 1)
+            if k:
+                hists.append(finish((k - 1) & 1))
+        hists.append(finish((steps - 1) & 1))
+        return hists
+
     def reset_timings(self):
         self._t = {k: [] for k in self._t}
 

@@ -36,6 +36,10 @@ def _worker(rank, world, port, n, seed, scheme, out_path):
             assert job.scheme == scheme
             assert (job.begin, job.end) == sharding.item_range(job.plan.items, rank, world)
             hist = job.step(timing=True)
+            # the pipelined steps bench.py times: three steps, each the whole histogram
+            piped = job.run(3, timing=True)
+            assert len(piped) == 3 and all(h.tolist() == hist.tolist() for h in piped)
+            assert job.timings()["count_ms"] is not None
             mine = job.my_pairs()
         np.savez(out_path % rank, hist=hist.astype(np.int64), mine=mine)
     finally:

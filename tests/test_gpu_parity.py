@@ -811,3 +811,18 @@ def test_nearest_max_d_near_limit(kind, max_d):
     idx, dist = barcode.nearest_whitelist(q, wl, max_distance=max_d, encoding=kind)
     ridx, rdist = O.c_nearest(kind, wl, q, max_d)
     assert np.array_equal(idx, ridx) and np.array_equal(dist, rdist)
+
+
+@pytest.mark.parametrize("scheme", [0, 1, 2])
+def test_sharded_run_pipelined_steps_match_oracle(scheme):
+    """ShardedAllPairs.run (what bench.py times): steps pipelined two deep over two count
+    buffers; every step's histogram equals step()'s and the oracle's (barcode.py:39-46)."""
+    n = 6_000 if scheme == 0 else 20_000
+    codes = synthetic.whitelist_codes(n, 16, 77 + scheme)
+    ref = O.c_hist16(codes)[0][:17].tolist()
+    with sharding.ShardedAllPairs(codes, 32, scheme) as job:
+        assert job.step().tolist() == ref
+        for steps in (1, 2, 5):
+            hists = job.run(steps, timing=True)
+            assert len(hists) == steps and all(h.tolist() == ref for h in hists)
+        assert job.step().tolist() == ref
