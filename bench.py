@@ -1,14 +1,16 @@
 """Benchmark: Hamming pair-comparisons/s, 737,280-barcode all-pairs histogram (BASELINE.json).
 
 One step = the whole hot path of Barcodes.summarize_hamming_distances on device-resident
-codes, as one rank runs it (sctools_amd.sharding.ShardedAllPairs.step): build the plan's
+codes, as one rank runs it (sctools_amd.sharding.ShardedAllPairs): build the plan's
 tables, count this rank's share of the work items, all-reduce the counts over RCCL
 (N > 1), copy them to the host, invert them to the exact histogram, then the numpy-exact
 summary.  At 737K 16-bp codes the library's AUTO scheme is SPECTRAL (the Walsh-Hadamard
 route): no pair is enumerated, yet the histogram of all P = n(n-1)/2
 pair distances is exact, so `value` is PAIR-EQUIVALENT throughput (P / step time, cost
-independent of n).  The pair-enumerating MOMENTS kernel is timed beside it (N = 1) as
-`pair_kernel`.
+independent of n).  The K timed steps run pipelined two deep (ShardedAllPairs.run): step
+k+1's kernels are queued before the host waits for step k's all-reduce and histogram, and
+every step's histogram is produced and checked.  The pair-enumerating MOMENTS kernel is
+timed beside it (N = 1) as `pair_kernel`.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
 
