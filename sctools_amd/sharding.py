@@ -58,6 +58,9 @@ class ShardedAllPairs:
         import torch
         self.group = group
         self.world, self.rank = _group_info(group)
+        # inside an initialised process group the counts are always all-reduced (a one-rank
+        # group too: the same collective path as N ranks, a no-op on the values)
+        self._reduce = _in_group()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         if isinstance(codes, np.ndarray):
             host = np.ascontiguousarray(codes, dtype=np.uint64).reshape(-1)
@@ -112,7 +115,7 @@ class ShardedAllPairs:
         self.plan.count(self.counts.data_ptr(), self.begin, self.end, 0, sptr)
         if timing:
             ev["c1"].record(s)
-        if self.world > 1:
+        if self._reduce:
             dist.all_reduce(self.counts, op=dist.ReduceOp.SUM, group=self.group)
         if timing:
             ev["a1"].record(s)
@@ -178,7 +181,7 @@ class ShardedAllPairs:
             ev["c1"].record(s)
             tail.wait_event(ev["c1"])
             with torch.cuda.stream(tail):
-                if self.world > 1:
+                if self._reduce:
                     dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=self.group)
                 if timing:
                     ev["a1"].record(tail)
@@ -249,6 +252,11 @@ def allpairs_wide_sharded(limbs, group=None, device=None):
     if world > 1:
         dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
     return hist.cpu().numpy().view(np.uint64)
+
+
+def _in_group():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
 
 
 def _group_info(group):

@@ -132,6 +132,10 @@ def _worker_rccl(rank, world, port, out_path):
         codes = synthetic.whitelist_codes(5_000, 16, 3)
         with sharding.ShardedAllPairs(codes, 32, _lib.SCHEME_SPECTRAL) as job:
             hist = job.step(timing=True)
+            # bench.py's pipelined steps: the all-reduce from the tail stream over RCCL
+            piped = job.run(3, timing=True)
+            assert all(h.tolist() == hist.tolist() for h in piped)
+            assert job.timings()["allreduce_us"] is not None
         np.savez(out_path % rank, t=t.cpu().numpy(), rows=torch.stack(rows).cpu().numpy(), hist=hist.astype(np.int64),
                  backend=np.array([dist.get_backend()]))
     finally:
