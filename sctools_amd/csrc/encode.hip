@@ -558,12 +558,26 @@ struct SrvMailbox {
   uint32_t more[(kSrvIn - kSrvInline) / 4];
   // control (host)
   alignas(64) uint32_t stop;
-  // response (device): the last served seq and its status; the launch id on exit
-  alignas(64) uint32_t done;
-  int32_t status;
-  uint32_t exit_gen;
+  // response line (device), written by one 16-lane store: resp[0] = the served seq,
+  // resp[1] = status, resp[2..14] = the outputs when they fit 52 bytes, resp[15] =
+  // line_check(resp[0..14]).  No fence orders the line's dwords, so the host takes the line
+  // only when the check matches (a torn write is waited out, never read).  Larger outputs go
+  // to `out` first, behind a release fence.
+  alignas(64) uint32_t resp[16];
+  // the launch id on exit (device)
+  alignas(64) uint32_t exit_gen;
   alignas(64) uint32_t out[kSrvOut / 4];
 };
+constexpr int kSrvInlineOut = 52;
+
+__host__ __device__ inline uint32_t line_check(const uint32_t* w) {
+  uint32_t h = 0x9E3779B9u;
+  for (int k = 0; k < 15; ++k) {
+    h = (h ^ w[k]) * 0x01000193u;
+    h ^= h >> 15;
+  }
+  return h;
+}
 static_assert(offsetof(SrvMailbox, more) == 64, "payload must continue the request line");
 
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
@@ -584,8 +598,11 @@ __global__ __launch_bounds__(64) void scalar_server_kernel(SrvMailbox* mb, uint3
   }
   __syncthreads();
   uint64_t t_last = wall_clock64();
-  for (;;) {
-    const uint32_t line = lane < 16 ? sys_load(&mb->req[lane]) : 0u;
+  // two polls in flight: the next line's load is issued before this one is examined, so a
+  // request is seen about half a PCIe round trip sooner than with one poll at a time
+  uint32_t line = lane < 16 ? sys_load(&mb->req[lane]) : 0u;
+  for (uint32_t it = 1;; ++it) {
+    const uint32_t ahead = lane < 16 ? sys_load(&mb->req[lane]) : 0u;
     const uint32_t seq = __builtin_amdgcn_readlane(line, 0);
     if (seq != served) {
       const uint32_t h1 = __builtin_amdgcn_readlane(line, 1), h2 = __builtin_amdgcn_readlane(line, 2),
@@ -645,20 +662,28 @@ __global__ __launch_bounds__(64) void scalar_server_kernel(SrvMailbox* mb, uint3
         }
       }
       __syncthreads();
-      for (int k = lane; k < out_words; k += 64)
-        __hip_atomic_store(&mb->out[k], out_l[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      if (lane == 0) {
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(&mb->status), (uint32_t)(op >= OP_ENCODE && op <= OP_HAMMING ? 0 : 1),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&mb->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      const bool inline_out = out_words * 4 <= kSrvInlineOut;
+      if (!inline_out) {
+        for (int k = lane; k < out_words; k += 64)
+          __hip_atomic_store(&mb->out[k], out_l[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       }
+      const uint32_t status = op >= OP_ENCODE && op <= OP_HAMMING ? 0u : 1u;
+      uint32_t v = lane == 0 ? seq : lane == 1 ? status : (lane < 15 && inline_out && lane - 2 < out_words) ? out_l[lane - 2] : 0u;
+      uint32_t w[15];
+#pragma unroll
+      for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_readlane(v, k);
+      if (lane == 15) v = line_check(w);
+      if (lane < 16) __hip_atomic_store(&mb->resp[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       served = seq;
       t_last = wall_clock64();
+      line = ahead;
       continue;
     }
-    if (sys_load(&mb->stop) != 0u || wall_clock64() - t_last > idle_ticks) break;
-    __builtin_amdgcn_s_sleep(2);
+    // the stop word costs a round trip of its own: looked at every 256th poll (~0.2 ms)
+    if ((it & 255) == 0 && sys_load(&mb->stop) != 0u) break;
+    if (wall_clock64() - t_last > idle_ticks) break;
+    line = ahead;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if (lane == 0) __hip_atomic_store(&mb->exit_gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -742,7 +767,7 @@ int server_launch(Server* sv) {
   const uint32_t gen = sv->gen.load() + 1;
   __atomic_store_n(&sv->mb->stop, 0u, __ATOMIC_RELEASE);
   sv->gen.store(gen);
-  hipLaunchKernelGGL(scalar_server_kernel, dim3(1), dim3(64), 0, sv->stream, sv->mb_dev, host_load(&sv->mb->done), gen,
+  hipLaunchKernelGGL(scalar_server_kernel, dim3(1), dim3(64), 0, sv->stream, sv->mb_dev, host_load(&sv->mb->resp[0]), gen,
                      sv->idle_ticks);
   SCT_LAUNCH_CHECK();
   g_srv_launches.fetch_add(1);
@@ -794,19 +819,27 @@ int srv_call(uint32_t op, int kind, int64_t n, int words, int L, int64_t stride,
   const uint32_t seq = ++sv->seq;
   __atomic_store_n(&mb->req[0], seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
+  uint32_t line[16];
+  auto answered = [&]() {  // the whole response line of this request, check included
+    if (host_load(&mb->resp[0]) != seq) return false;
+    for (int k = 0; k < 16; ++k) line[k] = host_load(&mb->resp[k]);
+    return line[0] == seq && line_check(line) == line[15];
+  };
   for (uint32_t spin = 1;; ++spin) {
-    if (host_load(&mb->done) == seq) break;
+    if (answered()) break;
     if (!server_running(sv)) {
-      if (host_load(&mb->done) == seq) break;  // served just before it left
+      if (answered()) break;  // served just before it left
       SCT_TRY(server_launch(sv));
       continue;
     }
     if ((spin & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
       return sct::fail(SCT_E_HIP, "scalar server: no answer in 10 s");
   }
-  if (host_load(&mb->status) != 0) return sct::fail(SCT_E_HIP, "scalar server: bad request");
+  if (line[1] != 0) return sct::fail(SCT_E_HIP, "scalar server: bad request");
+  const uint8_t* res = tout <= (size_t)kSrvInlineOut ? reinterpret_cast<const uint8_t*>(line + 2)
+                                                     : reinterpret_cast<const uint8_t*>(mb->out);
   for (int k = 0; k < NO; ++k)
-    if (outs[k].p && outs[k].bytes) memcpy(outs[k].p, reinterpret_cast<const uint8_t*>(mb->out) + oo[k], outs[k].bytes);
+    if (outs[k].p && outs[k].bytes) memcpy(outs[k].p, res + oo[k], outs[k].bytes);
   return SCT_OK;
 }
 }  // namespace
