@@ -535,10 +535,11 @@ extern "C" int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint6
 // hundred instructions.  Instead, the first such call of a host thread on a device launches
 // one 64-lane server kernel that polls a page-locked, host-coherent mailbox over PCIe:
 // the host writes the request (opcode, sizes, the packed inputs) and then its sequence
-// number; the wave sees the new number, pulls the payload into LDS with one round of
-// dword loads, runs the same per-record device functions as the batch kernels (one record
-// per lane, n <= 64), writes the outputs back with system-scope stores and publishes the
-// sequence number as done.  The wave exits after idle_ticks of its wall clock without a
+// number, all in one 64-B line the wave polls (larger payloads continue past it); the wave
+// runs the same per-record device functions as the batch kernels (one record per lane,
+// n <= 64) and answers with one checksummed 64-B response line (SrvMailbox::resp) that
+// carries the sequence number, the status and small outputs.  The wave exits after
+// idle_ticks of its wall clock without a
 // request, on the mailbox's stop word, or never while a request is pending; it always
 // writes its launch id to exit_gen last, so the host tells "exited" from "slow" without a
 // HIP call, and relaunches (the pending request is served first) when it finds its
