@@ -75,6 +75,7 @@ class ShardedAllPairs:
             code_bits = max(1, int(np.bitwise_or.reduce(host)).bit_length()) if n else 1
         self.n = n
         self.plan = _lib.AllPairsPlan(self.d_codes.data_ptr(), n, code_bits, scheme=scheme)
+        self._plan_args = (n, code_bits, scheme)
         self.begin, self.end = item_range(self.plan.items, self.rank, self.world)
         self.counts = torch.zeros(self.plan.ncounts, dtype=torch.int64, device=self.device)
         self.stream = torch.cuda.current_stream(self.device)
@@ -133,21 +134,26 @@ class ShardedAllPairs:
         """``steps`` whole steps, software-pipelined two deep; returns their histograms.
 
         Every step does all of ``step()``'s work -- zero, build, count, all-reduce, D2H,
-        exact inversion -- into one of two count buffers: step k + 1's build and count are
-        queued on the main stream before the host waits for step k, whose all-reduce and
-        read-back run on a tail stream, so they and the host's inversion overlap the next
-        step's kernels instead of leaving the GPU idle between steps."""
+        exact inversion -- with one of two plans and count buffers: step k + 1's build runs
+        on a build stream as soon as its plan's count of step k - 1 is done (beside step k's
+        count), its count is queued on the main stream before the host waits for step k, and
+        step k's all-reduce and read-back run on a tail stream, so they and the host's
+        inversion overlap the next step's kernels instead of leaving the GPU idle."""
         import torch
         import torch.distributed as dist
         if steps <= 0:
             return []
         if not hasattr(self, "_pipe"):
             dev = self.device
+            n, code_bits, scheme = self._plan_args
             self._pipe = {
+                "plans": [self.plan, _lib.AllPairsPlan(self.d_codes.data_ptr(), n, code_bits, scheme=scheme)],
+                "build": torch.cuda.Stream(dev),
+                "built": [torch.cuda.Event() for _ in range(2)],
                 "counts": [self.counts, torch.zeros_like(self.counts)],
                 "host": [torch.zeros(self.plan.ncounts, dtype=torch.int64).pin_memory() for _ in range(2)],
                 "tail": torch.cuda.Stream(dev),
-                "ev": [{k: torch.cuda.Event(enable_timing=True) for k in ("b0", "b1", "c1", "a1", "m0", "m1")}
+                "ev": [{k: torch.cuda.Event(enable_timing=True) for k in ("b0", "b1", "c0", "c1", "a1", "m0", "m1")}
                        for _ in range(2)],
                 "done": [torch.cuda.Event() for _ in range(2)],
                 "zero": [torch.cuda.Event() for _ in range(2)],
@@ -157,8 +163,17 @@ class ShardedAllPairs:
         s, side, tail, sptr = self.stream, self.side, pp["tail"], self.stream.cuda_stream
         moments = self.plan.scheme == _lib.SCHEME_MOMENTS
 
+        bs = pp["build"]
+
         def issue(b):
-            counts, ev = pp["counts"][b], pp["ev"][b]
+            counts, ev, plan = pp["counts"][b], pp["ev"][b], pp["plans"][b]
+            bs.wait_event(ev["c1"])  # this plan's count two steps ago no longer reads its tables
+            if timing:
+                ev["b0"].record(bs)
+            plan.build(bs.cuda_stream, self.begin, self.end)
+            if timing:
+                ev["b1"].record(bs)
+            pp["built"][b].record(bs)
             s.wait_event(pp["done"][b])  # this buffer's read-back two steps ago has finished
             counts.zero_()
             if moments:
@@ -166,18 +181,15 @@ class ShardedAllPairs:
                 side.wait_event(pp["zero"][b])
                 if timing:
                     ev["m0"].record(side)
-                self.plan.moments(counts.data_ptr(), self.rank, self.world, side.cuda_stream)
+                plan.moments(counts.data_ptr(), self.rank, self.world, side.cuda_stream)
                 if timing:
                     ev["m1"].record(side)
                 pp["mom"][b].record(side)
-            if timing:
-                ev["b0"].record(s)
-            self.plan.build(sptr, self.begin, self.end)
-            if moments:
                 s.wait_event(pp["mom"][b])
+            s.wait_event(pp["built"][b])
             if timing:
-                ev["b1"].record(s)
-            self.plan.count(counts.data_ptr(), self.begin, self.end, 0, sptr)
+                ev["c0"].record(s)
+            plan.count(counts.data_ptr(), self.begin, self.end, 0, sptr)
             ev["c1"].record(s)
             tail.wait_event(ev["c1"])
             with torch.cuda.stream(tail):
@@ -194,7 +206,7 @@ class ShardedAllPairs:
             if timing:
                 ev = pp["ev"][b]
                 self._t["build_ms"].append(ev["b0"].elapsed_time(ev["b1"]))
-                self._t["count_ms"].append(ev["b1"].elapsed_time(ev["c1"]))
+                self._t["count_ms"].append(ev["c0"].elapsed_time(ev["c1"]))
                 self._t["allreduce_us"].append(1e3 * ev["c1"].elapsed_time(ev["a1"]))
                 if moments:
                     self._t["moments_ms"].append(ev["m0"].elapsed_time(ev["m1"]))
@@ -215,6 +227,8 @@ class ShardedAllPairs:
         return {k: (float(np.mean(v)) if v else None) for k, v in self._t.items()}
 
     def close(self):
+        if hasattr(self, "_pipe"):
+            self._pipe["plans"][1].close()
         self.plan.close()
 
     def __enter__(self):
