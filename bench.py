@@ -7,9 +7,10 @@ tables, count this rank's share of the work items, all-reduce the counts over RC
 summary.  At 737K 16-bp codes the library's AUTO scheme is SPECTRAL (the Walsh-Hadamard
 route): no pair is enumerated, yet the histogram of all P = n(n-1)/2
 pair distances is exact, so `value` is PAIR-EQUIVALENT throughput (P / step time, cost
-independent of n).  The K timed steps run pipelined two deep (ShardedAllPairs.run): step
-k+1's kernels are queued before the host waits for step k's all-reduce and histogram, and
-every step's histogram is produced and checked.  The pair-enumerating MOMENTS kernel is
+independent of n).  The K timed steps run pipelined two deep (ShardedAllPairs.run, two
+plans): step k+1's build runs on its own stream beside step k's count, its count is queued
+before the host waits for step k's all-reduce and histogram, and every step's histogram is
+produced and checked (`ranks[].build_ms` is the build's overlapped span on its stream).  The pair-enumerating MOMENTS kernel is
 timed beside it (N = 1) as `pair_kernel`.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
