@@ -10,20 +10,26 @@ pair distances is exact, so `value` is PAIR-EQUIVALENT throughput (P / step time
 independent of n).  The K timed steps run pipelined two deep (ShardedAllPairs.run, two
 plans): step k+1's build runs on its own stream beside step k's count, its count is queued
 before the host waits for step k's all-reduce and histogram, and every step's histogram is
-produced and checked (`ranks[].build_ms` is the build's overlapped span on its stream).  The pair-enumerating MOMENTS kernel is
-timed beside it (N = 1) as `pair_kernel`.
+produced and checked.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2] [--no-paths] [--no-cpu]
 
 --gpus N > 1 without a launcher: bench.py itself starts N rank processes (one per GPU,
 backend nccl = RCCL) before anything touches a GPU, and exits non-zero if fewer than N
 GPUs are visible.  Under torchrun (WORLD_SIZE set) every process is one rank and
-WORLD_SIZE must equal --gpus.  Rank 0 prints one JSON line: `value` = all pairs of the
-whole job / max-over-ranks wall time of the K timed steps; `ranks` = per-rank count /
-all-reduce / step times.  `roofline` prices the dominant kernel with HIP events on the
-stream it runs on.  `cpu_baseline` (N = 1, rank 0) runs the C oracle restatement (test
-infrastructure, never the product) on this host's cores and checks its histogram
-against the GPU's.
+WORLD_SIZE must equal --gpus.  Rank 0 prints one JSON line:
+  value     all pairs of the whole job / max-over-ranks wall time of the K timed steps
+  ranks     per-rank count / all-reduce / build / own step times
+  roofline  the dominant kernel priced by HIP events recorded around every one of its
+            launches in the K timed steps, on the stream the launches run on
+            (sct_allpairs_timing); HBM against 8 TB/s and against a device copy measured
+            in the same run; the issue-rate picture (VALU / matrix-pipe busy) from the
+            committed PMC summary; the committed rocprof average beside the live one
+  paths     (N = 1) config 4 (100M-query nearest whitelist), config 5's 3.7M all-pairs and
+            its 1e9-read encode + GC, each timed here with its own roofline and a sampled
+            check against the oracle (none of them is inside the headline's timed region)
+  cpu_baseline  (N = 1) the C oracle restatement (test infrastructure, never the product)
+            on this host's cores, the histogram checked against the GPU's
 """
 
 import argparse
@@ -44,11 +50,10 @@ sys.path.insert(0, ROOT)
 # (measured 121 lane-ops/clk/CU for v_xor_b32, profiles/valu_peak_r01.json).
 VALU_PEAK_OPS = 256 * 128 * 2.4e9
 HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E (MI355X_MICROARCH.md)
+SIMDS = 256 * 4
 ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-bit code word
-# SPECTRAL tile kernel: per slice of 2^14 transform values, 14 butterfly levels (one add
-# or sub per value per level) and one square-accumulate per value
-SPECTRAL_OPS_PER_SLICE = (1 << 14) * (14 + 1)
 METRIC = "Hamming pair-comparisons/sec, 737K 10x whitelist all-pairs, 1-8 GPUs"
+PROFILE_ROUND = "r03"  # the committed rocprof / PMC summaries the line cites (profiles/)
 
 
 def parse(argv=None):
@@ -56,10 +61,12 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 5])
     ap.add_argument("--cpu-seconds", type=float, default=30.0,
                     help="CPU baseline budget: the whole job if it fits, else a row sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-paths", action="store_true", help="skip configs 4 / 5 (N = 1 paths)")
+    ap.add_argument("--path-steps", type=int, default=5)
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--scheme", default="auto", choices=["auto", "subsets", "moments", "spectral"])
     ap.add_argument("--pair-steps", type=int, default=5,
@@ -142,17 +149,22 @@ def _host_info():
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
+def host_threads():
+    """Every host core this job may use: OMP_NUM_THREADS when the box sets the CPU share,
+    else the affinity mask, capped by the cgroup quota (nproc counts the whole machine)."""
+    info = _host_info()
+    threads = int(info["omp_num_threads_env"] or 0) or info["affinity_cpus"] or 1
+    if info["cgroup_cpu_quota"]:
+        threads = max(1, min(threads, int(round(info["cgroup_cpu_quota"]))))
+    return threads, info
+
+
 def cpu_baseline(codes, gpu_hist, budget_s):
     """The C oracle (oracle/sct_oracle.c: encodings.py:113-121's popcount form over 32-bit
     AVX-512 lanes, OpenMP over rows) on every core this process may use: the whole job if it
     fits the budget (its histogram must equal the GPU's bin for bin), else rows [0, R)."""
     from oracle import oracle as O
-    info = _host_info()
-    # all host cores this job may use: OMP_NUM_THREADS when the box sets the CPU share,
-    # else the affinity mask (nproc counts the whole machine on a shared box)
-    threads = int(info["omp_num_threads_env"] or 0) or info["affinity_cpus"] or 1
-    if info["cgroup_cpu_quota"]:
-        threads = max(1, min(threads, int(round(info["cgroup_cpu_quota"]))))
+    threads, info = host_threads()
     n = codes.size
     P = n * (n - 1) // 2
     rows = 2048
@@ -187,47 +199,118 @@ def cpu_baseline(codes, gpu_hist, budget_s):
 
 
 # ------------------------------------------------------------------ rooflines
-def _traffic(name):
-    """HBM bytes per launch of the kernel from the committed PMC summary, or None."""
-    pmc = os.path.join(ROOT, "profiles", name)
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+def _profile(name):
+    """A committed PMC summary (profiles/pmc_<name>_<round>.json, tools/summarize_profile.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (name, PROFILE_ROUND))
+    if os.path.exists(path):
+        with open(path) as f:
+            return dict(json.load(f), file=os.path.relpath(path, ROOT))
     return None
 
 
-def spectral_roofline(tk, step_count_ms, my_slices):
-    """SPECTRAL's two kernels per chunk: seed (writes 2^14 int8 values per slice) and tile
-    (reads them back: 14-bit WHT on the matrix cores + F^2 binning).  Both move 16 KiB per
-    slice through HBM, so the roofline is HBM bandwidth; the slower kernel is reported."""
-    per_launch = tk["units"]
-    launches = -(-my_slices // per_launch)
-    algo_bytes = per_launch * (1 << 14)
-    kern = {"tile": {"kernel": "sct_spectral::tile_reg_p16_kernel (int8 seeds)", "ms": tk["kernel_ms"],
-                     "traffic": _traffic("pmc_spectral_latest.json")},
-            "seed": {"kernel": "sct_spectral::seed_kernel<int8_t>", "ms": tk["seed_ms"],
-                     "traffic": _traffic("pmc_spectral_seed_latest.json")}}
-    for k in kern.values():
-        k["achieved_gbs"] = algo_bytes / (k["ms"] * 1e-3) / 1e9
-        k["frac"] = k["achieved_gbs"] * 1e9 / HBM_PEAK_BPS
-    dom, other = ("seed", "tile") if tk["seed_ms"] >= tk["kernel_ms"] else ("tile", "seed")
+def _rocprof_avg_ms(kernel_substr):
+    """Average dispatch duration of a kernel in the committed rocprofv3 --kernel-trace --stats
+    summary of this bench command (profiles/<round>_kernel_stats.csv), or None."""
+    import csv
+    path = os.path.join(ROOT, "profiles", "%s_kernel_stats.csv" % PROFILE_ROUND)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if kernel_substr in r["Name"]:
+                return float(r["AverageNs"]) * 1e-6, int(r["Calls"])
+    return None, None
+
+
+def issue_picture(prof):
+    """Issue-rate picture of one kernel from its committed PMC summary: the fraction of the
+    SIMDs' cycles (at the clock the profiled run held) in which a VALU instruction is active
+    (SQ_ACTIVE_INST_VALU counts quad-cycles), the matrix pipe is busy (SQ_VALU_MFMA_BUSY_CYCLES),
+    and waves sit parked at s_waitcnt / barriers or stall on issue (SQ_WAIT_ANY /
+    SQ_WAIT_INST_ANY over SQ_WAVE_CYCLES).  None without a profile."""
+    if not prof or "pmc" not in prof:
+        return None
+    m, ns = prof["pmc"], prof.get("trace_avg_ns")
+    out = {"source": prof["file"]}
+    if "GRBM_GUI_ACTIVE" in m and ns:
+        cycles = m["GRBM_GUI_ACTIVE"] / 8  # 8 XCDs
+        out["clock_ghz"] = cycles / ns
+        slots = SIMDS * cycles
+        if "SQ_ACTIVE_INST_VALU" in m:
+            out["valu_busy_frac"] = 4 * m["SQ_ACTIVE_INST_VALU"] / slots
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+            out["mfma_busy_frac"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / slots
+    if "SQ_WAVE_CYCLES" in m:
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            if k in m:
+                out[k.lower()[3:] + "_frac_of_wave_cycles"] = m[k] / m["SQ_WAVE_CYCLES"]
+    if "hbm_bytes_per_launch" in prof:
+        out["hbm_bytes_per_launch"] = prof["hbm_bytes_per_launch"]
+    return out
+
+
+def copy_ceiling_gbs(dev, mib=2048, reps=5):
+    """Device-to-device copy bandwidth measured in this run (read + write bytes / time):
+    the practical HBM ceiling the kernels are compared with beside the 8 TB/s spec."""
+    import torch
+    a = torch.empty(mib << 20, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    gbs = 2 * a.numel() * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbs
+
+
+def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, names=("pmc_spectral_seed", "pmc_spectral")):
+    """SPECTRAL's two kernels per chunk: seed (writes 2^14 values per slice) and tile (reads
+    them back: 14-bit WHT + F^2 binning).  Each moves 2^14 * elem_bytes per slice through HBM
+    -- its algorithmic bytes -- so the HBM roofline prices both; the slower is reported.
+    kt = {kind: (ms summed, launches)} from the HIP events around every launch of the timed
+    steps."""
+    algo = slices_per_launch * (1 << 14) * elem_bytes
+    kern = {}
+    for k, label, prof_name, rp in (("seed", "sct_spectral::seed_kernel<%s>" % {1: "int8_t", 2: "int16_t", 4: "int32_t"}[elem_bytes],
+                                     names[0], "seed_kernel<"),
+                                    ("tile", "sct_spectral::tile_reg_kernel (int8 seeds)" if elem_bytes == 1
+                                     else "sct_spectral::tile_kernel<int%d_t>" % (8 * elem_bytes), names[1],
+                                     "tile_reg_kernel" if elem_bytes == 1 else "tile_kernel<")):
+        ms, nl = kt[k]
+        avg = ms / nl if nl else float("nan")
+        prof = _profile(prof_name) if elem_bytes == 1 else None
+        rms, rcalls = _rocprof_avg_ms(rp) if elem_bytes == 1 else (None, None)
+        gbs = algo / (avg * 1e-3) / 1e9
+        kern[k] = {"kernel": label, "ms": avg, "launches": nl, "achieved_gbs": gbs, "frac": gbs * 1e9 / HBM_PEAK_BPS,
+                   "frac_of_copy_ceiling": gbs / copy_gbs if copy_gbs else None,
+                   "traffic": prof.get("hbm_bytes_per_launch") if prof else None,
+                   "issue": issue_picture(prof),
+                   "rocprof": None if rms is None else {
+                       "avg_ms": rms, "calls": rcalls, "frac": algo / (rms * 1e-3) / HBM_PEAK_BPS,
+                       "source": "profiles/%s_kernel_stats.csv" % PROFILE_ROUND,
+                       "live_vs_rocprof": avg / rms - 1.0}}
+    dom, other = ("seed", "tile") if kern["seed"]["ms"] >= kern["tile"]["ms"] else ("tile", "seed")
     d = kern[dom]
-    tile_ops = per_launch * SPECTRAL_OPS_PER_SLICE / (tk["kernel_ms"] * 1e-3)
     return {"bound": "hbm", "achieved": d["achieved_gbs"], "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
             "frac": d["frac"], "traffic": d["traffic"], "kernel": d["kernel"], "kernel_ms": d["ms"],
+            "launches": d["launches"], "frac_of_copy_ceiling": d["frac_of_copy_ceiling"],
+            "copy_ceiling_gbs": copy_gbs, "issue": d["issue"], "rocprof": d["rocprof"],
             "other_kernel": dict(kern[other], name=other),
-            "slices_per_launch": per_launch, "launches_per_step": launches,
-            "algo_bytes_per_launch": algo_bytes,
-            "count_ms_per_step": step_count_ms,
-            "chunk_frac": 2 * algo_bytes / ((tk["seed_ms"] + tk["kernel_ms"]) * 1e-3) / HBM_PEAK_BPS,
-            "tile_valu_equivalent": {"algo_ops_per_slice": SPECTRAL_OPS_PER_SLICE, "achieved_tops": tile_ops / 1e12,
-                                     "peak_tops": VALU_PEAK_OPS / 1e12, "frac": tile_ops / VALU_PEAK_OPS,
-                                     "note": "14 butterfly add/subs + 1 square-accumulate per value as int32 "
-                                             "VALU ops; 12 of the 14 levels run on the matrix cores"},
-            "note": "kernel_ms: HIP events around 5 back-to-back launches of each kernel on the bench "
-                    "stream; algo bytes = the int8 seed values of one launch (the seed kernel writes them, "
-                    "the tile kernel reads them); traffic: HBM bytes per launch from PMC "
-                    "(tools/summarize_profile.py); chunk_frac = both kernels' bytes over their summed time"}
+            "slices_per_launch": slices_per_launch, "algo_bytes_per_launch": algo,
+            "count_ms_per_step": count_ms,
+            "chunk_frac": 2 * algo / ((kern["seed"]["ms"] + kern["tile"]["ms"]) * 1e-3) / HBM_PEAK_BPS,
+            "note": "kernel_ms: mean of HIP events recorded around every launch of this kernel in the K timed "
+                    "steps, on the stream the launches run on (sct_allpairs_timing); algo bytes = the seed "
+                    "values of one launch (the seed kernel writes them, the tile kernel reads them); traffic: "
+                    "HBM bytes per launch from PMC (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction); issue: "
+                    "VALU / matrix-pipe busy fractions of the SIMD cycles from PMC -- neither unit is saturated, "
+                    "the kernels sit between the HBM and issue ceilings (DESIGN.md §3.8); rocprof: the "
+                    "committed kernel-trace average of this command, profiled (lower clock)"}
 
 
 def issue_slots_per_pair(scheme):
@@ -239,16 +322,15 @@ def issue_slots_per_pair(scheme):
 
 
 def pair_roofline(job, my_pairs, kms, L):
-    achieved = my_pairs * ALGO_OPS_PER_PAIR / (kms * 1e-3)
     spp = issue_slots_per_pair(job.scheme) if L == 16 else float("nan")
     slots = my_pairs * spp / (kms * 1e-3)
-    t = job.timings()
-    return {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
-            "unit": "Tops/s", "frac": achieved / VALU_PEAK_OPS, "traffic": _traffic("pmc_allpairs_latest.json"),
-            "kernel": "allpairs_count_kernel<8>", "kernel_ms": kms, "algo_ops_per_pair": ALGO_OPS_PER_PAIR,
-            "issue_slots_per_pair": spp, "moments_ms": t["moments_ms"], "issue_slot_frac": slots / VALU_PEAK_OPS,
-            "note": "frac > 1: the bit-sliced kernel needs %.2f VALU issue slots per pair where SURVEY "
-                    "8(d)'s formulation needs 4 ops; issue_slot_frac is the VALU utilisation" % spp}
+    return {"bound": "valu_issue", "achieved": slots / 1e12, "peak": VALU_PEAK_OPS / 1e12,
+            "unit": "T issue slots/s", "frac": slots / VALU_PEAK_OPS, "traffic": None,
+            "kernel": "allpairs_count_kernel<8>", "kernel_ms": kms, "issue_slots_per_pair": spp,
+            "algo_ops_per_pair": ALGO_OPS_PER_PAIR,
+            "survey_ops_frac": my_pairs * ALGO_OPS_PER_PAIR / (kms * 1e-3) / VALU_PEAK_OPS,
+            "note": "the bit-sliced kernel needs %.2f VALU issue slots per pair (SURVEY 8(d)'s formulation: 4 "
+                    "ops); frac = issue slots used / the 78.6 T slots/s the chip offers at 2.4 GHz" % spp}
 
 
 def time_pair_kernel(d_codes, L, steps):
@@ -269,11 +351,154 @@ def time_pair_kernel(d_codes, L, steps):
         kms = job.timings()["count_ms"]
         spp = issue_slots_per_pair(job.scheme)
         return {"scheme": "moments", "value": P / dt, "unit": "pairs/s", "ms_per_step": dt * 1e3, "steps": steps,
-                "kernel_ms": kms, "kernel_frac": P * ALGO_OPS_PER_PAIR / (kms * 1e-3) / VALU_PEAK_OPS,
-                "issue_slots_per_pair": spp,
+                "kernel_ms": kms, "issue_slots_per_pair": spp,
                 "issue_slot_frac": P * spp / (kms * 1e-3) / VALU_PEAK_OPS,
-                "note": "kernel_frac counts SURVEY 8(d)'s 4 ops per pair and exceeds 1 because the kernel "
-                        "is bit-sliced; issue_slot_frac is the fraction of the VALU issue slots it uses"}
+                "note": "enumerates every pair; issue_slot_frac is the fraction of the VALU issue slots it uses"}
+
+
+# ------------------------------------------------------------------ configs 4 / 5 (N = 1)
+def _events_ms(fn, reps, dev):
+    import torch
+    fn()
+    s = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def path_config4(dev, reps, copy_gbs, threads):
+    """Config 4: nearest-whitelist correction of 100M ThreeBit observed barcodes against the
+    737,280-code whitelist at Hamming <= 1 (sct_nearest_query on device-resident queries)."""
+    import torch
+    from oracle import oracle as O
+    from sctools_amd import _lib, synthetic
+    n, L, seed = synthetic.CONFIGS[4]
+    nq = synthetic.CONFIG4_QUERIES
+    wl = synthetic.two_to_three(synthetic.whitelist_codes(n, L, seed), L)
+    q, pick, cls = synthetic.config4_queries(wl, nq, seed=4, device=dev)
+    d_wl = torch.from_numpy(wl.view(np.int64)).to(dev)
+    idx = torch.empty(nq, dtype=torch.int32, device=dev)
+    dist = torch.empty(nq, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    plan = _lib.NearestPlan(3, d_wl.data_ptr(), n, 3 * L, 1, stream)
+    torch.cuda.synchronize()
+    build_ms = (time.perf_counter() - t) * 1e3
+    ms = _events_ms(lambda: plan.query(q.data_ptr(), nq, idx.data_ptr(), dist.data_ptr(), stream), reps, dev)
+    index = plan.info()
+    plan.close()
+    exact = cls == 0
+    exact_ok = bool(torch.equal(idx[exact].long(), pick[exact])) and bool((dist[exact] == 0).all())
+    g = torch.Generator(device=dev).manual_seed(44)
+    samp = torch.randint(0, nq, (20_000,), device=dev, generator=g)
+    ridx, rdist = O.c_nearest(3, wl, q[samp].cpu().numpy().view(np.uint64), 1, threads=threads)
+    sample_ok = bool(np.array_equal(idx[samp].cpu().numpy(), ridx) and np.array_equal(dist[samp].cpu().numpy(), rdist))
+    algo = nq * (8 + 4 + 1)
+    gbs = algo / (ms * 1e-3) / 1e9
+    del q, pick, cls, idx, dist
+    torch.cuda.empty_cache()
+    return {"workload": "config 4: %d ThreeBit 16-bp observed barcodes (50%% exact, 25%% one substitution, "
+                        "15%% one N, 10%% random) vs the %d-code whitelist, Hamming <= 1" % (nq, n),
+            "value": nq / (ms * 1e-3), "unit": "queries/s", "ms": ms, "reps": reps, "index_build_ms": build_ms,
+            "index": index,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
+                         "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs,
+                         "algo_bytes_per_query": 13, "kernel": "sct_nearest_query",
+                         "note": "algorithmic bytes = the query stream (8 B in, 4 + 1 B out); the index "
+                                 "probes are extra (DESIGN.md §3.5)"},
+            "check": {"exact_draws_own_index": exact_ok, "sampled_vs_oracle": sample_ok,
+                      "sample": "20,000 random queries vs oracle.c_nearest (OpenMP brute force over the whole "
+                                "whitelist)"}}
+
+
+def path_config5_allpairs(dev, steps, copy_gbs):
+    """Config 5's all-pairs half on one GPU: 3,686,400 codes (6.79e12 pairs), SPECTRAL with
+    int16 seeds, pipelined steps as the headline."""
+    import torch
+    from oracle import oracle as O
+    from sctools_amd import _lib, sharding, synthetic
+    n, L, seed = synthetic.CONFIGS[5]
+    codes = synthetic.whitelist_codes(n, L, seed)
+    with sharding.ShardedAllPairs(codes, 2 * L) as job:
+        job.run(1)
+        job.kernel_timing(1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hists = job.run(steps)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        kt = job.kernel_timing(0)
+        info = job.plan.spectral_info()
+        roof = spectral_roofline(kt, min(info["chunk_slices"], job.end - job.begin), info["elem_bytes"], None, copy_gbs)
+        P = job.plan.pairs
+    hist = hists[-1]
+    ok_steps = all(np.array_equal(h, hist) for h in hists)
+    m_hist = O.moments_from_hist([int(x) for x in hist], order=2)
+    m_codes = O.moments_from_marginals(codes, order=2)
+    return {"workload": "config 5 all-pairs: %d-code 16-bp whitelist, all %d pairs" % (n, P),
+            "value": P / dt, "unit": "pairs/s", "ms_per_step": dt * 1e3, "steps": steps,
+            "roofline": {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel", "kernel_ms",
+                                              "launches", "frac_of_copy_ceiling", "other_kernel",
+                                              "algo_bytes_per_launch")},
+            "check": {"steps_agree": ok_steps, "pairs": int(hist.sum()) == P,
+                      "moments_vs_oracle_marginals": m_hist == m_codes,
+                      "sample": "M_1, M_2 (pairs agreeing on 1 / 2 chosen positions) from the histogram vs "
+                                "oracle.moments_from_marginals; the full bin-for-bin oracle check is "
+                                "tests/test_gpu_parity.py::test_allpairs_config5_spectral_bin_for_bin"}}
+
+
+def path_config5_encode(dev, reps, copy_gbs):
+    """Config 5's read stream: 1e9 random 28-bp reads (1 % with one N) generated on the device,
+    TwoBit encode + GC + flags (sct_encode) device-resident."""
+    import torch
+    from oracle import oracle as O
+    from sctools_amd import _lib, synthetic
+    n, L = synthetic.CONFIG5_READS, synthetic.CONFIG5_READ_LENGTH
+    g = torch.Generator(device=dev).manual_seed(5)
+    seqs = torch.randint(0, 4, (n, L), dtype=torch.uint8, device=dev, generator=g)
+    chunk = 50_000_000
+    for r0 in range(0, n, chunk):  # TwoBit values -> ASCII: A 65, C 67, T 84, G 71
+        x = seqs[r0:r0 + chunk]
+        x.copy_(65 + 2 * x + 15 * (x == 2).to(torch.uint8))
+    nrows = torch.arange(0, n, 100, device=dev)
+    seqs[nrows, torch.randint(0, L, (nrows.numel(),), device=dev, generator=g)] = ord("N")
+    codes = torch.empty(n, dtype=torch.int64, device=dev)
+    gc = torch.empty(n, dtype=torch.uint8, device=dev)
+    flags = torch.empty(n, dtype=torch.uint8, device=dev)
+    lib = _lib.lib()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def run():
+        _lib.check(lib.sct_encode(2, seqs.data_ptr(), n, L, L, codes.data_ptr(), gc.data_ptr(), flags.data_ptr(),
+                                  stream))
+    ms = _events_ms(run, reps, dev)
+    torch.cuda.synchronize()
+    gc_total = int(gc.sum(dtype=torch.int64))
+    want_gc = int((seqs == ord("C")).sum()) + int((seqs == ord("G")).sum())
+    nflag = int(flags.sum(dtype=torch.int64))
+    ok = True
+    for r in range(7, n, 1_000_000):
+        s = bytes(seqs[r].cpu().numpy().tobytes())
+        ok = ok and int(codes[r]) == O.two_bit_encode(s) and int(gc[r]) == s.count(b"C") + s.count(b"G")
+    algo = n * (L + 8 + 1 + 1)
+    gbs = algo / (ms * 1e-3) / 1e9
+    del seqs, codes, gc, flags
+    torch.cuda.empty_cache()
+    return {"workload": "config 5 read stream: %d random %d-bp reads (1%% with one N), TwoBit encode + GC + "
+                        "flags, device-resident" % (n, L),
+            "value": n / (ms * 1e-3), "unit": "reads/s", "ms": ms, "reps": reps,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
+                         "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs,
+                         "algo_bytes_per_read": L + 10, "kernel": "encode_tiled_kernel"},
+            "check": {"gc_total_vs_bytes": gc_total == want_gc, "flagged_reads": nflag == (n + 99) // 100,
+                      "sampled_vs_oracle": ok,
+                      "sample": "every 10^6-th read (offset 7) vs oracle.two_bit_encode; the GC total vs the C/G "
+                                "bytes counted by torch; one flag per N read"}}
 
 
 # ------------------------------------------------------------------ ranks
@@ -338,16 +563,18 @@ def run_rank(args, rank, world, local):
     # kernels are queued before the host waits for step k's histogram
     job.run(args.warmup)
     job.reset_timings()  # the timings cover the timed steps only
+    job.kernel_timing(1)  # HIP events around every kernel launch of the timed steps
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     hists = job.run(args.steps, timing=True)
     torch.cuda.synchronize()
+    mine = time.perf_counter() - t0  # this rank's own wall time, before waiting for the others
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    mine = time.perf_counter() - t0  # this rank's own wall time (before the max)
+    kt = job.kernel_timing(0)
     tm = job.timings()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -370,18 +597,19 @@ def run_rank(args, rank, world, local):
     P = job.plan.pairs
     assert int(hist.sum()) == P, "histogram does not cover every pair"
     summ = _lib.summary_from_hist(hist)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    if spectral:  # the tile / seed kernels apart: back-to-back launches between HIP events
-        scratch = torch.zeros(job.plan.ncounts, dtype=torch.int64, device=dev)
-        tk = job.plan.time_kernels(scratch.data_ptr(), job.begin, job.end, 5, stream)
-        roofline = spectral_roofline(tk, tm["count_ms"], job.end - job.begin)
+    copy_gbs = copy_ceiling_gbs(dev) if rank == 0 else None
+    if spectral:
+        info = job.plan.spectral_info()
+        roofline = spectral_roofline(kt, min(info["chunk_slices"], job.end - job.begin), info["elem_bytes"],
+                                     tm["count_ms"], copy_gbs)
     else:
-        roofline = pair_roofline(job, job.my_pairs(), tm["count_ms"], L)
+        roofline = pair_roofline(job, job.my_pairs(), kt["count"][0] / max(1, kt["count"][1]), L)
     pair_kernel = None
     if spectral and world == 1 and args.pair_steps > 0:
         pair_kernel = time_pair_kernel(job.d_codes, L, args.pair_steps)
     job.close()
 
+    out = None
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -416,8 +644,16 @@ def run_rank(args, rank, world, local):
         }
         if pair_kernel is not None:
             out["pair_kernel"] = pair_kernel
-        if not args.no_cpu and world == 1:
+    if rank == 0 and world == 1:
+        threads, _ = host_threads()
+        if not args.no_paths:
+            # configs 4 and 5 (BASELINE.json), each timed on its own after the headline
+            out["paths"] = {"config4_nearest": path_config4(dev, args.path_steps, copy_gbs, threads),
+                            "config5_allpairs": path_config5_allpairs(dev, max(2, args.path_steps), copy_gbs),
+                            "config5_encode": path_config5_encode(dev, max(2, args.path_steps // 2), copy_gbs)}
+        if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(codes, hist, args.cpu_seconds)
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -37,6 +37,23 @@ const char* sct_last_error(void);      /* thread-local, never NULL */
 int sct_device_count(int* count);      /* HIP devices visible to this process */
 int sct_set_device(int device);        /* select the device for later calls (hipSetDevice) */
 
+/* Launch-shape knobs.  None changes a result: they cut work into other chunk / grid sizes
+ * or pick between index layouts that give identical outputs, so tests can put seams inside
+ * small problems and benchmarks can sweep.  Process-global; the library reads no environment
+ * variable.  value < 0 restores the default.  Read when a plan is created (scalar: per call). */
+#define SCT_TUNE_SPECTRAL_CHUNK 1       /* slices per seed/tile pass (default 65536) */
+#define SCT_TUNE_SPECTRAL_MIN_N 2       /* AUTO takes SPECTRAL from this many 16-base codes (500000) */
+#define SCT_TUNE_ALLPAIRS_GRAB 3        /* pair kernel: work items per queue pull */
+#define SCT_TUNE_ALLPAIRS_FLUSH_ITEMS 4 /* pair kernel: flush lane counters every k items */
+#define SCT_TUNE_ALLPAIRS_GRID 5        /* pair kernel: persistent grid size */
+#define SCT_TUNE_NEAREST_SCHEME 6       /* 0 auto, 1 open addressing, 2 CSR buckets, 3 half keys */
+#define SCT_TUNE_NEAREST_LOAD 7         /* open addressing: table slots per whitelist code */
+#define SCT_TUNE_SCALAR_SERVER 8        /* 0: every scalar call is a kernel launch (default 1) */
+#define SCT_TUNE_SCALAR_IDLE_MS 9       /* the scalar server exits after this idle time (5) */
+#define SCT_TUNE_NKEYS 10
+int sct_tune_set(int key, int64_t value);
+int sct_tune_get(int key, int64_t* value);  /* -1 when unset */
+
 /* ---------------------------------------------------------------- encoders
  * kind = 2 (TwoBit) or 3 (ThreeBit).
  * Replaces TwoBit.encode  (src/sctools/encodings.py:75-88, map :53-69) and
@@ -126,9 +143,9 @@ int sct_hamming_pairs_host(int kind, const uint64_t* a, const uint64_t* b, int64
  * The *_host calls above with n <= 64 records (the drop-in's scalar methods, e.g.
  * TwoBit.encode / hamming_distance, encodings.py:75-121) are served by a resident
  * one-wave kernel per host thread and device that polls a page-locked mailbox, instead of
- * one kernel launch per call; it exits by itself after SCT_SCALAR_IDLE_MS (default 5) idle
+ * one kernel launch per call; it exits by itself after SCT_TUNE_SCALAR_IDLE_MS (default 5) idle
  * milliseconds and before any kernel that sizes its grid to the resident workgroups.
- * SCT_SCALAR_SERVER=0 turns it off (every call is then a launch).
+ * sct_tune_set(SCT_TUNE_SCALAR_SERVER, 0) turns it off (every call is then a launch).
  * sct_scalar_server_stop: ask every server of the process to exit and wait for it.
  * sct_scalar_server_status: server launches so far and servers running now (either may
  * be NULL).
@@ -226,6 +243,20 @@ int sct_allpairs_range_pairs(const sct_allpairs_plan* plan, int64_t item_begin, 
 int sct_allpairs_time_kernels(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
                               uint64_t* d_counts, int repeats, double* out, void* stream);
 
+/* SPECTRAL plans: bytes per seed value of the seed -> tile intermediate (1, 2 or 4: the
+ * densest transform column bounds it), slices per seed / tile launch, codes in the densest
+ * column.  Other schemes: SCT_E_INVALID. */
+int sct_allpairs_spectral_info(const sct_allpairs_plan* plan, int* elem_bytes, int64_t* chunk_slices,
+                               int* max_column);
+
+/* Bench aid: per-launch HIP-event timing of this plan's kernels, recorded on the stream each
+ * launch runs on (so it times the launches of a real run, pipelined or not).  mode 1 = start
+ * (zeroes the sums), 0 = stop, 2 = read and keep recording.  out (nullable, 8 doubles) =
+ * [ms, launches] summed over the recorded launches of kind 0 seed, 1 tile (SPECTRAL), 2 pair
+ * count kernel (SUBSETS / MOMENTS), 3 table build (one span per build call); the call waits
+ * for the recorded launches. */
+int sct_allpairs_timing(sct_allpairs_plan* plan, int mode, double* out);
+
 /* Host: SUBSETS counts -> histogram (exact Moebius inversion), hist[d] for d < nbins. */
 int sct_counts_to_hist(const uint64_t* counts, int nbins, uint64_t* hist);
 /* Host: counts of any scheme -> histogram (MOMENTS: exact rational solve of the
@@ -280,6 +311,11 @@ int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, int64_t nw, i
 int sct_nearest_plan_destroy(sct_nearest_plan* plan);
 int sct_nearest_query(sct_nearest_plan* plan, const uint64_t* d_queries, int64_t nq,
                       int32_t* d_index, uint8_t* d_dist, void* stream);
+/* the index layout the plan chose and its device bytes */
+#define SCT_NEAREST_OA 1       /* open-addressing tables of block-pair keys */
+#define SCT_NEAREST_CSR 2      /* CSR buckets per block */
+#define SCT_NEAREST_HALVES 3   /* sorted half-key tables (max_d <= 1, ACGT whitelists) */
+int sct_nearest_plan_info(const sct_nearest_plan* plan, int* scheme, int64_t* index_bytes);
 int sct_nearest_host(int kind, const uint64_t* whitelist, int64_t nw, const uint64_t* queries,
                      int64_t nq, int code_bits, int max_d, int32_t* index, uint8_t* dist);
 

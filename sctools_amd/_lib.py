@@ -28,6 +28,12 @@ SCHEME_SUBSETS = 0
 SCHEME_MOMENTS = 1
 SCHEME_SPECTRAL = 2
 
+# launch-shape knobs (sct_tune_set; none changes a result)
+TUNE_KEYS = {"spectral_chunk": 1, "spectral_min_n": 2, "allpairs_grab": 3, "allpairs_flush_items": 4,
+             "allpairs_grid": 5, "nearest_scheme": 6, "nearest_load": 7, "scalar_server": 8,
+             "scalar_idle_ms": 9}
+NEAREST_AUTO, NEAREST_OA, NEAREST_CSR, NEAREST_HALVES = 0, 1, 2, 3
+
 _i32, _i64, _dbl = ctypes.c_int, ctypes.c_int64, ctypes.c_double
 _vp = ctypes.c_void_p
 _p64 = ctypes.POINTER(ctypes.c_uint64)
@@ -38,6 +44,8 @@ SIGNATURES = {
     "sct_last_error": [],
     "sct_device_count": [ctypes.POINTER(_i32)],
     "sct_set_device": [_i32],
+    "sct_tune_set": [_i32, _i64],
+    "sct_tune_get": [_i32, ctypes.POINTER(_i64)],
     "sct_encode": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
     "sct_encode_host": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp],
     "sct_encode_stream_host": [_i32, _vp, _i64, _i32, _vp, _vp, _vp, _i64],
@@ -64,6 +72,9 @@ SIGNATURES = {
     "sct_allpairs_count": [_vp, _i64, _i64, _vp, _i32, _vp],
     "sct_allpairs_range_pairs": [_vp, _i64, _i64, ctypes.POINTER(_i64)],
     "sct_allpairs_time_kernels": [_vp, _i64, _i64, _vp, _i32, ctypes.POINTER(ctypes.c_double), _vp],
+    "sct_allpairs_timing": [_vp, _i32, ctypes.POINTER(ctypes.c_double)],
+    "sct_allpairs_spectral_info": [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i64), ctypes.POINTER(_i32)],
+    "sct_nearest_plan_info": [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i64)],
     "sct_allpairs_geometry": [_i64, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i64),
                               ctypes.POINTER(_i32), ctypes.POINTER(_i32)],
     "sct_counts_to_hist": [_vp, _i32, _vp],
@@ -160,6 +171,36 @@ def check(rc):
     if rc in (SCT_E_INVALID, SCT_E_RANGE):
         raise ValueError(msg)
     raise RuntimeError(msg)
+
+
+def tune_get(name):
+    v = _i64(0)
+    check(lib().sct_tune_get(TUNE_KEYS[name], ctypes.byref(v)))
+    return v.value
+
+
+def tune_set(name, value):
+    """Set a launch-shape knob (None or < 0 restores the default)."""
+    check(lib().sct_tune_set(TUNE_KEYS[name], -1 if value is None else int(value)))
+
+
+class tuning:
+    """Context manager: ``with tuning(spectral_chunk=1000): ...`` sets knobs and restores them."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+        self.saved = {}
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            self.saved[k] = tune_get(k)
+            tune_set(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            tune_set(k, v)
+        return False
 
 
 def _ptr(a):
@@ -534,6 +575,12 @@ class NearestPlan:
         check(self._lib.sct_nearest_plan_create(kind, _vp(d_whitelist_ptr), nw, code_bits, max_d,
                                                 _vp(stream), ctypes.byref(self._h)))
 
+    def info(self):
+        """dict(scheme: 'oa' | 'csr' | 'halves', index_bytes)."""
+        sc, nb = _i32(0), _i64(0)
+        check(self._lib.sct_nearest_plan_info(self._h, ctypes.byref(sc), ctypes.byref(nb)))
+        return {"scheme": {1: "oa", 2: "csr", 3: "halves"}.get(sc.value, str(sc.value)), "index_bytes": nb.value}
+
     def query(self, d_queries_ptr, nq, d_index_ptr, d_dist_ptr, stream=0):
         check(self._lib.sct_nearest_query(self._h, _vp(d_queries_ptr), nq, _vp(d_index_ptr),
                                           _vp(d_dist_ptr), _vp(stream)))
@@ -604,6 +651,20 @@ class AllPairsPlan:
         check(self._lib.sct_allpairs_time_kernels(self._h, begin, end, _vp(d_scratch_ptr), repeats, out,
                                                   _vp(stream)))
         return {"kernel_ms": out[0], "seed_ms": out[1], "units": int(out[2])}
+
+    def timing(self, mode):
+        """Per-launch HIP-event timing of this plan's kernels (sct_allpairs_timing): mode 1
+        start, 0 stop, 2 read.  Returns {kind: (ms summed, launches)} for seed, tile, count,
+        build."""
+        out = (ctypes.c_double * 8)()
+        check(self._lib.sct_allpairs_timing(self._h, mode, out))
+        return {k: (out[2 * i], int(out[2 * i + 1])) for i, k in enumerate(("seed", "tile", "count", "build"))}
+
+    def spectral_info(self):
+        """SPECTRAL plans: dict(elem_bytes, chunk_slices, max_column)."""
+        eb, ch, mc = _i32(0), _i64(0), _i32(0)
+        check(self._lib.sct_allpairs_spectral_info(self._h, ctypes.byref(eb), ctypes.byref(ch), ctypes.byref(mc)))
+        return {"elem_bytes": eb.value, "chunk_slices": ch.value, "max_column": mc.value}
 
     def range_pairs(self, begin, end):
         p = _i64(0)

@@ -21,6 +21,8 @@ from .stats import base4_entropy
 
 __all__ = ["Barcodes", "ObservedBarcodeSet", "PriorBarcodeSet", "nearest_whitelist"]
 
+_MIXED_SIGNS = ('barcode codes mix negative and non-negative integers: their XOR is negative and the '
+                'reference\'s distance loop (encodings.py:118, `while difference:`) never terminates on it')
 _SUMMARY_KEYS = ('minimum', '25th percentile', 'median', '75th percentile', 'maximum', 'average')
 
 
@@ -57,7 +59,14 @@ class Barcodes:
         """The unique keys in iteration order, as the kernels take them: np.uint64 (n,)
         when every key fits 64 bits, else (n, words) little-endian uint64 limbs.  Built from
         the mapping on every call (the reference re-reads ``self`` each time, barcode.py:42),
-        so a mapping changed in place is never served stale."""
+        so a mapping changed in place is never served stale.
+
+        Negative keys: the reference's ``a ^ b`` of two negative ints is non-negative and its
+        digit loop (encodings.py:113-121) counts it, so an all-negative key set is summarised
+        like any other: every key shares its bits from m = max bit_length(~k) upward (all
+        ones), so ``k & (2^m - 1)`` keeps every pairwise XOR unchanged.  A negative key next
+        to a non-negative one gives a negative XOR, on which the reference's ``while
+        difference:`` never ends; that raises ValueError here instead of hanging."""
         keys = self._data.keys()
         n = len(self._data)
         if not all(issubclass(t, (int, np.integer)) for t in set(map(type, keys))):
@@ -66,10 +75,13 @@ class Barcodes:
             for a, b in itertools.combinations(self._data, 2):
                 a ^ b
             return np.zeros(n, dtype=np.uint64)  # < 2 keys: no pair, nothing to compare
-        try:  # the common case (every key < 2^63) on numpy's fastest conversion
+        try:  # the common case (every key in int64) on numpy's fastest conversion
             arr = np.fromiter(keys, dtype=np.int64, count=n)
             if n and int(arr.min()) < 0:
-                raise ValueError('barcode codes must be non-negative integers')
+                if int(arr.max()) >= 0 and n >= 2:
+                    raise ValueError(_MIXED_SIGNS)
+                m = int((~arr).max()).bit_length()
+                return (arr & np.int64((1 << m) - 1)).view(np.uint64) if m < 63 else arr.view(np.uint64)
             return arr.view(np.uint64)
         except OverflowError:
             pass
@@ -79,9 +91,12 @@ class Barcodes:
             except OverflowError:
                 pass
         ints = [int(k) for k in keys]
-        if any(v < 0 for v in ints):
-            # the reference's `while difference:` never ends on a negative XOR (encodings.py:118)
-            raise ValueError('barcode codes must be non-negative integers')
+        neg = [v < 0 for v in ints]
+        if any(neg):
+            if not all(neg) and n >= 2:
+                raise ValueError(_MIXED_SIGNS)
+            mask = (1 << max((~v).bit_length() for v in ints)) - 1
+            ints = [v & mask for v in ints]
         return _lib.ints_to_limbs(ints)
 
     def hamming_histogram(self):

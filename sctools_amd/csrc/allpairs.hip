@@ -315,7 +315,8 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
   if constexpr (!MASKED) cnt0 += Gm::CB;
 }
 
-// Count-kernel variants (A/B-selectable with SCT_ALLPAIRS_VARIANT): the group-pair loop
+// Count-kernel variants (A/B-selectable with SCT_ALLPAIRS_VARIANT in the ablation build; the
+// product build instantiates only the shipped one per scheme): the group-pair loop
 // unrolled 1, 2, fully (3: LDS offsets become immediates) or 4 times.  A software-
 // pipelined form (next group pair's reads issued before this one's counting) and forced
 // occupancy (amdgpu_waves_per_eu) measured no faster and were dropped.
@@ -323,8 +324,8 @@ __device__ __forceinline__ void process_item(const uint4* __restrict__ tile, uin
 // capped at 512 / WAVES): variant 5 = unroll 2 held to 128 VGPRs (4 waves per SIMD).
 template <int V> struct Variant { static constexpr int UNROLL = V, ABL = 0, WAVES = 1; };
 template <> struct Variant<3> { static constexpr int UNROLL = 16, ABL = 0, WAVES = 1; };
-template <> struct Variant<5> { static constexpr int UNROLL = 2, ABL = 0, WAVES = 4; };
 #ifdef SCT_ABLATION
+template <> struct Variant<5> { static constexpr int UNROLL = 2, ABL = 0, WAVES = 4; };
 // ablation builds (wrong results, timing only): 11 no counting, 12 no tree, 13 no LDS reads,
 // 14 neither tree nor counting (the loop's fixed costs)
 template <> struct Variant<11> { static constexpr int UNROLL = 4, ABL = 1, WAVES = 1; };
@@ -708,19 +709,9 @@ bool mom_supported(int npp, int64_t n) { return npp * 2 == sct::kMomG && n <= 10
 // SPECTRAL: the same 16-base codes; its cost does not depend on n
 bool spectral_supported(int npp, int64_t n) { return mom_supported(npp, n); }
 // smallest n for which AUTO picks SPECTRAL over MOMENTS (measured crossover)
-int64_t spectral_min_n() {
-  const char* v = getenv("SCT_SPECTRAL_MIN_N");
-  return v ? atoll(v) : 500000;
-}
-// what SCT_ALLPAIRS_AUTO resolves to; SCT_ALLPAIRS_SCHEME=0/1/2 in the environment forces
-// SUBSETS / MOMENTS / SPECTRAL where the codes allow it
+int64_t spectral_min_n() { return sct::tune(SCT_TUNE_SPECTRAL_MIN_N, 500000); }
+// what SCT_ALLPAIRS_AUTO resolves to
 int auto_scheme(int npp, int64_t n) {
-  if (const char* v = getenv("SCT_ALLPAIRS_SCHEME")) {
-    const int f = atoi(v);
-    if (f == SCT_ALLPAIRS_SUBSETS) return f;
-    if (f == SCT_ALLPAIRS_MOMENTS && mom_supported(npp, n)) return f;
-    if (f == SCT_ALLPAIRS_SPECTRAL && spectral_supported(npp, n)) return f;
-  }
   if (spectral_supported(npp, n) && n >= spectral_min_n()) return SCT_ALLPAIRS_SPECTRAL;
   return mom_supported(npp, n) ? SCT_ALLPAIRS_MOMENTS : SCT_ALLPAIRS_SUBSETS;
 }
@@ -760,6 +751,7 @@ struct sct_allpairs_plan {
   int64_t mom_nwords = 0;
   int mom_nranges = 0;
   sct_spectral::State spec;  // SPECTRAL scheme (spectral.hip)
+  sct::LaunchTimer timer;    // bench aid (sct_allpairs_timing)
 };
 
 namespace {
@@ -777,6 +769,7 @@ struct CountKernels {
   using Fn = void (*)(const uint64_t*, const uint4*, int64_t, int64_t, int64_t, int64_t, int64_t,
                       int64_t, unsigned long long*, unsigned long long*);
   static Fn get(int variant, int scheme) {
+#ifdef SCT_ABLATION
     if constexpr (NPP == 8) {
       if (scheme == SCT_ALLPAIRS_MOMENTS) {
         switch (variant) {
@@ -784,29 +777,37 @@ struct CountKernels {
           case 3: return allpairs_count_kernel<NPP, 3, true>;
           case 4: return allpairs_count_kernel<NPP, 4, true>;
           case 5: return allpairs_count_kernel<NPP, 5, true>;
-#ifdef SCT_ABLATION
           case 11: return allpairs_count_kernel<NPP, 11, true>;
           case 12: return allpairs_count_kernel<NPP, 12, true>;
           case 13: return allpairs_count_kernel<NPP, 13, true>;
           case 14: return allpairs_count_kernel<NPP, 14, true>;
-#endif
           default: return allpairs_count_kernel<NPP, 2, true>;
         }
       }
       switch (variant) {
         case 1: return allpairs_count_kernel<NPP, 1, false>;
         case 3: return allpairs_count_kernel<NPP, 3, false>;
-#ifdef SCT_ABLATION
         case 11: return allpairs_count_kernel<NPP, 11, false>;
         case 12: return allpairs_count_kernel<NPP, 12, false>;
         case 13: return allpairs_count_kernel<NPP, 13, false>;
-#endif
         default: return allpairs_count_kernel<NPP, 2, false>;
       }
     } else {
       if (scheme == SCT_ALLPAIRS_MOMENTS) return nullptr;
       return variant == 1 ? allpairs_count_kernel<NPP, 1, false> : allpairs_count_kernel<NPP, 2, false>;
     }
+#else
+    // the shipped variants: MOMENTS unroll 1, SUBSETS at 16 bases full
+    // unroll, SUBSETS at other widths unroll 2
+    (void)variant;
+    if constexpr (NPP == 8) {
+      if (scheme == SCT_ALLPAIRS_MOMENTS) return allpairs_count_kernel<NPP, 1, true>;
+      return allpairs_count_kernel<NPP, 3, false>;
+    } else {
+      if (scheme == SCT_ALLPAIRS_MOMENTS) return nullptr;
+      return allpairs_count_kernel<NPP, 2, false>;
+    }
+#endif
   }
 };
 
@@ -824,9 +825,11 @@ int launch_count(sct_allpairs_plan* p, int64_t b, int64_t e, uint64_t* d_counts,
   if (p->flush_items > 0 && p->flush_items < flush) flush = p->flush_items;
   SCT_HIP(hipMemsetAsync(p->d_queue, 0, sizeof(unsigned long long), s));
   const uint64_t* codes = p->d_sorted ? p->d_sorted : p->d_codes;
+  hipEvent_t t0 = p->timer.start(s);
   hipLaunchKernelGGL(fn, dim3(grid), dim3(RB), 0, s, codes, p->d_table, p->n, p->nchunks, b, e,
                      p->grab, flush, p->d_queue, reinterpret_cast<unsigned long long*>(d_counts));
   SCT_LAUNCH_CHECK();
+  p->timer.stop(s, t0, sct::LaunchTimer::COUNT);
   return SCT_OK;
 }
 
@@ -975,9 +978,9 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
     // items = the 4096 transform slices; no selection table
     p->ncounts = sct_spectral::kNCounts;
     p->items = n >= 2 ? sct_spectral::kSlices : 0;
-    const char* c = getenv("SCT_SPECTRAL_CHUNK");
-    const int rc = sct_spectral::create(p->spec, p->d_codes, n, c ? atoll(c) : 65536, cus);
+    const int rc = sct_spectral::create(p->spec, p->d_codes, n, sct::tune(SCT_TUNE_SPECTRAL_CHUNK, 65536), cus);
     if (rc != SCT_OK) return cleanup(rc);
+    p->spec.timer = &p->timer;
     *plan = p;
     return SCT_OK;
   }
@@ -1030,22 +1033,19 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
   p->variant = p->scheme == SCT_ALLPAIRS_MOMENTS ? 1 : (p->npp == 8 ? 3 : 2);
   // MOMENTS: 32 items per pull halves the chunk re-staging (L2 -> LDS) at no cost in time
   if (p->scheme == SCT_ALLPAIRS_MOMENTS) p->grab = 32;
+#ifdef SCT_ABLATION
+  // timing-only build: count-kernel ablations 11..14 (wrong results by design)
   if (const char* v = getenv("SCT_ALLPAIRS_VARIANT")) {
     const int vv = atoi(v);
     if ((vv >= 1 && vv <= 3) || ((vv == 4 || vv == 5) && p->scheme == SCT_ALLPAIRS_MOMENTS) ||
         (vv >= 11 && vv <= 14))
       p->variant = vv;
   }
+#endif
   p->grid = grid_for(p->npp, cus, p->variant, p->scheme);
-  if (const char* f = getenv("SCT_ALLPAIRS_FLUSH_ITEMS")) p->flush_items = atoll(f);
-  if (const char* g = getenv("SCT_ALLPAIRS_GRAB")) {
-    const int gg = atoi(g);
-    if (gg > 0) p->grab = gg;
-  }
-  if (const char* g = getenv("SCT_ALLPAIRS_GRID")) {
-    const int gg = atoi(g);
-    if (gg > 0) p->grid = gg;
-  }
+  p->flush_items = sct::tune(SCT_TUNE_ALLPAIRS_FLUSH_ITEMS, 0);
+  if (const int64_t g = sct::tune(SCT_TUNE_ALLPAIRS_GRAB, 0); g > 0) p->grab = g;
+  if (const int64_t g = sct::tune(SCT_TUNE_ALLPAIRS_GRID, 0); g > 0) p->grid = (int)g;
   *plan = p;
   return SCT_OK;
 }
@@ -1148,6 +1148,7 @@ extern "C" int sct_allpairs_build_items(sct_allpairs_plan* plan, int64_t item_be
     c1 = 0;
   }
   const int64_t gp_per_chunk = plan->ct / 2;
+  hipEvent_t t0 = plan->timer.start(s);
   if (plan->scheme == SCT_ALLPAIRS_MOMENTS) {
     // every row block may be read: the whole (sorted) code list is needed
     size_t bytes = plan->sort_tmp_bytes;
@@ -1165,6 +1166,36 @@ extern "C" int sct_allpairs_build_items(sct_allpairs_plan* plan, int64_t item_be
                          s, plan->d_codes, plan->n, plan->npp, e0, e1, plan->d_table);
   }
   SCT_LAUNCH_CHECK();
+  plan->timer.stop(s, t0, sct::LaunchTimer::BUILD);
+  return SCT_OK;
+}
+
+extern "C" int sct_allpairs_spectral_info(const sct_allpairs_plan* plan, int* elem_bytes, int64_t* chunk_slices,
+                                          int* max_column) {
+  SCT_CHECK(plan != nullptr, "plan is NULL");
+  SCT_CHECK(plan->scheme == SCT_ALLPAIRS_SPECTRAL, "not a SPECTRAL plan");
+  if (elem_bytes) *elem_bytes = plan->spec.elem_bytes;
+  if (chunk_slices) *chunk_slices = plan->spec.chunk;
+  if (max_column) *max_column = (int)plan->spec.max_m;
+  return SCT_OK;
+}
+
+extern "C" int sct_allpairs_timing(sct_allpairs_plan* plan, int mode, double* out) {
+  SCT_CHECK(plan != nullptr, "plan is NULL");
+  SCT_CHECK(mode >= 0 && mode <= 2, "mode %d: 0 stop, 1 start, 2 read", mode);
+  sct::LaunchTimer& t = plan->timer;
+  if (mode == 1) {
+    t.reset();
+    t.on = true;
+  } else {
+    t.collect();
+    if (mode == 0) t.on = false;
+  }
+  if (out)
+    for (int k = 0; k < sct::LaunchTimer::NKINDS; ++k) {
+      out[2 * k] = t.ms[k];
+      out[2 * k + 1] = (double)t.launches[k];
+    }
   return SCT_OK;
 }
 

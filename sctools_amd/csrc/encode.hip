@@ -548,12 +548,15 @@ namespace {
 enum : uint32_t { OP_ENCODE = 1, OP_DECODE2 = 2, OP_DECODE3 = 3, OP_GC = 4, OP_HAMMING = 5 };
 constexpr int kSrvIn = 1024, kSrvOut = 1024, kSrvMaxN = 64;
 
-constexpr int kSrvInline = 32;  // payload bytes that ride in the request line itself
+constexpr int kSrvInline = 28;  // payload bytes that ride in the request line itself
 
 // One request line of 64 B: req[0] = seq (written last), req[1..7] = the packed fields,
-// req[8..15] = the first 32 payload bytes; the rest of the payload follows contiguously in
-// `more`.  The wave reads the whole line with one 64-B load per poll, so a scalar call
-// (payload <= 32 B: a pair of one-limb codes, a 32-base record) costs one PCIe read.
+// req[8..14] = the first 28 payload bytes, req[15] = line_check(req[0..14]); payload bytes
+// 28.. follow in `more`.  The wave reads the whole line with one 64-B load
+// per poll, so a scalar call (payload <= 28 B: a pair of one-limb codes, a 28-base record)
+// costs one PCIe read.  Nothing guarantees that the 16 dwords of one poll are one snapshot,
+// so the wave takes a new sequence number only with a matching check word: a line mixing
+// this request's seq with the previous request's fields is not accepted, only polled again.
 struct SrvMailbox {
   alignas(64) uint32_t req[16];
   uint32_t more[(kSrvIn - kSrvInline) / 4];
@@ -579,7 +582,7 @@ __host__ __device__ inline uint32_t line_check(const uint32_t* w) {
   }
   return h;
 }
-static_assert(offsetof(SrvMailbox, more) == 64, "payload must continue the request line");
+static_assert(offsetof(SrvMailbox, more) == 64, "the payload continues after the request line");
 
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -605,7 +608,14 @@ __global__ __launch_bounds__(64) void scalar_server_kernel(SrvMailbox* mb, uint3
   for (uint32_t it = 1;; ++it) {
     const uint32_t ahead = lane < 16 ? sys_load(&mb->req[lane]) : 0u;
     const uint32_t seq = __builtin_amdgcn_readlane(line, 0);
-    if (seq != served) {
+    bool arrived = seq != served;
+    if (arrived) {
+      uint32_t w[15];
+#pragma unroll
+      for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_readlane(line, k);
+      arrived = line_check(w) == __builtin_amdgcn_readlane(line, 15);
+    }
+    if (arrived) {
       const uint32_t h1 = __builtin_amdgcn_readlane(line, 1), h2 = __builtin_amdgcn_readlane(line, 2),
                      h3 = __builtin_amdgcn_readlane(line, 3), h4 = __builtin_amdgcn_readlane(line, 4),
                      h5 = __builtin_amdgcn_readlane(line, 5), h6 = __builtin_amdgcn_readlane(line, 6),
@@ -618,8 +628,8 @@ __global__ __launch_bounds__(64) void scalar_server_kernel(SrvMailbox* mb, uint3
       const int in_words = ((int)(h4 & 0xFFFFu) + 3) / 4, out_words = ((int)(h4 >> 16) + 3) / 4;
       const int io[2] = {off16(h5 & 0xFFFFu), off16(h5 >> 16)};
       const int oo[3] = {off16(h6 & 0xFFFFu), off16(h6 >> 16), off16(h7 & 0xFFFFu)};
-      // payload: the first 8 dwords came with the line; the rest (if any) in one more round trip
-      if (lane >= 8 && lane < 16 && lane - 8 < in_words) in_l[lane - 8] = line;
+      // payload: the first 7 dwords came with the line; the rest (if any) in one more round trip
+      if (lane >= 8 && lane < 15 && lane - 8 < in_words) in_l[lane - 8] = line;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       for (int k = kSrvInline / 4 + lane; k < in_words; k += 64) in_l[k] = sys_load(&mb->more[k - kSrvInline / 4]);
       for (int k = lane; k < out_words; k += 64) out_l[k] = 0u;
@@ -726,17 +736,39 @@ void stop_all_at_exit() {
   for (Server* sv : g_servers) server_stop(sv, 200000);
 }
 
-bool server_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("SCT_SCALAR_SERVER");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+bool server_enabled() { return sct::tune(SCT_TUNE_SCALAR_SERVER, 1) != 0; }
+
+// A host thread's servers (one per device).  When the thread ends its servers are stopped
+// and their stream and mailbox freed, so thread churn does not pile up resident waves,
+// streams and pinned memory; a server that does not confirm its exit is left alone (its
+// mailbox must outlive it).
+struct ThreadServers {
+  Server* per_dev[64] = {};
+  ~ThreadServers() {
+    for (Server*& sv : per_dev) {
+      if (!sv) continue;
+      std::lock_guard<std::mutex> g(g_srv_mu);
+      server_stop(sv, 1000000);
+      if (server_running(sv)) continue;
+      g_servers.erase(std::remove(g_servers.begin(), g_servers.end(), sv), g_servers.end());
+      int cur = -1;
+      if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(sv->device) == hipSuccess) {
+        (void)hipStreamSynchronize(sv->stream);
+        (void)hipStreamDestroy(sv->stream);
+        (void)hipHostFree(sv->mb);
+        (void)hipSetDevice(cur);
+      }
+      (void)hipGetLastError();
+      delete sv;
+      sv = nullptr;
+    }
+  }
+};
 
 // nullptr (error set) if the server cannot be created; callers then take the launch path
 Server* server() {
-  static thread_local Server* per_dev[64] = {};
+  static thread_local ThreadServers mine;
+  Server** per_dev = mine.per_dev;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   if (per_dev[dev]) return per_dev[dev];
@@ -744,9 +776,8 @@ Server* server() {
   sv->device = dev;
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
-  const char* e = getenv("SCT_SCALAR_IDLE_MS");
-  const double ms = e ? atof(e) : 5.0;
-  sv->idle_ticks = (uint64_t)(khz * (ms > 0 ? ms : 5.0));
+  const int64_t ms = sct::tune(SCT_TUNE_SCALAR_IDLE_MS, 5);
+  sv->idle_ticks = (uint64_t)khz * (uint64_t)(ms > 0 ? ms : 5);
   if (hipStreamCreateWithFlags(&sv->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&sv->mb, sizeof(SrvMailbox), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void**)&sv->mb_dev, sv->mb, 0) != hipSuccess) {
@@ -806,9 +837,13 @@ int srv_call(uint32_t op, int kind, int64_t n, int words, int L, int64_t stride,
   Server* sv = server();
   if (!sv) return 1;
   SrvMailbox* mb = sv->mb;
-  uint8_t* pay = reinterpret_cast<uint8_t*>(&mb->req[kSrvInline / 4]);
-  for (int k = 0; k < NI; ++k)
-    if (ins[k].bytes) memcpy(pay + io[k], ins[k].p, ins[k].bytes);
+  {  // payload bytes [0, 28) into req[8..14], the rest into `more`
+    uint8_t pay[kSrvIn];
+    for (int k = 0; k < NI; ++k)
+      if (ins[k].bytes) memcpy(pay + io[k], ins[k].p, ins[k].bytes);
+    memcpy(&mb->req[8], pay, std::min<size_t>(tin, kSrvInline));
+    if (tin > (size_t)kSrvInline) memcpy(mb->more, pay + kSrvInline, tin - kSrvInline);
+  }
   auto o16 = [](int32_t v) { return v < 0 ? 0xFFFFu : (uint32_t)v; };
   mb->req[1] = op | (uint32_t)kind << 8 | (uint32_t)words << 16;
   mb->req[2] = (uint32_t)n | (uint32_t)L << 16;
@@ -818,6 +853,12 @@ int srv_call(uint32_t op, int kind, int64_t n, int words, int L, int64_t stride,
   mb->req[6] = o16(oo[0]) | o16(oo[1]) << 16;
   mb->req[7] = o16(oo[2]);
   const uint32_t seq = ++sv->seq;
+  {
+    uint32_t w[15];
+    w[0] = seq;
+    for (int k = 1; k < 15; ++k) w[k] = mb->req[k];
+    mb->req[15] = line_check(w);
+  }
   __atomic_store_n(&mb->req[0], seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
   uint32_t line[16];

@@ -3,6 +3,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <atomic>
 #include <utility>
 
 #include "sct_common.h"
@@ -66,7 +67,31 @@ int stage_reserve(HostStage* st, size_t pinned_bytes, size_t dev_bytes) {
   return SCT_OK;
 }
 
+// Launch-shape knobs (sct_tune_set), stored as value + 1 (0 = unset: zero-initialised
+// before any constructor runs).  The library reads no environment variable; nothing here
+// changes a result.
+static std::atomic<int64_t> g_tune[SCT_TUNE_NKEYS];
+
+int64_t tune(int key, int64_t dflt) {
+  if (key <= 0 || key >= SCT_TUNE_NKEYS) return dflt;
+  const int64_t v = g_tune[key].load(std::memory_order_relaxed);
+  return v == 0 ? dflt : v - 1;
+}
+
 }  // namespace sct
+
+extern "C" int sct_tune_set(int key, int64_t value) {
+  SCT_CHECK(key > 0 && key < SCT_TUNE_NKEYS, "unknown tuning key %d", key);
+  sct::g_tune[key].store(value < 0 ? 0 : value + 1);
+  return SCT_OK;
+}
+
+extern "C" int sct_tune_get(int key, int64_t* value) {
+  SCT_CHECK(key > 0 && key < SCT_TUNE_NKEYS, "unknown tuning key %d", key);
+  SCT_CHECK(value != nullptr, "value is NULL");
+  *value = sct::tune(key, -1);
+  return SCT_OK;
+}
 
 extern "C" int sct_version(void) { return 1; }
 

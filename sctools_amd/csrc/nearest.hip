@@ -400,7 +400,7 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
   // Open addressing when the multi-index keys are nearly unique for random codes: s = 1 block
   // per key for max_d = 0 (the whole code), s = 2 (pairs of P = max_d + 2 blocks) for max_d 1..2,
   // if every key spans enough bases that 4^bases >= nw / 2, i.e. at most ~2 random codes share
-  // a key (SCT_NEAREST_SCHEME=csr / oa forces one).
+  // a key (sct_tune_set(SCT_TUNE_NEAREST_SCHEME, 1 / 2) forces open addressing / CSR).
   {
     const int P = max_d == 0 ? 1 : max_d + 2;
     const int sz = max_d == 0 ? 1 : 2;
@@ -408,10 +408,9 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
     int min_bases = G;  // the smallest key: two smallest blocks of a floor split
     if (sz == 2) min_bases = 2 * (G / P);
     bool oa = P <= G && nkeys <= MAX_KEYS && 2.0 * min_bases >= std::log2(0.5 * std::max<int64_t>(nw, 2));
-    if (const char* v = getenv("SCT_NEAREST_SCHEME")) {
-      if (!strcmp(v, "csr")) oa = false;
-      if (!strcmp(v, "oa")) oa = P <= G && nkeys <= MAX_KEYS;
-    }
+    const int64_t forced = sct::tune(SCT_TUNE_NEAREST_SCHEME, 0);
+    if (forced == 2) oa = false;
+    if (forced == 1) oa = P <= G && nkeys <= MAX_KEYS;
     if (oa) {
       uint64_t bmask[MAX_KEYS + 2] = {};
       for (int b = 0; b < P; ++b) {
@@ -443,13 +442,12 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
   }
   // Bucket count per part: a provisional table of ~nw/2 buckets counts the occupied ones
   // (~ the distinct block values: 4^8 = 65,536 for an 8-base ThreeBit block of a 737K
-  // whitelist, nw itself for max_d = 0), then the part gets ~SCT_NEAREST_LOAD (4) buckets per
+  // whitelist, nw itself for max_d = 0), then the part gets ~SCT_TUNE_NEAREST_LOAD (4) buckets per
   // distinct value, never more than the provisional count: the offset tables stay small
   // enough to live in each XCD's L2 while colliding block values add few extra entries.
   int lg0 = 0;
   while (lg0 < 28 && (1LL << lg0) * 2 < nw) ++lg0;
-  int load = 4;
-  if (const char* v = getenv("SCT_NEAREST_LOAD")) load = std::max(1, atoi(v));
+  const int load = (int)std::max<int64_t>(1, sct::tune(SCT_TUNE_NEAREST_LOAD, 4));
   for (int k = 0; k < p->nparts; ++k) {
     const int pos_lo = G * k / p->nparts, pos_hi = G * (k + 1) / p->nparts;
     Part& pt = p->parts.p[k];
@@ -515,6 +513,19 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
   }
   SCT_HIP(hipStreamSynchronize(s));  // the scratch buffers die with this call
   *out = p;
+  return SCT_OK;
+}
+
+extern "C" int sct_nearest_plan_info(const sct_nearest_plan* p, int* scheme, int64_t* index_bytes) {
+  SCT_CHECK(p != nullptr, "plan is NULL");
+  int64_t bytes = 0;
+  if (p->nkeys > 0) {
+    for (int k = 0; k < p->nkeys; ++k) bytes += (int64_t)(p->ot.t[k].gmask + 1) * kGroup * 16;
+  } else {
+    for (int k = 0; k < p->nparts; ++k) bytes += (p->nbuckets[k] + 1) * 4 + p->nw * 12;
+  }
+  if (scheme) *scheme = p->nkeys > 0 ? SCT_NEAREST_OA : SCT_NEAREST_CSR;
+  if (index_bytes) *index_bytes = bytes;
   return SCT_OK;
 }
 

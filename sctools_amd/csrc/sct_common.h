@@ -6,6 +6,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <vector>
+
 #include "../../include/sctools_hip.h"
 
 namespace sct {
@@ -59,10 +61,78 @@ constexpr size_t kZeroCopyBytes = 64 << 10;
 // it the caller's arrays are copied through per-call device allocations.
 constexpr size_t kStageBytes = 256ull << 20;
 
+// sct_tune_set value of `key`, or dflt when unset (host.cpp).
+int64_t tune(int key, int64_t dflt);
+
 // Stop the resident scalar servers (encode.hip) before a launch whose grid is sized to the
 // resident workgroups, so none of its workgroups waits behind a server wave's registers.
 // Cheap when no server runs.
 void scalar_quiesce();
+
+// Bench aid: per-launch HIP-event timing of a plan's kernels on the stream each launch runs on
+// (sct_allpairs_timing).  Off by default; when on, start() records an event before a launch
+// and stop() one after it, and collect() waits for the recorded pairs and sums their spans
+// per kind.  Events are pooled, so a timed run allocates nothing after its first steps.
+struct LaunchTimer {
+  enum Kind { SEED = 0, TILE = 1, COUNT = 2, BUILD = 3, NKINDS = 4 };
+  bool on = false;
+  double ms[NKINDS] = {};
+  int64_t launches[NKINDS] = {};
+  struct Rec {
+    hipEvent_t a, b;
+    int kind;
+  };
+  std::vector<Rec> pending;
+  std::vector<hipEvent_t> pool;
+
+  hipEvent_t take() {
+    hipEvent_t e = nullptr;
+    if (!pool.empty()) {
+      e = pool.back();
+      pool.pop_back();
+    } else if (hipEventCreate(&e) != hipSuccess) {
+      e = nullptr;
+    }
+    return e;
+  }
+  hipEvent_t start(hipStream_t s) {
+    if (!on) return nullptr;
+    hipEvent_t a = take();
+    if (a) (void)hipEventRecord(a, s);
+    return a;
+  }
+  void stop(hipStream_t s, hipEvent_t a, int kind) {
+    if (!on || !a) return;
+    hipEvent_t b = take();
+    if (!b) return;
+    (void)hipEventRecord(b, s);
+    pending.push_back(Rec{a, b, kind});
+  }
+  void collect() {
+    for (const Rec& r : pending) {
+      float t = 0;
+      if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+        ms[r.kind] += t;
+        launches[r.kind] += 1;
+      }
+      pool.push_back(r.a);
+      pool.push_back(r.b);
+    }
+    pending.clear();
+  }
+  void reset() {
+    collect();
+    for (auto& v : ms) v = 0;
+    for (auto& v : launches) v = 0;
+  }
+  ~LaunchTimer() {
+    for (const Rec& r : pending) {
+      (void)hipEventDestroy(r.a);
+      (void)hipEventDestroy(r.b);
+    }
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+  }
+};
 
 // Moment-assisted all-pairs scheme (SCT_ALLPAIRS_MOMENTS, 16-base TwoBit codes):
 // the count kernel accumulates only these 13 subset products of the distance bits

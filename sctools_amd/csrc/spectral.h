@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sct_common.h"
+
 namespace sct_spectral {
 
 constexpr int kSpaceBits = 32;                 // 16 bases: codes are points of Z_2^32
@@ -24,24 +26,12 @@ struct State {
   uint32_t* d_planes = nullptr;  // [groups][18] bit planes of the groups' code >> 14
   int64_t max_groups = 0;
   int elem_bytes = 1;            // seed -> tile intermediate: int8 / int16 / int32
-  bool mfma = true;              // int8 seeds: first 6 butterfly levels on the matrix cores
   uint16_t* d_order = nullptr;   // [2^17]: at [L, 2L) the offsets [0, L) sorted by digit weight
-  int tile_wgs = 2;              // resident MFMA-tile workgroups per CU
-  int tile_reg = 0;              // int8 seeds: the register-resident tile (one wave per slice), variant
-  int tile_reg_wgs = 2;          // its resident workgroups per CU
-  bool seed_db = false;          // int8 walk seed: double-buffered byte stage
-  bool seed_spread = false;      // int8 seeds: stores spread over the walk (16-slice blocks)
-  void* d_mx = nullptr;          // int8 seeds: the MFMA seed's operand tables (null: the walk seed)
-  int mx_form = 2;               // the MFMA seed's workgroup shape (A/B)
-  int ilv = 0;                   // int8: the direct MFMA seed + G-slice interleaved intermediate (G)
-  // seed / tile overlap: chunk j+1's seed (side stream, second buffer) runs beside chunk j's tile
-  bool overlap = false;
-  void* d_buf2 = nullptr;
-  hipStream_t side = nullptr;
-  hipEvent_t ev[5] = {};         // [0, 1] tile done with buffer 0 / 1, [2, 3] seed done, [4] start
+  int tile_wgs = 2;              // resident register-tile workgroups per CU
   void* d_buf = nullptr;         // chunk slices x 2^14 seed values
   int64_t chunk = 0;             // slices per pass
   int grid = 0;                  // compute units (the tile kernel's persistent grid)
+  sct::LaunchTimer* timer = nullptr;  // the plan's (bench aid), not owned
 };
 
 // allocate (chunk = slices held in HBM at once) and size the intermediate from the

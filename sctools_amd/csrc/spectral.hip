@@ -12,8 +12,9 @@
 //          column's codes: a Gray-code walk over 64 slices costs one XOR and one
 //          popcount per 32 codes per value.  |seed| <= codes in the column, so the
 //          values go to HBM as int8 (int16 / int32 for denser columns): 16 KB per slice
-//   tile   reads a slice back, butterflies over the 14 column bits (registers + LDS),
-//          F^2 binned by digit weight; writes nothing
+//   tile   reads a slice back, transforms it over the 14 column bits (int8 seeds: two
+//          64-point stages on the matrix cores + Parseval for the top digit), F^2 binned
+//          by digit weight; writes nothing
 // 8 GB of HBM traffic per job at int8, whatever n is.  Exact: |F| <= n < 2^31 in int32,
 // F^2 and S_w in uint64 (S_w <= 2^32 sum f^2).
 #include <string.h>
@@ -21,7 +22,6 @@
 #include <algorithm>
 #include <vector>
 #include <type_traits>
-
 
 #include "sct_common.h"
 #include "spectral.h"
@@ -36,9 +36,6 @@ constexpr int kWalkBits = 6;
 constexpr int kRegGroups = 2;             // seed: 32-code groups whose planes stay in registers
 constexpr int kSeedWalks = 16;            // seed: walks per workgroup (8: +5 %, 32: +5 % per launch)
 constexpr int kMaxOrder = 1 << 16;        // largest slice range with a digit-weight order table
-// MFMA tile: load the next slice while transforming this one.  Measured no faster (the
-// kernel is not waiting on HBM) and it costs 16 VGPRs: off.
-constexpr bool kTilePrefetch = false;
 
 // non-zero 2-bit digits of z
 __device__ __forceinline__ int digit_weight(uint32_t z) {
@@ -293,13 +290,6 @@ __device__ __forceinline__ int column_pos(int c) {
          ((c >> 12) << 12);
 }
 
-// The G-slice interleaved int8 layout (direct MFMA seed + ILV register tile), G = 4, 8, 16:
-// slice-relative index zr and 16-column block b; the 16-B chunks of G consecutive slices of one
-// block are contiguous (16 G bytes).  A group of G slices is G x 16 KB.
-template <int G>
-__device__ __forceinline__ size_t ilv_off(int zr, int b) {
-  return ((size_t)(zr / G) * (kLo / 16) + b) * (16 * G) + (zr % G) * 16;
-}
 
 // Byte (int8) / half (int16) transposes for the seed's store-out: p dwords hold P values of
 // consecutive slices for one column each; out[j] = the j-th values of all of them, packed.
@@ -315,25 +305,21 @@ __device__ __forceinline__ void transpose4x4_bytes(const uint32_t* d, uint32_t* 
   out[3] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
 }
 
+
 // buf[(z - z0) 2^14 + pos(c)] = sum over codes x of column c of (-1)^popc((x >> 14) & z)
 //                             = m(c) - 2 sum over groups of popc(XOR of the planes of z's bits).
-// A workgroup owns 256 columns and one 64-slice walk: each lane walks its column in Gray
-// order (one XOR per step from registers); the 64 x 256 values are staged in LDS as dwords
-// of 4 / sizeof(T) consecutive slices per column, transposed in registers and written as
-// 16-B chunks of slice rows.
-// ABL (ablation builds only, wrong results by design): 1 = no global stores, 2 = no
-// Gray walk (one group, no planes), 3 = no LDS staging/transposes.
-// DB: the int8 byte stage double-buffered (walk i + 1 writes the other buffer while walk i's
-// store-out may still read this one): one workgroup barrier per walk instead of two.
-template <typename T, int ABL, int kRegG, int NT = 256, bool DB = false>
-__device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
-                                                   const uint32_t* __restrict__ gofs,
-                                                   const uint32_t* __restrict__ off, int64_t max_groups,
-                                                   int z0, int z1, T* __restrict__ buf) {
+// A workgroup owns 256 columns and walks of 64 slices (blockIdx.y, strided): each lane walks
+// its column in Gray order (one XOR per step from registers).  int8: the raw popcount sums
+// are staged in LDS as bytes (row = slice, byte = column) and each thread forms m - 2 acc for
+// 16 columns of a slice row at once; int16 / int32: dwords of 4 / sizeof(T) consecutive
+// slices per column, transposed in registers; both written as 16-B chunks of slice rows.
+template <typename T>
+__device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes, const uint32_t* __restrict__ gofs,
+                                          const uint32_t* __restrict__ off, int z0, int z1, T* __restrict__ buf) {
+  constexpr int NT = 256;
   constexpr int P = 4 / sizeof(T);          // slices per staged dword
   constexpr int V = Chunk<T>::kVals;        // columns per 16-B output chunk
-  __shared__ uint32_t stage[(DB ? 2 : 1) * (kWalk / P) * NT];
-  int it = 0;  // this workgroup's walk count (DB: which buffer)
+  __shared__ uint32_t stage[(kWalk / P) * NT];
   const int tid = threadIdx.x;
   const int c0 = blockIdx.x * NT, c = c0 + tid;
   const int m = (int)(off[c + 1] - off[c]);
@@ -342,21 +328,19 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
   int wng = ng;
 #pragma unroll
   for (int s = 32; s; s >>= 1) wng = max(wng, __shfl_xor(wng, s));
-  // the first kRegG groups' planes stay in registers for all of this workgroup's walks
-  uint32_t pr[kRegG][kHiBits];
+  // the first kRegGroups groups' planes stay in registers for all of this workgroup's walks
+  uint32_t pr[kRegGroups][kHiBits];
 #pragma unroll
-  for (int g = 0; g < kRegG; ++g)
+  for (int g = 0; g < kRegGroups; ++g)
     if (g < ng) {
       load_planes(planes, (int64_t)g0 + g, pr[g]);
     } else {
 #pragma unroll
       for (int k = 0; k < kHiBits; ++k) pr[g][k] = 0u;
     }
-  // int8 byte store-out: this thread writes columns c0 + mcb .. + 15; mx = their m | 0x80
-  // as bytes (ABL 4 = the same path, for A/B against the ablations)
-  constexpr bool kByteStage = sizeof(T) == 1 && (ABL == 0 || ABL == 4 || ABL == 6 || ABL == 7 || (ABL >= 8 && ABL <= 10));
-  // ABL 6: each wave stages and stores its own 64 columns (no workgroup barrier)
-  const int mcb = ABL == 6 ? 64 * (tid >> 6) + 16 * (tid & 3) : (tid % (NT / 16)) * 16;
+  // int8 byte store-out: this thread writes columns c0 + mcb .. + 15; mx = their m | 0x80 as bytes
+  constexpr bool kByteStage = sizeof(T) == 1;
+  const int mcb = (tid % (NT / 16)) * 16;
   uint4 mx = make_uint4(0, 0, 0, 0);
   if constexpr (kByteStage) {
     uint32_t w[4];
@@ -373,43 +357,37 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
   }
   // Co-resident workgroups start together and run identical walks, so they stay in
   // lockstep: all 12 waves of a CU walk (VALU-bound) and then all store (HBM-bound).
-  // Starting them 0 / 1,536 / 3,072 cycles apart (about 1/6 and 1/3 of a walk) lets one
-  // workgroup's stores drain under another's walk: 0.35 -> 0.32-0.33 ms per launch
-  // (ABL 9 / 10: 2x / 4x the offset, smaller gains).
-  if constexpr (ABL == 0 || (ABL >= 8 && ABL <= 10)) {
-    constexpr int kS = ABL == 9 ? 48 : (ABL == 10 ? 96 : 24);
+  // Starting them 0 / 1,536 / 3,072 cycles apart lets one workgroup's stores drain under
+  // another's walk (What was tried (14)).
+  {
     const int ph = (blockIdx.x + blockIdx.y) % 3;
-    if (ph >= 1) __builtin_amdgcn_s_sleep(kS);
-    if (ph == 2) __builtin_amdgcn_s_sleep(kS);
+    if (ph >= 1) __builtin_amdgcn_s_sleep(24);
+    if (ph == 2) __builtin_amdgcn_s_sleep(24);
   }
   const int za = z0 & ~(kWalk - 1);
   const int nwalks = (z1 - za + kWalk - 1) / kWalk;
   for (int wk = blockIdx.y; wk < nwalks; wk += gridDim.y) {
-  const int zblk = za + wk * kWalk;
-  int acc[kWalk];
-  auto walk = [&](const uint32_t* p, auto first) {
-    uint32_t x = 0;
+    const int zblk = za + wk * kWalk;
+    int acc[kWalk];
+    auto walk = [&](const uint32_t* p, auto first) {
+      uint32_t x = 0;
 #pragma unroll
-    for (int k = kWalkBits; k < kHiBits; ++k)
-      if ((zblk >> k) & 1) x ^= p[k];
-    if constexpr (decltype(first)::value) acc[0] = __popc(x);
-    else acc[0] += __popc(x);
+      for (int k = kWalkBits; k < kHiBits; ++k)
+        if ((zblk >> k) & 1) x ^= p[k];
+      if constexpr (decltype(first)::value) acc[0] = __popc(x);
+      else acc[0] += __popc(x);
 #pragma unroll
-    for (int i = 1; i < kWalk; ++i) {
-      x ^= p[ctz_c(i)];
-      if constexpr (decltype(first)::value) acc[gray(i)] = __popc(x);
-      else acc[gray(i)] += __popc(x);
-    }
-  };
-  if constexpr (ABL == 2) {
-#pragma unroll
-    for (int i = 0; i < kWalk; ++i) acc[i] = (i * 5 + tid) & 31;
-  } else {
+      for (int i = 1; i < kWalk; ++i) {
+        x ^= p[ctz_c(i)];
+        if constexpr (decltype(first)::value) acc[gray(i)] = __popc(x);
+        else acc[gray(i)] += __popc(x);
+      }
+    };
     walk(pr[0], std::true_type());  // columns without codes: planes 0, popc 0
 #pragma unroll
-    for (int g = 1; g < kRegG; ++g)
+    for (int g = 1; g < kRegGroups; ++g)
       if (g < wng) walk(pr[g], std::false_type());
-    for (int g = kRegG; g < wng; ++g) {  // dense columns: the rest from L2
+    for (int g = kRegGroups; g < wng; ++g) {  // dense columns: the rest from L2
       uint32_t p[kHiBits];
       if (g < ng) {
         load_planes(planes, (int64_t)g0 + g, p);
@@ -419,286 +397,98 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes,
       }
       walk(p, std::false_type());
     }
-  }
-  if constexpr (ABL == 3) {
-    const int z = zblk + (tid & 63);
-    uint32_t w = 0;
+    if constexpr (kByteStage) {
+      // int8: the raw popcount sums go to LDS as bytes (row = slice, byte = column; no
+      // packing), and the store-out forms m - 2 acc for 16 columns at once:
+      //   ((m | 0x80) - 2 acc) ^ 0x80 per byte -- acc <= m <= 127, so 2 acc fits a byte
+      //   and m + 128 - 2 acc lies in [1, 255]: no carry or borrow crosses a byte.
+      uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
+      __syncthreads();  // the previous walk's store-out reads of `stage` are done
 #pragma unroll
-    for (int i = 0; i < kWalk; ++i) w += (uint32_t)acc[i] << (i & 7);
-    if (z >= z0 && z < z1)
-      reinterpret_cast<uint32_t*>(buf + (int64_t)(z - z0) * kLo + c0)[tid >> 6] = w;
-    continue;
-  }
-  if constexpr (kByteStage) {
-    // int8: the raw popcount sums go to LDS as bytes (row = slice, byte = column; no
-    // packing), and the store-out forms m - 2 acc for 16 columns at once:
-    //   ((m | 0x80) - 2 acc) ^ 0x80 per byte -- acc <= m <= 127, so 2 acc fits a byte
-    //   and m + 128 - 2 acc lies in [1, 255]: no carry or borrow crosses a byte.
-    uint8_t* st8 = reinterpret_cast<uint8_t*>(stage) + (DB ? (it++ & 1) * (kWalk * NT) : 0);
-    if constexpr (ABL == 6) {
-      uint8_t* w8 = st8 + 4096 * (tid >> 6);  // this wave's 64 slices x 64 columns
-      const int lane = tid & 63;
-      // the previous walk's reads of w8 are this wave's own, issued earlier: LDS keeps order
+      for (int i = 0; i < kWalk; ++i) st8[i * NT + tid] = (uint8_t)acc[i];
+      __syncthreads();
+      if (zblk >= z0 && zblk + kWalk <= z1) {  // the whole walk is in range: all loads, then all stores
+        uint4 v[kWalk / 16];
 #pragma unroll
-      for (int i = 0; i < kWalk; ++i) w8[i * 64 + lane] = (uint8_t)acc[i];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int r = 0; r < kWalk / 16; ++r)
+          v[r] = *reinterpret_cast<const uint4*>(st8 + (tid / (NT / 16) + 16 * r) * NT + mcb);
+#pragma unroll
+        for (int r = 0; r < kWalk / 16; ++r) {
+          const uint4 o = make_uint4((mx.x - (v[r].x + v[r].x)) ^ 0x80808080u, (mx.y - (v[r].y + v[r].y)) ^ 0x80808080u,
+                                     (mx.z - (v[r].z + v[r].z)) ^ 0x80808080u, (mx.w - (v[r].w + v[r].w)) ^ 0x80808080u);
+          const int z = zblk + tid / (NT / 16) + 16 * r;
+          *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + mcb)) = o;
+        }
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < kWalk / 16; ++r) {
-        const int row = (lane >> 2) + 16 * r;
-        const uint4 v = *reinterpret_cast<const uint4*>(w8 + row * 64 + 16 * (lane & 3));
+        const int row = tid / (NT / 16) + 16 * r;
+        const uint4 v = *reinterpret_cast<const uint4*>(st8 + row * NT + mcb);
         const uint4 o = make_uint4((mx.x - (v.x + v.x)) ^ 0x80808080u, (mx.y - (v.y + v.y)) ^ 0x80808080u,
                                    (mx.z - (v.z + v.z)) ^ 0x80808080u, (mx.w - (v.w + v.w)) ^ 0x80808080u);
         const int z = zblk + row;
         if (z >= z0 && z < z1)
           *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + mcb)) = o;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
       continue;
-    }
-    // the previous walk's store-out reads of this buffer are done (DB: the barrier after the
-    // previous walk's writes already ordered the reads of two walks ago, the last ones of it)
-    if constexpr (!DB) __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kWalk; ++i) st8[i * NT + tid] = (uint8_t)acc[i];
-    __syncthreads();
-    if (zblk >= z0 && zblk + kWalk <= z1) {  // the whole walk is in range: all loads, then all stores
-      uint4 v[kWalk / 16];
-#pragma unroll
-      for (int r = 0; r < kWalk / 16; ++r)
-        v[r] = *reinterpret_cast<const uint4*>(st8 + (tid / (NT / 16) + 16 * r) * NT + mcb);
-#pragma unroll
-      for (int r = 0; r < kWalk / 16; ++r) {
-        const uint4 o = make_uint4((mx.x - (v[r].x + v[r].x)) ^ 0x80808080u, (mx.y - (v[r].y + v[r].y)) ^ 0x80808080u,
-                                   (mx.z - (v[r].z + v[r].z)) ^ 0x80808080u, (mx.w - (v[r].w + v[r].w)) ^ 0x80808080u);
-        const int z = zblk + tid / (NT / 16) + 16 * r;
-        *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + mcb)) = o;
-      }
-      continue;
-    }
-#pragma unroll
-    for (int r = 0; r < kWalk / 16; ++r) {
-      const int row = tid / (NT / 16) + 16 * r;
-      const uint4 v = *reinterpret_cast<const uint4*>(st8 + row * NT + mcb);
-      const uint4 o = make_uint4((mx.x - (v.x + v.x)) ^ 0x80808080u, (mx.y - (v.y + v.y)) ^ 0x80808080u,
-                                 (mx.z - (v.z + v.z)) ^ 0x80808080u, (mx.w - (v.w + v.w)) ^ 0x80808080u);
-      const int z = zblk + row;
-      if (z >= z0 && z < z1)
-        *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + mcb)) = o;
-    }
-    continue;
-  }
-  __syncthreads();  // the previous walk's store-out reads of `stage` are done
-  // 4-dword groups of a 16-dword column block XOR-swizzled by the block, so the
-  // store-out's b128 reads of 16 consecutive columns are conflict-free
-  auto sidx = [](int row, int col) { return row * 256 + (col ^ (((col >> 6) & 3) << 2)); };
-#pragma unroll
-  for (int r = 0; r < kWalk / P; ++r) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int j = 0; j < P; ++j)
-      w |= ((uint32_t)(m - 2 * acc[r * P + j]) & (0xFFFFFFFFu >> (32 - 8 * sizeof(T)))) << (8 * sizeof(T) * j);
-    stage[sidx(r, tid)] = w;
-  }
-  __syncthreads();
-  // blocks of V columns x P slices: V dwords in, P chunks out
-  constexpr int kBlocks = (kWalk / P) * (256 / V);
-#pragma unroll
-  for (int r = 0; r < kBlocks / 256; ++r) {
-    const int b = tid + 256 * r, row = b / (256 / V), cb = (b % (256 / V)) * V;
-    uint32_t d[V];
-#pragma unroll
-    for (int k = 0; k < V; k += 4) {
-      const uint4 v = *reinterpret_cast<const uint4*>(stage + sidx(row, cb + k));
-      d[k] = v.x;
-      d[k + 1] = v.y;
-      d[k + 2] = v.z;
-      d[k + 3] = v.w;
-    }
-    uint32_t out[P][4];
-    if constexpr (P == 4) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint32_t t[4];
-        transpose4x4_bytes(d + 4 * k, t);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) out[j][k] = t[j];
-      }
-    } else if constexpr (P == 2) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        out[0][k] = __builtin_amdgcn_perm(d[2 * k + 1], d[2 * k], 0x05040100u);
-        out[1][k] = __builtin_amdgcn_perm(d[2 * k + 1], d[2 * k], 0x07060302u);
-      }
     } else {
+      __syncthreads();  // the previous walk's store-out reads of `stage` are done
+      // 4-dword groups of a 16-dword column block XOR-swizzled by the block, so the
+      // store-out's b128 reads of 16 consecutive columns are conflict-free
+      auto sidx = [](int row, int col) { return row * 256 + (col ^ (((col >> 6) & 3) << 2)); };
 #pragma unroll
-      for (int k = 0; k < 4; ++k) out[0][k] = d[k];
-    }
+      for (int r = 0; r < kWalk / P; ++r) {
+        uint32_t w = 0;
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
-      const int z = zblk + row * P + j;
-      if (z < z0 || z >= z1) continue;
-      if constexpr (ABL == 1) {
-        if ((out[j][0] ^ out[j][1] ^ out[j][2] ^ out[j][3]) != 0x12345678u) continue;
+        for (int j = 0; j < P; ++j)
+          w |= ((uint32_t)(m - 2 * acc[r * P + j]) & (0xFFFFFFFFu >> (32 - 8 * sizeof(T)))) << (8 * sizeof(T) * j);
+        stage[sidx(r, tid)] = w;
       }
-      *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + cb)) =
-          make_uint4(out[j][0], out[j][1], out[j][2], out[j][3]);
-    }
-  }
-  }
-}
-
-// int8 seeds, stores spread over the walk: the 64-slice Gray walk is cut into four 16-slice
-// blocks (the Gray order keeps each block's slices contiguous: steps 16 b .. 16 b + 15 visit
-// slices 16 gray(b) + 0..15), and each block is staged through one of two 4-KiB LDS buffers
-// (row = slice, byte = column) and stored at once, so a workgroup's HBM writes are spread
-// over its walk instead of bunched after it, and 16 running sums (not 64) stay in registers.
-// One barrier per block (double buffer).  The walk itself is seed_body's.
-template <int kRegG>
-__device__ __forceinline__ void seed_spread_body(const uint32_t* __restrict__ planes, const uint32_t* __restrict__ gofs,
-                                                 const uint32_t* __restrict__ off, int64_t max_groups, int z0, int z1,
-                                                 int8_t* __restrict__ buf) {
-  constexpr int NT = 256, kB = 16;  // threads (= columns), slices per block
-  __shared__ uint32_t stage[2][kB * NT / 4];
-  const int tid = threadIdx.x;
-  const int c0 = blockIdx.x * NT, c = c0 + tid;
-  const uint32_t g0 = gofs[c];
-  const int ng = (int)(gofs[c + 1] - g0);
-  int wng = ng;
+      __syncthreads();
+      // blocks of V columns x P slices: V dwords in, P chunks out
+      constexpr int kBlocks = (kWalk / P) * (256 / V);
 #pragma unroll
-  for (int s = 32; s; s >>= 1) wng = max(wng, __shfl_xor(wng, s));
-  uint32_t pr[kRegG][kHiBits];
+      for (int r = 0; r < kBlocks / 256; ++r) {
+        const int b = tid + 256 * r, row = b / (256 / V), cb = (b % (256 / V)) * V;
+        uint32_t d[V];
 #pragma unroll
-  for (int g = 0; g < kRegG; ++g)
-    if (g < ng) {
-      load_planes(planes, (int64_t)g0 + g, pr[g]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < kHiBits; ++k) pr[g][k] = 0u;
-    }
-  // store-out: this thread writes row tid / 16 of a block, columns c0 + mcb .. + 15
-  const int mcb = (tid % (NT / 16)) * 16, srow = tid / (NT / 16);
-  uint4 mx;
-  {
-    uint32_t w[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      w[k] = 0x80808080u;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int cc = c0 + mcb + 4 * k + b;
-        w[k] |= (off[cc + 1] - off[cc]) << (8 * b);
-      }
-    }
-    mx = make_uint4(w[0], w[1], w[2], w[3]);
-  }
-  const int za = z0 & ~(kWalk - 1);
-  const int nwalks = (z1 - za + kWalk - 1) / kWalk;
-  for (int wk = blockIdx.y; wk < nwalks; wk += gridDim.y) {
-    const int zblk = za + wk * kWalk;
-    uint32_t x[kRegG];  // each register group's XOR state, carried from block to block
-#pragma unroll
-    for (int g = 0; g < kRegG; ++g) {
-      x[g] = 0;
-#pragma unroll
-      for (int k = kWalkBits; k < kHiBits; ++k)
-        if ((zblk >> k) & 1) x[g] ^= pr[g][k];
-    }
-    auto block = [&](auto b_c) {
-      constexpr int b = decltype(b_c)::value;
-      constexpr int base = kB * gray(b);  // this block's first slice in the walk
-      int acc[kB];
-      // group 0 (every column; a column without codes has planes 0)
-#pragma unroll
-      for (int i = kB * b; i < kB * (b + 1); ++i) {
-        if (i > 0) x[0] ^= pr[0][ctz_c(i)];
-        acc[gray(i) - base] = __popc(x[0]);
-      }
-#pragma unroll
-      for (int g = 1; g < kRegG; ++g) {
-        if (g < wng) {
-#pragma unroll
-          for (int i = kB * b; i < kB * (b + 1); ++i) {
-            if (i > 0) x[g] ^= pr[g][ctz_c(i)];
-            acc[gray(i) - base] += __popc(x[g]);
-          }
+        for (int k = 0; k < V; k += 4) {
+          const uint4 v = *reinterpret_cast<const uint4*>(stage + sidx(row, cb + k));
+          d[k] = v.x;
+          d[k + 1] = v.y;
+          d[k + 2] = v.z;
+          d[k + 3] = v.w;
         }
-      }
-      for (int g = kRegG; g < wng; ++g) {  // dense columns: the rest from L2, state rebuilt
-        uint32_t p[kHiBits];
-        if (g < ng) {
-          load_planes(planes, (int64_t)g0 + g, p);
+        uint32_t out[P][4];
+        if constexpr (P == 2) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            out[0][k] = __builtin_amdgcn_perm(d[2 * k + 1], d[2 * k], 0x05040100u);
+            out[1][k] = __builtin_amdgcn_perm(d[2 * k + 1], d[2 * k], 0x07060302u);
+          }
         } else {
 #pragma unroll
-          for (int k = 0; k < kHiBits; ++k) p[k] = 0u;
+          for (int k = 0; k < 4; ++k) out[0][k] = d[k];
         }
-        uint32_t y = 0;
-        const int zs = zblk + gray(kB * b);  // the slice of the block's first step
 #pragma unroll
-        for (int k = 0; k < kHiBits; ++k)
-          if ((zs >> k) & 1) y ^= p[k];
-#pragma unroll
-        for (int i = kB * b; i < kB * (b + 1); ++i) {
-          if (i > kB * b) y ^= p[ctz_c(i)];
-          acc[gray(i) - base] += __popc(y);
+        for (int j = 0; j < P; ++j) {
+          const int z = zblk + row * P + j;
+          if (z < z0 || z >= z1) continue;
+          *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + cb)) =
+              make_uint4(out[j][0], out[j][1], out[j][2], out[j][3]);
         }
       }
-      uint8_t* st8 = reinterpret_cast<uint8_t*>(stage[b & 1]);
-#pragma unroll
-      for (int j = 0; j < kB; ++j) st8[j * NT + tid] = (uint8_t)acc[j];
-      __syncthreads();  // (buffer b & 1 was last read two blocks ago, before the previous barrier)
-      const uint4 v = *reinterpret_cast<const uint4*>(st8 + srow * NT + mcb);
-      // m - 2 acc per byte as ((m | 0x80) - 2 acc) ^ 0x80 (acc <= m <= 127: no carries)
-      const uint4 o = make_uint4((mx.x - (v.x + v.x)) ^ 0x80808080u, (mx.y - (v.y + v.y)) ^ 0x80808080u,
-                                 (mx.z - (v.z + v.z)) ^ 0x80808080u, (mx.w - (v.w + v.w)) ^ 0x80808080u);
-      const int z = zblk + base + srow;
-      if (z >= z0 && z < z1) *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + c0 + mcb) = o;
-    };
-    block(std::integral_constant<int, 0>());
-    block(std::integral_constant<int, 1>());
-    block(std::integral_constant<int, 2>());
-    block(std::integral_constant<int, 3>());
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void seed_spread_kernel(const uint32_t* __restrict__ planes,
-                                                          const uint32_t* __restrict__ gofs,
-                                                          const uint32_t* __restrict__ off, int64_t max_groups,
-                                                          int z0, int z1, int8_t* __restrict__ buf) {
-  seed_spread_body<kRegGroups>(planes, gofs, off, max_groups, z0, z1, buf);
-}
-
-template <typename T, int ABL = 0>
+template <typename T>
 __global__ __launch_bounds__(256) void seed_kernel(const uint32_t* __restrict__ planes,
                                                    const uint32_t* __restrict__ gofs,
-                                                   const uint32_t* __restrict__ off, int64_t max_groups,
-                                                   int z0, int z1, T* __restrict__ buf) {
-  seed_body<T, ABL, kRegGroups>(planes, gofs, off, max_groups, z0, z1, buf);
-}
-// the byte stage double-buffered (DB above)
-template <typename T>
-__global__ __launch_bounds__(256) void seed_db_kernel(const uint32_t* __restrict__ planes,
-                                                      const uint32_t* __restrict__ gofs,
-                                                      const uint32_t* __restrict__ off, int64_t max_groups,
-                                                      int z0, int z1, T* __restrict__ buf) {
-  seed_body<T, 0, kRegGroups, 256, true>(planes, gofs, off, max_groups, z0, z1, buf);
-}
-// store-width variant (A/B): 512 columns per workgroup (512-B slice-row segments)
-template <typename T>
-__global__ __launch_bounds__(512) void seed_wide_kernel(const uint32_t* __restrict__ planes,
-                                                        const uint32_t* __restrict__ gofs,
-                                                        const uint32_t* __restrict__ off, int64_t max_groups,
-                                                        int z0, int z1, T* __restrict__ buf) {
-  seed_body<T, 7, kRegGroups, 512>(planes, gofs, off, max_groups, z0, z1, buf);
-}
-// occupancy variant (A/B): one register-resident group, 4 waves per SIMD
-template <typename T>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void seed_r1_kernel(
-    const uint32_t* __restrict__ planes, const uint32_t* __restrict__ gofs, const uint32_t* __restrict__ off,
-    int64_t max_groups, int z0, int z1, T* __restrict__ buf) {
-  seed_body<T, 0, 1>(planes, gofs, off, max_groups, z0, z1, buf);
+                                                   const uint32_t* __restrict__ off, int z0, int z1,
+                                                   T* __restrict__ buf) {
+  seed_body<T>(planes, gofs, off, z0, z1, buf);
 }
 
 // LDS word of column e in the tile kernel: bits 2, 3, 4 XORed with bits 6, 5, 10, so the
@@ -706,14 +496,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
 // groups: e bits 0..3, 10 vary) are both conflict-free.
 __device__ __forceinline__ int swz(int e) {
   return e ^ (((e >> 6) & 1) << 2) ^ (((e >> 5) & 1) << 3) ^ (((e >> 10) & 1) << 4);
-}
-
-// int16 exchange (int8 seeds): dword of the element pair e >> 1, bits 1, 2, 3 XORed with
-// e bits 6, 7, 10: the phase-1 b64 stores (16-lane groups: e bits 4..7 vary) and the
-// phase-2 u16 loads (32-lane groups: e bits 0..3, 10 vary; pairs share a dword) are
-// conflict-free.
-__device__ __forceinline__ int swz16(int e) {
-  return (e >> 1) ^ (((e >> 6) & 1) << 1) ^ (((e >> 7) & 1) << 2) ^ (((e >> 10) & 1) << 3);
 }
 
 // Butterfly over a lane bit without LDS: v_permlane{32,16}_swap brings the partner lane's
@@ -731,23 +513,20 @@ __device__ __forceinline__ void lane_butterfly16(int32_t& a, int32_t& b) {
   b = (int32_t)(r[0] - r[1]);
 }
 
-// Per slice: WHT over the 14 column bits, then S_w += F^2 by digit weight.  Persistent:
-// workgroups stride over the chunk's slices; 17 global atomics per workgroup.
+// int16 / int32 seeds (columns of more than 127 codes, e.g. config 5): per slice the WHT over
+// the 14 column bits on the VALU, then S_w += F^2 by digit weight.  Persistent: workgroups
+// stride over the chunk's slices; 17 global atomics per workgroup.
 //   phase 1  registers q = e bits 0..3 + 16 * (12, 13); thread = e bits 4..11
 //   phase 2  registers q = e bits 4..9;  lane = e bits 0..3, 10, 11; wave = e bits 12, 13
 //   phase 3  lane bits 5, 4 (e 11, 10) by permlane swaps against q bits 1, 0 (e 5, 4):
 //            then q = (e 10, 11, 6..9), lane = e bits 0..5, wave = e bits 12, 13 -- whole
 //            2-bit digits, so an element's digit weight is thread constant + compile time.
-// ABL (ablation builds only, wrong results by design): 1 = no global loads, 2 = no LDS
-// exchange, 3 = no squares/bins, 4 = loads only.
-template <typename T, int ABL = 0>
+template <typename T>
 __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, int z0, int nslices,
                                                    unsigned long long* __restrict__ counts,
                                                    unsigned long long add_n = 0) {
-  // int8 seeds: after phase 1 |x| <= 64 * 127 fits int16, so the exchange takes 32 KB
-  // and three workgroups share a CU
-  constexpr bool kNarrow = sizeof(T) == 1;
-  __shared__ std::conditional_t<kNarrow, int16_t, int32_t> lds[kLo];
+  static_assert(sizeof(T) >= 2, "int8 seeds take tile_reg_kernel");
+  __shared__ int32_t lds[kLo];
   __shared__ unsigned long long bins[17];
   constexpr int V = Chunk<T>::kVals, L = Chunk<T>::kLog;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -757,49 +536,23 @@ __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, in
   for (int s = blockIdx.x; s < nslices; s += gridDim.x) {
     const T* row = buf + (int64_t)s * kLo;
     int32_t x[64];
-    if constexpr (ABL == 1) {
 #pragma unroll
-      for (int q = 0; q < 64; ++q) x[q] = (s * 7 + q * 3 + tid) & 127;
-    } else {
+    for (int j = 0; j < Chunk<T>::kPerThread; ++j) {
+      const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(row + tid * V + (j << (L + 8))));
+      const T* e = reinterpret_cast<const T*>(&v);
 #pragma unroll
-      for (int j = 0; j < Chunk<T>::kPerThread; ++j) {
-        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(row + tid * V + (j << (L + 8))));
-        const T* e = reinterpret_cast<const T*>(&v);
-#pragma unroll
-        for (int r = 0; r < V; ++r) x[j * V + r] = e[r];
-      }
-    }
-    if constexpr (ABL == 4) {
-      int32_t a = 0;
-#pragma unroll
-      for (int q = 0; q < 64; ++q) a += x[q];
-      if (a == 0x7fffffff) counts[0] = 1;
-      continue;
+      for (int r = 0; r < V; ++r) x[j * V + r] = e[r];
     }
     wht<64>(x);
-    if constexpr (ABL != 2) {
-      __syncthreads();  // the previous slice's phase-2 reads are done
-      if constexpr (kNarrow) {
+    __syncthreads();  // the previous slice's phase-2 reads are done
 #pragma unroll
-        for (int q = 0; q < 64; q += 4)
-          *reinterpret_cast<uint2*>(lds + 2 * swz16((q & 15) | (tid << 4) | ((q >> 4) << 12))) =
-              make_uint2(((uint32_t)x[q] & 0xFFFFu) | ((uint32_t)x[q + 1] << 16),
-                         ((uint32_t)x[q + 2] & 0xFFFFu) | ((uint32_t)x[q + 3] << 16));
-        __syncthreads();
-        const int a2 = 2 * swz16(t2) + (t2 & 1);  // the map is XOR-linear in e
+    for (int q = 0; q < 64; q += 4)
+      *reinterpret_cast<int4*>(lds + swz((q & 15) | (tid << 4) | ((q >> 4) << 12))) =
+          make_int4(x[q], x[q + 1], x[q + 2], x[q + 3]);
+    __syncthreads();
+    const int a2 = swz(t2);
 #pragma unroll
-        for (int q = 0; q < 64; ++q) x[q] = lds[a2 ^ (2 * swz16(q << 4))];
-      } else {
-#pragma unroll
-        for (int q = 0; q < 64; q += 4)
-          *reinterpret_cast<int4*>(lds + swz((q & 15) | (tid << 4) | ((q >> 4) << 12))) =
-              make_int4(x[q], x[q + 1], x[q + 2], x[q + 3]);
-        __syncthreads();
-        const int a2 = swz(t2);
-#pragma unroll
-        for (int q = 0; q < 64; ++q) x[q] = lds[a2 ^ swz(q << 4)];
-      }
-    }
+    for (int q = 0; q < 64; ++q) x[q] = lds[a2 ^ swz(q << 4)];
     wht<64>(x);
 #pragma unroll
     for (int q = 0; q < 64; ++q)
@@ -807,13 +560,6 @@ __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, in
 #pragma unroll
     for (int q = 0; q < 64; ++q)
       if (!(q & 1)) lane_butterfly16(x[q], x[q | 1]);  // e bit 10 <-> q bit 0 (e bit 4)
-    if constexpr (ABL == 3) {
-      int32_t a = 0;
-#pragma unroll
-      for (int q = 0; q < 64; ++q) a ^= x[q];
-      if (a == 0x7fffffff) counts[0] = 1;
-      continue;
-    }
     unsigned long long acc[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < 64; ++q)
@@ -829,17 +575,6 @@ __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, in
   if (add_n && blockIdx.x == 0 && tid == 0) atomicAdd(counts, add_n);  // n, once per job
 }
 
-// ---------------------------------------------------------------- MFMA tile (int8 seeds)
-// The first six butterfly levels are a 64-point Hadamard product on the matrix cores:
-// v_mfma_i32_16x16x64_i8 with A = 16 rows of H_64 (+-1 int8) and B = the int8 seed values
-// exactly as a 16-B load leaves them (lane l holds B[k = 16 (l >> 4) + j][n = l & 15],
-// verified by tools/mfma_i8_probe.hip), so the bytes go from HBM into the MFMA with no
-// unpacking.  Per slice, thread t's 16-B chunks j = 0..3 hold columns 16 t + r + 4096 j:
-// k = column bits 0..3 (r) and 8, 9 (lane bits 4, 5), n = column bits 4..7 (lane bits
-// 0..3).  Outputs C[row 4 (l >> 4) + i][col l & 15] of quarter q: transformed column bits
-// 0, 1 = i, 2, 3 = lane bits 4, 5, 8, 9 = q.  Then 2 register levels over j (bits 12, 13),
-// one int16 LDS exchange, 6 register levels over bits 4..7, 10, 11 -- whose register and
-// thread bits are whole 2-bit digits -- and the F^2 binning.
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef long v2l_t __attribute__((ext_vector_type(2)));
 typedef short v2s_t __attribute__((ext_vector_type(2)));
@@ -847,382 +582,7 @@ __device__ __forceinline__ v2l_t pack_v2l(const uint32_t* w) {
   return v2l_t{(long)(((uint64_t)w[1] << 32) | w[0]), (long)(((uint64_t)w[3] << 32) | w[2])};
 }
 
-
-// dword of the int16 pair holding column e: bits 0..4 = e1^e4, e2, e3^e5, e8^e6, e7, then
-// e4, e5, e6, e9..e13.  Conflict-free for the packed b32 stores (32-lane groups: e bits 2,
-// 4..7 vary) and the u16 loads (e bits 0..3, 8 vary; pairs share a dword).
-__device__ __forceinline__ int dmf(int e) {
-  return (((e >> 1) ^ (e >> 4)) & 1) | (((e >> 2) & 1) << 1) | ((((e >> 3) ^ (e >> 5)) & 1) << 2) |
-         ((((e >> 8) ^ (e >> 6)) & 1) << 3) | (((e >> 7) & 1) << 4) | (((e >> 4) & 7) << 5) | ((e >> 9) << 8);
-}
-
-// Slices: workgroup b takes a contiguous block of positions u; position u is slice
-// z0 + order[u] (order = a whole aligned chunk's offsets sorted by digit weight, so a
-// workgroup's slices share their weight for long runs and F^2 is binned in registers,
-// flushed to LDS only when it changes), or z0 + u (order = nullptr).
-// ABL (ablation builds only, wrong results by design): 1 = no global loads, 2 = no
-// phase-2 butterflies, 3 = no squares/bins, 4 = no LDS exchange, 5 = prefetch the next slice.
-template <int ABL>
-__device__ __forceinline__ void tile_mfma_body(const int8_t* __restrict__ buf, const uint16_t* __restrict__ order,
-                                               int z0, int nslices, unsigned long long* __restrict__ counts) {
-  __shared__ uint32_t lds32[kLo / 2];
-  __shared__ unsigned long long bins[17];
-  const int16_t* lds16 = reinterpret_cast<const int16_t*>(lds32);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid < 17) bins[tid] = 0;
-  v2l_t A[4];  // H_64 rows 16 q + (l & 15), columns 16 (l >> 4) + j
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    uint32_t w[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * q + (lane & 15), col = 16 * (lane >> 4) + 4 * d + r;
-        v |= ((__popc(row & col) & 1) ? 0xFFu : 0x01u) << (8 * r);
-      }
-      w[d] = v;
-    }
-    A[q] = v2l_t{(long)(((uint64_t)w[1] << 32) | w[0]), (long)(((uint64_t)w[3] << 32) | w[2])};
-  }
-  const int wt_thread = digit_weight((uint32_t)(lane & 15) | ((uint32_t)(lane >> 4) << 8) | ((uint32_t)wave << 12));
-  const int ew = ((lane >> 4) << 2) | ((lane & 15) << 4) | (wave << 10);       // store-side e bits
-  const int er = (lane & 15) | ((lane >> 4) << 8) | (wave << 12);              // load-side e bits
-  v2l_t B[4], Bn[4];
-  auto slice_of = [&](int u) { return order ? (int)order[u] : u; };
-  auto load = [&](int s, v2l_t* dst) {
-    const int8_t* row = buf + (int64_t)s * kLo;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      dst[j] = __builtin_nontemporal_load(reinterpret_cast<const v2l_t*>(row + 16 * tid + 4096 * j));
-  };
-  const int ub = (int)((int64_t)nslices * blockIdx.x / gridDim.x);
-  const int ue = (int)((int64_t)nslices * (blockIdx.x + 1) / gridDim.x);
-  unsigned long long tot[4] = {0, 0, 0, 0};
-  int cur_w = -1;
-  auto flush = [&]() {
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (tot[k]) atomicAdd(&bins[cur_w + wt_thread + k], tot[k]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) tot[k] = 0;
-  };
-  for (int u = ub; u < ue; ++u) {
-    const int s = slice_of(u);
-    if constexpr (ABL == 1) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) B[j] = v2l_t{(long)(s * 0x9E3779B97F4A7C15ull + j), (long)tid};
-    } else if constexpr (kTilePrefetch || ABL == 5) {
-      if (u == ub) load(s, Bn);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) B[j] = Bn[j];
-      if (u + 1 < ue) load(slice_of(u + 1), Bn);
-    } else {
-      load(s, B);
-    }
-    int32_t x[64];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const v4i_t c = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[q], B[j], v4i_t{0, 0, 0, 0}, 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) x[j * 16 + q * 4 + i] = c[i];
-      }
-    // pack column pairs (bit 0) into int16x2 -- |x| <= 64 * 127 here and <= 256 * 127
-    // after the next two levels -- and do those levels packed (v_pk_add/sub_u16; the
-    // arithmetic wraps mod 2^16 and the results are in range, so it is exact)
-    typedef short s2_t __attribute__((ext_vector_type(2)));
-    s2_t pk[32];  // pk[j * 8 + q * 2 + ip] = (x[k], x[k + 1]), k = j * 16 + q * 4 + 2 ip
-#pragma unroll
-    for (int k = 0; k < 64; k += 2)
-      pk[k / 2] = __builtin_bit_cast(s2_t, __builtin_amdgcn_perm((uint32_t)x[k + 1], (uint32_t)x[k], 0x05040100u));
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {  // column bits 12, 13 (registers j)
-      const s2_t a = pk[r], b = pk[8 + r], c = pk[16 + r], d = pk[24 + r];
-      const s2_t ab0 = a + b, ab1 = a - b, cd0 = c + d, cd1 = c - d;
-      pk[r] = ab0 + cd0;
-      pk[8 + r] = ab1 + cd1;
-      pk[16 + r] = ab0 - cd0;
-      pk[24 + r] = ab1 - cd1;
-    }
-    if constexpr (ABL == 4) {
-#pragma unroll
-      for (int k = 0; k < 32; ++k) {
-        const uint32_t w = __builtin_bit_cast(uint32_t, pk[k]);
-        x[2 * k] = (int16_t)w;
-        x[2 * k + 1] = (int32_t)w >> 16;
-      }
-    } else {
-    __syncthreads();  // the previous slice's loads from LDS are done
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int ip = 0; ip < 2; ++ip) {
-          const int e = ew | (2 * ip) | (q << 8) | (j << 12);
-          lds32[dmf(e)] = __builtin_bit_cast(uint32_t, pk[j * 8 + q * 2 + ip]);
-        }
-    __syncthreads();
-#pragma unroll
-    for (int q2 = 0; q2 < 64; ++q2) {  // registers = column bits 4..7, 10, 11
-      const int e = er | ((q2 & 15) << 4) | ((q2 >> 4) << 10);
-      x[q2] = lds16[2 * dmf(e) + (e & 1)];
-    }
-    }
-    if constexpr (ABL != 2) wht<64>(x);
-    const int wz = digit_weight((uint32_t)(z0 + s));  // workgroup-uniform
-    if (wz != cur_w) {
-      if (cur_w >= 0) flush();
-      cur_w = wz;
-    }
-    if constexpr (ABL == 3) {
-      int32_t a = 0;
-#pragma unroll
-      for (int q2 = 0; q2 < 64; ++q2) a ^= x[q2];
-      tot[0] += (unsigned)a;
-      continue;
-    }
-#pragma unroll
-    for (int q2 = 0; q2 < 64; ++q2)
-      tot[digit_weight_c((uint32_t)(q2 & 15)) + digit_weight_c((uint32_t)(q2 >> 4))] +=
-          (unsigned long long)((int64_t)x[q2] * x[q2]);
-  }
-  if (cur_w >= 0) flush();
-  __syncthreads();
-  if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
-}
-
-template <int ABL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_mfma_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts) {
-  tile_mfma_body<ABL>(buf, order, z0, nslices, counts);
-}
-
-// ---------------------------------------------------------------- two-stage MFMA tile
-// Both 64-point stages on the matrix cores.  Stage 1 as tile_mfma_kernel (column bits 0..3,
-// 8, 9) plus the 4-point transform over the load registers j (bits 12, 13) in int32; the
-// j = 0 MFMAs start from an accumulator of 128, which that transform spreads to every
-// output (H_4 (128, 0, 0, 0) = (128, 128, 128, 128)), so y = x + 128 leaves the stage.
-// One int16 LDS exchange (ds_write_b16), then stage 2 over bits 4..7, 10, 11 with
-// k = bits 4..7 (the 16 bytes a lane holds) + bits 10, 11 (lane bits 4, 5) and n = bits
-// 0..3: y = 256 h + l with h = the high byte of y and l - 128 = the low byte of y ^ 0x80
-// (both signed bytes), so x = 256 h + (l - 128) and H x = (H h << 8) + H (l - 128): two
-// i8 MFMAs per output tile, the first one's result shifted into the second's accumulator.
-// Stage-2 outputs: bits 0..3 = lane bits 0..3, 4, 5 = i, 6, 7 = lane bits 4, 5, 8, 9 =
-// the register group g, 10, 11 = the A quarter q, 12, 13 = the wave -- whole digits.
-// LDS element of column e: bits 4..7 in the low 4 bits (bit 7 ^= bit 3, so each 16-lane
-// group of the stage-2 b128 reads covers all 64 banks), bits 0..3 above them (bit 0 ^=
-// bit 2: the stage-1 b16 stores of lane bits 4 = 0 / 1 land on different banks), then 8..13.
-__device__ __forceinline__ int lds_e2(int e) {
-  const int lo4 = ((e >> 4) & 15) ^ (((e >> 3) & 1) << 3);
-  const int mid4 = (e & 15) ^ ((e >> 2) & 1);
-  return lo4 | (mid4 << 4) | ((e >> 8) << 8);
-}
-
-// ABL (ablation builds only, wrong results by design): 1 = no global loads, 2 = no squares,
-// 3 = no LDS exchange, 4 = no stage-2 MFMAs, 5 = no barriers
-template <bool PF, int STAGGER = 0, int ABL = 0>
-__device__ __forceinline__ void tile_mfma2_body(const int8_t* __restrict__ buf, const uint16_t* __restrict__ order,
-                                                int z0, int nslices, unsigned long long* __restrict__ counts,
-                                                unsigned long long add_n) {
-  __shared__ __attribute__((aligned(16))) int16_t lds[kLo];
-  __shared__ unsigned long long bins[17];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid < 17) bins[tid] = 0;
-  v2l_t A[4];  // H_64 rows 16 q + (l & 15), columns 16 (l >> 4) + j (both stages)
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    uint32_t w[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * q + (lane & 15), col = 16 * (lane >> 4) + 4 * d + r;
-        v |= ((__popc(row & col) & 1) ? 0xFFu : 0x01u) << (8 * r);
-      }
-      w[d] = v;
-    }
-    A[q] = v2l_t{(long)(((uint64_t)w[1] << 32) | w[0]), (long)(((uint64_t)w[3] << 32) | w[2])};
-  }
-  // stage-2 output bits 0..3 (two digits), 6, 7 and 12, 13 are thread constants
-  const int wt_thread = digit_weight((uint32_t)(lane & 15) | ((uint32_t)(lane >> 4) << 6) | ((uint32_t)wave << 12));
-  // stage-1 store base: e = i | (l >> 4) << 2 | (l & 15) << 4 | q << 8 | wave << 10 | j << 12
-  const int wbase = lds_e2(((lane >> 4) << 2) | ((lane & 15) << 4) | (wave << 10));
-  // stage-2 read base: e = (l & 15) | (l >> 4) << 10 | g << 8 | wave << 12, bits 4..7 = 0..15
-  const int rbase = lds_e2((lane & 15) | ((lane >> 4) << 10) | (wave << 12));
-  auto slice_of = [&](int u) { return order ? (int)order[u] : u; };
-  const int ub = (int)((int64_t)nslices * blockIdx.x / gridDim.x);
-  const int ue = (int)((int64_t)nslices * (blockIdx.x + 1) / gridDim.x);
-  unsigned long long tot[4] = {0, 0, 0, 0};
-  int cur_w = -1;
-  auto flush = [&]() {
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (tot[k]) atomicAdd(&bins[cur_w + wt_thread + k], tot[k]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) tot[k] = 0;
-  };
-  if constexpr (STAGGER > 0) {  // A/B: phase-offset co-resident workgroups
-    const int ph = blockIdx.x & 3;
-    for (int k = 0; k < ph; ++k) __builtin_amdgcn_s_sleep(STAGGER);
-  }
-  auto load = [&](int sl, v2l_t* dst) {
-    if constexpr (ABL == 1) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) dst[j] = v2l_t{(long)(sl * 0x9E3779B97F4A7C15ull + j), (long)tid};
-      return;
-    }
-    const int8_t* row = buf + (int64_t)sl * kLo;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      dst[j] = __builtin_nontemporal_load(reinterpret_cast<const v2l_t*>(row + 16 * tid + 4096 * j));
-  };
-  v2l_t Bn[4];
-  // PF: slice indices run two ahead (their table loads wait a whole slice) and the values
-  // one ahead (the next slice's loads fly while this one is transformed)
-  int s_cur = 0, s_nxt = 0;
-  if constexpr (PF) {
-    if (ub < ue) {
-      s_cur = slice_of(ub);
-      load(s_cur, Bn);
-    }
-    if (ub + 1 < ue) s_nxt = slice_of(ub + 1);
-  }
-  for (int u = ub; u < ue; ++u) {
-    v2l_t B[4];
-    int s;
-    if constexpr (PF) {
-      s = s_cur;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) B[j] = Bn[j];
-      if (u + 1 < ue) load(s_nxt, Bn);
-      s_cur = s_nxt;
-      if (u + 2 < ue) s_nxt = slice_of(u + 2);
-    } else {
-      s = slice_of(u);
-      load(s, B);
-    }
-    int32_t x[64];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int b0 = j == 0 ? 128 : 0;
-        const v4i_t c = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[q], B[j], v4i_t{b0, b0, b0, b0}, 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) x[j * 16 + q * 4 + i] = c[i];
-      }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {  // column bits 12, 13 (registers j)
-      const int32_t a = x[r], b = x[16 + r], c = x[32 + r], d = x[48 + r];
-      const int32_t ab0 = a + b, ab1 = a - b, cd0 = c + d, cd1 = c - d;
-      x[r] = ab0 + cd0;
-      x[16 + r] = ab1 + cd1;
-      x[32 + r] = ab0 - cd0;
-      x[48 + r] = ab1 - cd1;
-    }
-    if constexpr (ABL != 3) {
-    if constexpr (ABL != 5) __syncthreads();  // the previous slice's stage-2 reads are done
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)  // the offset is XOR-linear in e: wbase ^ lds_e2(i | q << 8 | j << 12)
-          lds[wbase ^ lds_e2(i | (q << 8) | (j << 12))] = (int16_t)x[j * 16 + q * 4 + i];
-    if constexpr (ABL != 5) __syncthreads();
-    }
-    const int wz = digit_weight((uint32_t)(z0 + s));  // workgroup-uniform
-    if (wz != cur_w) {
-      if (cur_w >= 0) flush();
-      cur_w = wz;
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int base = rbase ^ lds_e2(g << 8);
-      // base already carries the bit-7 swizzle (lds_e2 of e with bits 4..7 = 0)
-      uint4 h0, h1;
-      if constexpr (ABL == 3) {
-        h0 = make_uint4(x[16 * g], x[16 * g + 1], x[16 * g + 2], x[16 * g + 3]);
-        h1 = make_uint4(x[16 * g + 4], x[16 * g + 5], x[16 * g + 6], x[16 * g + 7]);
-      } else {
-        h0 = *reinterpret_cast<const uint4*>(lds + base);        // bits 4..6, bit 7 = 0
-        h1 = *reinterpret_cast<const uint4*>(lds + (base ^ 8));  // bit 7 = 1
-      }
-      const uint32_t d[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-      uint32_t lo[4], hi[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        lo[m] = __builtin_amdgcn_perm(d[2 * m + 1], d[2 * m], 0x06040200u) ^ 0x80808080u;
-        hi[m] = __builtin_amdgcn_perm(d[2 * m + 1], d[2 * m], 0x07050301u);
-      }
-      const v2l_t Bl = v2l_t{(long)(((uint64_t)lo[1] << 32) | lo[0]), (long)(((uint64_t)lo[3] << 32) | lo[2])};
-      const v2l_t Bh = v2l_t{(long)(((uint64_t)hi[1] << 32) | hi[0]), (long)(((uint64_t)hi[3] << 32) | hi[2])};
-      v4i_t c[4];  // the four quarters' high-byte products first: independent MFMAs
-      if constexpr (ABL == 4) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          c[q] = v4i_t{(int)lo[q], (int)hi[q], (int)(lo[q] ^ hi[(q + 1) & 3]), (int)(hi[q] + lo[(q + 2) & 3])};
-      } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) c[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[q], Bh, v4i_t{0, 0, 0, 0}, 0, 0, 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) c[q][i] <<= 8;
-        c[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[q], Bl, c[q], 0, 0, 0);
-      }
-      }
-      if constexpr (ABL == 2) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) tot[i] ^= (unsigned)c[q][i];
-      } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          tot[digit_weight_c((uint32_t)i) + digit_weight_c((uint32_t)g) + digit_weight_c((uint32_t)q)] +=
-              (unsigned long long)((int64_t)c[q][i] * c[q][i]);
-      }
-    }
-  }
-  if (cur_w >= 0) flush();
-  __syncthreads();
-  if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
-  if (add_n && blockIdx.x == 0 && tid == 0) atomicAdd(counts, add_n);  // n, once per job
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_mfma2_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_mfma2_body<false>(buf, order, z0, nslices, counts, add_n);
-}
-template <int STAGGER>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_mfma2_pf_st_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_mfma2_body<true, STAGGER>(buf, order, z0, nslices, counts, add_n);
-}
-template <int ABL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_mfma2_pf_abl_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_mfma2_body<true, 0, ABL>(buf, order, z0, nslices, counts, add_n);
-}
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tile_mfma2_pf_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_mfma2_body<true>(buf, order, z0, nslices, counts, add_n);
-}
-
-// ---------------------------------------------------------------- register-resident tile
+// ---------------------------------------------------------------- register-resident tile (int8 seeds)
 // One WAVE transforms one whole slice with no LDS exchange and no barrier.  Column bits:
 // P = 0..5 (digits 0-2), Q = 6..11 (digits 3-5), R = 12, 13 (digit 6).  Lane l's 16-B load
 // (plane R, load mt) holds columns 16 (l >> 4) + 64 (l & 15) + 1024 mt + 4096 R + j: a wave
@@ -1233,27 +593,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
 //     output rows m = 4 (l >> 4) + i.  So lane l holds Q bits 0, 1 = i, 2, 3 = l >> 4 and,
 //     over the 4 loads, Q bits 4, 5 = mt: 16 values that ARE stage 2's B operand (k = 16 (l >> 4)
 //     + 4 mt + i, a relabeling of whole Q digits), packed into bytes in registers.
-//   stage 2: H_64 over Q (A = the same H quarters) as the two-byte split of tile_mfma2
-//     (y = v + 128 = 256 h + l', v = 256 h + (l' - 128), two i8 MFMAs, the first shifted into
-//     the second's accumulator); outputs Q' rows 16 q2 + 4 (l >> 4) + i2: whole digits.
+//   stage 2: H_64 over Q (A = the same H quarters).  |v + 128| < 2^15 needs two bytes: with
+//     y = v + 128 = 256 h + l', v = 256 h + (l' - 128), so H v = (H h << 8) + H (l' - 128): two
+//     i8 MFMAs per output tile, the first shifted into the second's accumulator.  The byte
+//     split goes through int16 pairs (one v_perm packs two stage-1 outputs), which are also
+//     what the plane sums accumulate (v_pk_add_u16; the sum over the planes of v + 128 from
+//     -384 stays within +-32,640).  Outputs Q' rows 16 q2 + 4 (l >> 4) + i2: whole digits.
 //   R (one base digit) by Parseval instead of a butterfly: with G_R = the 12-bit transform of
 //     plane R and F(R') = sum_R (-1)^<R, R'> G_R,  F(0) = transform of sum_R D_R = sum_R C1_R
 //     (added after stage 1) and sum_{R' != 0} F(R')^2 = 4 sum_R G_R^2 - F(0)^2.  So every
 //     (P', Q') adds F(0)^2 to weight w and 4 sum G_R^2 - F(0)^2 to weight w + 1: five stage-2
 //     transforms per slice (4 planes + the sum), no exchange between planes.
+//   Two quarters' MFMA chains are interleaved per wave (stage 1 of both, both byte splits, both
+//     high-byte and both low-byte stage-2 groups, then both sets of squares), and the next
+//     plane's loads are in flight while this one is transformed: 167 VGPRs, 3 waves per SIMD.
 // Weight of (P', Q', R'): digits of l & 3, (l >> 2) & 3, l >> 4 (thread constant) + qn + q2
-// + i2 (compile time) + the slice's + [R' != 0].
-// QP: two quarters' chains interleaved in one wave (stage 1 of both, then both splits, then
-// both high-byte and both low-byte stage-2 MFMA groups), for MFMA/VALU overlap inside a wave.
-// ILV = G > 0: the intermediate in the G-slice interleaved layout (ilv_off<G>, written by the
-// direct MFMA seed).  A team of G / 4 workgroups -- blocks b, b + 8, ..: the same XCD under the
-// round-robin dispatch -- takes the G slices of one group at a time (workgroup k of the team,
-// wave w: slice G g + 4 k + w), so every 16 G-byte piece a wave reads 16 B of is read whole by
-// its team while it sits in that XCD's L2.
-template <bool PF, int ABL = 0, int QP = 0, int ILV = 0>
-__device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, const uint16_t* __restrict__ order,
-                                              int z0, int nslices, unsigned long long* __restrict__ counts,
-                                              unsigned long long add_n) {
+// + i2 (compile time) + the slice's + [R' != 0].  Each wave of the grid takes a contiguous run
+// of slice positions; position u is slice order[u] (a whole aligned chunk sorted by digit
+// weight, so the run's weight changes rarely and F^2 is binned in registers) or u.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_kernel(
+    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
+    unsigned long long* __restrict__ counts, unsigned long long add_n) {
   __shared__ unsigned long long bins[17];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < 17) bins[tid] = 0;
@@ -1276,14 +636,8 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
   }
   const int wt_thread = digit_weight((uint32_t)(lane & 15)) + digit_weight((uint32_t)(lane >> 4));
   const int lane_off = 16 * (lane >> 4) + 64 * (lane & 15);
-  // each wave of the grid takes a contiguous run of slice positions (ILV: each workgroup a
-  // contiguous run of 4-slice group positions)
-  constexpr int TS = ILV ? ILV / 4 : 1;  // workgroups per team
-  const int team_k = ILV ? (int)(blockIdx.x / 8) % TS : 0;
-  const int gw = ILV ? (int)(blockIdx.x / (8 * TS)) * 8 + (int)(blockIdx.x % 8) : blockIdx.x * 4 + wave;
-  const int GW = ILV ? (int)gridDim.x / TS : gridDim.x * 4;
-  const int nunits = ILV ? (nslices + ILV - 1) / ILV : nslices;
-  const int ub = (int)((int64_t)nunits * gw / GW), ue = (int)((int64_t)nunits * (gw + 1) / GW);
+  const int gw = blockIdx.x * 4 + wave, GW = gridDim.x * 4;
+  const int ub = (int)((int64_t)nslices * gw / GW), ue = (int)((int64_t)nslices * (gw + 1) / GW);
   unsigned long long accA[4] = {0, 0, 0, 0}, accB[4] = {0, 0, 0, 0};
   int cur_w = -1;
   auto flush = [&]() {
@@ -1297,68 +651,14 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
     }
   };
   auto load_plane = [&](int sl, int R, v2l_t* dst) {
-    if constexpr (ILV) {
-      const int8_t* p = buf + ilv_off<(ILV ? ILV : 4)>(sl, (lane >> 4) + 4 * (lane & 15) + 256 * R);
+    const int8_t* p = buf + (int64_t)sl * kLo + lane_off + 4096 * R;
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) dst[mt] = *reinterpret_cast<const v2l_t*>(p + 64 * 16 * ILV * mt);
-    } else {
-      const int8_t* p = buf + (int64_t)sl * kLo + lane_off + 4096 * R;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        dst[mt] = __builtin_nontemporal_load(reinterpret_cast<const v2l_t*>(p + 1024 * mt));
-    }
+    for (int mt = 0; mt < 4; ++mt)
+      dst[mt] = __builtin_nontemporal_load(reinterpret_cast<const v2l_t*>(p + 1024 * mt));
   };
-  // stage 2 of 16 values per lane (c1[mt][i] = v + 128 of stage 1, one quarter qn) -> squares
-  auto stage2 = [&](const v4i_t* c1, auto qn_c, unsigned long long* acc) {
-    constexpr int qn = decltype(qn_c)::value;
-    uint32_t lo[4], hi[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const uint32_t t1 = __builtin_amdgcn_perm((uint32_t)c1[mt][1], (uint32_t)c1[mt][0], 0x05010400u);
-      const uint32_t t2 = __builtin_amdgcn_perm((uint32_t)c1[mt][3], (uint32_t)c1[mt][2], 0x05010400u);
-      lo[mt] = __builtin_amdgcn_perm(t2, t1, 0x05040100u) ^ 0x80808080u;
-      hi[mt] = __builtin_amdgcn_perm(t2, t1, 0x07060302u);
-    }
-    const v2l_t Bl = v2l_t{(long)(((uint64_t)lo[1] << 32) | lo[0]), (long)(((uint64_t)lo[3] << 32) | lo[2])};
-    const v2l_t Bh = v2l_t{(long)(((uint64_t)hi[1] << 32) | hi[0]), (long)(((uint64_t)hi[3] << 32) | hi[2])};
-    v4i_t c[4];
-#pragma unroll
-    for (int q2 = 0; q2 < 4; ++q2) c[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bh, v4i_t{0, 0, 0, 0}, 0, 0, 0);
-#pragma unroll
-    for (int q2 = 0; q2 < 4; ++q2) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) c[q2][i] <<= 8;
-      c[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bl, c[q2], 0, 0, 0);
-    }
-#pragma unroll
-    for (int q2 = 0; q2 < 4; ++q2)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        constexpr int dummy = 0;
-        (void)dummy;
-        if constexpr (ABL == 2)
-          acc[0] ^= (unsigned)c[q2][i];
-        else
-          acc[digit_weight_c((uint32_t)qn) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
-              (unsigned long long)((int64_t)c[q2][i] * c[q2][i]);
-      }
-  };
-  auto split = [&](const v4i_t* c1, v2l_t& Bl, v2l_t& Bh) {
-    uint32_t lo[4], hi[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const uint32_t t1 = __builtin_amdgcn_perm((uint32_t)c1[mt][1], (uint32_t)c1[mt][0], 0x05010400u);
-      const uint32_t t2 = __builtin_amdgcn_perm((uint32_t)c1[mt][3], (uint32_t)c1[mt][2], 0x05010400u);
-      lo[mt] = __builtin_amdgcn_perm(t2, t1, 0x05040100u) ^ 0x80808080u;
-      hi[mt] = __builtin_amdgcn_perm(t2, t1, 0x07060302u);
-    }
-    Bl = v2l_t{(long)(((uint64_t)lo[1] << 32) | lo[0]), (long)(((uint64_t)lo[3] << 32) | lo[2])};
-    Bh = v2l_t{(long)(((uint64_t)hi[1] << 32) | hi[0]), (long)(((uint64_t)hi[3] << 32) | hi[2])};
-  };
-  // two quarters qa, qb at once (QP); `between` runs after the last MFMAs are issued and
-  // before the squares (QP 2: the next pair's stage 1)
+  // two quarters qa, qb of stage 2 from their byte splits, then their squares
   auto stage2x2B = [&](const v2l_t& Bla, const v2l_t& Bha, const v2l_t& Blb, const v2l_t& Bhb, auto qa_c,
-                       auto qb_c, unsigned long long* acc, auto&& between) {
+                       auto qb_c, unsigned long long* acc) {
     constexpr int qa = decltype(qa_c)::value, qb = decltype(qb_c)::value;
     v4i_t ca[4], cb[4];
 #pragma unroll
@@ -1375,7 +675,6 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
       for (int i = 0; i < 4; ++i) cb[q2][i] <<= 8;
       cb[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Blb, cb[q2], 0, 0, 0);
     }
-    between();
 #pragma unroll
     for (int q2 = 0; q2 < 4; ++q2)
 #pragma unroll
@@ -1386,35 +685,7 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
             (unsigned long long)((int64_t)cb[q2][i] * cb[q2][i]);
       }
   };
-  // one quarter from its split (QP 4)
-  auto stage2B = [&](const v2l_t& Bl, const v2l_t& Bh, auto qn_c, unsigned long long* acc) {
-    constexpr int qn = decltype(qn_c)::value;
-    v4i_t c[4];
-#pragma unroll
-    for (int q2 = 0; q2 < 4; ++q2) c[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bh, v4i_t{0, 0, 0, 0}, 0, 0, 0);
-#pragma unroll
-    for (int q2 = 0; q2 < 4; ++q2) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) c[q2][i] <<= 8;
-      c[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bl, c[q2], 0, 0, 0);
-    }
-#pragma unroll
-    for (int q2 = 0; q2 < 4; ++q2)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc[digit_weight_c((uint32_t)qn) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
-            (unsigned long long)((int64_t)c[q2][i] * c[q2][i]);
-  };
-  auto stage2x2 = [&](const v4i_t* c1a, const v4i_t* c1b, auto qa_c, auto qb_c, unsigned long long* acc,
-                      auto&& between) {
-    v2l_t Bla, Bha, Blb, Bhb;
-    split(c1a, Bla, Bha);
-    split(c1b, Blb, Bhb);
-    stage2x2B(Bla, Bha, Blb, Bhb, qa_c, qb_c, acc, between);
-  };
-  // QP 3: the split through int16 pairs (|v + 128| < 2^15), which are also what the plane sums
-  // accumulate: cs as packed int16 (sum over the planes of v + 128 from -384 stays within
-  // +-32,640), 32 VGPRs instead of 64
+  // int16 pairs (v + 128 of stage 1, |.| < 2^15) -> the high / low byte operands
   auto split16 = [&](const uint32_t (*pr)[2], v2l_t& Bl, v2l_t& Bh) {
     uint32_t lo[4], hi[4];
 #pragma unroll
@@ -1432,57 +703,29 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
       pr[mt][1] = __builtin_amdgcn_perm((uint32_t)c1[mt][3], (uint32_t)c1[mt][2], 0x05040100u);
     }
   };
-  // planes in turn (a runtime loop: one plane's 16 VGPRs of bytes live at a time, PF: the
-  // next plane's loads in flight), the per-plane sums of all four quarters carried across
+  // planes in turn (a runtime loop: one plane's 16 VGPRs of bytes live at a time, the next
+  // plane's loads in flight), the per-plane sums of all four quarters carried across
   for (int u = ub; u < ue; ++u) {
-    int s = order ? (int)order[u] : u;
-    if constexpr (ILV) {
-      s = ILV * s + 4 * team_k + wave;
-      if (s >= nslices) continue;
-    }
+    const int s = order ? (int)order[u] : u;
     const int wz = digit_weight((uint32_t)(z0 + s));  // wave-uniform
     if (wz != cur_w) {
       if (cur_w >= 0) flush();
       cur_w = wz;
     }
-    constexpr bool P16 = QP == 3 || QP == 4;
-    v4i_t cs[P16 ? 1 : 4][4];  // [qn][mt]: sum over the planes of v + 128, from -384 (-> sum v + 128)
-    uint32_t csp[P16 ? 4 : 1][4][2];  // QP 3, 4: the same as int16 pairs
-    if constexpr (P16) {
+    uint32_t csp[4][4][2];  // [qn][mt]: sum over the planes of v + 128 as int16 pairs, from -384
 #pragma unroll
-      for (int qn = 0; qn < 4; ++qn)
+    for (int qn = 0; qn < 4; ++qn)
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) csp[qn][mt][0] = csp[qn][mt][1] = 0xFE80FE80u;
-    } else {
-#pragma unroll
-      for (int qn = 0; qn < (P16 ? 1 : 4); ++qn)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) cs[qn][mt] = v4i_t{-384, -384, -384, -384};
-    }
+      for (int mt = 0; mt < 4; ++mt) csp[qn][mt][0] = csp[qn][mt][1] = 0xFE80FE80u;
     v2l_t dn[4];
-    if constexpr (PF) load_plane(s, 0, dn);
+    load_plane(s, 0, dn);
 #pragma unroll 1
     for (int R = 0; R < 4; ++R) {
       v2l_t d[4];
-      if constexpr (PF) {
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) d[mt] = dn[mt];
-        if (R < 3) load_plane(s, R + 1, dn);
-      } else {
-        load_plane(s, R, d);
-      }
-      auto quarter = [&](auto qn_c) {
-        constexpr int qn = decltype(qn_c)::value;
-        v4i_t c1[4];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          c1[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qn], v4i_t{128, 128, 128, 128}, 0, 0, 0);
-          cs[qn][mt] += c1[mt];
-        }
-        stage2(c1, qn_c, accB);
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      auto quarters = [&](auto qa_c, auto qb_c) {
+      for (int mt = 0; mt < 4; ++mt) d[mt] = dn[mt];
+      if (R < 3) load_plane(s, R + 1, dn);
+      auto quarters16 = [&](auto qa_c, auto qb_c) {
         constexpr int qa = decltype(qa_c)::value, qb = decltype(qb_c)::value;
         v4i_t c1a[4], c1b[4];
 #pragma unroll
@@ -1490,130 +733,34 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
           c1a[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qa], v4i_t{128, 128, 128, 128}, 0, 0, 0);
           c1b[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qb], v4i_t{128, 128, 128, 128}, 0, 0, 0);
         }
+        uint32_t pa[4][2], pb[4][2];
+        pairs16(c1a, pa);
+        pairs16(c1b, pb);
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          cs[qa][mt] += c1a[mt];
-          cs[qb][mt] += c1b[mt];
-        }
-        stage2x2(c1a, c1b, qa_c, qb_c, accB, [] {});
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            csp[qa][mt][h] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s_t, csp[qa][mt][h]) +
+                                                              __builtin_bit_cast(v2s_t, pa[mt][h]));
+            csp[qb][mt][h] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s_t, csp[qb][mt][h]) +
+                                                              __builtin_bit_cast(v2s_t, pb[mt][h]));
+          }
+        v2l_t Bla, Bha, Blb, Bhb;
+        split16(pa, Bla, Bha);
+        split16(pb, Blb, Bhb);
+        stage2x2B(Bla, Bha, Blb, Bhb, qa_c, qb_c, accB);
         __builtin_amdgcn_sched_barrier(0);
       };
-      if constexpr (QP == 4) {
-        auto quarter16 = [&](auto qn_c) {
-          constexpr int qn = decltype(qn_c)::value;
-          v4i_t c1[4];
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt)
-            c1[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qn], v4i_t{128, 128, 128, 128}, 0, 0, 0);
-          uint32_t pa[4][2];
-          pairs16(c1, pa);
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-              csp[qn][mt][h] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s_t, csp[qn][mt][h]) +
-                                                                __builtin_bit_cast(v2s_t, pa[mt][h]));
-          v2l_t Bl, Bh;
-          split16(pa, Bl, Bh);
-          stage2B(Bl, Bh, qn_c, accB);
-          __builtin_amdgcn_sched_barrier(0);
-        };
-        quarter16(std::integral_constant<int, 0>());
-        quarter16(std::integral_constant<int, 1>());
-        quarter16(std::integral_constant<int, 2>());
-        quarter16(std::integral_constant<int, 3>());
-      } else if constexpr (QP == 3) {
-        auto quarters16 = [&](auto qa_c, auto qb_c) {
-          constexpr int qa = decltype(qa_c)::value, qb = decltype(qb_c)::value;
-          v4i_t c1a[4], c1b[4];
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt) {
-            c1a[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qa], v4i_t{128, 128, 128, 128}, 0, 0, 0);
-            c1b[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[qb], v4i_t{128, 128, 128, 128}, 0, 0, 0);
-          }
-          uint32_t pa[4][2], pb[4][2];
-          pairs16(c1a, pa);
-          pairs16(c1b, pb);
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              csp[qa][mt][h] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s_t, csp[qa][mt][h]) +
-                                                                __builtin_bit_cast(v2s_t, pa[mt][h]));
-              csp[qb][mt][h] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s_t, csp[qb][mt][h]) +
-                                                                __builtin_bit_cast(v2s_t, pb[mt][h]));
-            }
-          v2l_t Bla, Bha, Blb, Bhb;
-          split16(pa, Bla, Bha);
-          split16(pb, Blb, Bhb);
-          stage2x2B(Bla, Bha, Blb, Bhb, qa_c, qb_c, accB, [] {});
-          __builtin_amdgcn_sched_barrier(0);
-        };
-        quarters16(std::integral_constant<int, 0>(), std::integral_constant<int, 1>());
-        quarters16(std::integral_constant<int, 2>(), std::integral_constant<int, 3>());
-      } else if constexpr (QP == 2) {
-        v4i_t c1[4][4];
-        auto s1 = [&](int q) {
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt) {
-            c1[q][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(d[mt], H[q], v4i_t{128, 128, 128, 128}, 0, 0, 0);
-          }
-        };
-        s1(0);
-        s1(1);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          cs[0][mt] += c1[0][mt];
-          cs[1][mt] += c1[1][mt];
-        }
-        stage2x2(c1[0], c1[1], std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), accB, [&] {
-          s1(2);
-          s1(3);
-        });
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          cs[2][mt] += c1[2][mt];
-          cs[3][mt] += c1[3][mt];
-        }
-        stage2x2(c1[2], c1[3], std::integral_constant<int, 2>(), std::integral_constant<int, 3>(), accB, [] {});
-        __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (QP) {
-        quarters(std::integral_constant<int, 0>(), std::integral_constant<int, 1>());
-        quarters(std::integral_constant<int, 2>(), std::integral_constant<int, 3>());
-      } else {
-        quarter(std::integral_constant<int, 0>());
-        quarter(std::integral_constant<int, 1>());
-        quarter(std::integral_constant<int, 2>());
-        quarter(std::integral_constant<int, 3>());
-      }
+      quarters16(std::integral_constant<int, 0>(), std::integral_constant<int, 1>());
+      quarters16(std::integral_constant<int, 2>(), std::integral_constant<int, 3>());
     }
-    if constexpr (QP == 4) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v2l_t Bl, Bh;
-        split16(csp[q], Bl, Bh);
-        if (q == 0) stage2B(Bl, Bh, std::integral_constant<int, 0>(), accA);
-        if (q == 1) stage2B(Bl, Bh, std::integral_constant<int, 1>(), accA);
-        if (q == 2) stage2B(Bl, Bh, std::integral_constant<int, 2>(), accA);
-        if (q == 3) stage2B(Bl, Bh, std::integral_constant<int, 3>(), accA);
-      }
-    } else if constexpr (QP == 3) {
-      v2l_t Bla, Bha, Blb, Bhb;
-      split16(csp[0], Bla, Bha);
-      split16(csp[1], Blb, Bhb);
-      stage2x2B(Bla, Bha, Blb, Bhb, std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), accA, [] {});
-      split16(csp[2], Bla, Bha);
-      split16(csp[3], Blb, Bhb);
-      stage2x2B(Bla, Bha, Blb, Bhb, std::integral_constant<int, 2>(), std::integral_constant<int, 3>(), accA, [] {});
-    } else if constexpr (QP) {
-      stage2x2(cs[0], cs[1], std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), accA, [] {});
-      stage2x2(cs[2], cs[3], std::integral_constant<int, 2>(), std::integral_constant<int, 3>(), accA, [] {});
-    } else {
-      stage2(cs[0], std::integral_constant<int, 0>(), accA);
-      stage2(cs[1], std::integral_constant<int, 1>(), accA);
-      stage2(cs[2], std::integral_constant<int, 2>(), accA);
-      stage2(cs[3], std::integral_constant<int, 3>(), accA);
-    }
+    v2l_t Bla, Bha, Blb, Bhb;
+    split16(csp[0], Bla, Bha);
+    split16(csp[1], Blb, Bhb);
+    stage2x2B(Bla, Bha, Blb, Bhb, std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), accA);
+    split16(csp[2], Bla, Bha);
+    split16(csp[3], Blb, Bhb);
+    stage2x2B(Bla, Bha, Blb, Bhb, std::integral_constant<int, 2>(), std::integral_constant<int, 3>(), accA);
   }
   if (cur_w >= 0) flush();
   __syncthreads();
@@ -1621,369 +768,9 @@ __device__ __forceinline__ void tile_reg_body(const int8_t* __restrict__ buf, co
   if (add_n && blockIdx.x == 0 && tid == 0) atomicAdd(counts, add_n);  // n, once per job
 }
 
-// 2 waves per SIMD, the next plane prefetched (195 VGPRs, no spill)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<true>(buf, order, z0, nslices, counts, add_n);
-}
-// two quarters per MFMA chain group (QP above)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_qp_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<true, 0, 1>(buf, order, z0, nslices, counts, add_n);
-}
-// the same with the plane sums as packed int16 (QP 3): 167 VGPRs, 3 waves per SIMD; at 3 waves
-// per SIMD without the next plane in flight
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_p16_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<true, 0, 3>(buf, order, z0, nslices, counts, add_n);
-}
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_reg_p16w3np_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<false, 0, 3>(buf, order, z0, nslices, counts, add_n);
-}
-// packed plane sums, one quarter at a time (QP 4), 3 waves per SIMD (at 4 the compiler spills)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_reg_q16w3_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<true, 0, 4>(buf, order, z0, nslices, counts, add_n);
-}
-// the same with the second pair's stage 1 issued before the first pair's squares
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_qp2_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<true, 0, 2>(buf, order, z0, nslices, counts, add_n);
-}
-// the same on the 4-slice interleaved intermediate (the direct MFMA seed's layout)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_ilv_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<true, 0, 1, 4>(buf, order, z0, nslices, counts, add_n);
-}
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_ilv8_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<true, 0, 1, 8>(buf, order, z0, nslices, counts, add_n);
-}
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_ilv16_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<true, 0, 1, 16>(buf, order, z0, nslices, counts, add_n);
-}
-// A/B: 2 waves per SIMD without the prefetch; 3 waves per SIMD (a few registers spilled)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_np_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<false>(buf, order, z0, nslices, counts, add_n);
-}
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile_reg_w3_kernel(
-    const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  tile_reg_body<false>(buf, order, z0, nslices, counts, add_n);
-}
-
-// ---------------------------------------------------------------- MFMA seed (int8 seeds)
-// The seed as a product of two +-1 matrices.  Split the slice z = (r: bits 8..17, zm: bits
-// 4..7, zn: bits 0..3) and each code's hi_k = code >> 14 the same way (r_k, x_k, y_k):
-//   D_z(c) = sum_k (-1)^(r.r_k) (-1)^(zm.x_k) (-1)^(zn.y_k) = sum_k A_r[zm][k] B[k][zn],
-//   A_r[zm][k] = s_k(r) (-1)^(zm.x_k),  B[k][zn] = (-1)^(zn.y_k),  s_k(r) = (-1)^(r.r_k),
-// so one v_mfma_i32_16x16x64_i8 gives a column's 256 slices (zm, zn) of one r from 64
-// codes.  A wave owns 16 consecutive columns; lane l's results are always the slices
-// (zm = 4 (l >> 4) + i, zn = l & 15), i = 0..3, whatever the column, so after the 16
-// columns' products each lane packs 4 slices x 16 columns into four 16-B chunks -- no
-// cross-lane transpose.  The chunks go through a 64-KB LDS stage so that the stores cover
-// whole 128-column lines (stored straight, 64 lanes hit 64 slices: 2x slower).  r runs a Gray walk: one bit b flips per step, and
-// A_r ^= PM_b (0xFE in the bytes of the codes with bit b of r_k set: +1 <-> -1 in int8).
-// The operands (A_0, B, PM per 64-code block) are built once per plan by seed_ops_kernel.
-// A column with 65..127 codes adds a second product for its codes 64.., whose A is rebuilt
-// from the table at every step (rare: a handful of columns at the headline sizes).
-// Per step and wave: 16 MFMAs for 4,096 values, 64 XORs, 48 byte packs, 4 LDS writes, 4 LDS
-// reads, 4 stores; one barrier per step.
-constexpr int kMxRBits = kHiBits - 8;  // r: the walked slice bits
-constexpr int kMxKB = 2;               // 64-code blocks per column (int8: <= 127 codes)
-constexpr int kMxCols = 16;            // columns per wave (one 16-B chunk per slice)
-constexpr int kMxSegBits = 5;          // r values per walk segment = 32
-
-// table layouts: a 16-column block's entries side by side (one base address, immediate offsets)
-__device__ __forceinline__ size_t mx_op(int c, int kb, int lane) {
-  return ((((size_t)(c >> 4) * kMxKB + kb) * 64 + lane) << 4) + (c & 15);
-}
-__device__ __forceinline__ size_t mx_pm(int c, int kb, int b, int g) {
-  return (((((size_t)(c >> 4) * kMxKB + kb) * kMxRBits + b) * 4 + g) << 4) + (c & 15);
-}
-
-
-// One thread per (column, 64-code block, lane): the lane's 16 bytes of A_0 and B in the
-// MFMA operand layout (byte j = code 64 kb + 16 (l >> 4) + j; rows / columns zm = zn =
-// l & 15; 0 past the column's codes), and for lanes 0, 16, 32, 48 the sign planes PM_b of
-// their 16 codes.
-__global__ __launch_bounds__(256) void seed_ops_kernel(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ off,
-                                                       v2l_t* __restrict__ opa, v2l_t* __restrict__ opb,
-                                                       v2l_t* __restrict__ opm) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  const int lane = t & 63, kb = (t >> 6) & (kMxKB - 1), c = t / (64 * kMxKB);
-  if (c >= kLo) return;
-  const int m = (int)(off[c + 1] - off[c]);
-  const uint32_t* h = hi + off[c];
-  const int g = lane >> 4, row = lane & 15;
-  uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, pm[kMxRBits][4] = {};
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int k = 64 * kb + 16 * g + j;
-    if (k < m) {
-      const uint32_t x = h[k];
-      a[j >> 2] |= ((__popc(row & (x >> 4) & 15) & 1) ? 0xFFu : 0x01u) << (8 * (j & 3));
-      b[j >> 2] |= ((__popc(row & x & 15) & 1) ? 0xFFu : 0x01u) << (8 * (j & 3));
-#pragma unroll
-      for (int bb = 0; bb < kMxRBits; ++bb)
-        if ((x >> (8 + bb)) & 1) pm[bb][j >> 2] |= 0xFEu << (8 * (j & 3));
-    }
-  }
-  opa[mx_op(c, kb, lane)] = pack_v2l(a);
-  opb[mx_op(c, kb, lane)] = pack_v2l(b);
-  if (row == 0)
-#pragma unroll
-    for (int bb = 0; bb < kMxRBits; ++bb) opm[mx_pm(c, kb, bb, g)] = pack_v2l(pm[bb]);
-}
-
-// codes 64.. of column c for slice bits 8..17 = r: A_r rebuilt from block 1 of the table
-__device__ __forceinline__ v4i_t seed_mx_block1(const v2l_t* __restrict__ opa, const v2l_t* __restrict__ opb,
-                                                          const v2l_t* __restrict__ opm, int c, int r, int lane,
-                                                          v4i_t acc) {
-  v2l_t a1 = opa[mx_op(c, 1, lane)];
-  for (int bb = 0; bb < kMxRBits; ++bb)
-    if ((r >> bb) & 1) a1 ^= opm[mx_pm(c, 1, bb, lane >> 4)];
-  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, opb[mx_op(c, 1, lane)], acc, 0, 0, 0);
-}
-
-// buf[(z - z0) 2^14 + c] = D_z(c) for z in [z0, z1); workgroup = 128 columns (128 / C waves
-// of C = 16 or 8 columns) x one walk segment of 2^kMxSegBits r values (blockIdx.y).
-// ABL (ablation builds only, wrong results by design): 1 = stores to one contiguous region
-// per workgroup (sequential writes), 2 = no global stores, 3 = no sign updates (A fixed),
-// 4 = no MFMAs, 5 = no LDS stage / barrier and no global stores.
-//
-// W waves of C columns: C x W = 128 columns per workgroup (whole 128-B lines per slice), or
-// C = 8, W = 8: 64 columns (half lines) with two co-resident workgroups per CU and the two
-// halves of every line given to workgroups 8 apart in dispatch order, which the dispatcher
-// places on the same XCD (round robin), so its L2 merges the halves.
-template <int C, int W, int ABL = 0>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(C == 16 ? 2 : 4))) void seed_mx_kernel(
-    const v2l_t* __restrict__ opa, const v2l_t* __restrict__ opb, const v2l_t* __restrict__ opm,
-    const uint32_t* __restrict__ off, int z0, int z1, int8_t* __restrict__ buf) {
-  constexpr int S = 1 << kMxSegBits, K4 = C / 4, RB = C * W, P = RB / 16;  // row bytes, 16-B positions
-  __shared__ v2l_t pm_s[W][kMxSegBits][C][4];  // the walk's planes (block 0)
-  __shared__ uint4 stage[2][256 * P];          // double-buffered store-out: 256 slices x RB bytes
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4;
-  int cblk = blockIdx.x, seg = blockIdx.y;
-  if constexpr (RB == 64) {  // 1-D grid: L = 16 u + 8 h + x (x = XCD slot), unit u * 8 + x = (pair, segment)
-    const int L = blockIdx.x, unit = (L >> 4) * 8 + (L & 7), npairs = kLo / 128;
-    cblk = 2 * (unit % npairs) + ((L >> 3) & 1);
-    seg = unit / npairs;
-  }
-  const int cw = cblk * RB, c0 = cw + wv * C;
-  for (int e = lane; e < C * kMxSegBits * 4; e += 64) {
-    const int cc = e % C, gg = (e / C) & 3, bb = e / (4 * C);
-    pm_s[wv][bb][cc][gg] = opm[mx_pm(c0 + cc, 0, bb, gg)];
-  }
-  unsigned ovf = 0;  // columns with more than 64 codes
-#pragma unroll
-  for (int cc = 0; cc < C; ++cc) ovf |= (unsigned)(off[c0 + cc + 1] - off[c0 + cc] > 64) << cc;
-  ovf = __builtin_amdgcn_readfirstlane(ovf);
-  v2l_t B[C];
-#pragma unroll
-  for (int cc = 0; cc < C; ++cc) B[cc] = opb[mx_op(c0 + cc, 0, lane)];
-  __syncthreads();
-  const int rs = ((z0 >> 8) & ~(S - 1)) + seg * S;  // the launch sizes the grid to the range
-  v2l_t A[C];
-#pragma unroll
-  for (int cc = 0; cc < C; ++cc) A[cc] = opa[mx_op(c0 + cc, 0, lane)];
-  for (int bb = kMxSegBits; bb < kMxRBits; ++bb)
-    if ((rs >> bb) & 1)
-#pragma unroll
-      for (int cc = 0; cc < C; ++cc) A[cc] ^= opm[mx_pm(c0 + cc, 0, bb, g)];
-#pragma unroll 1
-  for (int i = 0; i < S; ++i) {
-    if (i) {
-      const int bb = __builtin_ctz(i);
-#pragma unroll
-      for (int cc = 0; cc < C; ++cc)
-        if constexpr (ABL != 3) A[cc] ^= pm_s[wv][bb][cc][g];
-    }
-    const int r = rs ^ (i ^ (i >> 1));
-    if (r * 256 + 255 < z0 || r * 256 >= z1) continue;
-    uint32_t w[4][K4];  // [slice row 4 g + q][columns 4 k .. 4 k + 3]: low bytes of the products
-#pragma unroll
-    for (int k = 0; k < K4; ++k) {
-      v4i_t acc[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int cc = 4 * k + u;
-        if constexpr (ABL == 4)
-          acc[u] = v4i_t{(int)A[cc][0], (int)(A[cc][0] >> 32), (int)B[cc][1], (int)(B[cc][1] >> 32)};
-        else
-          acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[cc], B[cc], v4i_t{0, 0, 0, 0}, 0, 0, 0);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        w[q][k] = __builtin_amdgcn_perm((uint32_t)acc[1][q], (uint32_t)acc[0][q], 0x0c0c0400u) |
-                  __builtin_amdgcn_perm((uint32_t)acc[3][q], (uint32_t)acc[2][q], 0x04000c0cu);
-    }
-    for (unsigned ov = ovf; ov; ov &= ov - 1) {  // columns with codes 64..: add their products
-      const int cc = __builtin_ctz(ov);
-      const v4i_t a1 = seed_mx_block1(opa, opb, opm, c0 + cc, r, lane, v4i_t{0, 0, 0, 0});
-      const int sh = 8 * (cc & 3);
-#pragma unroll
-      for (int k = 0; k < K4; ++k)
-        if (k == (cc >> 2))
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {  // byte add mod 256: |D| <= 127, so the int8 sum is exact
-            const uint32_t t = ((w[q][k] >> sh) + (uint32_t)a1[q]) & 0xFFu;
-            w[q][k] = (w[q][k] & ~(0xFFu << sh)) | (t << sh);
-          }
-    }
-    if constexpr (ABL == 5) {
-      uint32_t x = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int k = 0; k < K4; ++k) x ^= w[q][k];
-      if (x == 0x12345678u) *reinterpret_cast<uint32_t*>(buf) = x;
-      continue;
-    }
-    // through LDS: each store instruction then covers 8 slices x 128 columns (whole lines)
-    // instead of 64 slices x C columns.  A slice's 128 B hold the waves' C-byte pieces at
-    // XOR-swizzled positions (conflict-free writes); 16-B position p of slice `row` holds
-    // columns 16 (p ^ swz(row)) .. + 15 in order.
-    // swizzle: a slice's C-byte pieces sit at XOR-permuted positions that keep every pair
-    // of 8-B pieces (one 16-B position) in column order; writes are bank-conflict-free
-    auto swz = [](int row) {  // in 16-B positions
-      return C == 16 ? (row & 7) : (RB == 128 ? ((row >> 1) & 7) : ((row >> 2) & 3));
-    };
-    uint4* stg = stage[i & 1];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int row = (4 * g + q) * 16 + (lane & 15);
-      if constexpr (C == 16)
-        stg[row * P + (wv ^ swz(row))] = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
-      else
-        reinterpret_cast<uint2*>(stg)[row * 2 * P + (wv ^ (2 * swz(row)))] = make_uint2(w[q][0], w[q][1]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < 256 * P / (64 * W); ++t) {
-      const int e = t * 64 * W + (int)threadIdx.x, row = e / P;
-      const int z = r * 256 + row;
-      if constexpr (ABL == 1) {
-        *reinterpret_cast<uint4*>(buf + ((int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * S + i) * (256 * RB) + 16 * e) = stg[e];
-      } else if constexpr (ABL == 2) {
-        const uint4 v = stg[e];
-        if ((v.x ^ v.y ^ v.z ^ v.w) == 0x12345678u) *reinterpret_cast<uint4*>(buf) = v;
-      } else if (z >= z0 && z < z1) {
-        *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + cw + 16 * ((e % P) ^ swz(row))) = stg[e];
-      }
-    }
-  }
-}
-
-// The MFMA seed storing straight into the 4-slice interleaved layout (ilv_off): no LDS stage
-// and no barrier.  Lane l's chunk for row q is slice r 256 + (4 (l >> 4) + q) 16 + (l & 15) of
-// the wave's 16-column block, so lanes 4k .. 4k + 3 write one contiguous 64-B piece and the
-// neighbouring wave (the next block) the other half of its 128-B line.  Workgroup = W waves
-// (16 W consecutive columns) x one walk segment of 2^kMxSegBits r values (blockIdx.y).
-template <int W, int G>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2))) void seed_mxd_kernel(
-    const v2l_t* __restrict__ opa, const v2l_t* __restrict__ opb, const v2l_t* __restrict__ opm,
-    const uint32_t* __restrict__ off, int z0, int z1, int8_t* __restrict__ buf) {
-  constexpr int C = 16, S = 1 << kMxSegBits;
-  __shared__ v2l_t pm_s[W][kMxSegBits][C][4];  // the walk's planes (block 0)
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4;
-  const int c0 = (blockIdx.x * W + wv) * C, seg = blockIdx.y;
-  for (int e = lane; e < C * kMxSegBits * 4; e += 64) {
-    const int cc = e % C, gg = (e / C) & 3, bb = e / (4 * C);
-    pm_s[wv][bb][cc][gg] = opm[mx_pm(c0 + cc, 0, bb, gg)];
-  }
-  unsigned ovf = 0;  // columns with more than 64 codes
-#pragma unroll
-  for (int cc = 0; cc < C; ++cc) ovf |= (unsigned)(off[c0 + cc + 1] - off[c0 + cc] > 64) << cc;
-  ovf = __builtin_amdgcn_readfirstlane(ovf);
-  v2l_t B[C];
-#pragma unroll
-  for (int cc = 0; cc < C; ++cc) B[cc] = opb[mx_op(c0 + cc, 0, lane)];
-  const int rs = ((z0 >> 8) & ~(S - 1)) + seg * S;  // the launch sizes the grid to the range
-  v2l_t A[C];
-#pragma unroll
-  for (int cc = 0; cc < C; ++cc) A[cc] = opa[mx_op(c0 + cc, 0, lane)];
-  for (int bb = kMxSegBits; bb < kMxRBits; ++bb)
-    if ((rs >> bb) & 1)
-#pragma unroll
-      for (int cc = 0; cc < C; ++cc) A[cc] ^= opm[mx_pm(c0 + cc, 0, bb, g)];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // pm_s: this wave's own writes
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  int8_t* bw = buf + ilv_off<G>(0, c0 >> 4);
-#pragma unroll 1
-  for (int i = 0; i < S; ++i) {
-    if (i) {
-      const int bb = __builtin_ctz(i);
-#pragma unroll
-      for (int cc = 0; cc < C; ++cc) A[cc] ^= pm_s[wv][bb][cc][g];
-    }
-    const int r = rs ^ (i ^ (i >> 1));
-    if (r * 256 + 255 < z0 || r * 256 >= z1) continue;
-    uint32_t w[4][4];  // [slice row 4 g + q][columns 4 k .. 4 k + 3]: low bytes of the products
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v4i_t acc[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[4 * k + u], B[4 * k + u], v4i_t{0, 0, 0, 0}, 0, 0, 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        w[q][k] = __builtin_amdgcn_perm((uint32_t)acc[1][q], (uint32_t)acc[0][q], 0x0c0c0400u) |
-                  __builtin_amdgcn_perm((uint32_t)acc[3][q], (uint32_t)acc[2][q], 0x04000c0cu);
-    }
-    for (unsigned ov = ovf; ov; ov &= ov - 1) {  // columns with codes 64..: add their products
-      const int cc = __builtin_ctz(ov);
-      const v4i_t a1 = seed_mx_block1(opa, opb, opm, c0 + cc, r, lane, v4i_t{0, 0, 0, 0});
-      const int sh = 8 * (cc & 3);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (k == (cc >> 2))
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {  // byte add mod 256: |D| <= 127, so the int8 sum is exact
-            const uint32_t t = ((w[q][k] >> sh) + (uint32_t)a1[q]) & 0xFFu;
-            w[q][k] = (w[q][k] & ~(0xFFu << sh)) | (t << sh);
-          }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int z = r * 256 + (4 * g + q) * 16 + (lane & 15);
-      if (z >= z0 && z < z1)
-        *reinterpret_cast<uint4*>(bw + ilv_off<G>(z - z0, 0)) = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
-    }
-  }
-}
-
 __global__ void max_column_kernel(const uint32_t* __restrict__ cnt, unsigned* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < kLo) atomicMax(out, cnt[c]);
-}
-
-__global__ void add_kernel(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
-
-// the MFMA seed's tables inside st.d_mx: A_0 and B [column][block][lane], PM [column][block][bit][lane group]
-struct MxTables {
-  v2l_t *a, *b, *m;
-};
-constexpr size_t kMxOpBytes = (size_t)kLo * kMxKB * 64 * sizeof(v2l_t);
-constexpr size_t kMxBytes = 2 * kMxOpBytes + (size_t)kLo * kMxKB * kMxRBits * 4 * sizeof(v2l_t);
-MxTables mx_tables(const State& st) {
-  char* p = static_cast<char*>(st.d_mx);
-  return MxTables{reinterpret_cast<v2l_t*>(p), reinterpret_cast<v2l_t*>(p + kMxOpBytes),
-                  reinterpret_cast<v2l_t*>(p + 2 * kMxOpBytes)};
 }
 
 template <typename T>
@@ -1992,102 +779,9 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
   const int walks = (z1 - (z0 & ~(kWalk - 1)) + kWalk - 1) / kWalk;
   // 16 walks per workgroup for a full chunk (measured best at 65,536 slices); smaller chunks
   // keep >= 64 workgroup rows so the grid still fills the chip
-  int per_wg = std::max(1, std::min(kSeedWalks, walks / 64));
-#ifdef SCT_ABLATION
-  if (const char* e = getenv("SCT_SEED_WALKS")) per_wg = std::max(1, atoi(e));
-#endif
+  const int per_wg = std::max(1, std::min(kSeedWalks, walks / 64));
   const dim3 sgrid(kLo / 256, (unsigned)((walks + per_wg - 1) / per_wg));
-#ifdef SCT_ABLATION
-  static const int sabl = getenv("SCT_SEED_ABL") ? atoi(getenv("SCT_SEED_ABL")) : 0;
-  if (sabl == 1)
-    hipLaunchKernelGGL((seed_kernel<T, 1>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
-                       st.max_groups, z0, z1, buf);
-  if (sabl == 2)
-    hipLaunchKernelGGL((seed_kernel<T, 2>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
-                       st.max_groups, z0, z1, buf);
-  if (sabl == 3)
-    hipLaunchKernelGGL((seed_kernel<T, 3>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
-                       st.max_groups, z0, z1, buf);
-  if (sabl == 4)
-    hipLaunchKernelGGL((seed_kernel<T, 4>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
-                       st.max_groups, z0, z1, buf);
-  if (sabl == 7 && sizeof(T) == 1)
-    hipLaunchKernelGGL(seed_wide_kernel<T>, dim3(kLo / 512, sgrid.y), dim3(512), 0, s, st.d_planes, st.d_gofs,
-                       st.d_off, st.max_groups, z0, z1, buf);
-  if (sabl == 8)
-    hipLaunchKernelGGL((seed_kernel<T, 8>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
-                       st.max_groups, z0, z1, buf);
-  if (sabl == 9)
-    hipLaunchKernelGGL((seed_kernel<T, 9>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
-                       st.max_groups, z0, z1, buf);
-  if (sabl == 10)
-    hipLaunchKernelGGL((seed_kernel<T, 10>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
-                       st.max_groups, z0, z1, buf);
-  if (sabl == 6)
-    hipLaunchKernelGGL((seed_kernel<T, 6>), sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
-                       st.max_groups, z0, z1, buf);
-  if (sabl == 5)
-    hipLaunchKernelGGL(seed_r1_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
-                       st.max_groups, z0, z1, buf);
-  if (sabl < 1 || sabl > 10)
-#endif
-  {
-    if (sizeof(T) == 1 && st.d_mx && st.ilv) {
-      const MxTables mx = mx_tables(st);
-      const int ra = (z0 >> 8) & ~((1 << kMxSegBits) - 1), rend = ((z1 - 1) >> 8) + 1;
-      const int nseg = (rend - ra + (1 << kMxSegBits) - 1) >> kMxSegBits;
-      constexpr int W = 4;
-      const dim3 xg(kLo / (16 * W), (unsigned)nseg);
-      int8_t* b8 = reinterpret_cast<int8_t*>(buf);
-      if (st.ilv == 16)
-        hipLaunchKernelGGL((seed_mxd_kernel<W, 16>), xg, dim3(64 * W), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1, b8);
-      else if (st.ilv == 8)
-        hipLaunchKernelGGL((seed_mxd_kernel<W, 8>), xg, dim3(64 * W), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1, b8);
-      else
-        hipLaunchKernelGGL((seed_mxd_kernel<W, 4>), xg, dim3(64 * W), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1, b8);
-    } else if (sizeof(T) == 1 && st.d_mx) {
-      const MxTables mx = mx_tables(st);
-      const int ra = (z0 >> 8) & ~((1 << kMxSegBits) - 1), rend = ((z1 - 1) >> 8) + 1;
-      const int nseg = (rend - ra + (1 << kMxSegBits) - 1) >> kMxSegBits;
-      const dim3 mgrid(kLo / 128, (unsigned)nseg);
-      const dim3 hgrid((unsigned)(2 * (kLo / 128) * nseg));  // the 64-column form: paired, 1-D
-      int8_t* b8 = reinterpret_cast<int8_t*>(buf);
-#define SCT_MX_L(C_, W_, A_, G_) \
-  hipLaunchKernelGGL((seed_mx_kernel<C_, W_, A_>), G_, dim3(64 * W_), 0, s, mx.a, mx.b, mx.m, st.d_off, z0, z1, b8)
-#ifdef SCT_ABLATION
-      // SCT_MX_ABL = ablation variant v on the shipped form (see seed_mx_kernel's ABL list)
-      if (const char* e = getenv("SCT_MX_ABL")) {
-        switch (atoi(e)) {
-          case 1: SCT_MX_L(8, 8, 1, hgrid); break;
-          case 2: SCT_MX_L(8, 8, 2, hgrid); break;
-          case 5: SCT_MX_L(8, 8, 5, hgrid); break;
-          default: SCT_MX_L(8, 8, 0, hgrid); break;
-        }
-        SCT_LAUNCH_CHECK();
-        return SCT_OK;
-      }
-#endif
-      // SCT_SPECTRAL_MX_FORM: 2 = 8-column waves x 16 (128-column workgroups, default: 0.354-
-      // 0.360 ms per launch), 1 = 16-column waves x 8 (0.383), 0 = 8-column waves x 8 with
-      // XCD-paired 64-column workgroups, two per CU (0.419: the half-line writes cost more
-      // than the second workgroup hides)
-      if (st.mx_form == 1)
-        SCT_MX_L(16, 8, 0, mgrid);
-      else if (st.mx_form == 0)
-        SCT_MX_L(8, 8, 0, hgrid);
-      else
-        SCT_MX_L(8, 16, 0, mgrid);
-#undef SCT_MX_L
-    } else if (sizeof(T) == 1 && st.seed_db)
-      hipLaunchKernelGGL(seed_db_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, st.max_groups,
-                         z0, z1, buf);
-    else if (sizeof(T) == 1 && st.seed_spread)
-      hipLaunchKernelGGL(seed_spread_kernel, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
-                         st.max_groups, z0, z1, reinterpret_cast<int8_t*>(buf));
-    else
-      hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, st.max_groups,
-                         z0, z1, buf);
-  }
+  hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, z0, z1, buf);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
@@ -2095,103 +789,30 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
 template <typename T>
 int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s, unsigned long long add_n = 0) {
   T* buf = reinterpret_cast<T*>(st.d_buf);
-  const dim3 grid((unsigned)std::min(st.grid * (sizeof(T) == 1 ? 3 : 2), z1 - z0));
-#ifdef SCT_ABLATION
-  static const int abl = getenv("SCT_SPECTRAL_ABL") ? atoi(getenv("SCT_SPECTRAL_ABL")) : 0;
-  if (abl == 1) hipLaunchKernelGGL((tile_kernel<T, 1>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, 0ull);
-  if (abl == 2) hipLaunchKernelGGL((tile_kernel<T, 2>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, 0ull);
-  if (abl == 3) hipLaunchKernelGGL((tile_kernel<T, 3>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, 0ull);
-  if (abl == 4) hipLaunchKernelGGL((tile_kernel<T, 4>), grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, 0ull);
-  if (abl >= 1 && abl <= 4) {
-    if (add_n) hipLaunchKernelGGL(add_kernel, dim3(1), dim3(1), 0, s, counts, add_n);
-    SCT_LAUNCH_CHECK();
-    return SCT_OK;
-  }
-#endif
   if constexpr (sizeof(T) == 1) {
-    if (st.mfma) {
-      // an aligned power-of-two range goes in digit-weight order (table 2^b at offset 2^b)
-      const int ns = z1 - z0;
-      const uint16_t* order =
-          ((ns & (ns - 1)) == 0 && ns <= kMaxOrder && z0 % ns == 0) ? st.d_order + ns : nullptr;
-      const dim3 mgrid((unsigned)std::min(st.grid * st.tile_wgs, z1 - z0));
-#ifdef SCT_ABLATION
-      static const int mabl = getenv("SCT_SPECTRAL_ABL") ? atoi(getenv("SCT_SPECTRAL_ABL")) : 0;
-      if ((mabl >= 11 && mabl <= 21) || (mabl >= 31 && mabl <= 35)) {
-        if (mabl == 11) hipLaunchKernelGGL(tile_mfma_kernel<1>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
-        if (mabl == 12) hipLaunchKernelGGL(tile_mfma_kernel<2>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
-        if (mabl == 13) hipLaunchKernelGGL(tile_mfma_kernel<3>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
-        if (mabl == 14) hipLaunchKernelGGL(tile_mfma_kernel<4>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
-        if (mabl == 15) hipLaunchKernelGGL(tile_mfma_kernel<5>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
-        if (mabl == 20) hipLaunchKernelGGL(tile_mfma2_pf_st_kernel<20>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
-        if (mabl == 31) hipLaunchKernelGGL(tile_mfma2_pf_abl_kernel<1>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
-        if (mabl == 32) hipLaunchKernelGGL(tile_mfma2_pf_abl_kernel<2>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
-        if (mabl == 33) hipLaunchKernelGGL(tile_mfma2_pf_abl_kernel<3>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
-        if (mabl == 34) hipLaunchKernelGGL(tile_mfma2_pf_abl_kernel<4>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
-        if (mabl == 35) hipLaunchKernelGGL(tile_mfma2_pf_abl_kernel<5>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
-        if (mabl == 21) hipLaunchKernelGGL(tile_mfma2_pf_st_kernel<40>, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
-        if (mabl == 17 || mabl == 19) {  // two-stage without prefetch / the one-stage kernel
-          int per_cu = 0;
-          if (mabl == 17) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma2_kernel, 256, 0);
-          else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma_kernel<0>, 256, 0);
-          const dim3 g2((unsigned)std::min(st.grid * std::max(per_cu, 1), z1 - z0));
-          if (mabl == 17) hipLaunchKernelGGL(tile_mfma2_kernel, g2, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, 0ull);
-          else hipLaunchKernelGGL(tile_mfma_kernel<0>, g2, dim3(256), 0, s, buf, order, z0, z1 - z0, counts);
-        }
-        if (add_n) hipLaunchKernelGGL(add_kernel, dim3(1), dim3(1), 0, s, counts, add_n);
-        SCT_LAUNCH_CHECK();
-        return SCT_OK;
-      }
-#endif
-      if (st.ilv) {
-        const int G = st.ilv, ts = G / 4;  // G-slice groups, in digit-weight order when aligned
-        const int ng = (z1 - z0 + G - 1) / G;
-        const uint16_t* gorder = ((ng & (ng - 1)) == 0 && ng <= kMaxOrder && z0 % G == 0 && (z0 / G) % ng == 0)
-                                     ? st.d_order + ng : nullptr;
-        // teams of ts workgroups 8 apart in dispatch order; whole rounds of 8 teams
-        const int teams = std::max(1, std::min(st.grid * st.tile_reg_wgs / ts, ng));
-        const dim3 igrid((unsigned)(8 * ts * ((teams + 7) / 8)));
-        const void* kf = G == 16 ? (const void*)tile_reg_ilv16_kernel
-                         : G == 8 ? (const void*)tile_reg_ilv8_kernel : (const void*)tile_reg_ilv_kernel;
-        void* args[] = {(void*)&buf, (void*)&gorder, (void*)&z0, nullptr, (void*)&counts, (void*)&add_n};
-        int ns = z1 - z0;
-        args[3] = (void*)&ns;
-        SCT_HIP(hipLaunchKernel(kf, igrid, dim3(256), args, 0, s));
-      } else if (st.tile_reg) {
-        const dim3 rgrid((unsigned)std::max(1, std::min(st.grid * st.tile_reg_wgs, (z1 - z0 + 3) / 4)));
-        if (st.tile_reg == 2)
-          hipLaunchKernelGGL(tile_reg_np_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
-        else if (st.tile_reg == 3)
-          hipLaunchKernelGGL(tile_reg_w3_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
-        else if (st.tile_reg == 4)
-          hipLaunchKernelGGL(tile_reg_qp_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
-        else if (st.tile_reg == 5)
-          hipLaunchKernelGGL(tile_reg_qp2_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
-        else if (st.tile_reg == 6)
-          hipLaunchKernelGGL(tile_reg_p16_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
-        else if (st.tile_reg == 8)
-          hipLaunchKernelGGL(tile_reg_p16w3np_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
-        else if (st.tile_reg == 9)
-          hipLaunchKernelGGL(tile_reg_q16w3_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
-
-        else
-          hipLaunchKernelGGL(tile_reg_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
-      } else {
-        hipLaunchKernelGGL(tile_mfma2_pf_kernel, mgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
-      }
-      SCT_LAUNCH_CHECK();
-      return SCT_OK;
-    }
+    // an aligned power-of-two range goes in digit-weight order (table 2^b at offset 2^b)
+    const int ns = z1 - z0;
+    const uint16_t* order = ((ns & (ns - 1)) == 0 && ns <= kMaxOrder && z0 % ns == 0) ? st.d_order + ns : nullptr;
+    const dim3 rgrid((unsigned)std::max(1, std::min(st.grid * st.tile_wgs, (z1 - z0 + 3) / 4)));
+    hipLaunchKernelGGL(tile_reg_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+  } else {
+    const dim3 grid((unsigned)std::min(st.grid * 2, z1 - z0));
+    hipLaunchKernelGGL(tile_kernel<T>, grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, add_n);
   }
-  hipLaunchKernelGGL(tile_kernel<T>, grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, add_n);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
 
 template <typename T>
 int launch_chunk(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s, unsigned long long add_n) {
-  const int rc = launch_seed<T>(st, z0, z1, s);
-  return rc != SCT_OK ? rc : launch_tile<T>(st, z0, z1, counts, s, add_n);
+  hipEvent_t t0 = st.timer ? st.timer->start(s) : nullptr;
+  int rc = launch_seed<T>(st, z0, z1, s);
+  if (st.timer) st.timer->stop(s, t0, sct::LaunchTimer::SEED);
+  if (rc != SCT_OK) return rc;
+  t0 = st.timer ? st.timer->start(s) : nullptr;
+  rc = launch_tile<T>(st, z0, z1, counts, s, add_n);
+  if (st.timer) st.timer->stop(s, t0, sct::LaunchTimer::TILE);
+  return rc;
 }
 
 // Bench aid: seed and tile kernels timed apart, each as `repeats` back-to-back launches on
@@ -2230,7 +851,7 @@ int time_chunk(State& st, int z0, int z1, unsigned long long* counts, int repeat
 int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus) {
   st.n = n;
   st.chunk = std::max<int64_t>(kWalk, std::min<int64_t>(chunk, kSlices));
-  st.grid = std::max(1, cus);  // CUs; the tile kernel runs 3 workgroups per CU (int8), else 2
+  st.grid = std::max(1, cus);  // CUs; the tile kernels' persistent grids are sized from it
   if (n < 2) return SCT_OK;
   SCT_HIP(hipMalloc(&st.d_hi, (size_t)n * 4));
   SCT_HIP(hipMalloc(&st.d_off, (size_t)(kLo + 1) * 4));
@@ -2249,47 +870,10 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   SCT_HIP(hipMemcpy(&maxm, dmax.p, 4, hipMemcpyDeviceToHost));
   st.max_m = maxm;
   st.elem_bytes = maxm <= 127 ? 1 : (maxm <= 32767 ? 2 : 4);
-  const char* mf = getenv("SCT_SPECTRAL_MFMA");  // 0: VALU tile kernel for int8 seeds too
-  st.mfma = !(mf && atoi(mf) == 0);
-  bool seed_mx = true;
-  {
-    int per_cu = 0;  // resident MFMA-tile workgroups per CU (VGPR / LDS bound)
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_mfma2_pf_kernel, 256, 0) != hipSuccess ||
-        per_cu <= 0)
-      per_cu = 2;
-    st.tile_wgs = per_cu;
-    // seed variant (int8): the Gray-walk popcount seed by default; "mx" = the MFMA seed,
-    // "spread" = the walk with its stores spread over the walk
-    const char* sv = getenv("SCT_SPECTRAL_SEED");
-    st.seed_spread = sv && !strcmp(sv, "spread");
-    st.seed_db = sv && !strcmp(sv, "db");
-    seed_mx = sv && (!strcmp(sv, "mx") || !strcmp(sv, "mxd"));
-    st.ilv = sv && !strcmp(sv, "mxd") ? 4 : 0;
-    if (st.ilv)
-      if (const char* g = getenv("SCT_SPECTRAL_ILV")) st.ilv = atoi(g) == 16 ? 16 : atoi(g) == 8 ? 8 : 4;
-    if (const char* f = getenv("SCT_SPECTRAL_MX_FORM")) st.mx_form = atoi(f);
-    // tile variant: the register-resident tile by default (r02 A/B on the 737K headline: 0.304 vs
-    // 0.320 ms per 65536 slices, count 2.39 vs 2.47 ms); "mfma2" = the LDS-exchange tile,
-    // reg_np / reg_w3 = register-tile ablations
-    const char* tv = getenv("SCT_SPECTRAL_TILE");
-    // (round 2, later: "reg_p16" is the default -- two quarters' MFMA chains interleaved and the
-    // plane sums as packed int16, 167 VGPRs, 3 waves per SIMD: 0.267-0.281 ms against 0.287-0.293
-    // for "reg_qp" (pairs, int32 sums, 2 waves per SIMD) and 0.291-0.306 for "reg" on the same boxes)
-    st.tile_reg = !tv ? 6 : !strcmp(tv, "mfma2") ? 0 : !strcmp(tv, "reg_np") ? 2 : !strcmp(tv, "reg_w3") ? 3
-                : !strcmp(tv, "reg") ? 1 : !strcmp(tv, "reg_qp2") ? 5 : !strcmp(tv, "reg_p16") ? 6
-                : !strcmp(tv, "reg_p16w3np") ? 8 : !strcmp(tv, "reg_q16w3") ? 9 : !strcmp(tv, "reg_qp") ? 4 : 6;
-    int per_cu_reg = 0;  // its resident workgroups per CU
-    const void* kf = st.tile_reg == 2 ? (const void*)tile_reg_np_kernel
-                     : st.tile_reg == 3 ? (const void*)tile_reg_w3_kernel
-                     : st.tile_reg == 4 ? (const void*)tile_reg_qp_kernel
-                     : st.tile_reg == 5 ? (const void*)tile_reg_qp2_kernel
-                     : st.tile_reg == 6 ? (const void*)tile_reg_p16_kernel
-                     : st.tile_reg == 8 ? (const void*)tile_reg_p16w3np_kernel
-                     : st.tile_reg == 9 ? (const void*)tile_reg_q16w3_kernel : (const void*)tile_reg_kernel;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_reg, kf, 256, 0) != hipSuccess || per_cu_reg <= 0)
-      per_cu_reg = 2;
-    st.tile_reg_wgs = per_cu_reg;
-  }
+  int per_cu = 0;  // resident register-tile workgroups per CU (VGPR bound: 3)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_reg_kernel, 256, 0) != hipSuccess || per_cu <= 0)
+    per_cu = 2;
+  st.tile_wgs = per_cu;
   {
     // for every power of two L <= 2^16: the offsets [0, L) sorted by digit weight, stored
     // at [L, 2L) (an aligned range of L slices adds a constant weight to all of them)
@@ -2302,39 +886,25 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
     SCT_HIP(hipMalloc(&st.d_order, order.size() * 2));
     SCT_HIP(hipMemcpy(st.d_order, order.data(), order.size() * 2, hipMemcpyHostToDevice));
   }
-  if (const char* w = getenv("SCT_SPECTRAL_BYTES")) {  // test hook: wider than needed
-    const int b = atoi(w);
-    if ((b == 2 || b == 4) && b > st.elem_bytes) st.elem_bytes = b;
-  }
   st.max_groups = sct::ceil_div(n, 32) + kLo;
   SCT_HIP(hipMalloc(&st.d_gofs, (size_t)(kLo + 1) * 4));
   SCT_HIP(hipMalloc(&st.d_hist, (size_t)kSortWGs * kLo * 4));
   SCT_HIP(hipMalloc(&st.d_planes, (size_t)st.max_groups * kPlaneWords * 4));
-  if (st.elem_bytes != 1) st.ilv = 0;
   const size_t buf_bytes = (size_t)((st.chunk + 15) & ~15ll) * kLo * st.elem_bytes;  // whole 16-slice groups
   SCT_HIP(hipMalloc(&st.d_buf, buf_bytes));
-  if (seed_mx && st.elem_bytes == 1) SCT_HIP(hipMalloc(&st.d_mx, kMxBytes));  // 84 MB
-  if (const char* ov = getenv("SCT_SPECTRAL_OVERLAP")) st.overlap = atoi(ov) != 0;
-  if (st.overlap) {
-    SCT_HIP(hipMalloc(&st.d_buf2, buf_bytes));
-    SCT_HIP(hipStreamCreateWithFlags(&st.side, hipStreamNonBlocking));
-    for (auto& e : st.ev) SCT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
   return SCT_OK;
 }
 
 void destroy(State& st) {
-  for (void* p : {(void*)st.d_hi, (void*)st.d_off, (void*)st.d_cnt, (void*)st.d_gofs, (void*)st.d_planes, (void*)st.d_hist,
-                  st.d_buf, (void*)st.d_order, st.d_mx, st.d_buf2})
+  for (void* p : {(void*)st.d_hi, (void*)st.d_off, (void*)st.d_cnt, (void*)st.d_gofs, (void*)st.d_planes,
+                  (void*)st.d_hist, st.d_buf, (void*)st.d_order})
     if (p) (void)hipFree(p);
-  for (auto e : st.ev)
-    if (e) (void)hipEventDestroy(e);
-  if (st.side) (void)hipStreamDestroy(st.side);
   st = State();
 }
 
 int build(State& st, const uint64_t* d_codes, hipStream_t s) {
   if (st.n < 2) return SCT_OK;
+  hipEvent_t t0 = st.timer ? st.timer->start(s) : nullptr;
   hipLaunchKernelGGL(column_hist_wg_kernel, dim3(kSortWGs), dim3(kSortThreads), 0, s, d_codes, st.n, st.d_hist);
   SCT_LAUNCH_CHECK();
   hipLaunchKernelGGL(column_prefix_kernel, dim3(kLo / 256), dim3(256), 0, s, st.d_hist, kSortWGs, st.d_cnt);
@@ -2352,12 +922,7 @@ int build(State& st, const uint64_t* d_codes, hipStream_t s) {
                        st.d_hi, st.d_off, st.d_gofs, st.max_groups, st.d_planes);
   }
   SCT_LAUNCH_CHECK();
-  if (st.d_mx) {
-    const MxTables mx = mx_tables(st);
-    hipLaunchKernelGGL(seed_ops_kernel, dim3(kLo * kMxKB * 64 / 256), dim3(256), 0, s, st.d_hi, st.d_off, mx.a, mx.b,
-                       mx.m);
-    SCT_LAUNCH_CHECK();
-  }
+  if (st.timer) st.timer->stop(s, t0, sct::LaunchTimer::BUILD);
   return SCT_OK;
 }
 
@@ -2365,34 +930,6 @@ int count(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_count
   SCT_CHECK(0 <= z_begin && z_begin <= z_end && z_end <= kSlices, "slice range [%lld, %lld)",
             (long long)z_begin, (long long)z_end);
   if (st.n < 2 || z_begin == z_end) return SCT_OK;
-  if (st.overlap && z_end - z_begin > st.chunk) {
-    // chunk j's seed runs on the side stream into buffer j % 2 once chunk j-2's tile has
-    // released it; chunk j's tile runs on s after that seed.  Launch order alternates so
-    // that seed j+1 is queued before tile j.
-    void* bufs[2] = {st.d_buf, st.d_buf2};
-    SCT_HIP(hipEventRecord(st.ev[4], s));
-    SCT_HIP(hipStreamWaitEvent(st.side, st.ev[4], 0));
-    int j = 0;
-    for (int64_t z0 = z_begin; z0 < z_end; z0 += st.chunk, ++j) {
-      const int z1 = (int)std::min<int64_t>(z_end, z0 + st.chunk);
-      if (j >= 2) SCT_HIP(hipStreamWaitEvent(st.side, st.ev[j & 1], 0));
-      st.d_buf = bufs[j & 1];
-      int rc = st.elem_bytes == 1   ? launch_seed<int8_t>(st, (int)z0, z1, st.side)
-               : st.elem_bytes == 2 ? launch_seed<int16_t>(st, (int)z0, z1, st.side)
-                                    : launch_seed<int32_t>(st, (int)z0, z1, st.side);
-      if (rc == SCT_OK) rc = hipEventRecord(st.ev[2 + (j & 1)], st.side) == hipSuccess ? SCT_OK : SCT_E_HIP;
-      if (rc == SCT_OK) rc = hipStreamWaitEvent(s, st.ev[2 + (j & 1)], 0) == hipSuccess ? SCT_OK : SCT_E_HIP;
-      const unsigned long long add_n = z0 == 0 ? (unsigned long long)st.n : 0ull;
-      if (rc == SCT_OK)
-        rc = st.elem_bytes == 1   ? launch_tile<int8_t>(st, (int)z0, z1, d_counts, s, add_n)
-             : st.elem_bytes == 2 ? launch_tile<int16_t>(st, (int)z0, z1, d_counts, s, add_n)
-                                  : launch_tile<int32_t>(st, (int)z0, z1, d_counts, s, add_n);
-      if (rc == SCT_OK) rc = hipEventRecord(st.ev[j & 1], s) == hipSuccess ? SCT_OK : SCT_E_HIP;
-      st.d_buf = bufs[0];
-      if (rc != SCT_OK) return rc;
-    }
-    return SCT_OK;
-  }
   for (int64_t z0 = z_begin; z0 < z_end; z0 += st.chunk) {
     const int z1 = (int)std::min<int64_t>(z_end, z0 + st.chunk);
     // d_counts[0] += n by the job's first tile launch (the range holding slice 0)

@@ -11,8 +11,10 @@ inverts the summed counts to the exact histogram.  Integer sums are order
 independent, so the result is bit-identical for any W.
 
 Nearest-whitelist correction (config 4) and the batch encoder split their records into
-contiguous ranges per rank with the whitelist replicated; ``gather_ranges`` all-gathers
-the per-rank results (no reduction).
+contiguous ranges per rank with the whitelist replicated and no collective:
+each rank reads only its own range of the input and keeps its own slice of the results.
+``gather_ranges`` (opt-in) all-gathers the slices when a caller wants the whole result
+on every rank.
 
 The reference (barcode.py:39-46) has no parallelism at all; this is new.
 """
@@ -145,9 +147,16 @@ class ShardedAllPairs:
             return []
         if not hasattr(self, "_pipe"):
             dev = self.device
-            n, code_bits, scheme = self._plan_args
+            n, code_bits, _ = self._plan_args
+            # the second plan takes the first one's RESOLVED scheme (AUTO resolves by n and the
+            # launch-shape knobs, which may have changed since), so both share one geometry
+            twin = _lib.AllPairsPlan(self.d_codes.data_ptr(), n, code_bits, scheme=self.plan.scheme)
+            if (twin.scheme, twin.items, twin.ncounts, twin.nbins) != \
+                    (self.plan.scheme, self.plan.items, self.plan.ncounts, self.plan.nbins):
+                twin.close()
+                raise RuntimeError("second plan's geometry differs from the first's")
             self._pipe = {
-                "plans": [self.plan, _lib.AllPairsPlan(self.d_codes.data_ptr(), n, code_bits, scheme=scheme)],
+                "plans": [self.plan, twin],
                 "build": torch.cuda.Stream(dev),
                 "built": [torch.cuda.Event() for _ in range(2)],
                 "counts": [self.counts, torch.zeros_like(self.counts)],
@@ -222,6 +231,21 @@ class ShardedAllPairs:
 
     def reset_timings(self):
         self._t = {k: [] for k in self._t}
+
+    def plans(self):
+        """The plan(s) this rank's steps launch on: one for step(), two once run() pipelined."""
+        return self._pipe["plans"] if hasattr(self, "_pipe") else [self.plan]
+
+    def kernel_timing(self, mode):
+        """Per-launch HIP-event timing of the steps' kernels on the streams they run on
+        (sct_allpairs_timing over every plan): mode 1 start, 0 stop, 2 read.  Returns
+        {kind: (ms summed, launches)} summed over the plans."""
+        tot = {}
+        for p in self.plans():
+            for k, (ms, n) in p.timing(mode).items():
+                a, b = tot.get(k, (0.0, 0))
+                tot[k] = (a + ms, b + n)
+        return tot
 
     def timings(self):
         return {k: (float(np.mean(v)) if v else None) for k, v in self._t.items()}
@@ -307,28 +331,40 @@ def gather_ranges(local, n, group=None):
                            for p, s in zip(parts, sizes)])
 
 
-def nearest_sharded(kind, whitelist, queries, max_d=1, code_bits=None, group=None, fn=None):
+def nearest_sharded(kind, whitelist, queries, max_d=1, code_bits=None, group=None, fn=None, gather=False):
     """Nearest-whitelist correction with the queries split into contiguous ranges, one per
-    rank (the whitelist replicated); returns the whole (index, dist) on every rank.  ``fn``
-    is the per-rank computation (default: the GPU path, ``_lib.nearest``)."""
+    rank, and the whitelist replicated.  Returns ``(begin, end, index, dist)``: this rank's
+    range ``item_range(len(queries), rank, W)`` and its results, with no collective (SURVEY
+    8(e): each GPU keeps its own result slice).  Only ``queries[begin:end]`` is read, so
+    ``queries`` may be a np.memmap of a file (or any sliceable sequence of uint64 codes).
+    ``gather=True`` all-gathers the slices into the whole (index, dist) on every rank
+    (then begin, end = 0, len(queries)).  ``fn`` is the per-rank computation (default: the
+    GPU path, ``_lib.nearest``)."""
     world, rank = _group_info(group)
-    q = np.ascontiguousarray(queries, dtype=np.uint64).reshape(-1)
-    b, e = item_range(q.size, rank, world)
+    nq = len(queries)
+    b, e = item_range(nq, rank, world)
+    q = np.ascontiguousarray(queries[b:e], dtype=np.uint64).reshape(-1)
     if code_bits is None:  # the block split's width, as barcode.nearest_whitelist picks it
         wl = np.ascontiguousarray(whitelist, dtype=np.uint64).reshape(-1)
         orv = int(np.bitwise_or.reduce(wl)) if wl.size else 0
         code_bits = min(64, max(orv.bit_length(), kind * (max_d + 1), 1))
-    idx, dist_ = (fn or _lib.nearest)(kind, whitelist, q[b:e], max_d, code_bits)
-    return gather_ranges(np.asarray(idx, dtype=np.int32), q.size, group), \
-        gather_ranges(np.asarray(dist_, dtype=np.uint8), q.size, group)
+    idx, dist_ = (fn or _lib.nearest)(kind, whitelist, q, max_d, code_bits)
+    idx, dist_ = np.asarray(idx, dtype=np.int32), np.asarray(dist_, dtype=np.uint8)
+    if gather:
+        return 0, nq, gather_ranges(idx, nq, group), gather_ranges(dist_, nq, group)
+    return b, e, idx, dist_
 
 
-def encode_sharded(kind, seqs, L, group=None, fn=None):
+def encode_sharded(kind, seqs, L, group=None, fn=None, gather=False):
     """TwoBit / ThreeBit batch encode with the records split into contiguous ranges, one per
-    rank; returns what ``fn`` (default ``_lib.encode``: codes, gc, flags) returns, gathered
-    over the ranks."""
+    rank.  Returns ``(begin, end, *outs)``: this rank's range and what ``fn`` (default
+    ``_lib.encode``: codes, gc, flags) returns for ``seqs[begin:end]`` -- the only records
+    this rank reads (``seqs`` may be a np.memmap) -- with no collective.  ``gather=True``
+    all-gathers every output over the ranks instead."""
     world, rank = _group_info(group)
-    seqs = np.asarray(seqs)
-    b, e = item_range(len(seqs), rank, world)
-    outs = (fn or _lib.encode)(kind, seqs[b:e], L)
-    return tuple(gather_ranges(None if o is None else np.asarray(o), len(seqs), group) for o in outs)
+    nrec = len(seqs)
+    b, e = item_range(nrec, rank, world)
+    outs = (fn or _lib.encode)(kind, np.asarray(seqs[b:e]), L)
+    if gather:
+        return (0, nrec) + tuple(gather_ranges(None if o is None else np.asarray(o), nrec, group) for o in outs)
+    return (b, e) + tuple(outs)

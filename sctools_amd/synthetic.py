@@ -10,12 +10,18 @@ up until it holds exactly ``n`` unique codes.
 
 import numpy as np
 
-#: BASELINE.json configs -> (n, L, seed)
+#: BASELINE.json configs -> (n, L, seed) of the whitelist (config 3 = config 2's set over 2/4/8
+#: GPUs; config 4's whitelist is config 2's set, ThreeBit-encoded, queried by CONFIG4_QUERIES
+#: observed barcodes; config 5 also streams CONFIG5_READS 28-bp reads)
 CONFIGS = {
     1: (10_000, 16, 1),
     2: (737_280, 16, 737_280),
+    3: (737_280, 16, 737_280),
+    4: (737_280, 16, 737_280),
     5: (3_686_400, 16, 5),
 }
+CONFIG4_QUERIES = 100_000_000
+CONFIG5_READS, CONFIG5_READ_LENGTH = 1_000_000_000, 28
 
 
 def whitelist_codes(n, barcode_length=16, seed=1):

@@ -1,7 +1,7 @@
 """CPU: host-side semantics of sctools_amd.barcode.Barcodes that need no kernel -- the
 key array is rebuilt from the mapping on every call (no stale cache), non-integer keys
 raise the reference's own TypeError from `a ^ b` (encodings.py:117 via barcode.py:42-43),
-keys >= 2^64 become multi-limb rows."""
+keys >= 2^64 become multi-limb rows, all-negative keys keep their pairwise XORs."""
 
 import numpy as np
 import pytest
@@ -33,10 +33,31 @@ def test_wide_and_negative_keys():
     arr = b.codes_array()
     assert arr.shape == (3, 2) and arr.dtype == np.uint64
     assert arr.tolist() == [[1, 0], [3, 64], [0, 1]]
-    with pytest.raises(ValueError):
+    with pytest.raises(ValueError):  # mixed signs: the reference's loop never ends
         barcode.Barcodes({-1: 1, 2 ** 65: 1}, 4).codes_array()
+    with pytest.raises(ValueError):
+        barcode.Barcodes({-5: 1, 7: 2}, 4).codes_array()
+    assert barcode.Barcodes({-5: 1}, 4).codes_array().size == 1  # one key: no pair, no XOR
     with pytest.raises(OverflowError):  # as the reference's np.fromiter (barcode.py:59)
         b.base_frequency()
+
+
+@pytest.mark.parametrize("keys", [
+    [-1, -2, -3, -4, -1000, -(2 ** 31)],
+    [-(2 ** 63), -1, -(2 ** 40) + 7, -12345],
+    [-(2 ** 70), -(2 ** 70) + 5, -3, -(2 ** 66) - 1],
+])
+def test_all_negative_keys_keep_every_pairwise_xor(keys):
+    """All-negative key sets (barcode.py:39-46 runs on them: a ^ b of two negatives is
+    non-negative): the kernel codes keep every pairwise XOR, so every distance, exactly."""
+    from oracle import oracle as O
+    from sctools_amd import _lib
+    arr = barcode.Barcodes({k: 1 for k in keys}, 16).codes_array()
+    vals = arr.tolist() if arr.ndim == 1 else _lib.limbs_to_ints(arr)
+    for i in range(len(keys)):
+        for j in range(i + 1, len(keys)):
+            assert vals[i] ^ vals[j] == keys[i] ^ keys[j]
+            assert O.two_bit_hamming(vals[i], vals[j]) == O.two_bit_hamming(keys[i], keys[j])
 
 
 def test_base4_entropy_golden(golden):

@@ -59,6 +59,50 @@ def test_ranks_on_gpu_match_oracle(tmp_path, scheme, world, n):
     assert shares == n * (n - 1) // 2
 
 
+def _worker_737k(rank, world, port, out_path):
+    """Config 3's per-rank path at full size: the 737,280-code set, SPECTRAL slice shards,
+    two pipelined steps (ShardedAllPairs.run, what bench.py times) and the gloo all-reduce."""
+    import torch
+    import torch.distributed as dist
+    from sctools_amd import _lib, sharding
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    _lib.check(_lib.lib().sct_set_device(0))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, L, seed = synthetic.CONFIGS[3]
+        codes = synthetic.whitelist_codes(n, L, seed)
+        with sharding.ShardedAllPairs(codes, 2 * L) as job:
+            assert job.scheme == _lib.SCHEME_SPECTRAL
+            hists = job.run(2)
+            assert hists[0].tolist() == hists[1].tolist()
+            np.savez(out_path % rank, hist=hists[0].astype(np.int64), mine=job.my_pairs(),
+                     rng=[job.begin, job.end])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_config3_737k_ranks_bin_for_bin(tmp_path, world):
+    """Config 3 (BASELINE.json): the 737,280-code all-pairs histogram sharded by transform
+    slices over W gloo ranks sharing the box's GPU, every rank's histogram bin for bin
+    against the C oracle's count of all 271,790,530,560 pairs (barcode.py:39-46), the ranks'
+    slice ranges tiling [0, 2^18) and their pair shares summing to P."""
+    out = str(tmp_path / "c3_%d.npz")
+    mp.spawn(_worker_737k, args=(world, _free_port(), out), nprocs=world, join=True)
+    n, L, seed = synthetic.CONFIGS[3]
+    ref = O.c_hist16(synthetic.whitelist_codes(n, L, seed))[0][:17]
+    shares, edges = 0, []
+    for r in range(world):
+        z = np.load(out % r)
+        assert z["hist"].tolist() == ref.tolist()
+        shares += int(z["mine"])
+        edges.append(tuple(z["rng"].tolist()))
+    assert shares == n * (n - 1) // 2
+    assert edges[0][0] == 0 and edges[-1][1] == 1 << 18
+    assert all(a[1] == b[0] for a, b in zip(edges, edges[1:]))
+
+
 def _records():
     """5,003 random 28-bp ACGT records, (n, 28) uint8."""
     rng = np.random.default_rng(3)
@@ -85,31 +129,38 @@ def _worker_records(rank, world, port, out_path):
     try:
         wl3 = synthetic.two_to_three(synthetic.whitelist_codes(20_000, 16, 5), 16)
         q = synthetic.config4_queries(wl3, 30_001, seed=9)[0].cpu().numpy().view(np.uint64)
-        idx, dist_ = sharding.nearest_sharded(3, wl3, q, 1)
-        codes, gc, flags = sharding.encode_sharded(2, _records(), 28)
+        qb, qe, idx, dist_ = sharding.nearest_sharded(3, wl3, q, 1)
+        eb, ee, codes, gc, flags = sharding.encode_sharded(2, _records(), 28)
         wide = sharding.allpairs_wide_sharded(_wide_limbs())
-        np.savez(out_path % rank, idx=idx, dist=dist_, codes=codes, gc=gc, q=q, wl=wl3, wide=wide)
+        np.savez(out_path % rank, qr=[qb, qe], er=[eb, ee], idx=idx, dist=dist_, codes=codes, gc=gc, q=q, wl=wl3,
+                 wide=wide)
     finally:
         dist.destroy_process_group()
 
 
 def test_record_sharding_on_gpu(tmp_path):
-    """Contiguous record ranges per rank (no reduction, one all-gather): every rank ends with
-    the oracle's whole nearest result and the oracle's encodings; the multi-limb all-pairs
-    histogram with its tile-pair items split over the ranks equals the oracle's."""
+    """Contiguous record ranges per rank with no collective: every rank's slice
+    equals the oracle's nearest result and encodings on that range; the multi-limb all-pairs
+    histogram with its tile-pair items split over the ranks (one all-reduce) equals the oracle's."""
     out = str(tmp_path / "q%d.npz")
     mp.spawn(_worker_records, args=(2, _free_port(), out), nprocs=2, join=True)
     z0 = np.load(out % 0)
     ref_idx, ref_dist = O.c_nearest(3, z0["wl"], z0["q"], 1)
     seqs = [bytes(r) for r in _records()]
     ref_codes = [O.two_bit_encode(s) for s in seqs]
+    ref_gc = [s.count(b"C") + s.count(b"G") for s in seqs]
+    ends = []
     for r in range(2):
         z = np.load(out % r)
-        assert z["idx"].tolist() == ref_idx.tolist()
-        assert z["dist"].tolist() == ref_dist.tolist()
-        assert z["codes"].reshape(-1).astype(np.uint64).tolist() == ref_codes
-        assert z["gc"].tolist() == [s.count(b"C") + s.count(b"G") for s in seqs]
+        qb, qe = z["qr"].tolist()
+        eb, ee = z["er"].tolist()
+        ends.append((qe, ee))
+        assert z["idx"].tolist() == ref_idx[qb:qe].tolist()
+        assert z["dist"].tolist() == ref_dist[qb:qe].tolist()
+        assert z["codes"].reshape(-1).astype(np.uint64).tolist() == ref_codes[eb:ee]
+        assert z["gc"].tolist() == ref_gc[eb:ee]
         assert z["wide"].tolist() == O.c_hist_wide(_wide_limbs()).tolist()
+    assert ends[-1] == (ref_idx.size, len(seqs))
 
 
 def _worker_rccl(rank, world, port, out_path):

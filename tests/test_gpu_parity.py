@@ -2,6 +2,7 @@
 fixtures generated from the reference and against the oracle restatement.
 Integer/byte/index work: every comparison is bit-exact."""
 
+import itertools
 import random
 
 import numpy as np
@@ -369,12 +370,11 @@ def test_allpairs_moments_scheme_matches_oracle(n):
     plan.close()
 
 
-def _spectral_hist(codes, ranges=None, chunk=None, monkeypatch=None):
+def _spectral_hist(codes, ranges=None, chunk=None):
     torch = pytest.importorskip("torch")
-    if chunk is not None:
-        monkeypatch.setenv("SCT_SPECTRAL_CHUNK", str(chunk))
     d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
-    plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=_lib.SCHEME_SPECTRAL)
+    with _lib.tuning(spectral_chunk=chunk):
+        plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=_lib.SCHEME_SPECTRAL)
     try:
         assert plan.scheme == _lib.SCHEME_SPECTRAL and plan.ncounts == 18
         assert plan.items == (1 << 18 if codes.size >= 2 else 0)
@@ -395,13 +395,11 @@ def _spectral_hist(codes, ranges=None, chunk=None, monkeypatch=None):
         plan.close()
 
 
-@pytest.mark.parametrize("width", ["1", "2", "4"])
 @pytest.mark.parametrize("n", [2, 3, 5, 1025, 20_000])
-def test_allpairs_spectral_scheme_matches_oracle(n, width, monkeypatch):
+def test_allpairs_spectral_scheme_matches_oracle(n):
     """SPECTRAL scheme (Walsh-Hadamard transform over Z_2^32, no pair enumerated) vs the
     C oracle, with duplicates (d = 0) and complementary codes (d = 16), counted in three
-    slice ranges; int8 / int16 / int32 seed intermediate."""
-    monkeypatch.setenv("SCT_SPECTRAL_BYTES", width)
+    slice ranges."""
     codes = synthetic.whitelist_codes(max(2, n - n // 8), 16, seed=n + 7)
     extra = []
     if n >= 5:
@@ -411,44 +409,35 @@ def test_allpairs_spectral_scheme_matches_oracle(n, width, monkeypatch):
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
-@pytest.mark.parametrize("tile,seed,overlap", [("reg", "", "0"), ("reg_qp", "", "0"), ("reg_qp2", "", "0"), ("reg_p16", "", "0"), ("reg_p16w3np", "", "0"), ("reg_q16w3", "", "0"), ("mfma2", "", "0"), ("reg_np", "", "0"),
-                                               ("reg_w3", "", "0"), ("reg", "walk", "0"), ("reg", "mx", "0"),
-                                               ("reg", "spread", "0"), ("reg", "walk", "1"), ("reg", "mx", "1"),
-                                               ("reg", "mxd", "0"), ("reg", "mxd", "1"),
-                                               ("reg", "db", "0")])
-def test_allpairs_spectral_kernel_variants(tile, seed, overlap, monkeypatch):
-    """Every tile / seed kernel variant, with and without the seed / tile overlap over two
-    streams, gives the oracle's histogram, with 1000-slice chunks (seams inside the range)."""
-    monkeypatch.setenv("SCT_SPECTRAL_TILE", tile)
-    monkeypatch.setenv("SCT_SPECTRAL_SEED", seed)
-    monkeypatch.setenv("SCT_SPECTRAL_OVERLAP", overlap)
+@pytest.mark.parametrize("dense", [200, 33_000])
+def test_allpairs_spectral_wide_intermediates(dense):
+    """A transform column (low 14 bits) of `dense` codes makes the seed -> tile intermediate
+    int16 (> 127 codes) or int32 (> 32,767): the VALU tile kernel on both, next to 3,000
+    sparse codes, duplicates and complements, in two slice ranges with 1000-slice chunks."""
+    rng = np.random.default_rng(dense)
+    hi = rng.choice(1 << 18, dense, replace=False).astype(np.uint64)
+    col = (hi << np.uint64(14)) | np.uint64(0x2345)
+    rest = synthetic.whitelist_codes(3000, 16, seed=dense + 1)
+    rest = rest[(rest & np.uint64(0x3FFF)) != np.uint64(0x2345)]
+    codes = np.concatenate([col, rest, col[:3], rest[:2] ^ np.uint64(0xFFFFFFFF)])
+    rng.shuffle(codes)
+    hist = _spectral_hist(codes, [(0, 4099), (4099, 1 << 18)], chunk=1000 if dense < 1000 else None)
+    assert hist.astype(np.int64).tolist() == O.c_hist16(codes)[0][:17].tolist()
+
+
+def test_allpairs_spectral_chunk_seams():
+    """The shipped seed / tile kernels with 1000-slice chunks (seams inside Gray walks and
+    inside the tile's digit-weight runs) and a range cut at 777."""
     codes = synthetic.whitelist_codes(30_000, 16, seed=5)
     codes = np.concatenate([codes, codes[:3], codes[3:5] ^ np.uint64(0xFFFFFFFF)])
-    hist = _spectral_hist(codes, [(0, 777), (777, 1 << 18)], chunk=1000, monkeypatch=monkeypatch)
+    hist = _spectral_hist(codes, [(0, 777), (777, 1 << 18)], chunk=1000)
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
-@pytest.mark.parametrize("group", ["4", "8", "16"])
-def test_allpairs_spectral_interleaved_groups(group, monkeypatch):
-    """The direct MFMA seed into the G-slice interleaved intermediate and the team-of-
-    workgroups tile reading it, G = 4 / 8 / 16: unaligned slice ranges (partial groups at
-    both ends), 1000-slice chunks, duplicates and complements."""
-    monkeypatch.setenv("SCT_SPECTRAL_SEED", "mxd")
-    monkeypatch.setenv("SCT_SPECTRAL_ILV", group)
-    codes = synthetic.whitelist_codes(25_000, 16, seed=int(group))
-    codes = np.concatenate([codes, codes[:4], codes[4:6] ^ np.uint64(0xFFFFFFFF)])
-    hist = _spectral_hist(codes, [(0, 333), (333, 70_001), (70_001, 1 << 18)], chunk=1000, monkeypatch=monkeypatch)
-    assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
-    full = _spectral_hist(codes)
-    assert full.tolist() == hist.tolist()
-
-
-@pytest.mark.parametrize("seed", ["mx", "walk", "mxd", "db"])
-def test_allpairs_spectral_column_sizes(seed, monkeypatch):
-    """Columns (low 14 bits) holding 63, 64, 65, 100 and 127 codes -- the MFMA seed's one- and
-    two-block columns and the int8 limit -- next to sparse ones, duplicates included; slice
-    ranges cut inside 256-slice tiles and walk segments."""
-    monkeypatch.setenv("SCT_SPECTRAL_SEED", seed)
+def test_allpairs_spectral_column_sizes():
+    """Columns (low 14 bits) holding 63, 64, 65, 100 and 127 codes -- two and four 32-code
+    plane groups (one and two register-resident, the rest from L2) and the int8 limit --
+    next to sparse ones, duplicates included; slice ranges cut inside walks."""
     rng = np.random.default_rng(21)
     bg = synthetic.whitelist_codes(5000, 16, seed=3)
     cols = (5, 6, 7, 20, 16383)
@@ -462,12 +451,10 @@ def test_allpairs_spectral_column_sizes(seed, monkeypatch):
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
-@pytest.mark.parametrize("tile", ["reg", "reg_qp", "reg_qp2", "reg_p16"])
-def test_allpairs_spectral_high_energy_planes(tile, monkeypatch):
+def test_allpairs_spectral_high_energy_planes():
     """Planes (column bits 12, 13) of large seeds in every slice -- 120 columns of 120 codes,
     110 of them sharing their high bits, in planes 0 and 2 -- beside sparse ones (squares
-    above 2^32 per plane, |G| above 2^16)."""
-    monkeypatch.setenv("SCT_SPECTRAL_TILE", tile)
+    above 2^32 per plane, |G| above 2^16, the packed int16 plane sums near their range)."""
     rng = np.random.default_rng(33)
     bg = synthetic.whitelist_codes(5000, 16, seed=8)
     parts = []
@@ -483,7 +470,7 @@ def test_allpairs_spectral_high_energy_planes(tile, monkeypatch):
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
-def test_allpairs_spectral_crowded_low_bits(monkeypatch):
+def test_allpairs_spectral_crowded_low_bits():
     """3000 codes sharing their low 14 bits (one transform column holds them all: 94
     32-code groups of bit planes, an int16 intermediate), plus codes that differ only
     there, with a 300-slice chunk (Gray walks cut by chunk seams)."""
@@ -491,7 +478,7 @@ def test_allpairs_spectral_crowded_low_bits(monkeypatch):
     hi = rng.integers(0, 1 << 12, 3000).astype(np.uint64)
     codes = (hi << np.uint64(20)) | np.uint64(0x5A5A5)
     codes = np.concatenate([codes, codes[:20] ^ np.uint64(0xFFFFF), rng.integers(0, 1 << 32, 50).astype(np.uint64)])
-    hist = _spectral_hist(codes, [(0, 1 << 18)], chunk=300, monkeypatch=monkeypatch)
+    hist = _spectral_hist(codes, [(0, 1 << 18)], chunk=300)
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
@@ -542,13 +529,19 @@ def _config4_queries(wl_seqs, nq, rng, alphabet=b"ACGT"):
     return picks
 
 
+_NEAREST_SCHEMES = {"auto": _lib.NEAREST_AUTO, "oa": _lib.NEAREST_OA, "csr": _lib.NEAREST_CSR}
+
+
 @pytest.mark.parametrize("scheme", ["auto", "csr", "oa"])
 @pytest.mark.parametrize("kind,max_d", [(3, 0), (3, 1), (3, 2), (3, 3), (2, 0), (2, 1), (2, 2)])
-def test_nearest_vs_bruteforce(kind, max_d, scheme, monkeypatch):
-    """Both index schemes (CSR buckets per block; open-addressing tables of block-pair
+def test_nearest_vs_bruteforce(kind, max_d, scheme):
+    """Every index scheme (CSR buckets per block; open-addressing tables of block-pair
     keys) against the brute force on config-4-shaped sets."""
-    if scheme != "auto":
-        monkeypatch.setenv("SCT_NEAREST_SCHEME", scheme)
+    with _lib.tuning(nearest_scheme=_NEAREST_SCHEMES[scheme]):
+        _nearest_vs_bruteforce(kind, max_d)
+
+
+def _nearest_vs_bruteforce(kind, max_d):
     rng = np.random.default_rng(100 + 10 * kind + max_d)
     wl_codes2 = synthetic.whitelist_codes(3000, 16, seed=kind * 7 + max_d)
     wl_seqs = synthetic.decode_ascii(wl_codes2, 16)
@@ -590,12 +583,11 @@ def test_barcodes_nearest_method(golden):
     assert idx.tolist() == rec["result"]["1"]["index"]
 
 
-def test_allpairs_counter_flush_path(monkeypatch):
+def test_allpairs_counter_flush_path():
     # force the in-kernel u32 -> u64 counter flush after every work-queue pull
-    monkeypatch.setenv("SCT_ALLPAIRS_FLUSH_ITEMS", "1")
-    monkeypatch.setenv("SCT_ALLPAIRS_GRAB", "3")
     codes = synthetic.whitelist_codes(9000, 16, seed=21)
-    hist = _lib.hamming_hist_allpairs(codes, 32)
+    with _lib.tuning(allpairs_flush_items=1, allpairs_grab=3):
+        hist = _lib.hamming_hist_allpairs(codes, 32)
     assert hist.astype(np.int64).tolist() == O.c_hist_rows(codes)[:17].tolist()
 
 
@@ -690,15 +682,21 @@ def test_allpairs_spectral_column_width_edges(m):
     assert hist.astype(np.int64).tolist() == O.c_hist16(codes)[0][:17].tolist()
 
 
-def test_allpairs_config5_spectral_vs_moments():
-    """Config 5's 3,686,400 codes (int16 intermediate, ~225 codes per column): SPECTRAL vs
-    the MOMENTS pair kernel over all 6.79e12 pairs, the pair count, and the mean distance
-    the per-position base counts imply."""
+def test_allpairs_config5_spectral_bin_for_bin():
+    """Config 5's 3,686,400 codes (int16 intermediate, ~225 codes per column): AUTO (=
+    SPECTRAL) bin for bin against the C oracle's count of all 6,794,770,636,800 pairs
+    (barcode.py:39-46; ~20 s on the box's 16 cores), and against the pair-enumerating MOMENTS
+    kernel and the mean distance the per-position base counts imply."""
     torch = pytest.importorskip("torch")
     n, L, seed = synthetic.CONFIGS[5]
     codes = synthetic.whitelist_codes(n, L, seed)
     d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
-    hs = sharding.allpairs_histogram_sharded(d_codes, 32, scheme=_lib.SCHEME_SPECTRAL)
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 32)
+    assert plan.scheme == _lib.SCHEME_SPECTRAL
+    plan.close()
+    hs = sharding.allpairs_histogram_sharded(d_codes, 32)
+    ref, _ = O.c_hist16(codes)
+    assert hs.astype(np.int64).tolist() == ref[:17].tolist()
     hm = sharding.allpairs_histogram_sharded(d_codes, 32, scheme=_lib.SCHEME_MOMENTS)
     assert hs.tolist() == hm.tolist()
     P = n * (n - 1) // 2
@@ -709,6 +707,65 @@ def test_allpairs_config5_spectral_vs_moments():
         cnt = np.bincount(bases[:, p].astype(np.int64), minlength=4).astype(object)
         agree += int(cnt.dot(cnt - 1)) // 2
     assert sum(d * int(x) for d, x in enumerate(hs)) == 16 * P - agree
+
+
+def test_encode_config5_1e9_reads_device_resident():
+    """Config 5's read stream at full size: 1e9 random 28-bp reads generated on the device
+    (1 % with one N), TwoBit-encoded with GC on the device (sct_encode, encodings.py:75-88,
+    102-111) in two record ranges, as two ranks would.  Every code, GC count and flag is
+    checked against values computed independently from the generating bases (torch, on the
+    device); every 10^6-th record also against the oracle's statement-for-statement encoder."""
+    torch = pytest.importorskip("torch")
+    n, L = synthetic.CONFIG5_READS, synthetic.CONFIG5_READ_LENGTH
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(5)
+    b = torch.randint(0, 4, (n, L), dtype=torch.uint8, device=dev, generator=g)  # TwoBit values A0 C1 T2 G3
+    seqs = torch.empty_like(b)
+    chunk = 50_000_000
+    for r0 in range(0, n, chunk):  # ASCII: A 65, C 67, T 84, G 71
+        x = b[r0:r0 + chunk]
+        seqs[r0:r0 + chunk] = 65 + 2 * x + 15 * (x == 2).to(torch.uint8)
+    nrows = torch.arange(0, n, 100, device=dev)  # 1 % of the reads get one N
+    npos = torch.randint(0, L, (nrows.numel(),), device=dev, generator=g)
+    seqs[nrows, npos] = ord("N")
+    codes = torch.empty(n, dtype=torch.int64, device=dev)
+    gc = torch.empty(n, dtype=torch.uint8, device=dev)
+    flags = torch.empty(n, dtype=torch.uint8, device=dev)
+    lib = _lib.lib()
+    for r0, r1 in ((0, n // 2), (n // 2, n)):
+        _lib.check(lib.sct_encode(2, seqs[r0].data_ptr(), r1 - r0, L, L, codes[r0].data_ptr(), gc[r0].data_ptr(),
+                                  flags[r0].data_ptr(), None))
+    torch.cuda.synchronize()
+    isn = torch.zeros(n, dtype=torch.bool, device=dev)
+    isn[nrows] = True
+    bad = 0
+    gc_total = 0
+    for r0 in range(0, n, chunk):
+        x = b[r0:r0 + chunk]
+        nm = isn[r0:r0 + chunk]
+        want = torch.zeros(x.shape[0], dtype=torch.int64, device=dev)
+        wgc = torch.zeros(x.shape[0], dtype=torch.int32, device=dev)
+        for i in range(L):
+            v = x[:, i].to(torch.int64)
+            want = (want << 2) | v
+            wgc += (v & 1).to(torch.int32)
+        # the N read: that base encodes as 0, is not GC, and flags the record (bit 0)
+        k = nrows[(nrows >= r0) & (nrows < r0 + x.shape[0])]
+        kp = npos[(nrows >= r0) & (nrows < r0 + x.shape[0])]
+        vk = b[k, kp].to(torch.int64)
+        want[k - r0] &= ~(vk << (2 * (L - 1 - kp)))
+        wgc[k - r0] -= (vk & 1).to(torch.int32)
+        bad += int((codes[r0:r0 + chunk] != want).sum())
+        bad += int((gc[r0:r0 + chunk].to(torch.int32) != wgc).sum())
+        bad += int((flags[r0:r0 + chunk] != nm.to(torch.uint8)).sum())
+        gc_total += int(gc[r0:r0 + chunk].to(torch.int64).sum())
+    assert bad == 0
+    assert gc_total == int((seqs == ord("C")).sum()) + int((seqs == ord("G")).sum())
+    for r in range(7, n, 1_000_000):  # (every 100th read holds an N: these hold none)
+        s = bytes(seqs[r].cpu().numpy().tobytes())
+        assert b"N" not in s
+        assert int(codes[r]) == O.two_bit_encode(s) and int(flags[r]) == 0
+        assert int(gc[r]) == s.count(b"C") + s.count(b"G")
 
 
 # ---------------------------------------------------------------- keys >= 2^64 (multi-limb)
@@ -764,7 +821,7 @@ def test_wide_kernel_item_ranges_sum_to_whole():
 
 # ---------------------------------------------------------------- config 4 at full size
 @pytest.mark.parametrize("scheme", ["auto", "csr"])
-def test_nearest_config4_full_size(scheme, monkeypatch):
+def test_nearest_config4_full_size(scheme):
     """Config 4 as specified: the 737,280-code ThreeBit whitelist and 100M observed
     barcodes (50 % exact, 25 % substitution, 15 % N, 10 % random) at max_d = 1.  Every
     exact draw must come back as its own index at distance 0, every one-edit query within
@@ -772,8 +829,6 @@ def test_nearest_config4_full_size(scheme, monkeypatch):
     force over the whole whitelist.  AUTO = the open-addressing pair-key tables; CSR = the
     per-block buckets."""
     torch = pytest.importorskip("torch")
-    if scheme != "auto":
-        monkeypatch.setenv("SCT_NEAREST_SCHEME", scheme)
     n, L, seed = synthetic.CONFIGS[2]
     wl = synthetic.two_to_three(synthetic.whitelist_codes(n, L, seed), L)
     nq = 100_000_000
@@ -781,7 +836,8 @@ def test_nearest_config4_full_size(scheme, monkeypatch):
     d_wl = torch.from_numpy(wl.view(np.int64)).cuda()
     idx = torch.empty(nq, dtype=torch.int32, device="cuda")
     dist = torch.empty(nq, dtype=torch.uint8, device="cuda")
-    plan = _lib.NearestPlan(3, d_wl.data_ptr(), n, 3 * L, 1)
+    with _lib.tuning(nearest_scheme=_NEAREST_SCHEMES[scheme]):
+        plan = _lib.NearestPlan(3, d_wl.data_ptr(), n, 3 * L, 1)
     plan.query(q.data_ptr(), nq, idx.data_ptr(), dist.data_ptr())
     torch.cuda.synchronize()
     plan.close()
@@ -826,3 +882,15 @@ def test_sharded_run_pipelined_steps_match_oracle(scheme):
             hists = job.run(steps, timing=True)
             assert len(hists) == steps and all(h.tolist() == ref for h in hists)
         assert job.step().tolist() == ref
+
+
+def test_all_negative_keys_summary():
+    """An all-negative key set through the drop-in (barcode.py:39-46: the reference's
+    ``a ^ b`` of two negatives is non-negative and its loop counts it): the summary of the
+    reference's own pair loop, restated (oracle.two_bit_hamming, encodings.py:113-121)."""
+    rng = np.random.default_rng(17)
+    keys = [-int(v) for v in rng.integers(1, 1 << 32, 300)] + [-(2 ** 40) - 3, -1]
+    keys = list(dict.fromkeys(keys))
+    d = [O.two_bit_hamming(a, b) for a, b in itertools.combinations(keys, 2)]
+    s = barcode.Barcodes.from_iterable_encoded(keys, 16)
+    assert s.summarize_hamming_distances() == O.summary_numpy(d)

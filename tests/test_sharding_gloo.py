@@ -109,16 +109,17 @@ def test_item_range_partitions():
             assert max(sizes) - min(sizes) <= 1
 
 
-def test_geometry_item_count_matches_oracle_enumeration(monkeypatch):
+def test_geometry_item_count_matches_oracle_enumeration():
     # 737K codes resolve to SPECTRAL (2^18 slice items); the pair-item geometry is MOMENTS'
     assert _lib.allpairs_geometry(737_280, 32)["items"] == 1 << 18
-    monkeypatch.setenv("SCT_ALLPAIRS_SCHEME", "1")
-    for n in (2, 100, 1024, 1025, 5000, 737_280):
-        geo = _lib.allpairs_geometry(n, 32)
-        rb, cb = geo["rows_per_item"], geo["cols_per_item"]
-        nch = -(-n // cb)
-        items = sum(max(0, -(-(min((c + 1) * cb, n) - 1) // rb)) for c in range(nch))
-        assert geo["items"] == items
+    with _lib.tuning(spectral_min_n=1 << 40):  # AUTO never takes SPECTRAL
+        for n in (2, 100, 1024, 1025, 5000, 737_280):
+            geo = _lib.allpairs_geometry(n, 32)
+            rb, cb = geo["rows_per_item"], geo["cols_per_item"]
+            nch = -(-n // cb)
+            items = sum(max(0, -(-(min((c + 1) * cb, n) - 1) // rb)) for c in range(nch))
+            assert geo["items"] == items
+    assert _lib.tune_get("spectral_min_n") == -1
 
 
 def _worker_spectral(rank, world, port, n, seed, out_path):
@@ -169,18 +170,24 @@ def _worker_ranges(rank, world, port, out_path):
         rng = np.random.default_rng(5)
         wl = np.unique(rng.integers(0, 1 << 48, 300, dtype=np.uint64))[:250]
         q = np.concatenate([wl[:40], wl[40:80] ^ np.uint64(1 << 7), rng.integers(0, 1 << 48, 37, dtype=np.uint64)])
-        idx, d = sharding.nearest_sharded(3, wl, q, 1, 48, fn=_oracle_nearest)
         seqs = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=(101, 16))
-        codes, gc, flags = sharding.encode_sharded(2, seqs, 16, fn=_oracle_encode)
-        np.savez(out_path % rank, idx=idx, d=d, codes=codes, gc=gc, flags=flags)
+        # default: this rank's slice only, no collective
+        qb, qe, idx, d = sharding.nearest_sharded(3, wl, q, 1, 48, fn=_oracle_nearest)
+        eb, ee, codes, gc, flags = sharding.encode_sharded(2, seqs, 16, fn=_oracle_encode)
+        # opt-in: the whole result on every rank
+        gb, ge, gidx, gd = sharding.nearest_sharded(3, wl, q, 1, 48, fn=_oracle_nearest, gather=True)
+        _, _, gcodes, ggc, gflags = sharding.encode_sharded(2, seqs, 16, fn=_oracle_encode, gather=True)
+        np.savez(out_path % rank, qr=[qb, qe, gb, ge], er=[eb, ee], idx=idx, d=d, codes=codes, gc=gc, flags=flags,
+                 gidx=gidx, gd=gd, gcodes=gcodes, ggc=ggc, gflags=gflags)
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_contiguous_range_sharding_gathers_whole_result(tmp_path, world):
-    """Config 4 / encoder sharding: contiguous record ranges per rank, whole
-    result all-gathered on every rank, identical to the unsharded computation."""
+def test_contiguous_range_sharding(tmp_path, world):
+    """Config 4 / encoder sharding: contiguous record ranges per rank, each rank
+    keeping only its own result slice (no collective); the slices tile the unsharded result.
+    The opt-in gather gives every rank the whole result."""
     port = _free_port()
     out = str(tmp_path / "ranges_%d.npz")
     mp.spawn(_worker_ranges, args=(world, port, out), nprocs=world, join=True)
@@ -191,8 +198,15 @@ def test_contiguous_range_sharding_gathers_whole_result(tmp_path, world):
     seqs = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=(101, 16))
     rcodes, rgc, _ = _oracle_encode(2, seqs, 16)
     assert (ridx[:40] == np.arange(40)).all() and (ridx[40:80] == np.arange(40, 80)).all()
-    for r in range(world):
-        z = np.load(out % r)
-        assert z["idx"].tolist() == ridx.tolist() and z["d"].tolist() == rd.tolist()
-        assert z["codes"].shape == (101, 1) and z["codes"].tolist() == rcodes.tolist()
-        assert z["gc"].tolist() == rgc.tolist() and z["flags"].shape == (101,)
+    parts = [np.load(out % r) for r in range(world)]
+    for r, z in enumerate(parts):
+        qb, qe, gb, ge = z["qr"].tolist()
+        eb, ee = z["er"].tolist()
+        assert (qb, qe) == sharding.item_range(q.size, r, world) and (gb, ge) == (0, q.size)
+        assert (eb, ee) == sharding.item_range(101, r, world)
+        assert z["idx"].tolist() == ridx[qb:qe].tolist() and z["d"].tolist() == rd[qb:qe].tolist()
+        assert z["codes"].tolist() == rcodes[eb:ee].tolist() and z["gc"].tolist() == rgc[eb:ee].tolist()
+        assert z["gidx"].tolist() == ridx.tolist() and z["gd"].tolist() == rd.tolist()
+        assert z["gcodes"].shape == (101, 1) and z["gcodes"].tolist() == rcodes.tolist()
+        assert z["ggc"].tolist() == rgc.tolist() and z["gflags"].shape == (101,)
+    assert np.concatenate([z["idx"] for z in parts]).tolist() == ridx.tolist()
