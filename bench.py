@@ -249,26 +249,23 @@ def issue_picture(prof):
     return out
 
 
-def copy_ceiling_gbs(dev, mib=2048, reps=5):
-    """Device-to-device copy bandwidth measured in this run (read + write bytes / time):
-    the practical HBM ceiling the kernels are compared with beside the 8 TB/s spec."""
+def copy_ceiling_gbs(dev, mib=4096, reps=5):
+    """Streaming device copy bandwidth measured in this run (sct_stream_copy: 16 B per lane,
+    nontemporal, read + write bytes / time): the practical HBM ceiling the kernels are
+    compared with beside the 8 TB/s spec."""
     import torch
+    from sctools_amd import _lib
     a = torch.empty(mib << 20, dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)
-    b.copy_(a)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    e1.synchronize()
-    gbs = 2 * a.numel() * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    lib = _lib.lib()
+    ms = _events_ms(lambda: _lib.check(lib.sct_stream_copy(b.data_ptr(), a.data_ptr(), a.numel(), stream)), reps, dev)
     del a, b
     torch.cuda.empty_cache()
-    return gbs
+    return 2 * (mib << 20) / (ms * 1e-3) / 1e9
 
 
-def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, names=("pmc_spectral_seed", "pmc_spectral")):
+def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, names=("spectral_seed", "spectral")):
     """SPECTRAL's two kernels per chunk: seed (writes 2^14 values per slice) and tile (reads
     them back: 14-bit WHT + F^2 binning).  Each moves 2^14 * elem_bytes per slice through HBM
     -- its algorithmic bytes -- so the HBM roofline prices both; the slower is reported.
@@ -277,10 +274,10 @@ def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, nam
     algo = slices_per_launch * (1 << 14) * elem_bytes
     kern = {}
     for k, label, prof_name, rp in (("seed", "sct_spectral::seed_kernel<%s>" % {1: "int8_t", 2: "int16_t", 4: "int32_t"}[elem_bytes],
-                                     names[0], "seed_kernel<"),
+                                     names[0], "seed_kernel<signed char>"),
                                     ("tile", "sct_spectral::tile_reg_kernel (int8 seeds)" if elem_bytes == 1
                                      else "sct_spectral::tile_kernel<int%d_t>" % (8 * elem_bytes), names[1],
-                                     "tile_reg_kernel" if elem_bytes == 1 else "tile_kernel<")):
+                                     "tile_reg_kernel")):
         ms, nl = kt[k]
         avg = ms / nl if nl else float("nan")
         prof = _profile(prof_name) if elem_bytes == 1 else None
@@ -400,6 +397,13 @@ def path_config4(dev, reps, copy_gbs, threads):
     sample_ok = bool(np.array_equal(idx[samp].cpu().numpy(), ridx) and np.array_equal(dist[samp].cpu().numpy(), rdist))
     algo = nq * (8 + 4 + 1)
     gbs = algo / (ms * 1e-3) / 1e9
+    prof = {}
+    for name in ("nearest", "nearest_index"):
+        pr = _profile(name)
+        if pr:
+            prof[name] = {k: pr.get(k) for k in ("file", "trace_avg_ns", "hbm_bytes_per_unit", "l2_hit_rate",
+                                                   "l2_requests_per_unit", "ea_read_requests_per_unit",
+                                                   "valu_busy_frac", "wait_any_frac_of_wave_cycles")}
     del q, pick, cls, idx, dist
     torch.cuda.empty_cache()
     return {"workload": "config 4: %d ThreeBit 16-bp observed barcodes (50%% exact, 25%% one substitution, "
@@ -409,6 +413,7 @@ def path_config4(dev, reps, copy_gbs, threads):
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
                          "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs,
                          "algo_bytes_per_query": 13, "kernel": "sct_nearest_query",
+                         "pmc": prof or None,
                          "note": "algorithmic bytes = the query stream (8 B in, 4 + 1 B out); the index "
                                  "probes are extra (DESIGN.md §3.5)"},
             "check": {"exact_draws_own_index": exact_ok, "sampled_vs_oracle": sample_ok,
@@ -479,7 +484,8 @@ def path_config5_encode(dev, reps, copy_gbs):
     ms = _events_ms(run, reps, dev)
     torch.cuda.synchronize()
     gc_total = int(gc.sum(dtype=torch.int64))
-    want_gc = int((seqs == ord("C")).sum()) + int((seqs == ord("G")).sum())
+    want_gc = sum(int((seqs[r0:r0 + chunk] == ord("C")).sum()) + int((seqs[r0:r0 + chunk] == ord("G")).sum())
+                  for r0 in range(0, n, chunk))
     nflag = int(flags.sum(dtype=torch.int64))
     ok = True
     for r in range(7, n, 1_000_000):

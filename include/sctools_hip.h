@@ -373,6 +373,11 @@ int sct_fastq_stream_chunk(sct_fastq_stream* stream, const uint8_t* buf, int64_t
 int sct_fastq_stream_fetch(sct_fastq_stream* stream, uint8_t* seq_out, uint8_t* qual_out, int32_t* seq_len,
                            int32_t* qual_len);
 
+/* ---------------------------------------------------------------- bench aid
+ * Streaming device copy (16 B per lane, nontemporal, resident grid) of `bytes` (a multiple
+ * of 16): the practical HBM ceiling bench.py prices the kernels against beside the spec. */
+int sct_stream_copy(void* d_dst, const void* d_src, int64_t bytes, void* stream);
+
 /* ---------------------------------------------------------------- summary
  * Replaces barcode.py:44-46 (np.percentile(distances,[0,25,50,75,100]) with numpy's
  * default 'linear' method, then np.mean) computed from the histogram alone,

@@ -103,6 +103,7 @@ SIGNATURES = {
                                ctypes.POINTER(_i64)],
     "sct_fastq_stream_fetch": [_vp, _vp, _vp, _vp, _vp],
     "sct_scalar_server_stop": [],
+    "sct_stream_copy": [_vp, _vp, _i64, _vp],
     "sct_scalar_server_status": [ctypes.POINTER(_i64), ctypes.POINTER(_i32)],
 }
 _RESTYPES = {"sct_last_error": ctypes.c_char_p}

@@ -285,6 +285,204 @@ __global__ __launch_bounds__(WG) void oa_query_kernel(const uint64_t* __restrict
   out_dist[i] = best_j < 0 ? (uint8_t)255 : (uint8_t)best_d;
 }
 
+// ---------------------------------------------------------------- half-key tables (max_d <= 1)
+// For max_d <= 1 and a whitelist whose G in-code positions are all A/C/G/T (every TwoBit
+// code; ThreeBit codes whose triplets are 1..4), split the positions into a high half A =
+// [GB, G) and a low half B = [0, GB) and give every half a 2-bit digit key (<= 8 digits:
+// 16 bits).  A code within distance 1 of the query agrees with it exactly on A or on B.
+// Two tables of the whitelist: sorted by (A, B) -- offA[key] .. offA[key + 1] holds the B
+// keys of the codes whose A key is `key`, as uint16 -- and sorted by (B, A) with the A keys.
+// At 737K 16-base codes both tables with their offsets take 3.5 MB: every XCD's 4 MB L2
+// holds them, so a query costs L2 hits instead of Infinity-Cache line fetches (the open-
+// addressing tables' 96 MB did not fit anywhere closer).  A query scans its A bucket (~11
+// entries, 16 B = 8 entries per load); an exact hit there settles it (every exact match lies
+// in that bucket, and the other table only adds codes >= 1 away); otherwise its B bucket,
+// skipping the codes that agree on A too (those were in the A bucket).  Each whitelist
+// entry is visited at most once, so two candidates at the best distance are two indices: a
+// tie.  The kernel writes the winner's table position (A order: p, B order: nw + p); a second
+// pass maps it to the whitelist index through permAB.
+// Entries are tested two per dword (SWAR): per 16-bit field the mismatching digits
+// m = ((x | x >> 1) & 0x5555) | invalid, x = entry ^ key; then d >= 1 iff m != 0 and d >= 2
+// iff m with its lowest set bit cleared != 0, both read off bit 15 of field + 0x7FFF (no
+// field exceeds 0x5555, so no carry leaves a field).
+// Query groups above the table's G positions are compared with the whitelist's zeros: they
+// add the same E to every distance.  A query digit that is not A/C/G/T (N, 0, 5, 7 in
+// ThreeBit) matches no whitelist digit.
+struct Halves {
+  int G, GA, GB;            // positions; high half A = [GB, G) (GA digits), low half B = [0, GB)
+  const uint32_t* offA;     // [4^GA + 1]
+  const uint16_t* entA;     // [nw] B keys, codes sorted by (A, B)
+  const uint32_t* offB;     // [4^GB + 1]
+  const uint16_t* entB;     // [nw] A keys, codes sorted by (B, A)
+  const uint32_t* permAB;   // [2 nw] whitelist index of each A-order, then B-order position
+  int64_t nw;
+};
+
+// Stride-3 -> stride-2 compaction of the 8 fields of a 24-bit ThreeBit half (field p at bit
+// 3p moves to bit 2p): three shift stages, stage j moving the fields whose p has bit j set.
+template <int W>
+constexpr uint32_t compact_mask(int j) {
+  uint32_t m = 0;
+  for (int p = 0; p < 8; ++p)
+    if ((p >> j) & 1) m |= ((1u << W) - 1) << (3 * p - (p & ((1 << j) - 1)));
+  return m;
+}
+template <int W>
+__device__ __forceinline__ uint32_t compact3to2(uint32_t x) {
+  x = (x & ~compact_mask<W>(0)) | ((x & compact_mask<W>(0)) >> 1);
+  x = (x & ~compact_mask<W>(1)) | ((x & compact_mask<W>(1)) >> 2);
+  x = (x & ~compact_mask<W>(2)) | ((x & compact_mask<W>(2)) >> 4);
+  return x;
+}
+
+// one ThreeBit half of `nd` triplets (bits 0..3 nd - 1 of h) -> 2-bit digit key (C 0, A 1,
+// G 2, T 3) and the invalid digits spread to the key's even bits
+__device__ __forceinline__ void half3(uint32_t h, int nd, uint32_t& key, uint32_t& spread) {
+  constexpr uint32_t M = 0x249249u;  // bit 3p, p < 8
+  const uint32_t live = nd >= 8 ? M : (M & ((1u << (3 * nd)) - 1));
+  const uint32_t a = h & live, b = (h >> 1) & live, c = (h >> 2) & live;
+  // valid triplets 1..4 (abc = 100, 010, 110, 001): d0 = !a, d1 = (a & b) | c
+  const uint32_t valid = (~c & (a | b)) | (c & ~a & ~b);
+  const uint32_t dig = ((~a & live) | (((a & b) | c) << 1));
+  key = compact3to2<2>(dig);
+  spread = compact3to2<1>(live & ~valid);
+}
+
+template <int KIND>
+__device__ __forceinline__ void halves_of(uint64_t q, const Halves& h, uint32_t& kA, uint32_t& sA, uint32_t& kB,
+                                          uint32_t& sB, int& E) {
+  const int top = KIND * h.G;
+  const uint64_t hi = top >= 64 ? 0ull : q >> top;
+  if constexpr (KIND == 2) {
+    E = __popcll((hi | (hi >> 1)) & 0x5555555555555555ull);
+    kB = (uint32_t)(q & ((1u << (2 * h.GB)) - 1));
+    kA = (uint32_t)(q >> (2 * h.GB)) & ((1u << (2 * h.GA)) - 1);
+    sA = sB = 0;
+  } else {
+    E = __popcll((hi | (hi >> 1) | (hi >> 2)) & 0x9249249249249249ull);
+    half3((uint32_t)(q & ((1u << (3 * h.GB)) - 1)), h.GB, kB, sB);
+    half3((uint32_t)((q >> (3 * h.GB)) & ((1u << (3 * h.GA)) - 1)), h.GA, kA, sA);
+  }
+}
+
+// Entries [b, e) of a uint16 table against the half key k (invalid digits `sp` spread to the
+// even bits): z0 / z1 count the entries at half distance 0 / 1, p0 / p1 the position of one.
+template <bool LEVEL0>
+__device__ __forceinline__ void scan_half(const uint16_t* __restrict__ ent, uint32_t b, uint32_t e, uint32_t k,
+                                          uint32_t sp, int& n0, uint32_t& p0, int& n1, uint32_t& p1) {
+  const uint32_t k2 = k | (k << 16), sp2 = sp | (sp << 16);
+  for (uint32_t c = b & ~7u; c < e; c += 8) {
+    const uint4 v = *reinterpret_cast<const uint4*>(ent + c);
+    // in-range entries of the chunk, in the layout below: entry 2k at bit 2k, 2k + 1 at 16 + 2k
+    const uint32_t lo = b > c ? b - c : 0u, hi = e - c < 8u ? e - c : 8u;
+    const uint32_t in8 = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+    const uint32_t inr = (in8 & 0x55u) | ((in8 & 0xAAu) << 15);
+    uint32_t f0 = 0, f1 = 0;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t x = w[q] ^ k2;
+      const uint32_t m = ((x | (x >> 1)) & 0x55555555u) | sp2;
+      const uint32_t t = m & ((m | 0x80008000u) - 0x00010001u);
+      const uint32_t ge1 = (m + 0x7FFF7FFFu) & 0x80008000u, ge2 = (t + 0x7FFF7FFFu) & 0x80008000u;
+      if constexpr (LEVEL0) f0 |= ((~ge1 & 0x80008000u) >> 15) << (2 * q);
+      f1 |= ((ge1 & ~ge2) >> 15) << (2 * q);
+    }
+    if constexpr (LEVEL0) {
+      f0 &= inr;
+      if (f0) {
+        n0 += __popc(f0);
+        const uint32_t bit = __ffs(f0) - 1;
+        p0 = c + (bit < 16 ? bit : bit - 15);
+      }
+    }
+    f1 &= inr;
+    if (f1) {
+      n1 += __popc(f1);
+      const uint32_t bit = __ffs(f1) - 1;
+      p1 = c + (bit < 16 ? bit : bit - 15);
+    }
+  }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(WG) void halves_query_kernel(const uint64_t* __restrict__ queries, int64_t nq, Halves h,
+                                                          int max_d, int32_t* __restrict__ out_pos,
+                                                          uint8_t* __restrict__ out_dist) {
+  const int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (i >= nq) return;
+  const uint64_t q = __builtin_nontemporal_load(queries + i);
+  uint32_t kA, sA, kB, sB;
+  int E;
+  halves_of<KIND>(q, h, kA, sA, kB, sB, E);
+  const int eff = max_d - E;  // in-table distance allowed
+  int nA0 = 0, nA1 = 0, nB0 = 0, nB1 = 0;
+  uint32_t pA0 = 0, pA1 = 0, pB0 = 0, pB1 = 0;
+  if (eff >= 0 && sA == 0)  // the A bucket: codes agreeing with q on A
+    scan_half<true>(h.entA, h.offA[kA], h.offA[kA + 1], kB, sB, nA0, pA0, nA1, pA1);
+  // an exact hit (unique or not) is final: the B table holds no other code at distance 0;
+  // in the B bucket the codes at A distance 0 are the A bucket's exact hits, not counted
+  if (eff >= 1 && nA0 == 0 && sB == 0)
+    scan_half<false>(h.entB, h.offB[kB], h.offB[kB + 1], kA, sA, nB0, pB0, nB1, pB1);
+  int32_t pos = -1;
+  uint8_t dist = 255;
+  if (nA0) {
+    pos = nA0 == 1 ? (int32_t)pA0 : -2;
+    dist = (uint8_t)E;
+  } else if (eff >= 1 && nA1 + nB1) {
+    pos = nA1 + nB1 >= 2 ? -2 : (nA1 ? (int32_t)pA1 : (int32_t)(h.nw + pB1));
+    dist = (uint8_t)(1 + E);
+  }
+  __builtin_nontemporal_store(pos, out_pos + i);
+  __builtin_nontemporal_store(dist, out_dist + i);
+}
+
+// table positions -> whitelist indices (-1 / -2 pass through): four queries per lane per
+// step, their perm loads independent
+__global__ __launch_bounds__(WG) void halves_index_kernel(int32_t* __restrict__ idx, int64_t nq,
+                                                          const uint32_t* __restrict__ perm, bool vec) {
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  const int64_t n4 = vec ? nq / 4 : 0;  // vec: idx is 16-B aligned
+  v4i* idx4 = reinterpret_cast<v4i*>(idx);
+  for (int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x; i < n4; i += (int64_t)gridDim.x * WG) {
+    v4i p = __builtin_nontemporal_load(idx4 + i);
+    v4i o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = p[k] >= 0 ? (int)perm[p[k]] : p[k];
+    __builtin_nontemporal_store(o, idx4 + i);
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * WG + threadIdx.x; i < nq; i += (int64_t)gridDim.x * WG)
+    if (idx[i] >= 0) idx[i] = (int32_t)perm[idx[i]];
+}
+
+// whitelist -> (A, B) and (B, A) sort keys; *bad = 1 if a code has a digit that is not A/C/G/T
+// in its G positions or any bit above them
+template <int KIND>
+__global__ void halves_keys_kernel(const uint64_t* __restrict__ wl, int64_t nw, Halves h,
+                                   uint32_t* __restrict__ keyAB, uint32_t* __restrict__ keyBA,
+                                   uint32_t* __restrict__ iota, unsigned* __restrict__ bad) {
+  for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j < nw; j += (int64_t)gridDim.x * WG) {
+    uint32_t kA, sA, kB, sB;
+    int E;
+    halves_of<KIND>(wl[j], h, kA, sA, kB, sB, E);
+    if (E || sA || sB) atomicOr(bad, 1u);
+    keyAB[j] = (kA << (2 * h.GB)) | kB;
+    keyBA[j] = (kB << (2 * h.GA)) | kA;
+    iota[j] = (uint32_t)j;
+  }
+}
+
+// sorted (hi << lowbits | lo) keys -> entries (lo, uint16) and bucket offsets of hi
+__global__ void halves_table_kernel(const uint32_t* __restrict__ sorted, int64_t nw, int lowbits, int64_t nbuckets,
+                                    uint16_t* __restrict__ ent, uint32_t* __restrict__ off) {
+  for (int64_t t = (int64_t)blockIdx.x * WG + threadIdx.x; t <= nw; t += (int64_t)gridDim.x * WG) {
+    const int64_t cur = t < nw ? (int64_t)(sorted[t] >> lowbits) : nbuckets;
+    const int64_t prev = t > 0 ? (int64_t)(sorted[t - 1] >> lowbits) : -1;
+    for (int64_t k = prev + 1; k <= cur; ++k) off[k] = (uint32_t)t;  // buckets (prev, cur] start at t
+    if (t < nw) ent[t] = (uint16_t)(sorted[t] & ((1u << lowbits) - 1));
+  }
+}
+
 template <int KIND>
 void launch_oa_query(int nt, unsigned blocks, hipStream_t s, const uint64_t* q, int64_t nq, const OTables& tb,
                      int max_d, int32_t* idx, uint8_t* dist) {
@@ -348,6 +546,9 @@ static int compute_dups(const uint64_t* d_whitelist, int64_t nw, uint8_t* dup, h
 struct sct_nearest_plan {
   int kind = 2, max_d = 0, nparts = 0, code_bits = 0;
   int64_t nw = 0;
+  bool halves = false;  // half-key tables (Halves) for max_d <= 1
+  Halves hv{};
+  void* hv_mem[5] = {};  // offA, entA, offB, entB, permA
   int nkeys = 0;  // > 0: open-addressing multi-index (OTables); 0: CSR per block (Parts)
   OTables ot{};
   Parts parts{};
@@ -359,6 +560,8 @@ struct sct_nearest_plan {
 
 extern "C" int sct_nearest_plan_destroy(sct_nearest_plan* p) {
   if (!p) return SCT_OK;
+  for (void* m : p->hv_mem)
+    if (m) (void)hipFree(m);
   for (int k = 0; k < MAX_KEYS; ++k)
     if (p->ot.t[k].slots) (void)hipFree(p->ot.t[k].slots);
   for (int k = 0; k < MAX_PARTS; ++k) {
@@ -367,6 +570,65 @@ extern "C" int sct_nearest_plan_destroy(sct_nearest_plan* p) {
     if (p->d_index[k]) (void)hipFree(p->d_index[k]);
   }
   delete p;
+  return SCT_OK;
+}
+
+// The half-key tables, if the whitelist allows them (SCT_OK with p->halves set), else SCT_OK
+// with p->halves false (the caller takes another layout).
+static int build_halves(sct_nearest_plan* p, const uint64_t* d_wl, int64_t nw, int G, hipStream_t s) {
+  Halves h{};
+  h.G = G;
+  h.GB = G / 2;
+  h.GA = G - h.GB;
+  h.nw = nw;
+  const int64_t nA = 1LL << (2 * h.GA), nB = 1LL << (2 * h.GB);
+  sct::DevBuf keyAB, keyBA, sAB, sBA, iota, bad, tmp;
+  const size_t n = (size_t)std::max<int64_t>(nw, 1);
+  SCT_HIP(keyAB.alloc(n * 4));
+  SCT_HIP(keyBA.alloc(n * 4));
+  SCT_HIP(sAB.alloc(n * 4));
+  SCT_HIP(sBA.alloc(n * 4));
+  SCT_HIP(iota.alloc(n * 4));
+  SCT_HIP(bad.alloc(4));
+  SCT_HIP(hipMemsetAsync(bad.p, 0, 4, s));
+  if (p->kind == 2)
+    hipLaunchKernelGGL(halves_keys_kernel<2>, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_wl, nw, h,
+                       (uint32_t*)keyAB.p, (uint32_t*)keyBA.p, (uint32_t*)iota.p, (unsigned*)bad.p);
+  else
+    hipLaunchKernelGGL(halves_keys_kernel<3>, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_wl, nw, h,
+                       (uint32_t*)keyAB.p, (uint32_t*)keyBA.p, (uint32_t*)iota.p, (unsigned*)bad.p);
+  SCT_LAUNCH_CHECK();
+  unsigned hbad = 0;
+  SCT_HIP(hipMemcpyAsync(&hbad, bad.p, 4, hipMemcpyDeviceToHost, s));
+  SCT_HIP(hipStreamSynchronize(s));
+  if (hbad) return SCT_OK;  // not applicable
+  // offA, entA, offB, entB (+16 B: the last chunk's load may run past nw), permAB
+  const size_t bytes[5] = {(size_t)(nA + 1) * 4, n * 2 + 16, (size_t)(nB + 1) * 4, n * 2 + 16, 2 * n * 4};
+  for (int k = 0; k < 5; ++k) SCT_HIP(hipMalloc(&p->hv_mem[k], bytes[k]));
+  h.offA = (const uint32_t*)p->hv_mem[0];
+  h.entA = (const uint16_t*)p->hv_mem[1];
+  h.offB = (const uint32_t*)p->hv_mem[2];
+  h.entB = (const uint16_t*)p->hv_mem[3];
+  h.permAB = (const uint32_t*)p->hv_mem[4];
+  const int bits = 2 * G;
+  size_t tb = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)nw, 0, bits, s);
+  SCT_HIP(tmp.alloc(tb));
+  uint32_t* perm = (uint32_t*)p->hv_mem[4];
+  size_t b1 = tb, b2 = tb;
+  SCT_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, b1, (const uint32_t*)keyAB.p, (uint32_t*)sAB.p,
+                                             (const uint32_t*)iota.p, perm, (int)nw, 0, bits, s));
+  SCT_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, b2, (const uint32_t*)keyBA.p, (uint32_t*)sBA.p,
+                                             (const uint32_t*)iota.p, perm + nw, (int)nw, 0, bits, s));
+  hipLaunchKernelGGL(halves_table_kernel, dim3(grid_for(nw + 1, 4096)), dim3(WG), 0, s, (const uint32_t*)sAB.p, nw,
+                     2 * h.GB, nA, (uint16_t*)p->hv_mem[1], (uint32_t*)p->hv_mem[0]);
+  hipLaunchKernelGGL(halves_table_kernel, dim3(grid_for(nw + 1, 4096)), dim3(WG), 0, s, (const uint32_t*)sBA.p, nw,
+                     2 * h.GA, nB, (uint16_t*)p->hv_mem[3], (uint32_t*)p->hv_mem[2]);
+  SCT_LAUNCH_CHECK();
+  SCT_HIP(hipStreamSynchronize(s));  // the scratch dies here
+  p->hv = h;
+  p->halves = true;
   return SCT_OK;
 }
 
@@ -393,6 +655,17 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
   p->nw = nw;
   p->code_bits = code_bits;
   p->nparts = max_d + 1;
+  {
+    // half-key tables: max_d <= 1, 2..16 positions, an A/C/G/T whitelist (checked on the device)
+    const int64_t forced = sct::tune(SCT_TUNE_NEAREST_SCHEME, 0);
+    if ((forced == 0 || forced == SCT_NEAREST_HALVES) && max_d <= 1 && G >= 2 && G <= 16 && nw > 0) {
+      if (int rc = build_halves(p, d_whitelist, nw, G, s); rc != SCT_OK) return fail_with(rc);
+      if (p->halves) {
+        *out = p;
+        return SCT_OK;
+      }
+    }
+  }
   sct::DevBuf dup;
   if (dup.alloc((size_t)std::max<int64_t>(nw, 1)) != hipSuccess)
     return fail_with(sct::fail(SCT_E_NOMEM, "dup flags"));
@@ -409,8 +682,8 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
     if (sz == 2) min_bases = 2 * (G / P);
     bool oa = P <= G && nkeys <= MAX_KEYS && 2.0 * min_bases >= std::log2(0.5 * std::max<int64_t>(nw, 2));
     const int64_t forced = sct::tune(SCT_TUNE_NEAREST_SCHEME, 0);
-    if (forced == 2) oa = false;
-    if (forced == 1) oa = P <= G && nkeys <= MAX_KEYS;
+    if (forced == SCT_NEAREST_CSR) oa = false;
+    if (forced == SCT_NEAREST_OA) oa = P <= G && nkeys <= MAX_KEYS;
     if (oa) {
       uint64_t bmask[MAX_KEYS + 2] = {};
       for (int b = 0; b < P; ++b) {
@@ -519,6 +792,12 @@ extern "C" int sct_nearest_plan_create(int kind, const uint64_t* d_whitelist, in
 extern "C" int sct_nearest_plan_info(const sct_nearest_plan* p, int* scheme, int64_t* index_bytes) {
   SCT_CHECK(p != nullptr, "plan is NULL");
   int64_t bytes = 0;
+  if (p->halves) {
+    bytes = ((1LL << (2 * p->hv.GA)) + (1LL << (2 * p->hv.GB)) + 2) * 4 + p->nw * 12;
+    if (scheme) *scheme = SCT_NEAREST_HALVES;
+    if (index_bytes) *index_bytes = bytes;
+    return SCT_OK;
+  }
   if (p->nkeys > 0) {
     for (int k = 0; k < p->nkeys; ++k) bytes += (int64_t)(p->ot.t[k].gmask + 1) * kGroup * 16;
   } else {
@@ -538,6 +817,19 @@ extern "C" int sct_nearest_query(sct_nearest_plan* p, const uint64_t* d_queries,
   hipStream_t s = sct::as_stream(stream);
   const unsigned blocks = (unsigned)sct::ceil_div(nq, WG);  // one query per thread
   SCT_CHECK(sct::ceil_div(nq, WG) < (1LL << 31), "too many queries for one launch");
+  if (p->halves) {
+    if (p->kind == 2)
+      hipLaunchKernelGGL(halves_query_kernel<2>, dim3(blocks), dim3(WG), 0, s, d_queries, nq, p->hv, p->max_d,
+                         d_index, d_dist);
+    else
+      hipLaunchKernelGGL(halves_query_kernel<3>, dim3(blocks), dim3(WG), 0, s, d_queries, nq, p->hv, p->max_d,
+                         d_index, d_dist);
+    SCT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(halves_index_kernel, dim3(grid_for(sct::ceil_div(nq, 4), 8192)), dim3(WG), 0, s, d_index, nq,
+                       p->hv.permAB, ((uintptr_t)d_index & 15) == 0);
+    SCT_LAUNCH_CHECK();
+    return SCT_OK;
+  }
   if (p->nkeys > 0) {
     if (p->kind == 2)
       launch_oa_query<2>(p->nkeys, blocks, s, d_queries, nq, p->ot, p->max_d, d_index, d_dist);

@@ -529,16 +529,87 @@ def _config4_queries(wl_seqs, nq, rng, alphabet=b"ACGT"):
     return picks
 
 
-_NEAREST_SCHEMES = {"auto": _lib.NEAREST_AUTO, "oa": _lib.NEAREST_OA, "csr": _lib.NEAREST_CSR}
+_NEAREST_SCHEMES = {"auto": _lib.NEAREST_AUTO, "oa": _lib.NEAREST_OA, "csr": _lib.NEAREST_CSR,
+                    "halves": _lib.NEAREST_HALVES}
 
 
-@pytest.mark.parametrize("scheme", ["auto", "csr", "oa"])
+@pytest.mark.parametrize("scheme", ["auto", "csr", "oa", "halves"])
 @pytest.mark.parametrize("kind,max_d", [(3, 0), (3, 1), (3, 2), (3, 3), (2, 0), (2, 1), (2, 2)])
 def test_nearest_vs_bruteforce(kind, max_d, scheme):
     """Every index scheme (CSR buckets per block; open-addressing tables of block-pair
     keys) against the brute force on config-4-shaped sets."""
     with _lib.tuning(nearest_scheme=_NEAREST_SCHEMES[scheme]):
         _nearest_vs_bruteforce(kind, max_d)
+
+
+@pytest.mark.parametrize("kind,L", [(3, 16), (2, 16), (3, 15), (2, 13), (3, 7), (2, 2)])
+@pytest.mark.parametrize("max_d", [0, 1])
+def test_nearest_halves_edges(kind, L, max_d):
+    """The half-key tables (max_d <= 1, A/C/G/T whitelists) against the brute force: odd and
+    short lengths, duplicated whitelist codes (ties at 0 and at 1), queries with N or invalid
+    triplets (0, 5, 7) in one or both halves, queries with bits above the whitelist's width
+    (every distance shifted by the same excess), and queries 1 away from two codes."""
+    rng = np.random.default_rng(1000 * kind + 10 * L + max_d)
+    n = min(4 ** L, 5000)
+    wl2 = synthetic.whitelist_codes(n, L, seed=L + kind)
+    wl = wl2 if kind == 2 else synthetic.two_to_three(wl2, L)
+    wl = np.concatenate([wl, wl[:7]])  # duplicates
+    picks = wl[rng.integers(0, wl.size, 3000)]
+    q = picks.copy()
+    pos = rng.integers(0, L, q.size).astype(np.uint64)
+    w = np.uint64(kind)
+    sub = rng.integers(0, 4, q.size).astype(np.uint64) + (np.uint64(1) if kind == 3 else np.uint64(0))
+    m = rng.random(q.size)
+    one = m < 0.3  # one substituted base (may equal the original)
+    q[one] = (q[one] & ~(np.uint64((1 << kind) - 1) << (w * pos[one]))) | (sub[one] << (w * pos[one]))
+    if kind == 3:
+        bad = (m >= 0.3) & (m < 0.5)  # one N / 0 / 5 / 7 triplet
+        val = rng.choice(np.array([0, 5, 6, 7], dtype=np.uint64), q.size)
+        q[bad] = (q[bad] & ~(np.uint64(7) << (w * pos[bad]))) | (val[bad] << (w * pos[bad]))
+        two = (m >= 0.5) & (m < 0.6)  # invalid triplets in both halves
+        q[two] = (q[two] & ~(np.uint64(7) << np.uint64(0))) | np.uint64(6)
+        q[two] = (q[two] & ~(np.uint64(7) << (w * np.uint64(L - 1)))) | (np.uint64(6) << (w * np.uint64(L - 1)))
+    hi = (m >= 0.6) & (m < 0.7)  # a non-zero group above the whitelist's width
+    top = min(63, kind * L + int(rng.integers(0, 3)))
+    q[hi] |= np.uint64(1) << np.uint64(top)
+    rnd = m >= 0.95
+    q[rnd] = rng.integers(0, 1 << min(63, kind * L), rnd.sum(), dtype=np.uint64)
+    with _lib.tuning(nearest_scheme=_lib.NEAREST_HALVES):
+        idx, dist = barcode.nearest_whitelist(q, wl, max_distance=max_d, encoding=kind)
+    ridx, rdist = O.c_nearest(kind, wl, q, max_d)
+    assert np.array_equal(idx, ridx) and np.array_equal(dist, rdist)
+    if L >= 2:  # the plan really took the half-key layout
+        import torch
+        d_wl = torch.from_numpy(wl.view(np.int64)).cuda()
+        with _lib.tuning(nearest_scheme=_lib.NEAREST_HALVES):
+            plan = _lib.NearestPlan(kind, d_wl.data_ptr(), wl.size, kind * L, max_d)
+        assert plan.info()["scheme"] == "halves"
+        # outputs at an offset that is not 16-B aligned (the index pass's scalar path)
+        d_q = torch.from_numpy(q.view(np.int64)).cuda()
+        out_i = torch.full((q.size + 3,), 7, dtype=torch.int32, device="cuda")
+        out_d = torch.zeros(q.size + 3, dtype=torch.uint8, device="cuda")
+        plan.query(d_q.data_ptr(), q.size, out_i[1:].data_ptr(), out_d[1:].data_ptr())
+        torch.cuda.synchronize()
+        assert out_i[1:q.size + 1].cpu().numpy().tolist() == ridx.tolist() and int(out_i[0]) == 7
+        assert out_d[1:q.size + 1].cpu().numpy().tolist() == rdist.tolist()
+        plan.close()
+
+
+def test_nearest_halves_falls_back_on_non_acgt_whitelists():
+    """A ThreeBit whitelist holding an N (or a shorter code) cannot use the half-key tables:
+    the plan takes another layout and the result is still the brute force's."""
+    import torch
+    wl = synthetic.two_to_three(synthetic.whitelist_codes(3000, 16, seed=9), 16)
+    wl[5] = (wl[5] & ~np.uint64(7)) | np.uint64(6)   # an N
+    wl[6] = wl[6] >> np.uint64(3)                    # a 15-base code
+    q = np.concatenate([wl[:500], wl[500:1000] ^ np.uint64(3 << 9)])
+    d_wl = torch.from_numpy(wl.view(np.int64)).cuda()
+    plan = _lib.NearestPlan(3, d_wl.data_ptr(), wl.size, 48, 1)
+    assert plan.info()["scheme"] != "halves"
+    plan.close()
+    idx, dist = barcode.nearest_whitelist(q, wl, max_distance=1, encoding=3)
+    ridx, rdist = O.c_nearest(3, wl, q, 1)
+    assert np.array_equal(idx, ridx) and np.array_equal(dist, rdist)
 
 
 def _nearest_vs_bruteforce(kind, max_d):
@@ -760,7 +831,9 @@ def test_encode_config5_1e9_reads_device_resident():
         bad += int((flags[r0:r0 + chunk] != nm.to(torch.uint8)).sum())
         gc_total += int(gc[r0:r0 + chunk].to(torch.int64).sum())
     assert bad == 0
-    assert gc_total == int((seqs == ord("C")).sum()) + int((seqs == ord("G")).sum())
+    want_gc = sum(int((seqs[r0:r0 + chunk] == ord("C")).sum()) + int((seqs[r0:r0 + chunk] == ord("G")).sum())
+                  for r0 in range(0, n, chunk))
+    assert gc_total == want_gc
     for r in range(7, n, 1_000_000):  # (every 100th read holds an N: these hold none)
         s = bytes(seqs[r].cpu().numpy().tobytes())
         assert b"N" not in s
@@ -820,16 +893,16 @@ def test_wide_kernel_item_ranges_sum_to_whole():
 
 
 # ---------------------------------------------------------------- config 4 at full size
-@pytest.mark.parametrize("scheme", ["auto", "csr"])
+@pytest.mark.parametrize("scheme", ["auto", "oa"])
 def test_nearest_config4_full_size(scheme):
     """Config 4 as specified: the 737,280-code ThreeBit whitelist and 100M observed
     barcodes (50 % exact, 25 % substitution, 15 % N, 10 % random) at max_d = 1.  Every
     exact draw must come back as its own index at distance 0, every one-edit query within
     distance 1; 20,000 sampled queries of every class bit-exact against the OpenMP brute
-    force over the whole whitelist.  AUTO = the open-addressing pair-key tables; CSR = the
-    per-block buckets."""
+    force over the whole whitelist.  AUTO = the half-key tables (L2-resident); OA = the
+    open-addressing pair-key tables."""
     torch = pytest.importorskip("torch")
-    n, L, seed = synthetic.CONFIGS[2]
+    n, L, seed = synthetic.CONFIGS[4]
     wl = synthetic.two_to_three(synthetic.whitelist_codes(n, L, seed), L)
     nq = 100_000_000
     q, pick, cls = synthetic.config4_queries(wl, nq, seed=4)
