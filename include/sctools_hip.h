@@ -248,6 +248,11 @@ int sct_allpairs_time_kernels(sct_allpairs_plan* plan, int64_t item_begin, int64
  * column.  Other schemes: SCT_E_INVALID. */
 int sct_allpairs_spectral_info(const sct_allpairs_plan* plan, int* elem_bytes, int64_t* chunk_slices,
                                int* max_column);
+/* SPECTRAL plans: the transform's column width, 14 (2^18 slices of 2^14 columns) or 16 for sets
+ * whose densest 14-bit column needs int16 seeds but whose densest 16-bit column holds <= 127
+ * codes (2^16 slices of 2^16 columns, int8 seeds; items stay 2^18 virtual slices, 4 per real
+ * slice).  Replaces nothing in the reference (an internal layout choice). */
+int sct_allpairs_spectral_columns(const sct_allpairs_plan* plan, int* column_bits);
 
 /* Bench aid: per-launch HIP-event timing of this plan's kernels, recorded on the stream each
  * launch runs on (so it times the launches of a real run, pipelined or not).  mode 1 = start

@@ -74,6 +74,7 @@ SIGNATURES = {
     "sct_allpairs_time_kernels": [_vp, _i64, _i64, _vp, _i32, ctypes.POINTER(ctypes.c_double), _vp],
     "sct_allpairs_timing": [_vp, _i32, ctypes.POINTER(ctypes.c_double)],
     "sct_allpairs_spectral_info": [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i64), ctypes.POINTER(_i32)],
+    "sct_allpairs_spectral_columns": [_vp, ctypes.POINTER(_i32)],
     "sct_nearest_plan_info": [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i64)],
     "sct_allpairs_geometry": [_i64, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i64),
                               ctypes.POINTER(_i32), ctypes.POINTER(_i32)],
@@ -662,10 +663,12 @@ class AllPairsPlan:
         return {k: (out[2 * i], int(out[2 * i + 1])) for i, k in enumerate(("seed", "tile", "count", "build"))}
 
     def spectral_info(self):
-        """SPECTRAL plans: dict(elem_bytes, chunk_slices, max_column)."""
+        """SPECTRAL plans: dict(elem_bytes, chunk_slices, max_column, column_bits)."""
         eb, ch, mc = _i32(0), _i64(0), _i32(0)
         check(self._lib.sct_allpairs_spectral_info(self._h, ctypes.byref(eb), ctypes.byref(ch), ctypes.byref(mc)))
-        return {"elem_bytes": eb.value, "chunk_slices": ch.value, "max_column": mc.value}
+        cb = _i32(0)
+        check(self._lib.sct_allpairs_spectral_columns(self._h, ctypes.byref(cb)))
+        return {"elem_bytes": eb.value, "chunk_slices": ch.value, "max_column": mc.value, "column_bits": cb.value}
 
     def range_pairs(self, begin, end):
         p = _i64(0)

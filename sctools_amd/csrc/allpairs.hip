@@ -1180,6 +1180,13 @@ extern "C" int sct_allpairs_spectral_info(const sct_allpairs_plan* plan, int* el
   return SCT_OK;
 }
 
+extern "C" int sct_allpairs_spectral_columns(const sct_allpairs_plan* plan, int* column_bits) {
+  SCT_CHECK(plan != nullptr && column_bits != nullptr, "NULL pointer");
+  SCT_CHECK(plan->scheme == SCT_ALLPAIRS_SPECTRAL, "not a SPECTRAL plan");
+  *column_bits = plan->spec.lo_bits;
+  return SCT_OK;
+}
+
 extern "C" int sct_allpairs_timing(sct_allpairs_plan* plan, int mode, double* out) {
   SCT_CHECK(plan != nullptr, "plan is NULL");
   SCT_CHECK(mode >= 0 && mode <= 2, "mode %d: 0 stop, 1 start, 2 read", mode);

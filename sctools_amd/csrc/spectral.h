@@ -14,6 +14,25 @@ constexpr int kLoBits = 14;                    // element index inside a slice (
 constexpr int kSlices = 1 << (kSpaceBits - kLoBits);  // work items: z >> 14
 constexpr int kNCounts = 1 + 17;               // [n, S_0..S_16]
 
+// non-zero 2-bit digits of z
+__device__ __forceinline__ int digit_weight(uint32_t z) {
+  return __popc((z | (z >> 1)) & 0x55555555u);
+}
+constexpr int digit_weight_c(uint32_t z) {
+  int w = 0;
+  for (; z; z >>= 2) w += (z & 3) != 0;
+  return w;
+}
+constexpr int gray(int i) { return i ^ (i >> 1); }
+constexpr int ctz_c(int i) {
+  int k = 0;
+  while (!(i & 1)) {
+    i >>= 1;
+    ++k;
+  }
+  return k;
+}
+
 // Device state of a SPECTRAL plan (owned by sct_allpairs_plan).
 struct State {
   int64_t n = 0;
@@ -32,7 +51,28 @@ struct State {
   int64_t chunk = 0;             // slices per pass
   int grid = 0;                  // compute units (the tile kernel's persistent grid)
   sct::LaunchTimer* timer = nullptr;  // the plan's (bench aid), not owned
+  // 16-bit columns (spectral16.hip): sets whose densest 14-bit column needs int16 seeds but
+  // whose densest 16-bit column holds <= 127 codes run the transform as 2^16 slices x 2^16
+  // columns with int8 seeds; the plan's items stay 2^18 virtual slices (4 per real slice)
+  int lo_bits = 14;
+  int64_t chunk16 = 0;           // real 16-bit slices per pass
 };
+
+constexpr int kLoBits16 = 16;
+constexpr int kSlices16 = 1 << (kSpaceBits - kLoBits16);
+
+// the 16-bit column path (spectral16.hip); the functions below dispatch to it when
+// st.lo_bits == 16.  max16: codes in the densest 16-bit column (<= 127); chunk in virtual
+// slices (4 per real one).
+int create16(State& st, const uint64_t* d_codes, int64_t n, unsigned max16, int64_t chunk, int cus);
+int build16(State& st, const uint64_t* d_codes, hipStream_t s);
+int count16(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_counts, hipStream_t s);
+int time_kernels16(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_counts, int repeats,
+                   hipStream_t s, double* seed_ms, double* tile_ms, int64_t* slices);
+// codes in the densest column of the low `lo_bits` bits (device scratch of 2^lo_bits words)
+int max_column(const uint64_t* d_codes, int64_t n, int lo_bits, unsigned* out);
+// the digit-weight slice order tables (st.d_order)
+int make_order_table(State& st);
 
 // allocate (chunk = slices held in HBM at once) and size the intermediate from the
 // codes' densest column; returns an SCT_* code

@@ -37,25 +37,6 @@ constexpr int kRegGroups = 2;             // seed: 32-code groups whose planes s
 constexpr int kSeedWalks = 16;            // seed: walks per workgroup (8: +5 %, 32: +5 % per launch)
 constexpr int kMaxOrder = 1 << 16;        // largest slice range with a digit-weight order table
 
-// non-zero 2-bit digits of z
-__device__ __forceinline__ int digit_weight(uint32_t z) {
-  return __popc((z | (z >> 1)) & 0x55555555u);
-}
-constexpr int digit_weight_c(uint32_t z) {
-  int w = 0;
-  for (; z; z >>= 2) w += (z & 3) != 0;
-  return w;
-}
-constexpr int gray(int i) { return i ^ (i >> 1); }
-constexpr int ctz_c(int i) {
-  int k = 0;
-  while (!(i & 1)) {
-    i >>= 1;
-    ++k;
-  }
-  return k;
-}
-
 // Bit planes of a 32-code group: planes + g * kPlaneWords holds its 18 planes (plane k bit j =
 // bit k of (code >> 14) of the group's j-th code) and 2 words of padding, so a group's planes
 // are five aligned 16-B words: one lane's group is 5 loads from 2 lines, not 18 from 18.
@@ -99,9 +80,10 @@ __device__ __forceinline__ void wht(int32_t* x) {
 // Counting sort of the codes by column (low 14 bits): only code >> 14 is kept, in column
 // order (the order inside a column is whatever the atomics give: every use of a column's
 // codes is an order-independent sum).
-__global__ void column_hist_kernel(const uint64_t* __restrict__ codes, int64_t n, uint32_t* __restrict__ cnt) {
+__global__ void column_hist_kernel(const uint64_t* __restrict__ codes, int64_t n, uint32_t* __restrict__ cnt,
+                                   uint32_t mask) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    atomicAdd(&cnt[codes[i] & (kLo - 1)], 1u);
+    atomicAdd(&cnt[codes[i] & mask], 1u);
 }
 
 // Privatised counting sort (the build of every step; no global atomics):
@@ -770,7 +752,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
 
 __global__ void max_column_kernel(const uint32_t* __restrict__ cnt, unsigned* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < kLo) atomicMax(out, cnt[c]);
+  atomicMax(out, cnt[c]);
 }
 
 template <typename T>
@@ -848,44 +830,60 @@ int time_chunk(State& st, int z0, int z1, unsigned long long* counts, int repeat
 
 }  // namespace
 
+int make_order_table(State& st) {
+  // for every power of two L <= 2^16: the offsets [0, L) sorted by digit weight, stored
+  // at [L, 2L) (an aligned range of L slices adds a constant weight to all of them)
+  std::vector<uint16_t> order(2 * kMaxOrder);
+  for (int len = 1; len <= kMaxOrder; len *= 2) {
+    uint16_t* o = order.data() + len;
+    for (int u = 0; u < len; ++u) o[u] = (uint16_t)u;
+    std::stable_sort(o, o + len, [](uint16_t a, uint16_t b) { return digit_weight_c(a) < digit_weight_c(b); });
+  }
+  SCT_HIP(hipMalloc(&st.d_order, order.size() * 2));
+  SCT_HIP(hipMemcpy(st.d_order, order.data(), order.size() * 2, hipMemcpyHostToDevice));
+  return SCT_OK;
+}
+
+int max_column(const uint64_t* d_codes, int64_t n, int lo_bits, unsigned* out) {
+  const int cols = 1 << lo_bits;
+  sct::DevBuf cnt, dmax;
+  SCT_HIP(cnt.alloc((size_t)cols * 4));
+  SCT_HIP(dmax.alloc(4));
+  SCT_HIP(hipMemset(cnt.p, 0, (size_t)cols * 4));
+  SCT_HIP(hipMemset(dmax.p, 0, 4));
+  hipLaunchKernelGGL(column_hist_kernel, dim3(1024), dim3(256), 0, 0, d_codes, n, (uint32_t*)cnt.p, (uint32_t)(cols - 1));
+  SCT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(max_column_kernel, dim3(cols / 256), dim3(256), 0, 0, (const uint32_t*)cnt.p, (unsigned*)dmax.p);
+  SCT_LAUNCH_CHECK();
+  SCT_HIP(hipMemcpy(out, dmax.p, 4, hipMemcpyDeviceToHost));
+  return SCT_OK;
+}
+
 int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus) {
   st.n = n;
   st.chunk = std::max<int64_t>(kWalk, std::min<int64_t>(chunk, kSlices));
   st.grid = std::max(1, cus);  // CUs; the tile kernels' persistent grids are sized from it
   if (n < 2) return SCT_OK;
+  // the densest column bounds |seed| and so the intermediate's width (the codes are fixed
+  // for the plan's life); a set too dense for int8 seeds on 14-bit columns takes 16-bit
+  // columns when every one of those holds <= 127 codes (spectral16.hip)
+  unsigned maxm = 0;
+  if (int rc = max_column(d_codes, n, kLoBits, &maxm); rc != SCT_OK) return rc;
+  if (maxm > 127) {
+    unsigned max16 = 0;
+    if (int rc = max_column(d_codes, n, kLoBits16, &max16); rc != SCT_OK) return rc;
+    if (max16 <= 127) return create16(st, d_codes, n, max16, chunk, cus);
+  }
   SCT_HIP(hipMalloc(&st.d_hi, (size_t)n * 4));
   SCT_HIP(hipMalloc(&st.d_off, (size_t)(kLo + 1) * 4));
   SCT_HIP(hipMalloc(&st.d_cnt, (size_t)2 * kLo * 4));  // counts, then scatter cursors
-  // the densest column bounds |seed| and so the intermediate's width (the codes are
-  // fixed for the plan's life)
-  SCT_HIP(hipMemset(st.d_cnt, 0, (size_t)kLo * 4));
-  hipLaunchKernelGGL(column_hist_kernel, dim3(1024), dim3(256), 0, 0, d_codes, n, st.d_cnt);
-  SCT_LAUNCH_CHECK();
-  sct::DevBuf dmax;
-  SCT_HIP(dmax.alloc(4));
-  SCT_HIP(hipMemset(dmax.p, 0, 4));
-  hipLaunchKernelGGL(max_column_kernel, dim3(kLo / 256), dim3(256), 0, 0, st.d_cnt, (unsigned*)dmax.p);
-  SCT_LAUNCH_CHECK();
-  unsigned maxm = 0;
-  SCT_HIP(hipMemcpy(&maxm, dmax.p, 4, hipMemcpyDeviceToHost));
   st.max_m = maxm;
   st.elem_bytes = maxm <= 127 ? 1 : (maxm <= 32767 ? 2 : 4);
   int per_cu = 0;  // resident register-tile workgroups per CU (VGPR bound: 3)
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_reg_kernel, 256, 0) != hipSuccess || per_cu <= 0)
     per_cu = 2;
   st.tile_wgs = per_cu;
-  {
-    // for every power of two L <= 2^16: the offsets [0, L) sorted by digit weight, stored
-    // at [L, 2L) (an aligned range of L slices adds a constant weight to all of them)
-    std::vector<uint16_t> order(2 * kMaxOrder);
-    for (int len = 1; len <= kMaxOrder; len *= 2) {
-      uint16_t* o = order.data() + len;
-      for (int u = 0; u < len; ++u) o[u] = (uint16_t)u;
-      std::stable_sort(o, o + len, [](uint16_t a, uint16_t b) { return digit_weight_c(a) < digit_weight_c(b); });
-    }
-    SCT_HIP(hipMalloc(&st.d_order, order.size() * 2));
-    SCT_HIP(hipMemcpy(st.d_order, order.data(), order.size() * 2, hipMemcpyHostToDevice));
-  }
+  if (int rc = make_order_table(st); rc != SCT_OK) return rc;
   st.max_groups = sct::ceil_div(n, 32) + kLo;
   SCT_HIP(hipMalloc(&st.d_gofs, (size_t)(kLo + 1) * 4));
   SCT_HIP(hipMalloc(&st.d_hist, (size_t)kSortWGs * kLo * 4));
@@ -904,6 +902,7 @@ void destroy(State& st) {
 
 int build(State& st, const uint64_t* d_codes, hipStream_t s) {
   if (st.n < 2) return SCT_OK;
+  if (st.lo_bits == kLoBits16) return build16(st, d_codes, s);
   hipEvent_t t0 = st.timer ? st.timer->start(s) : nullptr;
   hipLaunchKernelGGL(column_hist_wg_kernel, dim3(kSortWGs), dim3(kSortThreads), 0, s, d_codes, st.n, st.d_hist);
   SCT_LAUNCH_CHECK();
@@ -930,6 +929,7 @@ int count(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_count
   SCT_CHECK(0 <= z_begin && z_begin <= z_end && z_end <= kSlices, "slice range [%lld, %lld)",
             (long long)z_begin, (long long)z_end);
   if (st.n < 2 || z_begin == z_end) return SCT_OK;
+  if (st.lo_bits == kLoBits16) return count16(st, z_begin, z_end, d_counts, s);
   for (int64_t z0 = z_begin; z0 < z_end; z0 += st.chunk) {
     const int z1 = (int)std::min<int64_t>(z_end, z0 + st.chunk);
     // d_counts[0] += n by the job's first tile launch (the range holding slice 0)
@@ -946,6 +946,7 @@ int time_kernels(State& st, int64_t z_begin, int64_t z_end, unsigned long long* 
                  hipStream_t s, double* seed_ms, double* tile_ms, int64_t* slices) {
   SCT_CHECK(0 <= z_begin && z_begin < z_end && z_end <= kSlices && repeats > 0 && st.n >= 2,
             "time_kernels: empty range or plan");
+  if (st.lo_bits == kLoBits16) return time_kernels16(st, z_begin, z_end, d_counts, repeats, s, seed_ms, tile_ms, slices);
   const int z1 = (int)std::min<int64_t>(z_end, z_begin + st.chunk);
   *slices = z1 - z_begin;
   return st.elem_bytes == 1   ? time_chunk<int8_t>(st, (int)z_begin, z1, d_counts, repeats, s, seed_ms, tile_ms)

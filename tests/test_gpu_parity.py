@@ -753,6 +753,68 @@ def test_allpairs_spectral_column_width_edges(m):
     assert hist.astype(np.int64).tolist() == O.c_hist16(codes)[0][:17].tolist()
 
 
+def _dense_columns(splits, n_rand, seed):
+    """n_rand random 16-bp codes plus, per entry of `splits`, one 14-bit column holding
+    sum(split) codes (> 127: int16 seeds on 14-bit columns) spread over its four 16-bit
+    sub-columns as `split` (each <= 127)."""
+    rng = np.random.default_rng(seed)
+    parts, used = [], set()
+    for j, split in enumerate(splits):
+        col = int(rng.integers(0, 1 << 14))
+        while col in used:
+            col = int(rng.integers(0, 1 << 14))
+        used.add(col)
+        for s, k in enumerate(split):  # sub-column s: bits 14, 15 = s
+            hi = rng.choice(1 << 16, k, replace=False).astype(np.uint64)
+            parts.append((hi << np.uint64(16)) | np.uint64((s << 14) | col))
+    rest = synthetic.whitelist_codes(n_rand, 16, seed=seed)
+    rest = rest[~np.isin((rest & np.uint64(0x3FFF)).astype(np.int64), list(used))]
+    codes = np.concatenate(parts + [rest])
+    rng.shuffle(codes)
+    return codes
+
+
+@pytest.mark.parametrize("case", ["two_columns", "sub127", "ragged", "small_chunk"])
+def test_allpairs_spectral_16bit_columns(case):
+    """Sets whose densest 14-bit column needs int16 seeds but whose 16-bit columns hold <= 127
+    codes take the 16-bit-column transform (spectral16.hip): bin for bin against the C oracle.
+    Sub-columns of 127 (four groups, the int8 limit), 65 (the first third group), 0 and 1
+    codes; slice ranges cutting walks and chunks; a small chunk (several seed / tile passes
+    and their digit-weight orders)."""
+    torch = pytest.importorskip("torch")
+    splits = {"two_columns": [(40, 40, 40, 40), (100, 0, 1, 60)], "sub127": [(127, 65, 0, 3)],
+              "ragged": [(90, 90, 0, 0)], "small_chunk": [(33, 64, 96, 127)]}[case]
+    codes = _dense_columns(splits, 6000, seed=len(case))
+    ranges = [(0, 1 << 18)]
+    chunk = None
+    if case == "ragged":
+        ranges = [(0, 1001), (1001, 70001), (70001, 1 << 18)]
+    if case == "small_chunk":
+        chunk, ranges = 4096, [(0, 8192), (8192, 100000), (100000, 1 << 18)]
+    d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
+    with _lib.tuning(spectral_chunk=chunk):
+        plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=_lib.SCHEME_SPECTRAL)
+    info = plan.spectral_info()
+    plan.close()
+    assert info["column_bits"] == 16 and info["elem_bytes"] == 1 and info["max_column"] <= 127
+    hist = _spectral_hist(codes, ranges, chunk=chunk)
+    assert hist.astype(np.int64).tolist() == O.c_hist16(codes)[0][:17].tolist()
+
+
+def test_allpairs_spectral_16bit_not_taken():
+    """A 16-bit column of 128 codes: no int8 layout fits, so the plan keeps 14-bit columns with
+    int16 seeds (and stays exact)."""
+    torch = pytest.importorskip("torch")
+    codes = _dense_columns([(128, 10, 10, 10)], 3000, seed=9)
+    d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=_lib.SCHEME_SPECTRAL)
+    info = plan.spectral_info()
+    plan.close()
+    assert info["column_bits"] == 14 and info["elem_bytes"] == 2
+    hist = _spectral_hist(codes)
+    assert hist.astype(np.int64).tolist() == O.c_hist16(codes)[0][:17].tolist()
+
+
 def test_allpairs_config5_spectral_bin_for_bin():
     """Config 5's 3,686,400 codes (int16 intermediate, ~225 codes per column): AUTO (=
     SPECTRAL) bin for bin against the C oracle's count of all 6,794,770,636,800 pairs
@@ -764,6 +826,7 @@ def test_allpairs_config5_spectral_bin_for_bin():
     d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
     plan = _lib.AllPairsPlan(d_codes.data_ptr(), n, 32)
     assert plan.scheme == _lib.SCHEME_SPECTRAL
+    assert plan.spectral_info()["column_bits"] == 16  # int8 seeds on 16-bit columns
     plan.close()
     hs = sharding.allpairs_histogram_sharded(d_codes, 32)
     ref, _ = O.c_hist16(codes)
