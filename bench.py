@@ -265,23 +265,29 @@ def copy_ceiling_gbs(dev, mib=4096, reps=5):
     return 2 * (mib << 20) / (ms * 1e-3) / 1e9
 
 
-def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, names=("spectral_seed", "spectral")):
-    """SPECTRAL's two kernels per chunk: seed (writes 2^14 values per slice) and tile (reads
-    them back: 14-bit WHT + F^2 binning).  Each moves 2^14 * elem_bytes per slice through HBM
-    -- its algorithmic bytes -- so the HBM roofline prices both; the slower is reported.
-    kt = {kind: (ms summed, launches)} from the HIP events around every launch of the timed
-    steps."""
+def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, names=("spectral_seed", "spectral"),
+                      column_bits=14):
+    """SPECTRAL's two kernels per chunk: seed (writes 2^14 values per virtual slice) and tile
+    (reads them back: WHT over the columns + F^2 binning).  Each moves 2^14 * elem_bytes per
+    virtual slice through HBM -- its algorithmic bytes -- so the HBM roofline prices both; the
+    slower is reported.  column_bits 16 (dense sets, spectral16.hip): the same bytes, as 2^16
+    slices of 2^16 int8 values (4 virtual slices each).  kt = {kind: (ms summed, launches)} from
+    the HIP events around every launch of the timed steps."""
     algo = slices_per_launch * (1 << 14) * elem_bytes
     kern = {}
-    for k, label, prof_name, rp in (("seed", "sct_spectral::seed_kernel<%s>" % {1: "int8_t", 2: "int16_t", 4: "int32_t"}[elem_bytes],
-                                     names[0], "seed_kernel<signed char>"),
-                                    ("tile", "sct_spectral::tile_reg_kernel (int8 seeds)" if elem_bytes == 1
-                                     else "sct_spectral::tile_kernel<int%d_t>" % (8 * elem_bytes), names[1],
-                                     "tile_reg_kernel")):
+    if column_bits == 16:
+        kernels = (("seed", "sct_spectral::seed16_kernel (16-bit columns, int8)", names[0] + "16", "seed16_kernel"),
+                   ("tile", "sct_spectral::tile16_kernel (16-bit columns, int8)", names[1] + "16", "tile16_kernel"))
+    else:
+        kernels = (("seed", "sct_spectral::seed_kernel<%s>" % {1: "int8_t", 2: "int16_t", 4: "int32_t"}[elem_bytes],
+                    names[0], "seed_kernel<signed char>"),
+                   ("tile", "sct_spectral::tile_reg_kernel (int8 seeds)" if elem_bytes == 1
+                    else "sct_spectral::tile_kernel<int%d_t>" % (8 * elem_bytes), names[1], "tile_reg_kernel"))
+    for k, label, prof_name, rp in kernels:
         ms, nl = kt[k]
         avg = ms / nl if nl else float("nan")
-        prof = _profile(prof_name) if elem_bytes == 1 else None
-        rms, rcalls = _rocprof_avg_ms(rp) if elem_bytes == 1 else (None, None)
+        prof = _profile(prof_name) if elem_bytes == 1 and column_bits == 14 else None
+        rms, rcalls = _rocprof_avg_ms(rp) if elem_bytes == 1 and column_bits == 14 else (None, None)
         gbs = algo / (avg * 1e-3) / 1e9
         kern[k] = {"kernel": label, "ms": avg, "launches": nl, "achieved_gbs": gbs, "frac": gbs * 1e9 / HBM_PEAK_BPS,
                    "frac_of_copy_ceiling": gbs / copy_gbs if copy_gbs else None,
@@ -422,8 +428,8 @@ def path_config4(dev, reps, copy_gbs, threads):
 
 
 def path_config5_allpairs(dev, steps, copy_gbs):
-    """Config 5's all-pairs half on one GPU: 3,686,400 codes (6.79e12 pairs), SPECTRAL with
-    int16 seeds, pipelined steps as the headline."""
+    """Config 5's all-pairs half on one GPU: 3,686,400 codes (6.79e12 pairs), SPECTRAL on 16-bit
+    columns (int8 seeds; 14-bit columns would need int16), pipelined steps as the headline."""
     import torch
     from oracle import oracle as O
     from sctools_amd import _lib, sharding, synthetic
@@ -439,14 +445,15 @@ def path_config5_allpairs(dev, steps, copy_gbs):
         dt = (time.perf_counter() - t0) / steps
         kt = job.kernel_timing(0)
         info = job.plan.spectral_info()
-        roof = spectral_roofline(kt, min(info["chunk_slices"], job.end - job.begin), info["elem_bytes"], None, copy_gbs)
+        roof = spectral_roofline(kt, min(info["chunk_slices"], job.end - job.begin), info["elem_bytes"], None, copy_gbs,
+                                 column_bits=info["column_bits"])
         P = job.plan.pairs
     hist = hists[-1]
     ok_steps = all(np.array_equal(h, hist) for h in hists)
     m_hist = O.moments_from_hist([int(x) for x in hist], order=2)
     m_codes = O.moments_from_marginals(codes, order=2)
     return {"workload": "config 5 all-pairs: %d-code 16-bp whitelist, all %d pairs" % (n, P),
-            "value": P / dt, "unit": "pairs/s", "ms_per_step": dt * 1e3, "steps": steps,
+            "column_bits": info["column_bits"], "value": P / dt, "unit": "pairs/s", "ms_per_step": dt * 1e3, "steps": steps,
             "roofline": {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel", "kernel_ms",
                                               "launches", "frac_of_copy_ceiling", "other_kernel",
                                               "algo_bytes_per_launch")},
@@ -607,7 +614,7 @@ def run_rank(args, rank, world, local):
     if spectral:
         info = job.plan.spectral_info()
         roofline = spectral_roofline(kt, min(info["chunk_slices"], job.end - job.begin), info["elem_bytes"],
-                                     tm["count_ms"], copy_gbs)
+                                     tm["count_ms"], copy_gbs, column_bits=info["column_bits"])
     else:
         roofline = pair_roofline(job, job.my_pairs(), kt["count"][0] / max(1, kt["count"][1]), L)
     pair_kernel = None

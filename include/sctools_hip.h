@@ -50,7 +50,8 @@ int sct_set_device(int device);        /* select the device for later calls (hip
 #define SCT_TUNE_NEAREST_LOAD 7         /* open addressing: table slots per whitelist code */
 #define SCT_TUNE_SCALAR_SERVER 8        /* 0: every scalar call is a kernel launch (default 1) */
 #define SCT_TUNE_SCALAR_IDLE_MS 9       /* the scalar server exits after this idle time (5) */
-#define SCT_TUNE_NKEYS 10
+#define SCT_TUNE_SPECTRAL_COLUMNS 10   /* SPECTRAL column width: 0 auto, 14, or 16 (when int8 fits) */
+#define SCT_TUNE_NKEYS 11
 int sct_tune_set(int key, int64_t value);
 int sct_tune_get(int key, int64_t* value);  /* -1 when unset */
 

@@ -869,7 +869,8 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   // columns when every one of those holds <= 127 codes (spectral16.hip)
   unsigned maxm = 0;
   if (int rc = max_column(d_codes, n, kLoBits, &maxm); rc != SCT_OK) return rc;
-  if (maxm > 127) {
+  const int64_t force = sct::tune(SCT_TUNE_SPECTRAL_COLUMNS, 0);
+  if ((maxm > 127 && force != kLoBits) || force == kLoBits16) {
     unsigned max16 = 0;
     if (int rc = max_column(d_codes, n, kLoBits16, &max16); rc != SCT_OK) return rc;
     if (max16 <= 127) return create16(st, d_codes, n, max16, chunk, cus);

@@ -18,9 +18,8 @@
 //          G and T_s are each wave's own (as in spectral.hip); U_r needs all four waves: every
 //          wave adds its stage-1 outputs of plane r into an LDS image of U_r (ds_add_u32 on
 //          biased int16 pairs, no carry), and after a barrier wave q takes quarter q (P' bits
-//          4, 5) of every U_r and of V = sum_r U_r through stage 2.  Stage-2 inputs must be
-//          bytes: U_r and T_s by the two-byte split of spectral.hip, V (|V| <= 16 * 64 * 127)
-//          by a three-byte split.
+//          4, 5) of every U_r through stage 2 (the two-byte split of spectral.hip); V's
+//          transform is the sum of the four U_r transforms.
 // Build: the 2^16 columns keep per-workgroup counts and scatter cursors as packed bytes in
 // LDS (every column holds <= 127 codes, so no byte carries), 64 KB per workgroup.
 #include <algorithm>
@@ -36,7 +35,6 @@ constexpr int kLo16 = 1 << kLoBits16;               // columns
 constexpr int kHi16 = kSpaceBits - kLoBits16;       // 16 bit planes
 constexpr int kPW16 = 16;                           // plane words per group: four 16-B words
 constexpr int kWalk16 = 64, kWalkBits16 = 6;
-constexpr int kRegGroups16 = 2;
 constexpr int kSeedWalks16 = 16;
 constexpr int kSortWGs16 = 128, kSortThreads16 = 1024;
 constexpr int kChunk16 = 16384;                     // real slices per seed / tile pass: 1 GiB
@@ -185,7 +183,9 @@ __device__ __forceinline__ void load_planes16(const uint32_t* __restrict__ plane
 // ---------------------------------------------------------------- seed (int8)
 // buf[(z - z0) 2^16 + c] = m(c) - 2 sum over groups of popc(XOR of the planes of z's bits), a
 // workgroup = 256 columns x walks of 64 slices; int8 byte staging and store-out exactly as
-// seed_body<int8_t> in spectral.hip.
+// seed_body<int8_t> in spectral.hip; the first kRegGroups16 groups' planes stay in registers
+// (3 when a column can hold more than 64 codes, as config 5's do, else 2).
+template <int kRegGroups16>
 __global__ __launch_bounds__(256) void seed16_kernel(const uint32_t* __restrict__ planes,
                                                      const uint32_t* __restrict__ gofs,
                                                      const uint32_t* __restrict__ off, int z0, int z1,
@@ -284,19 +284,21 @@ __device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s_t, a) + __builtin_bit_cast(v2s_t, b));
 }
 
-// LDS image of U_r: word ((r * 4 + q) * 8 + 2 mt + h) * 64 + lane holds the int16 pair (h) of
-// stage-1 outputs of quarter q, load mt, lane -- the pairs16 layout of spectral.hip
-constexpr int kUWords = 4 * 4 * 8 * 64;
+// LDS image of U_r: 64-bit word ((r * 4 + q) * 4 + mt) * 64 + lane holds the two int16 pairs
+// (h = 0, 1) of stage-1 outputs of quarter q, load mt, lane -- the pairs16 layout of
+// spectral.hip -- so one ds_add_u64 / ds_read_b64 moves four values (no half ever carries, so
+// neither does the low dword)
+constexpr int kUWords = 4 * 4 * 4 * 64;
 
 // Stage-1 outputs y = v + 8192 (MFMA accumulator start 8192, |v| <= 64 * 127): every y lies
 // in [64, 16320], so the four waves' packed pairs add into one LDS word without a carry
 // (<= 65280 per half), and the two-byte split of y gives 256 hi + lo = v + 8064, whose
 // stage-2 transform exceeds H v by 64 * 8064 at Q' = 0 only -- the high-byte MFMA of the
 // q2 = 0 tile starts from -2016 there (-2016 * 256 = -516096).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile16_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile16_kernel(
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
     unsigned long long* __restrict__ counts, unsigned long long add_n) {
-  __shared__ uint32_t U[kUWords];
+  __shared__ unsigned long long U[kUWords];
   __shared__ unsigned long long bins[17];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;  // wave = S (column digit 7)
   if (tid < 17) bins[tid] = 0;
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) d[mt] = dn[mt];
       if (R < 3) load_plane(s, R + 1, dn);
-      uint32_t* Ur = U + R * (4 * 8 * 64) + lane;
+      unsigned long long* Ur = U + R * (4 * 4 * 64) + lane;
       auto quarters = [&](auto qa_c, auto qb_c) {
         constexpr int qa = decltype(qa_c)::value, qb = decltype(qb_c)::value;
         v4i_t c1a[4], c1b[4];
@@ -434,14 +436,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
         pairs16(c1a, pa);
         pairs16(c1b, pb);
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+        for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             csp[qa][mt][h] = pk_add16(csp[qa][mt][h], pa[mt][h]);
             csp[qb][mt][h] = pk_add16(csp[qb][mt][h], pb[mt][h]);
-            atomicAdd(Ur + (qa * 8 + 2 * mt + h) * 64, pa[mt][h]);
-            atomicAdd(Ur + (qb * 8 + 2 * mt + h) * 64, pb[mt][h]);
           }
+          atomicAdd(Ur + (qa * 4 + mt) * 64, ((unsigned long long)pa[mt][1] << 32) | pa[mt][0]);
+          atomicAdd(Ur + (qb * 4 + mt) * 64, ((unsigned long long)pb[mt][1] << 32) | pb[mt][0]);
+        }
         v2l_t Bla, Bha, Blb, Bhb;
         split16(pa, Bla, Bha);
         split16(pb, Blb, Bhb);
@@ -462,79 +465,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
       stage2x2(Bla, Bha, Blb, Bhb, std::integral_constant<int, 1>(), std::integral_constant<int, 1>(), false, accT);
     }
     __syncthreads();  // every wave's U adds are in
-    {  // quarter q = wave of U_0..U_3 and of V = sum_r U_r
+    {  // quarter q = wave of U_0..U_3; V = sum_r U_r from the sum of their stage-2 outputs
       uint32_t uu[4][4][2];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            uint32_t* p = U + ((r * 4 + wave) * 8 + 2 * mt + h) * 64 + lane;
-            uu[r][mt][h] = *p;
-            *p = 0u;  // read by this wave only: cleared for the next slice
-          }
-      // V: per value, sum_r (U_v + 32768) = V + 131072; y = V + 32896 -> three bytes
-      int32_t yv[4][4];  // [mt][value], values in pairs16 order (pair 0 lo, hi, pair 1 lo, hi)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          int32_t sum = 0;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sum += (int32_t)((uu[r][mt][j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
-          yv[mt][j] = sum - 131072 + 32896;
+        for (int mt = 0; mt < 4; ++mt) {
+          unsigned long long* p = U + ((r * 4 + wave) * 4 + mt) * 64 + lane;
+          const unsigned long long v = *p;
+          *p = 0ull;  // read by this wave only: cleared for the next slice
+          // + 0x8080 per half (mod 2^16) turns U + 32768 into U + 128 (the csp form)
+          uu[r][mt][0] = pk_add16((uint32_t)v, 0x80808080u);
+          uu[r][mt][1] = pk_add16((uint32_t)(v >> 32), 0x80808080u);
         }
-      // U_r: + 0x8080 per half (mod 2^16) turns U + 32768 into U + 128 (the csp form)
+      v4i_t fv[4] = {v4i_t{0, 0, 0, 0}, v4i_t{0, 0, 0, 0}, v4i_t{0, 0, 0, 0}, v4i_t{0, 0, 0, 0}};
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 4; r += 2) {
+        v2l_t Bla, Bha, Blb, Bhb;
+        split16(uu[r], Bla, Bha);
+        split16(uu[r + 1], Blb, Bhb);
+        v4i_t ca[4], cb[4];
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+        for (int q2 = 0; q2 < 4; ++q2) {
+          ca[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bha, v4i_t{0, 0, 0, 0}, 0, 0, 0);
+          cb[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bhb, v4i_t{0, 0, 0, 0}, 0, 0, 0);
+        }
 #pragma unroll
-          for (int h = 0; h < 2; ++h) uu[r][mt][h] = pk_add16(uu[r][mt][h], 0x80808080u);
-      v2l_t Bla, Bha, Blb, Bhb;
-      split16(uu[0], Bla, Bha);
-      split16(uu[1], Blb, Bhb);
-      stage2x2(Bla, Bha, Blb, Bhb, std::integral_constant<int, 0>(), std::integral_constant<int, 0>(), false, accU);
-      split16(uu[2], Bla, Bha);
-      split16(uu[3], Blb, Bhb);
-      stage2x2(Bla, Bha, Blb, Bhb, std::integral_constant<int, 0>(), std::integral_constant<int, 0>(), false, accU);
-      // V: V = 65536 t2 + 256 t1 + t0, t0 / t1 = bytes 0 / 1 of y minus 128, t2 = y >> 16
-      uint32_t b0[4], b1[4], b2[4];
+        for (int q2 = 0; q2 < 4; ++q2) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const uint32_t lo01 = __builtin_amdgcn_perm((uint32_t)yv[mt][1], (uint32_t)yv[mt][0], 0x05010400u);
-        const uint32_t lo23 = __builtin_amdgcn_perm((uint32_t)yv[mt][3], (uint32_t)yv[mt][2], 0x05010400u);
-        b0[mt] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u) ^ 0x80808080u;  // byte 0 of each
-        b1[mt] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u) ^ 0x80808080u;  // byte 1 of each
-        const uint32_t t01 = __builtin_amdgcn_perm((uint32_t)(yv[mt][1] >> 16), (uint32_t)(yv[mt][0] >> 16),
-                                                   0x05010400u);
-        const uint32_t t23 = __builtin_amdgcn_perm((uint32_t)(yv[mt][3] >> 16), (uint32_t)(yv[mt][2] >> 16),
-                                                   0x05010400u);
-        b2[mt] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
-      }
-      const v2l_t B0 = pack16(b0), B1 = pack16(b1), B2 = pack16(b2);
-      v4i_t cv[4];
+          for (int i = 0; i < 4; ++i) ca[q2][i] <<= 8;
+          ca[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Bla, ca[q2], 0, 0, 0);
 #pragma unroll
-      for (int q2 = 0; q2 < 4; ++q2) cv[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], B2, v4i_t{0, 0, 0, 0}, 0, 0, 0);
+          for (int i = 0; i < 4; ++i) cb[q2][i] <<= 8;
+          cb[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], Blb, cb[q2], 0, 0, 0);
+        }
 #pragma unroll
-      for (int q2 = 0; q2 < 4; ++q2) {
+        for (int q2 = 0; q2 < 4; ++q2)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) cv[q2][i] <<= 8;
-        cv[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], B1, cv[q2], 0, 0, 0);
-      }
-#pragma unroll
-      for (int q2 = 0; q2 < 4; ++q2) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) cv[q2][i] <<= 8;
-        cv[q2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(H[q2], B0, cv[q2], 0, 0, 0);
+          for (int i = 0; i < 4; ++i) {
+            const int k = digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i);
+            accU[k] += (unsigned long long)((int64_t)ca[q2][i] * ca[q2][i]);
+            accU[k] += (unsigned long long)((int64_t)cb[q2][i] * cb[q2][i]);
+            fv[q2][i] += ca[q2][i] + cb[q2][i];  // |V's transform| <= 64 * 16 * 8128
+          }
       }
 #pragma unroll
       for (int q2 = 0; q2 < 4; ++q2)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           accV[digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
-              (unsigned long long)((int64_t)cv[q2][i] * cv[q2][i]);
+              (unsigned long long)((int64_t)fv[q2][i] * fv[q2][i]);
     }
     __syncthreads();  // U cleared before the next slice's adds
   }
@@ -549,8 +529,9 @@ int launch_chunk16(State& st, int z0, int z1, unsigned long long* counts, hipStr
   hipEvent_t t0 = st.timer ? st.timer->start(s) : nullptr;
   const int walks = (z1 - (z0 & ~(kWalk16 - 1)) + kWalk16 - 1) / kWalk16;
   const int per_wg = std::max(1, std::min(kSeedWalks16, walks / 16));
-  hipLaunchKernelGGL(seed16_kernel, dim3(kLo16 / 256, (unsigned)((walks + per_wg - 1) / per_wg)), dim3(256), 0, s,
-                     st.d_planes, st.d_gofs, st.d_off, z0, z1, buf);
+  hipLaunchKernelGGL(st.max_m > 64 ? seed16_kernel<3> : seed16_kernel<2>,
+                     dim3(kLo16 / 256, (unsigned)((walks + per_wg - 1) / per_wg)), dim3(256), 0, s, st.d_planes,
+                     st.d_gofs, st.d_off, z0, z1, buf);
   SCT_LAUNCH_CHECK();
   if (st.timer) st.timer->stop(s, t0, sct::LaunchTimer::SEED);
   t0 = st.timer ? st.timer->start(s) : nullptr;
@@ -642,8 +623,9 @@ int time_kernels16(State& st, int64_t z_begin, int64_t z_end, unsigned long long
   const uint16_t* order = ((ns & (ns - 1)) == 0 && ns <= (1 << 16) && rb % ns == 0) ? st.d_order + ns : nullptr;
   SCT_HIP(hipEventRecord(e[0], s));
   for (int r = 0; rc == SCT_OK && r < repeats; ++r)
-    hipLaunchKernelGGL(seed16_kernel, dim3(kLo16 / 256, (unsigned)((walks + per_wg - 1) / per_wg)), dim3(256), 0, s,
-                       st.d_planes, st.d_gofs, st.d_off, (int)rb, (int)re, buf);
+    hipLaunchKernelGGL(st.max_m > 64 ? seed16_kernel<3> : seed16_kernel<2>,
+                       dim3(kLo16 / 256, (unsigned)((walks + per_wg - 1) / per_wg)), dim3(256), 0, s, st.d_planes,
+                       st.d_gofs, st.d_off, (int)rb, (int)re, buf);
   SCT_HIP(hipEventRecord(e[1], s));
   for (int r = 0; rc == SCT_OK && r < repeats; ++r)
     hipLaunchKernelGGL(tile16_kernel, dim3((unsigned)std::max(1, std::min(st.grid * st.tile_wgs, ns))), dim3(256), 0,
