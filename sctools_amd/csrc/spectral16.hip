@@ -524,21 +524,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   if (add_n && blockIdx.x == 0 && tid == 0) atomicAdd(counts, add_n);  // n, once per job
 }
 
-int launch_chunk16(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s, unsigned long long add_n) {
-  int8_t* buf = reinterpret_cast<int8_t*>(st.d_buf);
-  hipEvent_t t0 = st.timer ? st.timer->start(s) : nullptr;
+void launch_seed16(State& st, int8_t* buf, int z0, int z1, hipStream_t s) {
   const int walks = (z1 - (z0 & ~(kWalk16 - 1)) + kWalk16 - 1) / kWalk16;
   const int per_wg = std::max(1, std::min(kSeedWalks16, walks / 16));
   hipLaunchKernelGGL(st.max_m > 64 ? seed16_kernel<3> : seed16_kernel<2>,
                      dim3(kLo16 / 256, (unsigned)((walks + per_wg - 1) / per_wg)), dim3(256), 0, s, st.d_planes,
                      st.d_gofs, st.d_off, z0, z1, buf);
+}
+
+void launch_tile16(State& st, const int8_t* buf, int z0, int z1, unsigned long long* counts, hipStream_t s,
+                   unsigned long long add_n, int wgs_per_cu) {
+  const int ns = z1 - z0;
+  const uint16_t* order = ((ns & (ns - 1)) == 0 && ns <= (1 << 16) && z0 % ns == 0) ? st.d_order + ns : nullptr;
+  hipLaunchKernelGGL(tile16_kernel, dim3((unsigned)std::max(1, std::min(st.grid * wgs_per_cu, ns))), dim3(256), 0, s,
+                     buf, order, z0, ns, counts, add_n);
+}
+
+int launch_chunk16(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s, unsigned long long add_n) {
+  int8_t* buf = reinterpret_cast<int8_t*>(st.d_buf);
+  hipEvent_t t0 = st.timer ? st.timer->start(s) : nullptr;
+  launch_seed16(st, buf, z0, z1, s);
   SCT_LAUNCH_CHECK();
   if (st.timer) st.timer->stop(s, t0, sct::LaunchTimer::SEED);
   t0 = st.timer ? st.timer->start(s) : nullptr;
-  const int ns = z1 - z0;
-  const uint16_t* order = ((ns & (ns - 1)) == 0 && ns <= (1 << 16) && z0 % ns == 0) ? st.d_order + ns : nullptr;
-  hipLaunchKernelGGL(tile16_kernel, dim3((unsigned)std::max(1, std::min(st.grid * st.tile_wgs, ns))), dim3(256), 0, s,
-                     buf, order, z0, ns, counts, add_n);
+  launch_tile16(st, buf, z0, z1, counts, s, add_n, st.tile_wgs);
   SCT_LAUNCH_CHECK();
   if (st.timer) st.timer->stop(s, t0, sct::LaunchTimer::TILE);
   return SCT_OK;
