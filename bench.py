@@ -49,6 +49,7 @@ sys.path.insert(0, ROOT)
 # Full-rate VALU issue: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6 T lane-slots/s
 # (measured 121 lane-ops/clk/CU for v_xor_b32, profiles/valu_peak_r01.json).
 VALU_PEAK_OPS = 256 * 128 * 2.4e9
+L2_PEAK_BPS = 34.5e12  # aggregate L2 bandwidth, MI355X_MICROARCH.md §L2
 HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E (MI355X_MICROARCH.md)
 SIMDS = 256 * 4
 ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-bit code word
@@ -373,6 +374,20 @@ def _events_ms(fn, reps, dev):
     return e0.elapsed_time(e1) / reps
 
 
+def l2_roofline(prof, nq, ms):
+    """Config 4 against the L2 request ceiling: the half-key tables and permAB are L2-resident,
+    so every probe is an L2 request; requests per query from the committed PMC passes (query
+    kernel + index pass) x queries / the live time, against 34.5 TB/s of 128-B requests
+    (MI355X_MICROARCH.md §L2)."""
+    rq = sum((prof.get(k) or {}).get("l2_requests_per_unit") or 0.0 for k in ("nearest", "nearest_index"))
+    if not rq:
+        return None
+    ceil = L2_PEAK_BPS / 128.0
+    rate = rq * nq / (ms * 1e-3)
+    return {"requests_per_query": rq, "achieved": rate, "peak": ceil, "unit": "requests/s", "frac": rate / ceil,
+            "source": [prof[k]["file"] for k in ("nearest", "nearest_index") if k in prof]}
+
+
 def path_config4(dev, reps, copy_gbs, threads):
     """Config 4: nearest-whitelist correction of 100M ThreeBit observed barcodes against the
     737,280-code whitelist at Hamming <= 1 (sct_nearest_query on device-resident queries)."""
@@ -419,9 +434,11 @@ def path_config4(dev, reps, copy_gbs, threads):
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
                          "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs,
                          "algo_bytes_per_query": 13, "kernel": "sct_nearest_query",
+                         "l2": l2_roofline(prof, nq, ms),
                          "pmc": prof or None,
                          "note": "algorithmic bytes = the query stream (8 B in, 4 + 1 B out); the index "
-                                 "probes are extra (DESIGN.md §3.5)"},
+                                 "probes are extra and L2-resident: the binding ceiling is the L2 request "
+                                 "rate (`l2`, DESIGN.md §3.5)"},
             "check": {"exact_draws_own_index": exact_ok, "sampled_vs_oracle": sample_ok,
                       "sample": "20,000 random queries vs oracle.c_nearest (OpenMP brute force over the whole "
                                 "whitelist)"}}

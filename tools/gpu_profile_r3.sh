@@ -1,6 +1,7 @@
 # Round-3 profiles: rocprofv3 kernel trace + stats of the exact default bench command, PMC
 # passes (each its own run, within the per-block counter limits) of a short bench run, and
-# the same for config 4's nearest queries.  Output under gpurun_out/prof3/.
+# the same for config 4's nearest queries and for config 5's 16-bit-column SPECTRAL kernels
+# (tools/spectral_kernels.py 5).  Output under gpurun_out/prof3/.
 set -u
 cd "$GRAFT_REPO_ROOT"
 P=gpurun_out/prof3
@@ -14,6 +15,14 @@ for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES 
            "SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $pmc -d $P/pmc$i -o run --output-format csv -- $B > $P/pmc$i.log 2>&1 || echo "pmc pass $i failed"
+done
+S5="python3 tools/spectral_kernels.py 5 2"
+timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $P/s5trace -o run --output-format csv -- $S5 > $P/s5trace.log 2>&1 || exit 3
+i=0
+for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $pmc -d $P/s5pmc$i -o run --output-format csv -- $S5 > $P/s5pmc$i.log 2>&1 || echo "config-5 pmc pass $i failed"
 done
 N="python3 tools/nearest_run.py --reps 3"
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $P/ntrace -o run --output-format csv -- $N > $P/ntrace.log 2>&1 || exit 3

@@ -28,6 +28,8 @@ KERNELS = (
     ("spectral_seed", "seed_kernel<signed char>", "pmc", "trace", 65536, "slices"),
     ("spectral", "tile_reg_kernel", "pmc", "trace", 65536, "slices"),
     ("spectral_seed_int16", "seed_kernel<short>", "pmc", "trace", 65536, "slices"),
+    ("spectral_seed16", "seed16_kernel", "s5pmc", "s5trace", 16384, "slices of 2^16"),
+    ("spectral16", "tile16_kernel", "s5pmc", "s5trace", 16384, "slices of 2^16"),
     ("nearest", "halves_query_kernel", "npmc", "ntrace", 100_000_000, "queries"),
     ("nearest_index", "halves_index_kernel", "npmc", "ntrace", 100_000_000, "queries"),
 )
@@ -96,7 +98,8 @@ def main():
     a = ap.parse_args()
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
-    for trace, fn in (("trace", "%s_kernel_stats.csv"), ("ntrace", "%s_nearest_kernel_stats.csv")):
+    for trace, fn in (("trace", "%s_kernel_stats.csv"), ("ntrace", "%s_nearest_kernel_stats.csv"),
+                      ("s5trace", "%s_config5_kernel_stats.csv")):
         src = os.path.join(a.src, trace, "run_kernel_stats.csv")
         if os.path.exists(src):
             shutil.copy(src, os.path.join(dst, fn % a.round))
