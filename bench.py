@@ -277,11 +277,11 @@ def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, nam
     algo = slices_per_launch * (1 << 14) * elem_bytes
     kern = {}
     if column_bits == 16:
-        kernels = (("seed", "sct_spectral::seed16_kernel (16-bit columns, int8)", names[0] + "16", "seed16_kernel"),
+        kernels = (("seed", "sct_spectral::seed16_sm_kernel (16-bit columns, int8)", names[0] + "16", "seed16_sm_kernel"),
                    ("tile", "sct_spectral::tile16_kernel (16-bit columns, int8)", names[1] + "16", "tile16_kernel"))
     else:
-        kernels = (("seed", "sct_spectral::seed_kernel<%s>" % {1: "int8_t", 2: "int16_t", 4: "int32_t"}[elem_bytes],
-                    names[0], "seed_kernel<signed char>"),
+        kernels = (("seed", "sct_spectral::seed_sm_kernel (int8)" if elem_bytes == 1 else
+                    "sct_spectral::seed_kernel<int%d_t>" % (8 * elem_bytes), names[0], "seed_sm_kernel"),
                    ("tile", "sct_spectral::tile_reg_kernel (int8 seeds)" if elem_bytes == 1
                     else "sct_spectral::tile_kernel<int%d_t>" % (8 * elem_bytes), names[1], "tile_reg_kernel"))
     for k, label, prof_name, rp in kernels:

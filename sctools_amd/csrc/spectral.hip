@@ -273,28 +273,11 @@ __device__ __forceinline__ int column_pos(int c) {
 }
 
 
-// Byte (int8) / half (int16) transposes for the seed's store-out: p dwords hold P values of
-// consecutive slices for one column each; out[j] = the j-th values of all of them, packed.
-__device__ __forceinline__ void transpose4x4_bytes(const uint32_t* d, uint32_t* out) {
-  // d[0..3] bytes (slice 0..3) of columns 0..3  ->  out[j] = (d0.j, d1.j, d2.j, d3.j)
-  const uint32_t ab_lo = __builtin_amdgcn_perm(d[1], d[0], 0x05010400u);  // a0 b0 a1 b1
-  const uint32_t ab_hi = __builtin_amdgcn_perm(d[1], d[0], 0x07030602u);  // a2 b2 a3 b3
-  const uint32_t cd_lo = __builtin_amdgcn_perm(d[3], d[2], 0x05010400u);
-  const uint32_t cd_hi = __builtin_amdgcn_perm(d[3], d[2], 0x07030602u);
-  out[0] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u);  // a0 b0 c0 d0
-  out[1] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u);  // a1 b1 c1 d1
-  out[2] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u);
-  out[3] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
-}
-
-
-// buf[(z - z0) 2^14 + pos(c)] = sum over codes x of column c of (-1)^popc((x >> 14) & z)
-//                             = m(c) - 2 sum over groups of popc(XOR of the planes of z's bits).
-// A workgroup owns 256 columns and walks of 64 slices (blockIdx.y, strided): each lane walks
-// its column in Gray order (one XOR per step from registers).  int8: the raw popcount sums
-// are staged in LDS as bytes (row = slice, byte = column) and each thread forms m - 2 acc for
-// 16 columns of a slice row at once; int16 / int32: dwords of 4 / sizeof(T) consecutive
-// slices per column, transposed in registers; both written as 16-B chunks of slice rows.
+// int16 / int32 seeds (columns of more than 127 codes): a workgroup owns 256 columns and walks of
+// 64 slices (blockIdx.y, strided): each lane walks its column in Gray order (one XOR per step
+// from registers) group by group into a 64-value accumulator array; dwords of 4 / sizeof(T)
+// consecutive slices per column are staged in LDS, transposed in registers and written as 16-B
+// chunks of slice rows.  (int8 seeds: seed_sm_kernel below.)
 template <typename T>
 __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes, const uint32_t* __restrict__ gofs,
                                           const uint32_t* __restrict__ off, int z0, int z1, T* __restrict__ buf) {
@@ -320,23 +303,6 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes, c
 #pragma unroll
       for (int k = 0; k < kHiBits; ++k) pr[g][k] = 0u;
     }
-  // int8 byte store-out: this thread writes columns c0 + mcb .. + 15; mx = their m | 0x80 as bytes
-  constexpr bool kByteStage = sizeof(T) == 1;
-  const int mcb = (tid % (NT / 16)) * 16;
-  uint4 mx = make_uint4(0, 0, 0, 0);
-  if constexpr (kByteStage) {
-    uint32_t w[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      w[k] = 0x80808080u;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int cc = c0 + mcb + 4 * k + b;
-        w[k] |= (off[cc + 1] - off[cc]) << (8 * b);
-      }
-    }
-    mx = make_uint4(w[0], w[1], w[2], w[3]);
-  }
   // Co-resident workgroups start together and run identical walks, so they stay in
   // lockstep: all 12 waves of a CU walk (VALU-bound) and then all store (HBM-bound).
   // Starting them 0 / 1,536 / 3,072 cycles apart lets one workgroup's stores drain under
@@ -379,42 +345,7 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes, c
       }
       walk(p, std::false_type());
     }
-    if constexpr (kByteStage) {
-      // int8: the raw popcount sums go to LDS as bytes (row = slice, byte = column; no
-      // packing), and the store-out forms m - 2 acc for 16 columns at once:
-      //   ((m | 0x80) - 2 acc) ^ 0x80 per byte -- acc <= m <= 127, so 2 acc fits a byte
-      //   and m + 128 - 2 acc lies in [1, 255]: no carry or borrow crosses a byte.
-      uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
-      __syncthreads();  // the previous walk's store-out reads of `stage` are done
-#pragma unroll
-      for (int i = 0; i < kWalk; ++i) st8[i * NT + tid] = (uint8_t)acc[i];
-      __syncthreads();
-      if (zblk >= z0 && zblk + kWalk <= z1) {  // the whole walk is in range: all loads, then all stores
-        uint4 v[kWalk / 16];
-#pragma unroll
-        for (int r = 0; r < kWalk / 16; ++r)
-          v[r] = *reinterpret_cast<const uint4*>(st8 + (tid / (NT / 16) + 16 * r) * NT + mcb);
-#pragma unroll
-        for (int r = 0; r < kWalk / 16; ++r) {
-          const uint4 o = make_uint4((mx.x - (v[r].x + v[r].x)) ^ 0x80808080u, (mx.y - (v[r].y + v[r].y)) ^ 0x80808080u,
-                                     (mx.z - (v[r].z + v[r].z)) ^ 0x80808080u, (mx.w - (v[r].w + v[r].w)) ^ 0x80808080u);
-          const int z = zblk + tid / (NT / 16) + 16 * r;
-          *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + mcb)) = o;
-        }
-        continue;
-      }
-#pragma unroll
-      for (int r = 0; r < kWalk / 16; ++r) {
-        const int row = tid / (NT / 16) + 16 * r;
-        const uint4 v = *reinterpret_cast<const uint4*>(st8 + row * NT + mcb);
-        const uint4 o = make_uint4((mx.x - (v.x + v.x)) ^ 0x80808080u, (mx.y - (v.y + v.y)) ^ 0x80808080u,
-                                   (mx.z - (v.z + v.z)) ^ 0x80808080u, (mx.w - (v.w + v.w)) ^ 0x80808080u);
-        const int z = zblk + row;
-        if (z >= z0 && z < z1)
-          *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + column_pos<T>(c0 + mcb)) = o;
-      }
-      continue;
-    } else {
+    {
       __syncthreads();  // the previous walk's store-out reads of `stage` are done
       // 4-dword groups of a 16-dword column block XOR-swizzled by the block, so the
       // store-out's b128 reads of 16 consecutive columns are conflict-free
@@ -461,6 +392,114 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes, c
               make_uint4(out[j][0], out[j][1], out[j][2], out[j][3]);
         }
       }
+    }
+  }
+}
+
+// int8 seeds, step-major walk: per step every group's XOR and popcount, and the step's sum
+// goes to the byte stage at once -- no 64-value accumulator array, so the first three groups'
+// planes stay in registers at 4+ waves per SIMD.  G = the wave's group count (<= 3; a fourth
+// and later group, columns of > 96 codes, is walked afterwards from L2 into the lane's own
+// stage bytes).  Store-out as seed_body<int8_t>.
+template <int G>
+__device__ __forceinline__ void walk_sm(const uint32_t (*pr)[kHiBits], int zblk, uint8_t* st8, int tid) {
+  uint32_t x[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = kWalkBits; k < kHiBits; ++k)
+      if ((zblk >> k) & 1) v ^= pr[g][k];
+    x[g] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < kWalk; ++i) {
+    uint32_t a = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (i) x[g] ^= pr[g][ctz_c(i)];
+      a += __popc(x[g]);
+    }
+    st8[gray(i) * 256 + tid] = (uint8_t)a;
+    if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting steps
+  }
+}
+
+constexpr int kRegGroupsSM = 3;
+__global__ __launch_bounds__(256) void seed_sm_kernel(const uint32_t* __restrict__ planes,
+                                                      const uint32_t* __restrict__ gofs,
+                                                      const uint32_t* __restrict__ off, int z0, int z1,
+                                                      int8_t* __restrict__ buf) {
+  constexpr int NT = 256;
+  __shared__ uint32_t stage[kWalk * NT / 4];
+  uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.x * NT, c = c0 + tid;
+  const uint32_t g0 = gofs[c];
+  const int ng = (int)(gofs[c + 1] - g0);
+  int wng = ng;
+#pragma unroll
+  for (int s = 32; s; s >>= 1) wng = max(wng, __shfl_xor(wng, s));
+  uint32_t pr[kRegGroupsSM][kHiBits];
+#pragma unroll
+  for (int g = 0; g < kRegGroupsSM; ++g)
+    if (g < ng) {
+      load_planes(planes, (int64_t)g0 + g, pr[g]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kHiBits; ++k) pr[g][k] = 0u;
+    }
+  const int mcb = (tid % (NT / 16)) * 16;
+  uint32_t mx[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    mx[k] = 0x80808080u;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int cc = c0 + mcb + 4 * k + b;
+      mx[k] |= (off[cc + 1] - off[cc]) << (8 * b);
+    }
+  }
+  {
+    const int ph = (blockIdx.x + blockIdx.y) % 3;
+    if (ph >= 1) __builtin_amdgcn_s_sleep(24);
+    if (ph == 2) __builtin_amdgcn_s_sleep(24);
+  }
+  const int za = z0 & ~(kWalk - 1);
+  const int nwalks = (z1 - za + kWalk - 1) / kWalk;
+  for (int wk = blockIdx.y; wk < nwalks; wk += gridDim.y) {
+    const int zblk = za + wk * kWalk;
+    __syncthreads();  // the previous walk's store-out reads of `stage` are done
+    if (wng <= 1) walk_sm<1>(pr, zblk, st8, tid);
+    else if (wng == 2) walk_sm<2>(pr, zblk, st8, tid);
+    else walk_sm<3>(pr, zblk, st8, tid);
+    for (int g = kRegGroupsSM; g < wng; ++g) {  // columns of > 96 codes: the rest from L2
+      uint32_t p[kHiBits];
+      if (g < ng) {
+        load_planes(planes, (int64_t)g0 + g, p);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kHiBits; ++k) p[k] = 0u;
+      }
+      uint32_t x = 0;
+#pragma unroll
+      for (int k = kWalkBits; k < kHiBits; ++k)
+        if ((zblk >> k) & 1) x ^= p[k];
+#pragma unroll
+      for (int i = 0; i < kWalk; ++i) {
+        if (i) x ^= p[ctz_c(i)];
+        st8[gray(i) * NT + tid] += (uint8_t)__popc(x);
+        if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kWalk / 16; ++r) {
+      const int row = tid / (NT / 16) + 16 * r, z = zblk + row;
+      const uint4 v = *reinterpret_cast<const uint4*>(st8 + row * NT + mcb);
+      const uint4 o = make_uint4((mx[0] - (v.x + v.x)) ^ 0x80808080u, (mx[1] - (v.y + v.y)) ^ 0x80808080u,
+                                 (mx[2] - (v.z + v.z)) ^ 0x80808080u, (mx[3] - (v.w + v.w)) ^ 0x80808080u);
+      if (z >= z0 && z < z1) *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + c0 + mcb) = o;
     }
   }
 }
@@ -763,7 +802,10 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
   // keep >= 64 workgroup rows so the grid still fills the chip
   const int per_wg = std::max(1, std::min(kSeedWalks, walks / 64));
   const dim3 sgrid(kLo / 256, (unsigned)((walks + per_wg - 1) / per_wg));
-  hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, z0, z1, buf);
+  if constexpr (sizeof(T) == 1)
+    hipLaunchKernelGGL(seed_sm_kernel, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, z0, z1, buf);
+  else
+    hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, z0, z1, buf);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }

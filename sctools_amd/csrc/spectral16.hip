@@ -182,16 +182,42 @@ __device__ __forceinline__ void load_planes16(const uint32_t* __restrict__ plane
 
 // ---------------------------------------------------------------- seed (int8)
 // buf[(z - z0) 2^16 + c] = m(c) - 2 sum over groups of popc(XOR of the planes of z's bits), a
-// workgroup = 256 columns x walks of 64 slices; int8 byte staging and store-out exactly as
-// seed_body<int8_t> in spectral.hip; the first kRegGroups16 groups' planes stay in registers
-// (3 when a column can hold more than 64 codes, as config 5's do, else 2).
-template <int kRegGroups16>
-__global__ __launch_bounds__(256) void seed16_kernel(const uint32_t* __restrict__ planes,
-                                                     const uint32_t* __restrict__ gofs,
-                                                     const uint32_t* __restrict__ off, int z0, int z1,
-                                                     int8_t* __restrict__ buf) {
+// workgroup = 256 columns x walks of 64 slices: the step-major walk of seed_sm_kernel in
+// spectral.hip (per step every group's XOR and popcount, the sum straight into the byte stage;
+// the first three groups' planes in registers, a fourth from L2), int8 byte staging and
+// store-out as there.
+template <int G>
+__device__ __forceinline__ void walk_sm16(const uint32_t (*pr)[kHi16], int zblk, uint8_t* st8, int tid) {
+  uint32_t x[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = kWalkBits16; k < kHi16; ++k)
+      if ((zblk >> k) & 1) v ^= pr[g][k];
+    x[g] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < kWalk16; ++i) {
+    uint32_t a = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (i) x[g] ^= pr[g][ctz_c(i)];
+      a += __popc(x[g]);
+    }
+    st8[gray(i) * 256 + tid] = (uint8_t)a;
+    if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+constexpr int RG = 3;
+__global__ __launch_bounds__(256) void seed16_sm_kernel(const uint32_t* __restrict__ planes,
+                                                        const uint32_t* __restrict__ gofs,
+                                                        const uint32_t* __restrict__ off, int z0, int z1,
+                                                        int8_t* __restrict__ buf) {
   constexpr int NT = 256;
   __shared__ uint32_t stage[kWalk16 * NT / 4];
+  uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
   const int tid = threadIdx.x;
   const int c0 = blockIdx.x * NT, c = c0 + tid;
   const uint32_t g0 = gofs[c];
@@ -199,9 +225,9 @@ __global__ __launch_bounds__(256) void seed16_kernel(const uint32_t* __restrict_
   int wng = ng;
 #pragma unroll
   for (int s = 32; s; s >>= 1) wng = max(wng, __shfl_xor(wng, s));
-  uint32_t pr[kRegGroups16][kHi16];
+  uint32_t pr[RG][kHi16];
 #pragma unroll
-  for (int g = 0; g < kRegGroups16; ++g)
+  for (int g = 0; g < RG; ++g)
     if (g < ng) {
       load_planes16(planes, (int64_t)g0 + g, pr[g]);
     } else {
@@ -219,36 +245,20 @@ __global__ __launch_bounds__(256) void seed16_kernel(const uint32_t* __restrict_
       mx[k] |= (off[cc + 1] - off[cc]) << (8 * b);
     }
   }
-  {  // co-resident workgroups start apart (spectral.hip seed_body)
+  {
     const int ph = (blockIdx.x + blockIdx.y) % 3;
     if (ph >= 1) __builtin_amdgcn_s_sleep(24);
     if (ph == 2) __builtin_amdgcn_s_sleep(24);
   }
-  uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
   const int za = z0 & ~(kWalk16 - 1);
   const int nwalks = (z1 - za + kWalk16 - 1) / kWalk16;
   for (int wk = blockIdx.y; wk < nwalks; wk += gridDim.y) {
     const int zblk = za + wk * kWalk16;
-    int acc[kWalk16];
-    auto walk = [&](const uint32_t* p, auto first) {
-      uint32_t x = 0;
-#pragma unroll
-      for (int k = kWalkBits16; k < kHi16; ++k)
-        if ((zblk >> k) & 1) x ^= p[k];
-      if constexpr (decltype(first)::value) acc[0] = __popc(x);
-      else acc[0] += __popc(x);
-#pragma unroll
-      for (int i = 1; i < kWalk16; ++i) {
-        x ^= p[ctz_c(i)];
-        if constexpr (decltype(first)::value) acc[gray(i)] = __popc(x);
-        else acc[gray(i)] += __popc(x);
-      }
-    };
-    walk(pr[0], std::true_type());
-#pragma unroll
-    for (int g = 1; g < kRegGroups16; ++g)
-      if (g < wng) walk(pr[g], std::false_type());
-    for (int g = kRegGroups16; g < wng; ++g) {  // third and fourth groups from L2
+    __syncthreads();  // the previous walk's store-out reads of `stage` are done
+    if (wng <= 1) walk_sm16<1>(pr, zblk, st8, tid);
+    else if (wng == 2) walk_sm16<2>(pr, zblk, st8, tid);
+    else walk_sm16<3>(pr, zblk, st8, tid);
+    for (int g = RG; g < wng; ++g) {  // the groups past the register-resident ones, from L2
       uint32_t p[kHi16];
       if (g < ng) {
         load_planes16(planes, (int64_t)g0 + g, p);
@@ -256,11 +266,17 @@ __global__ __launch_bounds__(256) void seed16_kernel(const uint32_t* __restrict_
 #pragma unroll
         for (int k = 0; k < kHi16; ++k) p[k] = 0u;
       }
-      walk(p, std::false_type());
-    }
-    __syncthreads();  // the previous walk's store-out reads of `stage` are done
+      uint32_t x = 0;
 #pragma unroll
-    for (int i = 0; i < kWalk16; ++i) st8[i * NT + tid] = (uint8_t)acc[i];
+      for (int k = kWalkBits16; k < kHi16; ++k)
+        if ((zblk >> k) & 1) x ^= p[k];
+#pragma unroll
+      for (int i = 0; i < kWalk16; ++i) {
+        if (i) x ^= p[ctz_c(i)];
+        st8[gray(i) * NT + tid] += (uint8_t)__popc(x);
+        if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kWalk16 / 16; ++r) {
@@ -527,9 +543,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
 void launch_seed16(State& st, int8_t* buf, int z0, int z1, hipStream_t s) {
   const int walks = (z1 - (z0 & ~(kWalk16 - 1)) + kWalk16 - 1) / kWalk16;
   const int per_wg = std::max(1, std::min(kSeedWalks16, walks / 16));
-  hipLaunchKernelGGL(st.max_m > 64 ? seed16_kernel<3> : seed16_kernel<2>,
-                     dim3(kLo16 / 256, (unsigned)((walks + per_wg - 1) / per_wg)), dim3(256), 0, s, st.d_planes,
-                     st.d_gofs, st.d_off, z0, z1, buf);
+  hipLaunchKernelGGL(seed16_sm_kernel, dim3(kLo16 / 256, (unsigned)((walks + per_wg - 1) / per_wg)), dim3(256), 0, s,
+                     st.d_planes, st.d_gofs, st.d_off, z0, z1, buf);
 }
 
 void launch_tile16(State& st, const int8_t* buf, int z0, int z1, unsigned long long* counts, hipStream_t s,
@@ -626,15 +641,10 @@ int time_kernels16(State& st, int64_t z_begin, int64_t z_end, unsigned long long
   st.timer = nullptr;
   int rc = launch_chunk16(st, (int)rb, (int)re, d_counts, s, 0);  // warm
   int8_t* buf = reinterpret_cast<int8_t*>(st.d_buf);
-  const int walks = (int)((re - (rb & ~(kWalk16 - 1)) + kWalk16 - 1) / kWalk16);
-  const int per_wg = std::max(1, std::min(kSeedWalks16, walks / 16));
   const int ns = (int)(re - rb);
   const uint16_t* order = ((ns & (ns - 1)) == 0 && ns <= (1 << 16) && rb % ns == 0) ? st.d_order + ns : nullptr;
   SCT_HIP(hipEventRecord(e[0], s));
-  for (int r = 0; rc == SCT_OK && r < repeats; ++r)
-    hipLaunchKernelGGL(st.max_m > 64 ? seed16_kernel<3> : seed16_kernel<2>,
-                       dim3(kLo16 / 256, (unsigned)((walks + per_wg - 1) / per_wg)), dim3(256), 0, s, st.d_planes,
-                       st.d_gofs, st.d_off, (int)rb, (int)re, buf);
+  for (int r = 0; rc == SCT_OK && r < repeats; ++r) launch_seed16(st, buf, (int)rb, (int)re, s);
   SCT_HIP(hipEventRecord(e[1], s));
   for (int r = 0; rc == SCT_OK && r < repeats; ++r)
     hipLaunchKernelGGL(tile16_kernel, dim3((unsigned)std::max(1, std::min(st.grid * st.tile_wgs, ns))), dim3(256), 0,

@@ -753,6 +753,23 @@ def test_allpairs_spectral_column_width_edges(m):
     assert hist.astype(np.int64).tolist() == O.c_hist16(codes)[0][:17].tolist()
 
 
+@pytest.mark.parametrize("case", ["m127", "m97", "m65", "ragged"])
+def test_allpairs_spectral_seed_group_counts(case):
+    """The int8 seed's step-major walk against the C oracle for every group count: a column
+    of 127 codes (a fourth group from L2), 97 (the first fourth group), 65 (three groups in
+    registers) beside columns of one or two groups, and slice ranges that cut walks."""
+    m = {"m127": 127, "m97": 97, "m65": 65, "ragged": 40}[case]
+    rng = np.random.default_rng(m)
+    hi = np.unique(rng.integers(0, 1 << 18, 4 * m).astype(np.uint64))[:m]
+    col = (hi << np.uint64(14)) | np.uint64(0x2345)
+    rest = synthetic.whitelist_codes(7000, 16, seed=m)
+    rest = rest[(rest & np.uint64(0x3FFF)) != np.uint64(0x2345)]
+    codes = np.concatenate([col, rest])
+    ranges = [(0, 1 << 18)] if case != "ragged" else [(0, 1001), (1001, 70001), (70001, 1 << 18)]
+    hist = _spectral_hist(codes, ranges)
+    assert hist.astype(np.int64).tolist() == O.c_hist16(codes)[0][:17].tolist()
+
+
 def _dense_columns(splits, n_rand, seed):
     """n_rand random 16-bp codes plus, per entry of `splits`, one 14-bit column holding
     sum(split) codes (> 127: int16 seeds on 14-bit columns) spread over its four 16-bit
