@@ -34,7 +34,7 @@ constexpr int kHiBits = kSpaceBits - kLoBits;  // 18 bit planes
 constexpr int kWalk = 64;                 // slices per wave in the seed's Gray walk
 constexpr int kWalkBits = 6;
 constexpr int kRegGroups = 2;             // seed: 32-code groups whose planes stay in registers
-constexpr int kSeedWalks = 16;            // seed: walks per workgroup (8: +5 %, 32: +5 % per launch)
+constexpr int kSeedWalks = 16;            // seed: walks per workgroup (4-32 within noise, round 3)
 constexpr int kMaxOrder = 1 << 16;        // largest slice range with a digit-weight order table
 
 // Bit planes of a 32-code group: planes + g * kPlaneWords holds its 18 planes (plane k bit j =

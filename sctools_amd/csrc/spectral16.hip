@@ -210,7 +210,7 @@ __device__ __forceinline__ void walk_sm16(const uint32_t (*pr)[kHi16], int zblk,
   }
 }
 
-constexpr int RG = 3;
+constexpr int kRegGroups16 = 3;           // groups whose planes stay in registers
 __global__ __launch_bounds__(256) void seed16_sm_kernel(const uint32_t* __restrict__ planes,
                                                         const uint32_t* __restrict__ gofs,
                                                         const uint32_t* __restrict__ off, int z0, int z1,
@@ -225,9 +225,9 @@ __global__ __launch_bounds__(256) void seed16_sm_kernel(const uint32_t* __restri
   int wng = ng;
 #pragma unroll
   for (int s = 32; s; s >>= 1) wng = max(wng, __shfl_xor(wng, s));
-  uint32_t pr[RG][kHi16];
+  uint32_t pr[kRegGroups16][kHi16];
 #pragma unroll
-  for (int g = 0; g < RG; ++g)
+  for (int g = 0; g < kRegGroups16; ++g)
     if (g < ng) {
       load_planes16(planes, (int64_t)g0 + g, pr[g]);
     } else {
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void seed16_sm_kernel(const uint32_t* __restri
     if (wng <= 1) walk_sm16<1>(pr, zblk, st8, tid);
     else if (wng == 2) walk_sm16<2>(pr, zblk, st8, tid);
     else walk_sm16<3>(pr, zblk, st8, tid);
-    for (int g = RG; g < wng; ++g) {  // the groups past the register-resident ones, from L2
+    for (int g = kRegGroups16; g < wng; ++g) {  // the groups past the register-resident ones, from L2
       uint32_t p[kHi16];
       if (g < ng) {
         load_planes16(planes, (int64_t)g0 + g, p);
