@@ -531,6 +531,77 @@ def path_config5_encode(dev, reps, copy_gbs):
                                 "bytes counted by torch; one flag per N read"}}
 
 
+def _guarded(fn, *a):
+    """A side path that fails reports its error in the line instead of ending the bench."""
+    try:
+        return fn(*a)
+    except Exception as ex:  # noqa: BLE001 -- reported, never hidden
+        return {"error": "%s: %s" % (type(ex).__name__, ex)}
+
+
+def path_fastq(dev, reps, copy_gbs):
+    """SURVEY §8(f) rank 3, the FASTQ feed: a device-resident synthetic R1 FASTQ of 20M 69-byte
+    records (12-char name, 26-bp read, '+', 26 qualities), indexed (lines -> records, the '@'
+    name check, fastq.py:31-38, 143-150), CB 0:16 and UMI 16:24 sequence and quality slices
+    (TenXV2, fastq.py:188-200, platform.py:36-38) and the CBs TwoBit-encoded with GC."""
+    import torch
+    from oracle import oracle as O
+    from sctools_amd import _lib
+    n_rec = 20_000_000
+    g = torch.Generator(device=dev).manual_seed(6)
+    acgt = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    rec = torch.empty((n_rec, 69), dtype=torch.uint8, device=dev)
+    rec[:, 0] = ord("@")
+    rec[:, 1:12] = ord("r")
+    rec[:, 12] = 10
+    rec[:, 13:39] = acgt[torch.randint(0, 4, (n_rec, 26), device=dev, generator=g)]
+    rec[:, 39] = 10
+    rec[:, 40] = ord("+")
+    rec[:, 41] = 10
+    rec[:, 42:68] = ord("F")
+    rec[:, 68] = 10
+    buf = rec.reshape(-1)
+    nbytes = buf.numel()
+    seqs = torch.empty(n_rec * 24, dtype=torch.uint8, device=dev)  # span-major: CB rows, UMI rows
+    quals = torch.empty_like(seqs)
+    cb = seqs[:n_rec * 16].view(n_rec, 16)
+    umi = seqs[n_rec * 16:].view(n_rec, 8)
+    codes = torch.empty(n_rec, dtype=torch.int64, device=dev)
+    gc = torch.empty(n_rec, dtype=torch.uint8, device=dev)
+    flags = torch.empty(n_rec, dtype=torch.uint8, device=dev)
+    lib = _lib.lib()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    box = {}
+
+    def run():
+        ix = _lib.FastqIndex(buf.data_ptr(), nbytes, [nbytes], False, stream)
+        ix.extract_spans(buf.data_ptr(), [(0, 16), (16, 24)], seqs.data_ptr(), quals.data_ptr(), stream=stream)
+        _lib.check(lib.sct_encode(2, _lib._vp(cb.data_ptr()), n_rec, 16, 16, _lib._vp(codes.data_ptr()),
+                                  _lib._vp(gc.data_ptr()), _lib._vp(flags.data_ptr()), _lib._vp(stream)))
+        box["n"] = ix.nrecords
+        ix.close()
+    ms = _events_ms(run, reps, dev)
+    i = torch.randint(0, n_rec, (256,), device=dev, generator=g)
+    ok = box["n"] == n_rec and torch.equal(cb[i], rec[i, 13:29]) and torch.equal(umi[i], rec[i, 29:37]) \
+        and torch.equal(quals[:n_rec * 16].view(n_rec, 16)[i], rec[i, 42:58])
+    host = cb[i].cpu().numpy()
+    ok = ok and [O.two_bit_encode(bytes(r)) for r in host] == [int(x) for x in codes[i].cpu().numpy().view(np.uint64)]
+    algo = nbytes + n_rec * (16 + 8) * 2 + n_rec * (8 + 1 + 1)  # FASTQ once + slices + codes / GC / flags
+    gbs = algo / (ms * 1e-3) / 1e9
+    del rec, buf, seqs, quals, codes, gc, flags
+    torch.cuda.empty_cache()
+    return {"workload": "SURVEY 8(f) rank 3: %d-record synthetic R1 FASTQ (%d bytes, device-resident): index, "
+                        "CB/UMI sequence + quality slices, CB TwoBit encode + GC" % (n_rec, nbytes),
+            "value": n_rec / (ms * 1e-3), "unit": "records/s", "ms": ms, "reps": reps,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
+                         "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs,
+                         "algo_bytes_per_record": algo / n_rec, "kernel": "count_kernel + extract2_kernel",
+                         "note": "algorithmic bytes: the FASTQ once + the slices + codes; the index reads the "
+                                 "buffer a second time and syncs once for its record count (DESIGN.md §3.6)"},
+            "check": {"sampled": ok, "sample": "256 random records: CB / UMI / CB-quality slices equal the "
+                                               "record bytes, CB codes vs oracle.two_bit_encode"}}
+
+
 # ------------------------------------------------------------------ ranks
 def run_stub(args, rank, world):
     """Launcher check without a GPU: the ranks form a gloo group and all-reduce stub counts
@@ -680,7 +751,8 @@ def run_rank(args, rank, world, local):
             # configs 4 and 5 (BASELINE.json), each timed on its own after the headline
             out["paths"] = {"config4_nearest": path_config4(dev, args.path_steps, copy_gbs, threads),
                             "config5_allpairs": path_config5_allpairs(dev, max(2, args.path_steps), copy_gbs),
-                            "config5_encode": path_config5_encode(dev, max(2, args.path_steps // 2), copy_gbs)}
+                            "config5_encode": path_config5_encode(dev, max(2, args.path_steps // 2), copy_gbs),
+                            "fastq_ingest": _guarded(path_fastq, dev, max(2, args.path_steps), copy_gbs)}
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(codes, hist, args.cpu_seconds)
     if rank == 0:
