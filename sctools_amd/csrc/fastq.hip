@@ -246,14 +246,13 @@ __device__ __forceinline__ Line scan_line(const uint8_t* __restrict__ buf, int64
 //     end: the next line starts at the end and the line has no '\n'; bit 14 = "\r\n");
 //  2. the line after terminator t (global number g+1) belongs to record (g+1)/4: a name
 //     line (0) must start with '@' (fastq.py:35-36); for a sequence (1) or quality (3)
-//     line, one item per (line, span) finds the line's end at the tile's next terminator
+//     line, one item per line finds the line's end at the tile's next terminator
 //     (for the tile's last line: the next tile's first, or a short scan) and copies its
 //     slice (rows inside the tile from the tile's LDS copy).
 // Record 0's name line starts at byte 0, checked by thread 0 of tile 0.
 constexpr int MAX_SPANS = 8;
 struct Spans {
   int n, max_end, width;  // width = sum of the spans' widths
-  uint32_t inv_n;         // ceil(2^32 / n) for n >= 2: q / n = umulhi(q, inv_n) for q < 2^29
   int start[MAX_SPANS], end[MAX_SPANS];
   int64_t prefix[MAX_SPANS];  // sum of the widths of the spans before k
 };
@@ -263,10 +262,12 @@ constexpr int MAX_TERM = TILE + 16;  // terminators a tile can hold (+ virtual f
 // The extraction (round 2: fewer LDS bytes and one barrier fewer per tile than the first
 // version, which kept 32-bit terminators and an action array): terminators as
 // 16-bit tile offsets (bit 13 = virtual file end, bit 14 = "\r\n"; 8 KB), no action array --
-// a copy item (action a, span k) finds its line from the terminators around it (the line
-// after the tile's (te0 + 2a)-th terminator; te0 = 1 when the tile's first terminator number
-// is odd) -- so the name checks and the copies run in one phase after the terminators are
-// written.  13 KB of LDS: 7 resident workgroups per CU (4 for the first version).
+// a copy item (line a) finds its line from the terminators around it (the line after the
+// tile's (te0 + 2a)-th terminator; te0 = 1 when the tile's first terminator number is odd) and
+// copies every span of it in turn -- so the name checks and the copies run in one phase after
+// the terminators are written.  13 KB of LDS: 7 resident workgroups per CU (4 for the first
+// version).  Round 3: one item per line instead of per (line, span), so a line's end is found
+// once for all its spans: 20M records 1.33-1.35 -> 1.16-1.21 ms.
 constexpr uint16_t T16_OFF = 0x3FFF, T16_VIRT = 1u << 14, T16_CRLF = 1u << 15;
 static_assert(TILE + 16 <= T16_OFF, "16-bit terminator offsets");
 
@@ -338,11 +339,11 @@ __global__ __launch_bounds__(WG) void extract2_kernel(const uint8_t* __restrict_
       const uint8_t ch = o < TILE ? tile8[o] : buf[t0 + o];
       if (ch != '@') atomicMin(first_bad, (unsigned long long)((g0 + t + 1) >> 2));
     }
-    // sequence / quality lines: after even terminators; one item per (line, span)
+    // sequence / quality lines: after even terminators; one item per line, its spans in turn
+    // (the line's end is found once for all of them)
     const int te0 = (int)(g0 & 1);
     const int nact = tmax > te0 ? (tmax - te0 + 1) / 2 : 0;
-    for (int q = threadIdx.x; q < nact * sp.n; q += WG) {
-      const int a = sp.n == 1 ? q : (int)__umulhi((uint32_t)q, sp.inv_n), k = q - a * sp.n;  // q / n, q % n
+    for (int a = threadIdx.x; a < nact; a += WG) {
       const int t = te0 + 2 * a;
       const int64_t line = g0 + t + 1, rec = line >> 2;
       const bool is_seq = (line & 3) == 1;
@@ -380,49 +381,51 @@ __global__ __launch_bounds__(WG) void extract2_kernel(const uint8_t* __restrict_
       int32_t* len = is_seq ? seq_len : qual_len;
       uint8_t* out = is_seq ? seq_out : qual_out;
       const int64_t clen = cend - start, llen = clen + nl;
-      const int64_t sa = sp.start[k] < llen ? sp.start[k] : llen, sb = sp.end[k] < llen ? sp.end[k] : llen;
-      if (len) len[k * nrec + rec] = (int32_t)(sb - sa);
-      if (!out) continue;
-      const int w = sp.end[k] - sp.start[k];
-      uint8_t* o = out + sp.prefix[k] * nrec + rec * w;
-      const uint8_t* src = buf + t0 + start;
-      // fast path: a whole-width slice inside the line's content, a row of whole dwords:
-      // aligned dword loads + byte-align funnel shifts, dword stores
-      const int64_t s0 = t0 + start + sa;
-      const int64_t base = s0 & ~3LL;
-      const int nd = w / 4;
-      if (sb - sa == w && sb <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
-          ((uintptr_t)o & 3) == 0) {
-        // rows inside the tile read its LDS copy; the rest (lines running past it) read L2
-        const uint32_t* d = base + 4 * (nd + 1) <= t0 + TILE ? tile32 + ((base - t0) >> 2)
-                                                             : reinterpret_cast<const uint32_t*>(buf + base);
-        const uint32_t sh = (uint32_t)(s0 & 3);
-        uint32_t* od = reinterpret_cast<uint32_t*>(o);
-        if (nd == 4 && ((uintptr_t)o & 15) == 0) {
-          const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3], x4 = d[4];
-          *reinterpret_cast<uint4*>(o) =
-              make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                         __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+      for (int k = 0; k < sp.n; ++k) {
+        const int64_t sa = sp.start[k] < llen ? sp.start[k] : llen, sb = sp.end[k] < llen ? sp.end[k] : llen;
+        if (len) len[k * nrec + rec] = (int32_t)(sb - sa);
+        if (!out) continue;
+        const int w = sp.end[k] - sp.start[k];
+        uint8_t* o = out + sp.prefix[k] * nrec + rec * w;
+        const uint8_t* src = buf + t0 + start;
+        // fast path: a whole-width slice inside the line's content, a row of whole dwords:
+        // aligned dword loads + byte-align funnel shifts, dword stores
+        const int64_t s0 = t0 + start + sa;
+        const int64_t base = s0 & ~3LL;
+        const int nd = w / 4;
+        if (sb - sa == w && sb <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
+            ((uintptr_t)o & 3) == 0) {
+          // rows inside the tile read its LDS copy; the rest (lines running past it) read L2
+          const uint32_t* d = base + 4 * (nd + 1) <= t0 + TILE ? tile32 + ((base - t0) >> 2)
+                                                               : reinterpret_cast<const uint32_t*>(buf + base);
+          const uint32_t sh = (uint32_t)(s0 & 3);
+          uint32_t* od = reinterpret_cast<uint32_t*>(o);
+          if (nd == 4 && ((uintptr_t)o & 15) == 0) {
+            const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3], x4 = d[4];
+            *reinterpret_cast<uint4*>(o) =
+                make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                           __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+            continue;
+          }
+          if (nd == 2 && ((uintptr_t)o & 7) == 0) {
+            const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
+            *reinterpret_cast<uint2*>(o) =
+                make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
+            continue;
+          }
+          uint32_t lo = d[0];
+          for (int q2 = 0; q2 < nd; ++q2) {
+            const uint32_t hi = d[q2 + 1];
+            od[q2] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            lo = hi;
+          }
           continue;
         }
-        if (nd == 2 && ((uintptr_t)o & 7) == 0) {
-          const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
-          *reinterpret_cast<uint2*>(o) =
-              make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
-          continue;
-        }
-        uint32_t lo = d[0];
-        for (int q2 = 0; q2 < nd; ++q2) {
-          const uint32_t hi = d[q2 + 1];
-          od[q2] = __builtin_amdgcn_alignbyte(hi, lo, sh);
-          lo = hi;
-        }
-        continue;
-      }
 #pragma unroll 8
-      for (int j = 0; j < w; ++j) {
-        const int64_t i = sa + j;
-        o[j] = i < sb ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
+        for (int j = 0; j < w; ++j) {
+          const int64_t i = sa + j;
+          o[j] = i < sb ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
+        }
       }
     }
     g0_cur = g0_nxt;
@@ -629,7 +632,6 @@ extern "C" int sct_fastq_extract_spans(sct_fastq_index* ix, const uint8_t* d_buf
     pre += sp.end[k] - sp.start[k];
   }
   sp.width = (int)pre;
-  sp.inv_n = nspans >= 2 ? (uint32_t)((0xFFFFFFFFull + nspans) / nspans) : 0u;
   hipStream_t s = sct::as_stream(stream);
   SCT_HIP(hipMemsetAsync(ix->d_bad, 0xFF, 8, s));
   if (ix->nbytes > 0) {
