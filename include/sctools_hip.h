@@ -42,7 +42,7 @@ int sct_set_device(int device);        /* select the device for later calls (hip
  * small problems and benchmarks can sweep.  Process-global; the library reads no environment
  * variable.  value < 0 restores the default.  Read when a plan is created (scalar: per call). */
 #define SCT_TUNE_SPECTRAL_CHUNK 1       /* slices per seed/tile pass (default 65536) */
-#define SCT_TUNE_SPECTRAL_MIN_N 2       /* AUTO takes SPECTRAL from this many 16-base codes (500000) */
+#define SCT_TUNE_SPECTRAL_MIN_N 2       /* AUTO takes SPECTRAL from this many 16-base codes (325000) */
 #define SCT_TUNE_ALLPAIRS_GRAB 3        /* pair kernel: work items per queue pull */
 #define SCT_TUNE_ALLPAIRS_FLUSH_ITEMS 4 /* pair kernel: flush lane counters every k items */
 #define SCT_TUNE_ALLPAIRS_GRID 5        /* pair kernel: persistent grid size */
@@ -194,7 +194,7 @@ int sct_scalar_server_status(int64_t* launches, int* running);
  */
 typedef struct sct_allpairs_plan sct_allpairs_plan;
 
-#define SCT_ALLPAIRS_AUTO (-1)    /* 16 bases: SPECTRAL from 500K codes, else MOMENTS; else SUBSETS */
+#define SCT_ALLPAIRS_AUTO (-1)    /* 16 bases: SPECTRAL from 325K codes, else MOMENTS; else SUBSETS */
 #define SCT_ALLPAIRS_SUBSETS 0
 #define SCT_ALLPAIRS_MOMENTS 1
 #define SCT_ALLPAIRS_SPECTRAL 2

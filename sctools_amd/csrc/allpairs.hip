@@ -709,7 +709,7 @@ bool mom_supported(int npp, int64_t n) { return npp * 2 == sct::kMomG && n <= 10
 // SPECTRAL: the same 16-base codes; its cost does not depend on n
 bool spectral_supported(int npp, int64_t n) { return mom_supported(npp, n); }
 // smallest n for which AUTO picks SPECTRAL over MOMENTS (measured crossover)
-int64_t spectral_min_n() { return sct::tune(SCT_TUNE_SPECTRAL_MIN_N, 500000); }
+int64_t spectral_min_n() { return sct::tune(SCT_TUNE_SPECTRAL_MIN_N, 325000); }
 // what SCT_ALLPAIRS_AUTO resolves to
 int auto_scheme(int npp, int64_t n) {
   if (spectral_supported(npp, n) && n >= spectral_min_n()) return SCT_ALLPAIRS_SPECTRAL;

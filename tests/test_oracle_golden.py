@@ -228,11 +228,12 @@ def test_spectral_rejects_inconsistent_counts():
 
 
 def test_geometry_picks_spectral_for_large_whitelists():
-    """Host-only: AUTO resolves to SPECTRAL at 16 bases from 500K codes (the measured
+    """Host-only: AUTO resolves to SPECTRAL at 16 bases from 325K codes (the measured
     crossover; SCT_TUNE_SPECTRAL_MIN_N moves it): the 2^18 transform slices are the work items."""
     assert _lib.allpairs_geometry(3_700_000, 32)["items"] == 1 << 18
     assert _lib.allpairs_geometry(737_280, 32)["items"] == 1 << 18
-    assert _lib.allpairs_geometry(400_000, 32)["items"] != 1 << 18
+    assert _lib.allpairs_geometry(400_000, 32)["items"] == 1 << 18
+    assert _lib.allpairs_geometry(300_000, 32)["items"] != 1 << 18
     assert _lib.allpairs_geometry(3_700_000, 40)["items"] != 1 << 18  # 20 bases: SUBSETS
 
 
