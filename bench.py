@@ -26,8 +26,9 @@ WORLD_SIZE must equal --gpus.  Rank 0 prints one JSON line:
             in the same run; the issue-rate picture (VALU / matrix-pipe busy) from the
             committed PMC summary; the committed rocprof average beside the live one
   paths     (N = 1) config 4 (100M-query nearest whitelist), config 5's 3.7M all-pairs and
-            its 1e9-read encode + GC, each timed here with its own roofline and a sampled
-            check against the oracle (none of them is inside the headline's timed region)
+            its 1e9-read encode + GC, FASTQ CB/UMI extraction, whitelist-file ingest and
+            base_frequency, each timed here with its own roofline and a sampled check against
+            the oracle (none of them is inside the headline's timed region)
   cpu_baseline  (N = 1) the C oracle restatement (test infrastructure, never the product)
             on this host's cores, the histogram checked against the GPU's
 """
@@ -531,6 +532,75 @@ def path_config5_encode(dev, reps, copy_gbs):
                                 "bytes counted by torch; one flag per N read"}}
 
 
+def path_whitelist(dev, reps, copy_gbs):
+    """SURVEY §8(f) ranks 1 and 4 on config 5's whitelist: the 3,686,400-line 16-bp whitelist
+    file (device-resident bytes) split into `line[:-1]` records and TwoBit-encoded with GC
+    (sct_lines + sct_encode_var: Barcodes.from_whitelist, barcode.py:95-97), and
+    base_frequency over the codes (sct_base_frequency: barcode.py:48-70)."""
+    import ctypes
+
+    import torch
+    from oracle import oracle as O
+    from sctools_amd import _lib, synthetic
+    n, L, seed = synthetic.CONFIGS[5]
+    codes_h = synthetic.whitelist_codes(n, L, seed)
+    shifts = np.arange(2 * (L - 1), -1, -2, dtype=np.uint64)
+    text = np.frombuffer(b"ACTG", dtype=np.uint8)[((codes_h[:, None] >> shifts) & np.uint64(3)).astype(np.int64)]
+    text = np.concatenate([text, np.full((n, 1), 10, np.uint8)], axis=1)
+    buf = torch.from_numpy(text.reshape(-1)).to(dev)
+    nbytes = buf.numel()
+    starts = torch.empty(n, dtype=torch.int64, device=dev)
+    lens = torch.empty(n, dtype=torch.int32, device=dev)
+    codes = torch.empty(n, dtype=torch.int64, device=dev)
+    gc = torch.empty(n, dtype=torch.uint8, device=dev)
+    flags = torch.empty(n, dtype=torch.uint8, device=dev)
+    freq = torch.empty(L * 4, dtype=torch.int64, device=dev)
+    lib = _lib.lib()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    nl, mx = ctypes.c_int64(0), ctypes.c_int32(0)
+
+    def ingest():
+        _lib.check(lib.sct_lines(buf.data_ptr(), nbytes, n, starts.data_ptr(), lens.data_ptr(), ctypes.byref(nl),
+                                 ctypes.byref(mx), stream))
+        _lib.check(lib.sct_encode_var(2, buf.data_ptr(), starts.data_ptr(), lens.data_ptr(), nl.value, 1,
+                                      codes.data_ptr(), gc.data_ptr(), flags.data_ptr(), stream))
+
+    def basefreq():
+        _lib.check(lib.sct_base_frequency(codes.data_ptr(), n, L, freq.data_ptr(), stream))
+    ms_in = _events_ms(ingest, reps, dev)
+    ms_bf = _events_ms(basefreq, reps, dev)
+    torch.cuda.synchronize()
+    want = torch.from_numpy(codes_h.view(np.int64)).to(dev)
+    want_gc = torch.from_numpy(((text[:, :L] == ord("C")) | (text[:, :L] == ord("G"))).sum(1).astype(np.uint8)).to(dev)
+    ok_in = nl.value == n and mx.value == L and torch.equal(codes, want) and torch.equal(gc, want_gc) \
+        and not bool(flags.any())
+    ok_bf = np.array_equal(freq.cpu().numpy().view(np.uint64).reshape(L, 4), O.base_frequency_numpy(codes_h, L))
+    algo_in = nbytes + n * (8 + 1 + 1)
+    algo_bf = 8 * n
+    del buf, starts, lens, codes, gc, flags, freq
+    torch.cuda.empty_cache()
+
+    def roof(algo, ms, kernel, note):
+        gbs = algo / (ms * 1e-3) / 1e9
+        return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
+                "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs, "kernel": kernel,
+                "note": note}
+    return {"whitelist_ingest": {
+                "workload": "config 5's whitelist file: %d lines of 16 bases + LF (%d bytes, device-resident): "
+                            "line split (line[:-1]) + TwoBit encode + GC" % (n, nbytes),
+                "value": n / (ms_in * 1e-3), "unit": "lines/s", "ms": ms_in, "reps": reps,
+                "roofline": roof(algo_in, ms_in, "sct_lines + sct_encode_var",
+                                 "algorithmic bytes: the file once + codes / GC / flags; sct_lines returns the "
+                                 "line count to the host (one sync per call), inside the timed region"),
+                "check": {"every_line": ok_in, "sample": "all %d codes and GC counts vs the generating codes, "
+                                                         "no flags" % n}},
+            "base_frequency": {
+                "workload": "base_frequency over config 5's %d 16-bp codes (device-resident)" % n,
+                "value": n / (ms_bf * 1e-3), "unit": "codes/s", "ms": ms_bf, "reps": reps,
+                "roofline": roof(algo_bf, ms_bf, "base_frequency_kernel", "algorithmic bytes: the codes once"),
+                "check": {"vs_oracle": ok_bf, "sample": "the whole table vs oracle.base_frequency_numpy"}}}
+
+
 def _guarded(fn, *a):
     """A side path that fails reports its error in the line instead of ending the bench."""
     try:
@@ -753,6 +823,8 @@ def run_rank(args, rank, world, local):
                             "config5_allpairs": path_config5_allpairs(dev, max(2, args.path_steps), copy_gbs),
                             "config5_encode": path_config5_encode(dev, max(2, args.path_steps // 2), copy_gbs),
                             "fastq_ingest": _guarded(path_fastq, dev, max(2, args.path_steps), copy_gbs)}
+            wl = _guarded(path_whitelist, dev, max(5, args.path_steps), copy_gbs)
+            out["paths"].update(wl if "error" not in wl else {"whitelist_ingest": wl})
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(codes, hist, args.cpu_seconds)
     if rank == 0:

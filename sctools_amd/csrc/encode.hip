@@ -143,6 +143,76 @@ __global__ __launch_bounds__(WG) void encode_kernel(int kind, const uint8_t* __r
   }
 }
 
+// Variable-length records of one limb (the whitelist's lines): a workgroup's 256 records
+// usually lie in one short stretch of the buffer (consecutive lines), so it stages the
+// aligned 16-B blocks covering [min start, max end) in LDS with coalesced loads and each lane
+// packs its record from there.  Records spread wider than the stage are read from global
+// memory byte by byte (a uniform branch per workgroup).  Every staged 16-B block holds at
+// least one byte of some record, so no load leaves the pages the records lie in.
+constexpr int kVarStage = 8192;
+__global__ __launch_bounds__(WG) void encode_var_kernel(int kind, const uint8_t* __restrict__ buf, int64_t n,
+                                                        const int64_t* __restrict__ starts,
+                                                        const int32_t* __restrict__ lens,
+                                                        uint64_t* __restrict__ codes, uint8_t* __restrict__ gc,
+                                                        uint8_t* __restrict__ flags) {
+  __shared__ uint8_t lut[256];
+  __shared__ uint4 stage4[kVarStage / 16];
+  __shared__ unsigned long long lo_s, hi_s;
+  const uint8_t* stage = reinterpret_cast<const uint8_t*>(stage4);
+  fill_lut(lut, kind);
+  const int tid = threadIdx.x;
+  const uint64_t gcm = kind == 2 ? 0x5555555555555555ull : 0x9249249249249249ull;
+  for (int64_t r0 = (int64_t)blockIdx.x * WG; r0 < n; r0 += (int64_t)gridDim.x * WG) {
+    const int64_t r = r0 + tid;
+    const bool live = r < n;
+    const uintptr_t a = live ? (uintptr_t)(buf + starts[r]) : 0;
+    const int L = live ? lens[r] : 0;
+    if (tid == 0) {
+      lo_s = ~0ull;
+      hi_s = 0;
+    }
+    __syncthreads();
+    if (live && L > 0) {  // (an empty record reads nothing, wherever it starts)
+      atomicMin(&lo_s, (unsigned long long)a);
+      atomicMax(&hi_s, (unsigned long long)(a + L));
+    }
+    __syncthreads();
+    const uintptr_t a0 = (uintptr_t)lo_s & ~(uintptr_t)15, a1 = ((uintptr_t)hi_s + 15) & ~(uintptr_t)15;
+    const bool staged = hi_s > lo_s && a1 - a0 <= (uintptr_t)kVarStage;  // workgroup-uniform
+    if (staged) {
+      const int nblk = (int)((a1 - a0) >> 4);
+      for (int k = tid; k < nblk; k += WG) stage4[k] = reinterpret_cast<const uint4*>(a0)[k];
+      __syncthreads();
+    }
+    if (live) {
+      uint64_t code = 0;
+      uint32_t fl = 0;
+      if (staged) {
+        const uint8_t* rec = stage + (a - a0);
+        for (int p = 0; p < L; ++p) {
+          const uint32_t e = lut[rec[p]];
+          code = (code << kind) | (e & 7u);
+          fl |= e;
+        }
+      } else {
+        const uint8_t* rec = reinterpret_cast<const uint8_t*>(a);
+        for (int p = 0; p < L; ++p) {
+          const uint32_t e = lut[rec[p]];
+          code = (code << kind) | (e & 7u);
+          fl |= e;
+        }
+      }
+      codes[r] = code;
+      if (gc) {
+        const uint32_t g = (uint32_t)__popcll(code & gcm);
+        gc[r] = (uint8_t)(g > 255 ? 255 : g);
+      }
+      if (flags) flags[r] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
+    }
+    __syncthreads();  // stage and lo_s / hi_s are rewritten by the next round
+  }
+}
+
 // Contiguous records (stride == L, one limb): a workgroup stages 256 records with
 // coalesced 16-byte loads into LDS, then each lane packs its record from LDS (dword reads
 // when L % 4 == 0, conflict-free for odd L/4) through the LDS byte LUT.  The staging
@@ -378,24 +448,68 @@ __global__ __launch_bounds__(WG) void hamming_kernel(int kind, const uint64_t* _
     out[r] = hamming_record(kind, a + r * words, b + r * words, words);
 }
 
-// per-position base counts: LDS u32 tallies per workgroup, one u64 atomic per bin
+// Per-position base counts.  Base p of a code is bits 2j, 2j + 1 with j = L - 1 - p, and only
+// j < 32 can be non-zero, so the work is the 2-bit fields j of the codes: per 64 codes (one
+// per lane) and field j, the wave's ballots of the field's two bits land in lane j, which
+// counts the three non-zero values by popcount (value 0 = codes seen - the rest).  A wave
+// takes 4 x 64 codes per round (four loads in flight); wave tallies go to LDS, one u64 atomic
+// per (field, value) per workgroup; bases p < L - 32 are all 0 (n of them, added once by
+// workgroup 0).  JT = the field count when known at compile time (16-bp barcodes), else 0.
+template <int JT>
 __global__ __launch_bounds__(WG) void base_frequency_kernel(const uint64_t* __restrict__ codes,
                                                             int64_t n, int L,
                                                             unsigned long long* __restrict__ out) {
-  extern __shared__ uint32_t tally[];  // [L][4]
-  for (int k = threadIdx.x; k < 4 * L; k += WG) tally[k] = 0u;
+  constexpr int U = 4;
+  __shared__ unsigned long long tally[32][4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int J = JT ? JT : (L < 32 ? L : 32);  // fields with data
+  if (tid < 128) tally[tid >> 2][tid & 3] = 0;
   __syncthreads();
-  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
-    const uint64_t code = codes[r];
-    for (int p = 0; p < L; ++p) {
-      const int sh = 2 * (L - 1 - p);
-      const uint32_t v = sh < 64 ? (uint32_t)((code >> sh) & 3u) : 0u;
-      atomicAdd(&tally[4 * p + v], 1u);
+  unsigned long long c[4] = {0, 0, 0, 0};  // lane j: [codes seen, value 1, 2, 3] of field j
+  const int64_t step = (int64_t)gridDim.x * WG * U;
+  for (int64_t r0 = ((int64_t)blockIdx.x * WG + (tid & ~63)) * U; r0 < n; r0 += step) {
+    uint64_t code[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = r0 + 64 * u + lane;
+      code[u] = r < n ? codes[r] : 0ull;
+    }
+    c[0] += (unsigned long long)(n - r0 < 64 * U ? n - r0 : 64 * U);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint64_t mh = 0, ml = 0;
+      auto field = [&](int j) {
+        const uint32_t f = (uint32_t)(code[u] >> (2 * j)) & 3u;
+        const uint64_t bl = __ballot(f & 1u), bh = __ballot(f >> 1);
+        if (lane == j) {
+          ml = bl;
+          mh = bh;
+        }
+      };
+      if constexpr (JT > 0) {
+#pragma unroll
+        for (int j = 0; j < JT; ++j) field(j);
+      } else {
+        for (int j = 0; j < J; ++j) field(j);
+      }
+      c[1] += __popcll(ml & ~mh);
+      c[2] += __popcll(mh & ~ml);
+      c[3] += __popcll(mh & ml);
     }
   }
+  if (lane < J) {
+    atomicAdd(&tally[lane][0], c[0] - c[1] - c[2] - c[3]);
+    atomicAdd(&tally[lane][1], c[1]);
+    atomicAdd(&tally[lane][2], c[2]);
+    atomicAdd(&tally[lane][3], c[3]);
+  }
   __syncthreads();
-  for (int k = threadIdx.x; k < 4 * L; k += WG)
-    if (tally[k]) atomicAdd(out + k, (unsigned long long)tally[k]);
+  if (tid < 4 * J) {
+    const int j = tid >> 2, v = tid & 3;
+    if (tally[j][v]) atomicAdd(out + 4 * (L - 1 - j) + v, tally[j][v]);
+  }
+  if (blockIdx.x == 0)
+    for (int p = tid; p < L - 32; p += WG) out[4 * p] = (unsigned long long)n;
 }
 
 unsigned grid_for(int64_t n) {
@@ -457,6 +571,12 @@ extern "C" int sct_encode_var(int kind, const uint8_t* buf, const int64_t* start
   SCT_CHECK(n >= 0 && words >= 1, "bad n/words");
   if (n == 0) return SCT_OK;
   SCT_CHECK(buf && starts && lens && codes, "NULL pointer");
+  if (words == 1) {
+    hipLaunchKernelGGL(encode_var_kernel, dim3(grid_for(n)), dim3(WG), 0, sct::as_stream(stream), kind, buf, n,
+                       starts, lens, codes, gc, flags);
+    SCT_LAUNCH_CHECK();
+    return SCT_OK;
+  }
   hipLaunchKernelGGL(encode_kernel, dim3(grid_for(n)), dim3(WG), 0, sct::as_stream(stream), kind, buf, n,
                      (int64_t)0, 0, words, false, codes, gc, flags, starts, lens);
   SCT_LAUNCH_CHECK();
@@ -517,9 +637,13 @@ extern "C" int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint6
   if (L == 0) return SCT_OK;
   SCT_HIP(hipMemsetAsync(out, 0, (size_t)L * 4 * 8, sct::as_stream(stream)));
   if (n == 0) return SCT_OK;
-  const unsigned blocks = std::min<unsigned>(grid_for(n), 1024u);
-  hipLaunchKernelGGL(base_frequency_kernel, dim3(blocks), dim3(WG), (size_t)L * 16,
-                     sct::as_stream(stream), codes, n, L, reinterpret_cast<unsigned long long*>(out));
+  const unsigned blocks = (unsigned)std::min<int64_t>(sct::ceil_div(n, 4 * WG), 2048);
+  if (L == 16)
+    hipLaunchKernelGGL(base_frequency_kernel<16>, dim3(blocks), dim3(WG), 0, sct::as_stream(stream), codes, n, L,
+                       reinterpret_cast<unsigned long long*>(out));
+  else
+    hipLaunchKernelGGL(base_frequency_kernel<0>, dim3(blocks), dim3(WG), 0, sct::as_stream(stream), codes, n, L,
+                       reinterpret_cast<unsigned long long*>(out));
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }

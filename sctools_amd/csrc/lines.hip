@@ -9,12 +9,15 @@
 // [P_{g-1} + 1, P_g): start = P_{g-1} + 1 (0 for g = 0), length = P_g - start.
 //
 // Two passes over 4 KiB tiles (16 bytes per thread, SWAR '\n' compares): count each tile's
-// line ends, exclusive-scan them into every tile's first line number, then write each
-// line's (start, length); the variable-length TwoBit/ThreeBit encoder (sct_encode_var)
-// packs the lines straight from the file bytes.
+// line ends, exclusive-scan them into every tile's first line number, then store every end
+// as the next line's start; the lengths follow from consecutive starts.  The
+// variable-length TwoBit/ThreeBit encoder (sct_encode_var) packs the lines straight from
+// the file bytes.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 #include "sct_common.h"
 
@@ -52,11 +55,11 @@ __global__ __launch_bounds__(WG) void line_count_kernel(const uint8_t* __restric
   if (threadIdx.x == 0) counts[blockIdx.x] = tot;
 }
 
-// line g ends at byte P_g: starts[g + 1] = P_g + 1, lens[g] = P_g - starts[g]; the second
-// write needs starts[g], so every end is stored first (ends[g] = P_g), then lengths
-__global__ __launch_bounds__(WG) void line_ends_kernel(const uint8_t* __restrict__ buf, int64_t n,
-                                                       const unsigned long long* __restrict__ offsets,
-                                                       int64_t* __restrict__ ends) {
+// line g ends at byte P_g, so line g + 1 starts at P_g + 1: every end found is stored as the
+// next line's start (starts[0] = 0); the last line ends at the file's last byte
+__global__ __launch_bounds__(WG) void line_starts_kernel(const uint8_t* __restrict__ buf, int64_t n,
+                                                         const unsigned long long* __restrict__ offsets,
+                                                         int64_t nlines, int64_t* __restrict__ starts) {
   const int64_t p0 = (int64_t)blockIdx.x * TILE + threadIdx.x * 16;
   uint32_t m = p0 < n ? lf_mask(buf, n, p0) : 0u;
   using BS = hipcub::BlockScan<uint32_t, WG>;
@@ -64,21 +67,58 @@ __global__ __launch_bounds__(WG) void line_ends_kernel(const uint8_t* __restrict
   uint32_t pre;
   BS(tmp).ExclusiveSum(__popc(m), pre);
   int64_t g = (int64_t)offsets[blockIdx.x] + pre;
+  if (blockIdx.x == 0 && threadIdx.x == 0) starts[0] = 0;
   while (m) {
     const int j = __ffs(m) - 1;
     m &= m - 1;
-    ends[g++] = p0 + j;
+    if (++g < nlines) starts[g] = p0 + j + 1;
   }
 }
 
-__global__ void line_spans_kernel(const int64_t* __restrict__ ends, int64_t nlines, int64_t* __restrict__ starts,
-                                  int32_t* __restrict__ lens, int32_t* __restrict__ maxlen) {
+// chopped lengths: line g is [starts[g], P_g) with P_g = starts[g + 1] - 1 (the file's last
+// byte for the last line); the longest by a wave maximum, one atomic per wave
+__global__ __launch_bounds__(WG) void line_lens_kernel(const int64_t* __restrict__ starts, int64_t nlines,
+                                                       int64_t nbytes, int32_t* __restrict__ lens,
+                                                       int32_t* __restrict__ maxlen) {
+  int32_t mx = 0;
   for (int64_t g = (int64_t)blockIdx.x * WG + threadIdx.x; g < nlines; g += (int64_t)gridDim.x * WG) {
-    const int64_t s = g ? ends[g - 1] + 1 : 0;
-    const int64_t len = ends[g] - s;
-    starts[g] = s;
-    lens[g] = (int32_t)len;
-    atomicMax(maxlen, (int32_t)len);
+    const int64_t end = g + 1 < nlines ? starts[g + 1] - 1 : nbytes - 1;
+    const int32_t len = (int32_t)(end - starts[g]);
+    lens[g] = len;
+    mx = max(mx, len);
+  }
+#pragma unroll
+  for (int s = 32; s; s >>= 1) mx = max(mx, __shfl_xor(mx, s));
+  if ((threadIdx.x & 63) == 0 && mx > 0) atomicMax(maxlen, mx);
+}
+
+// Scratch of one call, allocated and freed in stream order (the device's default memory
+// pool, kept warm: its release threshold is raised once per device, so repeated calls reuse
+// the pool instead of mapping memory each time).
+struct StreamBuf {
+  void* p = nullptr;
+  hipStream_t s = nullptr;
+  ~StreamBuf() {
+    if (p) (void)hipFreeAsync(p, s);
+  }
+  hipError_t alloc(size_t bytes, hipStream_t st) {
+    s = st;
+    return hipMallocAsync(&p, bytes ? bytes : 1, st);
+  }
+};
+
+void keep_pool_warm() {
+  static std::mutex mu;
+  static std::vector<int> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> lk(mu);
+  if (std::find(done.begin(), done.end(), dev) != done.end()) return;
+  done.push_back(dev);
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
   }
 }
 
@@ -97,35 +137,36 @@ extern "C" int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines
   hipStream_t s = sct::as_stream(stream);
   const int64_t ntiles = sct::ceil_div(nbytes, TILE);
   SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
+  keep_pool_warm();
   size_t tb = 0;
   SCT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                            (int)(ntiles + 1), s));
-  sct::DevBuf cnt, off, tmp, mx;
-  SCT_HIP(cnt.alloc((size_t)(ntiles + 1) * 8));
-  SCT_HIP(off.alloc((size_t)(ntiles + 1) * 8));
-  SCT_HIP(tmp.alloc(tb));
-  SCT_HIP(mx.alloc(4));
-  SCT_HIP(hipMemsetAsync(cnt.p, 0, (size_t)(ntiles + 1) * 8, s));
-  hipLaunchKernelGGL(line_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes,
-                     (unsigned long long*)cnt.p);
+  // one scratch block: tile counts, their offsets, the scan's temporary storage, the maximum
+  const size_t cb = (size_t)(ntiles + 1) * 8, tb_al = (tb + 255) & ~(size_t)255;
+  StreamBuf scratch;
+  SCT_HIP(scratch.alloc(2 * cb + tb_al + 8, s));
+  unsigned long long* cnt = (unsigned long long*)scratch.p;
+  unsigned long long* off = cnt + (ntiles + 1);
+  void* tmp = (uint8_t*)scratch.p + 2 * cb;
+  int32_t* mx = (int32_t*)((uint8_t*)tmp + tb_al);
+  SCT_HIP(hipMemsetAsync(cnt, 0, cb, s));
+  hipLaunchKernelGGL(line_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, cnt);
   SCT_LAUNCH_CHECK();
-  SCT_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, (unsigned long long*)cnt.p, (unsigned long long*)off.p,
-                                           (int)(ntiles + 1), s));
+  SCT_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, off, (int)(ntiles + 1), s));
   unsigned long long total = 0;
-  SCT_HIP(hipMemcpyAsync(&total, (unsigned long long*)off.p + ntiles, 8, hipMemcpyDeviceToHost, s));
+  SCT_HIP(hipMemcpyAsync(&total, off + ntiles, 8, hipMemcpyDeviceToHost, s));
   SCT_HIP(hipStreamSynchronize(s));
   *nlines = (int64_t)total;
   if (max_lines < (int64_t)total || total == 0) return SCT_OK;
   SCT_CHECK(d_starts && d_lens, "NULL output");
-  sct::DevBuf ends;
-  SCT_HIP(ends.alloc((size_t)total * 8));
-  hipLaunchKernelGGL(line_ends_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes,
-                     (const unsigned long long*)off.p, (int64_t*)ends.p);
-  SCT_HIP(hipMemsetAsync(mx.p, 0, 4, s));
-  hipLaunchKernelGGL(line_spans_kernel, dim3((unsigned)std::min<int64_t>(sct::ceil_div((int64_t)total, WG), 8192)),
-                     dim3(WG), 0, s, (const int64_t*)ends.p, (int64_t)total, d_starts, d_lens, (int32_t*)mx.p);
+  hipLaunchKernelGGL(line_starts_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes,
+                     (const unsigned long long*)off, (int64_t)total, d_starts);
   SCT_LAUNCH_CHECK();
-  SCT_HIP(hipMemcpyAsync(max_len, mx.p, 4, hipMemcpyDeviceToHost, s));
+  SCT_HIP(hipMemsetAsync(mx, 0, 4, s));
+  hipLaunchKernelGGL(line_lens_kernel, dim3((unsigned)std::min<int64_t>(sct::ceil_div((int64_t)total, WG), 2048)),
+                     dim3(WG), 0, s, (const int64_t*)d_starts, (int64_t)total, nbytes, d_lens, mx);
+  SCT_LAUNCH_CHECK();
+  SCT_HIP(hipMemcpyAsync(max_len, mx, 4, hipMemcpyDeviceToHost, s));
   SCT_HIP(hipStreamSynchronize(s));
   return SCT_OK;
 }

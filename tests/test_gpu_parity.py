@@ -1047,3 +1047,74 @@ def test_all_negative_keys_summary():
     d = [O.two_bit_hamming(a, b) for a, b in itertools.combinations(keys, 2)]
     s = barcode.Barcodes.from_iterable_encoded(keys, 16)
     assert s.summarize_hamming_distances() == O.summary_numpy(d)
+
+
+# ---------------------------------------------------------------- one-limb variable-length encode, base_frequency
+@pytest.mark.parametrize("kind", [2, 3])
+@pytest.mark.parametrize("layout", ["lines", "scattered"])
+def test_encode_var_one_limb(kind, layout):
+    """sct_encode_var with one limb (encode_var_kernel): consecutive lines (staged through
+    LDS) and records scattered over a 4 MB buffer (the global-memory branch), with empty,
+    ambiguous and invalid records, vs oracle.two_bit_encode / three_bit_encode and the GC
+    bits (encodings.py:75-88, 102-111, 155-167, 182-192)."""
+    import torch
+    rng = np.random.default_rng(31 + kind)
+    maxL = 32 if kind == 2 else 21
+    n = 70_001
+    lens = rng.integers(0, maxL + 1, n).astype(np.int32)
+    alphabet = np.frombuffer(b"ACGTacgt", np.uint8)
+    recs = [alphabet[rng.integers(0, 8, L)].tobytes() for L in lens]
+    for i in rng.choice(n, 300, replace=False):
+        if lens[i]:
+            b = bytearray(recs[i])
+            b[rng.integers(0, lens[i])] = rng.choice(list(b"NRx#\r"))
+            recs[i] = bytes(b)
+    if layout == "lines":
+        data = b"".join(r + b"\n" for r in recs)
+        starts = np.cumsum([0] + [len(r) + 1 for r in recs[:-1]]).astype(np.int64)
+    else:
+        size = 4 << 20
+        buf = bytearray(rng.integers(0, 256, size, dtype=np.uint8).tobytes())
+        starts = rng.integers(0, size - maxL, n).astype(np.int64)
+        for s, r in zip(starts, recs):  # later records may overwrite earlier ones' bytes
+            buf[s:s + len(r)] = r
+        recs = [bytes(buf[s:s + L]) for s, L in zip(starts, lens)]
+        data = bytes(buf)
+    dev = torch.device("cuda", 0)
+    d_buf = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(dev)
+    d_st = torch.from_numpy(starts).to(dev)
+    d_len = torch.from_numpy(lens).to(dev)
+    codes = torch.empty(n, dtype=torch.int64, device=dev)
+    gc = torch.empty(n, dtype=torch.uint8, device=dev)
+    flags = torch.empty(n, dtype=torch.uint8, device=dev)
+    _lib.check(_lib.lib().sct_encode_var(kind, d_buf.data_ptr(), d_st.data_ptr(), d_len.data_ptr(), n, 1,
+                                         codes.data_ptr(), gc.data_ptr(), flags.data_ptr(), None))
+    torch.cuda.synchronize()
+    got = codes.cpu().numpy().view(np.uint64)
+    g, f = gc.cpu().numpy(), flags.cpu().numpy()
+    for i, r in enumerate(recs):
+        if kind == 3:
+            want = O.three_bit_encode(r)
+            assert (int(got[i]), int(g[i]), int(f[i])) == (want, O.three_bit_gc(want), 0), i
+            continue
+        amb = any(c in b"NRnr" for c in r)
+        bad = any(c not in b"ACGTacgtNRnr" for c in r)
+        assert int(f[i]) == (1 if amb else 0) | (2 if bad else 0), i
+        if not (amb or bad):
+            want = O.two_bit_encode(r)
+            assert (int(got[i]), int(g[i])) == (want, O.two_bit_gc(want, len(r))), i
+
+
+@pytest.mark.parametrize("L", [1, 7, 16, 31, 32, 33, 40])
+def test_base_frequency_lengths(L):
+    """base_frequency_kernel (ballot counts of the 2-bit fields) vs oracle.base_frequency_numpy
+    (barcode.py:48-70) for lengths around the 64-bit key width, ragged n, and n = 0, 1."""
+    rng = np.random.default_rng(L)
+    bits = min(2 * L, 64)
+    for n in (0, 1, 63, 65, 100_003):
+        codes = rng.integers(0, 1 << 62, n, dtype=np.uint64) * np.uint64(4) + rng.integers(0, 4, n, dtype=np.uint64)
+        if bits < 64:
+            codes &= np.uint64((1 << bits) - 1)
+        got = _lib.base_frequency(codes, L)
+        want = O.base_frequency_numpy(codes, L)
+        assert np.array_equal(got, want), (L, n)
