@@ -143,73 +143,57 @@ __global__ __launch_bounds__(WG) void encode_kernel(int kind, const uint8_t* __r
   }
 }
 
-// Variable-length records of one limb (the whitelist's lines): a workgroup's 256 records
-// usually lie in one short stretch of the buffer (consecutive lines), so it stages the
-// aligned 16-B blocks covering [min start, max end) in LDS with coalesced loads and each lane
-// packs its record from there.  Records spread wider than the stage are read from global
-// memory byte by byte (a uniform branch per workgroup).  Every staged 16-B block holds at
-// least one byte of some record, so no load leaves the pages the records lie in.
-constexpr int kVarStage = 8192;
+// Variable-length records of one limb (the whitelist's lines): each lane loads the aligned
+// dwords that hold its record (at most 9 for 32 bases: every load independent, and a wave's
+// loads of consecutive lines cover consecutive lines of memory), realigns them by the start's
+// byte offset and reads every position's LUT entry independently.  Only dwords holding a byte
+// of the record are loaded, so no load leaves the pages the record lies in.  Records longer
+// than 32 bytes take the byte loop.
 __global__ __launch_bounds__(WG) void encode_var_kernel(int kind, const uint8_t* __restrict__ buf, int64_t n,
                                                         const int64_t* __restrict__ starts,
                                                         const int32_t* __restrict__ lens,
                                                         uint64_t* __restrict__ codes, uint8_t* __restrict__ gc,
                                                         uint8_t* __restrict__ flags) {
   __shared__ uint8_t lut[256];
-  __shared__ uint4 stage4[kVarStage / 16];
-  __shared__ unsigned long long lo_s, hi_s;
-  const uint8_t* stage = reinterpret_cast<const uint8_t*>(stage4);
   fill_lut(lut, kind);
-  const int tid = threadIdx.x;
   const uint64_t gcm = kind == 2 ? 0x5555555555555555ull : 0x9249249249249249ull;
-  for (int64_t r0 = (int64_t)blockIdx.x * WG; r0 < n; r0 += (int64_t)gridDim.x * WG) {
-    const int64_t r = r0 + tid;
-    const bool live = r < n;
-    const uintptr_t a = live ? (uintptr_t)(buf + starts[r]) : 0;
-    const int L = live ? lens[r] : 0;
-    if (tid == 0) {
-      lo_s = ~0ull;
-      hi_s = 0;
-    }
-    __syncthreads();
-    if (live && L > 0) {  // (an empty record reads nothing, wherever it starts)
-      atomicMin(&lo_s, (unsigned long long)a);
-      atomicMax(&hi_s, (unsigned long long)(a + L));
-    }
-    __syncthreads();
-    const uintptr_t a0 = (uintptr_t)lo_s & ~(uintptr_t)15, a1 = ((uintptr_t)hi_s + 15) & ~(uintptr_t)15;
-    const bool staged = hi_s > lo_s && a1 - a0 <= (uintptr_t)kVarStage;  // workgroup-uniform
-    if (staged) {
-      const int nblk = (int)((a1 - a0) >> 4);
-      for (int k = tid; k < nblk; k += WG) stage4[k] = reinterpret_cast<const uint4*>(a0)[k];
-      __syncthreads();
-    }
-    if (live) {
-      uint64_t code = 0;
-      uint32_t fl = 0;
-      if (staged) {
-        const uint8_t* rec = stage + (a - a0);
-        for (int p = 0; p < L; ++p) {
-          const uint32_t e = lut[rec[p]];
+  for (int64_t r = (int64_t)blockIdx.x * WG + threadIdx.x; r < n; r += (int64_t)gridDim.x * WG) {
+    const uint8_t* rec = buf + starts[r];
+    const int L = lens[r];
+    uint64_t code = 0;
+    uint32_t fl = 0;
+    if (L == 0) {
+    } else if (L <= 32) {
+      const int o = (int)((uintptr_t)rec & 3), o8 = 8 * o;
+      const uint32_t* dw = reinterpret_cast<const uint32_t*>(rec - o);
+      uint32_t d[9], w[8];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {  // dword k of the record, clamped to its last one (no branch)
+        const int kk = 4 * k < o + L ? k : (o + L - 1) >> 2;
+        d[k] = __builtin_nontemporal_load(dw + kk);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) w[k] = (uint32_t)((((uint64_t)d[k + 1] << 32) | d[k]) >> o8);
+#pragma unroll
+      for (int p = 0; p < 32; ++p)
+        if (p < L) {
+          const uint32_t e = lut[(w[p >> 2] >> (8 * (p & 3))) & 0xFFu];
           code = (code << kind) | (e & 7u);
           fl |= e;
         }
-      } else {
-        const uint8_t* rec = reinterpret_cast<const uint8_t*>(a);
-        for (int p = 0; p < L; ++p) {
-          const uint32_t e = lut[rec[p]];
-          code = (code << kind) | (e & 7u);
-          fl |= e;
-        }
+    } else {
+      for (int p = 0; p < L; ++p) {
+        const uint32_t e = lut[rec[p]];
+        code = (code << kind) | (e & 7u);
+        fl |= e;
       }
-      codes[r] = code;
-      if (gc) {
-        const uint32_t g = (uint32_t)__popcll(code & gcm);
-        gc[r] = (uint8_t)(g > 255 ? 255 : g);
-      }
-      if (flags) flags[r] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
     }
-    __syncthreads();  // stage and lo_s / hi_s are rewritten by the next round
+    codes[r] = code;
+    if (gc) {
+      const uint32_t g = (uint32_t)__popcll(code & gcm);
+      gc[r] = (uint8_t)(g > 255 ? 255 : g);
+    }
+    if (flags) flags[r] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
   }
 }
 
@@ -449,67 +433,105 @@ __global__ __launch_bounds__(WG) void hamming_kernel(int kind, const uint64_t* _
 }
 
 // Per-position base counts.  Base p of a code is bits 2j, 2j + 1 with j = L - 1 - p, and only
-// j < 32 can be non-zero, so the work is the 2-bit fields j of the codes: per 64 codes (one
-// per lane) and field j, the wave's ballots of the field's two bits land in lane j, which
-// counts the three non-zero values by popcount (value 0 = codes seen - the rest).  A wave
-// takes 4 x 64 codes per round (four loads in flight); wave tallies go to LDS, one u64 atomic
-// per (field, value) per workgroup; bases p < L - 32 are all 0 (n of them, added once by
-// workgroup 0).  JT = the field count when known at compile time (16-bp barcodes), else 0.
-template <int JT>
+// j < 32 can be non-zero, so the work is the 32 2-bit fields j of the codes, counted in
+// registers with SWAR counters (no per-code atomics, no per-field loop): per code the
+// indicator masks of values 1, 2, 3 (bit 2j set when field j holds that value) are added into
+// nibble counters (fields 2i / 2i + 1 in nibble i of two words), folded every 15 codes into
+// byte counters (field 4k + q in byte k of word q), and those, every 255 codes or at the end,
+// are widened to 16-bit lanes, summed over the wave by shuffles and added to the workgroup's
+// LDS tally.  Each workgroup writes its 128 partials (bin-major), which
+// base_frequency_reduce_kernel sums: no same-address global atomics.  A lane's codes are
+// gridDim * 256 apart, so a wave's loads stay coalesced.
 __global__ __launch_bounds__(WG) void base_frequency_kernel(const uint64_t* __restrict__ codes,
-                                                            int64_t n, int L,
-                                                            unsigned long long* __restrict__ out) {
-  constexpr int U = 4;
+                                                            int64_t n, unsigned long long* __restrict__ part) {
+  constexpr uint64_t K5 = 0x5555555555555555ull, K1 = 0x1111111111111111ull, KF = 0x0F0F0F0F0F0F0F0Full;
   __shared__ unsigned long long tally[32][4];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int J = JT ? JT : (L < 32 ? L : 32);  // fields with data
   if (tid < 128) tally[tid >> 2][tid & 3] = 0;
   __syncthreads();
-  unsigned long long c[4] = {0, 0, 0, 0};  // lane j: [codes seen, value 1, 2, 3] of field j
-  const int64_t step = (int64_t)gridDim.x * WG * U;
-  for (int64_t r0 = ((int64_t)blockIdx.x * WG + (tid & ~63)) * U; r0 < n; r0 += step) {
-    uint64_t code[U];
+  const int64_t G = (int64_t)gridDim.x * WG;
+  unsigned long long seen = 0;
+  for (int64_t e0 = (int64_t)blockIdx.x * WG + tid; e0 - tid < n; e0 += 255 * G) {  // epochs of <= 255 codes per lane
+    uint64_t Q[3][4] = {};  // [value - 1][q]: byte k counts field 4k + q
+    for (int c = 0; c < 17; ++c) {
+      const int64_t c0 = e0 + (int64_t)c * 15 * G;
+      if (c0 - tid >= n) break;  // workgroup-uniform
+      uint64_t N[3][2] = {};  // [value - 1][field parity]: nibble i counts field 2i + parity
+      uint64_t xs[15];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t r = r0 + 64 * u + lane;
-      code[u] = r < n ? codes[r] : 0ull;
-    }
-    c[0] += (unsigned long long)(n - r0 < 64 * U ? n - r0 : 64 * U);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      uint64_t mh = 0, ml = 0;
-      auto field = [&](int j) {
-        const uint32_t f = (uint32_t)(code[u] >> (2 * j)) & 3u;
-        const uint64_t bl = __ballot(f & 1u), bh = __ballot(f >> 1);
-        if (lane == j) {
-          ml = bl;
-          mh = bh;
-        }
-      };
-      if constexpr (JT > 0) {
-#pragma unroll
-        for (int j = 0; j < JT; ++j) field(j);
-      } else {
-        for (int j = 0; j < J; ++j) field(j);
+      for (int u = 0; u < 15; ++u) {  // all 15 loads issued first (clamped, not branched around)
+        const int64_t r = c0 + u * G;
+        xs[u] = codes[r < n ? r : n - 1];
       }
-      c[1] += __popcll(ml & ~mh);
-      c[2] += __popcll(mh & ~ml);
-      c[3] += __popcll(mh & ml);
+#pragma unroll
+      for (int u = 0; u < 15; ++u) {
+        const int64_t r = c0 + u * G;
+        if (r < n) {
+          const uint64_t x = xs[u];
+          const uint64_t lo = x & K5, hi = (x >> 1) & K5, m3 = lo & hi, m[3] = {lo ^ m3, hi ^ m3, m3};
+#pragma unroll
+          for (int v = 0; v < 3; ++v) {
+            N[v][0] += m[v] & K1;
+            N[v][1] += (m[v] >> 2) & K1;
+          }
+          ++seen;
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        Q[v][0] += N[v][0] & KF;         // fields 4k
+        Q[v][2] += (N[v][0] >> 4) & KF;  // fields 4k + 2
+        Q[v][1] += N[v][1] & KF;         // fields 4k + 1
+        Q[v][3] += (N[v][1] >> 4) & KF;  // fields 4k + 3
+      }
     }
+    // bytes -> 16-bit lanes (even / odd bytes), summed over the wave (<= 64 * 255 per lane)
+#pragma unroll
+    for (int v = 0; v < 3; ++v)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          uint64_t w = (Q[v][q] >> (8 * h)) & 0x00FF00FF00FF00FFull;  // u16 lane i = byte 2i + h
+#pragma unroll
+          for (int o = 32; o; o >>= 1) w += __shfl_xor(w, o);
+          if (lane < 4) {  // lane i takes u16 lane i: byte k = 2i + h, field 4k + q
+            const int k = 2 * lane + h;
+            atomicAdd(&tally[4 * k + q][v + 1], (unsigned long long)((w >> (16 * lane)) & 0xFFFFu));
+          }
+        }
   }
-  if (lane < J) {
-    atomicAdd(&tally[lane][0], c[0] - c[1] - c[2] - c[3]);
-    atomicAdd(&tally[lane][1], c[1]);
-    atomicAdd(&tally[lane][2], c[2]);
-    atomicAdd(&tally[lane][3], c[3]);
-  }
+  for (int o = 32; o; o >>= 1) seen += __shfl_xor(seen, o);
+  if (lane == 0) atomicAdd(&tally[0][0], seen);  // codes seen; value 0 = seen - the rest
   __syncthreads();
-  if (tid < 4 * J) {
+  if (tid < 128) {
     const int j = tid >> 2, v = tid & 3;
-    if (tally[j][v]) atomicAdd(out + 4 * (L - 1 - j) + v, tally[j][v]);
+    unsigned long long t = tally[j][v];
+    if (v == 0) t = tally[0][0] - tally[j][1] - tally[j][2] - tally[j][3];
+    part[(size_t)tid * gridDim.x + blockIdx.x] = t;
   }
-  if (blockIdx.x == 0)
-    for (int p = tid; p < L - 32; p += WG) out[4 * p] = (unsigned long long)n;
+}
+
+// out[4 (L - 1 - j) + v] = the sum of the workgroups' partials of (j, v) (one workgroup per
+// bin); bases p < L - 32 are all 0: n of value 0
+__global__ __launch_bounds__(WG) void base_frequency_reduce_kernel(const unsigned long long* __restrict__ part,
+                                                                   int parts, int64_t n, int L,
+                                                                   unsigned long long* __restrict__ out) {
+  const int b = blockIdx.x, j = b >> 2, v = b & 3;
+  unsigned long long s = 0;
+  for (int i = threadIdx.x; i < parts; i += WG) s += part[(size_t)b * parts + i];
+#pragma unroll
+  for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o);
+  __shared__ unsigned long long ws[WG / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < WG / 64; ++w) s += ws[w];
+    if (j < 32 && j < L) out[4 * (L - 1 - j) + v] = s;
+  }
+  if (b == 0)
+    for (int p = threadIdx.x; p < L - 32; p += WG)
+      for (int k = 0; k < 4; ++k) out[4 * p + k] = k ? 0ull : (unsigned long long)n;
 }
 
 unsigned grid_for(int64_t n) {
@@ -572,7 +594,7 @@ extern "C" int sct_encode_var(int kind, const uint8_t* buf, const int64_t* start
   if (n == 0) return SCT_OK;
   SCT_CHECK(buf && starts && lens && codes, "NULL pointer");
   if (words == 1) {
-    hipLaunchKernelGGL(encode_var_kernel, dim3(grid_for(n)), dim3(WG), 0, sct::as_stream(stream), kind, buf, n,
+    hipLaunchKernelGGL(encode_var_kernel, dim3((unsigned)std::min<int64_t>(sct::ceil_div(n, WG), 1 << 30)), dim3(WG), 0, sct::as_stream(stream), kind, buf, n,
                        starts, lens, codes, gc, flags);
     SCT_LAUNCH_CHECK();
     return SCT_OK;
@@ -635,16 +657,23 @@ extern "C" int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint6
   SCT_CHECK(n >= 0 && L >= 0 && L <= 1024, "bad n/L");
   SCT_CHECK(out != nullptr && (n == 0 || codes != nullptr), "NULL pointer");
   if (L == 0) return SCT_OK;
-  SCT_HIP(hipMemsetAsync(out, 0, (size_t)L * 4 * 8, sct::as_stream(stream)));
-  if (n == 0) return SCT_OK;
-  const unsigned blocks = (unsigned)std::min<int64_t>(sct::ceil_div(n, 4 * WG), 2048);
-  if (L == 16)
-    hipLaunchKernelGGL(base_frequency_kernel<16>, dim3(blocks), dim3(WG), 0, sct::as_stream(stream), codes, n, L,
-                       reinterpret_cast<unsigned long long*>(out));
-  else
-    hipLaunchKernelGGL(base_frequency_kernel<0>, dim3(blocks), dim3(WG), 0, sct::as_stream(stream), codes, n, L,
-                       reinterpret_cast<unsigned long long*>(out));
-  SCT_LAUNCH_CHECK();
+  hipStream_t s = sct::as_stream(stream);
+  if (n == 0) {
+    SCT_HIP(hipMemsetAsync(out, 0, (size_t)L * 4 * 8, s));  // no code: every count 0
+    return SCT_OK;
+  }
+  const int blocks = (int)std::min<int64_t>(sct::ceil_div(n, 8 * WG), 1024);
+  void* part = nullptr;
+  sct::keep_pool_warm();
+  SCT_HIP(hipMallocAsync(&part, (size_t)128 * blocks * 8, s));
+  hipLaunchKernelGGL(base_frequency_kernel, dim3(blocks), dim3(WG), 0, s, codes, n, (unsigned long long*)part);
+  hipError_t le = hipGetLastError();
+  if (le == hipSuccess)
+    hipLaunchKernelGGL(base_frequency_reduce_kernel, dim3(128), dim3(WG), 0, s, (const unsigned long long*)part,
+                       blocks, n, L, reinterpret_cast<unsigned long long*>(out));
+  if (le == hipSuccess) le = hipGetLastError();
+  (void)hipFreeAsync(part, s);
+  if (le != hipSuccess) return sct::fail(SCT_E_HIP, "kernel launch: %s", hipGetErrorString(le));
   return SCT_OK;
 }
 

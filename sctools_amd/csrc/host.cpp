@@ -3,8 +3,11 @@
 #include <math.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <utility>
+#include <vector>
 
 #include "sct_common.h"
 
@@ -76,6 +79,21 @@ int64_t tune(int key, int64_t dflt) {
   if (key <= 0 || key >= SCT_TUNE_NKEYS) return dflt;
   const int64_t v = g_tune[key].load(std::memory_order_relaxed);
   return v == 0 ? dflt : v - 1;
+}
+
+void keep_pool_warm() {
+  static std::mutex mu;
+  static std::vector<int> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> lk(mu);
+  if (std::find(done.begin(), done.end(), dev) != done.end()) return;
+  done.push_back(dev);
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  }
 }
 
 }  // namespace sct

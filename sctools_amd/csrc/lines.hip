@@ -16,8 +16,6 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
-#include <mutex>
-#include <vector>
 
 #include "sct_common.h"
 
@@ -76,7 +74,7 @@ __global__ __launch_bounds__(WG) void line_starts_kernel(const uint8_t* __restri
 }
 
 // chopped lengths: line g is [starts[g], P_g) with P_g = starts[g + 1] - 1 (the file's last
-// byte for the last line); the longest by a wave maximum, one atomic per wave
+// byte for the last line); the longest by a workgroup maximum
 __global__ __launch_bounds__(WG) void line_lens_kernel(const int64_t* __restrict__ starts, int64_t nlines,
                                                        int64_t nbytes, int32_t* __restrict__ lens,
                                                        int32_t* __restrict__ maxlen) {
@@ -89,7 +87,16 @@ __global__ __launch_bounds__(WG) void line_lens_kernel(const int64_t* __restrict
   }
 #pragma unroll
   for (int s = 32; s; s >>= 1) mx = max(mx, __shfl_xor(mx, s));
-  if ((threadIdx.x & 63) == 0 && mx > 0) atomicMax(maxlen, mx);
+  // same-address atomics serialise at L2 (8,192 of them cost ~0.1 ms): one per workgroup,
+  // and only when it would raise the maximum already published
+  __shared__ int32_t wmax[WG / 64];
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 1; w < WG / 64; ++w) mx = max(mx, wmax[w]);
+    if (mx > __hip_atomic_load(maxlen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(maxlen, mx);
+  }
 }
 
 // Scratch of one call, allocated and freed in stream order (the device's default memory
@@ -107,21 +114,6 @@ struct StreamBuf {
   }
 };
 
-void keep_pool_warm() {
-  static std::mutex mu;
-  static std::vector<int> done;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return;
-  std::lock_guard<std::mutex> lk(mu);
-  if (std::find(done.begin(), done.end(), dev) != done.end()) return;
-  done.push_back(dev);
-  hipMemPool_t pool;
-  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-    uint64_t keep = UINT64_MAX;
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-  }
-}
-
 }  // namespace
 
 // Lines of a device buffer (binary mode) with the [:-1] chop: starts / lens of nlines lines
@@ -137,7 +129,7 @@ extern "C" int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines
   hipStream_t s = sct::as_stream(stream);
   const int64_t ntiles = sct::ceil_div(nbytes, TILE);
   SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
-  keep_pool_warm();
+  sct::keep_pool_warm();
   size_t tb = 0;
   SCT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                            (int)(ntiles + 1), s));

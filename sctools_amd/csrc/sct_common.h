@@ -61,6 +61,11 @@ constexpr size_t kZeroCopyBytes = 64 << 10;
 // it the caller's arrays are copied through per-call device allocations.
 constexpr size_t kStageBytes = 256ull << 20;
 
+// Raise the release threshold of the current device's default memory pool once, so that
+// per-call scratch from hipMallocAsync / hipFreeAsync is reused from the pool instead of
+// being mapped and unmapped around every stream synchronisation (host.cpp).
+void keep_pool_warm();
+
 // sct_tune_set value of `key`, or dflt when unset (host.cpp).
 int64_t tune(int key, int64_t dflt);
 
