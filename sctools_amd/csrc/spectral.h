@@ -24,6 +24,14 @@ constexpr int digit_weight_c(uint32_t z) {
   return w;
 }
 constexpr int gray(int i) { return i ^ (i >> 1); }
+// a + popcount(x) as one v_bcnt_u32_b32 with the running sum as its addend: the compiler
+// otherwise counts every group from 0 and sums the counts with v_add3 (one more VALU
+// instruction per walk step)
+__device__ __forceinline__ uint32_t popc_add(uint32_t x, uint32_t a) {
+  uint32_t r;
+  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(a));
+  return r;
+}
 constexpr int ctz_c(int i) {
   int k = 0;
   while (!(i & 1)) {

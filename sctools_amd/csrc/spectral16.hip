@@ -203,7 +203,7 @@ __device__ __forceinline__ void walk_sm16(const uint32_t (*pr)[kHi16], int zblk,
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       if (i) x[g] ^= pr[g][ctz_c(i)];
-      a += __popc(x[g]);
+      a = g ? popc_add(x[g], a) : (uint32_t)__popc(x[g]);  // one v_bcnt per group, no v_add3
     }
     st8[gray(i) * 256 + tid] = (uint8_t)a;
     if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
