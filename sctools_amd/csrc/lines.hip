@@ -55,9 +55,12 @@ __global__ __launch_bounds__(WG) void line_count_kernel(const uint8_t* __restric
 
 // line g ends at byte P_g, so line g + 1 starts at P_g + 1: every end found is stored as the
 // next line's start (starts[0] = 0); the last line ends at the file's last byte
+// (nlines = offsets[ntiles], read here: a capacity below it leaves the outputs untouched)
 __global__ __launch_bounds__(WG) void line_starts_kernel(const uint8_t* __restrict__ buf, int64_t n,
                                                          const unsigned long long* __restrict__ offsets,
-                                                         int64_t nlines, int64_t* __restrict__ starts) {
+                                                         int64_t ntiles, int64_t cap, int64_t* __restrict__ starts) {
+  const int64_t nlines = (int64_t)offsets[ntiles];
+  if (nlines > cap) return;
   const int64_t p0 = (int64_t)blockIdx.x * TILE + threadIdx.x * 16;
   uint32_t m = p0 < n ? lf_mask(buf, n, p0) : 0u;
   using BS = hipcub::BlockScan<uint32_t, WG>;
@@ -75,9 +78,12 @@ __global__ __launch_bounds__(WG) void line_starts_kernel(const uint8_t* __restri
 
 // chopped lengths: line g is [starts[g], P_g) with P_g = starts[g + 1] - 1 (the file's last
 // byte for the last line); the longest by a workgroup maximum
-__global__ __launch_bounds__(WG) void line_lens_kernel(const int64_t* __restrict__ starts, int64_t nlines,
+__global__ __launch_bounds__(WG) void line_lens_kernel(const int64_t* __restrict__ starts,
+                                                       const unsigned long long* __restrict__ total, int64_t cap,
                                                        int64_t nbytes, int32_t* __restrict__ lens,
                                                        int32_t* __restrict__ maxlen) {
+  const int64_t nlines = (int64_t)*total;
+  if (nlines > cap) return;  // workgroup-uniform: before the barrier below
   int32_t mx = 0;
   for (int64_t g = (int64_t)blockIdx.x * WG + threadIdx.x; g < nlines; g += (int64_t)gridDim.x * WG) {
     const int64_t end = g + 1 < nlines ? starts[g + 1] - 1 : nbytes - 1;
@@ -118,7 +124,7 @@ struct StreamBuf {
 
 // Lines of a device buffer (binary mode) with the [:-1] chop: starts / lens of nlines lines
 // (capacity max_lines; a sizing call with max_lines < the count fills nothing), the longest
-// chopped length in *max_len.  Synchronous on `stream`.
+// chopped length in *max_len.  Synchronous on `stream` (one synchronisation).
 extern "C" int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines, int64_t* d_starts,
                          int32_t* d_lens, int64_t* nlines, int32_t* max_len, void* stream) {
   SCT_CHECK(nlines != nullptr && max_len != nullptr, "NULL pointer");
@@ -145,21 +151,29 @@ extern "C" int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines
   hipLaunchKernelGGL(line_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, cnt);
   SCT_LAUNCH_CHECK();
   SCT_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, off, (int)(ntiles + 1), s));
+  const unsigned long long* d_total = off + ntiles;
   unsigned long long total = 0;
-  SCT_HIP(hipMemcpyAsync(&total, off + ntiles, 8, hipMemcpyDeviceToHost, s));
-  SCT_HIP(hipStreamSynchronize(s));
-  *nlines = (int64_t)total;
-  if (max_lines < (int64_t)total || total == 0) return SCT_OK;
-  SCT_CHECK(d_starts && d_lens, "NULL output");
+  if (max_lines <= 0 || !d_starts || !d_lens) {  // a sizing call: the count only
+    SCT_HIP(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, s));
+    SCT_HIP(hipStreamSynchronize(s));
+    *nlines = (int64_t)total;
+    return SCT_OK;
+  }
+  // the spans follow without waiting for the count: the kernels read it on the device and
+  // leave the outputs untouched when it exceeds max_lines; one synchronisation at the end
   hipLaunchKernelGGL(line_starts_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes,
-                     (const unsigned long long*)off, (int64_t)total, d_starts);
+                     (const unsigned long long*)off, ntiles, max_lines, d_starts);
   SCT_LAUNCH_CHECK();
   SCT_HIP(hipMemsetAsync(mx, 0, 4, s));
-  hipLaunchKernelGGL(line_lens_kernel, dim3((unsigned)std::min<int64_t>(sct::ceil_div((int64_t)total, WG), 2048)),
-                     dim3(WG), 0, s, (const int64_t*)d_starts, (int64_t)total, nbytes, d_lens, mx);
+  hipLaunchKernelGGL(line_lens_kernel, dim3((unsigned)std::min<int64_t>(sct::ceil_div(max_lines, WG), 2048)),
+                     dim3(WG), 0, s, (const int64_t*)d_starts, d_total, max_lines, nbytes, d_lens, mx);
   SCT_LAUNCH_CHECK();
-  SCT_HIP(hipMemcpyAsync(max_len, mx, 4, hipMemcpyDeviceToHost, s));
+  int32_t mlen = 0;
+  SCT_HIP(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, s));
+  SCT_HIP(hipMemcpyAsync(&mlen, mx, 4, hipMemcpyDeviceToHost, s));
   SCT_HIP(hipStreamSynchronize(s));
+  *nlines = (int64_t)total;
+  *max_len = (int64_t)total <= max_lines ? mlen : 0;
   return SCT_OK;
 }
 

@@ -1118,3 +1118,30 @@ def test_base_frequency_lengths(L):
         got = _lib.base_frequency(codes, L)
         want = O.base_frequency_numpy(codes, L)
         assert np.array_equal(got, want), (L, n)
+
+
+def test_lines_capacity_short_fills_nothing():
+    """sct_lines with room for fewer lines than the buffer holds reports the count, a longest
+    line of 0 and leaves the outputs untouched; with room for all of them it fills them
+    (barcode.py:96-97: every line's [:-1])."""
+    import ctypes
+
+    import torch
+    data = b"ACGT\nAC\n\nGGGGG\nT"
+    d_buf = torch.tensor(list(data), dtype=torch.uint8, device="cuda")
+    lib = _lib.lib()
+    for cap in (4, 5, 9):
+        starts = torch.full((9,), -7, dtype=torch.int64, device="cuda")
+        lens = torch.full((9,), -7, dtype=torch.int32, device="cuda")
+        nl, mx = ctypes.c_int64(0), ctypes.c_int32(0)
+        _lib.check(lib.sct_lines(d_buf.data_ptr(), len(data), cap, starts.data_ptr(), lens.data_ptr(),
+                                 ctypes.byref(nl), ctypes.byref(mx), None))
+        assert nl.value == 5
+        if cap < 5:
+            assert mx.value == 0 and (starts == -7).all() and (lens == -7).all()
+        else:
+            lines = data.split(b"\n")
+            want_len = [len(x) for x in lines[:-1]] + [len(lines[-1]) - 1]
+            assert lens[:5].tolist() == want_len and mx.value == max(want_len)
+            assert starts[:5].tolist() == [0, 5, 8, 9, 15]
+            assert (starts[5:] == -7).all()
