@@ -978,7 +978,7 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
     // items = the 4096 transform slices; no selection table
     p->ncounts = sct_spectral::kNCounts;
     p->items = n >= 2 ? sct_spectral::kSlices : 0;
-    const int rc = sct_spectral::create(p->spec, p->d_codes, n, sct::tune(SCT_TUNE_SPECTRAL_CHUNK, 65536), cus);
+    const int rc = sct_spectral::create(p->spec, p->d_codes, n, sct::tune(SCT_TUNE_SPECTRAL_CHUNK, 262144), cus);
     if (rc != SCT_OK) return cleanup(rc);
     p->spec.timer = &p->timer;
     *plan = p;

@@ -727,7 +727,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
   // planes in turn (a runtime loop: one plane's 16 VGPRs of bytes live at a time, the next
   // plane's loads in flight), the per-plane sums of all four quarters carried across
   for (int u = ub; u < ue; ++u) {
-    const int s = order ? (int)order[u] : u;
+    // (a chunk of 2^k > kMaxOrder slices: each aligned 2^16 block in its own weight order)
+    const int s = order ? ((u & ~(kMaxOrder - 1)) | (int)order[u & (kMaxOrder - 1)]) : u;
     const int wz = digit_weight((uint32_t)(z0 + s));  // wave-uniform
     if (wz != cur_w) {
       if (cur_w >= 0) flush();
@@ -816,7 +817,7 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
   if constexpr (sizeof(T) == 1) {
     // an aligned power-of-two range goes in digit-weight order (table 2^b at offset 2^b)
     const int ns = z1 - z0;
-    const uint16_t* order = ((ns & (ns - 1)) == 0 && ns <= kMaxOrder && z0 % ns == 0) ? st.d_order + ns : nullptr;
+    const uint16_t* order = ((ns & (ns - 1)) == 0 && z0 % ns == 0) ? st.d_order + std::min(ns, kMaxOrder) : nullptr;
     const dim3 rgrid((unsigned)std::max(1, std::min(st.grid * st.tile_wgs, (z1 - z0 + 3) / 4)));
     hipLaunchKernelGGL(tile_reg_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
   } else {
@@ -922,6 +923,9 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   SCT_HIP(hipMalloc(&st.d_cnt, (size_t)2 * kLo * 4));  // counts, then scatter cursors
   st.max_m = maxm;
   st.elem_bytes = maxm <= 127 ? 1 : (maxm <= 32767 ? 2 : 4);
+  // the intermediate holds one chunk: at most 4 GiB (all 2^18 slices at int8: one seed and one
+  // tile launch per count; int16 / int32 seeds take 2 / 4 passes)
+  st.chunk = std::min<int64_t>(st.chunk, (int64_t(4) << 30) / ((int64_t)kLo * st.elem_bytes));
   int per_cu = 0;  // resident register-tile workgroups per CU (VGPR bound: 3)
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_reg_kernel, 256, 0) != hipSuccess || per_cu <= 0)
     per_cu = 2;

@@ -37,7 +37,7 @@ constexpr int kPW16 = 16;                           // plane words per group: fo
 constexpr int kWalk16 = 64, kWalkBits16 = 6;
 constexpr int kSeedWalks16 = 16;
 constexpr int kSortWGs16 = 128, kSortThreads16 = 1024;
-constexpr int kChunk16 = 16384;                     // real slices per seed / tile pass: 1 GiB
+constexpr int kChunk16 = kSlices16;                 // at most every real slice in one seed / tile pass: 4 GiB
 
 __device__ __forceinline__ void wg_range16(int64_t n, int64_t& b, int64_t& e) {
   b = n * blockIdx.x / gridDim.x;

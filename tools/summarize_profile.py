@@ -25,11 +25,11 @@ SIMDS = 1024
 
 # (name, kernel-name substring, pmc pass dirs prefix, trace dir, units per launch, unit)
 KERNELS = (
-    ("spectral_seed", "seed_sm_kernel", "pmc", "trace", 65536, "slices"),
-    ("spectral", "tile_reg_kernel", "pmc", "trace", 65536, "slices"),
+    ("spectral_seed", "seed_sm_kernel", "pmc", "trace", 262144, "slices"),
+    ("spectral", "tile_reg_kernel", "pmc", "trace", 262144, "slices"),
     ("spectral_seed_int16", "seed_kernel<short>", "pmc", "trace", 65536, "slices"),
-    ("spectral_seed16", "seed16_sm_kernel", "s5pmc", "s5trace", 16384, "slices of 2^16"),
-    ("spectral16", "tile16_kernel", "s5pmc", "s5trace", 16384, "slices of 2^16"),
+    ("spectral_seed16", "seed16_sm_kernel", "s5pmc", "s5trace", 65536, "slices of 2^16"),
+    ("spectral16", "tile16_kernel", "s5pmc", "s5trace", 65536, "slices of 2^16"),
     ("nearest", "halves_query_kernel", "npmc", "ntrace", 100_000_000, "queries"),
     ("nearest_index", "halves_index_kernel", "npmc", "ntrace", 100_000_000, "queries"),
 )
