@@ -401,9 +401,9 @@ __device__ __forceinline__ void seed_body(const uint32_t* __restrict__ planes, c
 // planes stay in registers at 4+ waves per SIMD.  G = the wave's group count (<= 3; a fourth
 // and later group, columns of > 96 codes, is walked afterwards from L2 into the lane's own
 // stage bytes).  Store-out as seed_body<int8_t>.
+// the walk's start state: every group's planes XORed for the slice bits 6..17 of zblk
 template <int G>
-__device__ __forceinline__ void walk_sm(const uint32_t (*pr)[kHiBits], int zblk, uint8_t* st8, int tid) {
-  uint32_t x[G];
+__device__ __forceinline__ void walk_start(const uint32_t (*pr)[kHiBits], int zblk, uint32_t* x) {
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     uint32_t v = 0;
@@ -412,6 +412,12 @@ __device__ __forceinline__ void walk_sm(const uint32_t (*pr)[kHiBits], int zblk,
       if ((zblk >> k) & 1) v ^= pr[g][k];
     x[g] = v;
   }
+}
+
+// 64 Gray steps from the start state x; x is left at the last slice's state, which is the
+// start state with plane 5 flipped (gray(63) = 32)
+template <int G>
+__device__ __forceinline__ void walk_from(const uint32_t (*pr)[kHiBits], uint32_t* x, uint8_t* st8, int tid) {
 #pragma unroll
   for (int i = 0; i < kWalk; ++i) {
     uint32_t a = 0;
@@ -426,10 +432,87 @@ __device__ __forceinline__ void walk_sm(const uint32_t (*pr)[kHiBits], int zblk,
 }
 
 constexpr int kRegGroupsSM = 3;
-__global__ __launch_bounds__(256) void seed_sm_kernel(const uint32_t* __restrict__ planes,
-                                                      const uint32_t* __restrict__ gofs,
-                                                      const uint32_t* __restrict__ off, int z0, int z1,
-                                                      int8_t* __restrict__ buf) {
+constexpr int kMaxWalkBlockBits = 4;  // walks per Gray-ordered block: <= 16
+
+// after the register groups' walk of slices zblk..zblk + 63: the groups beyond them (columns of
+// > 96 codes) from L2 into the lane's stage bytes, then the stage to HBM as int8 m - 2 * sum
+__device__ __forceinline__ void seed_finish(const uint32_t* __restrict__ planes, uint32_t g0, int ng, int wng,
+                                            uint8_t* st8, int tid, const uint32_t* mx, int mcb, int c0, int zblk,
+                                            int z0, int z1, int8_t* __restrict__ buf) {
+  constexpr int NT = 256;
+  for (int g = kRegGroupsSM; g < wng; ++g) {
+    uint32_t p[kHiBits];
+    if (g < ng) {
+      load_planes(planes, (int64_t)g0 + g, p);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kHiBits; ++k) p[k] = 0u;
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = kWalkBits; k < kHiBits; ++k)
+      if ((zblk >> k) & 1) x ^= p[k];
+#pragma unroll
+    for (int i = 0; i < kWalk; ++i) {
+      if (i) x ^= p[ctz_c(i)];
+      st8[gray(i) * NT + tid] += (uint8_t)__popc(x);
+      if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kWalk / 16; ++r) {
+    const int row = tid / (NT / 16) + 16 * r, z = zblk + row;
+    const uint4 v = *reinterpret_cast<const uint4*>(st8 + row * NT + mcb);
+    const uint4 o = make_uint4((mx[0] - (v.x + v.x)) ^ 0x80808080u, (mx[1] - (v.y + v.y)) ^ 0x80808080u,
+                               (mx[2] - (v.z + v.z)) ^ 0x80808080u, (mx[3] - (v.w + v.w)) ^ 0x80808080u);
+    if (z >= z0 && z < z1) *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + c0 + mcb) = o;
+  }
+}
+
+// the workgroup's walks for a wave group count G: walks in blocks of 2^lp aligned on the
+// absolute walk index, each block in Gray order -- consecutive walks differ in one slice
+// bit (6 + t), so a walk starts from the previous one's last state with planes 5 and 6 + t
+// flipped: two XORs per group instead of the start state's twelve planes
+template <int G>
+__device__ __forceinline__ void seed_walks(const uint32_t (*pr)[kHiBits], const uint32_t* __restrict__ planes,
+                                           uint32_t g0, int ng, int wng, uint8_t* st8, int tid, const uint32_t* mx,
+                                           int mcb, int c0, int z0, int z1, int8_t* __restrict__ buf, int lp) {
+  const int wa = (z0 & ~(kWalk - 1)) >> kWalkBits, we = (z1 + kWalk - 1) >> kWalkBits, P = 1 << lp;
+  const int b1 = (we + P - 1) >> lp;
+  for (int b = (wa >> lp) + blockIdx.y; b < b1; b += gridDim.y) {
+    uint32_t x[G];
+    walk_start<G>(pr, (b << lp) << kWalkBits, x);
+    for (int j = 0; j < P; ++j) {  // workgroup-uniform
+      if (j) {
+        const int t = __builtin_ctz(j);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          uint32_t f = pr[g][kWalkBits - 1];
+#pragma unroll
+          for (int k = 0; k < kMaxWalkBlockBits; ++k)
+            if (k == t) f ^= pr[g][kWalkBits + k];
+          x[g] ^= f;
+        }
+      }
+      const int w = (b << lp) + (j ^ (j >> 1));
+      if (w < wa || w >= we) {  // outside the range: the state as if walked
+#pragma unroll
+        for (int g = 0; g < G; ++g) x[g] ^= pr[g][kWalkBits - 1];
+        continue;
+      }
+      __syncthreads();  // the previous walk's store-out reads of `stage` are done
+      walk_from<G>(pr, x, st8, tid);
+      seed_finish(planes, g0, ng, wng, st8, tid, mx, mcb, c0, w << kWalkBits, z0, z1, buf);
+    }
+  }
+}
+
+// 96 VGPRs: 5 waves per SIMD (the Gray-block state costs two more registers; at this bound the
+// compiler spills one 8-byte value, reloaded once per walk)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void seed_sm_kernel(
+    const uint32_t* __restrict__ planes, const uint32_t* __restrict__ gofs, const uint32_t* __restrict__ off, int z0,
+    int z1, int8_t* __restrict__ buf, int lp) {
   constexpr int NT = 256;
   __shared__ uint32_t stage[kWalk * NT / 4];
   uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
@@ -465,43 +548,9 @@ __global__ __launch_bounds__(256) void seed_sm_kernel(const uint32_t* __restrict
     if (ph >= 1) __builtin_amdgcn_s_sleep(24);
     if (ph == 2) __builtin_amdgcn_s_sleep(24);
   }
-  const int za = z0 & ~(kWalk - 1);
-  const int nwalks = (z1 - za + kWalk - 1) / kWalk;
-  for (int wk = blockIdx.y; wk < nwalks; wk += gridDim.y) {
-    const int zblk = za + wk * kWalk;
-    __syncthreads();  // the previous walk's store-out reads of `stage` are done
-    if (wng <= 1) walk_sm<1>(pr, zblk, st8, tid);
-    else if (wng == 2) walk_sm<2>(pr, zblk, st8, tid);
-    else walk_sm<3>(pr, zblk, st8, tid);
-    for (int g = kRegGroupsSM; g < wng; ++g) {  // columns of > 96 codes: the rest from L2
-      uint32_t p[kHiBits];
-      if (g < ng) {
-        load_planes(planes, (int64_t)g0 + g, p);
-      } else {
-#pragma unroll
-        for (int k = 0; k < kHiBits; ++k) p[k] = 0u;
-      }
-      uint32_t x = 0;
-#pragma unroll
-      for (int k = kWalkBits; k < kHiBits; ++k)
-        if ((zblk >> k) & 1) x ^= p[k];
-#pragma unroll
-      for (int i = 0; i < kWalk; ++i) {
-        if (i) x ^= p[ctz_c(i)];
-        st8[gray(i) * NT + tid] += (uint8_t)__popc(x);
-        if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < kWalk / 16; ++r) {
-      const int row = tid / (NT / 16) + 16 * r, z = zblk + row;
-      const uint4 v = *reinterpret_cast<const uint4*>(st8 + row * NT + mcb);
-      const uint4 o = make_uint4((mx[0] - (v.x + v.x)) ^ 0x80808080u, (mx[1] - (v.y + v.y)) ^ 0x80808080u,
-                                 (mx[2] - (v.z + v.z)) ^ 0x80808080u, (mx[3] - (v.w + v.w)) ^ 0x80808080u);
-      if (z >= z0 && z < z1) *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo + c0 + mcb) = o;
-    }
-  }
+  if (wng <= 1) seed_walks<1>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
+  else if (wng == 2) seed_walks<2>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
+  else seed_walks<3>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
 }
 
 template <typename T>
@@ -803,9 +852,14 @@ int launch_seed(State& st, int z0, int z1, hipStream_t s) {
   // keep >= 64 workgroup rows so the grid still fills the chip
   const int per_wg = std::max(1, std::min(kSeedWalks, walks / 64));
   const dim3 sgrid(kLo / 256, (unsigned)((walks + per_wg - 1) / per_wg));
-  if constexpr (sizeof(T) == 1)
-    hipLaunchKernelGGL(seed_sm_kernel, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, z0, z1, buf);
-  else
+  if constexpr (sizeof(T) == 1) {
+    int lp = 0;  // walks per Gray-ordered block: the largest power of two <= per_wg, <= 16
+    while (lp < kMaxWalkBlockBits && (2 << lp) <= per_wg) ++lp;
+    const int wa = (z0 & ~(kWalk - 1)) / kWalk, we = (z1 + kWalk - 1) / kWalk;
+    const int nb = ((we + (1 << lp) - 1) >> lp) - (wa >> lp);
+    hipLaunchKernelGGL(seed_sm_kernel, dim3(kLo / 256, (unsigned)nb), dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                       z0, z1, buf, lp);
+  } else
     hipLaunchKernelGGL(seed_kernel<T>, sgrid, dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off, z0, z1, buf);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
