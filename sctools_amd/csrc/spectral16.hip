@@ -187,8 +187,7 @@ __device__ __forceinline__ void load_planes16(const uint32_t* __restrict__ plane
 // the first three groups' planes in registers, a fourth from L2), int8 byte staging and
 // store-out as there.
 template <int G>
-__device__ __forceinline__ void walk_sm16(const uint32_t (*pr)[kHi16], int zblk, uint8_t* st8, int tid) {
-  uint32_t x[G];
+__device__ __forceinline__ void walk_start16(const uint32_t (*pr)[kHi16], int zblk, uint32_t* x) {
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     uint32_t v = 0;
@@ -197,6 +196,11 @@ __device__ __forceinline__ void walk_sm16(const uint32_t (*pr)[kHi16], int zblk,
       if ((zblk >> k) & 1) v ^= pr[g][k];
     x[g] = v;
   }
+}
+
+// 64 Gray steps from the start state x, which is left at the last slice's state (plane 5 flipped)
+template <int G>
+__device__ __forceinline__ void walk_from16(const uint32_t (*pr)[kHi16], uint32_t* x, uint8_t* st8, int tid) {
 #pragma unroll
   for (int i = 0; i < kWalk16; ++i) {
     uint32_t a = 0;
@@ -211,10 +215,82 @@ __device__ __forceinline__ void walk_sm16(const uint32_t (*pr)[kHi16], int zblk,
 }
 
 constexpr int kRegGroups16 = 3;           // groups whose planes stay in registers
-__global__ __launch_bounds__(256) void seed16_sm_kernel(const uint32_t* __restrict__ planes,
-                                                        const uint32_t* __restrict__ gofs,
-                                                        const uint32_t* __restrict__ off, int z0, int z1,
-                                                        int8_t* __restrict__ buf) {
+constexpr int kMaxWalkBlockBits16 = 4;    // walks per Gray-ordered block: <= 16
+
+// after the register groups' walk of slices zblk..zblk + 63: the groups past them from L2, then
+// the stage to HBM
+__device__ __forceinline__ void seed16_finish(const uint32_t* __restrict__ planes, uint32_t g0, int ng, int wng,
+                                              uint8_t* st8, int tid, const uint32_t* mx, int mcb, int c0, int zblk,
+                                              int z0, int z1, int8_t* __restrict__ buf) {
+  constexpr int NT = 256;
+  for (int g = kRegGroups16; g < wng; ++g) {  // the groups past the register-resident ones, from L2
+    uint32_t p[kHi16];
+    if (g < ng) {
+      load_planes16(planes, (int64_t)g0 + g, p);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kHi16; ++k) p[k] = 0u;
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = kWalkBits16; k < kHi16; ++k)
+      if ((zblk >> k) & 1) x ^= p[k];
+#pragma unroll
+    for (int i = 0; i < kWalk16; ++i) {
+      if (i) x ^= p[ctz_c(i)];
+      st8[gray(i) * NT + tid] += (uint8_t)__popc(x);
+      if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kWalk16 / 16; ++r) {
+    const int row = tid / (NT / 16) + 16 * r, z = zblk + row;
+    const uint4 v = *reinterpret_cast<const uint4*>(st8 + row * NT + mcb);
+    const uint4 o = make_uint4((mx[0] - (v.x + v.x)) ^ 0x80808080u, (mx[1] - (v.y + v.y)) ^ 0x80808080u,
+                               (mx[2] - (v.z + v.z)) ^ 0x80808080u, (mx[3] - (v.w + v.w)) ^ 0x80808080u);
+    if (z >= z0 && z < z1) *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo16 + c0 + mcb) = o;
+  }
+}
+
+// the walks in Gray-ordered blocks of 2^lp, as seed_walks in spectral.hip
+template <int G>
+__device__ __forceinline__ void seed16_walks(const uint32_t (*pr)[kHi16], const uint32_t* __restrict__ planes,
+                                             uint32_t g0, int ng, int wng, uint8_t* st8, int tid, const uint32_t* mx,
+                                             int mcb, int c0, int z0, int z1, int8_t* __restrict__ buf, int lp) {
+  const int wa = (z0 & ~(kWalk16 - 1)) >> kWalkBits16, we = (z1 + kWalk16 - 1) >> kWalkBits16, P = 1 << lp;
+  const int b1 = (we + P - 1) >> lp;
+  for (int b = (wa >> lp) + blockIdx.y; b < b1; b += gridDim.y) {
+    uint32_t x[G];
+    walk_start16<G>(pr, (b << lp) << kWalkBits16, x);
+    for (int j = 0; j < P; ++j) {  // workgroup-uniform
+      if (j) {
+        const int t = __builtin_ctz(j);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          uint32_t f = pr[g][kWalkBits16 - 1];
+#pragma unroll
+          for (int k = 0; k < kMaxWalkBlockBits16; ++k)
+            if (k == t) f ^= pr[g][kWalkBits16 + k];
+          x[g] ^= f;
+        }
+      }
+      const int w = (b << lp) + (j ^ (j >> 1));
+      if (w < wa || w >= we) {  // outside the range: the state as if walked
+#pragma unroll
+        for (int g = 0; g < G; ++g) x[g] ^= pr[g][kWalkBits16 - 1];
+        continue;
+      }
+      __syncthreads();  // the previous walk's store-out reads of `stage` are done
+      walk_from16<G>(pr, x, st8, tid);
+      seed16_finish(planes, g0, ng, wng, st8, tid, mx, mcb, c0, w << kWalkBits16, z0, z1, buf);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void seed16_sm_kernel(
+    const uint32_t* __restrict__ planes, const uint32_t* __restrict__ gofs, const uint32_t* __restrict__ off, int z0,
+    int z1, int8_t* __restrict__ buf, int lp) {
   constexpr int NT = 256;
   __shared__ uint32_t stage[kWalk16 * NT / 4];
   uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
@@ -250,43 +326,9 @@ __global__ __launch_bounds__(256) void seed16_sm_kernel(const uint32_t* __restri
     if (ph >= 1) __builtin_amdgcn_s_sleep(24);
     if (ph == 2) __builtin_amdgcn_s_sleep(24);
   }
-  const int za = z0 & ~(kWalk16 - 1);
-  const int nwalks = (z1 - za + kWalk16 - 1) / kWalk16;
-  for (int wk = blockIdx.y; wk < nwalks; wk += gridDim.y) {
-    const int zblk = za + wk * kWalk16;
-    __syncthreads();  // the previous walk's store-out reads of `stage` are done
-    if (wng <= 1) walk_sm16<1>(pr, zblk, st8, tid);
-    else if (wng == 2) walk_sm16<2>(pr, zblk, st8, tid);
-    else walk_sm16<3>(pr, zblk, st8, tid);
-    for (int g = kRegGroups16; g < wng; ++g) {  // the groups past the register-resident ones, from L2
-      uint32_t p[kHi16];
-      if (g < ng) {
-        load_planes16(planes, (int64_t)g0 + g, p);
-      } else {
-#pragma unroll
-        for (int k = 0; k < kHi16; ++k) p[k] = 0u;
-      }
-      uint32_t x = 0;
-#pragma unroll
-      for (int k = kWalkBits16; k < kHi16; ++k)
-        if ((zblk >> k) & 1) x ^= p[k];
-#pragma unroll
-      for (int i = 0; i < kWalk16; ++i) {
-        if (i) x ^= p[ctz_c(i)];
-        st8[gray(i) * NT + tid] += (uint8_t)__popc(x);
-        if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < kWalk16 / 16; ++r) {
-      const int row = tid / (NT / 16) + 16 * r, z = zblk + row;
-      const uint4 v = *reinterpret_cast<const uint4*>(st8 + row * NT + mcb);
-      const uint4 o = make_uint4((mx[0] - (v.x + v.x)) ^ 0x80808080u, (mx[1] - (v.y + v.y)) ^ 0x80808080u,
-                                 (mx[2] - (v.z + v.z)) ^ 0x80808080u, (mx[3] - (v.w + v.w)) ^ 0x80808080u);
-      if (z >= z0 && z < z1) *reinterpret_cast<uint4*>(buf + (int64_t)(z - z0) * kLo16 + c0 + mcb) = o;
-    }
-  }
+  if (wng <= 1) seed16_walks<1>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
+  else if (wng == 2) seed16_walks<2>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
+  else seed16_walks<3>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
 }
 
 // ---------------------------------------------------------------- tile
@@ -543,8 +585,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
 void launch_seed16(State& st, int8_t* buf, int z0, int z1, hipStream_t s) {
   const int walks = (z1 - (z0 & ~(kWalk16 - 1)) + kWalk16 - 1) / kWalk16;
   const int per_wg = std::max(1, std::min(kSeedWalks16, walks / 16));
-  hipLaunchKernelGGL(seed16_sm_kernel, dim3(kLo16 / 256, (unsigned)((walks + per_wg - 1) / per_wg)), dim3(256), 0, s,
-                     st.d_planes, st.d_gofs, st.d_off, z0, z1, buf);
+  int lp = 0;  // walks per Gray-ordered block: the largest power of two <= per_wg, <= 16
+  while (lp < kMaxWalkBlockBits16 && (2 << lp) <= per_wg) ++lp;
+  const int wa = (z0 & ~(kWalk16 - 1)) / kWalk16, we = (z1 + kWalk16 - 1) / kWalk16;
+  const int nb = ((we + (1 << lp) - 1) >> lp) - (wa >> lp);
+  hipLaunchKernelGGL(seed16_sm_kernel, dim3(kLo16 / 256, (unsigned)nb), dim3(256), 0, s, st.d_planes, st.d_gofs, st.d_off,
+                     z0, z1, buf, lp);
 }
 
 void launch_tile16(State& st, const int8_t* buf, int z0, int z1, unsigned long long* counts, hipStream_t s,
