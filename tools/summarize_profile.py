@@ -18,6 +18,7 @@ import csv
 import glob
 import json
 import os
+import statistics
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -36,14 +37,15 @@ KERNELS = (
 
 
 def pmc_means(src, prefix, kernel_substr):
-    agg = collections.defaultdict(float)
-    cnt = collections.Counter()
+    """Per counter, the median over the profiled dispatches of the kernel: a plan's first
+    dispatch into its freshly allocated 4 GiB intermediate runs up to 10x the cycles of the
+    others under the counter passes, and a mean over a handful of dispatches follows it."""
+    vals = collections.defaultdict(list)
     for f in glob.glob(os.path.join(src, prefix + "[0-9]*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             if kernel_substr in r["Kernel_Name"]:
-                agg[r["Counter_Name"]] += float(r["Counter_Value"])
-                cnt[r["Counter_Name"]] += 1
-    return {k: agg[k] / cnt[k] for k in agg}
+                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: statistics.median(v) for k, v in vals.items()}
 
 
 def kernel_avg_ns(stats_csv, kernel_substr):
@@ -83,7 +85,7 @@ def summarize(src, dst, rnd, name, kernel, prefix, trace, units, unit):
         out["l2_requests_per_unit"] = (m["TCC_HIT_sum"] + m["TCC_MISS_sum"]) / units
     if "TCC_EA0_RDREQ_sum" in m:
         out["ea_read_requests_per_unit"] = m["TCC_EA0_RDREQ_sum"] / units
-    out["note"] = ("per-launch means over every profiled dispatch of the kernel; FETCH_SIZE/WRITE_SIZE are KiB "
+    out["note"] = ("per-launch medians over the profiled dispatches of the kernel; FETCH_SIZE/WRITE_SIZE are KiB "
                    "per dispatch, reads doubled per the gfx950 correction; busy fractions are of 1024 SIMDs x "
                    "the profiled run's cycles")
     with open(os.path.join(dst, "pmc_%s_%s.json" % (name, rnd)), "w") as f:
