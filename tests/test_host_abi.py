@@ -106,3 +106,19 @@ def test_limb_roundtrip():
     assert limbs.shape[1] == 2
     assert _lib.limbs_to_ints(limbs) == vals
     assert _lib.limbs_to_ints(_lib.ints_to_limbs([5, 7])) == [5, 7]
+
+
+def test_tune_keys_match_header():
+    """_lib.TUNE_KEYS names exactly the SCT_TUNE_* keys include/sctools_hip.h defines, with the
+    same numbers, and every key round-trips through sct_tune_set / sct_tune_get (host only)."""
+    import os
+    import re
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "sctools_hip.h")).read()
+    defined = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"#define SCT_TUNE_(\w+)\s+(\d+)", hdr)}
+    nkeys = defined.pop("nkeys")
+    assert defined == _lib.TUNE_KEYS
+    assert sorted(defined.values()) == list(range(1, nkeys))
+    for name in _lib.TUNE_KEYS:
+        with _lib.tuning(**{name: 7}):
+            assert _lib.tune_get(name) == 7
+        assert _lib.tune_get(name) == -1
