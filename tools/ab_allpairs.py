@@ -1,5 +1,8 @@
 """Interleaved A/B timing of all-pairs count-kernel variants in ONE process.
 
+(Round 2 tool.  SCT_ALLPAIRS_VARIANT is read only by the ablation build (make ablation); grid,
+grab and the SPECTRAL chunk are sct_tune_set keys since round 3 -- tools/ab_seed_tune.py and
+tools/ab_nearest_tune.py are the current A/B drivers.)
 Variants are selected at plan creation through SCT_ALLPAIRS_VARIANT / _GRID / _GRAB and
 the count scheme (s=0 SUBSETS, s=1 MOMENTS, s=2 SPECTRAL with chunk=slices per pass); each round times every variant once (HIP
 events on the launch stream: the count kernel, and the moments pass separately); prints

@@ -1,7 +1,6 @@
 """Seed and tile kernel times of one SPECTRAL chunk (HIP events around back-to-back
-launches, sct_allpairs_time_kernels), median over R calls; one JSON line.  With the
-ablation library (SCTOOLS_HIP_LIB=...abl.so, SCT_SPECTRAL_ABL / SCT_SEED_ABL) the counts
-are wrong by design: nothing is checked here."""
+launches, sct_allpairs_time_kernels), median over R calls; one JSON line (the kernels the
+round-3 profile script traces for config 5).  Nothing is checked here."""
 import json
 import os
 import sys

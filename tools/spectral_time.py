@@ -1,6 +1,7 @@
 """Time one SPECTRAL count (seed + tile passes) on a config, HIP events, median of R runs.
-Used with the ablation library (SCTOOLS_HIP_LIB=sctools_amd/libsctools_hip_abl.so,
-SCT_SPECTRAL_ABL=1..4), whose counts are wrong by design: nothing is checked here."""
+Round 2 used it with the ablation library and SCT_SPECTRAL_ABL=1..4 (SPECTRAL ablations since
+removed from the sources; the ablation build now only varies the pair kernel).  Nothing is
+checked here."""
 import json
 import sys
 
