@@ -300,7 +300,7 @@ __global__ __launch_bounds__(WG) void oa_query_kernel(const uint64_t* __restrict
 // skipping the codes that agree on A too (those were in the A bucket).  Each whitelist
 // entry is visited at most once, so two candidates at the best distance are two indices: a
 // tie.  The kernel writes the winner's table position (A order: p, B order: nw + p); a second
-// pass maps it to the whitelist index through permAB.
+// pass maps it to the whitelist index through permAB, packed to ceil(log2 nw) bits per entry.
 // Entries are tested two per dword (SWAR): per 16-bit field the mismatching digits
 // m = ((x | x >> 1) & 0x5555) | invalid, x = entry ^ key; then d >= 1 iff m != 0 and d >= 2
 // iff m with its lowest set bit cleared != 0, both read off bit 15 of field + 0x7FFF (no
@@ -314,7 +314,8 @@ struct Halves {
   const uint16_t* entA;     // [nw] B keys, codes sorted by (A, B)
   const uint32_t* offB;     // [4^GB + 1]
   const uint16_t* entB;     // [nw] A keys, codes sorted by (B, A)
-  const uint32_t* permAB;   // [2 nw] whitelist index of each A-order, then B-order position
+  const uint32_t* permAB;   // [2 nw] whitelist index of each A-order, then B-order position (build only;
+                            // the index pass reads it packed, sct_nearest_plan::perm_packed)
   int64_t nw;
 };
 
@@ -456,10 +457,32 @@ __global__ __launch_bounds__(WG) void halves_query_kernel(const uint64_t* __rest
   __builtin_nontemporal_store(dist, out_dist + i);
 }
 
-// table positions -> whitelist indices (-1 / -2 pass through): four queries per lane per
-// step, their perm loads independent
+// permAB packed to pbits per entry (the whitelist index needs ceil(log2 nw) bits: 20 at 737K,
+// 3.7 MB instead of 5.9 -- it fits an XCD's 4 MB L2 while the index pass runs): output dword w
+// gathers the bits of the (at most three) entries overlapping bits [32 w, 32 w + 32)
+__global__ void pack_perm_kernel(const uint32_t* __restrict__ perm, int64_t n, int pbits, int64_t ndw,
+                                 uint32_t* __restrict__ out) {
+  for (int64_t w = (int64_t)blockIdx.x * WG + threadIdx.x; w < ndw; w += (int64_t)gridDim.x * WG) {
+    uint32_t v = 0;
+    for (int64_t e = (32 * w) / pbits; e < n && e * pbits < 32 * w + 32; ++e) {
+      const int64_t sh = e * pbits - 32 * w;
+      v |= sh >= 0 ? perm[e] << sh : perm[e] >> (-sh);
+    }
+    out[w] = v;
+  }
+}
+
+typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ int32_t unpack_perm(const uint32_t* __restrict__ packed, int pbits, int32_t p) {
+  const uint64_t bo = (uint64_t)p * pbits;
+  const u32x2_a4 d = *reinterpret_cast<const u32x2_a4*>(packed + (bo >> 5));  // one 8-byte load
+  return (int32_t)(((((uint64_t)d.y << 32) | d.x) >> (bo & 31)) & ((1ull << pbits) - 1));
+}
+
+// table positions -> whitelist indices (-1 / -2 pass through): four queries per lane per step,
+// their packed-perm loads independent
 __global__ __launch_bounds__(WG) void halves_index_kernel(int32_t* __restrict__ idx, int64_t nq,
-                                                          const uint32_t* __restrict__ perm, bool vec) {
+                                                          const uint32_t* __restrict__ packed, int pbits, bool vec) {
   typedef int v4i __attribute__((ext_vector_type(4)));
   const int64_t n4 = vec ? nq / 4 : 0;  // vec: idx is 16-B aligned
   v4i* idx4 = reinterpret_cast<v4i*>(idx);
@@ -467,11 +490,11 @@ __global__ __launch_bounds__(WG) void halves_index_kernel(int32_t* __restrict__ 
     v4i p = __builtin_nontemporal_load(idx4 + i);
     v4i o;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) o[k] = p[k] >= 0 ? (int)perm[p[k]] : p[k];
+    for (int k = 0; k < 4; ++k) o[k] = p[k] >= 0 ? unpack_perm(packed, pbits, p[k]) : p[k];
     __builtin_nontemporal_store(o, idx4 + i);
   }
   for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * WG + threadIdx.x; i < nq; i += (int64_t)gridDim.x * WG)
-    if (idx[i] >= 0) idx[i] = (int32_t)perm[idx[i]];
+    if (idx[i] >= 0) idx[i] = unpack_perm(packed, pbits, idx[i]);
 }
 
 // whitelist -> (A, B) and (B, A) sort keys; *bad = 1 if a code has a digit that is not A/C/G/T
@@ -568,6 +591,8 @@ struct sct_nearest_plan {
   bool halves = false;  // half-key tables (Halves) for max_d <= 1
   Halves hv{};
   void* hv_mem[5] = {};  // offA, entA, offB, entB, permA
+  uint32_t* perm_packed = nullptr;  // permAB at pbits per entry (+ 2 dwords of padding)
+  int pbits = 0;
   int nkeys = 0;  // > 0: open-addressing multi-index (OTables); 0: CSR per block (Parts)
   OTables ot{};
   Parts parts{};
@@ -581,6 +606,7 @@ extern "C" int sct_nearest_plan_destroy(sct_nearest_plan* p) {
   if (!p) return SCT_OK;
   for (void* m : p->hv_mem)
     if (m) (void)hipFree(m);
+  if (p->perm_packed) (void)hipFree(p->perm_packed);
   for (int k = 0; k < MAX_KEYS; ++k)
     if (p->ot.t[k].slots) (void)hipFree(p->ot.t[k].slots);
   for (int k = 0; k < MAX_PARTS; ++k) {
@@ -645,7 +671,20 @@ static int build_halves(sct_nearest_plan* p, const uint64_t* d_wl, int64_t nw, i
   hipLaunchKernelGGL(halves_table_kernel, dim3(grid_for(nw + 1, 4096)), dim3(WG), 0, s, (const uint32_t*)sBA.p, nw,
                      2 * h.GA, nB, (uint16_t*)p->hv_mem[3], (uint32_t*)p->hv_mem[2]);
   SCT_LAUNCH_CHECK();
-  SCT_HIP(hipStreamSynchronize(s));  // the scratch dies here
+  {
+    int pb = 1;
+    while (pb < 32 && (1LL << pb) < nw) ++pb;
+    const int64_t ndw = (2 * (int64_t)n * pb + 31) / 32 + 2;  // + 2: the last 8-byte load's second dword
+    SCT_HIP(hipMalloc(&p->perm_packed, (size_t)ndw * 4));
+    hipLaunchKernelGGL(pack_perm_kernel, dim3(grid_for(ndw, 4096)), dim3(WG), 0, s, (const uint32_t*)perm,
+                       (int64_t)(2 * n), pb, ndw, p->perm_packed);
+    SCT_LAUNCH_CHECK();
+    p->pbits = pb;
+  }
+  SCT_HIP(hipStreamSynchronize(s));  // the scratch dies here (and the unpacked permAB with it)
+  (void)hipFree(p->hv_mem[4]);
+  p->hv_mem[4] = nullptr;
+  h.permAB = nullptr;
   p->hv = h;
   p->halves = true;
   return SCT_OK;
@@ -812,7 +851,7 @@ extern "C" int sct_nearest_plan_info(const sct_nearest_plan* p, int* scheme, int
   SCT_CHECK(p != nullptr, "plan is NULL");
   int64_t bytes = 0;
   if (p->halves) {
-    bytes = ((1LL << (2 * p->hv.GA)) + (1LL << (2 * p->hv.GB)) + 2) * 4 + p->nw * 12;
+    bytes = ((1LL << (2 * p->hv.GA)) + (1LL << (2 * p->hv.GB)) + 2) * 4 + p->nw * 4 + (2 * p->nw * p->pbits + 31) / 32 * 4;
     if (scheme) *scheme = SCT_NEAREST_HALVES;
     if (index_bytes) *index_bytes = bytes;
     return SCT_OK;
@@ -841,7 +880,7 @@ extern "C" int sct_nearest_query(sct_nearest_plan* p, const uint64_t* d_queries,
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WG), 0, s, d_queries, nq, p->hv, p->max_d, d_index, d_dist);
     SCT_LAUNCH_CHECK();
     hipLaunchKernelGGL(halves_index_kernel, dim3(grid_for(sct::ceil_div(nq, 4), 8192)), dim3(WG), 0, s, d_index, nq,
-                       p->hv.permAB, ((uintptr_t)d_index & 15) == 0);
+                       (const uint32_t*)p->perm_packed, p->pbits, ((uintptr_t)d_index & 15) == 0);
     SCT_LAUNCH_CHECK();
     return SCT_OK;
   }
