@@ -929,13 +929,19 @@ int time_chunk(State& st, int z0, int z1, unsigned long long* counts, int repeat
 
 int make_order_table(State& st) {
   // for every power of two L <= 2^16: the offsets [0, L) sorted by digit weight, stored
-  // at [L, 2L) (an aligned range of L slices adds a constant weight to all of them)
-  std::vector<uint16_t> order(2 * kMaxOrder);
-  for (int len = 1; len <= kMaxOrder; len *= 2) {
-    uint16_t* o = order.data() + len;
-    for (int u = 0; u < len; ++u) o[u] = (uint16_t)u;
-    std::stable_sort(o, o + len, [](uint16_t a, uint16_t b) { return digit_weight_c(a) < digit_weight_c(b); });
-  }
+  // at [L, 2L) (an aligned range of L slices adds a constant weight to all of them); the
+  // same for every plan, so sorted once per process
+  static const std::vector<uint16_t> order = [] {
+    std::vector<uint16_t> o(2 * kMaxOrder);
+    for (int len = 1; len <= kMaxOrder; len *= 2) {  // a stable counting sort by weight (0..8)
+      int start[10] = {};
+      for (int u = 0; u < len; ++u) ++start[digit_weight_c((uint32_t)u) + 1];
+      for (int w = 1; w < 10; ++w) start[w] += start[w - 1];
+      uint16_t* b = o.data() + len;
+      for (int u = 0; u < len; ++u) b[start[digit_weight_c((uint32_t)u)]++] = (uint16_t)u;
+    }
+    return o;
+  }();
   SCT_HIP(hipMalloc(&st.d_order, order.size() * 2));
   SCT_HIP(hipMemcpy(st.d_order, order.data(), order.size() * 2, hipMemcpyHostToDevice));
   return SCT_OK;
