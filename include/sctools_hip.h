@@ -182,9 +182,13 @@ int sct_scalar_server_status(int64_t* launches, int* running);
  *   cut the count kernel's VALU work per pair.
  *
  * SCT_ALLPAIRS_SPECTRAL (the same 16-base codes): no pair is enumerated.  The histogram
- *   comes from the Walsh-Hadamard transform F of the codes' multiplicity over Z_2^32:
- *   d_counts[1+w] += S_w = sum of F(z)^2 over the z with w non-zero 2-bit digits,
- *   w = 0..16, and d_counts[0] += n once (by the range holding item 0).  ncounts = 18.
+ *   comes from the Walsh-Hadamard transform F of the codes' multiplicity f over Z_2^32:
+ *   S_w = sum of F(z)^2 over the z with w non-zero 2-bit digits, w = 0..16, accumulated as
+ *   three limbs that never carry (a multiset's sum_w S_w = 2^32 sum f^2 may exceed 2^64):
+ *   d_counts[2+w] += bits 0..31, d_counts[19+w] += bits 32..63, d_counts[36+w] += bits 64..
+ *   of every partial sum, so S_w = c[2+w] + 2^32 c[19+w] + 2^64 c[36+w]; d_counts[0] += n and
+ *   d_counts[1] += sum f^2 (computed from the sorted codes) once, by the range holding item
+ *   0.  ncounts = 53.  The host checks S_0 = n^2 and sum_w S_w = 2^32 sum f^2 exactly.
  *   The items are the 2^18 transform slices (z >> 14); the cost of a slice does not
  *   depend on n, so AUTO picks this scheme for large whitelists.  Only
  *   the counts of the whole job invert (host: Krawtchouk transform, checked exact).

@@ -409,8 +409,8 @@ def wide_range_pairs(n, begin, end):
 def counts_to_hist(counts, scheme=SCHEME_SUBSETS, nbins=None):
     """Counts of an all-pairs plan (any scheme) -> exact histogram (uint64[nbins])."""
     counts = np.ascontiguousarray(counts, dtype=np.uint64).reshape(-1)
-    if nbins is None:  # SPECTRAL counts carry n ahead of the 17 weight sums
-        nbins = counts.size - 1 if scheme == SCHEME_SPECTRAL else counts.size
+    if nbins is None:  # SPECTRAL counts: n, sum f^2 and three limbs of the 17 weight sums
+        nbins = 17 if scheme == SCHEME_SPECTRAL else counts.size
     hist = np.zeros(nbins, dtype=np.uint64)
     check(lib().sct_counts_to_hist_ex(scheme, _ptr(counts), counts.size, _ptr(hist), nbins))
     return hist

@@ -23,6 +23,8 @@ __all__ = ["Barcodes", "ObservedBarcodeSet", "PriorBarcodeSet", "nearest_whiteli
 
 _MIXED_SIGNS = ('barcode codes mix negative and non-negative integers: their XOR is negative and the '
                 'reference\'s distance loop (encodings.py:118, `while difference:`) never terminates on it')
+_NEGATIVE_OUTSIDE = ('nearest needs non-negative barcode codes: a negative key has no TwoBit distance '
+                     'to a non-negative query that the reference\'s distance loop (encodings.py:118) ends on')
 _SUMMARY_KEYS = ('minimum', '25th percentile', 'median', '75th percentile', 'maximum', 'average')
 
 
@@ -55,7 +57,7 @@ class Barcodes:
         return self._data[item]
 
     # ------------------------------------------------------------ device input
-    def codes_array(self):
+    def codes_array(self, mask_negative=True):
         """The unique keys in iteration order, as the kernels take them: np.uint64 (n,)
         when every key fits 64 bits, else (n, words) little-endian uint64 limbs.  Built from
         the mapping on every call (the reference re-reads ``self`` each time, barcode.py:42),
@@ -66,7 +68,9 @@ class Barcodes:
         like any other: every key shares its bits from m = max bit_length(~k) upward (all
         ones), so ``k & (2^m - 1)`` keeps every pairwise XOR unchanged.  A negative key next
         to a non-negative one gives a negative XOR, on which the reference's ``while
-        difference:`` never ends; that raises ValueError here instead of hanging."""
+        difference:`` never ends; that raises ValueError here instead of hanging.  The masking
+        only preserves XORs WITHIN the set, so callers comparing the codes with outside values
+        (``nearest``) pass ``mask_negative=False`` and get ValueError for any negative key."""
         keys = self._data.keys()
         n = len(self._data)
         if not all(issubclass(t, (int, np.integer)) for t in set(map(type, keys))):
@@ -78,6 +82,8 @@ class Barcodes:
         try:  # the common case (every key in int64) on numpy's fastest conversion
             arr = np.fromiter(keys, dtype=np.int64, count=n)
             if n and int(arr.min()) < 0:
+                if not mask_negative:
+                    raise ValueError(_NEGATIVE_OUTSIDE)
                 if int(arr.max()) >= 0 and n >= 2:
                     raise ValueError(_MIXED_SIGNS)
                 m = int((~arr).max()).bit_length()
@@ -93,6 +99,8 @@ class Barcodes:
         ints = [int(k) for k in keys]
         neg = [v < 0 for v in ints]
         if any(neg):
+            if not mask_negative:
+                raise ValueError(_NEGATIVE_OUTSIDE)
             if not all(neg) and n >= 2:
                 raise ValueError(_MIXED_SIGNS)
             mask = (1 << max((~v).bit_length() for v in ints)) - 1
@@ -122,7 +130,7 @@ class Barcodes:
         """For each TwoBit-encoded query, the index (in iteration order) of the unique
         closest barcode of this set within ``max_distance`` (TwoBit.hamming_distance),
         -2 for a tie, -1 for none; and that distance (255 for none)."""
-        codes = self.codes_array()
+        codes = self.codes_array(mask_negative=False)
         if codes.ndim != 1:
             raise ValueError('nearest needs barcode codes below 2**64')
         return nearest_whitelist(queries, codes, max_distance=max_distance, encoding='TwoBit')

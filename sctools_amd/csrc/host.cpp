@@ -236,14 +236,34 @@ const MomInverse& mom_inverse() {
 
 }  // namespace
 
-// SPECTRAL counts [n, S_0..S_16] -> hist.  Ordered pairs (self pairs included) at
-// distance d: N(d) = 2^-32 sum_w S_w K_d(w), K_d(w) = [t^d] (1 + 3t)^(16-w) (1 - t)^w
-// (per 2-bit digit: 3 non-zero XOR values, characters sum to 3 if z's digit is 0, else
-// -1); hist[d] = (N(d) - n [d = 0]) / 2.  Every step is checked exact.
+// SPECTRAL counts [n, sum f^2, S_w limbs 0 / 1 / 2] (spectral.h) -> hist.  Ordered pairs
+// (self pairs included) at distance d: N(d) = 2^-32 sum_w S_w K_d(w), K_d(w) = [t^d]
+// (1 + 3t)^(16-w) (1 - t)^w (per 2-bit digit: 3 non-zero XOR values, characters sum to 3 if
+// z's digit is 0, else -1); hist[d] = (N(d) - n [d = 0]) / 2.  Every step is checked exact,
+// and against the independently computed sum f^2: S_0 = F(0)^2 = n^2 and, by Parseval,
+// sum_w S_w = 2^32 sum f^2 -- a wrap of any S_w (mod 2^64) would break the latter.
 static int spectral_to_hist(const uint64_t* counts, int ncounts, uint64_t* hist, int nbins) {
   constexpr int G = 16;
-  SCT_CHECK(ncounts == G + 2 && nbins == G + 1, "SPECTRAL counts/hist hold %d/%d values (got %d, %d)",
-            G + 2, G + 1, ncounts, nbins);
+  constexpr int kLimb0 = 2, kLimb1 = kLimb0 + G + 1, kLimb2 = kLimb1 + G + 1, kCounts = kLimb2 + G + 1;
+  SCT_CHECK(ncounts == kCounts && nbins == G + 1, "SPECTRAL counts/hist hold %d/%d values (got %d, %d)",
+            kCounts, G + 1, ncounts, nbins);
+  __int128 S[G + 1];
+  unsigned __int128 sum_s = 0;
+  for (int w = 0; w <= G; ++w) {
+    // every limb is a sum of < 2^32 pieces (or small high words): none can be near 2^63
+    const uint64_t l0 = counts[kLimb0 + w], l1 = counts[kLimb1 + w], l2 = counts[kLimb2 + w];
+    SCT_CHECK(l0 < (1ull << 62) && l1 < (1ull << 62) && l2 < (1ull << 40),
+              "inconsistent SPECTRAL counts (limbs of S_%d)", w);
+    const unsigned __int128 v = (unsigned __int128)l0 + ((unsigned __int128)l1 << 32) + ((unsigned __int128)l2 << 64);
+    S[w] = (__int128)v;
+    sum_s += v;
+  }
+  const __int128 n = counts[0];
+  const unsigned __int128 sumsq = counts[1];
+  if (S[0] != n * n)
+    return sct::fail(SCT_E_RANGE, "inconsistent SPECTRAL counts (S_0 != n^2)");
+  if (n >= 2 && (sumsq < (unsigned __int128)n || sum_s != (sumsq << 32)))
+    return sct::fail(SCT_E_RANGE, "inconsistent SPECTRAL counts (sum_w S_w != 2^32 sum f^2)");
   struct Kraw {
     __int128 k[G + 1][G + 1];  // k[d][w]
     Kraw() {
@@ -259,11 +279,10 @@ static int spectral_to_hist(const uint64_t* counts, int ncounts, uint64_t* hist,
   };
   static const Kraw kraw;
   const auto& K = kraw.k;
-  const __int128 n = counts[0];
   __int128 total = 0;
   for (int d = 0; d <= G; ++d) {
-    __int128 s = 0;
-    for (int w = 0; w <= G; ++w) s += K[d][w] * (__int128)counts[1 + w];
+    __int128 s = 0;  // |K| < 3^16, S_w <= 2^32 n^2 <= 2^86 (n <= 1e8): no overflow
+    for (int w = 0; w <= G; ++w) s += K[d][w] * S[w];
     if (s % ((__int128)1 << 32) != 0)
       return sct::fail(SCT_E_RANGE, "inconsistent SPECTRAL counts (bin %d not integral)", d);
     __int128 h = s >> 32;

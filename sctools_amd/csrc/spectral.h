@@ -12,7 +12,37 @@ namespace sct_spectral {
 constexpr int kSpaceBits = 32;                 // 16 bases: codes are points of Z_2^32
 constexpr int kLoBits = 14;                    // element index inside a slice (one LDS tile)
 constexpr int kSlices = 1 << (kSpaceBits - kLoBits);  // work items: z >> 14
-constexpr int kNCounts = 1 + 17;               // [n, S_0..S_16]
+// SPECTRAL counts: [n, sum f^2, then S_w (w = 0..16) as three limbs summed separately]:
+//   counts[kLimb0 + w] += bits 0..31, counts[kLimb1 + w] += bits 32..63 and
+//   counts[kLimb2 + w] += bits 64.. of every partial sum a workgroup adds, so no limb
+//   ever carries (each add is < 2^32 or small) and S_w = l0 + 2^32 l1 + 2^64 l2 stays exact
+//   for any multiset (sum_w S_w = 2^32 sum f^2 can exceed 2^64), also after an int64
+//   all-reduce of the counts over ranks.  sum f^2 (the ordered pairs of equal codes, self
+//   pairs included) is computed independently from the sorted codes, so the host checks
+//   sum_w S_w == 2^32 sum f^2 exactly.
+constexpr int kNCounts = 2 + 3 * 17;
+constexpr int kLimb0 = 2, kLimb1 = kLimb0 + 17, kLimb2 = kLimb1 + 17;
+
+// counts[limbs of S_w] += lo + 2^32 hi (lo, hi: LDS partial sums of 32-bit pieces, or a 64-bit
+// value split as lo = v & 0xFFFFFFFF, hi = v >> 32; lo < 2^63, hi < 2^63)
+__device__ __forceinline__ void add_weight_sum(unsigned long long* counts, int w, unsigned long long lo,
+                                               unsigned long long hi) {
+  const unsigned long long b = hi + (lo >> 32);
+  if (lo & 0xFFFFFFFFull) atomicAdd(counts + kLimb0 + w, lo & 0xFFFFFFFFull);
+  if (b & 0xFFFFFFFFull) atomicAdd(counts + kLimb1 + w, b & 0xFFFFFFFFull);
+  if (b >> 32) atomicAdd(counts + kLimb2 + w, b >> 32);
+}
+__device__ __forceinline__ void add_weight_sum64(unsigned long long* counts, int w, unsigned long long v) {
+  add_weight_sum(counts, w, v & 0xFFFFFFFFull, v >> 32);
+}
+// the job's constants, once (by the launch holding slice 0): n and sum f^2
+__device__ __forceinline__ void add_job_constants(unsigned long long* counts, unsigned long long add_n,
+                                                  const unsigned long long* sumsq) {
+  if (add_n && blockIdx.x == 0 && threadIdx.x == 0) {
+    atomicAdd(counts, add_n);
+    atomicAdd(counts + 1, *sumsq);
+  }
+}
 
 // non-zero 2-bit digits of z
 __device__ __forceinline__ int digit_weight(uint32_t z) {
@@ -56,6 +86,7 @@ struct State {
   uint16_t* d_order = nullptr;   // [2^17]: at [L, 2L) the offsets [0, L) sorted by digit weight
   int tile_wgs = 2;              // resident register-tile workgroups per CU
   void* d_buf = nullptr;         // chunk slices x 2^14 seed values
+  size_t buf_bytes = 0;
   int64_t chunk = 0;             // slices per pass
   int grid = 0;                  // compute units (the tile kernel's persistent grid)
   sct::LaunchTimer* timer = nullptr;  // the plan's (bench aid), not owned
@@ -64,7 +95,15 @@ struct State {
   // columns with int8 seeds; the plan's items stay 2^18 virtual slices (4 per real slice)
   int lo_bits = 14;
   int64_t chunk16 = 0;           // real 16-bit slices per pass
+  // sum f^2 of the plan's codes (device word), computed by the plan's first build
+  unsigned long long* d_sumsq = nullptr;
+  bool sumsq_ready = false;
+  void* d_sumsq_tmp = nullptr;   // sort scratch when the intermediate is too small to lend it
 };
+
+// d_sumsq = sum over distinct codes of multiplicity^2 (radix sort of the low 32 bits + a
+// lower-bound pass), once per plan, on stream s (the intermediate d_buf is the scratch)
+int ensure_sumsq(State& st, const uint64_t* d_codes, hipStream_t s);
 
 constexpr int kLoBits16 = 16;
 constexpr int kSlices16 = 1 << (kSpaceBits - kLoBits16);

@@ -15,13 +15,16 @@
 //   tile   reads a slice back, transforms it over the 14 column bits (int8 seeds: two
 //          64-point stages on the matrix cores + Parseval for the top digit), F^2 binned
 //          by digit weight; writes nothing
-// 8 GB of HBM traffic per job at int8, whatever n is.  Exact: |F| <= n < 2^31 in int32,
-// F^2 and S_w in uint64 (S_w <= 2^32 sum f^2).
+// 8 GB of HBM traffic per job at int8, whatever n is.  Exact: |F| <= n <= 1e8 in int32,
+// F^2 in uint64, S_w in three non-carrying limbs (spectral.h: sum_w S_w = 2^32 sum f^2 exceeds
+// 2^64 for multisets with sum f^2 >= 2^32).
 #include <string.h>
 
 #include <algorithm>
 #include <vector>
 #include <type_traits>
+
+#include <hipcub/hipcub.hpp>
 
 #include "sct_common.h"
 #include "spectral.h"
@@ -583,9 +586,12 @@ __device__ __forceinline__ void lane_butterfly16(int32_t& a, int32_t& b) {
   b = (int32_t)(r[0] - r[1]);
 }
 
-// int16 / int32 seeds (columns of more than 127 codes, e.g. config 5): per slice the WHT over
-// the 14 column bits on the VALU, then S_w += F^2 by digit weight.  Persistent: workgroups
-// stride over the chunk's slices; 17 global atomics per workgroup.
+// int16 / int32 seeds (columns of more than 127 codes: dense sets and multisets with heavy
+// duplicates): per slice the WHT over the 14 column bits on the VALU, then S_w += F^2 by digit
+// weight.  Persistent: workgroups stride over the chunk's slices.  Here sum_w S_w = 2^32 sum f^2
+// can exceed 2^64, so every lane's per-slice sum (64 squares < 2^54 each: n <= 1e8) goes to the
+// LDS bins as its two 32-bit halves (bins_lo / bins_hi never carry: < 2^26 adds each) and the
+// bins to the counts' three limbs (add_weight_sum).
 //   phase 1  registers q = e bits 0..3 + 16 * (12, 13); thread = e bits 4..11
 //   phase 2  registers q = e bits 4..9;  lane = e bits 0..3, 10, 11; wave = e bits 12, 13
 //   phase 3  lane bits 5, 4 (e 11, 10) by permlane swaps against q bits 1, 0 (e 5, 4):
@@ -594,13 +600,14 @@ __device__ __forceinline__ void lane_butterfly16(int32_t& a, int32_t& b) {
 template <typename T>
 __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, int z0, int nslices,
                                                    unsigned long long* __restrict__ counts,
-                                                   unsigned long long add_n = 0) {
+                                                   unsigned long long add_n,
+                                                   const unsigned long long* __restrict__ sumsq) {
   static_assert(sizeof(T) >= 2, "int8 seeds take tile_reg_kernel");
   __shared__ int32_t lds[kLo];
-  __shared__ unsigned long long bins[17];
+  __shared__ unsigned long long bins_lo[17], bins_hi[17];
   constexpr int V = Chunk<T>::kVals, L = Chunk<T>::kLog;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid < 17) bins[tid] = 0;
+  if (tid < 17) bins_lo[tid] = bins_hi[tid] = 0;
   const int t2 = (lane & 15) | ((lane >> 4) << 10) | (wave << 12);  // phase-2 e base
   const int wt_thread = digit_weight((uint32_t)lane | ((uint32_t)wave << 12));
   for (int s = blockIdx.x; s < nslices; s += gridDim.x) {
@@ -637,12 +644,14 @@ __global__ __launch_bounds__(256) void tile_kernel(const T* __restrict__ buf, in
           (unsigned long long)((int64_t)x[q] * x[q]);
     const int w0 = digit_weight((uint32_t)(z0 + s)) + wt_thread;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (acc[k]) atomicAdd(&bins[w0 + k], acc[k]);
+    for (int k = 0; k < 4; ++k) {
+      if (acc[k] & 0xFFFFFFFFull) atomicAdd(&bins_lo[w0 + k], acc[k] & 0xFFFFFFFFull);
+      if (acc[k] >> 32) atomicAdd(&bins_hi[w0 + k], acc[k] >> 32);
+    }
   }
   __syncthreads();
-  if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
-  if (add_n && blockIdx.x == 0 && tid == 0) atomicAdd(counts, add_n);  // n, once per job
+  if (tid < 17) add_weight_sum(counts, tid, bins_lo[tid], bins_hi[tid]);
+  add_job_constants(counts, add_n, sumsq);
 }
 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
@@ -683,7 +692,9 @@ __device__ __forceinline__ v2l_t pack_v2l(const uint32_t* w) {
 // weight, so the run's weight changes rarely and F^2 is binned in registers) or u.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tile_reg_kernel(
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+    unsigned long long* __restrict__ counts, unsigned long long add_n, const unsigned long long* __restrict__ sumsq) {
+  // int8 seeds: every column holds <= 127 codes, so sum_w S_w = 2^32 sum f^2 <= 2^32 * 2^14 * 127^2
+  // < 2^62 and 64-bit register / LDS sums cannot wrap
   __shared__ unsigned long long bins[17];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < 17) bins[tid] = 0;
@@ -835,8 +846,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
   }
   if (cur_w >= 0) flush();
   __syncthreads();
-  if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
-  if (add_n && blockIdx.x == 0 && tid == 0) atomicAdd(counts, add_n);  // n, once per job
+  if (tid < 17) add_weight_sum64(counts, tid, bins[tid]);
+  add_job_constants(counts, add_n, sumsq);
+}
+
+// sum f^2 (ensure_sumsq): SPECTRAL codes are < 2^32, so the low 32 bits are the code
+__global__ void low32_kernel(const uint64_t* __restrict__ codes, int64_t n, uint32_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (uint32_t)codes[i];
+}
+
+// sorted codes: sum over i of 2 r_i + 1, r_i = #{j < i : key j = key i} (a code of multiplicity f
+// adds 1 + 3 + ... + 2f - 1 = f^2); r_i by a lower-bound search when the left neighbour is equal
+__global__ __launch_bounds__(256) void sumsq_kernel(const uint32_t* __restrict__ sorted, int64_t n,
+                                                    unsigned long long* __restrict__ out) {
+  unsigned long long acc = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = sorted[i];
+    int64_t r = 0;
+    if (i > 0 && sorted[i - 1] == v) {
+      int64_t a = 0, b = i - 1;  // first index holding v lies in [a, b]
+      while (a < b) {
+        const int64_t m = (a + b) >> 1;
+        if (sorted[m] < v) a = m + 1;
+        else b = m;
+      }
+      r = i - a;
+    }
+    acc += 2 * (unsigned long long)r + 1;
+  }
+#pragma unroll
+  for (int s = 32; s; s >>= 1) acc += __shfl_xor(acc, s);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
 
 __global__ void max_column_kernel(const uint32_t* __restrict__ cnt, unsigned* __restrict__ out) {
@@ -873,10 +914,12 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
     const int ns = z1 - z0;
     const uint16_t* order = ((ns & (ns - 1)) == 0 && z0 % ns == 0) ? st.d_order + std::min(ns, kMaxOrder) : nullptr;
     const dim3 rgrid((unsigned)std::max(1, std::min(st.grid * st.tile_wgs, (z1 - z0 + 3) / 4)));
-    hipLaunchKernelGGL(tile_reg_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n);
+    hipLaunchKernelGGL(tile_reg_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n,
+                       (const unsigned long long*)st.d_sumsq);
   } else {
     const dim3 grid((unsigned)std::min(st.grid * 2, z1 - z0));
-    hipLaunchKernelGGL(tile_kernel<T>, grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, add_n);
+    hipLaunchKernelGGL(tile_kernel<T>, grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, add_n,
+                       (const unsigned long long*)st.d_sumsq);
   }
   SCT_LAUNCH_CHECK();
   return SCT_OK;
@@ -995,20 +1038,48 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   SCT_HIP(hipMalloc(&st.d_gofs, (size_t)(kLo + 1) * 4));
   SCT_HIP(hipMalloc(&st.d_hist, (size_t)kSortWGs * kLo * 4));
   SCT_HIP(hipMalloc(&st.d_planes, (size_t)st.max_groups * kPlaneWords * 4));
-  const size_t buf_bytes = (size_t)((st.chunk + 15) & ~15ll) * kLo * st.elem_bytes;  // whole 16-slice groups
-  SCT_HIP(hipMalloc(&st.d_buf, buf_bytes));
+  st.buf_bytes = (size_t)((st.chunk + 15) & ~15ll) * kLo * st.elem_bytes;  // whole 16-slice groups
+  SCT_HIP(hipMalloc(&st.d_buf, st.buf_bytes));
+  SCT_HIP(hipMalloc(&st.d_sumsq, sizeof(unsigned long long)));
   return SCT_OK;
 }
 
 void destroy(State& st) {
   for (void* p : {(void*)st.d_hi, (void*)st.d_off, (void*)st.d_cnt, (void*)st.d_gofs, (void*)st.d_planes,
-                  (void*)st.d_hist, st.d_buf, (void*)st.d_order})
+                  (void*)st.d_hist, st.d_buf, (void*)st.d_order, (void*)st.d_sumsq, st.d_sumsq_tmp})
     if (p) (void)hipFree(p);
   st = State();
 }
 
+int ensure_sumsq(State& st, const uint64_t* d_codes, hipStream_t s) {
+  if (st.sumsq_ready) return SCT_OK;
+  // scratch: low 32 bits (4n), sorted (4n), radix-sort temp
+  size_t tmp = 0;
+  SCT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)st.n, 0,
+                                            32, s));
+  const size_t keys = ((size_t)st.n * 4 + 255) & ~(size_t)255;
+  const size_t need = 2 * keys + tmp;
+  char* base = reinterpret_cast<char*>(st.d_buf);
+  if (need > st.buf_bytes) {  // a small test chunk: scratch of its own, kept for the plan's life
+    SCT_HIP(hipMalloc(&st.d_sumsq_tmp, need));
+    base = reinterpret_cast<char*>(st.d_sumsq_tmp);
+  }
+  uint32_t* k0 = reinterpret_cast<uint32_t*>(base);
+  uint32_t* k1 = reinterpret_cast<uint32_t*>(base + keys);
+  const int blocks = (int)std::min<int64_t>(2048, sct::ceil_div(st.n, 256));
+  hipLaunchKernelGGL(low32_kernel, dim3(blocks), dim3(256), 0, s, d_codes, st.n, k0);
+  SCT_LAUNCH_CHECK();
+  SCT_HIP(hipcub::DeviceRadixSort::SortKeys(base + 2 * keys, tmp, k0, k1, (int)st.n, 0, 32, s));
+  SCT_HIP(hipMemsetAsync(st.d_sumsq, 0, sizeof(unsigned long long), s));
+  hipLaunchKernelGGL(sumsq_kernel, dim3(blocks), dim3(256), 0, s, k1, st.n, st.d_sumsq);
+  SCT_LAUNCH_CHECK();
+  st.sumsq_ready = true;
+  return SCT_OK;
+}
+
 int build(State& st, const uint64_t* d_codes, hipStream_t s) {
   if (st.n < 2) return SCT_OK;
+  if (int rc = ensure_sumsq(st, d_codes, s); rc != SCT_OK) return rc;
   if (st.lo_bits == kLoBits16) return build16(st, d_codes, s);
   hipEvent_t t0 = st.timer ? st.timer->start(s) : nullptr;
   hipLaunchKernelGGL(column_hist_wg_kernel, dim3(kSortWGs), dim3(kSortThreads), 0, s, d_codes, st.n, st.d_hist);

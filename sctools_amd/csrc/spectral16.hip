@@ -355,7 +355,9 @@ constexpr int kUWords = 4 * 4 * 4 * 64;
 // q2 = 0 tile starts from -2016 there (-2016 * 256 = -516096).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tile16_kernel(
     const int8_t* __restrict__ buf, const uint16_t* __restrict__ order, int z0, int nslices,
-    unsigned long long* __restrict__ counts, unsigned long long add_n) {
+    unsigned long long* __restrict__ counts, unsigned long long add_n, const unsigned long long* __restrict__ sumsq) {
+  // every 16-bit column holds <= 127 codes: sum_w S_w = 2^32 sum f^2 <= 2^32 * 2^16 * 127^2 < 2^62,
+  // so the 64-bit register / LDS sums cannot wrap
   __shared__ unsigned long long U[kUWords];
   __shared__ unsigned long long bins[17];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;  // wave = S (column digit 7)
@@ -578,8 +580,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   }
   if (cur_w >= 0) flush();
   __syncthreads();
-  if (tid < 17 && bins[tid]) atomicAdd(counts + 1 + tid, bins[tid]);
-  if (add_n && blockIdx.x == 0 && tid == 0) atomicAdd(counts, add_n);  // n, once per job
+  if (tid < 17) add_weight_sum64(counts, tid, bins[tid]);
+  add_job_constants(counts, add_n, sumsq);
 }
 
 void launch_seed16(State& st, int8_t* buf, int z0, int z1, hipStream_t s) {
@@ -598,7 +600,7 @@ void launch_tile16(State& st, const int8_t* buf, int z0, int z1, unsigned long l
   const int ns = z1 - z0;
   const uint16_t* order = ((ns & (ns - 1)) == 0 && ns <= (1 << 16) && z0 % ns == 0) ? st.d_order + ns : nullptr;
   hipLaunchKernelGGL(tile16_kernel, dim3((unsigned)std::max(1, std::min(st.grid * wgs_per_cu, ns))), dim3(256), 0, s,
-                     buf, order, z0, ns, counts, add_n);
+                     buf, order, z0, ns, counts, add_n, (const unsigned long long*)st.d_sumsq);
 }
 
 int launch_chunk16(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s, unsigned long long add_n) {
@@ -638,7 +640,9 @@ int create16(State& st, const uint64_t* d_codes, int64_t n, unsigned max16, int6
   SCT_HIP(hipMalloc(&st.d_gofs, (size_t)(kLo16 + 1) * 4));
   SCT_HIP(hipMalloc(&st.d_hist, (size_t)kSortWGs16 * kLo16));
   SCT_HIP(hipMalloc(&st.d_planes, (size_t)st.max_groups * kPW16 * 4));
-  SCT_HIP(hipMalloc(&st.d_buf, (size_t)st.chunk16 * kLo16));
+  st.buf_bytes = (size_t)st.chunk16 * kLo16;
+  SCT_HIP(hipMalloc(&st.d_buf, st.buf_bytes));
+  SCT_HIP(hipMalloc(&st.d_sumsq, sizeof(unsigned long long)));
   return SCT_OK;
 }
 
@@ -694,7 +698,7 @@ int time_kernels16(State& st, int64_t z_begin, int64_t z_end, unsigned long long
   SCT_HIP(hipEventRecord(e[1], s));
   for (int r = 0; rc == SCT_OK && r < repeats; ++r)
     hipLaunchKernelGGL(tile16_kernel, dim3((unsigned)std::max(1, std::min(st.grid * st.tile_wgs, ns))), dim3(256), 0,
-                       s, buf, order, (int)rb, ns, d_counts, 0ull);
+                       s, buf, order, (int)rb, ns, d_counts, 0ull, (const unsigned long long*)st.d_sumsq);
   SCT_HIP(hipEventRecord(e[2], s));
   st.timer = keep;
   if (rc != SCT_OK) return rc;

@@ -60,6 +60,18 @@ def test_all_negative_keys_keep_every_pairwise_xor(keys):
             assert O.two_bit_hamming(vals[i], vals[j]) == O.two_bit_hamming(keys[i], keys[j])
 
 
+@pytest.mark.parametrize("keys", [[-3, -7, -12], [-(2 ** 70), -5], [-1]])
+def test_nearest_rejects_negative_keys(keys):
+    """Barcodes.nearest compares the set's codes with OUTSIDE queries, where the pairwise
+    masking of all-negative keys would give plausible but wrong matches: any
+    negative key raises ValueError before a device call, while the pairwise codes of the
+    same set stay available to the summary."""
+    b = barcode.Barcodes({k: 1 for k in keys}, 16)
+    with pytest.raises(ValueError, match="non-negative"):
+        b.nearest(np.array([0, 5], dtype=np.uint64))
+    assert len(b.codes_array()) == len(keys)
+
+
 def test_base4_entropy_golden(golden):
     """stats.base4_entropy on the reference's own base counts reproduces the
     effective_diversity the reference computed from them, bit for bit."""

@@ -82,7 +82,7 @@ def _worker_737k(rank, world, port, out_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_config3_737k_ranks_bin_for_bin(tmp_path, world):
     """Config 3 (BASELINE.json): the 737,280-code all-pairs histogram sharded by transform
     slices over W gloo ranks sharing the box's GPU, every rank's histogram bin for bin

@@ -376,7 +376,7 @@ def _spectral_hist(codes, ranges=None, chunk=None):
     with _lib.tuning(spectral_chunk=chunk):
         plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=_lib.SCHEME_SPECTRAL)
     try:
-        assert plan.scheme == _lib.SCHEME_SPECTRAL and plan.ncounts == 18
+        assert plan.scheme == _lib.SCHEME_SPECTRAL and plan.ncounts == 53
         assert plan.items == (1 << 18 if codes.size >= 2 else 0)
         counts = torch.zeros(plan.ncounts, dtype=torch.int64, device="cuda")
         items = plan.items
@@ -500,6 +500,51 @@ def test_allpairs_spectral_is_auto_for_large_whitelists():
     hm = mom.counts_to_hist(counts.cpu().numpy().view(np.uint64))
     mom.close()
     assert hs.tolist() == hm.tolist()
+
+
+def _heavy_multiset(case):
+    """Observed-barcode multisets whose sum f^2 exceeds 2^32 (so sum_w S_w = 2^32 sum f^2
+    exceeds 2^64): shuffled, with the seed width they force."""
+    rng = np.random.default_rng({"one_heavy": 1, "zipf": 2, "int16_heavy": 3}[case])
+    if case == "one_heavy":  # 330K unique codes + one of them 70K times more (int32 seeds)
+        wl = synthetic.whitelist_codes(330_000, 16, seed=41)
+        codes, width = np.concatenate([wl, np.full(70_000, wl[12345], dtype=np.uint64)]), 4
+    elif case == "zipf":  # 400K cells, multiplicity ~ 80000 / rank^1.3 (int32 seeds)
+        wl = synthetic.whitelist_codes(400_000, 16, seed=42)
+        rng.shuffle(wl)
+        f = np.maximum(1, (80_000 / np.arange(1, wl.size + 1) ** 1.3).astype(np.int64))
+        codes, width = np.repeat(wl, f), 4
+    else:  # 8 codes x 30,000 in 8 columns (<= 32,767 codes each: int16 seeds) + 400K unique
+        wl = synthetic.whitelist_codes(400_008, 16, seed=43)
+        codes, width = np.concatenate([wl, np.repeat(wl[:8], 29_999)]), 2
+    rng.shuffle(codes)
+    _, f = np.unique(codes, return_counts=True)
+    assert int((f.astype(np.int64) ** 2).sum()) >= 1 << 32
+    return codes, width
+
+
+@pytest.mark.parametrize("case", ["one_heavy", "zipf", "int16_heavy"])
+def test_allpairs_spectral_heavy_multisets_bin_for_bin(case):
+    """SPECTRAL on multisets with sum f^2 >= 2^32: the weight sums exceed
+    2^64 in total, so the device accumulates them in non-carrying limbs and the host checks
+    sum_w S_w == 2^32 sum f^2 against the sorted-code count.  Forced SPECTRAL over two slice
+    ranges, AUTO through the one-shot host entry point, and the product's sharded driver, each
+    bin for bin against the C oracle's pair loop (encodings.py:113-121: equal codes are
+    distance 0)."""
+    torch = pytest.importorskip("torch")
+    codes, width = _heavy_multiset(case)
+    ref, _ = O.c_hist16(codes)
+    ref = ref[:17].tolist()
+    d_codes = torch.from_numpy(codes.view(np.int64)).cuda()
+    plan = _lib.AllPairsPlan(d_codes.data_ptr(), codes.size, 32, scheme=_lib.SCHEME_SPECTRAL)
+    try:
+        assert plan.spectral_info()["elem_bytes"] == width
+    finally:
+        plan.close()
+    assert _spectral_hist(codes, [(0, 70_001), (70_001, 1 << 18)]).astype(np.int64).tolist() == ref
+    assert codes.size >= 325_000  # AUTO = SPECTRAL
+    assert _lib.hamming_hist_allpairs(codes, 32).astype(np.int64).tolist() == ref
+    assert sharding.allpairs_histogram_sharded(codes, 32).astype(np.int64).tolist() == ref
 
 
 # ---------------------------------------------------------------- nearest whitelist

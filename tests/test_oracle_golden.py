@@ -201,7 +201,11 @@ def test_spectral_identity_small_space(seed):
         got.append((N - (n if d == 0 else 0)) // 2)
     assert got == _pair_hist_digits(codes, G)
     # and the forward map the tests use gives the same S
-    assert O.spectral_counts_from_hist(got, n).tolist() == [n] + S
+    assert O.spectral_weight_sums(got, n) == S
+    c = O.spectral_counts_from_hist(got, n)
+    assert c[0] == n and int(c[1]) == 2 * got[0] + n
+    W = G + 1
+    assert [int(c[2 + w]) + (int(c[2 + W + w]) << 32) + (int(c[2 + 2 * W + w]) << 64) for w in range(W)] == S
 
 
 def test_spectral_counts_invert_on_reference_histograms(golden, golden_10k):
@@ -220,7 +224,10 @@ def test_spectral_rejects_inconsistent_counts():
     hist = [0, 0, 0, 1, 0, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0]  # 3 codes
     c = O.spectral_counts_from_hist(hist, 3)
     assert _lib.counts_to_hist(c, _lib.SCHEME_SPECTRAL).tolist() == hist
-    for i, delta in ((4, 1), (0, 1), (17, 1 << 32)):
+    # S_2 + 1; n + 1 (S_0 != n^2); S_15 + 2^32; sum f^2 + 1; S_3 + 2^64 (what a 2^64 wrap of one
+    # weight sum would do: every Krawtchouk bin stays integral and even, only the check
+    # sum_w S_w == 2^32 sum f^2 sees it)
+    for i, delta in ((4, 1), (0, 1), (17, 1 << 32), (1, 1), (39, 1)):
         bad = c.copy()
         bad[i] += np.uint64(delta)
         with pytest.raises(ValueError):

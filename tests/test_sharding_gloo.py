@@ -130,9 +130,9 @@ def _worker_spectral(rank, world, port, n, seed, out_path):
     try:
         codes = synthetic.whitelist_codes(n, 16, seed)
         full = O.spectral_counts_from_hist(O.c_hist_rows(codes)[:17], n).astype(object)
-        share = [int(x) * (rank + 1) // world - int(x) * rank // world for x in full[1:]]
+        share = [int(x) * (rank + 1) // world - int(x) * rank // world for x in full[2:]]
         b, _ = sharding.item_range(1 << 18, rank, world)
-        counts = torch.tensor([n if b == 0 else 0] + share, dtype=torch.int64)
+        counts = torch.tensor([n if b == 0 else 0, int(full[1]) if b == 0 else 0] + share, dtype=torch.int64)
         hist = sharding.combine_counts(counts, None, _lib.SCHEME_SPECTRAL, 17)
         np.save(out_path % rank, hist.astype(np.int64))
     finally:

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu --durations=25 \
   ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; [ $rc -gt 1 ] && exit $rc
+rc=$?; echo "pytest rc=$rc"; [ $rc -ne 0 ] && exit $rc
 if [ "${PROFILE:-1}" = "1" ]; then
   bash tools/gpu_profile_r3.sh || exit $?
   python tools/summarize_profile.py --round r03 > gpurun_out/summarize.log 2>&1 || exit 4
