@@ -601,6 +601,51 @@ def path_whitelist(dev, reps, copy_gbs):
                 "check": {"vs_oracle": ok_bf, "sample": "the whole table vs oracle.base_frequency_numpy"}}}
 
 
+def path_dropin(dev, reps, want_summary):
+    """The drop-in call itself, as a reference user makes it: Barcodes(dict of the 737,280
+    config-2 codes).summarize_hamming_distances() (barcode.py:39-46), host dict in, summary dict
+    out -- the key conversion, the H2D copy, the plan (probe, build, count: SPECTRAL) on the
+    device's cached workspace, the exact inversion and the numpy-exact summary, wall-clock per
+    call after one warm call; and the same call split into its host and device parts."""
+    import torch
+    from sctools_amd import _lib, barcode, synthetic
+    n, L, seed = synthetic.CONFIGS[2]
+    codes = synthetic.whitelist_codes(n, L, seed)
+    b = barcode.Barcodes(dict.fromkeys((int(c) for c in codes), 1), L)
+    first = b.summarize_hamming_distances()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        r = b.summarize_hamming_distances()
+        ts.append((time.perf_counter() - t) * 1e3)
+    parts = {"codes_array_ms": [], "hist_call_ms": [], "summary_ms": []}
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        arr = b.codes_array()
+        t1 = time.perf_counter()
+        h = _lib.hamming_hist_allpairs(arr, 2 * L, distinct=True)  # as hamming_histogram() calls it
+        t2 = time.perf_counter()
+        _lib.summary_from_hist(h)
+        t3 = time.perf_counter()
+        parts["codes_array_ms"].append((t1 - t0) * 1e3)
+        parts["hist_call_ms"].append((t2 - t1) * 1e3)
+        parts["summary_ms"].append((t3 - t2) * 1e3)
+    med = lambda v: float(sorted(v)[len(v) // 2])  # noqa: E731
+    ms = med(ts)
+    P = n * (n - 1) // 2
+    got = [float(r[k]) for k in ("minimum", "25th percentile", "median", "75th percentile", "maximum", "average")]
+    return {"workload": "Barcodes(dict of the %d config-2 codes, L=%d).summarize_hamming_distances(): host keys in, "
+                        "summary dict out, one call at a time" % (n, L),
+            "value": P / (ms * 1e-3), "unit": "pair-equivalents/s", "ms": ms, "ms_all": ts, "reps": reps,
+            "breakdown_ms": {k: med(v) for k, v in parts.items()},
+            "note": "hist_call = sct_hamming_hist_allpairs_host: H2D of the codes, plan on the cached workspace "
+                    "(probe + one sync), build, count (SPECTRAL), D2H, exact inversion; codes_array = the "
+                    "mapping's keys -> uint64 with the reference's type semantics (host)",
+            "check": {"summary_equals_headline": got == [float(x) for x in want_summary]
+                      and [float(first[k]) for k in first] == got}}
+
+
 def _guarded(fn, *a):
     """A side path that fails reports its error in the line instead of ending the bench."""
     try:
@@ -825,6 +870,8 @@ def run_rank(args, rank, world, local):
                             "fastq_ingest": _guarded(path_fastq, dev, max(2, args.path_steps), copy_gbs)}
             wl = _guarded(path_whitelist, dev, max(5, args.path_steps), copy_gbs)
             out["paths"].update(wl if "error" not in wl else {"whitelist_ingest": wl})
+            if args.config == 2:
+                out["paths"]["dropin_summary_737k"] = _guarded(path_dropin, dev, max(5, args.path_steps), summ)
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(codes, hist, args.cpu_seconds)
     if rank == 0:

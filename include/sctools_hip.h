@@ -51,7 +51,8 @@ int sct_set_device(int device);        /* select the device for later calls (hip
 #define SCT_TUNE_SCALAR_SERVER 8        /* 0: every scalar call is a kernel launch (default 1) */
 #define SCT_TUNE_SCALAR_IDLE_MS 9       /* the scalar server exits after this idle time (5) */
 #define SCT_TUNE_SPECTRAL_COLUMNS 10   /* SPECTRAL column width: 0 auto, 14, or 16 (when int8 fits) */
-#define SCT_TUNE_NKEYS 11
+#define SCT_TUNE_PLAN_CACHE 11          /* 0: every all-pairs plan allocates its own buffers (default 1) */
+#define SCT_TUNE_NKEYS 12
 int sct_tune_set(int key, int64_t value);
 int sct_tune_get(int key, int64_t* value);  /* -1 when unset */
 
@@ -203,11 +204,21 @@ typedef struct sct_allpairs_plan sct_allpairs_plan;
 #define SCT_ALLPAIRS_MOMENTS 1
 #define SCT_ALLPAIRS_SPECTRAL 2
 
+/* Plan flags (sct_allpairs_plan_create_ex2):
+ * SCT_ALLPAIRS_DISTINCT  the caller promises pairwise-distinct codes (the keys of a mapping, as
+ *   Barcodes.summarize_hamming_distances has them, barcode.py:39-46), so SPECTRAL takes
+ *   sum f^2 = n instead of sorting the codes; a broken promise fails the host's exact check
+ *   (SCT_E_RANGE), it never yields a histogram. */
+#define SCT_ALLPAIRS_DISTINCT 1
+
 /* = sct_allpairs_plan_create_ex(..., SCT_ALLPAIRS_AUTO, plan) */
 int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int code_bits,
                              sct_allpairs_plan** plan);
 int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, int code_bits, int scheme,
                                 sct_allpairs_plan** plan);
+/* = sct_allpairs_plan_create_ex with SCT_ALLPAIRS_* flags */
+int sct_allpairs_plan_create_ex2(const uint64_t* d_codes, int64_t n, int code_bits, int scheme, int flags,
+                                 sct_allpairs_plan** plan);
 int sct_allpairs_plan_destroy(sct_allpairs_plan* plan);
 /* nbins = max distance + 1 = 2*ceil(code_bits/4)+1; items = number of work items */
 int sct_allpairs_plan_info(const sct_allpairs_plan* plan, int* nbins, int64_t* items,
@@ -279,6 +290,17 @@ int sct_counts_to_hist_ex(int scheme, const uint64_t* counts, int ncounts, uint6
  * unordered pairs of the n codes.  hist must hold nbins = 2*ceil(code_bits/4)+1. */
 int sct_hamming_hist_allpairs_host(const uint64_t* codes, int64_t n, int code_bits,
                                    uint64_t* hist, int nbins);
+/* the same with SCT_ALLPAIRS_* plan flags */
+int sct_hamming_hist_allpairs_host_ex(const uint64_t* codes, int64_t n, int code_bits, int flags,
+                                      uint64_t* hist, int nbins);
+
+/* Plan cache: a plan created while no other plan holds its device's cached buffers borrows
+ * them (the SPECTRAL intermediate of up to 4 GiB, codes, bit planes, order table) and leaves
+ * them allocated when destroyed, so repeated one-shot calls map no device memory (the
+ * drop-in's summarize_hamming_distances, barcode.py:39-46, is one such call).  This frees
+ * every idle cache (all devices); a cache lent to a live plan is freed when that plan is
+ * destroyed.  sct_tune_set(SCT_TUNE_PLAN_CACHE, 0) turns the cache off. */
+int sct_allpairs_cache_release(void);
 
 /* ---------------------------------------------------------------- all-pairs, wide codes
  * The same pair loop (barcode.py:42-43) for keys of any width up to 256 limbs: codes are

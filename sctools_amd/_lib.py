@@ -31,7 +31,7 @@ SCHEME_SPECTRAL = 2
 # launch-shape knobs (sct_tune_set; none changes a result)
 TUNE_KEYS = {"spectral_chunk": 1, "spectral_min_n": 2, "allpairs_grab": 3, "allpairs_flush_items": 4,
              "allpairs_grid": 5, "nearest_scheme": 6, "nearest_load": 7, "scalar_server": 8,
-             "scalar_idle_ms": 9, "spectral_columns": 10}
+             "scalar_idle_ms": 9, "spectral_columns": 10, "plan_cache": 11}
 NEAREST_AUTO, NEAREST_OA, NEAREST_CSR, NEAREST_HALVES = 0, 1, 2, 3
 
 _i32, _i64, _dbl = ctypes.c_int, ctypes.c_int64, ctypes.c_double
@@ -81,6 +81,9 @@ SIGNATURES = {
     "sct_counts_to_hist": [_vp, _i32, _vp],
     "sct_counts_to_hist_ex": [_i32, _vp, _i32, _vp, _i32],
     "sct_hamming_hist_allpairs_host": [_vp, _i64, _i32, _vp, _i32],
+    "sct_hamming_hist_allpairs_host_ex": [_vp, _i64, _i32, _i32, _vp, _i32],
+    "sct_allpairs_plan_create_ex2": [_vp, _i64, _i32, _i32, _i32, ctypes.POINTER(_vp)],
+    "sct_allpairs_cache_release": [],
     "sct_summary_from_hist": [_vp, _i32, _vp],
     "sct_allpairs_wide_geometry": [_i64, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_i32)],
     "sct_allpairs_wide_range_pairs": [_i64, _i64, _i64, ctypes.POINTER(_i64)],
@@ -370,16 +373,28 @@ def nbins_for_bits(code_bits):
     return 2 * ((max(1, int(code_bits)) + 3) // 4) + 1
 
 
-def hamming_hist_allpairs(codes, code_bits=None):
-    """Histogram (uint64[nbins]) of TwoBit distances over all unordered pairs of codes."""
+ALLPAIRS_DISTINCT = 1  # plan flag: the caller promises pairwise-distinct codes
+
+
+def hamming_hist_allpairs(codes, code_bits=None, distinct=False):
+    """Histogram (uint64[nbins]) of TwoBit distances over all unordered pairs of codes.
+    distinct=True promises pairwise-distinct codes (mapping keys): SPECTRAL then skips its
+    sort for sum f^2; a broken promise raises ValueError (the host's exact check), never a
+    wrong histogram."""
     codes = np.ascontiguousarray(codes, dtype=np.uint64).reshape(-1)
-    if code_bits is None:
-        code_bits = int(np.bitwise_or.reduce(codes)).bit_length() if codes.size else 1
+    if code_bits is None:  # bit_length(max) = bit_length(OR) for non-negative codes
+        code_bits = int(codes.max()).bit_length() if codes.size else 1
     code_bits = max(1, code_bits)
     nbins = nbins_for_bits(code_bits)
     hist = np.zeros(nbins, dtype=np.uint64)
-    check(lib().sct_hamming_hist_allpairs_host(_ptr(codes), codes.size, code_bits, _ptr(hist), nbins))
+    check(lib().sct_hamming_hist_allpairs_host_ex(_ptr(codes), codes.size, code_bits,
+                                                  ALLPAIRS_DISTINCT if distinct else 0, _ptr(hist), nbins))
     return hist
+
+
+def release_plan_cache():
+    """Free the device buffers all-pairs plans keep cached between calls (sct_allpairs_cache_release)."""
+    check(lib().sct_allpairs_cache_release())
 
 
 def hamming_hist_allpairs_wide(limbs):
@@ -613,11 +628,11 @@ class AllPairsPlan:
     ``ncounts`` is the length of the uint64 counts vector that ``moments`` and ``count``
     accumulate into; ``counts_to_hist`` inverts the counts of the whole job."""
 
-    def __init__(self, d_codes_ptr, n, code_bits=0, scheme=SCHEME_AUTO):
+    def __init__(self, d_codes_ptr, n, code_bits=0, scheme=SCHEME_AUTO, distinct=False):
         self._lib = lib()
         self._h = _vp()
-        check(self._lib.sct_allpairs_plan_create_ex(_vp(d_codes_ptr), n, code_bits, scheme,
-                                                    ctypes.byref(self._h)))
+        check(self._lib.sct_allpairs_plan_create_ex2(_vp(d_codes_ptr), n, code_bits, scheme,
+                                                     ALLPAIRS_DISTINCT if distinct else 0, ctypes.byref(self._h)))
         nb, items, pairs = _i32(0), _i64(0), _i64(0)
         check(self._lib.sct_allpairs_plan_info(self._h, ctypes.byref(nb), ctypes.byref(items), ctypes.byref(pairs)))
         self.nbins, self.items, self.pairs = nb.value, items.value, pairs.value

@@ -15,7 +15,7 @@ from collections.abc import Mapping
 
 import numpy as np
 
-from . import _lib
+from . import _lib, _pykeys
 from .encodings import TwoBit
 from .stats import base4_entropy
 
@@ -73,22 +73,20 @@ class Barcodes:
         (``nearest``) pass ``mask_negative=False`` and get ValueError for any negative key."""
         keys = self._data.keys()
         n = len(self._data)
+        # the common case (Python-int keys within int64) in one C loop (csrc/pykeys.c): the type
+        # check and the conversion together; every other case takes the general path below
+        arr = np.empty(n, dtype=np.int64)
+        status, got = _pykeys.keys_to_int64(self._data if type(self._data) in (dict, Counter) else keys, arr)
+        if status == 0 and got == n:
+            return self._finish_int64(arr, mask_negative)
         if not all(issubclass(t, (int, np.integer)) for t in set(map(type, keys))):
             # the reference's pair loop dies at its first ``a ^ b`` on a non-integer key
             # (encodings.py:117 via barcode.py:42-43): raise exactly that TypeError
             for a, b in itertools.combinations(self._data, 2):
                 a ^ b
             return np.zeros(n, dtype=np.uint64)  # < 2 keys: no pair, nothing to compare
-        try:  # the common case (every key in int64) on numpy's fastest conversion
-            arr = np.fromiter(keys, dtype=np.int64, count=n)
-            if n and int(arr.min()) < 0:
-                if not mask_negative:
-                    raise ValueError(_NEGATIVE_OUTSIDE)
-                if int(arr.max()) >= 0 and n >= 2:
-                    raise ValueError(_MIXED_SIGNS)
-                m = int((~arr).max()).bit_length()
-                return (arr & np.int64((1 << m) - 1)).view(np.uint64) if m < 63 else arr.view(np.uint64)
-            return arr.view(np.uint64)
+        try:  # numpy integer keys within int64
+            return self._finish_int64(np.fromiter(keys, dtype=np.int64, count=n), mask_negative)
         except OverflowError:
             pass
         if not any(isinstance(k, np.signedinteger) and k < 0 for k in keys):  # (numpy would wrap those)
@@ -107,13 +105,25 @@ class Barcodes:
             ints = [v & mask for v in ints]
         return _lib.ints_to_limbs(ints)
 
+    @staticmethod
+    def _finish_int64(arr, mask_negative):
+        """int64 keys -> the kernels' uint64 codes (negative keys: see codes_array)."""
+        if arr.size and int(arr.min()) < 0:
+            if not mask_negative:
+                raise ValueError(_NEGATIVE_OUTSIDE)
+            if int(arr.max()) >= 0 and arr.size >= 2:
+                raise ValueError(_MIXED_SIGNS)
+            m = int((~arr).max()).bit_length()
+            return (arr & np.int64((1 << m) - 1)).view(np.uint64) if m < 63 else arr.view(np.uint64)
+        return arr.view(np.uint64)
+
     def hamming_histogram(self):
         """np.uint64 histogram H[d] of TwoBit distances over all unordered pairs."""
         codes = self.codes_array()
         if codes.ndim == 2:  # keys >= 2^64: the multi-limb pair kernel
             hist = _lib.hamming_hist_allpairs_wide(codes)
         else:
-            hist = _lib.hamming_hist_allpairs(codes)
+            hist = _lib.hamming_hist_allpairs(codes, distinct=True)  # mapping keys: distinct
         want = (self._barcode_length + 1) if isinstance(self._barcode_length, int) else 0
         if want > hist.size:  # bins up to the barcode length, as np.bincount(minlength=L+1)
             hist = np.concatenate([hist, np.zeros(want - hist.size, dtype=hist.dtype)])

@@ -525,17 +525,6 @@ __global__ __launch_bounds__(256) void allpairs_build_tri_kernel(const uint64_t*
   }
 }
 
-__global__ void or_reduce_kernel(const uint64_t* __restrict__ codes, int64_t n,
-                                 unsigned long long* out) {
-  unsigned long long v = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    v |= codes[i];
-#pragma unroll
-  for (int s = 32; s >= 1; s >>= 1) v |= __shfl_xor(v, s, 64);
-  if ((threadIdx.x & 63) == 0 && v) atomicOr(out, v);
-}
-
 // ---------------------------------------------------------------- agreement moments
 // M_k = #(pair, k-set of positions S) with the pair agreeing on all of S
 //     = sum over pairs of C(16 - d, k) = sum_{|S|=k} sum_{pattern} C(count_S(pattern), 2),
@@ -918,7 +907,13 @@ extern "C" int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int 
 
 extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, int code_bits,
                                            int scheme, sct_allpairs_plan** plan) {
+  return sct_allpairs_plan_create_ex2(d_codes, n, code_bits, scheme, 0, plan);
+}
+
+extern "C" int sct_allpairs_plan_create_ex2(const uint64_t* d_codes, int64_t n, int code_bits, int scheme,
+                                            int flags, sct_allpairs_plan** plan) {
   SCT_CHECK(plan != nullptr, "plan is NULL");
+  SCT_CHECK((flags & ~SCT_ALLPAIRS_DISTINCT) == 0, "unknown plan flags 0x%x", flags);
   SCT_CHECK(scheme == SCT_ALLPAIRS_AUTO || scheme == SCT_ALLPAIRS_SUBSETS ||
                 scheme == SCT_ALLPAIRS_MOMENTS || scheme == SCT_ALLPAIRS_SPECTRAL,
             "unknown scheme %d", scheme);
@@ -935,22 +930,21 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
   hipError_t e = hipGetDevice(&p->device);
   if (e != hipSuccess) return cleanup(sct::fail(SCT_E_HIP, "hipGetDevice: %s", hipGetErrorString(e)));
   p->n = n;
-  unsigned long long orv = 0;
+  // the device's cached buffers (plan cache, spectral.h) when no other plan holds them
+  p->spec.ws = sct_spectral::ws_acquire();
+  // one probe of the codes: their OR (code width) and the densest transform columns (SPECTRAL's
+  // seed width), one synchronisation
+  unsigned long long probe[3] = {0, 0, 0};
   if (n > 0) {
-    e = hipMalloc(&p->d_codes, (size_t)n * 8);
-    if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "hipMalloc codes: %s", hipGetErrorString(e)));
-    e = hipMemcpy(p->d_codes, d_codes, (size_t)n * 8, hipMemcpyDefault);
+    void* dc = nullptr;
+    if (int rc = sct_spectral::ws_get(p->spec.ws, sct_spectral::W_CODES, (size_t)n * 8, &dc); rc != SCT_OK)
+      return cleanup(rc);
+    p->d_codes = reinterpret_cast<uint64_t*>(dc);
+    e = hipMemcpyAsync(p->d_codes, d_codes, (size_t)n * 8, hipMemcpyDefault, 0);
     if (e != hipSuccess) return cleanup(sct::fail(SCT_E_HIP, "copy codes: %s", hipGetErrorString(e)));
-    unsigned long long* d_or = nullptr;
-    e = hipMalloc(&d_or, 8);
-    if (e != hipSuccess) return cleanup(sct::fail(SCT_E_NOMEM, "hipMalloc: %s", hipGetErrorString(e)));
-    (void)hipMemset(d_or, 0, 8);
-    const int blocks = (int)std::min<int64_t>(1024, sct::ceil_div(n, 256));
-    hipLaunchKernelGGL(or_reduce_kernel, dim3(blocks), dim3(256), 0, 0, p->d_codes, n, d_or);
-    e = hipMemcpy(&orv, d_or, 8, hipMemcpyDeviceToHost);
-    (void)hipFree(d_or);
-    if (e != hipSuccess) return cleanup(sct::fail(SCT_E_HIP, "or-reduce: %s", hipGetErrorString(e)));
+    if (int rc = sct_spectral::probe(p->spec.ws, p->d_codes, n, probe); rc != SCT_OK) return cleanup(rc);
   }
+  const unsigned long long orv = probe[0];
   int need = 0;
   while (need < 64 && (orv >> need)) ++need;
   if (code_bits <= 0) code_bits = need;
@@ -978,7 +972,9 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
     // items = the 4096 transform slices; no selection table
     p->ncounts = sct_spectral::kNCounts;
     p->items = n >= 2 ? sct_spectral::kSlices : 0;
-    const int rc = sct_spectral::create(p->spec, p->d_codes, n, sct::tune(SCT_TUNE_SPECTRAL_CHUNK, 262144), cus);
+    p->spec.distinct = (flags & SCT_ALLPAIRS_DISTINCT) != 0;
+    const int rc = sct_spectral::create(p->spec, p->d_codes, n, sct::tune(SCT_TUNE_SPECTRAL_CHUNK, 262144), cus,
+                                        (unsigned)probe[1], (unsigned)probe[2]);
     if (rc != SCT_OK) return cleanup(rc);
     p->spec.timer = &p->timer;
     *plan = p;
@@ -1052,7 +1048,7 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
 
 extern "C" int sct_allpairs_plan_destroy(sct_allpairs_plan* plan) {
   if (!plan) return SCT_OK;
-  if (plan->d_codes) (void)hipFree(plan->d_codes);
+  if (plan->d_codes) sct_spectral::ws_put(plan->spec.ws, plan->d_codes);  // (the workspace: kept)
   if (plan->d_sorted) (void)hipFree(plan->d_sorted);
   if (plan->d_sort_tmp) (void)hipFree(plan->d_sort_tmp);
   if (plan->d_table) (void)hipFree(plan->d_table);
@@ -1113,6 +1109,7 @@ extern "C" int sct_allpairs_moments(sct_allpairs_plan* plan, int part, int npart
                      plan->d_msrc, plan->d_msrc + kMomNPair,
                      reinterpret_cast<unsigned long long*>(d_counts) + 1 + sct::kMomNProd);
   SCT_LAUNCH_CHECK();
+  sct_spectral::note_stream(plan->spec, s);
   return SCT_OK;
 }
 
@@ -1137,7 +1134,11 @@ extern "C" int sct_allpairs_build_items(sct_allpairs_plan* plan, int64_t item_be
             "item range [%lld, %lld) outside [0, %lld)", (long long)item_begin, (long long)item_end,
             (long long)plan->items);
   hipStream_t s = sct::as_stream(stream);
-  if (plan->scheme == SCT_ALLPAIRS_SPECTRAL) return sct_spectral::build(plan->spec, plan->d_codes, s);
+  if (plan->scheme == SCT_ALLPAIRS_SPECTRAL) {
+    const int rc = sct_spectral::build(plan->spec, plan->d_codes, s);
+    sct_spectral::note_stream(plan->spec, s);
+    return rc;
+  }
   if (plan->table_entries == 0) return SCT_OK;
   // only the column chunks the items read (a rank of a sharded job builds its own slice)
   int64_t c0 = 0, c1 = plan->nchunks;
@@ -1167,6 +1168,7 @@ extern "C" int sct_allpairs_build_items(sct_allpairs_plan* plan, int64_t item_be
   }
   SCT_LAUNCH_CHECK();
   plan->timer.stop(s, t0, sct::LaunchTimer::BUILD);
+  sct_spectral::note_stream(plan->spec, s);
   return SCT_OK;
 }
 
@@ -1215,10 +1217,13 @@ extern "C" int sct_allpairs_count(sct_allpairs_plan* plan, int64_t item_begin, i
             "item range [%lld, %lld) outside [0, %lld)", (long long)item_begin,
             (long long)item_end, (long long)plan->items);
   if (item_begin == item_end) return SCT_OK;
-  if (plan->scheme == SCT_ALLPAIRS_SPECTRAL)
-    return sct_spectral::count(plan->spec, item_begin, item_end,
-                               reinterpret_cast<unsigned long long*>(d_counts), sct::as_stream(stream));
-  return dispatch_count(plan, item_begin, item_end, d_counts, grid, sct::as_stream(stream));
+  hipStream_t s = sct::as_stream(stream);
+  const int rc = plan->scheme == SCT_ALLPAIRS_SPECTRAL
+                     ? sct_spectral::count(plan->spec, item_begin, item_end,
+                                           reinterpret_cast<unsigned long long*>(d_counts), s)
+                     : dispatch_count(plan, item_begin, item_end, d_counts, grid, s);
+  sct_spectral::note_stream(plan->spec, s);
+  return rc;
 }
 
 extern "C" int sct_allpairs_time_kernels(sct_allpairs_plan* plan, int64_t item_begin, int64_t item_end,
@@ -1229,6 +1234,7 @@ extern "C" int sct_allpairs_time_kernels(sct_allpairs_plan* plan, int64_t item_b
             "item range [%lld, %lld) outside [0, %lld) or repeats < 1", (long long)item_begin,
             (long long)item_end, (long long)plan->items);
   hipStream_t s = sct::as_stream(stream);
+  sct_spectral::note_stream(plan->spec, s);  // (the call synchronises before it returns)
   if (plan->scheme == SCT_ALLPAIRS_SPECTRAL) {
     int64_t slices = 0;
     const int rc = sct_spectral::time_kernels(plan->spec, item_begin, item_end,
@@ -1316,13 +1322,24 @@ extern "C" int sct_allpairs_range_pairs(const sct_allpairs_plan* plan, int64_t i
 
 extern "C" int sct_hamming_hist_allpairs_host(const uint64_t* codes, int64_t n, int code_bits,
                                               uint64_t* hist, int nbins) {
+  return sct_hamming_hist_allpairs_host_ex(codes, n, code_bits, 0, hist, nbins);
+}
+
+extern "C" int sct_hamming_hist_allpairs_host_ex(const uint64_t* codes, int64_t n, int code_bits, int flags,
+                                                 uint64_t* hist, int nbins) {
   SCT_CHECK(hist != nullptr, "hist is NULL");
   SCT_CHECK(n >= 0 && (n == 0 || codes != nullptr), "bad codes");
-  sct::DevBuf dcodes, dcounts;
-  SCT_HIP(dcodes.alloc((size_t)n * 8));
-  if (n) SCT_HIP(hipMemcpy(dcodes.p, codes, (size_t)n * 8, hipMemcpyHostToDevice));
+  // codes and counts through the thread's cached staging buffer (no per-call hipMalloc); the
+  // plan borrows the device's cached workspace, so after the first call nothing is mapped
+  sct::HostStage* hs = sct::host_stage();
+  if (!hs) return SCT_E_HIP;
+  const size_t cbytes = ((size_t)n * 8 + 255) & ~(size_t)255;
+  if (int rc = sct::stage_reserve(hs, 0, cbytes + 129 * 8); rc != SCT_OK) return rc;
+  uint64_t* d_codes = reinterpret_cast<uint64_t*>(hs->dev);
+  uint64_t* d_counts = reinterpret_cast<uint64_t*>(hs->dev + cbytes);
+  if (n) SCT_HIP(hipMemcpyAsync(d_codes, codes, (size_t)n * 8, hipMemcpyHostToDevice, 0));
   sct_allpairs_plan* plan = nullptr;
-  int rc = sct_allpairs_plan_create((const uint64_t*)dcodes.p, n, code_bits, &plan);
+  int rc = sct_allpairs_plan_create_ex2(d_codes, n, code_bits, SCT_ALLPAIRS_AUTO, flags, &plan);
   if (rc != SCT_OK) return rc;
   struct Guard {
     sct_allpairs_plan* p;
@@ -1331,20 +1348,24 @@ extern "C" int sct_hamming_hist_allpairs_host(const uint64_t* codes, int64_t n, 
   if (plan->nbins != nbins)
     return sct::fail(SCT_E_INVALID, "hist holds %d bins, plan needs %d", nbins, plan->nbins);
   const int nc = plan->ncounts;
-  SCT_HIP(dcounts.alloc((size_t)nc * 8));
-  SCT_HIP(hipMemset(dcounts.p, 0, (size_t)nc * 8));
+  SCT_HIP(hipMemsetAsync(d_counts, 0, (size_t)nc * 8, 0));
   rc = sct_allpairs_build(plan, nullptr);
   if (rc != SCT_OK) return rc;
-  rc = sct_allpairs_moments(plan, 0, 1, (uint64_t*)dcounts.p, nullptr);
+  rc = sct_allpairs_moments(plan, 0, 1, d_counts, nullptr);
   if (rc != SCT_OK) return rc;
-  rc = sct_allpairs_count(plan, 0, plan->items, (uint64_t*)dcounts.p, 0, nullptr);
+  rc = sct_allpairs_count(plan, 0, plan->items, d_counts, 0, nullptr);
   if (rc != SCT_OK) return rc;
   uint64_t counts[129];
-  SCT_HIP(hipMemcpy(counts, dcounts.p, (size_t)nc * 8, hipMemcpyDeviceToHost));
+  SCT_HIP(hipMemcpy(counts, d_counts, (size_t)nc * 8, hipMemcpyDeviceToHost));
   // counts[0]: pairs counted (SUBSETS, MOMENTS) or the code count (SPECTRAL)
   const int64_t expect = plan->scheme == SCT_ALLPAIRS_SPECTRAL ? n : n * (n - 1) / 2;
   if ((int64_t)counts[0] != (n >= 2 ? expect : 0))
     return sct::fail(SCT_E_HIP, "pair count mismatch: counted %llu, expected %lld",
                      (unsigned long long)counts[0], (long long)expect);
   return sct_counts_to_hist_ex(plan->scheme, counts, nc, hist, nbins);
+}
+
+extern "C" int sct_allpairs_cache_release(void) {
+  sct_spectral::ws_release_all();
+  return SCT_OK;
 }

@@ -5,6 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+#include <vector>
+
 #include "sct_common.h"
 
 namespace sct_spectral {
@@ -40,7 +43,7 @@ __device__ __forceinline__ void add_job_constants(unsigned long long* counts, un
                                                   const unsigned long long* sumsq) {
   if (add_n && blockIdx.x == 0 && threadIdx.x == 0) {
     atomicAdd(counts, add_n);
-    atomicAdd(counts + 1, *sumsq);
+    atomicAdd(counts + 1, sumsq ? *sumsq : add_n);  // no sumsq: the caller promised distinct codes
   }
 }
 
@@ -71,8 +74,33 @@ constexpr int ctz_c(int i) {
   return k;
 }
 
+// Per-device cache of an all-pairs plan's device buffers (DESIGN.md §3.8 "plan cache"): a plan
+// created while its device's workspace is idle borrows it -- its buffers are grow-only slots kept
+// across plans, so a one-shot call (plan create, build, count, destroy) maps no memory after the
+// first one: no 4 GiB hipMalloc / hipFree, no order-table upload.  A plan created while the
+// workspace is lent out (a second live plan on the device) allocates its own buffers as before.
+// sct_allpairs_cache_release() frees the idle workspaces.
+enum WsSlot {
+  W_CODES, W_HI, W_OFF, W_CNT, W_GOFS, W_HIST, W_PLANES, W_BUF, W_SUMSQ, W_SUMSQ_TMP, W_PROBE, W_ORDER,
+  W_COUNTS, W_NSLOTS
+};
+struct Workspace;
+// the current device's workspace, lent to the caller, or nullptr when it is lent out already
+Workspace* ws_acquire();
+// give it back (its buffers stay allocated unless a release was asked for meanwhile)
+void ws_release(Workspace* ws);
+// slot `slot` of at least `bytes` (grow-only); ws == nullptr: a plain hipMalloc
+int ws_get(Workspace* ws, int slot, size_t bytes, void** p);
+// free p unless it came from a workspace
+void ws_put(Workspace* ws, void* p);
+// the digit-weight order table is the same for every plan: uploaded once per workspace
+bool* ws_order_ready(Workspace* ws);
+// free every idle workspace (all devices); one lent out is freed when its plan returns it
+void ws_release_all();
+
 // Device state of a SPECTRAL plan (owned by sct_allpairs_plan).
 struct State {
+  Workspace* ws = nullptr;       // the borrowed workspace, or nullptr (buffers owned)
   int64_t n = 0;
   uint32_t* d_hi = nullptr;      // code >> 14 of every code, grouped by column (low 14 bits)
   uint32_t* d_off = nullptr;     // [2^14 + 1] first code of each low-14-bit column
@@ -98,8 +126,17 @@ struct State {
   // sum f^2 of the plan's codes (device word), computed by the plan's first build
   unsigned long long* d_sumsq = nullptr;
   bool sumsq_ready = false;
+  // the caller promised pairwise-distinct codes (SCT_ALLPAIRS_DISTINCT): sum f^2 = n, no sort;
+  // a broken promise fails the host's exact check sum_w S_w == 2^32 n, never a silent result
+  bool distinct = false;
+  const unsigned long long* sumsq_ptr() const { return distinct ? nullptr : d_sumsq; }
   void* d_sumsq_tmp = nullptr;   // sort scratch when the intermediate is too small to lend it
+  // streams the plan enqueued work on, each with an event recorded after its last enqueue: a
+  // borrowed workspace goes back only once they have passed (the next plan may use another stream)
+  std::vector<std::pair<hipStream_t, hipEvent_t>> used;
 };
+// record that work of the plan was enqueued on s (call after the enqueue)
+void note_stream(State& st, hipStream_t s);
 
 // d_sumsq = sum over distinct codes of multiplicity^2 (radix sort of the low 32 bits + a
 // lower-bound pass), once per plan, on stream s (the intermediate d_buf is the scratch)
@@ -112,6 +149,9 @@ constexpr int kSlices16 = 1 << (kSpaceBits - kLoBits16);
 // st.lo_bits == 16.  max16: codes in the densest 16-bit column (<= 127); chunk in virtual
 // slices (4 per real one).
 int create16(State& st, const uint64_t* d_codes, int64_t n, unsigned max16, int64_t chunk, int cus);
+// the intermediate of `bytes`, halved (with *chunk) while the device cannot hold it, down to a
+// floor of `min_chunk` slices (a smaller chunk only costs launches)
+int alloc_buf(State& st, int64_t* chunk, int64_t min_chunk, size_t bytes_per_slice);
 int build16(State& st, const uint64_t* d_codes, hipStream_t s);
 int count16(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_counts, hipStream_t s);
 int time_kernels16(State& st, int64_t z_begin, int64_t z_end, unsigned long long* d_counts, int repeats,
@@ -122,8 +162,12 @@ int max_column(const uint64_t* d_codes, int64_t n, int lo_bits, unsigned* out);
 int make_order_table(State& st);
 
 // allocate (chunk = slices held in HBM at once) and size the intermediate from the
-// codes' densest column; returns an SCT_* code
-int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus);
+// codes' densest column (max14 / max16: codes in the densest 14- / 16-bit column, from the
+// plan's probe); returns an SCT_* code
+int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus, unsigned max14, unsigned max16);
+// one pass over the codes: their OR and the densest 14- and 16-bit columns, into out[0..2]
+// (host; one synchronisation); scratch from the plan's workspace slot W_PROBE
+int probe(Workspace* ws, const uint64_t* d_codes, int64_t n, unsigned long long* out);
 void destroy(State& st);
 // group the codes by column + bit planes (any slice range needs all of them)
 int build(State& st, const uint64_t* d_codes, hipStream_t s);

@@ -24,6 +24,8 @@
 #include <vector>
 #include <type_traits>
 
+#include <mutex>
+
 #include <hipcub/hipcub.hpp>
 
 #include "sct_common.h"
@@ -78,15 +80,6 @@ __device__ __forceinline__ void wht(int32_t* x) {
         x[i] = a + b;
         x[i | h] = a - b;
       }
-}
-
-// Counting sort of the codes by column (low 14 bits): only code >> 14 is kept, in column
-// order (the order inside a column is whatever the atomics give: every use of a column's
-// codes is an order-independent sum).
-__global__ void column_hist_kernel(const uint64_t* __restrict__ codes, int64_t n, uint32_t* __restrict__ cnt,
-                                   uint32_t mask) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    atomicAdd(&cnt[codes[i] & mask], 1u);
 }
 
 // Privatised counting sort (the build of every step; no global atomics):
@@ -880,9 +873,37 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const uint32_t* __restrict__
   if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
 
-__global__ void max_column_kernel(const uint32_t* __restrict__ cnt, unsigned* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  atomicMax(out, cnt[c]);
+// the plan's probe (one pass over the codes): their OR, and the code counts of every 14- and
+// 16-bit column (global atomics: 737K codes over 2^14 / 2^16 counters barely contend)
+__global__ __launch_bounds__(256) void probe_kernel(const uint64_t* __restrict__ codes, int64_t n,
+                                                    uint32_t* __restrict__ cnt14, uint32_t* __restrict__ cnt16,
+                                                    unsigned long long* __restrict__ out) {
+  unsigned long long o = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t x = codes[i];
+    o |= x;
+    atomicAdd(&cnt14[x & (kLo - 1)], 1u);
+    atomicAdd(&cnt16[x & 0xFFFFu], 1u);
+  }
+#pragma unroll
+  for (int s = 32; s; s >>= 1) o |= __shfl_xor(o, s);
+  if ((threadIdx.x & 63) == 0 && o) atomicOr(out, o);
+}
+// out[1] = max cnt14, out[2] = max cnt16 (grid covers the 2^16 counters)
+__global__ __launch_bounds__(256) void probe_max_kernel(const uint32_t* __restrict__ cnt14,
+                                                        const uint32_t* __restrict__ cnt16,
+                                                        unsigned long long* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  unsigned m14 = c < kLo ? cnt14[c] : 0u, m16 = cnt16[c];
+#pragma unroll
+  for (int s = 32; s; s >>= 1) {
+    m14 = max(m14, (unsigned)__shfl_xor(m14, s));
+    m16 = max(m16, (unsigned)__shfl_xor(m16, s));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (m14) atomicMax(out + 1, (unsigned long long)m14);
+    if (m16) atomicMax(out + 2, (unsigned long long)m16);
+  }
 }
 
 template <typename T>
@@ -915,11 +936,11 @@ int launch_tile(State& st, int z0, int z1, unsigned long long* counts, hipStream
     const uint16_t* order = ((ns & (ns - 1)) == 0 && z0 % ns == 0) ? st.d_order + std::min(ns, kMaxOrder) : nullptr;
     const dim3 rgrid((unsigned)std::max(1, std::min(st.grid * st.tile_wgs, (z1 - z0 + 3) / 4)));
     hipLaunchKernelGGL(tile_reg_kernel, rgrid, dim3(256), 0, s, buf, order, z0, z1 - z0, counts, add_n,
-                       (const unsigned long long*)st.d_sumsq);
+                       st.sumsq_ptr());
   } else {
     const dim3 grid((unsigned)std::min(st.grid * 2, z1 - z0));
     hipLaunchKernelGGL(tile_kernel<T>, grid, dim3(256), 0, s, buf, z0, z1 - z0, counts, add_n,
-                       (const unsigned long long*)st.d_sumsq);
+                       st.sumsq_ptr());
   }
   SCT_LAUNCH_CHECK();
   return SCT_OK;
@@ -970,10 +991,109 @@ int time_chunk(State& st, int z0, int z1, unsigned long long* counts, int repeat
 
 }  // namespace
 
+// ---------------------------------------------------------------- plan cache (workspace)
+struct Workspace {
+  int device = -1;
+  bool busy = false;
+  bool release = false;  // sct_allpairs_cache_release() while lent out: free on return
+  bool order_ready = false;
+  void* p[W_NSLOTS] = {};
+  size_t cap[W_NSLOTS] = {};
+};
+
+namespace {
+std::mutex g_ws_mu;
+Workspace* g_ws[64] = {};
+
+void ws_free(Workspace* ws) {
+  for (int k = 0; k < W_NSLOTS; ++k)
+    if (ws->p[k]) (void)hipFree(ws->p[k]);
+  delete ws;
+}
+}  // namespace
+
+Workspace* ws_acquire() {
+  if (sct::tune(SCT_TUNE_PLAN_CACHE, 1) == 0) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  Workspace*& ws = g_ws[dev];
+  if (!ws) {
+    ws = new Workspace();
+    ws->device = dev;
+  }
+  if (ws->busy) return nullptr;
+  ws->busy = true;
+  ws->release = false;
+  return ws;
+}
+
+void ws_release(Workspace* ws) {
+  if (!ws) return;
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  ws->busy = false;
+  if (ws->release) {
+    g_ws[ws->device] = nullptr;
+    ws_free(ws);
+  }
+}
+
+int ws_get(Workspace* ws, int slot, size_t bytes, void** p) {
+  bytes = std::max<size_t>(bytes, 256);
+  if (!ws) {
+    SCT_HIP(hipMalloc(p, bytes));
+    return SCT_OK;
+  }
+  if (ws->cap[slot] < bytes) {  // grow (rare: a larger set than any before on this device)
+    if (ws->p[slot]) (void)hipFree(ws->p[slot]);
+    ws->p[slot] = nullptr;
+    ws->cap[slot] = 0;
+    if (slot == W_ORDER) ws->order_ready = false;
+    SCT_HIP(hipMalloc(&ws->p[slot], bytes));
+    ws->cap[slot] = bytes;
+  }
+  *p = ws->p[slot];
+  return SCT_OK;
+}
+
+void ws_put(Workspace* ws, void* p) {
+  if (!ws && p) (void)hipFree(p);
+}
+
+bool* ws_order_ready(Workspace* ws) { return ws ? &ws->order_ready : nullptr; }
+
+void ws_release_all() {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  for (auto& ws : g_ws) {
+    if (!ws) continue;
+    if (ws->busy) {
+      ws->release = true;
+      continue;
+    }
+    int cur = 0;
+    const bool dev_ok = hipGetDevice(&cur) == hipSuccess && hipSetDevice(ws->device) == hipSuccess;
+    ws_free(ws);
+    if (dev_ok) (void)hipSetDevice(cur);
+    ws = nullptr;
+  }
+}
+
+void note_stream(State& st, hipStream_t s) {
+  for (auto& u : st.used)
+    if (u.first == s) {
+      (void)hipEventRecord(u.second, s);
+      return;
+    }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return;
+  (void)hipEventRecord(e, s);
+  st.used.emplace_back(s, e);
+}
+
 int make_order_table(State& st) {
   // for every power of two L <= 2^16: the offsets [0, L) sorted by digit weight, stored
   // at [L, 2L) (an aligned range of L slices adds a constant weight to all of them); the
-  // same for every plan, so sorted once per process
+  // same for every plan, so sorted once per process and uploaded once per workspace
   static const std::vector<uint16_t> order = [] {
     std::vector<uint16_t> o(2 * kMaxOrder);
     for (int len = 1; len <= kMaxOrder; len *= 2) {  // a stable counting sort by weight (0..8)
@@ -985,27 +1105,56 @@ int make_order_table(State& st) {
     }
     return o;
   }();
-  SCT_HIP(hipMalloc(&st.d_order, order.size() * 2));
-  SCT_HIP(hipMemcpy(st.d_order, order.data(), order.size() * 2, hipMemcpyHostToDevice));
+  void* p = nullptr;
+  if (int rc = ws_get(st.ws, W_ORDER, order.size() * 2, &p); rc != SCT_OK) return rc;
+  st.d_order = reinterpret_cast<uint16_t*>(p);
+  bool* ready = ws_order_ready(st.ws);
+  if (!ready || !*ready) {
+    SCT_HIP(hipMemcpy(st.d_order, order.data(), order.size() * 2, hipMemcpyHostToDevice));
+    if (ready) *ready = true;
+  }
   return SCT_OK;
 }
 
-int max_column(const uint64_t* d_codes, int64_t n, int lo_bits, unsigned* out) {
-  const int cols = 1 << lo_bits;
-  sct::DevBuf cnt, dmax;
-  SCT_HIP(cnt.alloc((size_t)cols * 4));
-  SCT_HIP(dmax.alloc(4));
-  SCT_HIP(hipMemset(cnt.p, 0, (size_t)cols * 4));
-  SCT_HIP(hipMemset(dmax.p, 0, 4));
-  hipLaunchKernelGGL(column_hist_kernel, dim3(1024), dim3(256), 0, 0, d_codes, n, (uint32_t*)cnt.p, (uint32_t)(cols - 1));
-  SCT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(max_column_kernel, dim3(cols / 256), dim3(256), 0, 0, (const uint32_t*)cnt.p, (unsigned*)dmax.p);
-  SCT_LAUNCH_CHECK();
-  SCT_HIP(hipMemcpy(out, dmax.p, 4, hipMemcpyDeviceToHost));
+int probe(Workspace* ws, const uint64_t* d_codes, int64_t n, unsigned long long* out) {
+  void* p = nullptr;
+  constexpr size_t kWords = (size_t)kLo + (1u << 16);
+  if (int rc = ws_get(ws, W_PROBE, kWords * 4 + 32, &p); rc != SCT_OK) return rc;
+  struct Put {
+    Workspace* ws;
+    void* p;
+    ~Put() { ws_put(ws, p); }
+  } put{ws, p};
+  uint32_t* cnt14 = reinterpret_cast<uint32_t*>(p);
+  uint32_t* cnt16 = cnt14 + kLo;
+  unsigned long long* res = reinterpret_cast<unsigned long long*>(cnt16 + (1u << 16));
+  SCT_HIP(hipMemsetAsync(p, 0, kWords * 4 + 32, 0));
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(1024, sct::ceil_div(n, 256)));
+  if (n > 0) {
+    hipLaunchKernelGGL(probe_kernel, dim3(blocks), dim3(256), 0, 0, d_codes, n, cnt14, cnt16, res);
+    SCT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(probe_max_kernel, dim3((1u << 16) / 256), dim3(256), 0, 0, cnt14, cnt16, res);
+    SCT_LAUNCH_CHECK();
+  }
+  SCT_HIP(hipMemcpy(out, res, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return SCT_OK;
 }
 
-int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus) {
+int alloc_buf(State& st, int64_t* chunk, int64_t min_chunk, size_t bytes_per_slice) {
+  for (;;) {
+    const size_t bytes = (size_t)((*chunk + 15) & ~15ll) * bytes_per_slice;  // whole 16-slice groups
+    const int rc = ws_get(st.ws, W_BUF, bytes, &st.d_buf);
+    if (rc == SCT_OK) {
+      st.buf_bytes = bytes;
+      return SCT_OK;
+    }
+    (void)hipGetLastError();  // clear the out-of-memory state
+    if (rc != SCT_E_NOMEM || *chunk / 2 < min_chunk) return rc;
+    *chunk /= 2;
+  }
+}
+
+int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus, unsigned max14, unsigned max16) {
   st.n = n;
   st.chunk = std::max<int64_t>(kWalk, std::min<int64_t>(chunk, kSlices));
   st.grid = std::max(1, cus);  // CUs; the tile kernels' persistent grids are sized from it
@@ -1013,46 +1162,56 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   // the densest column bounds |seed| and so the intermediate's width (the codes are fixed
   // for the plan's life); a set too dense for int8 seeds on 14-bit columns takes 16-bit
   // columns when every one of those holds <= 127 codes (spectral16.hip)
-  unsigned maxm = 0;
-  if (int rc = max_column(d_codes, n, kLoBits, &maxm); rc != SCT_OK) return rc;
+  const unsigned maxm = max14;
   const int64_t force = sct::tune(SCT_TUNE_SPECTRAL_COLUMNS, 0);
-  if ((maxm > 127 && force != kLoBits) || force == kLoBits16) {
-    unsigned max16 = 0;
-    if (int rc = max_column(d_codes, n, kLoBits16, &max16); rc != SCT_OK) return rc;
-    if (max16 <= 127) return create16(st, d_codes, n, max16, chunk, cus);
-  }
-  SCT_HIP(hipMalloc(&st.d_hi, (size_t)n * 4));
-  SCT_HIP(hipMalloc(&st.d_off, (size_t)(kLo + 1) * 4));
-  SCT_HIP(hipMalloc(&st.d_cnt, (size_t)2 * kLo * 4));  // counts, then scatter cursors
+  if (((maxm > 127 && force != kLoBits) || force == kLoBits16) && max16 <= 127)
+    return create16(st, d_codes, n, max16, chunk, cus);
+  void* p = nullptr;
+  auto get = [&](int slot, size_t bytes, auto** out) {
+    const int rc = ws_get(st.ws, slot, bytes, &p);
+    if (rc == SCT_OK) *out = reinterpret_cast<std::remove_reference_t<decltype(**out)>*>(p);
+    return rc;
+  };
+  if (int rc = get(W_HI, (size_t)n * 4, &st.d_hi); rc != SCT_OK) return rc;
+  if (int rc = get(W_OFF, (size_t)(kLo + 1) * 4, &st.d_off); rc != SCT_OK) return rc;
+  if (int rc = get(W_CNT, (size_t)2 * kLo * 4, &st.d_cnt); rc != SCT_OK) return rc;  // counts, then cursors
   st.max_m = maxm;
   st.elem_bytes = maxm <= 127 ? 1 : (maxm <= 32767 ? 2 : 4);
   // the intermediate holds one chunk: at most 4 GiB (all 2^18 slices at int8: one seed and one
   // tile launch per count; int16 / int32 seeds take 2 / 4 passes)
   st.chunk = std::min<int64_t>(st.chunk, (int64_t(4) << 30) / ((int64_t)kLo * st.elem_bytes));
-  int per_cu = 0;  // resident register-tile workgroups per CU (VGPR bound: 3)
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_reg_kernel, 256, 0) != hipSuccess || per_cu <= 0)
-    per_cu = 2;
+  static const int per_cu = [] {  // resident register-tile workgroups per CU (VGPR bound: 3)
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, tile_reg_kernel, 256, 0) != hipSuccess || v <= 0) v = 2;
+    return v;
+  }();
   st.tile_wgs = per_cu;
   if (int rc = make_order_table(st); rc != SCT_OK) return rc;
   st.max_groups = sct::ceil_div(n, 32) + kLo;
-  SCT_HIP(hipMalloc(&st.d_gofs, (size_t)(kLo + 1) * 4));
-  SCT_HIP(hipMalloc(&st.d_hist, (size_t)kSortWGs * kLo * 4));
-  SCT_HIP(hipMalloc(&st.d_planes, (size_t)st.max_groups * kPlaneWords * 4));
-  st.buf_bytes = (size_t)((st.chunk + 15) & ~15ll) * kLo * st.elem_bytes;  // whole 16-slice groups
-  SCT_HIP(hipMalloc(&st.d_buf, st.buf_bytes));
-  SCT_HIP(hipMalloc(&st.d_sumsq, sizeof(unsigned long long)));
+  if (int rc = get(W_GOFS, (size_t)(kLo + 1) * 4, &st.d_gofs); rc != SCT_OK) return rc;
+  if (int rc = get(W_HIST, (size_t)kSortWGs * kLo * 4, &st.d_hist); rc != SCT_OK) return rc;
+  if (int rc = get(W_PLANES, (size_t)st.max_groups * kPlaneWords * 4, &st.d_planes); rc != SCT_OK) return rc;
+  if (int rc = alloc_buf(st, &st.chunk, std::min<int64_t>(st.chunk, 4096), (size_t)kLo * st.elem_bytes); rc != SCT_OK)
+    return rc;
+  if (int rc = get(W_SUMSQ, sizeof(unsigned long long), &st.d_sumsq); rc != SCT_OK) return rc;
   return SCT_OK;
 }
 
 void destroy(State& st) {
+  // the plan's work has to be done before its buffers serve another plan (or are freed)
+  for (auto& u : st.used) {
+    (void)hipEventSynchronize(u.second);
+    (void)hipEventDestroy(u.second);
+  }
   for (void* p : {(void*)st.d_hi, (void*)st.d_off, (void*)st.d_cnt, (void*)st.d_gofs, (void*)st.d_planes,
                   (void*)st.d_hist, st.d_buf, (void*)st.d_order, (void*)st.d_sumsq, st.d_sumsq_tmp})
-    if (p) (void)hipFree(p);
+    ws_put(st.ws, p);
+  ws_release(st.ws);
   st = State();
 }
 
 int ensure_sumsq(State& st, const uint64_t* d_codes, hipStream_t s) {
-  if (st.sumsq_ready) return SCT_OK;
+  if (st.sumsq_ready || st.distinct) return SCT_OK;
   // scratch: low 32 bits (4n), sorted (4n), radix-sort temp
   size_t tmp = 0;
   SCT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)st.n, 0,
@@ -1061,7 +1220,7 @@ int ensure_sumsq(State& st, const uint64_t* d_codes, hipStream_t s) {
   const size_t need = 2 * keys + tmp;
   char* base = reinterpret_cast<char*>(st.d_buf);
   if (need > st.buf_bytes) {  // a small test chunk: scratch of its own, kept for the plan's life
-    SCT_HIP(hipMalloc(&st.d_sumsq_tmp, need));
+    if (int rc = ws_get(st.ws, W_SUMSQ_TMP, need, &st.d_sumsq_tmp); rc != SCT_OK) return rc;
     base = reinterpret_cast<char*>(st.d_sumsq_tmp);
   }
   uint32_t* k0 = reinterpret_cast<uint32_t*>(base);

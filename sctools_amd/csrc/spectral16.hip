@@ -600,7 +600,7 @@ void launch_tile16(State& st, const int8_t* buf, int z0, int z1, unsigned long l
   const int ns = z1 - z0;
   const uint16_t* order = ((ns & (ns - 1)) == 0 && ns <= (1 << 16) && z0 % ns == 0) ? st.d_order + ns : nullptr;
   hipLaunchKernelGGL(tile16_kernel, dim3((unsigned)std::max(1, std::min(st.grid * wgs_per_cu, ns))), dim3(256), 0, s,
-                     buf, order, z0, ns, counts, add_n, (const unsigned long long*)st.d_sumsq);
+                     buf, order, z0, ns, counts, add_n, st.sumsq_ptr());
 }
 
 int launch_chunk16(State& st, int z0, int z1, unsigned long long* counts, hipStream_t s, unsigned long long add_n) {
@@ -628,21 +628,29 @@ int create16(State& st, const uint64_t* d_codes, int64_t n, unsigned max16, int6
   st.elem_bytes = 1;
   st.chunk16 = std::max<int64_t>(kWalk16, std::min<int64_t>(kChunk16, chunk / 4));
   st.chunk = 4 * st.chunk16;  // in virtual slices (the plan's items)
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile16_kernel, 256, 0) != hipSuccess || per_cu <= 0)
-    per_cu = 2;
+  static const int per_cu = [] {
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, tile16_kernel, 256, 0) != hipSuccess || v <= 0) v = 2;
+    return v;
+  }();
   st.tile_wgs = per_cu;
   if (int rc = make_order_table(st); rc != SCT_OK) return rc;
   st.max_groups = sct::ceil_div(n, 32) + kLo16;
-  SCT_HIP(hipMalloc(&st.d_hi, (size_t)n * 4));
-  SCT_HIP(hipMalloc(&st.d_off, (size_t)(kLo16 + 1) * 4));
-  SCT_HIP(hipMalloc(&st.d_cnt, (size_t)kLo16 * 4));
-  SCT_HIP(hipMalloc(&st.d_gofs, (size_t)(kLo16 + 1) * 4));
-  SCT_HIP(hipMalloc(&st.d_hist, (size_t)kSortWGs16 * kLo16));
-  SCT_HIP(hipMalloc(&st.d_planes, (size_t)st.max_groups * kPW16 * 4));
-  st.buf_bytes = (size_t)st.chunk16 * kLo16;
-  SCT_HIP(hipMalloc(&st.d_buf, st.buf_bytes));
-  SCT_HIP(hipMalloc(&st.d_sumsq, sizeof(unsigned long long)));
+  void* p = nullptr;
+  auto get = [&](int slot, size_t bytes, auto** out) {
+    const int rc = ws_get(st.ws, slot, bytes, &p);
+    if (rc == SCT_OK) *out = reinterpret_cast<std::remove_reference_t<decltype(**out)>*>(p);
+    return rc;
+  };
+  if (int rc = get(W_HI, (size_t)n * 4, &st.d_hi); rc != SCT_OK) return rc;
+  if (int rc = get(W_OFF, (size_t)(kLo16 + 1) * 4, &st.d_off); rc != SCT_OK) return rc;
+  if (int rc = get(W_CNT, (size_t)kLo16 * 4, &st.d_cnt); rc != SCT_OK) return rc;
+  if (int rc = get(W_GOFS, (size_t)(kLo16 + 1) * 4, &st.d_gofs); rc != SCT_OK) return rc;
+  if (int rc = get(W_HIST, (size_t)kSortWGs16 * kLo16, &st.d_hist); rc != SCT_OK) return rc;
+  if (int rc = get(W_PLANES, (size_t)st.max_groups * kPW16 * 4, &st.d_planes); rc != SCT_OK) return rc;
+  if (int rc = alloc_buf(st, &st.chunk16, std::min<int64_t>(st.chunk16, 1024), (size_t)kLo16); rc != SCT_OK) return rc;
+  st.chunk = 4 * st.chunk16;
+  if (int rc = get(W_SUMSQ, sizeof(unsigned long long), &st.d_sumsq); rc != SCT_OK) return rc;
   return SCT_OK;
 }
 
@@ -698,7 +706,7 @@ int time_kernels16(State& st, int64_t z_begin, int64_t z_end, unsigned long long
   SCT_HIP(hipEventRecord(e[1], s));
   for (int r = 0; rc == SCT_OK && r < repeats; ++r)
     hipLaunchKernelGGL(tile16_kernel, dim3((unsigned)std::max(1, std::min(st.grid * st.tile_wgs, ns))), dim3(256), 0,
-                       s, buf, order, (int)rb, ns, d_counts, 0ull, (const unsigned long long*)st.d_sumsq);
+                       s, buf, order, (int)rb, ns, d_counts, 0ull, st.sumsq_ptr());
   SCT_HIP(hipEventRecord(e[2], s));
   st.timer = keep;
   if (rc != SCT_OK) return rc;

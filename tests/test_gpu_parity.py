@@ -502,6 +502,58 @@ def test_allpairs_spectral_is_auto_for_large_whitelists():
     assert hs.tolist() == hm.tolist()
 
 
+def test_plan_cache_reuse_and_release():
+    """The plan cache (sct_allpairs_cache_release, SCT_TUNE_PLAN_CACHE): one-shot calls on sets
+    of different sizes and seed widths reuse (and grow) the device's cached buffers; a plan
+    created while another holds the cache owns its buffers; a plan counted on a side stream and
+    destroyed hands the cache to the next plan only after its work is done; release and the
+    cache switched off give the same histograms.  Each against the C oracle."""
+    torch = pytest.importorskip("torch")
+    sets = [synthetic.whitelist_codes(n, 16, seed=n) for n in (400_000, 2_000, 350_000)]
+    sets.append(np.concatenate([sets[1], np.repeat(sets[1][:3], 200)]))  # forced SPECTRAL: int16 seeds
+    refs = [O.c_hist16(c)[0][:17].tolist() for c in sets]
+    for c, ref in zip(sets, refs):  # AUTO: SPECTRAL, MOMENTS, SPECTRAL, MOMENTS
+        assert _lib.hamming_hist_allpairs(c, 32).astype(np.int64).tolist() == ref
+    for c, ref in zip(sets, refs):  # forced SPECTRAL at every size
+        assert _spectral_hist(c).astype(np.int64).tolist() == ref
+    # a live plan holds the cache: a second plan meanwhile owns its buffers
+    d0 = torch.from_numpy(sets[0].view(np.int64)).cuda()
+    holder = _lib.AllPairsPlan(d0.data_ptr(), sets[0].size, 32, scheme=_lib.SCHEME_SPECTRAL)
+    assert _spectral_hist(sets[2]).astype(np.int64).tolist() == refs[2]
+    # the holder counts on a side stream and is destroyed without a host sync
+    side = torch.cuda.Stream()
+    counts = torch.zeros(holder.ncounts, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    holder.build(side.cuda_stream)
+    holder.count(counts.data_ptr(), stream=side.cuda_stream)
+    holder.close()
+    side.synchronize()
+    assert holder.counts_to_hist(counts.cpu().numpy().view(np.uint64)).astype(np.int64).tolist() == refs[0]
+    assert _spectral_hist(sets[2]).astype(np.int64).tolist() == refs[2]
+    _lib.release_plan_cache()
+    assert _lib.hamming_hist_allpairs(sets[0], 32).astype(np.int64).tolist() == refs[0]
+    with _lib.tuning(plan_cache=0):
+        assert _lib.hamming_hist_allpairs(sets[2], 32).astype(np.int64).tolist() == refs[2]
+    _lib.release_plan_cache()
+
+
+def test_distinct_promise_skips_sort_and_is_checked():
+    """SCT_ALLPAIRS_DISTINCT (Barcodes' mapping keys): SPECTRAL takes sum f^2 = n without its
+    sort; the histogram still matches the oracle, and a set that breaks the promise (one
+    duplicate among 400K codes) raises ValueError from the host's exact check instead of
+    returning a histogram -- with and without the promise the honest path stays exact."""
+    codes = synthetic.whitelist_codes(400_000, 16, seed=77)
+    ref = O.c_hist16(codes)[0][:17].tolist()
+    assert _lib.hamming_hist_allpairs(codes, 32, distinct=True).astype(np.int64).tolist() == ref
+    dup = codes.copy()
+    dup[-1] = dup[0]
+    with pytest.raises(ValueError, match="sum f"):
+        _lib.hamming_hist_allpairs(dup, 32, distinct=True)
+    assert _lib.hamming_hist_allpairs(dup, 32).astype(np.int64).tolist() == O.c_hist16(dup)[0][:17].tolist()
+    b = barcode.Barcodes({int(c): 1 for c in codes}, 16)
+    assert b.hamming_histogram().astype(np.int64).tolist() == ref
+
+
 def _heavy_multiset(case):
     """Observed-barcode multisets whose sum f^2 exceeds 2^32 (so sum_w S_w = 2^32 sum f^2
     exceeds 2^64): shuffled, with the seed width they force."""
