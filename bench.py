@@ -403,14 +403,26 @@ def path_config4(dev, reps, copy_gbs, threads):
     idx = torch.empty(nq, dtype=torch.int32, device=dev)
     dist = torch.empty(nq, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    plan = _lib.NearestPlan(3, d_wl.data_ptr(), n, 3 * L, 1, stream)
-    torch.cuda.synchronize()
-    build_ms = (time.perf_counter() - t) * 1e3
+    builds = []
+    for _ in range(3):  # the index build, wall-clock (its one synchronisation included); the last plan is kept
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        plan = _lib.NearestPlan(3, d_wl.data_ptr(), n, 3 * L, 1, stream)
+        torch.cuda.synchronize()
+        builds.append((time.perf_counter() - t) * 1e3)
+        if len(builds) < 3:
+            plan.close()
+    build_ms = sorted(builds)[1]
     ms = _events_ms(lambda: plan.query(q.data_ptr(), nq, idx.data_ptr(), dist.data_ptr(), stream), reps, dev)
     index = plan.info()
     plan.close()
+    torch.cuda.synchronize()  # one-shot: a fresh index and one query pass, wall-clock
+    t = time.perf_counter()
+    once = _lib.NearestPlan(3, d_wl.data_ptr(), n, 3 * L, 1, stream)
+    once.query(q.data_ptr(), nq, idx.data_ptr(), dist.data_ptr(), stream)
+    torch.cuda.synchronize()
+    oneshot_ms = (time.perf_counter() - t) * 1e3
+    once.close()
     exact = cls == 0
     exact_ok = bool(torch.equal(idx[exact].long(), pick[exact])) and bool((dist[exact] == 0).all())
     g = torch.Generator(device=dev).manual_seed(44)
@@ -431,6 +443,7 @@ def path_config4(dev, reps, copy_gbs, threads):
     return {"workload": "config 4: %d ThreeBit 16-bp observed barcodes (50%% exact, 25%% one substitution, "
                         "15%% one N, 10%% random) vs the %d-code whitelist, Hamming <= 1" % (nq, n),
             "value": nq / (ms * 1e-3), "unit": "queries/s", "ms": ms, "reps": reps, "index_build_ms": build_ms,
+            "index_build_ms_all": builds, "build_plus_query_ms": build_ms + ms, "oneshot_build_and_query_ms": oneshot_ms,
             "index": index,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
                          "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs,

@@ -664,15 +664,14 @@ extern "C" int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint6
   }
   const int blocks = (int)std::min<int64_t>(sct::ceil_div(n, 8 * WG), 1024);
   void* part = nullptr;
-  sct::keep_pool_warm();
-  SCT_HIP(hipMallocAsync(&part, (size_t)128 * blocks * 8, s));
+  SCT_HIP(sct::pool_alloc(&part, (size_t)128 * blocks * 8, s));
   hipLaunchKernelGGL(base_frequency_kernel, dim3(blocks), dim3(WG), 0, s, codes, n, (unsigned long long*)part);
   hipError_t le = hipGetLastError();
   if (le == hipSuccess)
     hipLaunchKernelGGL(base_frequency_reduce_kernel, dim3(128), dim3(WG), 0, s, (const unsigned long long*)part,
                        blocks, n, L, reinterpret_cast<unsigned long long*>(out));
   if (le == hipSuccess) le = hipGetLastError();
-  (void)hipFreeAsync(part, s);
+  sct::pool_free(part, s);
   if (le != hipSuccess) return sct::fail(SCT_E_HIP, "kernel launch: %s", hipGetErrorString(le));
   return SCT_OK;
 }

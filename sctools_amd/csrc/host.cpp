@@ -81,19 +81,46 @@ int64_t tune(int key, int64_t dflt) {
   return v == 0 ? dflt : v - 1;
 }
 
-void keep_pool_warm() {
+// The library's own stream-ordered memory pool per device (the device's DEFAULT
+// pool, which PyTorch and other libraries share, is left alone).  Its release threshold is
+// raised once, so per-call scratch is reused from the pool instead of being mapped and unmapped
+// around every stream synchronisation.
+static hipMemPool_t private_pool(int dev) {
   static std::mutex mu;
-  static std::vector<int> done;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return;
+  static hipMemPool_t pools[64] = {};
+  static bool tried[64] = {};
+  if (dev < 0 || dev >= 64) return nullptr;
   std::lock_guard<std::mutex> lk(mu);
-  if (std::find(done.begin(), done.end(), dev) != done.end()) return;
-  done.push_back(dev);
-  hipMemPool_t pool;
-  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-    uint64_t keep = UINT64_MAX;
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  if (!tried[dev]) {
+    tried[dev] = true;
+    hipMemPoolProps props = {};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    hipMemPool_t pool = nullptr;
+    if (hipMemPoolCreate(&pool, &props) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+      pools[dev] = pool;
+    } else {
+      (void)hipGetLastError();
+    }
   }
+  return pools[dev];
+}
+
+hipError_t pool_alloc(void** p, size_t bytes, hipStream_t s) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  bytes = bytes ? bytes : 1;
+  hipMemPool_t pool = private_pool(dev);
+  return pool ? hipMallocFromPoolAsync(p, bytes, pool, s) : hipMallocAsync(p, bytes, s);
+}
+
+void pool_free(void* p, hipStream_t s) {
+  if (p) (void)hipFreeAsync(p, s);
 }
 
 }  // namespace sct

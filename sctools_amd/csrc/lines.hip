@@ -105,18 +105,17 @@ __global__ __launch_bounds__(WG) void line_lens_kernel(const int64_t* __restrict
   }
 }
 
-// Scratch of one call, allocated and freed in stream order (the device's default memory
-// pool, kept warm: its release threshold is raised once per device, so repeated calls reuse
-// the pool instead of mapping memory each time).
+// Scratch of one call, allocated and freed in stream order from the library's private memory
+// pool (sct::pool_alloc: its memory stays in the pool, so repeated calls map nothing).
 struct StreamBuf {
   void* p = nullptr;
   hipStream_t s = nullptr;
   ~StreamBuf() {
-    if (p) (void)hipFreeAsync(p, s);
+    sct::pool_free(p, s);
   }
   hipError_t alloc(size_t bytes, hipStream_t st) {
     s = st;
-    return hipMallocAsync(&p, bytes ? bytes : 1, st);
+    return sct::pool_alloc(&p, bytes, st);
   }
 };
 
@@ -135,7 +134,6 @@ extern "C" int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines
   hipStream_t s = sct::as_stream(stream);
   const int64_t ntiles = sct::ceil_div(nbytes, TILE);
   SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
-  sct::keep_pool_warm();
   size_t tb = 0;
   SCT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                            (int)(ntiles + 1), s));

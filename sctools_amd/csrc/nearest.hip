@@ -497,31 +497,78 @@ __global__ __launch_bounds__(WG) void halves_index_kernel(int32_t* __restrict__ 
     if (idx[i] >= 0) idx[i] = unpack_perm(packed, pbits, idx[i]);
 }
 
-// whitelist -> (A, B) and (B, A) sort keys; *bad = 1 if a code has a digit that is not A/C/G/T
-// in its G positions or any bit above them
+// Half-key table build (round 4: a counting sort by bucket with no host synchronisation before
+// the end -- the order inside a bucket is irrelevant, a query scans its whole bucket):
+//   count    per code its A and B keys: atomic bucket counts; *bad = 1 if a code has a digit that
+//            is not A/C/G/T in its G positions or any bit above them (the layout is then dropped)
+//   scan     one workgroup: offsets of both tables, the cursors in place
+//   scatter  per code: one slot in its A bucket (entry = its B key) and one in its B bucket
+//            (entry = its A key), the whitelist index of both slots into permAB
 template <int KIND>
-__global__ void halves_keys_kernel(const uint64_t* __restrict__ wl, int64_t nw, Halves h,
-                                   uint32_t* __restrict__ keyAB, uint32_t* __restrict__ keyBA,
-                                   uint32_t* __restrict__ iota, unsigned* __restrict__ bad) {
+__global__ void halves_count_kernel(const uint64_t* __restrict__ wl, int64_t nw, Halves h,
+                                    uint32_t* __restrict__ cntA, uint32_t* __restrict__ cntB,
+                                    unsigned* __restrict__ bad) {
+  bool b = false;
   for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j < nw; j += (int64_t)gridDim.x * WG) {
     uint32_t kA, sA, kB, sB;
     int E;
     halves_of<KIND>(wl[j], h, kA, sA, kB, sB, E);
-    if (E || sA || sB) atomicOr(bad, 1u);
-    keyAB[j] = (kA << (2 * h.GB)) | kB;
-    keyBA[j] = (kB << (2 * h.GA)) | kA;
-    iota[j] = (uint32_t)j;
+    b |= (E | sA | sB) != 0;
+    atomicAdd(&cntA[kA], 1u);
+    atomicAdd(&cntB[kB], 1u);
   }
+  if (b) atomicOr(bad, 1u);
 }
 
-// sorted (hi << lowbits | lo) keys -> entries (lo, uint16) and bucket offsets of hi
-__global__ void halves_table_kernel(const uint32_t* __restrict__ sorted, int64_t nw, int lowbits, int64_t nbuckets,
-                                    uint16_t* __restrict__ ent, uint32_t* __restrict__ off) {
-  for (int64_t t = (int64_t)blockIdx.x * WG + threadIdx.x; t <= nw; t += (int64_t)gridDim.x * WG) {
-    const int64_t cur = t < nw ? (int64_t)(sorted[t] >> lowbits) : nbuckets;
-    const int64_t prev = t > 0 ? (int64_t)(sorted[t - 1] >> lowbits) : -1;
-    for (int64_t k = prev + 1; k <= cur; ++k) off[k] = (uint32_t)t;  // buckets (prev, cur] start at t
-    if (t < nw) ent[t] = (uint16_t)(sorted[t] & ((1u << lowbits) - 1));
+// exclusive scan of cnt[0, n) by one 1024-thread workgroup into off[0, n] and cnt (the cursors)
+__device__ __forceinline__ void block_scan_offsets(uint32_t* __restrict__ cnt, int64_t n, uint32_t* __restrict__ off,
+                                                   uint32_t* wsum) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t per = (n + 1023) / 1024, b = std::min<int64_t>(n, t * per), e = std::min<int64_t>(n, b + per);
+  uint32_t s = 0;
+  for (int64_t i = b; i < e; ++i) s += cnt[i];
+  uint32_t is = s;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t a = __shfl_up(is, d);
+    if (lane >= d) is += a;
+  }
+  if (lane == 63) wsum[wave] = is;
+  __syncthreads();
+  uint32_t run = is - s;
+  for (int w = 0; w < wave; ++w) run += wsum[w];
+  for (int64_t i = b; i < e; ++i) {
+    const uint32_t c = cnt[i];
+    off[i] = run;
+    cnt[i] = run;
+    run += c;
+  }
+  if (t == 1023) off[n] = run;
+  __syncthreads();  // wsum is reused
+}
+
+__global__ __launch_bounds__(1024) void halves_scan_kernel(uint32_t* __restrict__ cntA, int64_t nA,
+                                                           uint32_t* __restrict__ offA, uint32_t* __restrict__ cntB,
+                                                           int64_t nB, uint32_t* __restrict__ offB) {
+  __shared__ uint32_t wsum[16];
+  block_scan_offsets(cntA, nA, offA, wsum);
+  block_scan_offsets(cntB, nB, offB, wsum);
+}
+
+template <int KIND>
+__global__ void halves_scatter_kernel(const uint64_t* __restrict__ wl, int64_t nw, Halves h,
+                                      uint32_t* __restrict__ curA, uint32_t* __restrict__ curB,
+                                      uint16_t* __restrict__ entA, uint16_t* __restrict__ entB,
+                                      uint32_t* __restrict__ perm) {
+  for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j < nw; j += (int64_t)gridDim.x * WG) {
+    uint32_t kA, sA, kB, sB;
+    int E;
+    halves_of<KIND>(wl[j], h, kA, sA, kB, sB, E);
+    const uint32_t pA = atomicAdd(&curA[kA], 1u), pB = atomicAdd(&curB[kB], 1u);
+    entA[pA] = (uint16_t)kB;
+    perm[pA] = (uint32_t)j;
+    entB[pB] = (uint16_t)kA;
+    perm[nw + pB] = (uint32_t)j;
   }
 }
 
@@ -590,8 +637,8 @@ struct sct_nearest_plan {
   int64_t nw = 0;
   bool halves = false;  // half-key tables (Halves) for max_d <= 1
   Halves hv{};
-  void* hv_mem[5] = {};  // offA, entA, offB, entB, permA
-  uint32_t* perm_packed = nullptr;  // permAB at pbits per entry (+ 2 dwords of padding)
+  void* hv_mem[1] = {};  // one block: offA, offB, entA, entB, packed permAB
+  uint32_t* perm_packed = nullptr;  // permAB at pbits per entry (+ 2 dwords of padding), inside hv_mem[0]
   int pbits = 0;
   int nkeys = 0;  // > 0: open-addressing multi-index (OTables); 0: CSR per block (Parts)
   OTables ot{};
@@ -606,7 +653,6 @@ extern "C" int sct_nearest_plan_destroy(sct_nearest_plan* p) {
   if (!p) return SCT_OK;
   for (void* m : p->hv_mem)
     if (m) (void)hipFree(m);
-  if (p->perm_packed) (void)hipFree(p->perm_packed);
   for (int k = 0; k < MAX_KEYS; ++k)
     if (p->ot.t[k].slots) (void)hipFree(p->ot.t[k].slots);
   for (int k = 0; k < MAX_PARTS; ++k) {
@@ -619,7 +665,8 @@ extern "C" int sct_nearest_plan_destroy(sct_nearest_plan* p) {
 }
 
 // The half-key tables, if the whitelist allows them (SCT_OK with p->halves set), else SCT_OK
-// with p->halves false (the caller takes another layout).
+// with p->halves false (the caller takes another layout).  One device allocation for the
+// plan's tables, scratch from the library's pool, one synchronisation (for the layout check).
 static int build_halves(sct_nearest_plan* p, const uint64_t* d_wl, int64_t nw, int G, hipStream_t s) {
   Halves h{};
   h.G = G;
@@ -627,64 +674,62 @@ static int build_halves(sct_nearest_plan* p, const uint64_t* d_wl, int64_t nw, i
   h.GA = G - h.GB;
   h.nw = nw;
   const int64_t nA = 1LL << (2 * h.GA), nB = 1LL << (2 * h.GB);
-  sct::DevBuf keyAB, keyBA, sAB, sBA, iota, bad, tmp;
   const size_t n = (size_t)std::max<int64_t>(nw, 1);
-  SCT_HIP(keyAB.alloc(n * 4));
-  SCT_HIP(keyBA.alloc(n * 4));
-  SCT_HIP(sAB.alloc(n * 4));
-  SCT_HIP(sBA.alloc(n * 4));
-  SCT_HIP(iota.alloc(n * 4));
-  SCT_HIP(bad.alloc(4));
-  SCT_HIP(hipMemsetAsync(bad.p, 0, 4, s));
-  if (p->kind == 2)
-    hipLaunchKernelGGL(halves_keys_kernel<2>, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_wl, nw, h,
-                       (uint32_t*)keyAB.p, (uint32_t*)keyBA.p, (uint32_t*)iota.p, (unsigned*)bad.p);
-  else
-    hipLaunchKernelGGL(halves_keys_kernel<3>, dim3(grid_for(nw, 4096)), dim3(WG), 0, s, d_wl, nw, h,
-                       (uint32_t*)keyAB.p, (uint32_t*)keyBA.p, (uint32_t*)iota.p, (unsigned*)bad.p);
-  SCT_LAUNCH_CHECK();
-  unsigned hbad = 0;
-  SCT_HIP(hipMemcpyAsync(&hbad, bad.p, 4, hipMemcpyDeviceToHost, s));
-  SCT_HIP(hipStreamSynchronize(s));
-  if (hbad) return SCT_OK;  // not applicable
-  // offA, entA, offB, entB (+16 B: the last chunk's load may run past nw), permAB
-  const size_t bytes[5] = {(size_t)(nA + 1) * 4, n * 2 + 16, (size_t)(nB + 1) * 4, n * 2 + 16, 2 * n * 4};
-  for (int k = 0; k < 5; ++k) SCT_HIP(hipMalloc(&p->hv_mem[k], bytes[k]));
-  h.offA = (const uint32_t*)p->hv_mem[0];
-  h.entA = (const uint16_t*)p->hv_mem[1];
-  h.offB = (const uint32_t*)p->hv_mem[2];
-  h.entB = (const uint16_t*)p->hv_mem[3];
-  h.permAB = (const uint32_t*)p->hv_mem[4];
-  const int bits = 2 * G;
-  size_t tb = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)nw, 0, bits, s);
-  SCT_HIP(tmp.alloc(tb));
-  uint32_t* perm = (uint32_t*)p->hv_mem[4];
-  size_t b1 = tb, b2 = tb;
-  SCT_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, b1, (const uint32_t*)keyAB.p, (uint32_t*)sAB.p,
-                                             (const uint32_t*)iota.p, perm, (int)nw, 0, bits, s));
-  SCT_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, b2, (const uint32_t*)keyBA.p, (uint32_t*)sBA.p,
-                                             (const uint32_t*)iota.p, perm + nw, (int)nw, 0, bits, s));
-  hipLaunchKernelGGL(halves_table_kernel, dim3(grid_for(nw + 1, 4096)), dim3(WG), 0, s, (const uint32_t*)sAB.p, nw,
-                     2 * h.GB, nA, (uint16_t*)p->hv_mem[1], (uint32_t*)p->hv_mem[0]);
-  hipLaunchKernelGGL(halves_table_kernel, dim3(grid_for(nw + 1, 4096)), dim3(WG), 0, s, (const uint32_t*)sBA.p, nw,
-                     2 * h.GA, nB, (uint16_t*)p->hv_mem[3], (uint32_t*)p->hv_mem[2]);
-  SCT_LAUNCH_CHECK();
-  {
-    int pb = 1;
-    while (pb < 32 && (1LL << pb) < nw) ++pb;
-    const int64_t ndw = (2 * (int64_t)n * pb + 31) / 32 + 2;  // + 2: the last 8-byte load's second dword
-    SCT_HIP(hipMalloc(&p->perm_packed, (size_t)ndw * 4));
+  int pb = 1;  // bits of a packed whitelist index
+  while (pb < 32 && (1LL << pb) < nw) ++pb;
+  const int64_t ndw = (2 * (int64_t)n * pb + 31) / 32 + 2;  // + 2: the last 8-byte load's second dword
+  // the plan's tables: offA, offB, entA, entB (+16 B: the last chunk's load may run past nw), packed permAB
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t oOffA = 0, oOffB = oOffA + al((nA + 1) * 4), oEntA = oOffB + al((nB + 1) * 4);
+  const size_t oEntB = oEntA + al(n * 2 + 16), oPack = oEntB + al(n * 2 + 16), total = oPack + al(ndw * 4);
+  SCT_HIP(hipMalloc(&p->hv_mem[0], total));
+  char* base = reinterpret_cast<char*>(p->hv_mem[0]);
+  h.offA = reinterpret_cast<const uint32_t*>(base + oOffA);
+  h.offB = reinterpret_cast<const uint32_t*>(base + oOffB);
+  h.entA = reinterpret_cast<const uint16_t*>(base + oEntA);
+  h.entB = reinterpret_cast<const uint16_t*>(base + oEntB);
+  p->perm_packed = reinterpret_cast<uint32_t*>(base + oPack);
+  p->pbits = pb;
+  // scratch: bucket counts / cursors of both tables, permAB unpacked, the layout flag
+  const size_t sCnt = 0, sPerm = sCnt + al((nA + nB) * 4), sBad = sPerm + al(2 * n * 4), sTotal = sBad + 256;
+  void* scratch = nullptr;
+  SCT_HIP(sct::pool_alloc(&scratch, sTotal, s));
+  char* sb = reinterpret_cast<char*>(scratch);
+  uint32_t* cntA = reinterpret_cast<uint32_t*>(sb + sCnt);
+  uint32_t* cntB = cntA + nA;
+  uint32_t* perm = reinterpret_cast<uint32_t*>(sb + sPerm);
+  unsigned* bad = reinterpret_cast<unsigned*>(sb + sBad);
+  hipError_t e = hipMemsetAsync(sb, 0, sPerm, s);
+  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, 4, s);
+  const unsigned g = grid_for(nw, 4096);
+  if (e == hipSuccess) {
+    if (p->kind == 2)
+      hipLaunchKernelGGL(halves_count_kernel<2>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB, bad);
+    else
+      hipLaunchKernelGGL(halves_count_kernel<3>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB, bad);
+    hipLaunchKernelGGL(halves_scan_kernel, dim3(1), dim3(1024), 0, s, cntA, nA, (uint32_t*)h.offA, cntB, nB,
+                       (uint32_t*)h.offB);
+    if (p->kind == 2)
+      hipLaunchKernelGGL(halves_scatter_kernel<2>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB,
+                         (uint16_t*)h.entA, (uint16_t*)h.entB, perm);
+    else
+      hipLaunchKernelGGL(halves_scatter_kernel<3>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB,
+                         (uint16_t*)h.entA, (uint16_t*)h.entB, perm);
     hipLaunchKernelGGL(pack_perm_kernel, dim3(grid_for(ndw, 4096)), dim3(WG), 0, s, (const uint32_t*)perm,
                        (int64_t)(2 * n), pb, ndw, p->perm_packed);
-    SCT_LAUNCH_CHECK();
-    p->pbits = pb;
+    e = hipGetLastError();
   }
-  SCT_HIP(hipStreamSynchronize(s));  // the scratch dies here (and the unpacked permAB with it)
-  (void)hipFree(p->hv_mem[4]);
-  p->hv_mem[4] = nullptr;
-  h.permAB = nullptr;
+  unsigned hbad = 1;
+  if (e == hipSuccess) e = hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s);
+  sct::pool_free(scratch, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return sct::fail(SCT_E_HIP, "half-key build: %s", hipGetErrorString(e));
+  if (hbad) {  // not applicable: another layout
+    (void)hipFree(p->hv_mem[0]);
+    p->hv_mem[0] = nullptr;
+    p->perm_packed = nullptr;
+    return SCT_OK;
+  }
   p->hv = h;
   p->halves = true;
   return SCT_OK;

@@ -61,10 +61,10 @@ constexpr size_t kZeroCopyBytes = 64 << 10;
 // it the caller's arrays are copied through per-call device allocations.
 constexpr size_t kStageBytes = 256ull << 20;
 
-// Raise the release threshold of the current device's default memory pool once, so that
-// per-call scratch from hipMallocAsync / hipFreeAsync is reused from the pool instead of
-// being mapped and unmapped around every stream synchronisation (host.cpp).
-void keep_pool_warm();
+// Stream-ordered scratch from the library's private memory pool of the current device (host.cpp;
+// the device's default pool is not touched): released memory stays in the pool for the next call.
+hipError_t pool_alloc(void** p, size_t bytes, hipStream_t s);
+void pool_free(void* p, hipStream_t s);
 
 // sct_tune_set value of `key`, or dflt when unset (host.cpp).
 int64_t tune(int key, int64_t dflt);
