@@ -572,23 +572,27 @@ def path_whitelist(dev, reps, copy_gbs):
     stream = torch.cuda.current_stream(dev).cuda_stream
     nl, mx = ctypes.c_int64(0), ctypes.c_int32(0)
 
-    def ingest():
-        _lib.check(lib.sct_lines(buf.data_ptr(), nbytes, n, starts.data_ptr(), lens.data_ptr(), ctypes.byref(nl),
-                                 ctypes.byref(mx), stream))
-        _lib.check(lib.sct_encode_var(2, buf.data_ptr(), starts.data_ptr(), lens.data_ptr(), nl.value, 1,
-                                      codes.data_ptr(), gc.data_ptr(), flags.data_ptr(), stream))
+    d_n = torch.zeros(1, dtype=torch.int64, device=dev)
+    d_mx = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def ingest():  # one pass, asynchronous (the count and the longest line stay on the device)
+        _lib.check(lib.sct_whitelist_encode(buf.data_ptr(), nbytes, 2, 1, n, codes.data_ptr(), starts.data_ptr(),
+                                            lens.data_ptr(), gc.data_ptr(), flags.data_ptr(), d_n.data_ptr(),
+                                            d_mx.data_ptr(), stream))
 
     def basefreq():
         _lib.check(lib.sct_base_frequency(codes.data_ptr(), n, L, freq.data_ptr(), stream))
     ms_in = _events_ms(ingest, reps, dev)
     ms_bf = _events_ms(basefreq, reps, dev)
     torch.cuda.synchronize()
+    nl.value, mx.value = int(d_n.item()), int(d_mx.item())
     want = torch.from_numpy(codes_h.view(np.int64)).to(dev)
     want_gc = torch.from_numpy(((text[:, :L] == ord("C")) | (text[:, :L] == ord("G"))).sum(1).astype(np.uint8)).to(dev)
     ok_in = nl.value == n and mx.value == L and torch.equal(codes, want) and torch.equal(gc, want_gc) \
-        and not bool(flags.any())
+        and not bool(flags.any()) and torch.equal(starts, torch.arange(n, device=dev) * (L + 1)) \
+        and bool((lens == L).all())
     ok_bf = np.array_equal(freq.cpu().numpy().view(np.uint64).reshape(L, 4), O.base_frequency_numpy(codes_h, L))
-    algo_in = nbytes + n * (8 + 1 + 1)
+    algo_in = nbytes + n * (8 + 8 + 4 + 1 + 1)
     algo_bf = 8 * n
     del buf, starts, lens, codes, gc, flags, freq
     torch.cuda.empty_cache()
@@ -602,11 +606,11 @@ def path_whitelist(dev, reps, copy_gbs):
                 "workload": "config 5's whitelist file: %d lines of 16 bases + LF (%d bytes, device-resident): "
                             "line split (line[:-1]) + TwoBit encode + GC" % (n, nbytes),
                 "value": n / (ms_in * 1e-3), "unit": "lines/s", "ms": ms_in, "reps": reps,
-                "roofline": roof(algo_in, ms_in, "sct_lines + sct_encode_var",
-                                 "algorithmic bytes: the file once + codes / GC / flags; sct_lines returns the "
-                                 "line count to the host (one sync per call), inside the timed region"),
-                "check": {"every_line": ok_in, "sample": "all %d codes and GC counts vs the generating codes, "
-                                                         "no flags" % n}},
+                "roofline": roof(algo_in, ms_in, "sct_whitelist_encode (whitelist_fused_kernel, one pass)",
+                                 "algorithmic bytes: the file once + codes / starts / lens / GC / flags; one "
+                                 "kernel with a decoupled look-back for the line numbers, no host sync"),
+                "check": {"every_line": ok_in, "sample": "all %d codes, GC counts, starts and lengths vs the "
+                                                         "generating codes, no flags" % n}},
             "base_frequency": {
                 "workload": "base_frequency over config 5's %d 16-bp codes (device-resident)" % n,
                 "value": n / (ms_bf * 1e-3), "unit": "codes/s", "ms": ms_bf, "reps": reps,
@@ -699,19 +703,19 @@ def path_fastq(dev, reps, copy_gbs):
     flags = torch.empty(n_rec, dtype=torch.uint8, device=dev)
     lib = _lib.lib()
     stream = torch.cuda.current_stream(dev).cuda_stream
-    box = {}
+    d_ends = torch.tensor([nbytes], dtype=torch.int64, device=dev)
+    status = torch.zeros(3, dtype=torch.int64, device=dev)
+    spans = np.array([[0, 16], [16, 24]], dtype=np.int32)
 
-    def run():
-        ix = _lib.FastqIndex(buf.data_ptr(), nbytes, [nbytes], False, stream)
-        ix.extract_spans(buf.data_ptr(), [(0, 16), (16, 24)], seqs.data_ptr(), quals.data_ptr(), stream=stream)
-        _lib.check(lib.sct_encode(2, _lib._vp(cb.data_ptr()), n_rec, 16, 16, _lib._vp(codes.data_ptr()),
-                                  _lib._vp(gc.data_ptr()), _lib._vp(flags.data_ptr()), _lib._vp(stream)))
-        box["n"] = ix.nrecords
-        ix.close()
+    def run():  # one pass: index + CB / UMI slices + the CB encode, asynchronous (no host sync)
+        _lib.check(lib.sct_fastq_extract_fused(
+            buf.data_ptr(), nbytes, d_ends.data_ptr(), 1, 0, spans.ctypes.data, 2, n_rec, seqs.data_ptr(),
+            quals.data_ptr(), None, None, codes.data_ptr(), gc.data_ptr(), flags.data_ptr(), status.data_ptr(), stream))
     ms = _events_ms(run, reps, dev)
     i = torch.randint(0, n_rec, (256,), device=dev, generator=g)
-    ok = box["n"] == n_rec and torch.equal(cb[i], rec[i, 13:29]) and torch.equal(umi[i], rec[i, 29:37]) \
-        and torch.equal(quals[:n_rec * 16].view(n_rec, 16)[i], rec[i, 42:58])
+    st = status.cpu().tolist()
+    ok = st[0] == 4 * n_rec and st[1] == 0 and torch.equal(cb[i], rec[i, 13:29]) and torch.equal(umi[i], rec[i, 29:37]) \
+        and torch.equal(quals[:n_rec * 16].view(n_rec, 16)[i], rec[i, 42:58]) and not bool(flags.any())
     host = cb[i].cpu().numpy()
     ok = ok and [O.two_bit_encode(bytes(r)) for r in host] == [int(x) for x in codes[i].cpu().numpy().view(np.uint64)]
     algo = nbytes + n_rec * (16 + 8) * 2 + n_rec * (8 + 1 + 1)  # FASTQ once + slices + codes / GC / flags
@@ -723,9 +727,10 @@ def path_fastq(dev, reps, copy_gbs):
             "value": n_rec / (ms * 1e-3), "unit": "records/s", "ms": ms, "reps": reps,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
                          "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs,
-                         "algo_bytes_per_record": algo / n_rec, "kernel": "count_kernel + extract2_kernel",
-                         "note": "algorithmic bytes: the FASTQ once + the slices + codes; the index reads the "
-                                 "buffer a second time and syncs once for its record count (DESIGN.md §3.6)"},
+                         "algo_bytes_per_record": algo / n_rec, "kernel": "fastq_fused_kernel (sct_fastq_extract_fused)",
+                         "note": "algorithmic bytes: the FASTQ once + the slices + codes; one kernel reads the "
+                                 "buffer once (decoupled look-back for the line numbers, the CB encode fused), "
+                                 "no host sync (DESIGN.md §3.6)"},
             "check": {"sampled": ok, "sample": "256 random records: CB / UMI / CB-quality slices equal the "
                                                "record bytes, CB codes vs oracle.two_bit_encode"}}
 

@@ -52,7 +52,8 @@ int sct_set_device(int device);        /* select the device for later calls (hip
 #define SCT_TUNE_SCALAR_IDLE_MS 9       /* the scalar server exits after this idle time (5) */
 #define SCT_TUNE_SPECTRAL_COLUMNS 10   /* SPECTRAL column width: 0 auto, 14, or 16 (when int8 fits) */
 #define SCT_TUNE_PLAN_CACHE 11          /* 0: every all-pairs plan allocates its own buffers (default 1) */
-#define SCT_TUNE_NKEYS 12
+#define SCT_TUNE_ENCODE_GRID 12         /* tiled encoder grid: 0 resident workgroups (default), 1 one per tile */
+#define SCT_TUNE_NKEYS 13
 int sct_tune_set(int key, int64_t value);
 int sct_tune_get(int key, int64_t* value);  /* -1 when unset */
 
@@ -100,6 +101,14 @@ int sct_encode_var(int kind, const uint8_t* buf, const int64_t* starts, const in
  * call with max_lines = 0 to learn nlines and max_len, then with room for nlines. */
 int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines, int64_t* d_starts, int32_t* d_lens,
               int64_t* nlines, int32_t* max_len, void* stream);
+/* sct_whitelist_encode (device, ASYNCHRONOUS on stream: no host synchronisation): the same
+ * split, chop and encode in one pass over the file (a decoupled look-back numbers the lines);
+ * *d_nlines (int64) and *d_maxlen (int32, the longest chopped line) are written on the device;
+ * lines g < max_lines get d_starts[g], d_lens[g], `words` limbs of d_codes, d_gc[g] (nullable)
+ * and d_flags[g] (nullable: bit 0 ambiguous, bit 1 invalid byte, bit 2 too long for `words`). */
+int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int kind, int words, int64_t max_lines,
+                         uint64_t* d_codes, int64_t* d_starts, int32_t* d_lens, uint8_t* d_gc, uint8_t* d_flags,
+                         int64_t* d_nlines, int32_t* d_maxlen, void* stream);
 int sct_whitelist_encode_host(const uint8_t* buf, int64_t nbytes, int kind, int words, int64_t max_lines,
                               int64_t* nlines, int32_t* max_len, uint64_t* codes, int64_t* starts,
                               int32_t* lens, uint8_t* flags);
@@ -380,6 +389,17 @@ int sct_fastq_index_info(const sct_fastq_index* index, int64_t* nrecords, int64_
 int sct_fastq_extract_spans(sct_fastq_index* index, const uint8_t* d_buf, const int32_t* spans,
                             int nspans, uint8_t* d_seq, uint8_t* d_qual, int32_t* d_seq_len,
                             int32_t* d_qual_len, int64_t* first_bad_name, void* stream);
+/* One pass (index + extraction in one read of the buffer, asynchronous on `stream`, no host
+ * synchronisation): d_file_ends is DEVICE memory; rows are laid out by the caller's capacity
+ * (span k's row r at out + cap_records * prefix_k + r * width_k; lengths at len + k * cap + r);
+ * d_status (3 int64, device): [0] line count (records = lines / 4; rows of an incomplete trailing
+ * record are not meaningful), [1] ~(first bad-name record) or 0, [2] non-ASCII seen (text mode
+ * rejects it).  d_codes0 / d_gc0 / d_flags0 (nullable): span 0's sequence rows TwoBit-encoded
+ * (width <= 32) as sct_encode would encode those rows. */
+int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, const int64_t* d_file_ends, int nfiles,
+                            int text_mode, const int32_t* spans, int nspans, int64_t cap_records, uint8_t* d_seq,
+                            uint8_t* d_qual, int32_t* d_seq_len, int32_t* d_qual_len, uint64_t* d_codes0,
+                            uint8_t* d_gc0, uint8_t* d_flags0, int64_t* d_status, void* stream);
 /* Host convenience: spans = nspans (start, end) pairs.  Call with max_records < the record
  * count to learn nrecords (outputs untouched); then with room for nrecords:
  * seq_out/qual_out (nullable) = span k's rows at offset sum_{i<k} nrecords*width_i,

@@ -31,7 +31,8 @@ SCHEME_SPECTRAL = 2
 # launch-shape knobs (sct_tune_set; none changes a result)
 TUNE_KEYS = {"spectral_chunk": 1, "spectral_min_n": 2, "allpairs_grab": 3, "allpairs_flush_items": 4,
              "allpairs_grid": 5, "nearest_scheme": 6, "nearest_load": 7, "scalar_server": 8,
-             "scalar_idle_ms": 9, "spectral_columns": 10, "plan_cache": 11}
+             "scalar_idle_ms": 9, "spectral_columns": 10, "plan_cache": 11,
+             "encode_grid": 12}
 NEAREST_AUTO, NEAREST_OA, NEAREST_CSR, NEAREST_HALVES = 0, 1, 2, 3
 
 _i32, _i64, _dbl = ctypes.c_int, ctypes.c_int64, ctypes.c_double
@@ -51,6 +52,7 @@ SIGNATURES = {
     "sct_encode_stream_host": [_i32, _vp, _i64, _i32, _vp, _vp, _vp, _i64],
     "sct_encode_var": [_i32, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp],
     "sct_lines": [_vp, _i64, _i64, _vp, _vp, ctypes.POINTER(_i64), ctypes.POINTER(_i32), _vp],
+    "sct_whitelist_encode": [_vp, _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "sct_whitelist_encode_host": [_vp, _i64, _i32, _i32, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i32), _vp,
                                   _vp, _vp, _vp],
     "sct_decode2": [_vp, _i64, _i32, _i32, _vp, _vp],
@@ -101,6 +103,8 @@ SIGNATURES = {
     "sct_fastq_extract_host": [_vp, _i64, _vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _i64,
                                ctypes.POINTER(_i64), ctypes.POINTER(_i64)],
     "sct_base_frequency_host": [_vp, _i64, _i32, _vp],
+    "sct_fastq_extract_fused": [_vp, _i64, _vp, _i32, _i32, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                _vp, _vp],
     "sct_fastq_stream_create": [_i32, _vp, _i32, _i32, ctypes.POINTER(_vp)],
     "sct_fastq_stream_destroy": [_vp],
     "sct_fastq_stream_chunk": [_vp, _vp, _i64, _vp, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_i64),

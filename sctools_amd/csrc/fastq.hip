@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "sct_common.h"
+#include "encode_common.h"
 
 namespace {
 
@@ -433,6 +434,238 @@ __global__ __launch_bounds__(WG) void extract2_kernel(const uint8_t* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- one pass (round 4)
+// fastq_fused_kernel: the index and the extraction in ONE read of the buffer.  Each tile (one
+// per workgroup, dynamic ids) numbers its terminators with a decoupled look-back over its
+// predecessors' terminator counts (as lines.hip's whitelist ingest) instead of a count pass +
+// scan + host synchronisation; the rest is extract2_kernel's per-line work, except that
+//   - the record count is unknown while the tile runs: every line's slices are written (rows
+//     of records >= cap skipped), the output is laid out by the caller's capacity cap
+//     (span k's row r at out + cap * prefix_k + r * width_k), and the line count goes to
+//     d_status[0] (records = lines / 4; rows of an incomplete trailing record are garbage);
+//   - a tile's last line ends at the next tile's first terminator, which is found by the
+//     bounded scan (at most the spans' end bytes) instead of the count pass's table;
+//   - a bad name is reported as the max of ~record (d_status[1], 0 = none), so the host can
+//     drop one that lies in the incomplete trailing record;
+//   - optionally span 0's sequence rows are TwoBit-encoded as they are written (one limb,
+//     width <= 32; gc and flags as sct_encode over those rows), instead of a second kernel.
+struct FqStatus {
+  unsigned long long flag, agg, incl;  // flag 1: agg published, 2: incl (the inclusive count) too
+};
+
+__global__ __launch_bounds__(WG) void fastq_fused_kernel(
+    const uint8_t* __restrict__ buf, int64_t n, Files fs, int text, FqStatus* __restrict__ status,
+    unsigned* __restrict__ ctr, int64_t ntiles, int64_t cap, Spans sp, uint8_t* __restrict__ seq_out,
+    uint8_t* __restrict__ qual_out, int32_t* __restrict__ seq_len, int32_t* __restrict__ qual_len,
+    uint64_t* __restrict__ codes0, uint8_t* __restrict__ gc0, uint8_t* __restrict__ flags0,
+    unsigned long long* __restrict__ d_status) {
+  __shared__ uint16_t term[MAX_TERM];
+  __shared__ uint4 tile_bytes[TILE / 16];
+  __shared__ uint32_t w_cnt[WG / 64];
+  __shared__ int64_t s_tile;
+  __shared__ unsigned long long s_g0;
+  __shared__ uint8_t lut[256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_tile = (int64_t)atomicAdd(ctr, 1u);
+  if (codes0)
+    for (int c = tid; c < 256; c += WG) lut[c] = lut_entry(2, c);
+  __syncthreads();
+  const int64_t tile = s_tile, t0 = tile * TILE, p0 = t0 + (int64_t)tid * TB;
+  uint4 cur[SEG];
+#pragma unroll
+  for (int k = 0; k < SEG; ++k) cur[k] = load16(buf, n, p0 + 16 * k);
+  bool ends_here;
+  {  // a file end in this tile (wave-uniform): the first file ending after t0
+    int lo = 0, hi = fs.nfiles;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (fs.ends[mid] <= t0) lo = mid + 1; else hi = mid;
+    }
+    ends_here = lo < fs.nfiles && fs.ends[lo] <= t0 + TILE + 16;
+  }
+  Span spn{0, 0, 0, 0};
+  if (p0 < n) spn = thread_span(buf, n, fs, text, p0, cur, ends_here);
+  if (spn.na) atomicOr(reinterpret_cast<unsigned*>(d_status + 2), 1u);
+#pragma unroll
+  for (int k = 0; k < SEG; ++k) tile_bytes[tid * SEG + k] = p0 + 16 * k < n ? cur[k] : make_uint4(0, 0, 0, 0);
+  const uint32_t tbits = spn.m | spn.vbits, c = __popc(tbits);
+  uint32_t ic = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t a = __shfl_up(ic, d);
+    if (lane >= d) ic += a;
+  }
+  if (lane == 63) w_cnt[wave] = ic;
+  __syncthreads();
+  uint32_t pre = ic - c, ntile = 0;
+#pragma unroll
+  for (int w = 0; w < WG / 64; ++w) {
+    if (w < wave) pre += w_cnt[w];
+    ntile += w_cnt[w];
+  }
+  {
+    uint32_t bits = tbits, at = pre;
+    while (bits) {
+      const int j = __ffs(bits) - 1;
+      bits &= bits - 1;
+      const uint32_t off = (uint32_t)(tid * TB + j);
+      term[at++] = (spn.m >> j & 1u) ? (uint16_t)(off | ((spn.crlf >> j & 1u) ? T16_CRLF : 0u))
+                                     : (uint16_t)((off + 1) | T16_VIRT);  // the file ends after byte off
+    }
+  }
+  if (wave == 0) {  // the look-back: terminators before this tile
+    FqStatus* me = status + tile;
+    unsigned long long excl = 0;
+    if (tile == 0) {
+      if (lane == 0) {
+        __hip_atomic_store(&me->incl, (unsigned long long)ntile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&me->flag, 2ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      if (lane == 0) {
+        __hip_atomic_store(&me->agg, (unsigned long long)ntile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&me->flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      for (int64_t base = tile - 1;; base -= 64) {
+        const int64_t k = base - lane;
+        unsigned long long f = 2, v = 0;
+        if (k >= 0) {
+          do {
+            f = __hip_atomic_load(&status[k].flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          } while (f == 0);
+          v = __hip_atomic_load(f == 2 ? &status[k].incl : &status[k].agg, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const unsigned long long incl = __ballot(f == 2);
+        const int stop = incl ? __ffsll((long long)incl) - 1 : 63;
+        if (lane > stop) v = 0;
+#pragma unroll
+        for (int sh = 32; sh; sh >>= 1) v += __shfl_xor(v, sh);
+        excl += v;
+        if (incl) break;
+      }
+      if (lane == 0) {
+        __hip_atomic_store(&me->incl, excl + ntile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&me->flag, 2ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (lane == 0) {
+      s_g0 = excl;
+      if (tile == ntiles - 1) d_status[0] = excl + ntile;  // every line ends at a terminator
+    }
+  }
+  __syncthreads();
+  const int64_t g0 = (int64_t)s_g0;
+  const uint8_t* tile8 = reinterpret_cast<const uint8_t*>(tile_bytes);
+  const uint32_t* tile32 = reinterpret_cast<const uint32_t*>(tile_bytes);
+  if (tile == 0 && tid == 0 && n > 0 && buf[0] != '@') atomicMax(d_status + 1, ~0ull);  // record 0
+  const int tmax = (int)ntile;
+  // name lines: after terminators g = 3 (mod 4)
+  for (int t = (int)((3 - (g0 & 3)) & 3) + 4 * tid; t < tmax; t += 4 * WG) {
+    const uint32_t e = term[t];
+    const int64_t o = (int64_t)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // the line's start in the tile
+    if (t0 + o >= n) continue;  // no line after the buffer's last terminator
+    const uint8_t ch = o < TILE ? tile8[o] : buf[t0 + o];
+    if (ch != '@') atomicMax(d_status + 1, ~(unsigned long long)((g0 + t + 1) >> 2));
+  }
+  // sequence / quality lines: after even terminators; one item per line, its spans in turn
+  const int te0 = (int)(g0 & 1);
+  const int nact = tmax > te0 ? (tmax - te0 + 1) / 2 : 0;
+  for (int a = tid; a < nact; a += WG) {
+    const int t = te0 + 2 * a;
+    const int64_t line = g0 + t + 1, rec = line >> 2;
+    const uint32_t e = term[t];
+    const int start = (int)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // <= TILE
+    if (rec >= cap || t0 + start >= n) continue;
+    const bool is_seq = (line & 3) == 1;
+    int64_t cend;  // content end relative to the tile start
+    int nl;
+    if (t + 1 < tmax) {  // the line ends at the tile's next terminator
+      const uint32_t f = term[t + 1];
+      cend = (int64_t)(f & T16_OFF) - ((f & T16_CRLF) ? 1 : 0);
+      nl = (f & T16_VIRT) ? 0 : 1;
+    } else {  // the tile's last line: scan (max_end bytes, within its file)
+      const int64_t next = t0 + start;
+      int lo = 0, hi = fs.nfiles;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (fs.ends[mid] <= next) lo = mid + 1; else hi = mid;
+      }
+      const int64_t fe = lo < fs.nfiles ? fs.ends[lo] : n;
+      const int64_t lim = next + sp.max_end < fe ? next + sp.max_end : fe;
+      cend = lim - t0;
+      nl = lim == fe ? 0 : 1;  // longer than the window: its end is irrelevant
+      for (int64_t i = next; i < lim; ++i) {
+        const uint8_t ch = buf[i];
+        if (ch == '\n' || (text && ch == '\r')) {
+          cend = i - t0;
+          nl = 1;
+          break;
+        }
+      }
+    }
+    int32_t* len = is_seq ? seq_len : qual_len;
+    uint8_t* out = is_seq ? seq_out : qual_out;
+    const int64_t clen = cend - start, llen = clen + nl;
+    for (int k = 0; k < sp.n; ++k) {
+      const int64_t sa = sp.start[k] < llen ? sp.start[k] : llen, sb = sp.end[k] < llen ? sp.end[k] : llen;
+      if (len) len[k * cap + rec] = (int32_t)(sb - sa);
+      if (!out) continue;
+      const int w = sp.end[k] - sp.start[k];
+      uint8_t* o = out + sp.prefix[k] * cap + rec * w;
+      const uint8_t* src = buf + t0 + start;
+      const int64_t s0 = t0 + start + sa;
+      const int64_t base = s0 & ~3LL;
+      const int nd = w / 4;
+      if (sb - sa == w && sb <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
+          ((uintptr_t)o & 3) == 0) {
+        const uint32_t* d = base + 4 * (nd + 1) <= t0 + TILE ? tile32 + ((base - t0) >> 2)
+                                                             : reinterpret_cast<const uint32_t*>(buf + base);
+        const uint32_t sh = (uint32_t)(s0 & 3);
+        uint32_t* od = reinterpret_cast<uint32_t*>(o);
+        if (nd == 4 && ((uintptr_t)o & 15) == 0) {
+          const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3], x4 = d[4];
+          *reinterpret_cast<uint4*>(o) =
+              make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                         __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+        } else if (nd == 2 && ((uintptr_t)o & 7) == 0) {
+          const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
+          *reinterpret_cast<uint2*>(o) =
+              make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
+        } else {
+          uint32_t lo = d[0];
+          for (int q2 = 0; q2 < nd; ++q2) {
+            const uint32_t hi = d[q2 + 1];
+            od[q2] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            lo = hi;
+          }
+        }
+      } else {
+#pragma unroll 8
+        for (int j = 0; j < w; ++j) {
+          const int64_t i = sa + j;
+          o[j] = i < sb ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
+        }
+      }
+      if (k == 0 && is_seq && codes0) {  // span 0's row (as written, zero-padded) -> TwoBit
+        uint64_t code = 0;
+        uint32_t fl = 0;
+        for (int j = 0; j < w; ++j) {
+          const uint32_t en = lut[o[j]];
+          code = (code << 2) | (en & 7u);
+          fl |= en;
+        }
+        codes0[rec] = code;
+        if (gc0) {
+          const uint32_t g = (uint32_t)__popcll(code & 0x5555555555555555ull);
+          gc0[rec] = (uint8_t)(g > 255 ? 255 : g);
+        }
+        if (flags0) flags0[rec] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
+      }
+    }
+  }
+}
+
 // grid of the persistent tile kernels: every resident workgroup slot once (at most ntiles)
 unsigned resident_grid(const void* kernel, int64_t ntiles) {
   sct::scalar_quiesce();
@@ -658,6 +891,57 @@ namespace {
     if (rc_ != SCT_OK) return rc_; \
   } while (0)
 }  // namespace
+
+// One pass (fastq_fused_kernel), asynchronous on `stream`: the concatenated files in d_buf,
+// their cumulative ends in d_file_ends (DEVICE memory, nfiles entries, the last = nbytes).
+// Rows are laid out by cap_records (span k's row r at out + cap * prefix_k + r * width_k, its
+// length at len + k * cap + r); d_status (3 x int64, device) receives the line count
+// (records = lines / 4), ~(first bad-name record) or 0, and a text-mode non-ASCII flag.
+// d_codes0 / d_gc0 / d_flags0 (nullable): span 0's sequence rows TwoBit-encoded (width <= 32).
+extern "C" int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, const int64_t* d_file_ends, int nfiles,
+                                       int text_mode, const int32_t* spans, int nspans, int64_t cap_records,
+                                       uint8_t* d_seq, uint8_t* d_qual, int32_t* d_seq_len, int32_t* d_qual_len,
+                                       uint64_t* d_codes0, uint8_t* d_gc0, uint8_t* d_flags0, int64_t* d_status,
+                                       void* stream) {
+  SCT_CHECK(d_status != nullptr && nfiles >= 1 && d_file_ends != nullptr, "bad arguments");
+  SCT_CHECK(nbytes >= 0 && (nbytes == 0 || d_buf != nullptr) && cap_records >= 0, "bad buffer");
+  SCT_CHECK(nspans >= 0 && nspans <= MAX_SPANS && (nspans == 0 || spans), "0..%d spans", MAX_SPANS);
+  Spans sp{};
+  sp.n = nspans;
+  int64_t pre = 0;
+  for (int k = 0; k < nspans; ++k) {
+    SCT_CHECK(0 <= spans[2 * k] && spans[2 * k] <= spans[2 * k + 1] && spans[2 * k + 1] <= 4096,
+              "span %d = [%d, %d) unsupported", k, spans[2 * k], spans[2 * k + 1]);
+    sp.start[k] = spans[2 * k];
+    sp.end[k] = spans[2 * k + 1];
+    sp.prefix[k] = pre;
+    sp.max_end = std::max(sp.max_end, sp.end[k]);
+    pre += sp.end[k] - sp.start[k];
+  }
+  sp.width = (int)pre;
+  SCT_CHECK(!d_codes0 || (nspans >= 1 && sp.end[0] - sp.start[0] <= 32 && d_seq), "span 0 encode needs width <= 32");
+  hipStream_t s = sct::as_stream(stream);
+  SCT_HIP(hipMemsetAsync(d_status, 0, 24, s));
+  if (nbytes == 0) return SCT_OK;
+  const int64_t ntiles = sct::ceil_div(nbytes, TILE);
+  SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
+  void* scratch = nullptr;
+  const size_t sbytes = (size_t)ntiles * sizeof(FqStatus) + 256;
+  SCT_HIP(sct::pool_alloc(&scratch, sbytes, s));
+  hipError_t e = hipMemsetAsync(scratch, 0, sbytes, s);
+  if (e == hipSuccess) {
+    FqStatus* st = reinterpret_cast<FqStatus*>(scratch);
+    unsigned* ctr = reinterpret_cast<unsigned*>(reinterpret_cast<uint8_t*>(scratch) + (size_t)ntiles * sizeof(FqStatus));
+    hipLaunchKernelGGL(fastq_fused_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes,
+                       Files{d_file_ends, nfiles}, text_mode ? 1 : 0, st, ctr, ntiles, cap_records, sp, d_seq,
+                       d_qual, d_seq_len, d_qual_len, d_codes0, d_gc0, d_flags0,
+                       reinterpret_cast<unsigned long long*>(d_status));
+    e = hipGetLastError();
+  }
+  sct::pool_free(scratch, s);
+  if (e != hipSuccess) return sct::fail(SCT_E_HIP, "fastq fused: %s", hipGetErrorString(e));
+  return SCT_OK;
+}
 
 extern "C" int sct_fastq_extract_host(const uint8_t* buf, int64_t nbytes, const int64_t* file_ends,
                                       int nfiles, int text_mode, const int32_t* spans, int nspans,

@@ -8,16 +8,18 @@
 // last byte ('\n', or the file's last byte), line g's chopped content is
 // [P_{g-1} + 1, P_g): start = P_{g-1} + 1 (0 for g = 0), length = P_g - start.
 //
-// Two passes over 4 KiB tiles (16 bytes per thread, SWAR '\n' compares): count each tile's
-// line ends, exclusive-scan them into every tile's first line number, then store every end
-// as the next line's start; the lengths follow from consecutive starts.  The
-// variable-length TwoBit/ThreeBit encoder (sct_encode_var) packs the lines straight from
-// the file bytes.
+// sct_whitelist_encode (the ingest Barcodes.from_whitelist takes, round 4): ONE pass over 4 KiB
+// tiles (16 bytes per thread, SWAR '\n' compares) with a decoupled look-back for the line
+// numbers, each line encoded from the file bytes by the lane holding its end (below).
+// sct_lines (kept for callers that want only the spans): two passes -- count each tile's line
+// ends, exclusive-scan them, then store every end as the next line's start; the lengths follow
+// from consecutive starts.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 
 #include "sct_common.h"
+#include "encode_common.h"
 
 namespace {
 
@@ -105,6 +107,209 @@ __global__ __launch_bounds__(WG) void line_lens_kernel(const int64_t* __restrict
   }
 }
 
+// ---------------------------------------------------------------- one-pass ingest (round 4)
+// sct_whitelist_encode: the line split, the [:-1] chop and the encoder in ONE kernel over 4 KiB
+// tiles that reads the file once.  Tiles take dynamic ids (so a tile's predecessors are running
+// or done) and find the line count and the last line end before them by a decoupled look-back
+// (Merrill & Garland's single-pass scan): each tile publishes its aggregate (line ends, last end
+// position), then a wave reads up to 64 predecessors' status words at once, summing aggregates
+// back to the nearest tile whose inclusive prefix is published, and publishes its own inclusive
+// prefix.  Line g ends at the g-th line end P_g (a '\n', or the file's last byte) and its
+// chopped content is [P_{g-1} + 1, P_g): each lane encodes the lines ending in its 16 bytes,
+// the first one starting after the latest end before the lane (an exclusive max-scan).  The
+// line count and the longest line stay on the device: no host synchronisation.
+// A tile's aggregate and inclusive prefix live in separate words: a reader that saw the
+// aggregate flag must still read the aggregate after the owner has published its inclusive
+// prefix (one shared value word would hand it the inclusive count as if it were the aggregate).
+struct TileStatus {
+  unsigned long long flag;  // 0 none, 1 aggregate, 2 inclusive prefix
+  unsigned long long agg_count;
+  long long agg_last;       // position of the tile's last line end, -1 if none
+  unsigned long long incl_count;
+  long long incl_last;      // the last line end up to the tile's end, -1 if none
+};
+constexpr unsigned long long kAgg = 1, kIncl = 2;
+
+__device__ __forceinline__ void publish(TileStatus* st, unsigned long long flag, unsigned long long count,
+                                        long long last) {
+  unsigned long long* c = flag == kIncl ? &st->incl_count : &st->agg_count;
+  long long* l = flag == kIncl ? &st->incl_last : &st->agg_last;
+  __hip_atomic_store(c, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(l, last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&st->flag, flag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one record [rec, rec + L) through the LUT: the one-limb dword path of encode_var_kernel
+// (encode.hip) for L <= 32, else the generic limb loop; too long for `words` limbs: flag 4
+template <int KIND>
+__device__ __forceinline__ void encode_line(const uint8_t* lut, const uint8_t* rec, int L, int words, uint64_t* out,
+                                            uint32_t& g, uint32_t& fl) {
+  constexpr uint64_t gcm = KIND == 2 ? 0x5555555555555555ull : 0x9249249249249249ull;
+  if ((int64_t)KIND * L > 64 * (int64_t)words) {
+    for (int w = 0; w < words; ++w) out[w] = 0;
+    g = 0;
+    fl = 4;
+    return;
+  }
+  if (words == 1 && L <= 32) {
+    uint64_t code = 0;
+    uint32_t f = 0;
+    if (L > 0) {
+      const int o = (int)((uintptr_t)rec & 3), o8 = 8 * o;
+      const uint32_t* dw = reinterpret_cast<const uint32_t*>(rec - o);
+      uint32_t d[9], w[8];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {  // dword k of the record, clamped to its last one
+        const int kk = 4 * k < o + L ? k : (o + L - 1) >> 2;
+        d[k] = dw[kk];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) w[k] = (uint32_t)((((uint64_t)d[k + 1] << 32) | d[k]) >> o8);
+#pragma unroll
+      for (int p = 0; p < 32; ++p)
+        if (p < L) {
+          const uint32_t e = lut[(w[p >> 2] >> (8 * (p & 3))) & 0xFFu];
+          code = (code << KIND) | (e & 7u);
+          f |= e;
+        }
+    }
+    out[0] = code;
+    g = (uint32_t)__popcll(code & gcm);
+    fl = ((f & F_AMBIG) ? 1u : 0u) | ((f & F_INVALID) ? 2u : 0u);
+    return;
+  }
+  RecordReader rd{rec, false, 0u, -1};
+  encode_record(lut, KIND, rd, L, words, out, g, fl);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(WG) void whitelist_fused_kernel(
+    const uint8_t* __restrict__ buf, int64_t n, int64_t ntiles, TileStatus* __restrict__ status,
+    unsigned* __restrict__ tile_ctr, int64_t cap, int words, uint64_t* __restrict__ codes,
+    int64_t* __restrict__ starts, int32_t* __restrict__ lens, uint8_t* __restrict__ gc, uint8_t* __restrict__ flags,
+    unsigned long long* __restrict__ d_nlines, int32_t* __restrict__ d_maxlen) {
+  __shared__ uint8_t lut[256];
+  __shared__ int64_t s_tile;
+  __shared__ uint32_t w_cnt[WG / 64];
+  __shared__ long long w_last[WG / 64];
+  __shared__ unsigned long long s_excl;
+  __shared__ long long s_excl_last;
+  __shared__ int32_t w_max[WG / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  for (int c = t; c < 256; c += WG) lut[c] = lut_entry(KIND, c);
+  if (t == 0) s_tile = (int64_t)atomicAdd(tile_ctr, 1u);
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t p0 = tile * TILE + t * 16;
+  uint32_t m = p0 < n ? lf_mask(buf, n, p0) : 0u;
+  const uint32_t c = __popc(m);
+  const long long mylast = m ? p0 + 31 - __clz(m) : -1;
+  // wave-inclusive sum of c and max of mylast, then across the 4 waves
+  uint32_t ic = c;
+  long long il = mylast;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t a = __shfl_up(ic, d);
+    const long long b = __shfl_up(il, d);
+    if (lane >= d) {
+      ic += a;
+      il = max(il, b);
+    }
+  }
+  if (lane == 63) {
+    w_cnt[wave] = ic;
+    w_last[wave] = il;
+  }
+  __syncthreads();
+  uint32_t xc = ic - c, tot = 0;  // exclusive within the tile
+  long long xl = __shfl_up(il, 1), tlast = -1;
+  if (lane == 0) xl = -1;
+#pragma unroll
+  for (int w = 0; w < WG / 64; ++w) {
+    if (w < wave) {
+      xc += w_cnt[w];
+      xl = max(xl, w_last[w]);
+    }
+    tot += w_cnt[w];
+    tlast = max(tlast, w_last[w]);
+  }
+  if (wave == 0) {  // the look-back
+    TileStatus* me = status + tile;
+    unsigned long long excl = 0;
+    long long elast = -1;
+    if (tile == 0) {
+      if (lane == 0) publish(me, kIncl, tot, tlast);
+    } else {
+      if (lane == 0) publish(me, kAgg, tot, tlast);
+      bool found = false;
+      for (int64_t base = tile - 1;; base -= 64) {
+        const int64_t k = base - lane;
+        unsigned long long f = kIncl, cnt = 0;
+        long long last = -1;
+        if (k >= 0) {
+          do {
+            f = __hip_atomic_load(&status[k].flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          } while (f == 0);
+          const bool inc = f == kIncl;
+          cnt = __hip_atomic_load(inc ? &status[k].incl_count : &status[k].agg_count, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+          last = __hip_atomic_load(inc ? &status[k].incl_last : &status[k].agg_last, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const unsigned long long incl = __ballot(f == kIncl);
+        const int stop = incl ? __ffsll((long long)incl) - 1 : 63;  // nearest inclusive prefix
+        unsigned long long v = lane <= stop ? cnt : 0ull;
+#pragma unroll
+        for (int s = 32; s; s >>= 1) v += __shfl_xor(v, s);
+        excl += v;
+        if (!found) {  // the nearest predecessor with a line end (or an inclusive prefix's last)
+          const unsigned long long has = __ballot(lane <= stop && last >= 0);
+          if (has) {
+            elast = __shfl(last, __ffsll((long long)has) - 1);
+            found = true;
+          }
+        }
+        if (incl) break;
+      }
+      if (lane == 0) publish(me, kIncl, excl + tot, tlast >= 0 ? tlast : elast);
+    }
+    if (lane == 0) {
+      s_excl = excl;
+      s_excl_last = elast;
+    }
+  }
+  __syncthreads();
+  const uint64_t g0 = s_excl + xc;
+  long long prev = max(s_excl_last, xl);
+  int32_t mx = 0;
+  for (uint64_t g = g0; m; ++g) {
+    const int j = __ffs(m) - 1;
+    m &= m - 1;
+    const long long P = p0 + j, start = prev + 1;
+    const int32_t L = (int32_t)(P - start);
+    prev = P;
+    mx = max(mx, L);
+    if ((int64_t)g < cap) {
+      uint32_t gg, fl;
+      encode_line<KIND>(lut, buf + start, L, words, codes + g * words, gg, fl);
+      starts[g] = start;
+      lens[g] = L;
+      if (gc) gc[g] = (uint8_t)(gg > 255 ? 255 : gg);
+      if (flags) flags[g] = (uint8_t)fl;
+    }
+  }
+#pragma unroll
+  for (int s = 32; s; s >>= 1) mx = max(mx, __shfl_xor(mx, s));
+  if (lane == 0) w_max[wave] = mx;
+  __syncthreads();
+  if (t == 0) {
+#pragma unroll
+    for (int w = 1; w < WG / 64; ++w) mx = max(mx, w_max[w]);
+    if (mx > __hip_atomic_load(d_maxlen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(d_maxlen, mx);
+    if (tile == ntiles - 1) *d_nlines = s_excl + tot;
+  }
+}
+
 // Scratch of one call, allocated and freed in stream order from the library's private memory
 // pool (sct::pool_alloc: its memory stays in the pool, so repeated calls map nothing).
 struct StreamBuf {
@@ -175,6 +380,39 @@ extern "C" int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines
   return SCT_OK;
 }
 
+// One pass: lines + [:-1] chop + encode (whitelist_fused_kernel), asynchronous on `stream`: the
+// line count and the longest chopped line go to d_nlines / d_maxlen; lines g < max_lines are
+// written (starts, lens, words limbs of codes, gc and flags nullable; flags bit 2 = a line
+// too long for `words` limbs).
+extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int kind, int words, int64_t max_lines,
+                                    uint64_t* d_codes, int64_t* d_starts, int32_t* d_lens, uint8_t* d_gc,
+                                    uint8_t* d_flags, int64_t* d_nlines, int32_t* d_maxlen, void* stream) {
+  SCT_CHECK(kind == 2 || kind == 3, "kind must be 2 or 3");
+  SCT_CHECK(words >= 1 && d_nlines != nullptr && d_maxlen != nullptr, "bad arguments");
+  SCT_CHECK(nbytes >= 0 && (nbytes == 0 || d_buf != nullptr), "bad buffer");
+  SCT_CHECK(max_lines <= 0 || (d_codes && d_starts && d_lens), "NULL output");
+  hipStream_t s = sct::as_stream(stream);
+  SCT_HIP(hipMemsetAsync(d_maxlen, 0, 4, s));
+  if (nbytes == 0) {
+    SCT_HIP(hipMemsetAsync(d_nlines, 0, 8, s));
+    return SCT_OK;
+  }
+  const int64_t ntiles = sct::ceil_div(nbytes, TILE);
+  SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
+  const size_t sbytes = (size_t)ntiles * sizeof(TileStatus) + 256;
+  StreamBuf scratch;
+  SCT_HIP(scratch.alloc(sbytes, s));
+  SCT_HIP(hipMemsetAsync(scratch.p, 0, sbytes, s));
+  TileStatus* status = reinterpret_cast<TileStatus*>(scratch.p);
+  unsigned* ctr = reinterpret_cast<unsigned*>(reinterpret_cast<uint8_t*>(scratch.p) + (size_t)ntiles * sizeof(TileStatus));
+  const int64_t cap = max_lines > 0 ? max_lines : 0;
+  auto kern = kind == 2 ? whitelist_fused_kernel<2> : whitelist_fused_kernel<3>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, ntiles, status, ctr, cap, words,
+                     d_codes, d_starts, d_lens, d_gc, d_flags, reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen);
+  SCT_LAUNCH_CHECK();
+  return SCT_OK;
+}
+
 // Host convenience for Barcodes.from_whitelist: the file's bytes in, every line's [:-1]
 // encoded (kind 2 TwoBit / 3 ThreeBit) as `words` limbs, plus each line's start, chopped
 // length and flags (sct_encode's: bit 0 ambiguous base, bit 1 invalid byte).  Call with
@@ -188,43 +426,34 @@ extern "C" int sct_whitelist_encode_host(const uint8_t* buf, int64_t nbytes, int
   SCT_CHECK(nbytes >= 0 && (nbytes == 0 || buf), "bad buffer");
   sct::HostStage* st = sct::host_stage();
   if (!st) return SCT_E_HIP;
-  sct::DevBuf d_buf;
-  SCT_HIP(d_buf.alloc((size_t)nbytes));
-  if (nbytes) SCT_HIP(hipMemcpyAsync(d_buf.p, buf, (size_t)nbytes, hipMemcpyHostToDevice, st->stream));
-  int64_t n = 0;
-  int rc = sct_lines((const uint8_t*)d_buf.p, nbytes, 0, nullptr, nullptr, &n, max_len, st->stream);
+  // device: the file, then (a filling call) starts, lens, codes, flags, then the count and the longest
+  const int64_t cap = max_lines > 0 ? max_lines : 0;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t oS = al((size_t)nbytes), oL = oS + al((size_t)cap * 8), oC = oL + al((size_t)cap * 4);
+  const size_t oF = oC + al((size_t)cap * words * 8), oN = oF + al((size_t)cap), total = oN + 256;
+  if (int rc = sct::stage_reserve(st, 64, total); rc != SCT_OK) return rc;
+  uint8_t* d = st->dev;
+  if (nbytes) SCT_HIP(hipMemcpyAsync(d, buf, (size_t)nbytes, hipMemcpyHostToDevice, st->stream));
+  int64_t* d_n = reinterpret_cast<int64_t*>(d + oN);
+  int32_t* d_mx = reinterpret_cast<int32_t*>(d + oN + 8);
+  int rc = sct_whitelist_encode(d, nbytes, kind, words, cap, reinterpret_cast<uint64_t*>(d + oC),
+                                reinterpret_cast<int64_t*>(d + oS), reinterpret_cast<int32_t*>(d + oL), nullptr,
+                                d + oF, d_n, d_mx, st->stream);
   if (rc != SCT_OK) return rc;
+  int64_t* h = reinterpret_cast<int64_t*>(st->pinned);
+  SCT_HIP(hipMemcpyAsync(h, d_n, 16, hipMemcpyDeviceToHost, st->stream));
+  SCT_HIP(hipStreamSynchronize(st->stream));
+  const int64_t n = h[0];
   *nlines = n;
-  if (max_lines < n || n == 0) {
-    if (n == 0) *max_len = 0;
-    if (max_lines < n) {  // the sizing call also needs the longest line
-      sct::DevBuf s0, l0;
-      SCT_HIP(s0.alloc((size_t)n * 8));
-      SCT_HIP(l0.alloc((size_t)n * 4));
-      int64_t n2 = 0;
-      rc = sct_lines((const uint8_t*)d_buf.p, nbytes, n, (int64_t*)s0.p, (int32_t*)l0.p, &n2, max_len, st->stream);
-      if (rc != SCT_OK) return rc;
-    }
-    return SCT_OK;
-  }
+  *max_len = n ? reinterpret_cast<int32_t*>(h + 1)[0] : 0;
+  if (cap < n || n == 0) return SCT_OK;  // a sizing call (or an empty file): outputs untouched
   SCT_CHECK(codes && starts && lens && flags, "NULL output");
-  sct::DevBuf ds, dl, dc, df;
-  SCT_HIP(ds.alloc((size_t)n * 8));
-  SCT_HIP(dl.alloc((size_t)n * 4));
-  SCT_HIP(dc.alloc((size_t)n * words * 8));
-  SCT_HIP(df.alloc((size_t)n));
-  int64_t n2 = 0;
-  rc = sct_lines((const uint8_t*)d_buf.p, nbytes, n, (int64_t*)ds.p, (int32_t*)dl.p, &n2, max_len, st->stream);
-  if (rc != SCT_OK) return rc;
   SCT_CHECK((int64_t)kind * *max_len <= (int64_t)words * 64, "words %d too few for lines of %d bases", words,
             *max_len);
-  rc = sct_encode_var(kind, (const uint8_t*)d_buf.p, (const int64_t*)ds.p, (const int32_t*)dl.p, n, words,
-                      (uint64_t*)dc.p, nullptr, (uint8_t*)df.p, st->stream);
-  if (rc != SCT_OK) return rc;
-  SCT_HIP(hipMemcpyAsync(codes, dc.p, (size_t)n * words * 8, hipMemcpyDeviceToHost, st->stream));
-  SCT_HIP(hipMemcpyAsync(starts, ds.p, (size_t)n * 8, hipMemcpyDeviceToHost, st->stream));
-  SCT_HIP(hipMemcpyAsync(lens, dl.p, (size_t)n * 4, hipMemcpyDeviceToHost, st->stream));
-  SCT_HIP(hipMemcpyAsync(flags, df.p, (size_t)n, hipMemcpyDeviceToHost, st->stream));
+  SCT_HIP(hipMemcpyAsync(codes, d + oC, (size_t)n * words * 8, hipMemcpyDeviceToHost, st->stream));
+  SCT_HIP(hipMemcpyAsync(starts, d + oS, (size_t)n * 8, hipMemcpyDeviceToHost, st->stream));
+  SCT_HIP(hipMemcpyAsync(lens, d + oL, (size_t)n * 4, hipMemcpyDeviceToHost, st->stream));
+  SCT_HIP(hipMemcpyAsync(flags, d + oF, (size_t)n, hipMemcpyDeviceToHost, st->stream));
   SCT_HIP(hipStreamSynchronize(st->stream));
   return SCT_OK;
 }

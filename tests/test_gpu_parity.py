@@ -1242,3 +1242,78 @@ def test_lines_capacity_short_fills_nothing():
             assert lens[:5].tolist() == want_len and mx.value == max(want_len)
             assert starts[:5].tolist() == [0, 5, 8, 9, 15]
             assert (starts[5:] == -7).all()
+
+
+def _ref_lines(data):
+    """(start, chopped length) of every line as barcode.py:95-97 iterates a binary file:
+    lines end at '\\n' (included), a last line may lack it, `line[:-1]` drops the last byte."""
+    out, pos = [], 0
+    while pos < len(data):
+        e = data.find(b"\n", pos)
+        e = len(data) - 1 if e < 0 else e
+        out.append((pos, e - pos))
+        pos = e + 1
+    return out
+
+
+def _ingest_cases():
+    rng = np.random.default_rng(404)
+    alpha = np.frombuffer(b"ACGTacgtNRY", dtype=np.uint8)
+    cases = {"tiny": b"ACGT\nAC\n\nGGGGG\nT", "crlf": b"ACGTACGT\r\nGGCC\r\n", "empty_lines": b"\n\n\nA\n",
+             "no_final_lf": b"ACGTTGCA\nACG", "single_byte": b"A", "only_lf": b"\n"}
+    parts = []  # ragged lines: 0-40 bytes (TwoBit > 32 bases: two limbs; flag 4 at words = 1)
+    for k in range(30_000):
+        L = int(rng.integers(0, 41)) if k % 97 else int(rng.integers(200, 9000))  # some lines span tiles
+        parts.append(alpha[rng.integers(0, alpha.size, L)].tobytes() + b"\n")
+    parts.append(b"X" * 20_000)  # a final line of 20 KB without '\n': tiles with no line end at all
+    cases["ragged"] = b"".join(parts)
+    return cases
+
+
+@pytest.mark.parametrize("name", list(_ingest_cases()))
+@pytest.mark.parametrize("kind,words", [(2, 1), (2, 2), (3, 1), (3, 2)])
+def test_whitelist_encode_one_pass(name, kind, words):
+    """sct_whitelist_encode (one pass, decoupled look-back, asynchronous) against
+    the reference's binary line loop with `line[:-1]` (barcode.py:95-97) and the oracle's
+    encoders (encodings.py:75-88 / 155-167): line count, longest line, every start, length,
+    code limb, GC count and flag; lines too long for `words` limbs carry flag 4; a capacity
+    below the count writes only the lines below it."""
+    import torch
+    data = _ingest_cases()[name]
+    ref = _ref_lines(data)
+    n = len(ref)
+    d_buf = torch.tensor(list(data), dtype=torch.uint8, device="cuda")
+    lib = _lib.lib()
+    for cap in (n, max(0, n - 3)):
+        codes = torch.full((max(1, n) * words,), -5, dtype=torch.int64, device="cuda")
+        starts = torch.full((max(1, n),), -5, dtype=torch.int64, device="cuda")
+        lens = torch.full((max(1, n),), -5, dtype=torch.int32, device="cuda")
+        gc = torch.zeros(max(1, n), dtype=torch.uint8, device="cuda")
+        flags = torch.full((max(1, n),), 77, dtype=torch.uint8, device="cuda")
+        d_n = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+        d_mx = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+        _lib.check(lib.sct_whitelist_encode(d_buf.data_ptr(), len(data), kind, words, cap, codes.data_ptr(),
+                                            starts.data_ptr(), lens.data_ptr(), gc.data_ptr(), flags.data_ptr(),
+                                            d_n.data_ptr(), d_mx.data_ptr(), None))
+        torch.cuda.synchronize()
+        assert int(d_n.item()) == n and int(d_mx.item()) == max([L for _, L in ref], default=0)
+        st, ln = starts.cpu().numpy(), lens.cpu().numpy()
+        cd = codes.cpu().numpy().view(np.uint64).reshape(-1, words)
+        fl, g = flags.cpu().numpy(), gc.cpu().numpy()
+        assert st[:cap].tolist() == [s for s, _ in ref[:cap]] and ln[:cap].tolist() == [L for _, L in ref[:cap]]
+        assert (st[cap:n] == -5).all() and (fl[cap:n] == 77).all()
+        enc = O.two_bit_encode if kind == 2 else O.three_bit_encode
+        for i, (s0, L) in enumerate(ref[:cap]):
+            rec = data[s0:s0 + L]
+            if kind * L > 64 * words:
+                assert fl[i] == 4
+                continue
+            amb = kind == 2 and any(b in b"MRWSYKVHDBNmrwsykvhdbn" for b in rec)
+            bad = kind == 2 and any(b not in b"ACGTacgtMRWSYKVHDBNmrwsykvhdbn" for b in rec)
+            assert fl[i] == (1 if amb else 0) | (2 if bad else 0), (i, rec)
+            if amb or bad:
+                continue
+            want = enc(rec)
+            assert _lib.limbs_to_ints(cd[i:i + 1])[0] == want, (i, rec)
+            gcw = rec.upper().count(b"C") + rec.upper().count(b"G")
+            assert g[i] == min(255, gcw)
