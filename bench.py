@@ -211,9 +211,17 @@ def _profile(name):
 
 
 def _rocprof_avg_ms(kernel_substr):
-    """Average dispatch duration of a kernel in the committed rocprofv3 --kernel-trace --stats
-    summary of this bench command (profiles/<round>_kernel_stats.csv), or None."""
+    """Average dispatch duration of a kernel in the committed rocprofv3 kernel trace of this
+    bench command: over the timed steps' dispatches (profiles/<round>_timed_dispatches.json,
+    the last K dispatches, the launches the live HIP events time) when present, else the
+    --stats average of every dispatch (profiles/<round>_kernel_stats.csv); or None."""
     import csv
+    win = os.path.join(ROOT, "profiles", "%s_timed_dispatches.json" % PROFILE_ROUND)
+    if os.path.exists(win):
+        with open(win) as f:
+            k = json.load(f)["kernels"].get(kernel_substr)
+        if k:
+            return k["avg_ns"] * 1e-6, k["window"]
     path = os.path.join(ROOT, "profiles", "%s_kernel_stats.csv" % PROFILE_ROUND)
     if not os.path.exists(path):
         return None, None
@@ -297,7 +305,9 @@ def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, nam
                    "issue": issue_picture(prof),
                    "rocprof": None if rms is None else {
                        "avg_ms": rms, "calls": rcalls, "frac": algo / (rms * 1e-3) / HBM_PEAK_BPS,
-                       "source": "profiles/%s_kernel_stats.csv" % PROFILE_ROUND,
+                       "source": "profiles/%s_timed_dispatches.json (the timed steps' dispatches of the rocprofv3 "
+                                 "kernel trace of this command; every dispatch: profiles/%s_kernel_stats.csv)"
+                                 % (PROFILE_ROUND, PROFILE_ROUND),
                        "live_vs_rocprof": avg / rms - 1.0}}
     dom, other = ("seed", "tile") if kern["seed"]["ms"] >= kern["tile"]["ms"] else ("tile", "seed")
     d = kern[dom]
@@ -727,7 +737,7 @@ def path_fastq(dev, reps, copy_gbs):
             "value": n_rec / (ms * 1e-3), "unit": "records/s", "ms": ms, "reps": reps,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
                          "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs,
-                         "algo_bytes_per_record": algo / n_rec, "kernel": "fastq_fused_kernel (sct_fastq_extract_fused)",
+                         "algo_bytes_per_record": algo / n_rec, "kernel": "fastq_range_kernel (sct_fastq_extract_fused)",
                          "note": "algorithmic bytes: the FASTQ once + the slices + codes; one kernel reads the "
                                  "buffer once (decoupled look-back for the line numbers, the CB encode fused), "
                                  "no host sync (DESIGN.md §3.6)"},

@@ -389,12 +389,12 @@ int sct_fastq_index_info(const sct_fastq_index* index, int64_t* nrecords, int64_
 int sct_fastq_extract_spans(sct_fastq_index* index, const uint8_t* d_buf, const int32_t* spans,
                             int nspans, uint8_t* d_seq, uint8_t* d_qual, int32_t* d_seq_len,
                             int32_t* d_qual_len, int64_t* first_bad_name, void* stream);
-/* One pass (index + extraction in one read of the buffer, asynchronous on `stream`, no host
- * synchronisation): d_file_ends is DEVICE memory; rows are laid out by the caller's capacity
- * (span k's row r at out + cap_records * prefix_k + r * width_k; lengths at len + k * cap + r);
- * d_status (3 int64, device): [0] line count (records = lines / 4; rows of an incomplete trailing
- * record are not meaningful), [1] ~(first bad-name record) or 0, [2] non-ASCII seen (text mode
- * rejects it).  d_codes0 / d_gc0 / d_flags0 (nullable): span 0's sequence rows TwoBit-encoded
+/* Index and extraction in one call (a count pass, then the extraction; asynchronous on
+ * `stream`, no host synchronisation): d_file_ends is DEVICE memory; rows are laid out by the
+ * caller's capacity (span k's row r at out + cap_records * prefix_k + r * width_k; lengths at
+ * len + k * cap + r; records >= cap_records are not written); d_status (3 int64, device): [0]
+ * line count (records = lines / 4), [1] ~(first bad-name record) or 0, [2] non-ASCII seen (text
+ * mode rejects it).  d_codes0 / d_gc0 / d_flags0 (nullable): span 0's sequence rows TwoBit-encoded
  * (width <= 32) as sct_encode would encode those rows. */
 int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, const int64_t* d_file_ends, int nfiles,
                             int text_mode, const int32_t* spans, int nspans, int64_t cap_records, uint8_t* d_seq,

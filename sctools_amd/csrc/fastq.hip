@@ -31,6 +31,7 @@
 
 #include "sct_common.h"
 #include "encode_common.h"
+#include "tile_prefix.h"
 
 namespace {
 
@@ -434,48 +435,25 @@ __global__ __launch_bounds__(WG) void extract2_kernel(const uint8_t* __restrict_
   }
 }
 
-// ---------------------------------------------------------------- one pass (round 4)
-// fastq_fused_kernel: the index and the extraction in ONE read of the buffer.  Each tile (one
-// per workgroup, dynamic ids) numbers its terminators with a decoupled look-back over its
-// predecessors' terminator counts (as lines.hip's whitelist ingest) instead of a count pass +
-// scan + host synchronisation; the rest is extract2_kernel's per-line work, except that
-//   - the record count is unknown while the tile runs: every line's slices are written (rows
-//     of records >= cap skipped), the output is laid out by the caller's capacity cap
-//     (span k's row r at out + cap * prefix_k + r * width_k), and the line count goes to
-//     d_status[0] (records = lines / 4; rows of an incomplete trailing record are garbage);
-//   - a tile's last line ends at the next tile's first terminator, which is found by the
-//     bounded scan (at most the spans' end bytes) instead of the count pass's table;
-//   - a bad name is reported as the max of ~record (d_status[1], 0 = none), so the host can
-//     drop one that lies in the incomplete trailing record;
-//   - optionally span 0's sequence rows are TwoBit-encoded as they are written (one limb,
-//     width <= 32; gc and flags as sct_encode over those rows), instead of a second kernel.
-struct FqStatus {
-  unsigned long long flag, agg, incl;  // flag 1: agg published, 2: incl (the inclusive count) too
-};
-
-__global__ __launch_bounds__(WG) void fastq_fused_kernel(
-    const uint8_t* __restrict__ buf, int64_t n, Files fs, int text, FqStatus* __restrict__ status,
-    unsigned* __restrict__ ctr, int64_t ntiles, int64_t cap, Spans sp, uint8_t* __restrict__ seq_out,
-    uint8_t* __restrict__ qual_out, int32_t* __restrict__ seq_len, int32_t* __restrict__ qual_len,
-    uint64_t* __restrict__ codes0, uint8_t* __restrict__ gc0, uint8_t* __restrict__ flags0,
-    unsigned long long* __restrict__ d_status) {
-  __shared__ uint16_t term[MAX_TERM];
-  __shared__ uint4 tile_bytes[TILE / 16];
-  __shared__ uint32_t w_cnt[WG / 64];
-  __shared__ int64_t s_tile;
-  __shared__ unsigned long long s_g0;
-  __shared__ uint8_t lut[256];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_tile = (int64_t)atomicAdd(ctr, 1u);
-  if (codes0)
-    for (int c = tid; c < 256; c += WG) lut[c] = lut_entry(2, c);
-  __syncthreads();
-  const int64_t tile = s_tile, t0 = tile * TILE, p0 = t0 + (int64_t)tid * TB;
+// ---------------------------------------------------------------- without an index (round 4)
+// sct_fastq_extract_fused: fq_count_kernel (one 8 KiB tile per workgroup: a one-pass grid streams
+// the buffer at the copy rate, where the persistent count_kernel loop stayed near 4 TB/s) writes
+// every tile's terminator count and first terminator (count_kernel's encoding) and the non-ASCII
+// flag; tile_sums_reduce_kernel sums the counts into the coarse levels of tile_prefix.h; then
+// fastq_range_kernel gives each workgroup a contiguous range of tiles: it takes its first tile's
+// line number and the total line count from the tile sums once, and walks its range carrying the
+// line number (extract2_kernel's per-tile work, next tile's bytes loaded while this one is worked).
+// No scan launch, no host synchronisation, and no atomics on shared words: publishing into the
+// coarse levels with atomics cost 608 us for 1.38 GB (every tile in flight adds to one word).
+__global__ __launch_bounds__(WG) void fq_count_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs, int text,
+                                                      sct::TileSums ts, uint32_t* __restrict__ first,
+                                                      unsigned* __restrict__ flags) {
+  const int64_t tile = blockIdx.x, t0 = tile * TILE, p0 = t0 + (int64_t)threadIdx.x * TB;
   uint4 cur[SEG];
 #pragma unroll
   for (int k = 0; k < SEG; ++k) cur[k] = load16(buf, n, p0 + 16 * k);
   bool ends_here;
-  {  // a file end in this tile (wave-uniform): the first file ending after t0
+  {
     int lo = 0, hi = fs.nfiles;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
@@ -483,186 +461,260 @@ __global__ __launch_bounds__(WG) void fastq_fused_kernel(
     }
     ends_here = lo < fs.nfiles && fs.ends[lo] <= t0 + TILE + 16;
   }
-  Span spn{0, 0, 0, 0};
-  if (p0 < n) spn = thread_span(buf, n, fs, text, p0, cur, ends_here);
-  if (spn.na) atomicOr(reinterpret_cast<unsigned*>(d_status + 2), 1u);
-#pragma unroll
-  for (int k = 0; k < SEG; ++k) tile_bytes[tid * SEG + k] = p0 + 16 * k < n ? cur[k] : make_uint4(0, 0, 0, 0);
-  const uint32_t tbits = spn.m | spn.vbits, c = __popc(tbits);
-  uint32_t ic = c;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t a = __shfl_up(ic, d);
-    if (lane >= d) ic += a;
-  }
-  if (lane == 63) w_cnt[wave] = ic;
-  __syncthreads();
-  uint32_t pre = ic - c, ntile = 0;
-#pragma unroll
-  for (int w = 0; w < WG / 64; ++w) {
-    if (w < wave) pre += w_cnt[w];
-    ntile += w_cnt[w];
-  }
-  {
-    uint32_t bits = tbits, at = pre;
-    while (bits) {
+  unsigned long long c = 0;
+  uint32_t na = 0, f = ~0u;
+  if (p0 < n) {
+    const Span sp = thread_span(buf, n, fs, text, p0, cur, ends_here);
+    const uint32_t bits = sp.m | sp.vbits;
+    c = __popc(bits);
+    na = sp.na;
+    if (bits) {
       const int j = __ffs(bits) - 1;
-      bits &= bits - 1;
-      const uint32_t off = (uint32_t)(tid * TB + j);
-      term[at++] = (spn.m >> j & 1u) ? (uint16_t)(off | ((spn.crlf >> j & 1u) ? T16_CRLF : 0u))
-                                     : (uint16_t)((off + 1) | T16_VIRT);  // the file ends after byte off
+      f = (sp.m >> j & 1u) ? ((uint32_t)(threadIdx.x * TB + j) << 2) | ((sp.crlf >> j & 1u) ? 2u : 0u)
+                           : ((uint32_t)(threadIdx.x * TB + j + 1) << 2) | 1u;
     }
   }
-  if (wave == 0) {  // the look-back: terminators before this tile
-    FqStatus* me = status + tile;
-    unsigned long long excl = 0;
-    if (tile == 0) {
-      if (lane == 0) {
-        __hip_atomic_store(&me->incl, (unsigned long long)ntile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&me->flag, 2ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else {
-      if (lane == 0) {
-        __hip_atomic_store(&me->agg, (unsigned long long)ntile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&me->flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      for (int64_t base = tile - 1;; base -= 64) {
-        const int64_t k = base - lane;
-        unsigned long long f = 2, v = 0;
-        if (k >= 0) {
-          do {
-            f = __hip_atomic_load(&status[k].flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-          } while (f == 0);
-          v = __hip_atomic_load(f == 2 ? &status[k].incl : &status[k].agg, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
-        }
-        const unsigned long long incl = __ballot(f == 2);
-        const int stop = incl ? __ffsll((long long)incl) - 1 : 63;
-        if (lane > stop) v = 0;
+  if (na) atomicOr(flags, 1u);
 #pragma unroll
-        for (int sh = 32; sh; sh >>= 1) v += __shfl_xor(v, sh);
-        excl += v;
-        if (incl) break;
-      }
-      if (lane == 0) {
-        __hip_atomic_store(&me->incl, excl + ntile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&me->flag, 2ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (lane == 0) {
-      s_g0 = excl;
-      if (tile == ntiles - 1) d_status[0] = excl + ntile;  // every line ends at a terminator
-    }
+  for (int o = 32; o; o >>= 1) {
+    c += __shfl_xor(c, o);
+    f = min(f, (uint32_t)__shfl_xor(f, o));
+  }
+  __shared__ unsigned long long wc[WG / 64];
+  __shared__ uint32_t wf[WG / 64];
+  if ((threadIdx.x & 63) == 0) {
+    wc[threadIdx.x >> 6] = c;
+    wf[threadIdx.x >> 6] = f;
   }
   __syncthreads();
-  const int64_t g0 = (int64_t)s_g0;
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < WG / 64; ++w) {
+      c += wc[w];
+      f = min(f, wf[w]);
+    }
+    sct::tile_publish(ts, tile, c, -1);
+    first[tile] = f;
+  }
+}
+
+// 4 bytes of a row through the TwoBit LUT (lut_entry: code in bits 0..2, flags above)
+__device__ __forceinline__ void enc_dword(const uint8_t* lut, uint32_t y, uint64_t& code, uint32_t& fl) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const uint32_t e = lut[(y >> (8 * b)) & 0xFFu];
+    code = (code << 2) | (e & 7u);
+    fl |= e;
+  }
+}
+
+// Rows of records >= cap are skipped; span k's row r at out + cap * prefix_k + r * width_k, its
+// length at len + k * cap + r; d_status[0] = the line count, d_status[1] = ~(first bad-name
+// record) or 0 (records < lines / 4 only, as extract2_kernel); optionally span 0's sequence rows
+// TwoBit-encoded as they are written (one limb, width <= 32; gc and flags as sct_encode's).
+__global__ __launch_bounds__(WG) void fastq_range_kernel(
+    const uint8_t* __restrict__ buf, int64_t n, Files fs, int text, sct::TileSums ts,
+    const uint32_t* __restrict__ first, int64_t ntiles, int64_t per_wg, int64_t cap, Spans sp,
+    uint8_t* __restrict__ seq_out, uint8_t* __restrict__ qual_out, int32_t* __restrict__ seq_len,
+    int32_t* __restrict__ qual_len, uint64_t* __restrict__ codes0, uint8_t* __restrict__ gc0,
+    uint8_t* __restrict__ flags0, unsigned long long* __restrict__ d_status) {
+  __shared__ uint16_t term[MAX_TERM];
+  __shared__ uint4 tile_bytes[TILE / 16];
+  __shared__ uint32_t w_cnt[WG / 64];
+  __shared__ unsigned long long s_g0, s_total;
+  __shared__ long long s_unused;
+  __shared__ unsigned long long red[3][WG / 64];
+  __shared__ uint8_t lut[256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int64_t tile = (int64_t)blockIdx.x * per_wg;
+  if (tile >= ntiles) return;  // (the whole workgroup)
+  const int64_t tend = tile + per_wg < ntiles ? tile + per_wg : ntiles;
+  if (codes0)
+    for (int c = tid; c < 256; c += WG) lut[c] = lut_entry(2, c);
+  uint4 cur[SEG], nxt[SEG];
+#pragma unroll
+  for (int k = 0; k < SEG; ++k) cur[k] = load16(buf, n, tile * TILE + (int64_t)tid * TB + 16 * k);
+  // (its barriers also cover the LUT)
+  sct::tile_prefix<WG>(ts, tile, &s_g0, &s_unused, red, (ntiles + 1023) >> 10, &s_total);
+  int64_t g0 = (int64_t)s_g0;  // global number of the current tile's first terminator
+  const int64_t nrec = (int64_t)(s_total >> 2);
+  const int64_t lim_g = 4 * nrec - 1;  // terminators beyond the last record's line 3 end nothing
+  if (blockIdx.x == 0 && tid == 0) {
+    d_status[0] = s_total;
+    if (nrec > 0 && buf[0] != '@') atomicMax(d_status + 1, ~0ull);  // record 0's name line
+  }
+  uint32_t nf_cur = tile + 1 < ntiles ? first[tile + 1] : ~0u;
+  FileCursor fc;
   const uint8_t* tile8 = reinterpret_cast<const uint8_t*>(tile_bytes);
   const uint32_t* tile32 = reinterpret_cast<const uint32_t*>(tile_bytes);
-  if (tile == 0 && tid == 0 && n > 0 && buf[0] != '@') atomicMax(d_status + 1, ~0ull);  // record 0
-  const int tmax = (int)ntile;
-  // name lines: after terminators g = 3 (mod 4)
-  for (int t = (int)((3 - (g0 & 3)) & 3) + 4 * tid; t < tmax; t += 4 * WG) {
-    const uint32_t e = term[t];
-    const int64_t o = (int64_t)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // the line's start in the tile
-    if (t0 + o >= n) continue;  // no line after the buffer's last terminator
-    const uint8_t ch = o < TILE ? tile8[o] : buf[t0 + o];
-    if (ch != '@') atomicMax(d_status + 1, ~(unsigned long long)((g0 + t + 1) >> 2));
-  }
-  // sequence / quality lines: after even terminators; one item per line, its spans in turn
-  const int te0 = (int)(g0 & 1);
-  const int nact = tmax > te0 ? (tmax - te0 + 1) / 2 : 0;
-  for (int a = tid; a < nact; a += WG) {
-    const int t = te0 + 2 * a;
-    const int64_t line = g0 + t + 1, rec = line >> 2;
-    const uint32_t e = term[t];
-    const int start = (int)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // <= TILE
-    if (rec >= cap || t0 + start >= n) continue;
-    const bool is_seq = (line & 3) == 1;
-    int64_t cend;  // content end relative to the tile start
-    int nl;
-    if (t + 1 < tmax) {  // the line ends at the tile's next terminator
-      const uint32_t f = term[t + 1];
-      cend = (int64_t)(f & T16_OFF) - ((f & T16_CRLF) ? 1 : 0);
-      nl = (f & T16_VIRT) ? 0 : 1;
-    } else {  // the tile's last line: scan (max_end bytes, within its file)
-      const int64_t next = t0 + start;
-      int lo = 0, hi = fs.nfiles;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (fs.ends[mid] <= next) lo = mid + 1; else hi = mid;
-      }
-      const int64_t fe = lo < fs.nfiles ? fs.ends[lo] : n;
-      const int64_t lim = next + sp.max_end < fe ? next + sp.max_end : fe;
-      cend = lim - t0;
-      nl = lim == fe ? 0 : 1;  // longer than the window: its end is irrelevant
-      for (int64_t i = next; i < lim; ++i) {
-        const uint8_t ch = buf[i];
-        if (ch == '\n' || (text && ch == '\r')) {
-          cend = i - t0;
-          nl = 1;
-          break;
-        }
+  for (; tile < tend; ++tile) {
+    const int64_t ntl = tile + 1;
+    const bool more = ntl < tend;
+#pragma unroll
+    for (int k = 0; k < SEG; ++k)
+      nxt[k] = more ? load16(buf, n, ntl * TILE + (int64_t)tid * TB + 16 * k) : make_uint4(0, 0, 0, 0);
+    const uint32_t nf_nxt = more && ntl + 1 < ntiles ? first[ntl + 1] : ~0u;
+    const int64_t t0 = tile * TILE, p0 = t0 + (int64_t)tid * TB;
+    const bool ends_here = fc.advance(fs, t0);
+    Span spn{0, 0, 0, 0};
+    if (p0 < n) spn = thread_span(buf, n, fs, text, p0, cur, ends_here);
+    __syncthreads();  // the previous tile's readers of tile_bytes / term are done
+#pragma unroll
+    for (int k = 0; k < SEG; ++k) {
+      tile_bytes[tid * SEG + k] = p0 + 16 * k < n ? cur[k] : make_uint4(0, 0, 0, 0);
+      cur[k] = nxt[k];
+    }
+    const uint32_t tbits = spn.m | spn.vbits, c = __popc(tbits);
+    uint32_t ic = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t x = __shfl_up(ic, d);
+      if (lane >= d) ic += x;
+    }
+    if (lane == 63) w_cnt[wave] = ic;
+    __syncthreads();
+    uint32_t pre = ic - c, ntile = 0;
+#pragma unroll
+    for (int w = 0; w < WG / 64; ++w) {
+      if (w < wave) pre += w_cnt[w];
+      ntile += w_cnt[w];
+    }
+    {
+      uint32_t bits = tbits, at = pre;
+      while (bits) {
+        const int j = __ffs(bits) - 1;
+        bits &= bits - 1;
+        const uint32_t off = (uint32_t)(tid * TB + j);
+        term[at++] = (spn.m >> j & 1u) ? (uint16_t)(off | ((spn.crlf >> j & 1u) ? T16_CRLF : 0u))
+                                       : (uint16_t)((off + 1) | T16_VIRT);  // the file ends after byte off
       }
     }
-    int32_t* len = is_seq ? seq_len : qual_len;
-    uint8_t* out = is_seq ? seq_out : qual_out;
-    const int64_t clen = cend - start, llen = clen + nl;
-    for (int k = 0; k < sp.n; ++k) {
-      const int64_t sa = sp.start[k] < llen ? sp.start[k] : llen, sb = sp.end[k] < llen ? sp.end[k] : llen;
-      if (len) len[k * cap + rec] = (int32_t)(sb - sa);
-      if (!out) continue;
-      const int w = sp.end[k] - sp.start[k];
-      uint8_t* o = out + sp.prefix[k] * cap + rec * w;
-      const uint8_t* src = buf + t0 + start;
-      const int64_t s0 = t0 + start + sa;
-      const int64_t base = s0 & ~3LL;
-      const int nd = w / 4;
-      if (sb - sa == w && sb <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
-          ((uintptr_t)o & 3) == 0) {
-        const uint32_t* d = base + 4 * (nd + 1) <= t0 + TILE ? tile32 + ((base - t0) >> 2)
-                                                             : reinterpret_cast<const uint32_t*>(buf + base);
-        const uint32_t sh = (uint32_t)(s0 & 3);
-        uint32_t* od = reinterpret_cast<uint32_t*>(o);
-        if (nd == 4 && ((uintptr_t)o & 15) == 0) {
-          const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3], x4 = d[4];
-          *reinterpret_cast<uint4*>(o) =
-              make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                         __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
-        } else if (nd == 2 && ((uintptr_t)o & 7) == 0) {
-          const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
-          *reinterpret_cast<uint2*>(o) =
-              make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
-        } else {
-          uint32_t lo = d[0];
-          for (int q2 = 0; q2 < nd; ++q2) {
-            const uint32_t hi = d[q2 + 1];
-            od[q2] = __builtin_amdgcn_alignbyte(hi, lo, sh);
-            lo = hi;
+    __syncthreads();
+    const uint32_t nf = nf_cur;
+    const int tmax = (int)(g0 + ntile <= lim_g ? ntile : (lim_g > g0 ? lim_g - g0 : 0));
+    // name lines: after terminators g = 3 (mod 4)
+    for (int t = (int)((3 - (g0 & 3)) & 3) + 4 * tid; t < tmax; t += 4 * WG) {
+      const uint32_t e = term[t];
+      const int64_t o = (int64_t)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // the line's start in the tile
+      const uint8_t ch = o < TILE ? tile8[o] : buf[t0 + o];
+      if (ch != '@') atomicMax(d_status + 1, ~(unsigned long long)((g0 + t + 1) >> 2));
+    }
+    // sequence / quality lines: after even terminators; one item per line, its spans in turn
+    const int te0 = (int)(g0 & 1);
+    const int nact = tmax > te0 ? (tmax - te0 + 1) / 2 : 0;
+    for (int a = tid; a < nact; a += WG) {
+      const int t = te0 + 2 * a;
+      const int64_t line = g0 + t + 1, rec = line >> 2;
+      if (rec >= cap) continue;
+      const bool is_seq = (line & 3) == 1;
+      const uint32_t e = term[t];
+      const int start = (int)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // <= TILE
+      int64_t cend;  // content end relative to the tile start
+      int nl;
+      if (t + 1 < (int)ntile) {  // the line ends at the tile's next terminator
+        const uint32_t f = term[t + 1];
+        cend = (int64_t)(f & T16_OFF) - ((f & T16_CRLF) ? 1 : 0);
+        nl = (f & T16_VIRT) ? 0 : 1;
+      } else if (nf != ~0u) {  // the tile's last line ends at the next tile's first terminator
+        cend = TILE + (int64_t)(nf >> 2) - ((nf & 2u) ? 1 : 0);
+        nl = (nf & 1u) ? 0 : 1;
+      } else {  // no terminator in the next tile either: scan (max_end bytes, within its file)
+        const int64_t next = t0 + start;
+        int lo = 0, hi = fs.nfiles;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (fs.ends[mid] <= next) lo = mid + 1; else hi = mid;
+        }
+        const int64_t fe = lo < fs.nfiles ? fs.ends[lo] : n;
+        const int64_t lim = next + sp.max_end < fe ? next + sp.max_end : fe;
+        cend = lim - t0;
+        nl = lim == fe ? 0 : 1;  // longer than the window: its end is irrelevant
+        for (int64_t i = next; i < lim; ++i) {
+          const uint8_t ch = buf[i];
+          if (ch == '\n' || (text && ch == '\r')) {
+            cend = i - t0;
+            nl = 1;
+            break;
           }
         }
-      } else {
-#pragma unroll 8
-        for (int j = 0; j < w; ++j) {
-          const int64_t i = sa + j;
-          o[j] = i < sb ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
-        }
       }
-      if (k == 0 && is_seq && codes0) {  // span 0's row (as written, zero-padded) -> TwoBit
+      int32_t* len = is_seq ? seq_len : qual_len;
+      uint8_t* out = is_seq ? seq_out : qual_out;
+      const int64_t clen = cend - start, llen = clen + nl;
+      for (int k = 0; k < sp.n; ++k) {
+        const int64_t sa = sp.start[k] < llen ? sp.start[k] : llen, sb = sp.end[k] < llen ? sp.end[k] : llen;
+        if (len) len[k * cap + rec] = (int32_t)(sb - sa);
+        if (!out) continue;
+        const bool enc = k == 0 && is_seq && codes0 != nullptr;
         uint64_t code = 0;
         uint32_t fl = 0;
-        for (int j = 0; j < w; ++j) {
-          const uint32_t en = lut[o[j]];
-          code = (code << 2) | (en & 7u);
-          fl |= en;
+        const int w = sp.end[k] - sp.start[k];
+        uint8_t* o = out + sp.prefix[k] * cap + rec * w;
+        const uint8_t* src = buf + t0 + start;
+        // fast path: a whole-width slice inside the line's content, a row of whole dwords:
+        // aligned dword loads + byte-align funnel shifts, dword stores (the code from the same
+        // registers)
+        const int64_t s0 = t0 + start + sa;
+        const int64_t base = s0 & ~3LL;
+        const int nd = w / 4;
+        if (sb - sa == w && sb <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
+            ((uintptr_t)o & 3) == 0) {
+          const uint32_t* d = base + 4 * (nd + 1) <= t0 + TILE ? tile32 + ((base - t0) >> 2)
+                                                               : reinterpret_cast<const uint32_t*>(buf + base);
+          const uint32_t sh = (uint32_t)(s0 & 3);
+          uint32_t* od = reinterpret_cast<uint32_t*>(o);
+          if (nd == 4 && ((uintptr_t)o & 15) == 0) {
+            const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3], x4 = d[4];
+            const uint4 y = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                                       __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+            *reinterpret_cast<uint4*>(o) = y;
+            if (enc) {
+              enc_dword(lut, y.x, code, fl);
+              enc_dword(lut, y.y, code, fl);
+              enc_dword(lut, y.z, code, fl);
+              enc_dword(lut, y.w, code, fl);
+            }
+          } else if (nd == 2 && ((uintptr_t)o & 7) == 0) {
+            const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
+            const uint2 y = make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
+            *reinterpret_cast<uint2*>(o) = y;
+            if (enc) {
+              enc_dword(lut, y.x, code, fl);
+              enc_dword(lut, y.y, code, fl);
+            }
+          } else {
+            uint32_t lo = d[0];
+            for (int q2 = 0; q2 < nd; ++q2) {
+              const uint32_t hi = d[q2 + 1], y = __builtin_amdgcn_alignbyte(hi, lo, sh);
+              od[q2] = y;
+              if (enc) enc_dword(lut, y, code, fl);
+              lo = hi;
+            }
+          }
+        } else {
+#pragma unroll 8
+          for (int j = 0; j < w; ++j) {
+            const int64_t i = sa + j;
+            const uint8_t v = i < sb ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
+            o[j] = v;
+            if (enc) {
+              const uint32_t en = lut[v];
+              code = (code << 2) | (en & 7u);
+              fl |= en;
+            }
+          }
         }
-        codes0[rec] = code;
-        if (gc0) {
-          const uint32_t g = (uint32_t)__popcll(code & 0x5555555555555555ull);
-          gc0[rec] = (uint8_t)(g > 255 ? 255 : g);
+        if (enc) {  // span 0's row (as written, zero-padded) -> TwoBit
+          codes0[rec] = code;
+          if (gc0) {
+            const uint32_t g = (uint32_t)__popcll(code & 0x5555555555555555ull);
+            gc0[rec] = (uint8_t)(g > 255 ? 255 : g);
+          }
+          if (flags0) flags0[rec] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
         }
-        if (flags0) flags0[rec] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
       }
     }
+    g0 += ntile;
+    nf_cur = nf_nxt;
   }
 }
 
@@ -892,10 +944,11 @@ namespace {
   } while (0)
 }  // namespace
 
-// One pass (fastq_fused_kernel), asynchronous on `stream`: the concatenated files in d_buf,
-// their cumulative ends in d_file_ends (DEVICE memory, nfiles entries, the last = nbytes).
-// Rows are laid out by cap_records (span k's row r at out + cap * prefix_k + r * width_k, its
-// length at len + k * cap + r); d_status (3 x int64, device) receives the line count
+// Extraction without an index (fq_count_kernel, tile_sums_reduce_kernel, fastq_range_kernel),
+// asynchronous on `stream`: the concatenated files in d_buf, their cumulative ends in d_file_ends
+// (DEVICE memory, nfiles entries, the last = nbytes).  Rows are laid out by cap_records (span
+// k's row r at out + cap * prefix_k + r * width_k, its length at len + k * cap + r; rows of
+// records >= cap_records are not written); d_status (3 x int64, device) receives the line count
 // (records = lines / 4), ~(first bad-name record) or 0, and a text-mode non-ASCII flag.
 // d_codes0 / d_gc0 / d_flags0 (nullable): span 0's sequence rows TwoBit-encoded (width <= 32).
 extern "C" int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, const int64_t* d_file_ends, int nfiles,
@@ -926,18 +979,22 @@ extern "C" int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, con
   const int64_t ntiles = sct::ceil_div(nbytes, TILE);
   SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
   void* scratch = nullptr;
-  const size_t sbytes = (size_t)ntiles * sizeof(FqStatus) + 256;
-  SCT_HIP(sct::pool_alloc(&scratch, sbytes, s));
-  hipError_t e = hipMemsetAsync(scratch, 0, sbytes, s);
-  if (e == hipSuccess) {
-    FqStatus* st = reinterpret_cast<FqStatus*>(scratch);
-    unsigned* ctr = reinterpret_cast<unsigned*>(reinterpret_cast<uint8_t*>(scratch) + (size_t)ntiles * sizeof(FqStatus));
-    hipLaunchKernelGGL(fastq_fused_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes,
-                       Files{d_file_ends, nfiles}, text_mode ? 1 : 0, st, ctr, ntiles, cap_records, sp, d_seq,
-                       d_qual, d_seq_len, d_qual_len, d_codes0, d_gc0, d_flags0,
-                       reinterpret_cast<unsigned long long*>(d_status));
-    e = hipGetLastError();
-  }
+  const size_t sbytes = sct::tile_sums_bytes(ntiles), fbytes = (size_t)ntiles * 4;
+  SCT_HIP(sct::pool_alloc(&scratch, sbytes + fbytes, s));
+  const sct::TileSums ts = sct::tile_sums_at(scratch, ntiles, false);
+  uint32_t* first = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(scratch) + sbytes);
+  const Files fs{d_file_ends, nfiles};
+  hipLaunchKernelGGL(fq_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, fs, text_mode ? 1 : 0, ts,
+                     first, reinterpret_cast<unsigned*>(d_status + 2));
+  hipLaunchKernelGGL(sct::tile_sums_reduce_kernel, dim3((unsigned)sct::ceil_div(ntiles, 1024)), dim3(64), 0, s, ts,
+                     ntiles);
+  // contiguous tile ranges, one per resident workgroup slot
+  const int64_t grid = resident_grid((const void*)fastq_range_kernel, ntiles);
+  const int64_t per_wg = sct::ceil_div(ntiles, grid);
+  hipLaunchKernelGGL(fastq_range_kernel, dim3((unsigned)sct::ceil_div(ntiles, per_wg)), dim3(WG), 0, s, d_buf, nbytes,
+                     fs, text_mode ? 1 : 0, ts, (const uint32_t*)first, ntiles, per_wg, cap_records, sp, d_seq, d_qual,
+                     d_seq_len, d_qual_len, d_codes0, d_gc0, d_flags0, reinterpret_cast<unsigned long long*>(d_status));
+  hipError_t e = hipGetLastError();
   sct::pool_free(scratch, s);
   if (e != hipSuccess) return sct::fail(SCT_E_HIP, "fastq fused: %s", hipGetErrorString(e));
   return SCT_OK;

@@ -8,9 +8,10 @@
 // last byte ('\n', or the file's last byte), line g's chopped content is
 // [P_{g-1} + 1, P_g): start = P_{g-1} + 1 (0 for g = 0), length = P_g - start.
 //
-// sct_whitelist_encode (the ingest Barcodes.from_whitelist takes, round 4): ONE pass over 4 KiB
-// tiles (16 bytes per thread, SWAR '\n' compares) with a decoupled look-back for the line
-// numbers, each line encoded from the file bytes by the lane holding its end (below).
+// sct_whitelist_encode (the ingest Barcodes.from_whitelist takes, round 4): a count pass over
+// 4 KiB tiles (16 bytes per thread, SWAR '\n' compares), a reduction of the tile counts, and an
+// encode pass in which each line is encoded by the lane holding its end (below); no scan launch
+// and no host synchronisation.
 // sct_lines (kept for callers that want only the spans): two passes -- count each tile's line
 // ends, exclusive-scan them, then store every end as the next line's start; the lengths follow
 // from consecutive starts.
@@ -20,6 +21,7 @@
 
 #include "sct_common.h"
 #include "encode_common.h"
+#include "tile_prefix.h"
 
 namespace {
 
@@ -107,36 +109,39 @@ __global__ __launch_bounds__(WG) void line_lens_kernel(const int64_t* __restrict
   }
 }
 
-// ---------------------------------------------------------------- one-pass ingest (round 4)
-// sct_whitelist_encode: the line split, the [:-1] chop and the encoder in ONE kernel over 4 KiB
-// tiles that reads the file once.  Tiles take dynamic ids (so a tile's predecessors are running
-// or done) and find the line count and the last line end before them by a decoupled look-back
-// (Merrill & Garland's single-pass scan): each tile publishes its aggregate (line ends, last end
-// position), then a wave reads up to 64 predecessors' status words at once, summing aggregates
-// back to the nearest tile whose inclusive prefix is published, and publishes its own inclusive
-// prefix.  Line g ends at the g-th line end P_g (a '\n', or the file's last byte) and its
-// chopped content is [P_{g-1} + 1, P_g): each lane encodes the lines ending in its 16 bytes,
-// the first one starting after the latest end before the lane (an exclusive max-scan).  The
-// line count and the longest line stay on the device: no host synchronisation.
-// A tile's aggregate and inclusive prefix live in separate words: a reader that saw the
-// aggregate flag must still read the aggregate after the owner has published its inclusive
-// prefix (one shared value word would hand it the inclusive count as if it were the aggregate).
-struct TileStatus {
-  unsigned long long flag;  // 0 none, 1 aggregate, 2 inclusive prefix
-  unsigned long long agg_count;
-  long long agg_last;       // position of the tile's last line end, -1 if none
-  unsigned long long incl_count;
-  long long incl_last;      // the last line end up to the tile's end, -1 if none
-};
-constexpr unsigned long long kAgg = 1, kIncl = 2;
-
-__device__ __forceinline__ void publish(TileStatus* st, unsigned long long flag, unsigned long long count,
-                                        long long last) {
-  unsigned long long* c = flag == kIncl ? &st->incl_count : &st->agg_count;
-  long long* l = flag == kIncl ? &st->incl_last : &st->agg_last;
-  __hip_atomic_store(c, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(l, last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&st->flag, flag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+// ---------------------------------------------------------------- ingest in two passes (round 4)
+// sct_whitelist_encode: wl_count_kernel counts each 4 KiB tile's line ends and its last one and
+// tile_sums_reduce_kernel sums them into the 3-level tile sums (tile_prefix.h); whitelist_fused_kernel
+// reads the tile again, takes its first line number and the last line end before it from those
+// sums, and encodes every line ending in the tile: line g ends at the g-th line end P_g (a '\n',
+// or the file's last byte) and its chopped content is [P_{g-1} + 1, P_g); each lane encodes the
+// lines ending in its 16 bytes, the first one starting after the latest end before the lane (an
+// exclusive max-scan).  The line count and the longest line stay on the device (no host
+// synchronisation); a 62.7 MB whitelist's second read comes from the Infinity Cache.
+__global__ __launch_bounds__(WG) void wl_count_kernel(const uint8_t* __restrict__ buf, int64_t n, sct::TileSums ts) {
+  const int64_t tile = blockIdx.x, p0 = tile * TILE + threadIdx.x * 16;
+  const uint32_t m = p0 < n ? lf_mask(buf, n, p0) : 0u;
+  unsigned long long c = __popc(m);
+  long long last = m ? p0 + 31 - __clz(m) : -1;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    c += __shfl_xor(c, o);
+    last = max(last, __shfl_xor(last, o));
+  }
+  __shared__ unsigned long long wc[WG / 64];
+  __shared__ long long wl[WG / 64];
+  if ((threadIdx.x & 63) == 0) {
+    wc[threadIdx.x >> 6] = c;
+    wl[threadIdx.x >> 6] = last;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < WG / 64; ++w) {
+      c += wc[w];
+      last = max(last, wl[w]);
+    }
+    sct::tile_publish(ts, tile, c, last);
+  }
 }
 
 // one record [rec, rec + L) through the LUT: the one-limb dword path of encode_var_kernel
@@ -182,121 +187,114 @@ __device__ __forceinline__ void encode_line(const uint8_t* lut, const uint8_t* r
   encode_record(lut, KIND, rd, L, words, out, g, fl);
 }
 
+// the 16 bytes at p0 (zero past n) and their line ends (lf_mask)
+__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ buf, int64_t n, int64_t p0) {
+  if (p0 + 16 <= n) return *reinterpret_cast<const uint4*>(buf + p0);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (int j = 0; j < 16 && p0 + j < n; ++j) w[j >> 2] |= (uint32_t)buf[p0 + j] << (8 * (j & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ uint32_t lf_mask_v(uint4 v, int64_t n, int64_t p0) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // (bytes past n are zero, never '\n')
+    const uint32_t x = w[k] ^ 0x0A0A0A0Au;
+    const uint32_t hi = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+    m |= (((hi >> 7) & 1u) | ((hi >> 14) & 2u) | ((hi >> 21) & 4u) | ((hi >> 28) & 8u)) << (4 * k);
+  }
+  if (n > 0 && p0 <= n - 1 && n - 1 < p0 + 16) m |= 1u << (n - 1 - p0);
+  return m;
+}
+
+// A contiguous range of per_wg tiles per workgroup: the first tile's line number and last line
+// end before it from the tile sums (once), then tile by tile (the next tile's bytes loaded while
+// this one is encoded), carrying both; the tile's bytes are staged in LDS and every line that
+// starts inside the tile is encoded from there (only a tile's first line may start before it).
 template <int KIND>
 __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
-    const uint8_t* __restrict__ buf, int64_t n, int64_t ntiles, TileStatus* __restrict__ status,
-    unsigned* __restrict__ tile_ctr, int64_t cap, int words, uint64_t* __restrict__ codes,
-    int64_t* __restrict__ starts, int32_t* __restrict__ lens, uint8_t* __restrict__ gc, uint8_t* __restrict__ flags,
-    unsigned long long* __restrict__ d_nlines, int32_t* __restrict__ d_maxlen) {
+    const uint8_t* __restrict__ buf, int64_t n, int64_t ntiles, int64_t per_wg, sct::TileSums ts, int64_t cap,
+    int words, uint64_t* __restrict__ codes, int64_t* __restrict__ starts, int32_t* __restrict__ lens,
+    uint8_t* __restrict__ gc, uint8_t* __restrict__ flags, unsigned long long* __restrict__ d_nlines,
+    int32_t* __restrict__ d_maxlen) {
   __shared__ uint8_t lut[256];
-  __shared__ int64_t s_tile;
+  __shared__ uint4 tile_bytes[TILE / 16 + 1];  // (+16: encode_line's dword reads stay inside)
   __shared__ uint32_t w_cnt[WG / 64];
   __shared__ long long w_last[WG / 64];
   __shared__ unsigned long long s_excl;
   __shared__ long long s_excl_last;
+  __shared__ unsigned long long red[3][WG / 64];
   __shared__ int32_t w_max[WG / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  int64_t tile = (int64_t)blockIdx.x * per_wg;
+  if (tile >= ntiles) return;  // (the whole workgroup)
+  const int64_t tend = tile + per_wg < ntiles ? tile + per_wg : ntiles;
   for (int c = t; c < 256; c += WG) lut[c] = lut_entry(KIND, c);
-  if (t == 0) s_tile = (int64_t)atomicAdd(tile_ctr, 1u);
-  __syncthreads();
-  const int64_t tile = s_tile;
-  const int64_t p0 = tile * TILE + t * 16;
-  uint32_t m = p0 < n ? lf_mask(buf, n, p0) : 0u;
-  const uint32_t c = __popc(m);
-  const long long mylast = m ? p0 + 31 - __clz(m) : -1;
-  // wave-inclusive sum of c and max of mylast, then across the 4 waves
-  uint32_t ic = c;
-  long long il = mylast;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t a = __shfl_up(ic, d);
-    const long long b = __shfl_up(il, d);
-    if (lane >= d) {
-      ic += a;
-      il = max(il, b);
-    }
-  }
-  if (lane == 63) {
-    w_cnt[wave] = ic;
-    w_last[wave] = il;
-  }
-  __syncthreads();
-  uint32_t xc = ic - c, tot = 0;  // exclusive within the tile
-  long long xl = __shfl_up(il, 1), tlast = -1;
-  if (lane == 0) xl = -1;
-#pragma unroll
-  for (int w = 0; w < WG / 64; ++w) {
-    if (w < wave) {
-      xc += w_cnt[w];
-      xl = max(xl, w_last[w]);
-    }
-    tot += w_cnt[w];
-    tlast = max(tlast, w_last[w]);
-  }
-  if (wave == 0) {  // the look-back
-    TileStatus* me = status + tile;
-    unsigned long long excl = 0;
-    long long elast = -1;
-    if (tile == 0) {
-      if (lane == 0) publish(me, kIncl, tot, tlast);
-    } else {
-      if (lane == 0) publish(me, kAgg, tot, tlast);
-      bool found = false;
-      for (int64_t base = tile - 1;; base -= 64) {
-        const int64_t k = base - lane;
-        unsigned long long f = kIncl, cnt = 0;
-        long long last = -1;
-        if (k >= 0) {
-          do {
-            f = __hip_atomic_load(&status[k].flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-          } while (f == 0);
-          const bool inc = f == kIncl;
-          cnt = __hip_atomic_load(inc ? &status[k].incl_count : &status[k].agg_count, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-          last = __hip_atomic_load(inc ? &status[k].incl_last : &status[k].agg_last, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-        const unsigned long long incl = __ballot(f == kIncl);
-        const int stop = incl ? __ffsll((long long)incl) - 1 : 63;  // nearest inclusive prefix
-        unsigned long long v = lane <= stop ? cnt : 0ull;
-#pragma unroll
-        for (int s = 32; s; s >>= 1) v += __shfl_xor(v, s);
-        excl += v;
-        if (!found) {  // the nearest predecessor with a line end (or an inclusive prefix's last)
-          const unsigned long long has = __ballot(lane <= stop && last >= 0);
-          if (has) {
-            elast = __shfl(last, __ffsll((long long)has) - 1);
-            found = true;
-          }
-        }
-        if (incl) break;
-      }
-      if (lane == 0) publish(me, kIncl, excl + tot, tlast >= 0 ? tlast : elast);
-    }
-    if (lane == 0) {
-      s_excl = excl;
-      s_excl_last = elast;
-    }
-  }
-  __syncthreads();
-  const uint64_t g0 = s_excl + xc;
-  long long prev = max(s_excl_last, xl);
+  if (t == 0) tile_bytes[TILE / 16] = make_uint4(0, 0, 0, 0);
+  uint4 cur = load16(buf, n, tile * TILE + t * 16);
+  sct::tile_prefix<WG>(ts, tile, &s_excl, &s_excl_last, red);  // (its barriers also cover the LUT)
+  uint64_t g_base = s_excl;
+  long long last_base = s_excl_last;
+  const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(tile_bytes);
   int32_t mx = 0;
-  for (uint64_t g = g0; m; ++g) {
-    const int j = __ffs(m) - 1;
-    m &= m - 1;
-    const long long P = p0 + j, start = prev + 1;
-    const int32_t L = (int32_t)(P - start);
-    prev = P;
-    mx = max(mx, L);
-    if ((int64_t)g < cap) {
-      uint32_t gg, fl;
-      encode_line<KIND>(lut, buf + start, L, words, codes + g * words, gg, fl);
-      starts[g] = start;
-      lens[g] = L;
-      if (gc) gc[g] = (uint8_t)(gg > 255 ? 255 : gg);
-      if (flags) flags[g] = (uint8_t)fl;
+  for (; tile < tend; ++tile) {
+    const int64_t t0 = tile * TILE, p0 = t0 + t * 16;
+    const uint4 nxt = tile + 1 < tend ? load16(buf, n, p0 + TILE) : make_uint4(0, 0, 0, 0);
+    uint32_t m = p0 < n ? lf_mask_v(cur, n, p0) : 0u;
+    __syncthreads();  // the previous tile's readers of tile_bytes / w_cnt / w_last are done
+    tile_bytes[t] = cur;
+    cur = nxt;
+    const uint32_t c = __popc(m);
+    const long long mylast = m ? p0 + 31 - __clz(m) : -1;
+    // wave-inclusive sum of c and max of mylast, then across the 4 waves
+    uint32_t ic = c;
+    long long il = mylast;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t a = __shfl_up(ic, d);
+      const long long b = __shfl_up(il, d);
+      if (lane >= d) {
+        ic += a;
+        il = max(il, b);
+      }
     }
+    if (lane == 63) {
+      w_cnt[wave] = ic;
+      w_last[wave] = il;
+    }
+    __syncthreads();
+    uint32_t xc = ic - c, tot = 0;  // exclusive within the tile
+    long long xl = __shfl_up(il, 1), tl = -1;
+    if (lane == 0) xl = -1;
+#pragma unroll
+    for (int w = 0; w < WG / 64; ++w) {
+      if (w < wave) {
+        xc += w_cnt[w];
+        xl = max(xl, w_last[w]);
+      }
+      tot += w_cnt[w];
+      tl = max(tl, w_last[w]);
+    }
+    long long prev = max(last_base, xl);
+    for (uint64_t g = g_base + xc; m; ++g) {
+      const int j = __ffs(m) - 1;
+      m &= m - 1;
+      const long long P = p0 + j, start = prev + 1;
+      const int32_t L = (int32_t)(P - start);
+      prev = P;
+      mx = max(mx, L);
+      if ((int64_t)g < cap) {
+        uint32_t gg, fl;
+        const uint8_t* src = start >= t0 ? lds8 + (start - t0) : buf + start;
+        encode_line<KIND>(lut, src, L, words, codes + g * words, gg, fl);
+        starts[g] = start;
+        lens[g] = L;
+        if (gc) gc[g] = (uint8_t)(gg > 255 ? 255 : gg);
+        if (flags) flags[g] = (uint8_t)fl;
+      }
+    }
+    g_base += tot;
+    last_base = max(last_base, tl);
   }
 #pragma unroll
   for (int s = 32; s; s >>= 1) mx = max(mx, __shfl_xor(mx, s));
@@ -306,8 +304,17 @@ __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
 #pragma unroll
     for (int w = 1; w < WG / 64; ++w) mx = max(mx, w_max[w]);
     if (mx > __hip_atomic_load(d_maxlen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(d_maxlen, mx);
-    if (tile == ntiles - 1) *d_nlines = s_excl + tot;
+    if (tend == ntiles) *d_nlines = g_base;
   }
+}
+
+// persistent grid: the resident workgroup slots of `kernel` (at most ntiles)
+int64_t resident_slots(const void* kernel, int64_t ntiles) {
+  sct::scalar_quiesce();
+  int dev = 0, cus = 256, per_cu = 0;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, WG, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
+  return std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)cus * per_cu));
 }
 
 // Scratch of one call, allocated and freed in stream order from the library's private memory
@@ -399,16 +406,20 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   }
   const int64_t ntiles = sct::ceil_div(nbytes, TILE);
   SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
-  const size_t sbytes = (size_t)ntiles * sizeof(TileStatus) + 256;
   StreamBuf scratch;
-  SCT_HIP(scratch.alloc(sbytes, s));
-  SCT_HIP(hipMemsetAsync(scratch.p, 0, sbytes, s));
-  TileStatus* status = reinterpret_cast<TileStatus*>(scratch.p);
-  unsigned* ctr = reinterpret_cast<unsigned*>(reinterpret_cast<uint8_t*>(scratch.p) + (size_t)ntiles * sizeof(TileStatus));
+  SCT_HIP(scratch.alloc(sct::tile_sums_bytes(ntiles), s));
+  const sct::TileSums ts = sct::tile_sums_at(scratch.p, ntiles, true);
+  hipLaunchKernelGGL(wl_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, ts);
+  SCT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sct::tile_sums_reduce_kernel, dim3((unsigned)sct::ceil_div(ntiles, 1024)), dim3(64), 0, s, ts,
+                     ntiles);
+  SCT_LAUNCH_CHECK();
   const int64_t cap = max_lines > 0 ? max_lines : 0;
   auto kern = kind == 2 ? whitelist_fused_kernel<2> : whitelist_fused_kernel<3>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, ntiles, status, ctr, cap, words,
-                     d_codes, d_starts, d_lens, d_gc, d_flags, reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen);
+  const int64_t per_wg = sct::ceil_div(ntiles, resident_slots((const void*)kern, ntiles));
+  hipLaunchKernelGGL(kern, dim3((unsigned)sct::ceil_div(ntiles, per_wg)), dim3(WG), 0, s, d_buf, nbytes, ntiles,
+                     per_wg, ts, cap, words, d_codes, d_starts, d_lens, d_gc, d_flags,
+                     reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }

@@ -286,7 +286,7 @@ def _fused_cases(fq_golden, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("text_mode", [0, 1])
 def test_fastq_fused_one_pass_vs_indexed(fq_golden, tmp_path, text_mode):
-    """sct_fastq_extract_fused (index + extraction in one read, decoupled look-back; VERDICT r3
+    """sct_fastq_extract_fused (no index, no scan launch, no host synchronisation; VERDICT r3
     #6) against the indexed two-pass path (itself pinned to the reference's golden outputs
     above): record count, first bad name, every span's sequence / quality rows and lengths, and
     the in-kernel TwoBit encode of span 0's rows against sct_encode of the same rows."""

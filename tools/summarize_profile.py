@@ -33,7 +33,25 @@ KERNELS = (
     ("spectral16", "tile16_kernel", "s5pmc", "s5trace", 65536, "slices of 2^16"),
     ("nearest", "halves_query_kernel", "npmc", "ntrace", 100_000_000, "queries"),
     ("nearest_index", "halves_index_kernel", "npmc", "ntrace", 100_000_000, "queries"),
+    ("whitelist_fused", "whitelist_fused_kernel", "ipmc", "itrace", 3_686_400, "lines"),
+    ("fastq_range", "fastq_range_kernel", "ipmc", "itrace", 20_000_000, "records"),
 )
+
+
+def timed_window(src, trace, kernel_substr, last):
+    """Mean duration of the LAST `last` dispatches of a kernel in a kernel trace: the dispatches
+    of the bench's timed steps (the warm-up steps and a plan's first launch into a fresh
+    intermediate come first), i.e. the launches the bench line's HIP events time."""
+    path = os.path.join(src, trace, "run_kernel_trace.csv")
+    if not os.path.exists(path):
+        return None
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(path))
+         if kernel_substr in r["Kernel_Name"]]
+    if not d:
+        return None
+    w = d[-last:]
+    return {"kernel": kernel_substr, "dispatches": len(d), "window": len(w), "avg_ns": sum(w) / len(w),
+            "all_avg_ns": sum(d) / len(d)}
 
 
 def pmc_means(src, prefix, kernel_substr):
@@ -101,10 +119,17 @@ def main():
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
     for trace, fn in (("trace", "%s_kernel_stats.csv"), ("ntrace", "%s_nearest_kernel_stats.csv"),
-                      ("s5trace", "%s_config5_kernel_stats.csv")):
+                      ("s5trace", "%s_config5_kernel_stats.csv"), ("itrace", "%s_ingest_kernel_stats.csv")):
         src = os.path.join(a.src, trace, "run_kernel_stats.csv")
         if os.path.exists(src):
             shutil.copy(src, os.path.join(dst, fn % a.round))
+    ap_steps = int(os.environ.get("BENCH_STEPS", "20"))
+    win = {k: timed_window(a.src, "trace", k, ap_steps) for k in ("tile_reg_kernel", "seed_sm_kernel")}
+    with open(os.path.join(dst, "%s_timed_dispatches.json" % a.round), "w") as f:
+        json.dump({"command": "python3 bench.py --gpus 1 --steps %d --warmup 5" % ap_steps, "kernels": win,
+                   "note": "rocprofv3 kernel trace of the command; avg_ns = the last `window` dispatches of "
+                           "the kernel (the timed steps), all_avg_ns = every dispatch"}, f, indent=1)
+    print("timed window", json.dumps(win))
     for name, kernel, prefix, trace, units, unit in KERNELS:
         r = summarize(a.src, dst, a.round, name, kernel, prefix, trace, units, unit)
         print(name, json.dumps({k: v for k, v in (r or {}).items() if k != "pmc"}, indent=1))
