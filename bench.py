@@ -616,9 +616,10 @@ def path_whitelist(dev, reps, copy_gbs):
                 "workload": "config 5's whitelist file: %d lines of 16 bases + LF (%d bytes, device-resident): "
                             "line split (line[:-1]) + TwoBit encode + GC" % (n, nbytes),
                 "value": n / (ms_in * 1e-3), "unit": "lines/s", "ms": ms_in, "reps": reps,
-                "roofline": roof(algo_in, ms_in, "sct_whitelist_encode (whitelist_fused_kernel, one pass)",
-                                 "algorithmic bytes: the file once + codes / starts / lens / GC / flags; one "
-                                 "kernel with a decoupled look-back for the line numbers, no host sync"),
+                "roofline": roof(algo_in, ms_in, "sct_whitelist_encode (wl_count_kernel + whitelist_fused_kernel)",
+                                 "algorithmic bytes: the file once + codes / starts / lens / GC / flags; a count "
+                                 "pass, a one-wave reduction of the tile counts and the encode pass (no scan "
+                                 "launch, no host sync)"),
                 "check": {"every_line": ok_in, "sample": "all %d codes, GC counts, starts and lengths vs the "
                                                          "generating codes, no flags" % n}},
             "base_frequency": {
@@ -720,7 +721,8 @@ def path_fastq(dev, reps, copy_gbs):
     def run():  # one pass: index + CB / UMI slices + the CB encode, asynchronous (no host sync)
         _lib.check(lib.sct_fastq_extract_fused(
             buf.data_ptr(), nbytes, d_ends.data_ptr(), 1, 0, spans.ctypes.data, 2, n_rec, seqs.data_ptr(),
-            quals.data_ptr(), None, None, codes.data_ptr(), gc.data_ptr(), flags.data_ptr(), status.data_ptr(), stream))
+            quals.data_ptr(), None, None, codes.data_ptr(), gc.data_ptr(), flags.data_ptr(), 2, status.data_ptr(),
+            stream))
     ms = _events_ms(run, reps, dev)
     i = torch.randint(0, n_rec, (256,), device=dev, generator=g)
     st = status.cpu().tolist()
@@ -738,11 +740,109 @@ def path_fastq(dev, reps, copy_gbs):
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
                          "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs,
                          "algo_bytes_per_record": algo / n_rec, "kernel": "fastq_range_kernel (sct_fastq_extract_fused)",
-                         "note": "algorithmic bytes: the FASTQ once + the slices + codes; one kernel reads the "
-                                 "buffer once (decoupled look-back for the line numbers, the CB encode fused), "
-                                 "no host sync (DESIGN.md §3.6)"},
+                         "note": "algorithmic bytes: the FASTQ once + the slices + codes; a count pass, a "
+                                 "one-wave reduction of the tile counts, and the extraction (contiguous tile "
+                                 "ranges carrying the line numbers, the CB encode fused); no scan launch, no "
+                                 "host sync (DESIGN.md §3.6)"},
             "check": {"sampled": ok, "sample": "256 random records: CB / UMI / CB-quality slices equal the "
                                                "record bytes, CB codes vs oracle.two_bit_encode"}}
+
+
+def path_pipeline(dev, reps, copy_gbs, threads):
+    """The correction flow end to end at size (VERDICT r3 missing #4): a device-resident R1 FASTQ
+    whose 20M cell barcodes are config 4's observed barcodes (50 % whitelist draws, 25 % one
+    substitution, 15 % one N, 10 % random), the CB / UMI slices (fastq.py:188-200, TenXV2
+    platform.py:36-37) with the CB ThreeBit-encoded as it is sliced (N kept,
+    encodings.py:155-167), then the nearest whitelist barcode at Hamming <= 1 (config 4's index
+    over the 737,280-code whitelist, encodings.py:194-202).  Timed: extraction + query; the
+    index is built once beside it (`index_build_ms`)."""
+    import torch
+    from oracle import oracle as O
+    from sctools_amd import _lib, synthetic
+    n, L, seed = synthetic.CONFIGS[4]
+    n_rec = 20_000_000
+    wl = synthetic.two_to_three(synthetic.whitelist_codes(n, L, seed), L)
+    q, pick, cls = synthetic.config4_queries(wl, n_rec, seed=7, device=dev)
+    g = torch.Generator(device=dev).manual_seed(8)
+    acgt = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    three = torch.tensor(list(b"?CAGT?N?"), dtype=torch.uint8, device=dev)  # ThreeBit value -> base
+    rec = torch.empty((n_rec, 69), dtype=torch.uint8, device=dev)
+    rec[:, 0] = ord("@")
+    rec[:, 1:12] = ord("r")
+    rec[:, 12] = 10
+    for p_ in range(L):  # the CB: the query's bases, MSB-first
+        rec[:, 13 + p_] = three[(q >> (3 * (L - 1 - p_))) & 7]
+    rec[:, 29:39] = acgt[torch.randint(0, 4, (n_rec, 10), device=dev, generator=g)]
+    rec[:, 39] = 10
+    rec[:, 40] = ord("+")
+    rec[:, 41] = 10
+    rec[:, 42:68] = ord("F")
+    rec[:, 68] = 10
+    buf = rec.reshape(-1)
+    nbytes = buf.numel()
+    seqs = torch.empty(n_rec * 24, dtype=torch.uint8, device=dev)
+    quals = torch.empty_like(seqs)
+    codes = torch.empty(n_rec, dtype=torch.int64, device=dev)
+    flags = torch.empty(n_rec, dtype=torch.uint8, device=dev)
+    idx = torch.empty(n_rec, dtype=torch.int32, device=dev)
+    dist = torch.empty(n_rec, dtype=torch.uint8, device=dev)
+    lib = _lib.lib()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    d_ends = torch.tensor([nbytes], dtype=torch.int64, device=dev)
+    status = torch.zeros(3, dtype=torch.int64, device=dev)
+    spans = np.array([[0, 16], [16, 24]], dtype=np.int32)
+    d_wl = torch.from_numpy(wl.view(np.int64)).to(dev)
+    for k in range(2):  # the second build is the one reported (the first pays the first-use costs)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        plan = _lib.NearestPlan(3, d_wl.data_ptr(), n, 3 * L, 1, stream)
+        torch.cuda.synchronize()
+        build_ms = (time.perf_counter() - t) * 1e3
+        if k == 0:
+            plan.close()
+
+    def extract():
+        _lib.check(lib.sct_fastq_extract_fused(
+            buf.data_ptr(), nbytes, d_ends.data_ptr(), 1, 0, spans.ctypes.data, 2, n_rec, seqs.data_ptr(),
+            quals.data_ptr(), None, None, codes.data_ptr(), None, flags.data_ptr(), 3, status.data_ptr(), stream))
+
+    def query():
+        plan.query(codes.data_ptr(), n_rec, idx.data_ptr(), dist.data_ptr(), stream)
+
+    def run():
+        extract()
+        query()
+    ms = _events_ms(run, reps, dev)
+    ms_x = _events_ms(extract, reps, dev)
+    ms_q = _events_ms(query, reps, dev)
+    plan.close()
+    torch.cuda.synchronize()
+    st = status.cpu().tolist()
+    ok_codes = st[0] == 4 * n_rec and st[1] == 0 and bool(torch.equal(codes, q)) and not bool(flags.any())
+    exact = cls == 0
+    ok_exact = bool(torch.equal(idx[exact].long(), pick[exact])) and bool((dist[exact] == 0).all())
+    samp = torch.randint(0, n_rec, (20_000,), device=dev, generator=g)
+    ridx, rdist = O.c_nearest(3, wl, q[samp].cpu().numpy().view(np.uint64), 1, threads=threads)
+    ok_samp = bool(np.array_equal(idx[samp].cpu().numpy(), ridx) and np.array_equal(dist[samp].cpu().numpy(), rdist))
+    algo = nbytes + n_rec * (16 + 8) * 2 + n_rec * (8 + 1) + n_rec * (8 + 4 + 1)
+    gbs = algo / (ms * 1e-3) / 1e9
+    del rec, buf, seqs, quals, codes, flags, idx, dist, q, pick, cls
+    torch.cuda.empty_cache()
+    return {"workload": "FASTQ -> CB ThreeBit -> nearest whitelist at size: %d-record R1 FASTQ (%d bytes, "
+                        "device-resident) whose CBs are config 4's observed barcodes, vs the %d-code "
+                        "whitelist at Hamming <= 1" % (n_rec, nbytes, n),
+            "value": n_rec / (ms * 1e-3), "unit": "records/s", "ms": ms, "reps": reps,
+            "extract_ms": ms_x, "query_ms": ms_q, "index_build_ms": build_ms,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
+                         "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs,
+                         "algo_bytes_per_record": algo / n_rec,
+                         "kernel": "fastq_range_kernel (ThreeBit CB fused) + halves_query_kernel",
+                         "note": "algorithmic bytes: the FASTQ once + slices + codes / flags written, the "
+                                 "codes read again by the query + index / distance written"},
+            "check": {"codes_equal_queries": ok_codes, "exact_draws_own_index": ok_exact,
+                      "sampled_vs_oracle": ok_samp,
+                      "sample": "every CB code equals the query it was printed from; every exact draw finds "
+                                "its own index; 20,000 random records vs oracle.c_nearest"}}
 
 
 # ------------------------------------------------------------------ ranks
@@ -895,7 +995,9 @@ def run_rank(args, rank, world, local):
             out["paths"] = {"config4_nearest": path_config4(dev, args.path_steps, copy_gbs, threads),
                             "config5_allpairs": path_config5_allpairs(dev, max(2, args.path_steps), copy_gbs),
                             "config5_encode": path_config5_encode(dev, max(2, args.path_steps // 2), copy_gbs),
-                            "fastq_ingest": _guarded(path_fastq, dev, max(2, args.path_steps), copy_gbs)}
+                            "fastq_ingest": _guarded(path_fastq, dev, max(2, args.path_steps), copy_gbs),
+                            "fastq_to_nearest": _guarded(path_pipeline, dev, max(2, args.path_steps), copy_gbs,
+                                                         threads)}
             wl = _guarded(path_whitelist, dev, max(5, args.path_steps), copy_gbs)
             out["paths"].update(wl if "error" not in wl else {"whitelist_ingest": wl})
             if args.config == 2:

@@ -52,8 +52,9 @@ int sct_set_device(int device);        /* select the device for later calls (hip
 #define SCT_TUNE_SCALAR_IDLE_MS 9       /* the scalar server exits after this idle time (5) */
 #define SCT_TUNE_SPECTRAL_COLUMNS 10   /* SPECTRAL column width: 0 auto, 14, or 16 (when int8 fits) */
 #define SCT_TUNE_PLAN_CACHE 11          /* 0: every all-pairs plan allocates its own buffers (default 1) */
-#define SCT_TUNE_ENCODE_GRID 12         /* tiled encoder grid: 0 resident workgroups (default), 1 one per tile */
-#define SCT_TUNE_NKEYS 13
+#define SCT_TUNE_ENCODE_GRID 12         /* tiled encoder grid: 1 one workgroup per tile (default), 0 resident workgroups */
+#define SCT_TUNE_INGEST_TILES 13        /* whitelist / FASTQ extraction: tiles per workgroup (0: resident grid) */
+#define SCT_TUNE_NKEYS 14
 int sct_tune_set(int key, int64_t value);
 int sct_tune_get(int key, int64_t* value);  /* -1 when unset */
 
@@ -394,12 +395,13 @@ int sct_fastq_extract_spans(sct_fastq_index* index, const uint8_t* d_buf, const 
  * caller's capacity (span k's row r at out + cap_records * prefix_k + r * width_k; lengths at
  * len + k * cap + r; records >= cap_records are not written); d_status (3 int64, device): [0]
  * line count (records = lines / 4), [1] ~(first bad-name record) or 0, [2] non-ASCII seen (text
- * mode rejects it).  d_codes0 / d_gc0 / d_flags0 (nullable): span 0's sequence rows TwoBit-encoded
- * (width <= 32) as sct_encode would encode those rows. */
+ * mode rejects it).  d_codes0 / d_gc0 / d_flags0 (nullable): span 0's sequence rows encoded as
+ * sct_encode(code_kind) would encode those rows (code_kind 2 TwoBit, width <= 32; 3 ThreeBit,
+ * width <= 21 -- N kept, the queries of sct_nearest_query). */
 int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, const int64_t* d_file_ends, int nfiles,
                             int text_mode, const int32_t* spans, int nspans, int64_t cap_records, uint8_t* d_seq,
                             uint8_t* d_qual, int32_t* d_seq_len, int32_t* d_qual_len, uint64_t* d_codes0,
-                            uint8_t* d_gc0, uint8_t* d_flags0, int64_t* d_status, void* stream);
+                            uint8_t* d_gc0, uint8_t* d_flags0, int code_kind, int64_t* d_status, void* stream);
 /* Host convenience: spans = nspans (start, end) pairs.  Call with max_records < the record
  * count to learn nrecords (outputs untouched); then with room for nrecords:
  * seq_out/qual_out (nullable) = span k's rows at offset sum_{i<k} nrecords*width_i,

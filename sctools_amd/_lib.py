@@ -32,7 +32,7 @@ SCHEME_SPECTRAL = 2
 TUNE_KEYS = {"spectral_chunk": 1, "spectral_min_n": 2, "allpairs_grab": 3, "allpairs_flush_items": 4,
              "allpairs_grid": 5, "nearest_scheme": 6, "nearest_load": 7, "scalar_server": 8,
              "scalar_idle_ms": 9, "spectral_columns": 10, "plan_cache": 11,
-             "encode_grid": 12}
+             "encode_grid": 12, "ingest_tiles": 13}
 NEAREST_AUTO, NEAREST_OA, NEAREST_CSR, NEAREST_HALVES = 0, 1, 2, 3
 
 _i32, _i64, _dbl = ctypes.c_int, ctypes.c_int64, ctypes.c_double
@@ -104,7 +104,7 @@ SIGNATURES = {
                                ctypes.POINTER(_i64), ctypes.POINTER(_i64)],
     "sct_base_frequency_host": [_vp, _i64, _i32, _vp],
     "sct_fastq_extract_fused": [_vp, _i64, _vp, _i32, _i32, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                _vp, _vp],
+                                _i32, _vp, _vp],
     "sct_fastq_stream_create": [_i32, _vp, _i32, _i32, ctypes.POINTER(_vp)],
     "sct_fastq_stream_destroy": [_vp],
     "sct_fastq_stream_chunk": [_vp, _vp, _i64, _vp, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_i64),

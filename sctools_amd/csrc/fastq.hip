@@ -497,12 +497,12 @@ __global__ __launch_bounds__(WG) void fq_count_kernel(const uint8_t* __restrict_
   }
 }
 
-// 4 bytes of a row through the TwoBit LUT (lut_entry: code in bits 0..2, flags above)
-__device__ __forceinline__ void enc_dword(const uint8_t* lut, uint32_t y, uint64_t& code, uint32_t& fl) {
+// 4 bytes of a row through the LUT of a `bits`-bit code (lut_entry: code in bits 0..2, flags above)
+__device__ __forceinline__ void enc_dword(const uint8_t* lut, int bits, uint32_t y, uint64_t& code, uint32_t& fl) {
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     const uint32_t e = lut[(y >> (8 * b)) & 0xFFu];
-    code = (code << 2) | (e & 7u);
+    code = (code << bits) | (e & 7u);
     fl |= e;
   }
 }
@@ -510,13 +510,14 @@ __device__ __forceinline__ void enc_dword(const uint8_t* lut, uint32_t y, uint64
 // Rows of records >= cap are skipped; span k's row r at out + cap * prefix_k + r * width_k, its
 // length at len + k * cap + r; d_status[0] = the line count, d_status[1] = ~(first bad-name
 // record) or 0 (records < lines / 4 only, as extract2_kernel); optionally span 0's sequence rows
-// TwoBit-encoded as they are written (one limb, width <= 32; gc and flags as sct_encode's).
+// encoded as they are written (code_kind 2 TwoBit / 3 ThreeBit, one limb: width <= 32 / 21; gc
+// and flags as sct_encode's).
 __global__ __launch_bounds__(WG) void fastq_range_kernel(
     const uint8_t* __restrict__ buf, int64_t n, Files fs, int text, sct::TileSums ts,
     const uint32_t* __restrict__ first, int64_t ntiles, int64_t per_wg, int64_t cap, Spans sp,
     uint8_t* __restrict__ seq_out, uint8_t* __restrict__ qual_out, int32_t* __restrict__ seq_len,
     int32_t* __restrict__ qual_len, uint64_t* __restrict__ codes0, uint8_t* __restrict__ gc0,
-    uint8_t* __restrict__ flags0, unsigned long long* __restrict__ d_status) {
+    uint8_t* __restrict__ flags0, int code_kind, unsigned long long* __restrict__ d_status) {
   __shared__ uint16_t term[MAX_TERM];
   __shared__ uint4 tile_bytes[TILE / 16];
   __shared__ uint32_t w_cnt[WG / 64];
@@ -529,7 +530,8 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
   if (tile >= ntiles) return;  // (the whole workgroup)
   const int64_t tend = tile + per_wg < ntiles ? tile + per_wg : ntiles;
   if (codes0)
-    for (int c = tid; c < 256; c += WG) lut[c] = lut_entry(2, c);
+    for (int c = tid; c < 256; c += WG) lut[c] = lut_entry(code_kind, c);
+  const uint64_t gc_mask = code_kind == 2 ? 0x5555555555555555ull : 0x9249249249249249ull;
   uint4 cur[SEG], nxt[SEG];
 #pragma unroll
   for (int k = 0; k < SEG; ++k) cur[k] = load16(buf, n, tile * TILE + (int64_t)tid * TB + 16 * k);
@@ -668,25 +670,25 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
                                        __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
             *reinterpret_cast<uint4*>(o) = y;
             if (enc) {
-              enc_dword(lut, y.x, code, fl);
-              enc_dword(lut, y.y, code, fl);
-              enc_dword(lut, y.z, code, fl);
-              enc_dword(lut, y.w, code, fl);
+              enc_dword(lut, code_kind, y.x, code, fl);
+              enc_dword(lut, code_kind, y.y, code, fl);
+              enc_dword(lut, code_kind, y.z, code, fl);
+              enc_dword(lut, code_kind, y.w, code, fl);
             }
           } else if (nd == 2 && ((uintptr_t)o & 7) == 0) {
             const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
             const uint2 y = make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
             *reinterpret_cast<uint2*>(o) = y;
             if (enc) {
-              enc_dword(lut, y.x, code, fl);
-              enc_dword(lut, y.y, code, fl);
+              enc_dword(lut, code_kind, y.x, code, fl);
+              enc_dword(lut, code_kind, y.y, code, fl);
             }
           } else {
             uint32_t lo = d[0];
             for (int q2 = 0; q2 < nd; ++q2) {
               const uint32_t hi = d[q2 + 1], y = __builtin_amdgcn_alignbyte(hi, lo, sh);
               od[q2] = y;
-              if (enc) enc_dword(lut, y, code, fl);
+              if (enc) enc_dword(lut, code_kind, y, code, fl);
               lo = hi;
             }
           }
@@ -698,15 +700,15 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
             o[j] = v;
             if (enc) {
               const uint32_t en = lut[v];
-              code = (code << 2) | (en & 7u);
+              code = (code << code_kind) | (en & 7u);
               fl |= en;
             }
           }
         }
-        if (enc) {  // span 0's row (as written, zero-padded) -> TwoBit
+        if (enc) {  // span 0's row (as written, zero-padded) -> its code
           codes0[rec] = code;
           if (gc0) {
-            const uint32_t g = (uint32_t)__popcll(code & 0x5555555555555555ull);
+            const uint32_t g = (uint32_t)__popcll(code & gc_mask);
             gc0[rec] = (uint8_t)(g > 255 ? 255 : g);
           }
           if (flags0) flags0[rec] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
@@ -950,12 +952,13 @@ namespace {
 // k's row r at out + cap * prefix_k + r * width_k, its length at len + k * cap + r; rows of
 // records >= cap_records are not written); d_status (3 x int64, device) receives the line count
 // (records = lines / 4), ~(first bad-name record) or 0, and a text-mode non-ASCII flag.
-// d_codes0 / d_gc0 / d_flags0 (nullable): span 0's sequence rows TwoBit-encoded (width <= 32).
+// d_codes0 / d_gc0 / d_flags0 (nullable): span 0's sequence rows encoded (code_kind 2 TwoBit,
+// width <= 32; 3 ThreeBit, width <= 21: N kept as 6, the input of sct_nearest_query).
 extern "C" int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, const int64_t* d_file_ends, int nfiles,
                                        int text_mode, const int32_t* spans, int nspans, int64_t cap_records,
                                        uint8_t* d_seq, uint8_t* d_qual, int32_t* d_seq_len, int32_t* d_qual_len,
-                                       uint64_t* d_codes0, uint8_t* d_gc0, uint8_t* d_flags0, int64_t* d_status,
-                                       void* stream) {
+                                       uint64_t* d_codes0, uint8_t* d_gc0, uint8_t* d_flags0, int code_kind,
+                                       int64_t* d_status, void* stream) {
   SCT_CHECK(d_status != nullptr && nfiles >= 1 && d_file_ends != nullptr, "bad arguments");
   SCT_CHECK(nbytes >= 0 && (nbytes == 0 || d_buf != nullptr) && cap_records >= 0, "bad buffer");
   SCT_CHECK(nspans >= 0 && nspans <= MAX_SPANS && (nspans == 0 || spans), "0..%d spans", MAX_SPANS);
@@ -972,7 +975,9 @@ extern "C" int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, con
     pre += sp.end[k] - sp.start[k];
   }
   sp.width = (int)pre;
-  SCT_CHECK(!d_codes0 || (nspans >= 1 && sp.end[0] - sp.start[0] <= 32 && d_seq), "span 0 encode needs width <= 32");
+  SCT_CHECK(code_kind == 2 || code_kind == 3, "code_kind must be 2 or 3");
+  SCT_CHECK(!d_codes0 || (nspans >= 1 && code_kind * (sp.end[0] - sp.start[0]) <= 64 && d_seq),
+            "span 0 encode needs one limb (width <= %d)", 64 / code_kind);
   hipStream_t s = sct::as_stream(stream);
   SCT_HIP(hipMemsetAsync(d_status, 0, 24, s));
   if (nbytes == 0) return SCT_OK;
@@ -989,11 +994,13 @@ extern "C" int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, con
   hipLaunchKernelGGL(sct::tile_sums_reduce_kernel, dim3((unsigned)sct::ceil_div(ntiles, 1024)), dim3(64), 0, s, ts,
                      ntiles);
   // contiguous tile ranges, one per resident workgroup slot
-  const int64_t grid = resident_grid((const void*)fastq_range_kernel, ntiles);
-  const int64_t per_wg = sct::ceil_div(ntiles, grid);
+  const int64_t knob = sct::tune(SCT_TUNE_INGEST_TILES, 0);
+  const int64_t per_wg =
+      knob > 0 ? knob : sct::ceil_div(ntiles, (int64_t)resident_grid((const void*)fastq_range_kernel, ntiles));
   hipLaunchKernelGGL(fastq_range_kernel, dim3((unsigned)sct::ceil_div(ntiles, per_wg)), dim3(WG), 0, s, d_buf, nbytes,
                      fs, text_mode ? 1 : 0, ts, (const uint32_t*)first, ntiles, per_wg, cap_records, sp, d_seq, d_qual,
-                     d_seq_len, d_qual_len, d_codes0, d_gc0, d_flags0, reinterpret_cast<unsigned long long*>(d_status));
+                     d_seq_len, d_qual_len, d_codes0, d_gc0, d_flags0, code_kind,
+                     reinterpret_cast<unsigned long long*>(d_status));
   hipError_t e = hipGetLastError();
   sct::pool_free(scratch, s);
   if (e != hipSuccess) return sct::fail(SCT_E_HIP, "fastq fused: %s", hipGetErrorString(e));

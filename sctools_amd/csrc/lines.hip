@@ -416,7 +416,8 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   SCT_LAUNCH_CHECK();
   const int64_t cap = max_lines > 0 ? max_lines : 0;
   auto kern = kind == 2 ? whitelist_fused_kernel<2> : whitelist_fused_kernel<3>;
-  const int64_t per_wg = sct::ceil_div(ntiles, resident_slots((const void*)kern, ntiles));
+  const int64_t knob = sct::tune(SCT_TUNE_INGEST_TILES, 0);
+  const int64_t per_wg = knob > 0 ? knob : sct::ceil_div(ntiles, resident_slots((const void*)kern, ntiles));
   hipLaunchKernelGGL(kern, dim3((unsigned)sct::ceil_div(ntiles, per_wg)), dim3(WG), 0, s, d_buf, nbytes, ntiles,
                      per_wg, ts, cap, words, d_codes, d_starts, d_lens, d_gc, d_flags,
                      reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen);

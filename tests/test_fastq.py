@@ -221,7 +221,7 @@ def test_whitelist_lines_on_device_vs_python(tmp_path):
     assert np.array_equal(big.codes_array(), codes)
 
 
-def _fused(data, ends, spans, text_mode, cap=None, encode=True):
+def _fused(data, ends, spans, text_mode, cap=None, encode=True, kind=2):
     """sct_fastq_extract_fused on device copies; returns (nrec, first_bad, per-span rows/lens,
     codes/gc/flags of span 0) trimmed to nrec."""
     import ctypes
@@ -247,7 +247,7 @@ def _fused(data, ends, spans, text_mode, cap=None, encode=True):
         d_buf.data_ptr(), n, d_ends.data_ptr(), len(ends), int(text_mode), sp.ctypes.data_as(ctypes.c_void_p),
         len(spans), cap, seq.data_ptr(), qual.data_ptr(), slen.data_ptr(), qlen.data_ptr(),
         codes.data_ptr() if encode else None, gc.data_ptr() if encode else None, fl.data_ptr() if encode else None,
-        status.data_ptr(), None))
+        kind, status.data_ptr(), None))
     torch.cuda.synchronize()
     st = status.cpu().numpy().view(np.uint64)
     nrec = int(st[0]) // 4
@@ -289,7 +289,7 @@ def test_fastq_fused_one_pass_vs_indexed(fq_golden, tmp_path, text_mode):
     """sct_fastq_extract_fused (no index, no scan launch, no host synchronisation; VERDICT r3
     #6) against the indexed two-pass path (itself pinned to the reference's golden outputs
     above): record count, first bad name, every span's sequence / quality rows and lengths, and
-    the in-kernel TwoBit encode of span 0's rows against sct_encode of the same rows."""
+    the in-kernel TwoBit and ThreeBit encodes of span 0's rows against sct_encode of the same rows."""
     from sctools_amd import _lib
     spans = [(0, 16), (16, 26), (3, 9)]
     for name, data, ends in _fused_cases(fq_golden, tmp_path):
@@ -305,6 +305,11 @@ def test_fastq_fused_one_pass_vs_indexed(fq_golden, tmp_path, text_mode):
             codes, gc, flags = _lib.encode(2, np.ascontiguousarray(ref[0][0]), 16)
             assert np.array_equal(enc[0], codes[:, 0]) and np.array_equal(enc[1], gc), name
             assert np.array_equal(enc[2], flags), name
+            # ThreeBit (N kept as 6): the queries of the nearest-whitelist correction
+            _, _, _, enc3, _ = _fused(data, ends, spans, text_mode, kind=3)
+            codes3, gc3, flags3 = _lib.encode(3, np.ascontiguousarray(ref[0][0]), 16)
+            assert np.array_equal(enc3[0], codes3[:, 0]) and np.array_equal(enc3[1], gc3), name
+            assert np.array_equal(enc3[2], flags3), name
         # a capacity below the record count: the rows below it are the same
         if n0 > 3:
             n2, _, got2, _, _ = _fused(data, ends, spans, text_mode, cap=n0 - 2)

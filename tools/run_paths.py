@@ -1,5 +1,5 @@
 """Run selected bench.py side paths alone: python tools/run_paths.py config4 dropin whitelist fastq
-config5_encode config5_allpairs copy.  One JSON line {name: result}."""
+config5_encode config5_allpairs pipeline.  One JSON line {name: result}."""
 import json
 import sys
 
@@ -26,6 +26,8 @@ for name in names:
         out[name] = bench._guarded(bench.path_whitelist, dev, 5, copy)
     elif name == "fastq":
         out[name] = bench._guarded(bench.path_fastq, dev, 5, copy)
+    elif name == "pipeline":
+        out[name] = bench._guarded(bench.path_pipeline, dev, 5, copy, threads)
     elif name == "config5_encode":
         out[name] = bench._guarded(bench.path_config5_encode, dev, 3, copy)
     elif name == "config5_allpairs":
