@@ -53,7 +53,8 @@ int sct_set_device(int device);        /* select the device for later calls (hip
 #define SCT_TUNE_SPECTRAL_COLUMNS 10   /* SPECTRAL column width: 0 auto, 14, or 16 (when int8 fits) */
 #define SCT_TUNE_PLAN_CACHE 11          /* 0: every all-pairs plan allocates its own buffers (default 1) */
 #define SCT_TUNE_ENCODE_GRID 12         /* tiled encoder grid: 1 one workgroup per tile (default), 0 resident workgroups */
-#define SCT_TUNE_INGEST_TILES 13        /* whitelist / FASTQ extraction: tiles per workgroup (0: resident grid) */
+#define SCT_TUNE_INGEST_TILES 13        /* whitelist / FASTQ extraction: tiles per workgroup (0: one range per
+                                           resident slot, the whitelist's default; FASTQ default 8) */
 #define SCT_TUNE_NKEYS 14
 int sct_tune_set(int key, int64_t value);
 int sct_tune_get(int key, int64_t* value);  /* -1 when unset */

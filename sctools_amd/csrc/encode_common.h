@@ -9,6 +9,21 @@ namespace {
 
 constexpr uint8_t F_AMBIG = 0x40, F_INVALID = 0x80;
 
+// Pointers typed as LDS (address space 3): reads through them are ds_read.  A generic pointer
+// that may point at LDS or at global memory compiles to flat loads, and the compiler waits
+// vmcnt(0) AND lgkmcnt(0) after every flat load -- draining the tile prefetch and every
+// outstanding store of the workgroup's loop each time (the ingest kernels' tile loops).
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+template <class T>
+__device__ __forceinline__ lds_u32* as_lds32(T* p) {
+  return (lds_u32*)(p);
+}
+template <class T>
+__device__ __forceinline__ lds_u8* as_lds8(T* p) {
+  return (lds_u8*)(p);
+}
+
 // LUT entry: low 3 bits = code, 0x40 = IUPAC ambiguous (TwoBit), 0x80 = invalid (TwoBit)
 __host__ __device__ inline uint8_t lut_entry(int kind, int c) {
   if (kind == 2) {

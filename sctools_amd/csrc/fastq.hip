@@ -994,9 +994,13 @@ extern "C" int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, con
   hipLaunchKernelGGL(sct::tile_sums_reduce_kernel, dim3((unsigned)sct::ceil_div(ntiles, 1024)), dim3(64), 0, s, ts,
                      ntiles);
   // contiguous tile ranges, one per resident workgroup slot
-  const int64_t knob = sct::tune(SCT_TUNE_INGEST_TILES, 0);
-  const int64_t per_wg =
-      knob > 0 ? knob : sct::ceil_div(ntiles, (int64_t)resident_grid((const void*)fastq_range_kernel, ntiles));
+  // contiguous ranges of 8 tiles (64 KiB) per workgroup: 1.09-1.10 ms per 20M records against
+  // 1.13-1.20 for one range per resident slot and 1.55 for one tile per workgroup (same box,
+  // tools/ingest_tiles_ab.py); SCT_TUNE_INGEST_TILES = 0 sizes the ranges to the resident grid
+  const int64_t knob = sct::tune(SCT_TUNE_INGEST_TILES, -1);
+  const int64_t per_wg = knob > 0   ? knob
+                         : knob < 0 ? 8
+                                    : sct::ceil_div(ntiles, (int64_t)resident_grid((const void*)fastq_range_kernel, ntiles));
   hipLaunchKernelGGL(fastq_range_kernel, dim3((unsigned)sct::ceil_div(ntiles, per_wg)), dim3(WG), 0, s, d_buf, nbytes,
                      fs, text_mode ? 1 : 0, ts, (const uint32_t*)first, ntiles, per_wg, cap_records, sp, d_seq, d_qual,
                      d_seq_len, d_qual_len, d_codes0, d_gc0, d_flags0, code_kind,

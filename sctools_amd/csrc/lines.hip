@@ -47,6 +47,26 @@ __device__ __forceinline__ uint32_t lf_mask(const uint8_t* __restrict__ buf, int
   return m;
 }
 
+// the 16 bytes at p0 (zero past n) and their line ends (lf_mask)
+__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ buf, int64_t n, int64_t p0) {
+  if (p0 + 16 <= n) return *reinterpret_cast<const uint4*>(buf + p0);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (int j = 0; j < 16 && p0 + j < n; ++j) w[j >> 2] |= (uint32_t)buf[p0 + j] << (8 * (j & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ uint32_t lf_mask_v(uint4 v, int64_t n, int64_t p0) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // (bytes past n are zero, never '\n')
+    const uint32_t x = w[k] ^ 0x0A0A0A0Au;
+    const uint32_t hi = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+    m |= (((hi >> 7) & 1u) | ((hi >> 14) & 2u) | ((hi >> 21) & 4u) | ((hi >> 28) & 8u)) << (4 * k);
+  }
+  if (n > 0 && p0 <= n - 1 && n - 1 < p0 + 16) m |= 1u << (n - 1 - p0);
+  return m;
+}
+
 __global__ __launch_bounds__(WG) void line_count_kernel(const uint8_t* __restrict__ buf, int64_t n,
                                                         unsigned long long* __restrict__ counts) {
   const int64_t p0 = (int64_t)blockIdx.x * TILE + threadIdx.x * 16;
@@ -110,19 +130,33 @@ __global__ __launch_bounds__(WG) void line_lens_kernel(const int64_t* __restrict
 }
 
 // ---------------------------------------------------------------- ingest in two passes (round 4)
-// sct_whitelist_encode: wl_count_kernel counts each 4 KiB tile's line ends and its last one and
-// tile_sums_reduce_kernel sums them into the 3-level tile sums (tile_prefix.h); whitelist_fused_kernel
-// reads the tile again, takes its first line number and the last line end before it from those
-// sums, and encodes every line ending in the tile: line g ends at the g-th line end P_g (a '\n',
-// or the file's last byte) and its chopped content is [P_{g-1} + 1, P_g); each lane encodes the
-// lines ending in its 16 bytes, the first one starting after the latest end before the lane (an
-// exclusive max-scan).  The line count and the longest line stay on the device (no host
-// synchronisation); a 62.7 MB whitelist's second read comes from the Infinity Cache.
+// sct_whitelist_encode: wl_count_kernel counts each 16 KiB tile's line ends and its last one,
+// tile_sums_reduce_kernel sums them into the 3-level tile sums (tile_prefix.h), and
+// whitelist_fused_kernel reads the tiles again, takes its first tile's line number and the last
+// line end before it from those sums, and encodes every line ending in its tiles: line g ends at
+// the g-th line end P_g (a '\n', or the file's last byte) and its chopped content is
+// [P_{g-1} + 1, P_g); each lane encodes the lines ending in its 16-byte pieces, the first one
+// starting after the latest end before the piece.  The line count and the longest line stay on
+// the device (no host synchronisation); a 62.7 MB whitelist's second read comes from the
+// Infinity Cache.  A tile is NSUB = 4 sub-tiles of 4 KiB (the lane's piece j at 4096 j + 16 lane:
+// every load instruction coalesced): 16 KiB per barrier pair and per wait for the loop's loads
+// and stores, which drain at every wait (vmcnt(0): the stores' count varies by line).
+constexpr int NSUB = 4, WTILE = NSUB * TILE;
+
 __global__ __launch_bounds__(WG) void wl_count_kernel(const uint8_t* __restrict__ buf, int64_t n, sct::TileSums ts) {
-  const int64_t tile = blockIdx.x, p0 = tile * TILE + threadIdx.x * 16;
-  const uint32_t m = p0 < n ? lf_mask(buf, n, p0) : 0u;
-  unsigned long long c = __popc(m);
-  long long last = m ? p0 + 31 - __clz(m) : -1;
+  const int64_t t0 = (int64_t)blockIdx.x * WTILE;
+  uint4 v[NSUB];
+#pragma unroll
+  for (int j = 0; j < NSUB; ++j) v[j] = load16(buf, n, t0 + j * TILE + threadIdx.x * 16);
+  unsigned long long c = 0;
+  long long last = -1;
+#pragma unroll
+  for (int j = 0; j < NSUB; ++j) {
+    const int64_t p0 = t0 + j * TILE + threadIdx.x * 16;
+    const uint32_t m = p0 < n ? lf_mask_v(v[j], n, p0) : 0u;
+    c += __popc(m);
+    if (m) last = p0 + 31 - __clz(m);  // (sub-tiles in byte order)
+  }
 #pragma unroll
   for (int o = 32; o; o >>= 1) {
     c += __shfl_xor(c, o);
@@ -140,16 +174,70 @@ __global__ __launch_bounds__(WG) void wl_count_kernel(const uint8_t* __restrict_
       c += wc[w];
       last = max(last, wl[w]);
     }
-    sct::tile_publish(ts, tile, c, last);
+    sct::tile_publish(ts, blockIdx.x, c, last);
   }
 }
 
-// one record [rec, rec + L) through the LUT: the one-limb dword path of encode_var_kernel
-// (encode.hip) for L <= 32, else the generic limb loop; too long for `words` limbs: flag 4
+// one record of L <= 32 bytes at byte offset o (0..3) of an aligned dword window, one limb:
+// dw(k) = dword k of the window (the window's dwords past the record's last are not read).
+// Fast path, 4 bases per step without the LUT (VALU-bound before: the 32-step LUT loop cost
+// ~380 instructions per line, PMC): an upper-case A/C/G/T byte c has TwoBit value
+// v = x ^ (x >> 1), x = ((c >> 1) ^ (c >> 2)) & 3 (A 0, C 1, T 2, G 3), and a byte is one of
+// them iff mapping v back through the table "ACTG" (one v_perm) returns it; the four values go
+// MSB-first into 8 (TwoBit) or 12 (ThreeBit: v_perm through "2143") bits by two shift-ors.  Any
+// other byte in the record (lower case, N, IUPAC, invalid) takes the LUT loop.
+template <int KIND, class DW>
+__device__ __forceinline__ void encode_line1(const uint8_t* lut, DW dw, int o, int L, uint64_t* out, uint32_t& g,
+                                             uint32_t& fl) {
+  constexpr uint64_t gcm = KIND == 2 ? 0x5555555555555555ull : 0x9249249249249249ull;
+  uint64_t code = 0;
+  uint32_t f = 0;
+  if (L > 0) {
+    const int last = (o + L - 1) >> 2;  // the window's last dword
+    const int nd = (L + 3) >> 2;
+    uint32_t lo = dw(0), bad = 0;
+    for (int k = 0; k < nd; ++k) {
+      const uint32_t hi = dw(k + 1 <= last ? k + 1 : last);
+      const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)o);  // bytes 4k .. 4k + 3
+      lo = hi;
+      const int r = L - 4 * k < 4 ? L - 4 * k : 4;
+      const uint32_t x = ((w >> 1) ^ (w >> 2)) & 0x03030303u;
+      const uint32_t v = x ^ ((x >> 1) & 0x01010101u);
+      const uint32_t keep = r == 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1u;
+      bad |= (__builtin_amdgcn_perm(0u, 0x47544341u, v) ^ w) & keep;  // "ACTG"[v] == the byte?
+      const uint32_t y = __builtin_amdgcn_perm(0u, KIND == 2 ? v : __builtin_amdgcn_perm(0u, 0x03040102u, v),
+                                               0x00010203u);  // byte-reversed values
+      uint32_t pk;
+      if (KIND == 2) {  // v3 v2 at bits 0, 2 and v1 v0 at 16, 18; then v1 v0 down to 4, 6
+        const uint32_t a = (y | (y >> 6)) & 0x000F000Fu;
+        pk = (a | (a >> 12)) & 0xFFu;
+      } else {  // v3 v2 at bits 0, 3 and v1 v0 at 16, 19; then v1 v0 down to 6, 9
+        const uint32_t a = (y | (y >> 5)) & 0x003F003Fu;
+        pk = (a | (a >> 10)) & 0xFFFu;
+      }
+      pk >>= KIND * (4 - r);
+      code = (code << (KIND * r)) | pk;
+    }
+    if (bad) {  // the LUT loop (ambiguous / invalid / lower-case bytes; rare: one read per byte)
+      code = 0;
+      for (int p = 0; p < L; ++p) {
+        const uint32_t e = lut[(dw((o + p) >> 2) >> (8 * ((o + p) & 3))) & 0xFFu];
+        code = (code << KIND) | (e & 7u);
+        f |= e;
+      }
+    }
+  }
+  out[0] = code;
+  g = (uint32_t)__popcll(code & gcm);
+  fl = ((f & F_AMBIG) ? 1u : 0u) | ((f & F_INVALID) ? 2u : 0u);
+}
+
+// one record [rec, rec + L) of global memory through the LUT: the one-limb dword path of
+// encode_var_kernel (encode.hip) for L <= 32, else the generic limb loop; too long for `words`
+// limbs: flag 4
 template <int KIND>
 __device__ __forceinline__ void encode_line(const uint8_t* lut, const uint8_t* rec, int L, int words, uint64_t* out,
                                             uint32_t& g, uint32_t& fl) {
-  constexpr uint64_t gcm = KIND == 2 ? 0x5555555555555555ull : 0x9249249249249249ull;
   if ((int64_t)KIND * L > 64 * (int64_t)words) {
     for (int w = 0; w < words; ++w) out[w] = 0;
     g = 0;
@@ -157,60 +245,23 @@ __device__ __forceinline__ void encode_line(const uint8_t* lut, const uint8_t* r
     return;
   }
   if (words == 1 && L <= 32) {
-    uint64_t code = 0;
-    uint32_t f = 0;
-    if (L > 0) {
-      const int o = (int)((uintptr_t)rec & 3), o8 = 8 * o;
-      const uint32_t* dw = reinterpret_cast<const uint32_t*>(rec - o);
-      uint32_t d[9], w[8];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {  // dword k of the record, clamped to its last one
-        const int kk = 4 * k < o + L ? k : (o + L - 1) >> 2;
-        d[k] = dw[kk];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) w[k] = (uint32_t)((((uint64_t)d[k + 1] << 32) | d[k]) >> o8);
-#pragma unroll
-      for (int p = 0; p < 32; ++p)
-        if (p < L) {
-          const uint32_t e = lut[(w[p >> 2] >> (8 * (p & 3))) & 0xFFu];
-          code = (code << KIND) | (e & 7u);
-          f |= e;
-        }
-    }
-    out[0] = code;
-    g = (uint32_t)__popcll(code & gcm);
-    fl = ((f & F_AMBIG) ? 1u : 0u) | ((f & F_INVALID) ? 2u : 0u);
+    const int o = (int)((uintptr_t)rec & 3);
+    const uint32_t* dw = reinterpret_cast<const uint32_t*>(rec - o);
+    encode_line1<KIND>(lut, [&](int k) { return dw[k]; }, o, L, out, g, fl);
     return;
   }
   RecordReader rd{rec, false, 0u, -1};
   encode_record(lut, KIND, rd, L, words, out, g, fl);
 }
 
-// the 16 bytes at p0 (zero past n) and their line ends (lf_mask)
-__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ buf, int64_t n, int64_t p0) {
-  if (p0 + 16 <= n) return *reinterpret_cast<const uint4*>(buf + p0);
-  uint32_t w[4] = {0, 0, 0, 0};
-  for (int j = 0; j < 16 && p0 + j < n; ++j) w[j >> 2] |= (uint32_t)buf[p0 + j] << (8 * (j & 3));
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
-__device__ __forceinline__ uint32_t lf_mask_v(uint4 v, int64_t n, int64_t p0) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t m = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {  // (bytes past n are zero, never '\n')
-    const uint32_t x = w[k] ^ 0x0A0A0A0Au;
-    const uint32_t hi = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
-    m |= (((hi >> 7) & 1u) | ((hi >> 14) & 2u) | ((hi >> 21) & 4u) | ((hi >> 28) & 8u)) << (4 * k);
-  }
-  if (n > 0 && p0 <= n - 1 && n - 1 < p0 + 16) m |= 1u << (n - 1 - p0);
-  return m;
-}
-
 // A contiguous range of per_wg tiles per workgroup: the first tile's line number and last line
 // end before it from the tile sums (once), then tile by tile (the next tile's bytes loaded while
-// this one is encoded), carrying both; the tile's bytes are staged in LDS and every line that
-// starts inside the tile is encoded from there (only a tile's first line may start before it).
+// this one is worked), carrying both.  Within a tile the line ends are numbered without
+// shuffle chains: a lane's exclusive count from ballots of its count's bits (mbcnt), the last
+// end before its piece from the nearest lower lane with one (one bpermute), the wave's totals
+// by readlane; the 4 sub-tiles x 4 waves then combine through LDS.  The tile's bytes are staged
+// in LDS and every line that starts inside the tile is encoded from there (ds_read; only a
+// tile's first line may start before it).
 template <int KIND>
 __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
     const uint8_t* __restrict__ buf, int64_t n, int64_t ntiles, int64_t per_wg, sct::TileSums ts, int64_t cap,
@@ -218,9 +269,9 @@ __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
     uint8_t* __restrict__ gc, uint8_t* __restrict__ flags, unsigned long long* __restrict__ d_nlines,
     int32_t* __restrict__ d_maxlen) {
   __shared__ uint8_t lut[256];
-  __shared__ uint4 tile_bytes[TILE / 16 + 1];  // (+16: encode_line's dword reads stay inside)
-  __shared__ uint32_t w_cnt[WG / 64];
-  __shared__ long long w_last[WG / 64];
+  __shared__ uint4 tile_bytes[WTILE / 16 + 1];  // (+16: encode_line1's dword reads stay inside)
+  __shared__ uint32_t w_cnt[NSUB][WG / 64];
+  __shared__ int32_t w_last[NSUB][WG / 64];  // in-tile offset of the wave's last line end, -1: none
   __shared__ unsigned long long s_excl;
   __shared__ long long s_excl_last;
   __shared__ unsigned long long red[3][WG / 64];
@@ -230,71 +281,110 @@ __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
   if (tile >= ntiles) return;  // (the whole workgroup)
   const int64_t tend = tile + per_wg < ntiles ? tile + per_wg : ntiles;
   for (int c = t; c < 256; c += WG) lut[c] = lut_entry(KIND, c);
-  if (t == 0) tile_bytes[TILE / 16] = make_uint4(0, 0, 0, 0);
-  uint4 cur = load16(buf, n, tile * TILE + t * 16);
+  if (t == 0) tile_bytes[WTILE / 16] = make_uint4(0, 0, 0, 0);
+  uint4 cur[NSUB];
+#pragma unroll
+  for (int j = 0; j < NSUB; ++j) cur[j] = load16(buf, n, tile * WTILE + j * TILE + t * 16);
   sct::tile_prefix<WG>(ts, tile, &s_excl, &s_excl_last, red);  // (its barriers also cover the LUT)
   uint64_t g_base = s_excl;
   long long last_base = s_excl_last;
-  const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(tile_bytes);
+  lds_u32* lds32 = as_lds32(tile_bytes);
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
   int32_t mx = 0;
   for (; tile < tend; ++tile) {
-    const int64_t t0 = tile * TILE, p0 = t0 + t * 16;
-    const uint4 nxt = tile + 1 < tend ? load16(buf, n, p0 + TILE) : make_uint4(0, 0, 0, 0);
-    uint32_t m = p0 < n ? lf_mask_v(cur, n, p0) : 0u;
-    __syncthreads();  // the previous tile's readers of tile_bytes / w_cnt / w_last are done
-    tile_bytes[t] = cur;
-    cur = nxt;
-    const uint32_t c = __popc(m);
-    const long long mylast = m ? p0 + 31 - __clz(m) : -1;
-    // wave-inclusive sum of c and max of mylast, then across the 4 waves
-    uint32_t ic = c;
-    long long il = mylast;
+    const int64_t t0 = tile * WTILE;
+    const bool more = tile + 1 < tend;
+    uint4 nxt[NSUB];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t a = __shfl_up(ic, d);
-      const long long b = __shfl_up(il, d);
-      if (lane >= d) {
-        ic += a;
-        il = max(il, b);
+    for (int j = 0; j < NSUB; ++j)
+      nxt[j] = more ? load16(buf, n, t0 + WTILE + j * TILE + t * 16) : make_uint4(0, 0, 0, 0);
+    uint32_t m[NSUB], xc[NSUB];
+    int32_t xl[NSUB];
+    __syncthreads();  // the previous tile's readers of tile_bytes / w_cnt / w_last are done
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) {
+      const int64_t p0 = t0 + j * TILE + t * 16;
+      m[j] = p0 < n ? lf_mask_v(cur[j], n, p0) : 0u;
+      tile_bytes[j * WG + t] = cur[j];
+      cur[j] = nxt[j];
+
+      const uint32_t c = __popc(m[j]);  // <= 16: five bits
+      uint32_t ex = 0, tot = 0;
+#pragma unroll
+      for (int b = 0; b < 5; ++b) {
+        const uint64_t bb = __ballot((c >> b) & 1u);
+        ex += (uint32_t)__popcll(bb & lt_mask) << b;
+        tot += (uint32_t)__popcll(bb) << b;
       }
-    }
-    if (lane == 63) {
-      w_cnt[wave] = ic;
-      w_last[wave] = il;
+      xc[j] = ex;
+      const int32_t mylast = m[j] ? j * TILE + t * 16 + 31 - __clz(m[j]) : -1;
+      const uint64_t has = __ballot(m[j] != 0u), lower = has & lt_mask;
+      const int src = lower ? 63 - __clzll(lower) : lane;
+      const int32_t pl = __shfl(mylast, src);
+      xl[j] = lower ? pl : -1;
+      if (lane == 0) {
+        w_cnt[j][wave] = tot;
+        w_last[j][wave] = has ? __builtin_amdgcn_readlane(mylast, 63 - __clzll(has)) : -1;
+      }
     }
     __syncthreads();
-    uint32_t xc = ic - c, tot = 0;  // exclusive within the tile
-    long long xl = __shfl_up(il, 1), tl = -1;
-    if (lane == 0) xl = -1;
+    // prefix of the (sub-tile, wave) pieces before this one, in byte order; the tile's totals
+    uint32_t pre = 0, tot = 0;
+    int32_t plast = -1, tlast = -1;
 #pragma unroll
-    for (int w = 0; w < WG / 64; ++w) {
-      if (w < wave) {
-        xc += w_cnt[w];
-        xl = max(xl, w_last[w]);
+    for (int j = 0; j < NSUB; ++j)
+#pragma unroll
+      for (int w = 0; w < WG / 64; ++w) {
+        const uint32_t cw = w_cnt[j][w];
+        const int32_t lw = w_last[j][w];
+        tot += cw;
+        tlast = max(tlast, lw);
       }
-      tot += w_cnt[w];
-      tl = max(tl, w_last[w]);
-    }
-    long long prev = max(last_base, xl);
-    for (uint64_t g = g_base + xc; m; ++g) {
-      const int j = __ffs(m) - 1;
-      m &= m - 1;
-      const long long P = p0 + j, start = prev + 1;
-      const int32_t L = (int32_t)(P - start);
-      prev = P;
-      mx = max(mx, L);
-      if ((int64_t)g < cap) {
-        uint32_t gg, fl;
-        const uint8_t* src = start >= t0 ? lds8 + (start - t0) : buf + start;
-        encode_line<KIND>(lut, src, L, words, codes + g * words, gg, fl);
-        starts[g] = start;
-        lens[g] = L;
-        if (gc) gc[g] = (uint8_t)(gg > 255 ? 255 : gg);
-        if (flags) flags[g] = (uint8_t)fl;
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) {
+      uint32_t pj = pre;
+      int32_t lj = plast;
+#pragma unroll
+      for (int w = 0; w < WG / 64; ++w)
+        if (w < wave) {
+          pj += w_cnt[j][w];
+          lj = max(lj, w_last[j][w]);
+        }
+      uint32_t mm = m[j];
+      const int32_t prev_in = max(lj, xl[j]);  // in-tile offset of the last end before the piece, -1: none
+      long long prev = prev_in >= 0 ? t0 + prev_in : last_base;
+      const int64_t p0 = t0 + j * TILE + t * 16;
+      for (uint64_t g = g_base + pj + xc[j]; mm; ++g) {
+        const int b = __ffs(mm) - 1;
+        mm &= mm - 1;
+        const long long P = p0 + b, start = prev + 1;
+        const int32_t L = (int32_t)(P - start);
+        prev = P;
+        mx = max(mx, L);
+        if ((int64_t)g < cap) {
+          uint32_t gg, fl;
+          const int off = (int)(start - t0);
+          if (start >= t0 && words == 1 && KIND * L <= 64) {  // inside the tile: from its LDS copy
+            const int o = off & 3, w0 = off >> 2;
+            encode_line1<KIND>(lut, [&](int k) { return lds32[w0 + k]; }, o, L, codes + g, gg, fl);
+          } else {
+            encode_line<KIND>(lut, buf + start, L, words, codes + g * words, gg, fl);
+          }
+          starts[g] = start;
+          lens[g] = L;
+          if (gc) gc[g] = (uint8_t)(gg > 255 ? 255 : gg);
+          if (flags) flags[g] = (uint8_t)fl;
+        }
+      }
+      // the next sub-tile's pieces follow all of this one's
+#pragma unroll
+      for (int w = 0; w < WG / 64; ++w) {
+        pre += w_cnt[j][w];
+        plast = max(plast, w_last[j][w]);
       }
     }
     g_base += tot;
-    last_base = max(last_base, tl);
+    if (tlast >= 0) last_base = t0 + tlast;
   }
 #pragma unroll
   for (int s = 32; s; s >>= 1) mx = max(mx, __shfl_xor(mx, s));
@@ -404,7 +494,7 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
     SCT_HIP(hipMemsetAsync(d_nlines, 0, 8, s));
     return SCT_OK;
   }
-  const int64_t ntiles = sct::ceil_div(nbytes, TILE);
+  const int64_t ntiles = sct::ceil_div(nbytes, WTILE);
   SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
   StreamBuf scratch;
   SCT_HIP(scratch.alloc(sct::tile_sums_bytes(ntiles), s));
@@ -416,6 +506,8 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   SCT_LAUNCH_CHECK();
   const int64_t cap = max_lines > 0 ? max_lines : 0;
   auto kern = kind == 2 ? whitelist_fused_kernel<2> : whitelist_fused_kernel<3>;
+  // one range per resident slot (0.081 ms for config 5's whitelist; one 16 KiB tile per
+  // workgroup 0.088, tools/ingest_tiles_ab.py); SCT_TUNE_INGEST_TILES > 0 fixes the range
   const int64_t knob = sct::tune(SCT_TUNE_INGEST_TILES, 0);
   const int64_t per_wg = knob > 0 ? knob : sct::ceil_div(ntiles, resident_slots((const void*)kern, ntiles));
   hipLaunchKernelGGL(kern, dim3((unsigned)sct::ceil_div(ntiles, per_wg)), dim3(WG), 0, s, d_buf, nbytes, ntiles,
