@@ -546,8 +546,10 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
   }
   uint32_t nf_cur = tile + 1 < ntiles ? first[tile + 1] : ~0u;
   FileCursor fc;
-  const uint8_t* tile8 = reinterpret_cast<const uint8_t*>(tile_bytes);
-  const uint32_t* tile32 = reinterpret_cast<const uint32_t*>(tile_bytes);
+  // LDS-typed views of the tile (ds_read): a pointer that may be LDS or global compiles to flat
+  // loads, after each of which the compiler waits for every load and store in flight
+  lds_u8* tile8 = as_lds8(tile_bytes);
+  lds_u32* tile32 = as_lds32(tile_bytes);
   for (; tile < tend; ++tile) {
     const int64_t ntl = tile + 1;
     const bool more = ntl < tend;
@@ -660,12 +662,14 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
         const int nd = w / 4;
         if (sb - sa == w && sb <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
             ((uintptr_t)o & 3) == 0) {
-          const uint32_t* d = base + 4 * (nd + 1) <= t0 + TILE ? tile32 + ((base - t0) >> 2)
-                                                               : reinterpret_cast<const uint32_t*>(buf + base);
+          const bool lds = base + 4 * (nd + 1) <= t0 + TILE;
+          const int lb = (int)((base - t0) >> 2);
+          const uint32_t* gd = reinterpret_cast<const uint32_t*>(buf + base);
+          auto d = [&](int k) { return lds ? tile32[lb + k] : gd[k]; };  // two loads, no pointer select
           const uint32_t sh = (uint32_t)(s0 & 3);
           uint32_t* od = reinterpret_cast<uint32_t*>(o);
           if (nd == 4 && ((uintptr_t)o & 15) == 0) {
-            const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3], x4 = d[4];
+            const uint32_t x0 = d(0), x1 = d(1), x2 = d(2), x3 = d(3), x4 = d(4);
             const uint4 y = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
                                        __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
             *reinterpret_cast<uint4*>(o) = y;
@@ -676,7 +680,7 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
               enc_dword(lut, code_kind, y.w, code, fl);
             }
           } else if (nd == 2 && ((uintptr_t)o & 7) == 0) {
-            const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
+            const uint32_t x0 = d(0), x1 = d(1), x2 = d(2);
             const uint2 y = make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
             *reinterpret_cast<uint2*>(o) = y;
             if (enc) {
@@ -684,9 +688,9 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
               enc_dword(lut, code_kind, y.y, code, fl);
             }
           } else {
-            uint32_t lo = d[0];
+            uint32_t lo = d(0);
             for (int q2 = 0; q2 < nd; ++q2) {
-              const uint32_t hi = d[q2 + 1], y = __builtin_amdgcn_alignbyte(hi, lo, sh);
+              const uint32_t hi = d(q2 + 1), y = __builtin_amdgcn_alignbyte(hi, lo, sh);
               od[q2] = y;
               if (enc) enc_dword(lut, code_kind, y, code, fl);
               lo = hi;

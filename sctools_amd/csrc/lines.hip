@@ -143,8 +143,10 @@ __global__ __launch_bounds__(WG) void line_lens_kernel(const int64_t* __restrict
 // and stores, which drain at every wait (vmcnt(0): the stores' count varies by line).
 constexpr int NSUB = 4, WTILE = NSUB * TILE;
 
-__global__ __launch_bounds__(WG) void wl_count_kernel(const uint8_t* __restrict__ buf, int64_t n, sct::TileSums ts) {
+__global__ __launch_bounds__(WG) void wl_count_kernel(const uint8_t* __restrict__ buf, int64_t n, sct::TileSums ts,
+                                                      int32_t* __restrict__ d_maxlen) {
   const int64_t t0 = (int64_t)blockIdx.x * WTILE;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *d_maxlen = 0;  // (the encode pass raises it; no memset launch)
   uint4 v[NSUB];
 #pragma unroll
   for (int j = 0; j < NSUB; ++j) v[j] = load16(buf, n, t0 + j * TILE + threadIdx.x * 16);
@@ -489,8 +491,8 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   SCT_CHECK(nbytes >= 0 && (nbytes == 0 || d_buf != nullptr), "bad buffer");
   SCT_CHECK(max_lines <= 0 || (d_codes && d_starts && d_lens), "NULL output");
   hipStream_t s = sct::as_stream(stream);
-  SCT_HIP(hipMemsetAsync(d_maxlen, 0, 4, s));
   if (nbytes == 0) {
+    SCT_HIP(hipMemsetAsync(d_maxlen, 0, 4, s));
     SCT_HIP(hipMemsetAsync(d_nlines, 0, 8, s));
     return SCT_OK;
   }
@@ -499,7 +501,7 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   StreamBuf scratch;
   SCT_HIP(scratch.alloc(sct::tile_sums_bytes(ntiles), s));
   const sct::TileSums ts = sct::tile_sums_at(scratch.p, ntiles, true);
-  hipLaunchKernelGGL(wl_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, ts);
+  hipLaunchKernelGGL(wl_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, ts, d_maxlen);
   SCT_LAUNCH_CHECK();
   hipLaunchKernelGGL(sct::tile_sums_reduce_kernel, dim3((unsigned)sct::ceil_div(ntiles, 1024)), dim3(64), 0, s, ts,
                      ntiles);
