@@ -35,6 +35,8 @@ KERNELS = (
     ("nearest_index", "halves_index_kernel", "npmc", "ntrace", 100_000_000, "queries"),
     ("whitelist_fused", "whitelist_fused_kernel", "ipmc", "itrace", 3_686_400, "lines"),
     ("fastq_range", "fastq_range_kernel", "ipmc", "itrace", 20_000_000, "records"),
+    ("whitelist_count", "wl_count_kernel", "ipmc", "itrace", 3_686_400, "lines"),
+    ("fastq_count", "fq_count_kernel", "ipmc", "itrace", 20_000_000, "records"),
 )
 
 
