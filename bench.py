@@ -55,7 +55,7 @@ HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E (MI355X_MICROARCH.md)
 SIMDS = 256 * 4
 ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-bit code word
 METRIC = "Hamming pair-comparisons/sec, 737K 10x whitelist all-pairs, 1-8 GPUs"
-PROFILE_ROUND = "r03"  # the committed rocprof / PMC summaries the line cites (profiles/)
+PROFILE_ROUND = "r04"  # the committed rocprof / PMC summaries the line cites (profiles/)
 
 
 def parse(argv=None):

@@ -463,7 +463,22 @@ __global__ __launch_bounds__(WG) void fq_count_kernel(const uint8_t* __restrict_
   }
   unsigned long long c = 0;
   uint32_t na = 0, f = ~0u;
-  if (p0 < n) {
+  if (!text && !ends_here && p0 + TB <= n) {
+    // binary mode, no file end near the tile, a whole span: count the '\n' bytes straight from
+    // the SWAR zero-byte bits (no per-byte mask: the count pass was VALU-bound, PMC 0.97 busy)
+#pragma unroll
+    for (int k = 0; k < SEG; ++k) {
+      const uint32_t w[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t hi = eq_bytes(w[q], 0x0A0A0A0Au) & 0x80808080u;
+        c += __popc(hi);
+        na |= w[q];
+        if (hi && f == ~0u) f = (uint32_t)(threadIdx.x * TB + 16 * k + 4 * q + (__builtin_ctz(hi) >> 3)) << 2;
+      }
+    }
+    na &= 0x80808080u;
+  } else if (p0 < n) {
     const Span sp = thread_span(buf, n, fs, text, p0, cur, ends_here);
     const uint32_t bits = sp.m | sp.vbits;
     c = __popc(bits);

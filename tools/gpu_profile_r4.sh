@@ -18,7 +18,7 @@ for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES 
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $pmc -d $P/pmc$i -o run --output-format csv -- $B > $P/pmc$i.log 2>&1 || echo "pmc pass $i failed"
 done
-I="python3 tools/run_paths.py whitelist fastq"
+I="python3 tools/run_paths.py whitelist fastq pipeline"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $P/itrace -o run --output-format csv -- $I > $P/itrace.log 2>&1 || exit 3
 i=0
 for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \

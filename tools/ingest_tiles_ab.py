@@ -15,7 +15,7 @@ torch.cuda.set_device(0)
 copy = 6300.0
 settings = [int(x) for x in (sys.argv[1:] or ["0", "1", "2", "4", "16", "64"])]
 res = {k: {"wl_ms": [], "fq_ms": [], "ok": True} for k in settings}
-for rnd in range(2):
+for rnd in range(int(__import__("os").environ.get("ROUNDS", "2"))):
     for k in settings:
         with _lib.tuning(ingest_tiles=k):
             w = bench.path_whitelist(dev, 5, copy)["whitelist_ingest"]
