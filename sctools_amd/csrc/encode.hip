@@ -179,16 +179,32 @@ __global__ __launch_bounds__(WG) void encode_tiled_kernel(const uint8_t* __restr
           // (u >> 1) & 3 per byte (A 0, C 1, T 2, G 3), gathered MSB-first into one byte by
           // one multiply: v * (1 + 2^10 + 2^20 + 2^30) puts byte j's value at bits 30 - 2j,
           // every other partial product in a disjoint 2-bit slot below 24 (no carries).
-          // A record with any other byte takes the LUT loop below (flags, N draws).
+          // A byte that is not a base (N, IUPAC, invalid: 1 % of config 5's reads) has code bits
+          // 0 (lut & 7 for every such byte), so it is cleared through the byte mask of the
+          // mismatch and only its flag is read from the LUT -- every lane runs the same steps
+          // (the divergent 28-step LUT loop this replaces cost 1.2 ms of 7.8 on config 5's 1e9
+          // reads: half the waves carried a read with an N).  One limb: L <= 32, <= 8 dwords.
           const uint32_t* rw = reinterpret_cast<const uint32_t*>(rec);
-          uint32_t bad = 0;
-          for (int k = 0; k < (L >> 2); ++k) {
-            const uint32_t u = rw[k] & 0xDFDFDFDFu;
-            bad |= u ^ __builtin_amdgcn_perm(0x47010154u, 0x43014101u, u & 0x07070707u);
-            code = (code << 8) | (((u >> 1) & 0x03030303u) * 0x40100401u >> 24);
+          uint32_t nzs[8], anyb = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            nzs[k] = 0;
+            if (k < (L >> 2)) {
+              const uint32_t u = rw[k] & 0xDFDFDFDFu;
+              const uint32_t d = u ^ __builtin_amdgcn_perm(0x47010154u, 0x43014101u, u & 0x07070707u);
+              const uint32_t nz = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;  // bit 7: differs
+              const uint32_t v = ((u >> 1) & 0x03030303u) & ~((nz - (nz >> 7)) | nz);
+              code = (code << 8) | ((v * 0x40100401u) >> 24);
+              nzs[k] = nz;
+              anyb |= nz;
+            }
           }
-          done = bad == 0;
-          if (!done) code = 0;
+          if (anyb) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              for (uint32_t b = nzs[k]; b; b &= b - 1) fl |= lut[(rw[k] >> (__builtin_ctz(b) - 7)) & 0xFFu];
+          }
+          done = true;
         }
         if (done) {
         } else if ((L & 3) == 0) {

@@ -16,6 +16,9 @@ seqs = torch.randint(0, 4, (n, L), dtype=torch.uint8, device=dev, generator=g)
 for r0 in range(0, n, 50_000_000):
     x = seqs[r0:r0 + 50_000_000]
     x.copy_(65 + 2 * x + 15 * (x == 2).to(torch.uint8))
+if __import__("os").environ.get("WITH_N"):  # 1 % of the reads with one N, as bench.path_config5_encode
+    nrows = torch.arange(0, n, 100, device=dev)
+    seqs[nrows, torch.randint(0, L, (nrows.numel(),), device=dev, generator=g)] = ord("N")
 out = {k: torch.empty(n, dtype=t, device=dev) for k, t in (("c0", torch.int64), ("c1", torch.int64),
                                                             ("g", torch.uint8), ("f", torch.uint8))}
 lib = _lib.lib()
