@@ -1267,13 +1267,24 @@ def _ingest_cases():
         parts.append(alpha[rng.integers(0, alpha.size, L)].tobytes() + b"\n")
     parts.append(b"X" * 20_000)  # a final line of 20 KB without '\n': tiles with no line end at all
     cases["ragged"] = b"".join(parts)
+    # upper-case A/C/G/T only (the SWAR path, no LUT fallback): every length 0-40 at every
+    # alignment, lines crossing the 4 KiB sub-tiles and 16 KiB tiles, a few N lines among them
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    parts = []
+    for k in range(60_000):
+        L = k % 41 if k % 211 else int(rng.integers(100, 3000))
+        rec = acgt[rng.integers(0, 4, L)].tobytes()
+        if k % 1009 == 5 and L:
+            rec = rec[:L // 2] + b"N" + rec[L // 2 + 1:]
+        parts.append(rec + b"\n")
+    cases["acgt"] = b"".join(parts)
     return cases
 
 
 @pytest.mark.parametrize("name", list(_ingest_cases()))
 @pytest.mark.parametrize("kind,words", [(2, 1), (2, 2), (3, 1), (3, 2)])
 def test_whitelist_encode_one_pass(name, kind, words):
-    """sct_whitelist_encode (one pass, decoupled look-back, asynchronous) against
+    """sct_whitelist_encode (count pass, tile-sum reduction, encode pass; asynchronous) against
     the reference's binary line loop with `line[:-1]` (barcode.py:95-97) and the oracle's
     encoders (encodings.py:75-88 / 155-167): line count, longest line, every start, length,
     code limb, GC count and flag; lines too long for `words` limbs carry flag 4; a capacity
