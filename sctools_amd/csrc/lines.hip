@@ -61,7 +61,10 @@ __device__ __forceinline__ uint32_t lf_mask_v(uint4 v, int64_t n, int64_t p0) {
   for (int k = 0; k < 4; ++k) {  // (bytes past n are zero, never '\n')
     const uint32_t x = w[k] ^ 0x0A0A0A0Au;
     const uint32_t hi = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
-    m |= (((hi >> 7) & 1u) | ((hi >> 14) & 2u) | ((hi >> 21) & 4u) | ((hi >> 28) & 8u)) << (4 * k);
+    // bits 7, 15, 23, 31 -> 0..3 by one multiply: (hi >> 7) * (2^28 + 2^21 + 2^14 + 2^7) puts
+    // byte j's bit at 28 + j and every other partial product at a distinct bit below 24 or
+    // past 31 (tests/test_swar_host.py)
+    m |= (((hi >> 7) * 0x10204080u) >> 28) << (4 * k);
   }
   if (n > 0 && p0 <= n - 1 && n - 1 < p0 + 16) m |= 1u << (n - 1 - p0);
   return m;
@@ -196,29 +199,43 @@ __device__ __forceinline__ void encode_line1(const uint8_t* lut, DW dw, int o, i
   uint32_t f = 0;
   if (L > 0) {
     const int last = (o + L - 1) >> 2;  // the window's last dword
-    const int nd = (L + 3) >> 2;
+    const int nfull = L >> 2, r = L & 3;
     uint32_t lo = dw(0), bad = 0;
-    for (int k = 0; k < nd; ++k) {
+    // whole dwords (4 bases each), then the last r bases
+    for (int k = 0; k < nfull; ++k) {
       const uint32_t hi = dw(k + 1 <= last ? k + 1 : last);
       const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)o);  // bytes 4k .. 4k + 3
       lo = hi;
-      const int r = L - 4 * k < 4 ? L - 4 * k : 4;
       const uint32_t x = ((w >> 1) ^ (w >> 2)) & 0x03030303u;
       const uint32_t v = x ^ ((x >> 1) & 0x01010101u);
-      const uint32_t keep = r == 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1u;
-      bad |= (__builtin_amdgcn_perm(0u, 0x47544341u, v) ^ w) & keep;  // "ACTG"[v] == the byte?
+      bad |= __builtin_amdgcn_perm(0u, 0x47544341u, v) ^ w;  // "ACTG"[v] == the byte?
       const uint32_t y = __builtin_amdgcn_perm(0u, KIND == 2 ? v : __builtin_amdgcn_perm(0u, 0x03040102u, v),
                                                0x00010203u);  // byte-reversed values
-      uint32_t pk;
       if (KIND == 2) {  // v3 v2 at bits 0, 2 and v1 v0 at 16, 18; then v1 v0 down to 4, 6
         const uint32_t a = (y | (y >> 6)) & 0x000F000Fu;
-        pk = (a | (a >> 12)) & 0xFFu;
+        code = (code << 8) | ((a | (a >> 12)) & 0xFFu);
       } else {  // v3 v2 at bits 0, 3 and v1 v0 at 16, 19; then v1 v0 down to 6, 9
+        const uint32_t a = (y | (y >> 5)) & 0x003F003Fu;
+        code = (code << 12) | ((a | (a >> 10)) & 0xFFFu);
+      }
+    }
+    if (r) {
+      const uint32_t hi = dw(nfull + 1 <= last ? nfull + 1 : last);
+      const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)o);
+      const uint32_t x = ((w >> 1) ^ (w >> 2)) & 0x03030303u;
+      const uint32_t v = x ^ ((x >> 1) & 0x01010101u);
+      bad |= (__builtin_amdgcn_perm(0u, 0x47544341u, v) ^ w) & ((1u << (8 * r)) - 1u);
+      const uint32_t y = __builtin_amdgcn_perm(0u, KIND == 2 ? v : __builtin_amdgcn_perm(0u, 0x03040102u, v),
+                                               0x00010203u);
+      uint32_t pk;
+      if (KIND == 2) {
+        const uint32_t a = (y | (y >> 6)) & 0x000F000Fu;
+        pk = (a | (a >> 12)) & 0xFFu;
+      } else {
         const uint32_t a = (y | (y >> 5)) & 0x003F003Fu;
         pk = (a | (a >> 10)) & 0xFFFu;
       }
-      pk >>= KIND * (4 - r);
-      code = (code << (KIND * r)) | pk;
+      code = (code << (KIND * r)) | (pk >> (KIND * (4 - r)));
     }
     if (bad) {  // the LUT loop (ambiguous / invalid / lower-case bytes; rare: one read per byte)
       code = 0;

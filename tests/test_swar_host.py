@@ -93,3 +93,5 @@ def test_newline_count_bits():
         hi = ~((((x & 0x7F7F7F7F) + 0x7F7F7F7F) & 0xFFFFFFFF) | x | 0x7F7F7F7F) & 0xFFFFFFFF
         assert bin(hi).count("1") == int((b == 10).sum())
         assert [i for i in range(4) if (hi >> (8 * i + 7)) & 1] == [i for i in range(4) if b[i] == 10]
+        m4 = (((hi >> 7) * 0x10204080) & 0xFFFFFFFF) >> 28  # lines.hip lf_mask_v's gather
+        assert m4 == sum(1 << i for i in range(4) if b[i] == 10)
