@@ -347,6 +347,14 @@ __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
       }
     }
     __syncthreads();
+    // the tile's outputs from its first line on (uniform bases), and how many of them fit
+    const uint32_t cap_rel = (int64_t)g_base >= cap ? 0u
+                             : (uint32_t)(cap - (int64_t)g_base < (int64_t)0xFFFFFFFF ? cap - (int64_t)g_base : 0xFFFFFFFF);
+    uint64_t* codes_t = codes + g_base * (uint64_t)words;
+    int64_t* starts_t = starts + g_base;
+    int32_t* lens_t = lens + g_base;
+    uint8_t* gc_t = gc ? gc + g_base : nullptr;
+    uint8_t* flags_t = flags ? flags + g_base : nullptr;
     // prefix of the (sub-tile, wave) pieces before this one, in byte order; the tile's totals
     uint32_t pre = 0, tot = 0;
     int32_t plast = -1, tlast = -1;
@@ -371,28 +379,30 @@ __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
         }
       uint32_t mm = m[j];
       const int32_t prev_in = max(lj, xl[j]);  // in-tile offset of the last end before the piece, -1: none
-      long long prev = prev_in >= 0 ? t0 + prev_in : last_base;
-      const int64_t p0 = t0 + j * TILE + t * 16;
-      for (uint64_t g = g_base + pj + xc[j]; mm; ++g) {
+      // in-tile offsets and line numbers relative to the tile's first line (32-bit: the stores
+      // take a uniform base + a 32-bit offset, no 64-bit address arithmetic per line)
+      const int32_t p0r = j * TILE + t * 16;
+      int64_t prev = prev_in >= 0 ? t0 + prev_in : last_base;  // global position of the previous end
+      for (uint32_t li = pj + xc[j]; mm; ++li) {
         const int b = __ffs(mm) - 1;
         mm &= mm - 1;
-        const long long P = p0 + b, start = prev + 1;
-        const int32_t L = (int32_t)(P - start);
-        prev = P;
+        const int32_t Pr = p0r + b;
+        const int64_t start = prev + 1;
+        const int32_t L = (int32_t)(t0 + Pr - start);
+        prev = t0 + Pr;
         mx = max(mx, L);
-        if ((int64_t)g < cap) {
+        if (li < cap_rel) {
           uint32_t gg, fl;
-          const int off = (int)(start - t0);
           if (start >= t0 && words == 1 && KIND * L <= 64) {  // inside the tile: from its LDS copy
-            const int o = off & 3, w0 = off >> 2;
-            encode_line1<KIND>(lut, [&](int k) { return lds32[w0 + k]; }, o, L, codes + g, gg, fl);
+            const int off = (int)(start - t0), o = off & 3, w0 = off >> 2;
+            encode_line1<KIND>(lut, [&](int k) { return lds32[w0 + k]; }, o, L, codes_t + li, gg, fl);
           } else {
-            encode_line<KIND>(lut, buf + start, L, words, codes + g * words, gg, fl);
+            encode_line<KIND>(lut, buf + start, L, words, codes_t + (size_t)li * words, gg, fl);
           }
-          starts[g] = start;
-          lens[g] = L;
-          if (gc) gc[g] = (uint8_t)(gg > 255 ? 255 : gg);
-          if (flags) flags[g] = (uint8_t)fl;
+          starts_t[li] = start;
+          lens_t[li] = L;
+          if (gc) gc_t[li] = (uint8_t)(gg > 255 ? 255 : gg);
+          if (flags) flags_t[li] = (uint8_t)fl;
         }
       }
       // the next sub-tile's pieces follow all of this one's
