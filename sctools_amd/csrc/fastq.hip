@@ -67,7 +67,9 @@ __device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t pat) {
   return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
 }
 __device__ __forceinline__ uint32_t byte_mask4(uint32_t hi_bits) {  // bit 7 of byte k -> bit k
-  return ((hi_bits >> 7) & 1u) | ((hi_bits >> 14) & 2u) | ((hi_bits >> 21) & 4u) | ((hi_bits >> 28) & 8u);
+  // one multiply: (hi >> 7) * (2^28 + 2^21 + 2^14 + 2^7) puts byte k's bit at 28 + k and every
+  // other partial product at a distinct bit below 24 or past 31 (tests/test_swar_host.py)
+  return ((hi_bits >> 7) * 0x10204080u) >> 28;
 }
 
 // the 16 bytes at p0 (zero past n)
@@ -461,8 +463,7 @@ __global__ __launch_bounds__(WG) void fq_count_kernel(const uint8_t* __restrict_
     }
     ends_here = lo < fs.nfiles && fs.ends[lo] <= t0 + TILE + 16;
   }
-  unsigned long long c = 0;
-  uint32_t na = 0, f = ~0u;
+  uint32_t c = 0, na = 0, f = ~0u;  // (a tile holds at most 8,192 terminators)
   if (!text && !ends_here && p0 + TB <= n) {
     // binary mode, no file end near the tile, a whole span: count the '\n' bytes straight from
     // the SWAR zero-byte bits (no per-byte mask: the count pass was VALU-bound, PMC 0.97 busy)
@@ -495,7 +496,7 @@ __global__ __launch_bounds__(WG) void fq_count_kernel(const uint8_t* __restrict_
     c += __shfl_xor(c, o);
     f = min(f, (uint32_t)__shfl_xor(f, o));
   }
-  __shared__ unsigned long long wc[WG / 64];
+  __shared__ uint32_t wc[WG / 64];
   __shared__ uint32_t wf[WG / 64];
   if ((threadIdx.x & 63) == 0) {
     wc[threadIdx.x >> 6] = c;
