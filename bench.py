@@ -221,15 +221,15 @@ def _rocprof_avg_ms(kernel_substr):
         with open(win) as f:
             k = json.load(f)["kernels"].get(kernel_substr)
         if k:
-            return k["avg_ns"] * 1e-6, k["window"]
+            return k["avg_ns"] * 1e-6, k["window"], k.get("live_vs_trace_same_run")
     path = os.path.join(ROOT, "profiles", "%s_kernel_stats.csv" % PROFILE_ROUND)
     if not os.path.exists(path):
-        return None, None
+        return None, None, None
     with open(path) as f:
         for r in csv.DictReader(f):
             if kernel_substr in r["Name"]:
-                return float(r["AverageNs"]) * 1e-6, int(r["Calls"])
-    return None, None
+                return float(r["AverageNs"]) * 1e-6, int(r["Calls"]), None
+    return None, None, None
 
 
 def issue_picture(prof):
@@ -297,7 +297,7 @@ def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, nam
         ms, nl = kt[k]
         avg = ms / nl if nl else float("nan")
         prof = _profile(prof_name) if elem_bytes == 1 and column_bits == 14 else None
-        rms, rcalls = _rocprof_avg_ms(rp) if elem_bytes == 1 and column_bits == 14 else (None, None)
+        rms, rcalls, same_run = _rocprof_avg_ms(rp) if elem_bytes == 1 and column_bits == 14 else (None, None, None)
         gbs = algo / (avg * 1e-3) / 1e9
         kern[k] = {"kernel": label, "ms": avg, "launches": nl, "achieved_gbs": gbs, "frac": gbs * 1e9 / HBM_PEAK_BPS,
                    "frac_of_copy_ceiling": gbs / copy_gbs if copy_gbs else None,
@@ -308,7 +308,11 @@ def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, nam
                        "source": "profiles/%s_timed_dispatches.json (the timed steps' dispatches of the rocprofv3 "
                                  "kernel trace of this command; every dispatch: profiles/%s_kernel_stats.csv)"
                                  % (PROFILE_ROUND, PROFILE_ROUND),
-                       "live_vs_rocprof": avg / rms - 1.0}}
+                       "live_vs_rocprof": avg / rms - 1.0,
+                       "profiled_run_live_vs_rocprof": same_run,
+                       "note": "live_vs_rocprof compares this run with a trace taken on another box (boxes differ "
+                               "by up to ~10 %); profiled_run_live_vs_rocprof compares the profiled command's own "
+                               "HIP-event time with its trace (same box, same run)"}}
     dom, other = ("seed", "tile") if kern["seed"]["ms"] >= kern["tile"]["ms"] else ("tile", "seed")
     d = kern[dom]
     return {"bound": "hbm", "achieved": d["achieved_gbs"], "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",

@@ -127,10 +127,24 @@ def main():
             shutil.copy(src, os.path.join(dst, fn % a.round))
     ap_steps = int(os.environ.get("BENCH_STEPS", "20"))
     win = {k: timed_window(a.src, "trace", k, ap_steps) for k in ("tile_reg_kernel", "seed_sm_kernel")}
+    # the profiled command's own bench line: its live HIP-event kernel times, same box and run
+    live = {}
+    log = os.path.join(a.src, "trace.log")
+    if os.path.exists(log):
+        for line in open(log):
+            if line.startswith("{") and '"roofline"' in line:
+                r = json.loads(line)["roofline"]
+                live = {"tile_reg_kernel": r.get("kernel_ms"), "seed_sm_kernel": (r.get("other_kernel") or {}).get("ms")}
+    for k, w in win.items():
+        if w and live.get(k):
+            w["live_ms_same_run"] = live[k]
+            w["live_vs_trace_same_run"] = live[k] / (w["avg_ns"] * 1e-6) - 1.0
     with open(os.path.join(dst, "%s_timed_dispatches.json" % a.round), "w") as f:
         json.dump({"command": "python3 bench.py --gpus 1 --steps %d --warmup 5" % ap_steps, "kernels": win,
                    "note": "rocprofv3 kernel trace of the command; avg_ns = the last `window` dispatches of "
-                           "the kernel (the timed steps), all_avg_ns = every dispatch"}, f, indent=1)
+                           "the kernel (the timed steps), all_avg_ns = every dispatch; live_ms_same_run = "
+                           "the HIP-event kernel time the same profiled command printed (same box, same run)"},
+                  f, indent=1)
     print("timed window", json.dumps(win))
     for name, kernel, prefix, trace, units, unit in KERNELS:
         r = summarize(a.src, dst, a.round, name, kernel, prefix, trace, units, unit)
