@@ -15,6 +15,7 @@ constexpr uint8_t F_AMBIG = 0x40, F_INVALID = 0x80;
 // outstanding store of the workgroup's loop each time (the ingest kernels' tile loops).
 typedef __attribute__((address_space(3))) const uint32_t lds_u32;
 typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+typedef __attribute__((address_space(3))) const uint16_t lds_u16;
 template <class T>
 __device__ __forceinline__ lds_u32* as_lds32(T* p) {
   return (lds_u32*)(p);
@@ -22,6 +23,10 @@ __device__ __forceinline__ lds_u32* as_lds32(T* p) {
 template <class T>
 __device__ __forceinline__ lds_u8* as_lds8(T* p) {
   return (lds_u8*)(p);
+}
+template <class T>
+__device__ __forceinline__ lds_u16* as_lds16(T* p) {
+  return (lds_u16*)(p);
 }
 
 // LUT entry: low 3 bits = code, 0x40 = IUPAC ambiguous (TwoBit), 0x80 = invalid (TwoBit)

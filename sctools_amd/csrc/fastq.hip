@@ -523,6 +523,169 @@ __device__ __forceinline__ void enc_dword(const uint8_t* lut, int bits, uint32_t
   }
 }
 
+// The per-tile work after the tile's terminators are in LDS (term, in byte order; the tile's
+// bytes in tile8 / tile32, and `head` bytes of the next tile after them): the '@' check of every
+// name line and every sequence / quality line's span slices (one item per line, its spans in
+// turn; rows of records >= cap skipped).  Terminators [0, tmax) end lines of records that count
+// (tmax < ntile drops an incomplete trailing record); g0 = the tile's first terminator's global
+// number; nf = the next tile's first terminator (count_kernel's encoding), or ~0u: the tile's last
+// line is then scanned for, in LDS when it ends within the staged head.
+struct TileOut {
+  uint8_t* seq_out;
+  uint8_t* qual_out;
+  int32_t* seq_len;
+  int32_t* qual_len;
+  uint64_t* codes0;
+  uint8_t* gc0;
+  uint8_t* flags0;
+  int code_kind;
+  uint64_t gc_mask;
+  int64_t cap;
+  unsigned long long* d_status;
+};
+
+__device__ __forceinline__ void tile_items(lds_u16* term, lds_u8* tile8, lds_u32* tile32, const uint8_t* lut,
+                                           int ntile, int tmax, int64_t g0, int64_t t0, uint32_t nf, int head,
+                                           const uint8_t* __restrict__ buf, int64_t n, Files fs, int text,
+                                           const Spans& sp, const TileOut& to) {
+  const int tid = threadIdx.x;
+    // name lines: after terminators g = 3 (mod 4)
+    for (int t = (int)((3 - (g0 & 3)) & 3) + 4 * tid; t < tmax; t += 4 * WG) {
+      const uint32_t e = term[t];
+      const int64_t o = (int64_t)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // the line's start in the tile
+      const uint8_t ch = o < TILE + head ? tile8[o] : buf[t0 + o];
+      if (ch != '@') atomicMax(to.d_status + 1, ~(unsigned long long)((g0 + t + 1) >> 2));
+    }
+    // sequence / quality lines: after even terminators; one item per line, its spans in turn
+    const int te0 = (int)(g0 & 1);
+    const int nact = tmax > te0 ? (tmax - te0 + 1) / 2 : 0;
+    for (int a = tid; a < nact; a += WG) {
+      const int t = te0 + 2 * a;
+      const int64_t line = g0 + t + 1, rec = line >> 2;
+      if (rec >= to.cap) continue;
+      const bool is_seq = (line & 3) == 1;
+      const uint32_t e = term[t];
+      const int start = (int)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // <= TILE
+      int64_t cend;  // content end relative to the tile start
+      int nl;
+      if (t + 1 < (int)ntile) {  // the line ends at the tile's next terminator
+        const uint32_t f = term[t + 1];
+        cend = (int64_t)(f & T16_OFF) - ((f & T16_CRLF) ? 1 : 0);
+        nl = (f & T16_VIRT) ? 0 : 1;
+      } else if (nf != ~0u) {  // the tile's last line ends at the next tile's first terminator
+        cend = TILE + (int64_t)(nf >> 2) - ((nf & 2u) ? 1 : 0);
+        nl = (nf & 1u) ? 0 : 1;
+      } else {  // the next tile's first terminator unknown: scan (max_end bytes, within its file)
+        const int64_t next = t0 + start;
+        int lo = 0, hi = fs.nfiles;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (fs.ends[mid] <= next) lo = mid + 1; else hi = mid;
+        }
+        const int64_t fe = lo < fs.nfiles ? fs.ends[lo] : n;
+        const int64_t lim = next + sp.max_end < fe ? next + sp.max_end : fe;
+        cend = lim - t0;
+        nl = lim == fe ? 0 : 1;  // longer than the window: its end is irrelevant
+        if (lim - t0 <= TILE + head) {  // inside the tile and the next tile's head staged after it
+          for (int i = start; i < (int)(lim - t0); ++i) {
+            const uint8_t ch = tile8[i];
+            if (ch == '\n' || (text && ch == '\r')) {
+              cend = i;
+              nl = 1;
+              break;
+            }
+          }
+        } else {
+          for (int64_t i = next; i < lim; ++i) {
+            const uint8_t ch = buf[i];
+            if (ch == '\n' || (text && ch == '\r')) {
+              cend = i - t0;
+              nl = 1;
+              break;
+            }
+          }
+        }
+      }
+      int32_t* len = is_seq ? to.seq_len : to.qual_len;
+      uint8_t* out = is_seq ? to.seq_out : to.qual_out;
+      const int64_t clen = cend - start, llen = clen + nl;
+      for (int k = 0; k < sp.n; ++k) {
+        const int64_t sa = sp.start[k] < llen ? sp.start[k] : llen, sb = sp.end[k] < llen ? sp.end[k] : llen;
+        if (len) len[k * to.cap + rec] = (int32_t)(sb - sa);
+        if (!out) continue;
+        const bool enc = k == 0 && is_seq && to.codes0 != nullptr;
+        uint64_t code = 0;
+        uint32_t fl = 0;
+        const int w = sp.end[k] - sp.start[k];
+        uint8_t* o = out + sp.prefix[k] * to.cap + rec * w;
+        const uint8_t* src = buf + t0 + start;
+        // fast path: a whole-width slice inside the line's content, a row of whole dwords:
+        // aligned dword loads + byte-align funnel shifts, dword stores (the code from the same
+        // registers)
+        const int64_t s0 = t0 + start + sa;
+        const int64_t base = s0 & ~3LL;
+        const int nd = w / 4;
+        if (sb - sa == w && sb <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
+            ((uintptr_t)o & 3) == 0) {
+          const bool lds = base + 4 * (nd + 1) <= t0 + TILE;
+          const int lb = (int)((base - t0) >> 2);
+          const uint32_t* gd = reinterpret_cast<const uint32_t*>(buf + base);
+          auto d = [&](int k) { return lds ? tile32[lb + k] : gd[k]; };  // two loads, no pointer select
+          const uint32_t sh = (uint32_t)(s0 & 3);
+          uint32_t* od = reinterpret_cast<uint32_t*>(o);
+          if (nd == 4 && ((uintptr_t)o & 15) == 0) {
+            const uint32_t x0 = d(0), x1 = d(1), x2 = d(2), x3 = d(3), x4 = d(4);
+            const uint4 y = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                                       __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+            *reinterpret_cast<uint4*>(o) = y;
+            if (enc) {
+              enc_dword(lut, to.code_kind, y.x, code, fl);
+              enc_dword(lut, to.code_kind, y.y, code, fl);
+              enc_dword(lut, to.code_kind, y.z, code, fl);
+              enc_dword(lut, to.code_kind, y.w, code, fl);
+            }
+          } else if (nd == 2 && ((uintptr_t)o & 7) == 0) {
+            const uint32_t x0 = d(0), x1 = d(1), x2 = d(2);
+            const uint2 y = make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
+            *reinterpret_cast<uint2*>(o) = y;
+            if (enc) {
+              enc_dword(lut, to.code_kind, y.x, code, fl);
+              enc_dword(lut, to.code_kind, y.y, code, fl);
+            }
+          } else {
+            uint32_t lo = d(0);
+            for (int q2 = 0; q2 < nd; ++q2) {
+              const uint32_t hi = d(q2 + 1), y = __builtin_amdgcn_alignbyte(hi, lo, sh);
+              od[q2] = y;
+              if (enc) enc_dword(lut, to.code_kind, y, code, fl);
+              lo = hi;
+            }
+          }
+        } else {
+#pragma unroll 8
+          for (int j = 0; j < w; ++j) {
+            const int64_t i = sa + j;
+            const uint8_t v = i < sb ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
+            o[j] = v;
+            if (enc) {
+              const uint32_t en = lut[v];
+              code = (code << to.code_kind) | (en & 7u);
+              fl |= en;
+            }
+          }
+        }
+        if (enc) {  // span 0's row (as written, zero-padded) -> its code
+          to.codes0[rec] = code;
+          if (to.gc0) {
+            const uint32_t g = (uint32_t)__popcll(code & to.gc_mask);
+            to.gc0[rec] = (uint8_t)(g > 255 ? 255 : g);
+          }
+          if (to.flags0) to.flags0[rec] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
+        }
+      }
+    }
+}
+
 // Rows of records >= cap are skipped; span k's row r at out + cap * prefix_k + r * width_k, its
 // length at len + k * cap + r; d_status[0] = the line count, d_status[1] = ~(first bad-name
 // record) or 0 (records < lines / 4 only, as extract2_kernel); optionally span 0's sequence rows
@@ -547,7 +710,8 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
   const int64_t tend = tile + per_wg < ntiles ? tile + per_wg : ntiles;
   if (codes0)
     for (int c = tid; c < 256; c += WG) lut[c] = lut_entry(code_kind, c);
-  const uint64_t gc_mask = code_kind == 2 ? 0x5555555555555555ull : 0x9249249249249249ull;
+  const TileOut to{seq_out, qual_out, seq_len, qual_len, codes0, gc0, flags0, code_kind,
+                   code_kind == 2 ? 0x5555555555555555ull : 0x9249249249249249ull, cap, d_status};
   uint4 cur[SEG], nxt[SEG];
 #pragma unroll
   for (int k = 0; k < SEG; ++k) cur[k] = load16(buf, n, tile * TILE + (int64_t)tid * TB + 16 * k);
@@ -609,135 +773,191 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
       }
     }
     __syncthreads();
-    const uint32_t nf = nf_cur;
     const int tmax = (int)(g0 + ntile <= lim_g ? ntile : (lim_g > g0 ? lim_g - g0 : 0));
-    // name lines: after terminators g = 3 (mod 4)
-    for (int t = (int)((3 - (g0 & 3)) & 3) + 4 * tid; t < tmax; t += 4 * WG) {
-      const uint32_t e = term[t];
-      const int64_t o = (int64_t)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // the line's start in the tile
-      const uint8_t ch = o < TILE ? tile8[o] : buf[t0 + o];
-      if (ch != '@') atomicMax(d_status + 1, ~(unsigned long long)((g0 + t + 1) >> 2));
-    }
-    // sequence / quality lines: after even terminators; one item per line, its spans in turn
-    const int te0 = (int)(g0 & 1);
-    const int nact = tmax > te0 ? (tmax - te0 + 1) / 2 : 0;
-    for (int a = tid; a < nact; a += WG) {
-      const int t = te0 + 2 * a;
-      const int64_t line = g0 + t + 1, rec = line >> 2;
-      if (rec >= cap) continue;
-      const bool is_seq = (line & 3) == 1;
-      const uint32_t e = term[t];
-      const int start = (int)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // <= TILE
-      int64_t cend;  // content end relative to the tile start
-      int nl;
-      if (t + 1 < (int)ntile) {  // the line ends at the tile's next terminator
-        const uint32_t f = term[t + 1];
-        cend = (int64_t)(f & T16_OFF) - ((f & T16_CRLF) ? 1 : 0);
-        nl = (f & T16_VIRT) ? 0 : 1;
-      } else if (nf != ~0u) {  // the tile's last line ends at the next tile's first terminator
-        cend = TILE + (int64_t)(nf >> 2) - ((nf & 2u) ? 1 : 0);
-        nl = (nf & 1u) ? 0 : 1;
-      } else {  // no terminator in the next tile either: scan (max_end bytes, within its file)
-        const int64_t next = t0 + start;
-        int lo = 0, hi = fs.nfiles;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (fs.ends[mid] <= next) lo = mid + 1; else hi = mid;
-        }
-        const int64_t fe = lo < fs.nfiles ? fs.ends[lo] : n;
-        const int64_t lim = next + sp.max_end < fe ? next + sp.max_end : fe;
-        cend = lim - t0;
-        nl = lim == fe ? 0 : 1;  // longer than the window: its end is irrelevant
-        for (int64_t i = next; i < lim; ++i) {
-          const uint8_t ch = buf[i];
-          if (ch == '\n' || (text && ch == '\r')) {
-            cend = i - t0;
-            nl = 1;
-            break;
-          }
-        }
-      }
-      int32_t* len = is_seq ? seq_len : qual_len;
-      uint8_t* out = is_seq ? seq_out : qual_out;
-      const int64_t clen = cend - start, llen = clen + nl;
-      for (int k = 0; k < sp.n; ++k) {
-        const int64_t sa = sp.start[k] < llen ? sp.start[k] : llen, sb = sp.end[k] < llen ? sp.end[k] : llen;
-        if (len) len[k * cap + rec] = (int32_t)(sb - sa);
-        if (!out) continue;
-        const bool enc = k == 0 && is_seq && codes0 != nullptr;
-        uint64_t code = 0;
-        uint32_t fl = 0;
-        const int w = sp.end[k] - sp.start[k];
-        uint8_t* o = out + sp.prefix[k] * cap + rec * w;
-        const uint8_t* src = buf + t0 + start;
-        // fast path: a whole-width slice inside the line's content, a row of whole dwords:
-        // aligned dword loads + byte-align funnel shifts, dword stores (the code from the same
-        // registers)
-        const int64_t s0 = t0 + start + sa;
-        const int64_t base = s0 & ~3LL;
-        const int nd = w / 4;
-        if (sb - sa == w && sb <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
-            ((uintptr_t)o & 3) == 0) {
-          const bool lds = base + 4 * (nd + 1) <= t0 + TILE;
-          const int lb = (int)((base - t0) >> 2);
-          const uint32_t* gd = reinterpret_cast<const uint32_t*>(buf + base);
-          auto d = [&](int k) { return lds ? tile32[lb + k] : gd[k]; };  // two loads, no pointer select
-          const uint32_t sh = (uint32_t)(s0 & 3);
-          uint32_t* od = reinterpret_cast<uint32_t*>(o);
-          if (nd == 4 && ((uintptr_t)o & 15) == 0) {
-            const uint32_t x0 = d(0), x1 = d(1), x2 = d(2), x3 = d(3), x4 = d(4);
-            const uint4 y = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                                       __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
-            *reinterpret_cast<uint4*>(o) = y;
-            if (enc) {
-              enc_dword(lut, code_kind, y.x, code, fl);
-              enc_dword(lut, code_kind, y.y, code, fl);
-              enc_dword(lut, code_kind, y.z, code, fl);
-              enc_dword(lut, code_kind, y.w, code, fl);
-            }
-          } else if (nd == 2 && ((uintptr_t)o & 7) == 0) {
-            const uint32_t x0 = d(0), x1 = d(1), x2 = d(2);
-            const uint2 y = make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
-            *reinterpret_cast<uint2*>(o) = y;
-            if (enc) {
-              enc_dword(lut, code_kind, y.x, code, fl);
-              enc_dword(lut, code_kind, y.y, code, fl);
-            }
-          } else {
-            uint32_t lo = d(0);
-            for (int q2 = 0; q2 < nd; ++q2) {
-              const uint32_t hi = d(q2 + 1), y = __builtin_amdgcn_alignbyte(hi, lo, sh);
-              od[q2] = y;
-              if (enc) enc_dword(lut, code_kind, y, code, fl);
-              lo = hi;
-            }
-          }
-        } else {
-#pragma unroll 8
-          for (int j = 0; j < w; ++j) {
-            const int64_t i = sa + j;
-            const uint8_t v = i < sb ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
-            o[j] = v;
-            if (enc) {
-              const uint32_t en = lut[v];
-              code = (code << code_kind) | (en & 7u);
-              fl |= en;
-            }
-          }
-        }
-        if (enc) {  // span 0's row (as written, zero-padded) -> its code
-          codes0[rec] = code;
-          if (gc0) {
-            const uint32_t g = (uint32_t)__popcll(code & gc_mask);
-            gc0[rec] = (uint8_t)(g > 255 ? 255 : g);
-          }
-          if (flags0) flags0[rec] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
-        }
-      }
-    }
+    tile_items(as_lds16(term), tile8, tile32, lut, (int)ntile, tmax, g0, t0, nf_cur, 0, buf, n, fs, text, sp, to);
     g0 += ntile;
     nf_cur = nf_nxt;
   }
+}
+
+// ---------------------------------------------------------------- one pass (round 4)
+// fastq_onepass_kernel<RT>: every byte read once.  A workgroup takes a ticket (ranges are taken
+// in ticket order, so a range only ever waits on ranges whose workgroups are already running),
+// loads its range of RT tiles into registers (RT x 32 bytes per thread), counts the range's
+// terminators and publishes that count, then looks back over its predecessors' published words
+// -- all 256 threads at once, one predecessor each -- until one holds an inclusive prefix, and
+// publishes its own inclusive prefix (one 64-bit word: flag in bits 62-63, count below).  Then
+// the range's tiles are worked from the registers as fastq_range_kernel works them, the next
+// tile's first 64 bytes staged in LDS after each tile for its last line's end.  The line total
+// is known only at the last range, so rows are written for every record < cap (those of an
+// incomplete trailing record are not meaningful) and fastq_onepass_finish_kernel drops a first
+// bad name that lies beyond the complete records.
+constexpr unsigned long long kAgg = 1ull << 62, kIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
+
+template <int RT>
+__global__ __launch_bounds__(WG) void fastq_onepass_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs,
+                                                           int text, int64_t ntiles, int64_t nranges,
+                                                           unsigned long long* __restrict__ rstat,
+                                                           unsigned* __restrict__ ctr, Spans sp, TileOut to) {
+  __shared__ uint16_t term[MAX_TERM];
+  __shared__ uint4 tile_bytes[TILE / 16 + 4];  // the tile, then the next tile's first 64 bytes
+  __shared__ uint32_t w_cnt[WG / 64];
+  __shared__ unsigned long long w_sum[WG / 64];
+  __shared__ int w_first[WG / 64];
+  __shared__ int64_t s_r;
+  __shared__ uint8_t lut[256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_r = (int64_t)atomicAdd(ctr, 1u);
+  if (to.codes0)
+    for (int c = tid; c < 256; c += WG) lut[c] = lut_entry(to.code_kind, c);
+  __syncthreads();
+  const int64_t r = s_r, tile0 = r * RT;
+  // the range's bytes (thread tid: bytes tid * 32 .. + 31 of each tile) and, for threads 0 and 1,
+  // the next range's first 64 bytes
+  uint4 cur[RT + 1][SEG];
+#pragma unroll
+  for (int i = 0; i < RT; ++i)
+#pragma unroll
+    for (int k = 0; k < SEG; ++k)
+      cur[i][k] = tile0 + i < ntiles ? load16(buf, n, (tile0 + i) * TILE + (int64_t)tid * TB + 16 * k)
+                                     : make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < SEG; ++k)
+    cur[RT][k] = tid < 2 && tile0 + RT < ntiles ? load16(buf, n, (tile0 + RT) * TILE + (int64_t)tid * TB + 16 * k)
+                                                : make_uint4(0, 0, 0, 0);
+  // phase 1: the range's terminator count
+  uint32_t c = 0, na = 0;
+  {
+    FileCursor fc;
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+      if (tile0 + i >= ntiles) break;
+      const int64_t t0 = (tile0 + i) * TILE, p0 = t0 + (int64_t)tid * TB;
+      const bool ends_here = fc.advance(fs, t0);
+      if (!text && !ends_here && p0 + TB <= n) {
+#pragma unroll
+        for (int k = 0; k < SEG; ++k) {
+          const uint32_t w[4] = {cur[i][k].x, cur[i][k].y, cur[i][k].z, cur[i][k].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) c += __popc(eq_bytes(w[q], 0x0A0A0A0Au));
+          na |= (w[0] | w[1] | w[2] | w[3]) & 0x80808080u;
+        }
+      } else if (p0 < n) {
+        const Span spn = thread_span(buf, n, fs, text, p0, cur[i], ends_here);
+        c += __popc(spn.m | spn.vbits);
+        na |= spn.na;
+      }
+    }
+  }
+  if (na) atomicOr(reinterpret_cast<unsigned*>(to.d_status + 2), 1u);
+  unsigned long long agg = c;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) agg += __shfl_xor(agg, o);
+  if (lane == 0) w_sum[wave] = agg;
+  __syncthreads();
+  agg = 0;
+#pragma unroll
+  for (int w = 0; w < WG / 64; ++w) agg += w_sum[w];
+  if (tid == 0) __hip_atomic_store(rstat + r, kAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // look-back: thread t reads predecessor base - t; the nearest inclusive one ends the walk
+  unsigned long long excl = 0;
+  for (int64_t base = r - 1;; base -= WG) {
+    const int64_t idx = base - tid;
+    unsigned long long v = kIncl;  // before range 0: an inclusive prefix of 0
+    if (idx >= 0) {
+      v = __hip_atomic_load(rstat + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // a running predecessor publishes its count without waiting on anything; the bound only
+      // guarantees an exit
+      for (int spin = 0; (v >> 62) == 0 && spin < (1 << 22); ++spin) {
+        __builtin_amdgcn_s_sleep(1);
+        v = __hip_atomic_load(rstat + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    const bool incl = (v >> 62) == 2;
+    const unsigned long long bal = __ballot(incl);
+    const int wfirst = bal ? __builtin_ctzll(bal) : 64;
+    __syncthreads();  // the previous round's readers of w_first / w_sum are done
+    if (lane == 0) w_first[wave] = wfirst;
+    __syncthreads();
+    int first = WG;  // the lowest thread (nearest predecessor) holding an inclusive prefix
+#pragma unroll
+    for (int w = 0; w < WG / 64; ++w)
+      if (first == WG && w_first[w] < 64) first = 64 * w + w_first[w];
+    unsigned long long part = tid <= first ? (v & kValMask) : 0ull;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) part += __shfl_xor(part, o);
+    if (lane == 0) w_sum[wave] = part;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < WG / 64; ++w) excl += w_sum[w];
+    if (first < WG) break;
+  }
+  if (tid == 0) {
+    __hip_atomic_store(rstat + r, kIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (r == nranges - 1) atomicMax(to.d_status, excl + agg);  // the line total
+    if (r == 0 && n > 0 && buf[0] != '@') atomicMax(to.d_status + 1, ~0ull);  // record 0's name line
+  }
+  // phase 2: the tiles from the registers (rotated down one tile per step)
+  lds_u8* tile8 = as_lds8(tile_bytes);
+  lds_u32* tile32 = as_lds32(tile_bytes);
+  int64_t g0 = (int64_t)excl;
+  FileCursor fc;
+#pragma unroll 1
+  for (int i = 0; i < RT; ++i) {
+    const int64_t tile = tile0 + i;
+    if (tile >= ntiles) break;
+    const int64_t t0 = tile * TILE, p0 = t0 + (int64_t)tid * TB;
+    const bool ends_here = fc.advance(fs, t0);
+    Span spn{0, 0, 0, 0};
+    if (p0 < n) spn = thread_span(buf, n, fs, text, p0, cur[0], ends_here);
+    __syncthreads();  // the previous tile's readers of tile_bytes / term are done
+#pragma unroll
+    for (int k = 0; k < SEG; ++k) {
+      tile_bytes[tid * SEG + k] = p0 + 16 * k < n ? cur[0][k] : make_uint4(0, 0, 0, 0);
+      if (tid < 2) tile_bytes[TILE / 16 + tid * SEG + k] = cur[1][k];  // the next tile's head
+    }
+#pragma unroll
+    for (int j = 0; j < RT; ++j)
+#pragma unroll
+      for (int k = 0; k < SEG; ++k) cur[j][k] = cur[j + 1][k];
+    const uint32_t tbits = spn.m | spn.vbits, cc = __popc(tbits);
+    uint32_t ic = cc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t x = __shfl_up(ic, d);
+      if (lane >= d) ic += x;
+    }
+    if (lane == 63) w_cnt[wave] = ic;
+    __syncthreads();
+    uint32_t pre = ic - cc, ntile = 0;
+#pragma unroll
+    for (int w = 0; w < WG / 64; ++w) {
+      if (w < wave) pre += w_cnt[w];
+      ntile += w_cnt[w];
+    }
+    {
+      uint32_t bits = tbits, at = pre;
+      while (bits) {
+        const int j = __ffs(bits) - 1;
+        bits &= bits - 1;
+        const uint32_t off = (uint32_t)(tid * TB + j);
+        term[at++] = (spn.m >> j & 1u) ? (uint16_t)(off | ((spn.crlf >> j & 1u) ? T16_CRLF : 0u))
+                                       : (uint16_t)((off + 1) | T16_VIRT);  // the file ends after byte off
+      }
+    }
+    __syncthreads();
+    // every record < cap is written (the total is not known yet); the caller reads lines / 4
+    tile_items(as_lds16(term), tile8, tile32, lut, (int)ntile, (int)ntile, g0, t0, ~0u, 64, buf, n, fs, text, sp,
+               to);
+    g0 += ntile;
+  }
+}
+
+// after fastq_onepass_kernel: a first bad name beyond the complete records is none (a kernel of
+// one thread: a completion counter in the pass cost one same-address atomic per range)
+__global__ void fastq_onepass_finish_kernel(unsigned long long* __restrict__ d_status) {
+  const unsigned long long total = d_status[0], bad = d_status[1];
+  if (bad && ~bad >= (total >> 2)) d_status[1] = 0ull;
 }
 
 // grid of the persistent tile kernels: every resident workgroup slot once (at most ntiles)
@@ -1003,6 +1223,34 @@ extern "C" int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, con
   if (nbytes == 0) return SCT_OK;
   const int64_t ntiles = sct::ceil_div(nbytes, TILE);
   SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
+  const TileOut to{d_seq, d_qual, d_seq_len, d_qual_len, d_codes0, d_gc0, d_flags0, code_kind,
+                   code_kind == 2 ? 0x5555555555555555ull : 0x9249249249249249ull, cap_records,
+                   reinterpret_cast<unsigned long long*>(d_status)};
+  // SCT_TUNE_FASTQ_ONEPASS: 4 or 8 = one pass over ranges of that many tiles, 0 = count pass first
+  const int64_t onepass = sct::tune(SCT_TUNE_FASTQ_ONEPASS, 0);
+  if (onepass == 2 || onepass == 4 || onepass == 8) {
+    const int RT = (int)onepass;
+    const int64_t nranges = sct::ceil_div(ntiles, RT);
+    SCT_CHECK(nranges < (1LL << 31), "buffer too large");
+    void* scr = nullptr;
+    const size_t rbytes = (size_t)nranges * 8 + 16;
+    SCT_HIP(sct::pool_alloc(&scr, rbytes, s));
+    hipError_t e1 = hipMemsetAsync(scr, 0, rbytes, s);
+    if (e1 == hipSuccess) {
+      auto* rstat = reinterpret_cast<unsigned long long*>(scr);
+      auto* ctr = reinterpret_cast<unsigned*>(rstat + nranges);
+      const Files fs{d_file_ends, nfiles};
+      auto kern = RT == 2 ? fastq_onepass_kernel<2> : RT == 4 ? fastq_onepass_kernel<4> : fastq_onepass_kernel<8>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)nranges), dim3(WG), 0, s, d_buf, nbytes, fs, text_mode ? 1 : 0, ntiles,
+                         nranges, rstat, ctr, sp, to);
+      hipLaunchKernelGGL(fastq_onepass_finish_kernel, dim3(1), dim3(1), 0, s,
+                         reinterpret_cast<unsigned long long*>(d_status));
+      e1 = hipGetLastError();
+    }
+    sct::pool_free(scr, s);
+    if (e1 != hipSuccess) return sct::fail(SCT_E_HIP, "fastq one pass: %s", hipGetErrorString(e1));
+    return SCT_OK;
+  }
   void* scratch = nullptr;
   const size_t sbytes = sct::tile_sums_bytes(ntiles), fbytes = (size_t)ntiles * 4;
   SCT_HIP(sct::pool_alloc(&scratch, sbytes + fbytes, s));

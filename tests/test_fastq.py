@@ -284,12 +284,19 @@ def _fused_cases(fq_golden, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("onepass", [0, 4, 8])
 @pytest.mark.parametrize("text_mode", [0, 1])
-def test_fastq_fused_one_pass_vs_indexed(fq_golden, tmp_path, text_mode):
+def test_fastq_fused_one_pass_vs_indexed(fq_golden, tmp_path, text_mode, onepass):
     """sct_fastq_extract_fused (no index, no scan launch, no host synchronisation; VERDICT r3
-    #6) against the indexed two-pass path (itself pinned to the reference's golden outputs
+    #6; onepass 4 / 8: every byte read once, a look-back over ranges of that many tiles) against the indexed two-pass path (itself pinned to the reference's golden outputs
     above): record count, first bad name, every span's sequence / quality rows and lengths, and
     the in-kernel TwoBit and ThreeBit encodes of span 0's rows against sct_encode of the same rows."""
+    from sctools_amd import _lib
+    with _lib.tuning(fastq_onepass=onepass):
+        _fused_check(fq_golden, tmp_path, text_mode)
+
+
+def _fused_check(fq_golden, tmp_path, text_mode):
     from sctools_amd import _lib
     spans = [(0, 16), (16, 26), (3, 9)]
     for name, data, ends in _fused_cases(fq_golden, tmp_path):
