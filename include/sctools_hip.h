@@ -55,8 +55,10 @@ int sct_set_device(int device);        /* select the device for later calls (hip
 #define SCT_TUNE_ENCODE_GRID 12         /* tiled encoder grid: 1 one workgroup per tile (default), 0 resident workgroups */
 #define SCT_TUNE_INGEST_TILES 13        /* whitelist / FASTQ extraction: tiles per workgroup (0: one range per
                                            resident slot, the whitelist's default; FASTQ default 8) */
-#define SCT_TUNE_FASTQ_ONEPASS 14       /* sct_fastq_extract_fused: 4 / 8 = one pass over ranges of that many
-                                           tiles (look-back), 0 = count pass first (default) */
+#define SCT_TUNE_FASTQ_ONEPASS 14       /* sct_fastq_extract_fused: 0 = count pass first (default); 2 / 4 / 8 = one
+                                           pass, a look-back over ranges of that many 8 KiB tiles held in
+                                           registers; 104 / 108 / 116 / 132 = the same over 4-32 tiles, the
+                                           extraction reading them again */
 #define SCT_TUNE_NKEYS 15
 int sct_tune_set(int key, int64_t value);
 int sct_tune_get(int key, int64_t* value);  /* -1 when unset */

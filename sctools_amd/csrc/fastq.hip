@@ -794,7 +794,10 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
 // bad name that lies beyond the complete records.
 constexpr unsigned long long kAgg = 1ull << 62, kIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
 
-template <int RT>
+// HOLD: the range stays in registers from the count to the extraction (RT x 8 VGPRs); else the
+// extraction reads the tiles again -- from L2, where the count just brought them (the range is
+// RT x 8 KiB per workgroup) -- with the next tile's loads in flight, as fastq_range_kernel
+template <int RT, bool HOLD>
 __global__ __launch_bounds__(WG) void fastq_onepass_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs,
                                                            int text, int64_t ntiles, int64_t nranges,
                                                            unsigned long long* __restrict__ rstat,
@@ -813,27 +816,30 @@ __global__ __launch_bounds__(WG) void fastq_onepass_kernel(const uint8_t* __rest
   __syncthreads();
   const int64_t r = s_r, tile0 = r * RT;
   // the range's bytes (thread tid: bytes tid * 32 .. + 31 of each tile) and, for threads 0 and 1,
-  // the next range's first 64 bytes
-  uint4 cur[RT + 1][SEG];
+  // the next range's first 64 bytes; without HOLD the count loads PB tiles at a time
+  constexpr int PB = HOLD ? RT : (RT < 4 ? RT : 4);
+  uint4 cur[PB + 1][SEG];
+  uint32_t c = 0, na = 0;
+  FileCursor fc1;
+#pragma unroll 1
+  for (int b0 = 0; b0 < RT; b0 += PB) {
 #pragma unroll
-  for (int i = 0; i < RT; ++i)
+    for (int i = 0; i < PB; ++i)
+#pragma unroll
+      for (int k = 0; k < SEG; ++k)
+        cur[i][k] = tile0 + b0 + i < ntiles ? load16(buf, n, (tile0 + b0 + i) * TILE + (int64_t)tid * TB + 16 * k)
+                                            : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int k = 0; k < SEG; ++k)
-      cur[i][k] = tile0 + i < ntiles ? load16(buf, n, (tile0 + i) * TILE + (int64_t)tid * TB + 16 * k)
-                                     : make_uint4(0, 0, 0, 0);
+      cur[PB][k] = HOLD && tid < 2 && tile0 + RT < ntiles
+                       ? load16(buf, n, (tile0 + RT) * TILE + (int64_t)tid * TB + 16 * k)
+                       : make_uint4(0, 0, 0, 0);
+    // phase 1: the range's terminator count
 #pragma unroll
-  for (int k = 0; k < SEG; ++k)
-    cur[RT][k] = tid < 2 && tile0 + RT < ntiles ? load16(buf, n, (tile0 + RT) * TILE + (int64_t)tid * TB + 16 * k)
-                                                : make_uint4(0, 0, 0, 0);
-  // phase 1: the range's terminator count
-  uint32_t c = 0, na = 0;
-  {
-    FileCursor fc;
-#pragma unroll
-    for (int i = 0; i < RT; ++i) {
-      if (tile0 + i >= ntiles) break;
-      const int64_t t0 = (tile0 + i) * TILE, p0 = t0 + (int64_t)tid * TB;
-      const bool ends_here = fc.advance(fs, t0);
+    for (int i = 0; i < PB; ++i) {
+      if (tile0 + b0 + i >= ntiles) break;
+      const int64_t t0 = (tile0 + b0 + i) * TILE, p0 = t0 + (int64_t)tid * TB;
+      const bool ends_here = fc1.advance(fs, t0);
       if (!text && !ends_here && p0 + TB <= n) {
 #pragma unroll
         for (int k = 0; k < SEG; ++k) {
@@ -902,24 +908,42 @@ __global__ __launch_bounds__(WG) void fastq_onepass_kernel(const uint8_t* __rest
   lds_u32* tile32 = as_lds32(tile_bytes);
   int64_t g0 = (int64_t)excl;
   FileCursor fc;
+  uint4 ca[SEG], cb[SEG];  // (!HOLD) this tile's bytes and the next tile's
+  if (!HOLD) {
+#pragma unroll
+    for (int k = 0; k < SEG; ++k) ca[k] = load16(buf, n, tile0 * TILE + (int64_t)tid * TB + 16 * k);
+  }
 #pragma unroll 1
   for (int i = 0; i < RT; ++i) {
     const int64_t tile = tile0 + i;
     if (tile >= ntiles) break;
     const int64_t t0 = tile * TILE, p0 = t0 + (int64_t)tid * TB;
+    if (!HOLD) {  // the next tile (all threads) or, after the range's last, the next range's head
+      const bool all = i + 1 < RT, need = tile + 1 < ntiles && (all || tid < 2);
+#pragma unroll
+      for (int k = 0; k < SEG; ++k)
+        cb[k] = need ? load16(buf, n, t0 + TILE + (int64_t)tid * TB + 16 * k) : make_uint4(0, 0, 0, 0);
+    }
+    const uint4* a0 = HOLD ? cur[0] : ca;
+    const uint4* a1 = HOLD ? cur[1] : cb;
     const bool ends_here = fc.advance(fs, t0);
     Span spn{0, 0, 0, 0};
-    if (p0 < n) spn = thread_span(buf, n, fs, text, p0, cur[0], ends_here);
+    if (p0 < n) spn = thread_span(buf, n, fs, text, p0, a0, ends_here);
     __syncthreads();  // the previous tile's readers of tile_bytes / term are done
 #pragma unroll
     for (int k = 0; k < SEG; ++k) {
-      tile_bytes[tid * SEG + k] = p0 + 16 * k < n ? cur[0][k] : make_uint4(0, 0, 0, 0);
-      if (tid < 2) tile_bytes[TILE / 16 + tid * SEG + k] = cur[1][k];  // the next tile's head
+      tile_bytes[tid * SEG + k] = p0 + 16 * k < n ? a0[k] : make_uint4(0, 0, 0, 0);
+      if (tid < 2) tile_bytes[TILE / 16 + tid * SEG + k] = a1[k];  // the next tile's head
     }
+    if (HOLD) {
 #pragma unroll
-    for (int j = 0; j < RT; ++j)
+      for (int j = 0; j < PB; ++j)
 #pragma unroll
-      for (int k = 0; k < SEG; ++k) cur[j][k] = cur[j + 1][k];
+        for (int k = 0; k < SEG; ++k) cur[j][k] = cur[j + 1][k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < SEG; ++k) ca[k] = cb[k];
+    }
     const uint32_t tbits = spn.m | spn.vbits, cc = __popc(tbits);
     uint32_t ic = cc;
 #pragma unroll
@@ -1228,8 +1252,9 @@ extern "C" int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, con
                    reinterpret_cast<unsigned long long*>(d_status)};
   // SCT_TUNE_FASTQ_ONEPASS: 4 or 8 = one pass over ranges of that many tiles, 0 = count pass first
   const int64_t onepass = sct::tune(SCT_TUNE_FASTQ_ONEPASS, 0);
-  if (onepass == 2 || onepass == 4 || onepass == 8) {
-    const int RT = (int)onepass;
+  const bool hold = onepass < 100;
+  const int RT = (int)(hold ? onepass : onepass - 100);
+  if ((hold && (RT == 2 || RT == 4 || RT == 8)) || (!hold && (RT == 4 || RT == 8 || RT == 16 || RT == 32))) {
     const int64_t nranges = sct::ceil_div(ntiles, RT);
     SCT_CHECK(nranges < (1LL << 31), "buffer too large");
     void* scr = nullptr;
@@ -1240,7 +1265,12 @@ extern "C" int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, con
       auto* rstat = reinterpret_cast<unsigned long long*>(scr);
       auto* ctr = reinterpret_cast<unsigned*>(rstat + nranges);
       const Files fs{d_file_ends, nfiles};
-      auto kern = RT == 2 ? fastq_onepass_kernel<2> : RT == 4 ? fastq_onepass_kernel<4> : fastq_onepass_kernel<8>;
+      auto kern = hold ? (RT == 2 ? fastq_onepass_kernel<2, true> : RT == 4 ? fastq_onepass_kernel<4, true>
+                                                                             : fastq_onepass_kernel<8, true>)
+                       : (RT == 4    ? fastq_onepass_kernel<4, false>
+                          : RT == 8  ? fastq_onepass_kernel<8, false>
+                          : RT == 16 ? fastq_onepass_kernel<16, false>
+                                     : fastq_onepass_kernel<32, false>);
       hipLaunchKernelGGL(kern, dim3((unsigned)nranges), dim3(WG), 0, s, d_buf, nbytes, fs, text_mode ? 1 : 0, ntiles,
                          nranges, rstat, ctr, sp, to);
       hipLaunchKernelGGL(fastq_onepass_finish_kernel, dim3(1), dim3(1), 0, s,

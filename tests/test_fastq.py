@@ -284,7 +284,7 @@ def _fused_cases(fq_golden, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("onepass", [0, 4, 8])
+@pytest.mark.parametrize("onepass", [0, 4, 8, 108, 132])
 @pytest.mark.parametrize("text_mode", [0, 1])
 def test_fastq_fused_one_pass_vs_indexed(fq_golden, tmp_path, text_mode, onepass):
     """sct_fastq_extract_fused (no index, no scan launch, no host synchronisation; VERDICT r3
