@@ -556,14 +556,15 @@ __device__ __forceinline__ void tile_items(lds_u16* term, lds_u8* tile8, lds_u32
       const uint8_t ch = o < TILE + head ? tile8[o] : buf[t0 + o];
       if (ch != '@') atomicMax(to.d_status + 1, ~(unsigned long long)((g0 + t + 1) >> 2));
     }
-    // sequence / quality lines: after even terminators; one item per line, its spans in turn
-    const int te0 = (int)(g0 & 1);
-    const int nact = tmax > te0 ? (tmax - te0 + 1) / 2 : 0;
-    for (int a = tid; a < nact; a += WG) {
-      const int t = te0 + 2 * a;
+    // sequence / quality lines: one item per line, its spans in turn; the first half of the
+    // workgroup takes the sequence lines (after terminators t = -g0 mod 4), the second half the
+    // quality lines (t = 2 - g0 mod 4), so every wave runs one kind (the CB encode is not carried
+    // through the quality lines' waves)
+    constexpr int HALF = WG / 2;
+    const bool is_seq = tid < HALF;
+    for (int t = (int)(((is_seq ? 0 : 2) - g0) & 3) + 4 * (tid & (HALF - 1)); t < tmax; t += 4 * HALF) {
       const int64_t line = g0 + t + 1, rec = line >> 2;
       if (rec >= to.cap) continue;
-      const bool is_seq = (line & 3) == 1;
       const uint32_t e = term[t];
       const int start = (int)(e & T16_OFF) + ((e & T16_VIRT) ? 0 : 1);  // <= TILE
       int64_t cend;  // content end relative to the tile start
