@@ -146,21 +146,69 @@ __global__ __launch_bounds__(WG) void line_lens_kernel(const int64_t* __restrict
 // and stores, which drain at every wait (vmcnt(0): the stores' count varies by line).
 constexpr int NSUB = 4, WTILE = NSUB * TILE;
 
+// Fixed-stride files (every line S bytes with its '\n', the usual whitelist): the stride is the
+// first line's length (S = its '\n' position + 1, taken from the file's first 64 bytes by every
+// workgroup); a tile is flagged when any of its line ends is not at a position = S - 1 (mod S).
+// The encode pass then numbers lines by arithmetic (line g ends at g S + S - 1) when no tile is
+// flagged and S divides the file size.
+constexpr int kMaxStride = 64;
+
+// S, or 0 when the first 64 bytes hold no '\n'; every thread of the workgroup (one barrier)
+__device__ __forceinline__ int file_stride(const uint8_t* __restrict__ buf, int64_t n, int* s_stride) {
+  if (threadIdx.x == 0) {
+    int S = 0;
+    for (int k = 0; k < kMaxStride / 16 && !S; ++k) {
+      const int64_t p = 16 * k;
+      if (p >= n) break;
+      const uint32_t m = lf_mask_v(load16(buf, n, p), n, p);  // (a file's last byte counts as an end)
+      if (m) S = 16 * k + __ffs(m);
+    }
+    *s_stride = S;
+  }
+  __syncthreads();
+  return *s_stride;
+}
+
 __global__ __launch_bounds__(WG) void wl_count_kernel(const uint8_t* __restrict__ buf, int64_t n, sct::TileSums ts,
                                                       int32_t* __restrict__ d_maxlen) {
   const int64_t t0 = (int64_t)blockIdx.x * WTILE;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *d_maxlen = 0;  // (the encode pass raises it; no memset launch)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *d_maxlen = 0;  // (the encode pass raises it; no memset launch)
+    *ts.fany = 0u;  // (the reduction ORs the tile flags into it)
+  }
   uint4 v[NSUB];
 #pragma unroll
   for (int j = 0; j < NSUB; ++j) v[j] = load16(buf, n, t0 + j * TILE + threadIdx.x * 16);
+  __shared__ int s_stride;
+  __shared__ uint32_t s_t0mod;
+  const int S = file_stride(buf, n, &s_stride);
+  if (threadIdx.x == 0 && S) s_t0mod = (uint32_t)(t0 % S);
+  __syncthreads();
+  const uint32_t t0mod = S ? s_t0mod : 0u;
+  const float invS = S ? 1.0f / (float)S : 0.0f;
   unsigned long long c = 0;
   long long last = -1;
+  uint32_t odd = S ? 0u : 1u;  // a line end off the stride
 #pragma unroll
   for (int j = 0; j < NSUB; ++j) {
     const int64_t p0 = t0 + j * TILE + threadIdx.x * 16;
     const uint32_t m = p0 < n ? lf_mask_v(v[j], n, p0) : 0u;
     c += __popc(m);
     if (m) last = p0 + 31 - __clz(m);  // (sub-tiles in byte order)
+    if (S && p0 < n) {
+      // p0 mod S from the tile's t0 mod S and the in-tile offset r < 2^14 (float quotient: off by
+      // at most one below, fixed by one compare)
+      const uint32_t r = (uint32_t)(j * TILE + threadIdx.x * 16);
+      const uint32_t q = (uint32_t)((float)r * invS);
+      uint32_t ph = r - q * (uint32_t)S;
+      if (ph >= (uint32_t)S) ph -= S;
+      ph += t0mod;
+      if (ph >= (uint32_t)S) ph -= S;
+      uint32_t e = 0;  // the ends a stride-S file has in these bytes
+      for (uint32_t b = (uint32_t)S - 1u - ph; b < 16u; b += (uint32_t)S) e |= 1u << b;
+      const uint32_t valid = p0 + 16 <= n ? 0xFFFFu : (1u << (n - p0)) - 1u;
+      odd |= (m ^ e) & valid;
+    }
   }
 #pragma unroll
   for (int o = 32; o; o >>= 1) {
@@ -169,17 +217,23 @@ __global__ __launch_bounds__(WG) void wl_count_kernel(const uint8_t* __restrict_
   }
   __shared__ unsigned long long wc[WG / 64];
   __shared__ long long wl[WG / 64];
+  __shared__ uint32_t wodd[WG / 64];
+  const uint64_t oddw = __ballot(odd != 0u);
   if ((threadIdx.x & 63) == 0) {
     wc[threadIdx.x >> 6] = c;
     wl[threadIdx.x >> 6] = last;
+    wodd[threadIdx.x >> 6] = oddw ? 1u : 0u;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    uint32_t f = wodd[0];
     for (int w = 1; w < WG / 64; ++w) {
       c += wc[w];
       last = max(last, wl[w]);
+      f |= wodd[w];
     }
     sct::tile_publish(ts, blockIdx.x, c, last);
+    ts.f0[blockIdx.x] = f;
   }
 }
 
@@ -304,10 +358,50 @@ __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
   uint4 cur[NSUB];
 #pragma unroll
   for (int j = 0; j < NSUB; ++j) cur[j] = load16(buf, n, tile * WTILE + j * TILE + t * 16);
-  sct::tile_prefix<WG>(ts, tile, &s_excl, &s_excl_last, red);  // (its barriers also cover the LUT)
+  lds_u32* lds32 = as_lds32(tile_bytes);
+  __shared__ int s_stride;
+  const int S = file_stride(buf, n, &s_stride);  // (its barrier also covers the LUT)
+  if (S > 0 && *ts.fany == 0u && n % S == 0 && words == 1 && KIND * (S - 1) <= 64) {
+    // a fixed-stride file: line g is [g S, g S + S - 1); the lines ending in a tile are
+    // g in [t0 / S, t1 / S), one per thread (consecutive lanes, consecutive lines: every store
+    // coalesced), no numbering
+    const int L = S - 1;
+    for (; tile < tend; ++tile) {
+      const int64_t t0 = tile * WTILE, t1 = t0 + WTILE < n ? t0 + WTILE : n;
+      __syncthreads();  // the previous tile's readers of tile_bytes are done
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j) tile_bytes[j * WG + t] = cur[j];
+      if (tile + 1 < tend) {
+#pragma unroll
+        for (int j = 0; j < NSUB; ++j) cur[j] = load16(buf, n, t0 + WTILE + j * TILE + t * 16);
+      }
+      __syncthreads();
+      const int64_t gB = t1 / S;
+      for (int64_t g = t0 / S + t; g < gB; g += WG) {
+        if (g >= cap) break;
+        const int64_t start = g * S;
+        uint32_t gg, fl;
+        if (start >= t0) {
+          const int off = (int)(start - t0), o = off & 3, w0 = off >> 2;
+          encode_line1<KIND>(lut, [&](int k) { return lds32[w0 + k]; }, o, L, codes + g, gg, fl);
+        } else {
+          encode_line<KIND>(lut, buf + start, L, 1, codes + g, gg, fl);
+        }
+        starts[g] = start;
+        lens[g] = L;
+        if (gc) gc[g] = (uint8_t)(gg > 255 ? 255 : gg);
+        if (flags) flags[g] = (uint8_t)fl;
+      }
+    }
+    if (t == 0) {
+      if (L > __hip_atomic_load(d_maxlen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(d_maxlen, L);
+      if (tend == ntiles) *d_nlines = (unsigned long long)(n / S);
+    }
+    return;
+  }
+  sct::tile_prefix<WG>(ts, tile, &s_excl, &s_excl_last, red);
   uint64_t g_base = s_excl;
   long long last_base = s_excl_last;
-  lds_u32* lds32 = as_lds32(tile_bytes);
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   int32_t mx = 0;
   for (; tile < tend; ++tile) {
@@ -526,8 +620,8 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   const int64_t ntiles = sct::ceil_div(nbytes, WTILE);
   SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
   StreamBuf scratch;
-  SCT_HIP(scratch.alloc(sct::tile_sums_bytes(ntiles), s));
-  const sct::TileSums ts = sct::tile_sums_at(scratch.p, ntiles, true);
+  SCT_HIP(scratch.alloc(sct::tile_sums_bytes(ntiles, true), s));
+  const sct::TileSums ts = sct::tile_sums_at(scratch.p, ntiles, true, true);
   hipLaunchKernelGGL(wl_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, ts, d_maxlen);
   SCT_LAUNCH_CHECK();
   hipLaunchKernelGGL(sct::tile_sums_reduce_kernel, dim3((unsigned)sct::ceil_div(ntiles, 1024)), dim3(64), 0, s, ts,

@@ -22,14 +22,16 @@ struct TileSums {
   unsigned long long* l0;  // nullable: [ntiles] last position + 1 of tile t, 0 if none
   unsigned long long* l1;  // maxima over blocks of 32
   unsigned long long* l2;  // maxima over blocks of 1024
+  uint32_t* f0;            // nullable: [ntiles] flags of tile t (written by its count workgroup)
+  uint32_t* fany;          // with f0: the OR of every f0 (zeroed by the count pass's workgroup 0)
 };
 
-// bytes of the scratch for ntiles tiles: c0 | l0 | c1 | c2 | l1 | l2
-inline size_t tile_sums_bytes(int64_t ntiles) {
+// bytes of the scratch for ntiles tiles: c0 | l0 | c1 | c2 | l1 | l2 (| f0 | fany)
+inline size_t tile_sums_bytes(int64_t ntiles, bool with_flags = false) {
   const size_t n1 = (size_t)((ntiles + 31) >> 5), n2 = (size_t)((ntiles + 1023) >> 10);
-  return 16 * ((size_t)ntiles + n1 + n2);
+  return 16 * ((size_t)ntiles + n1 + n2) + (with_flags ? 4 * (size_t)ntiles + 8 : 0);
 }
-inline TileSums tile_sums_at(void* base, int64_t ntiles, bool with_last) {
+inline TileSums tile_sums_at(void* base, int64_t ntiles, bool with_last, bool with_flags = false) {
   unsigned long long* p = reinterpret_cast<unsigned long long*>(base);
   const int64_t n1 = (ntiles + 31) >> 5, n2 = (ntiles + 1023) >> 10;
   TileSums s;
@@ -39,6 +41,8 @@ inline TileSums tile_sums_at(void* base, int64_t ntiles, bool with_last) {
   s.c2 = s.c1 + n1;
   s.l1 = s.c2 + n2;
   s.l2 = s.l1 + n1;
+  s.f0 = with_flags ? reinterpret_cast<uint32_t*>(s.l2 + n2) : nullptr;
+  s.fany = with_flags ? s.f0 + ntiles : nullptr;
   return s;
 }
 
@@ -74,6 +78,14 @@ static __global__ __launch_bounds__(64) void tile_sums_reduce_kernel(TileSums s,
   if (lane == 0) {
     s.c2[blockIdx.x] = cs;
     if (s.l0) s.l2[blockIdx.x] = ls;
+  }
+  if (s.f0) {  // the OR of the tile flags: an atomic only from a block that has one set
+    uint32_t f = 0;
+    for (int k = 0; k < 16; ++k)
+      if (t0 + k < ntiles) f |= s.f0[t0 + k];
+#pragma unroll
+    for (int o = 32; o; o >>= 1) f |= __shfl_xor(f, o);
+    if (lane == 0 && f) atomicOr(s.fany, f);
   }
 }
 

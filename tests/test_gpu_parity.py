@@ -1278,6 +1278,20 @@ def _ingest_cases():
             rec = rec[:L // 2] + b"N" + rec[L // 2 + 1:]
         parts.append(rec + b"\n")
     cases["acgt"] = b"".join(parts)
+    # fixed-stride files (the encode pass numbers lines by arithmetic): 16 / 32 / 21 bases, empty
+    # lines, a stride-4 file whose last line has no '\n' (its last base is chopped, as the
+    # reference's line[:-1]), N and lower-case lines among them, and one line end off the stride
+    # in a 340 KB file (every other tile fixed: the file must take the general path)
+    for L in (16, 32, 21):
+        recs = [acgt[rng.integers(0, 4, L)].tobytes() for _ in range(20_000 if L == 16 else 8_000)]
+        recs[7] = b"N" + recs[7][1:]
+        recs[11] = recs[11].lower()
+        cases["fixed%d" % L] = b"\n".join(recs) + b"\n"
+    cases["fixed_empty"] = b"\n" * 20_000
+    cases["fixed_no_final_lf"] = b"ACG\n" * 10_000 + b"TGCA"
+    odd = bytearray(b"ACGTACGTACGTACGT\n" * 20_000)
+    odd[170_000:170_017] = b"ACGTACGTACGTACG\nA"  # one end moved by one byte
+    cases["fixed_one_off"] = bytes(odd)
     return cases
 
 
