@@ -712,16 +712,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
   const int lane_off = 16 * (lane >> 4) + 64 * (lane & 15);
   const int gw = blockIdx.x * 4 + wave, GW = gridDim.x * 4;
   const int ub = (int)((int64_t)nslices * gw / GW), ue = (int)((int64_t)nslices * (gw + 1) / GW);
-  unsigned long long accA[4] = {0, 0, 0, 0}, accB[4] = {0, 0, 0, 0};
+  // the squares of the two interleaved quarters go to separate sums (two dependency chains per
+  // weight instead of one), added at the flush
+  unsigned long long accA[4] = {0, 0, 0, 0}, accB[4] = {0, 0, 0, 0}, accB2[4] = {0, 0, 0, 0};
   int cur_w = -1;
   auto flush = [&]() {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (accA[k]) atomicAdd(&bins[cur_w + wt_thread + k], accA[k]);
-      const unsigned long long b = 4 * accB[k] - accA[k];
+      const unsigned long long b = 4 * (accB[k] + accB2[k]) - accA[k];
       if (b) atomicAdd(&bins[cur_w + wt_thread + k + 1], b);
       accA[k] = 0;
       accB[k] = 0;
+      accB2[k] = 0;
     }
   };
   auto load_plane = [&](int sl, int R, v2l_t* dst) {
@@ -732,7 +735,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
   };
   // two quarters qa, qb of stage 2 from their byte splits, then their squares
   auto stage2x2B = [&](const v2l_t& Bla, const v2l_t& Bha, const v2l_t& Blb, const v2l_t& Bhb, auto qa_c,
-                       auto qb_c, unsigned long long* acc) {
+                       auto qb_c, unsigned long long* acc, unsigned long long* acc2) {
     constexpr int qa = decltype(qa_c)::value, qb = decltype(qb_c)::value;
     v4i_t ca[4], cb[4];
 #pragma unroll
@@ -755,7 +758,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
       for (int i = 0; i < 4; ++i) {
         acc[digit_weight_c((uint32_t)qa) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
             (unsigned long long)((int64_t)ca[q2][i] * ca[q2][i]);
-        acc[digit_weight_c((uint32_t)qb) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
+        acc2[digit_weight_c((uint32_t)qb) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
             (unsigned long long)((int64_t)cb[q2][i] * cb[q2][i]);
       }
   };
@@ -823,7 +826,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
         v2l_t Bla, Bha, Blb, Bhb;
         split16(pa, Bla, Bha);
         split16(pb, Blb, Bhb);
-        stage2x2B(Bla, Bha, Blb, Bhb, qa_c, qb_c, accB);
+        stage2x2B(Bla, Bha, Blb, Bhb, qa_c, qb_c, accB, accB2);
         __builtin_amdgcn_sched_barrier(0);
       };
       quarters16(std::integral_constant<int, 0>(), std::integral_constant<int, 1>());
@@ -832,10 +835,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     v2l_t Bla, Bha, Blb, Bhb;
     split16(csp[0], Bla, Bha);
     split16(csp[1], Blb, Bhb);
-    stage2x2B(Bla, Bha, Blb, Bhb, std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), accA);
+    stage2x2B(Bla, Bha, Blb, Bhb, std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), accA, accA);
     split16(csp[2], Bla, Bha);
     split16(csp[3], Blb, Bhb);
-    stage2x2B(Bla, Bha, Blb, Bhb, std::integral_constant<int, 2>(), std::integral_constant<int, 3>(), accA);
+    stage2x2B(Bla, Bha, Blb, Bhb, std::integral_constant<int, 2>(), std::integral_constant<int, 3>(), accA, accA);
   }
   if (cur_w >= 0) flush();
   __syncthreads();
