@@ -59,7 +59,9 @@ int sct_set_device(int device);        /* select the device for later calls (hip
                                            pass, a look-back over ranges of that many 8 KiB tiles held in
                                            registers; 104 / 108 / 116 / 132 = the same over 4-32 tiles, the
                                            extraction reading them again */
-#define SCT_TUNE_NKEYS 15
+#define SCT_TUNE_INGEST_DIRECT 15       /* whitelist ingest: up to this many 16 KiB tiles (4096) the encode pass
+                                           sums the per-tile counts itself, no reduction launch */
+#define SCT_TUNE_NKEYS 16
 int sct_tune_set(int key, int64_t value);
 int sct_tune_get(int key, int64_t* value);  /* -1 when unset */
 

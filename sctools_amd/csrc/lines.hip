@@ -337,8 +337,8 @@ __device__ __forceinline__ void encode_line(const uint8_t* lut, const uint8_t* r
 // tile's first line may start before it).
 template <int KIND>
 __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
-    const uint8_t* __restrict__ buf, int64_t n, int64_t ntiles, int64_t per_wg, sct::TileSums ts, int64_t cap,
-    int words, uint64_t* __restrict__ codes, int64_t* __restrict__ starts, int32_t* __restrict__ lens,
+    const uint8_t* __restrict__ buf, int64_t n, int64_t ntiles, int64_t per_wg, sct::TileSums ts, int direct,
+    int64_t cap, int words, uint64_t* __restrict__ codes, int64_t* __restrict__ starts, int32_t* __restrict__ lens,
     uint8_t* __restrict__ gc, uint8_t* __restrict__ flags, unsigned long long* __restrict__ d_nlines,
     int32_t* __restrict__ d_maxlen) {
   __shared__ uint8_t lut[256];
@@ -360,8 +360,12 @@ __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
   for (int j = 0; j < NSUB; ++j) cur[j] = load16(buf, n, tile * WTILE + j * TILE + t * 16);
   lds_u32* lds32 = as_lds32(tile_bytes);
   __shared__ int s_stride;
+  __shared__ uint32_t s_fany;
   const int S = file_stride(buf, n, &s_stride);  // (its barrier also covers the LUT)
-  if (S > 0 && *ts.fany == 0u && n % S == 0 && words == 1 && KIND * (S - 1) <= 64) {
+  // direct: the tile prefix and the flags straight from the per-tile words (no reduction launch)
+  if (direct) sct::tile_prefix_direct<WG>(ts, tile, ntiles, &s_excl, &s_excl_last, &s_fany, red);
+  const uint32_t fany = direct ? s_fany : *ts.fany;
+  if (S > 0 && fany == 0u && n % S == 0 && words == 1 && KIND * (S - 1) <= 64) {
     // a fixed-stride file: line g is [g S, g S + S - 1); the lines ending in a tile are
     // g in [t0 / S, t1 / S), one per thread (consecutive lanes, consecutive lines: every store
     // coalesced), no numbering
@@ -399,7 +403,7 @@ __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
     }
     return;
   }
-  sct::tile_prefix<WG>(ts, tile, &s_excl, &s_excl_last, red);
+  if (!direct) sct::tile_prefix<WG>(ts, tile, &s_excl, &s_excl_last, red);
   uint64_t g_base = s_excl;
   long long last_base = s_excl_last;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -624,9 +628,14 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   const sct::TileSums ts = sct::tile_sums_at(scratch.p, ntiles, true, true);
   hipLaunchKernelGGL(wl_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, ts, d_maxlen);
   SCT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(sct::tile_sums_reduce_kernel, dim3((unsigned)sct::ceil_div(ntiles, 1024)), dim3(64), 0, s, ts,
-                     ntiles);
-  SCT_LAUNCH_CHECK();
+  // up to 4,096 tiles (64 MiB) every encode workgroup reads the per-tile words itself (<= 16 per
+  // thread) instead of waiting for a reduction launch
+  const int direct = ntiles <= sct::tune(SCT_TUNE_INGEST_DIRECT, 4096) ? 1 : 0;
+  if (!direct) {
+    hipLaunchKernelGGL(sct::tile_sums_reduce_kernel, dim3((unsigned)sct::ceil_div(ntiles, 1024)), dim3(64), 0, s, ts,
+                       ntiles);
+    SCT_LAUNCH_CHECK();
+  }
   const int64_t cap = max_lines > 0 ? max_lines : 0;
   auto kern = kind == 2 ? whitelist_fused_kernel<2> : whitelist_fused_kernel<3>;
   // one range per resident slot (0.081 ms for config 5's whitelist; one 16 KiB tile per
@@ -634,7 +643,7 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   const int64_t knob = sct::tune(SCT_TUNE_INGEST_TILES, 0);
   const int64_t per_wg = knob > 0 ? knob : sct::ceil_div(ntiles, resident_slots((const void*)kern, ntiles));
   hipLaunchKernelGGL(kern, dim3((unsigned)sct::ceil_div(ntiles, per_wg)), dim3(WG), 0, s, d_buf, nbytes, ntiles,
-                     per_wg, ts, cap, words, d_codes, d_starts, d_lens, d_gc, d_flags,
+                     per_wg, ts, direct, cap, words, d_codes, d_starts, d_lens, d_gc, d_flags,
                      reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen);
   SCT_LAUNCH_CHECK();
   return SCT_OK;

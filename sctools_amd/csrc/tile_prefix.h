@@ -150,4 +150,47 @@ __device__ __forceinline__ void tile_prefix(const TileSums& s, int64_t t, unsign
   __syncthreads();
 }
 
+// Without the coarse levels (small buffers: ntiles up to a few thousand): every thread of the
+// workgroup sums tile t's exclusive count and the last position before it straight from c0 / l0,
+// and ORs every tile's flag (f0, nullable) -- ntiles / WG loads per thread, no reduction launch.
+template <int WG>
+__device__ __forceinline__ void tile_prefix_direct(const TileSums& s, int64_t t, int64_t ntiles, unsigned long long* cnt,
+                                                   long long* last, uint32_t* flags_any,
+                                                   unsigned long long (*red)[WG / 64]) {
+  unsigned long long sum = 0, mx = 0, fl = 0;
+  for (int64_t k = threadIdx.x; k < ntiles; k += WG) {
+    if (k < t) {
+      sum += s.c0[k];
+      if (s.l0) mx = mx > s.l0[k] ? mx : s.l0[k];
+    }
+    if (s.f0) fl |= s.f0[k];
+  }
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    sum += __shfl_xor(sum, o);
+    fl |= __shfl_xor(fl, o);
+    const unsigned long long m2 = __shfl_xor(mx, o);
+    mx = mx > m2 ? mx : m2;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = sum;
+    red[1][wave] = mx;
+    red[2][wave] = fl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long a = 0, b = 0, c = 0;
+    for (int w = 0; w < WG / 64; ++w) {
+      a += red[0][w];
+      b = b > red[1][w] ? b : red[1][w];
+      c |= red[2][w];
+    }
+    *cnt = a;
+    *last = (long long)b - 1;
+    *flags_any = (uint32_t)c;
+  }
+  __syncthreads();
+}
+
 }  // namespace sct

@@ -1298,6 +1298,18 @@ def _ingest_cases():
 @pytest.mark.parametrize("name", list(_ingest_cases()))
 @pytest.mark.parametrize("kind,words", [(2, 1), (2, 2), (3, 1), (3, 2)])
 def test_whitelist_encode_one_pass(name, kind, words):
+    _whitelist_encode_check(name, kind, words)
+
+
+@pytest.mark.parametrize("name", ["ragged", "acgt", "fixed16", "fixed_one_off"])
+def test_whitelist_encode_with_reduction_launch(name):
+    """The same with the tile prefixes from the coarse sums of tile_sums_reduce_kernel (the form
+    buffers above 64 MiB take), not summed by every encode workgroup."""
+    with _lib.tuning(ingest_direct=0):
+        _whitelist_encode_check(name, 2, 1)
+
+
+def _whitelist_encode_check(name, kind, words):
     """sct_whitelist_encode (count pass, tile-sum reduction, encode pass; asynchronous) against
     the reference's binary line loop with `line[:-1]` (barcode.py:95-97) and the oracle's
     encoders (encodings.py:75-88 / 155-167): line count, longest line, every start, length,
