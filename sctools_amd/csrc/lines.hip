@@ -375,47 +375,62 @@ __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
       // straight from memory (L2 / the Infinity Cache: the count pass just read them) -- 4 or 5
       // aligned dwords per line, all loads issued at once, no LDS staging, no barriers
       const int64_t t1 = tend * WTILE < n ? tend * WTILE : n, gB = t1 / S;
-      for (int64_t g = tile * WTILE / S + t; g < gB; g += WG) {
-        if (g >= cap) break;
-        const int64_t start = g * S;
-        const uint32_t o = (uint32_t)(start & 3);
-        uint32_t gg, fl;
-        if (start - o + 20 <= n) {
-          const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + (start - o));
-          const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = o ? w[4] : 0u;
-          const uint32_t x[4] = {__builtin_amdgcn_alignbyte(d1, d0, o), __builtin_amdgcn_alignbyte(d2, d1, o),
-                                 __builtin_amdgcn_alignbyte(d3, d2, o), __builtin_amdgcn_alignbyte(d4, d3, o)};
-          uint64_t code = 0;
-          uint32_t bad = 0;
+      const int64_t gend = gB < cap ? gB : (cap > 0 ? cap : 0);
+      constexpr int U = 4;  // lines per thread per step, all their loads issued before any is used
+      for (int64_t g0 = tile * WTILE / S + t; g0 < gend; g0 += U * WG) {
+        uint32_t d[U][5];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t u = ((x[k] >> 1) ^ (x[k] >> 2)) & 0x03030303u;
-            const uint32_t v = u ^ ((u >> 1) & 0x01010101u);
-            bad |= __builtin_amdgcn_perm(0u, 0x47544341u, v) ^ x[k];
-            const uint32_t y =
-                __builtin_amdgcn_perm(0u, KIND == 2 ? v : __builtin_amdgcn_perm(0u, 0x03040102u, v), 0x00010203u);
-            if (KIND == 2) {
-              const uint32_t a = (y | (y >> 6)) & 0x000F000Fu;
-              code = (code << 8) | ((a | (a >> 12)) & 0xFFu);
-            } else {
-              const uint32_t a = (y | (y >> 5)) & 0x003F003Fu;
-              code = (code << 12) | ((a | (a >> 10)) & 0xFFFu);
+        for (int u = 0; u < U; ++u) {
+          const int64_t g = g0 + (int64_t)u * WG, start = g * S;
+          const uint32_t o = (uint32_t)(start & 3);
+          if (g < gend && start - o + 20 <= n) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + (start - o));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[u][k] = w[k];
+            d[u][4] = o ? w[4] : 0u;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t g = g0 + (int64_t)u * WG, start = g * S;
+          if (g >= gend) break;
+          const uint32_t o = (uint32_t)(start & 3);
+          uint32_t gg, fl;
+          bool done = false;
+          if (start - o + 20 <= n) {
+            uint64_t code = 0;
+            uint32_t bad = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const uint32_t x = __builtin_amdgcn_alignbyte(d[u][k + 1], d[u][k], o);
+              const uint32_t uu = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
+              const uint32_t v = uu ^ ((uu >> 1) & 0x01010101u);
+              bad |= __builtin_amdgcn_perm(0u, 0x47544341u, v) ^ x;
+              const uint32_t y =
+                  __builtin_amdgcn_perm(0u, KIND == 2 ? v : __builtin_amdgcn_perm(0u, 0x03040102u, v), 0x00010203u);
+              if (KIND == 2) {
+                const uint32_t a = (y | (y >> 6)) & 0x000F000Fu;
+                code = (code << 8) | ((a | (a >> 12)) & 0xFFu);
+              } else {
+                const uint32_t a = (y | (y >> 5)) & 0x003F003Fu;
+                code = (code << 12) | ((a | (a >> 10)) & 0xFFFu);
+              }
+            }
+            if (!bad) {
+              codes[g] = code;
+              gg = (uint32_t)__popcll(code & (KIND == 2 ? 0x5555555555555555ull : 0x9249249249249249ull));
+              fl = 0;
+              done = true;
             }
           }
-          if (bad) {
-            encode_line<KIND>(lut, buf + start, L, 1, codes + g, gg, fl);
-          } else {
-            codes[g] = code;
-            gg = (uint32_t)__popcll(code & (KIND == 2 ? 0x5555555555555555ull : 0x9249249249249249ull));
-            fl = 0;
-          }
-        } else {  // the file's last line: its window would read past the buffer
-          encode_line<KIND>(lut, buf + start, L, 1, codes + g, gg, fl);
+          // a line with another byte (the LUT), or the file's last line (its window would read
+          // past the buffer)
+          if (!done) encode_line<KIND>(lut, buf + start, L, 1, codes + g, gg, fl);
+          starts[g] = start;
+          lens[g] = L;
+          if (gc) gc[g] = (uint8_t)gg;
+          if (flags) flags[g] = (uint8_t)fl;
         }
-        starts[g] = start;
-        lens[g] = L;
-        if (gc) gc[g] = (uint8_t)gg;
-        if (flags) flags[g] = (uint8_t)fl;
       }
       tile = tend;  // (the range is done)
     }
