@@ -40,6 +40,10 @@ constexpr int TILE = 8192;  // bytes per thread-block tile
 constexpr int TB = TILE / WG;  // bytes per thread
 constexpr int SEG = TB / 16;   // 16-B loads per thread
 
+#ifndef SCT_FQ_ABL
+#define SCT_FQ_ABL 0  // timing-only ablations of fastq_range_kernel (tools/gpu_fastq_abl.sh)
+#endif
+
 struct Files {
   const int64_t* ends;  // cumulative end offsets, nfiles entries
   int nfiles;
@@ -513,16 +517,6 @@ __global__ __launch_bounds__(WG) void fq_count_kernel(const uint8_t* __restrict_
   }
 }
 
-// 4 bytes of a row through the LUT of a `bits`-bit code (lut_entry: code in bits 0..2, flags above)
-__device__ __forceinline__ void enc_dword(const uint8_t* lut, int bits, uint32_t y, uint64_t& code, uint32_t& fl) {
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const uint32_t e = lut[(y >> (8 * b)) & 0xFFu];
-    code = (code << bits) | (e & 7u);
-    fl |= e;
-  }
-}
-
 // The per-tile work after the tile's terminators are in LDS (term, in byte order; the tile's
 // bytes in tile8 / tile32, and `head` bytes of the next tile after them): the '@' check of every
 // name line and every sequence / quality line's span slices (one item per line, its spans in
@@ -544,6 +538,145 @@ struct TileOut {
   unsigned long long* d_status;
 };
 
+// The 16 bytes at tile-relative offset s (>= 0): from the staged tile when lds (the 5-dword window
+// lies in LDS), else from global memory (gt = the tile's first dword; the window lies in the buffer).
+// One branch per window, not per dword: a per-dword LDS-or-global select compiled to a masked
+// branch and a wait around every load.
+__device__ __forceinline__ uint4 bytes16_at(lds_u32* tile32, const uint32_t* __restrict__ gt, int s, bool lds) {
+  const int d = s >> 2;
+  const uint32_t sh = (uint32_t)(s & 3);
+  uint32_t x0, x1, x2, x3, x4;
+  if (lds) {
+    x0 = tile32[d], x1 = tile32[d + 1], x2 = tile32[d + 2], x3 = tile32[d + 3], x4 = tile32[d + 4];
+  } else {
+    x0 = gt[d], x1 = gt[d + 1], x2 = gt[d + 2], x3 = gt[d + 3], x4 = gt[d + 4];
+  }
+  return make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                    __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+}
+
+// the first m (1..16) bytes of y to o in pieces of G bytes (G: the largest of 16 / 8 / 4 / 2 / 1
+// dividing the row width and the rows' base address; m is a multiple of G; both uniform)
+__device__ __forceinline__ void store_row16(uint8_t* o, const uint4 y, int m, int G) {
+  const uint32_t d[4] = {y.x, y.y, y.z, y.w};
+  if (G == 16) {
+    *reinterpret_cast<uint4*>(o) = y;
+  } else if (G == 8) {
+    *reinterpret_cast<uint2*>(o) = make_uint2(d[0], d[1]);
+    if (m > 8) *reinterpret_cast<uint2*>(o + 8) = make_uint2(d[2], d[3]);
+  } else if (G == 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (4 * j < m) reinterpret_cast<uint32_t*>(o)[j] = d[j];
+  } else if (G == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (2 * j < m) reinterpret_cast<uint16_t*>(o)[j] = (uint16_t)(d[j >> 1] >> (16 * (j & 1)));
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < m) o[j] = (uint8_t)(d[j >> 2] >> (8 * (j & 3)));
+  }
+}
+
+// r (1..4) bases of the dword w, MSB-first onto code, without the LUT (lines.hip encode_line1's
+// SWAR: A/C/G/T upper case exactly; any other byte sets `bad`, and the row takes the LUT)
+__device__ __forceinline__ void swar_bases(uint32_t w, int r, int kind, uint64_t& code, uint32_t& bad) {
+  const uint32_t x = ((w >> 1) ^ (w >> 2)) & 0x03030303u;
+  const uint32_t v = x ^ ((x >> 1) & 0x01010101u);
+  const uint32_t keep = r >= 4 ? ~0u : (1u << (8 * r)) - 1u;
+  bad |= (__builtin_amdgcn_perm(0u, 0x47544341u, v) ^ w) & keep;  // "ACTG"[v] == the byte?
+  if (kind == 2) {
+    const uint32_t y = __builtin_amdgcn_perm(0u, v, 0x00010203u);
+    const uint32_t a = (y | (y >> 6)) & 0x000F000Fu, pk = (a | (a >> 12)) & 0xFFu;
+    code = (code << (2 * r)) | (pk >> (2 * (4 - r)));
+  } else {
+    const uint32_t y = __builtin_amdgcn_perm(0u, __builtin_amdgcn_perm(0u, 0x03040102u, v), 0x00010203u);
+    const uint32_t a = (y | (y >> 5)) & 0x003F003Fu, pk = (a | (a >> 10)) & 0xFFFu;
+    code = (code << (3 * r)) | (pk >> (3 * (4 - r)));
+  }
+}
+
+// One sequence / quality line's spans (NS > 0: that many, unrolled -- the span table in scalar
+// registers; 0: sp.n in a loop).  The line starts at tile offset `start`, its content is clen bytes,
+// llen with the '\n'.  A whole-width slice inside the content (the usual case) goes 16 bytes at a
+// time from the staged tile (lines crossing the tile end: from global memory) to its row in pieces
+// as wide as the row layout allows, span 0 of a sequence line TwoBit / ThreeBit-encoded from the
+// same registers (SWAR; the LUT only for rows with other bytes); any other slice byte by byte
+// ('\n' past the content, zero padding past the line, as the reference's slice of the line).
+template <int NS>
+__device__ __forceinline__ void line_spans(const Spans& sp, const TileOut& to, bool is_seq, int64_t rec, int start,
+                                           int clen, int llen, lds_u32* tile32, const uint8_t* lut,
+                                           const uint8_t* __restrict__ buf, int64_t n, int64_t t0, int lim_lds) {
+  int32_t* len = is_seq ? to.seq_len : to.qual_len;
+  uint8_t* out = is_seq ? to.seq_out : to.qual_out;
+  const uint32_t* gt = reinterpret_cast<const uint32_t*>(buf + t0);
+  const int64_t lim_g = n - t0;
+  const int nsp = NS ? NS : sp.n;
+#pragma unroll 1
+  for (int k = 0; k < nsp; ++k) {
+    const int s_k = sp.start[k], e_k = sp.end[k], w = e_k - s_k;
+    const int sa = s_k < llen ? s_k : llen, sb = e_k < llen ? e_k : llen;
+    if (len) len[k * to.cap + rec] = sb - sa;
+    if (!out) continue;
+    const bool enc = SCT_FQ_ABL != 3 && k == 0 && is_seq && to.codes0 != nullptr;
+    uint8_t* row0 = out + sp.prefix[k] * to.cap;
+    uint8_t* o = row0 + rec * w;
+    uint64_t code = 0;
+    uint32_t fl = 0;
+    const int s0 = start + sa;                    // the slice's tile offset
+    const int wend = s0 + ((w + 15) & ~15) + 4;   // end of the last 16-byte window's dwords
+    bool lut_row = false;
+    if (sb - sa == w && sb <= clen && w > 0 && w <= 64 && wend <= lim_g) {
+      const bool lds = wend <= lim_lds;
+      const uintptr_t ob = (uintptr_t)row0;
+      const int G = ((w | (int)ob) & 15) == 0 ? 16 : ((w | (int)ob) & 7) == 0 ? 8 : ((w | (int)ob) & 3) == 0 ? 4
+                  : ((w | (int)ob) & 1) == 0 ? 2 : 1;
+      uint32_t bad = 0;
+      for (int c = 0; c < w; c += 16) {
+        const uint4 y = bytes16_at(tile32, gt, s0 + c, lds);
+        const int m = w - c < 16 ? w - c : 16;
+        store_row16(o + c, y, m, G);
+        if (enc) {
+          const uint32_t d[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (4 * j < m) swar_bases(d[j], m - 4 * j < 4 ? m - 4 * j : 4, to.code_kind, code, bad);
+        }
+      }
+      lut_row = enc && bad != 0;
+    } else {
+      const uint8_t* src = buf + t0 + start;
+#pragma unroll 8
+      for (int j = 0; j < w; ++j) {
+        const int i = sa + j;
+        o[j] = i < sb ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
+      }
+      lut_row = enc;
+    }
+    if (lut_row) {  // span 0's row (as written, zero-padded) through the LUT
+      code = 0;
+      const uint8_t* src = buf + t0 + start;
+      for (int j = 0; j < w; ++j) {
+        const int i = sa + j;
+        const uint8_t v = i < sb ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
+        const uint32_t en = lut[v];
+        code = (code << to.code_kind) | (en & 7u);
+        fl |= en;
+      }
+    }
+    if (enc) {
+      to.codes0[rec] = code;
+      if (to.gc0) {
+        const uint32_t g = (uint32_t)__popcll(code & to.gc_mask);
+        to.gc0[rec] = (uint8_t)(g > 255 ? 255 : g);
+      }
+      if (to.flags0) to.flags0[rec] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
+    }
+  }
+}
+
+
 __device__ __forceinline__ void tile_items(lds_u16* term, lds_u8* tile8, lds_u32* tile32, const uint8_t* lut,
                                            int ntile, int tmax, int64_t g0, int64_t t0, uint32_t nf, int head,
                                            const uint8_t* __restrict__ buf, int64_t n, Files fs, int text,
@@ -561,7 +694,12 @@ __device__ __forceinline__ void tile_items(lds_u16* term, lds_u8* tile8, lds_u32
     // quality lines (t = 2 - g0 mod 4), so every wave runs one kind (the CB encode is not carried
     // through the quality lines' waves)
     constexpr int HALF = WG / 2;
-    const bool is_seq = tid < HALF;
+    // wave-uniform, and visibly so (readfirstlane): the row pointers and the store-width branches
+    // of line_spans stay scalar
+    const bool is_seq = __builtin_amdgcn_readfirstlane(tid) < HALF;
+#if SCT_FQ_ABL == 2
+    return;
+#endif
     for (int t = (int)(((is_seq ? 0 : 2) - g0) & 3) + 4 * (tid & (HALF - 1)); t < tmax; t += 4 * HALF) {
       const int64_t line = g0 + t + 1, rec = line >> 2;
       if (rec >= to.cap) continue;
@@ -607,83 +745,8 @@ __device__ __forceinline__ void tile_items(lds_u16* term, lds_u8* tile8, lds_u32
           }
         }
       }
-      int32_t* len = is_seq ? to.seq_len : to.qual_len;
-      uint8_t* out = is_seq ? to.seq_out : to.qual_out;
-      const int64_t clen = cend - start, llen = clen + nl;
-      for (int k = 0; k < sp.n; ++k) {
-        const int64_t sa = sp.start[k] < llen ? sp.start[k] : llen, sb = sp.end[k] < llen ? sp.end[k] : llen;
-        if (len) len[k * to.cap + rec] = (int32_t)(sb - sa);
-        if (!out) continue;
-        const bool enc = k == 0 && is_seq && to.codes0 != nullptr;
-        uint64_t code = 0;
-        uint32_t fl = 0;
-        const int w = sp.end[k] - sp.start[k];
-        uint8_t* o = out + sp.prefix[k] * to.cap + rec * w;
-        const uint8_t* src = buf + t0 + start;
-        // fast path: a whole-width slice inside the line's content, a row of whole dwords:
-        // aligned dword loads + byte-align funnel shifts, dword stores (the code from the same
-        // registers)
-        const int64_t s0 = t0 + start + sa;
-        const int64_t base = s0 & ~3LL;
-        const int nd = w / 4;
-        if (sb - sa == w && sb <= clen && (w & 3) == 0 && w <= 64 && base + 4 * (nd + 1) <= n &&
-            ((uintptr_t)o & 3) == 0) {
-          const bool lds = base + 4 * (nd + 1) <= t0 + TILE;
-          const int lb = (int)((base - t0) >> 2);
-          const uint32_t* gd = reinterpret_cast<const uint32_t*>(buf + base);
-          auto d = [&](int k) { return lds ? tile32[lb + k] : gd[k]; };  // two loads, no pointer select
-          const uint32_t sh = (uint32_t)(s0 & 3);
-          uint32_t* od = reinterpret_cast<uint32_t*>(o);
-          if (nd == 4 && ((uintptr_t)o & 15) == 0) {
-            const uint32_t x0 = d(0), x1 = d(1), x2 = d(2), x3 = d(3), x4 = d(4);
-            const uint4 y = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                                       __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
-            *reinterpret_cast<uint4*>(o) = y;
-            if (enc) {
-              enc_dword(lut, to.code_kind, y.x, code, fl);
-              enc_dword(lut, to.code_kind, y.y, code, fl);
-              enc_dword(lut, to.code_kind, y.z, code, fl);
-              enc_dword(lut, to.code_kind, y.w, code, fl);
-            }
-          } else if (nd == 2 && ((uintptr_t)o & 7) == 0) {
-            const uint32_t x0 = d(0), x1 = d(1), x2 = d(2);
-            const uint2 y = make_uint2(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh));
-            *reinterpret_cast<uint2*>(o) = y;
-            if (enc) {
-              enc_dword(lut, to.code_kind, y.x, code, fl);
-              enc_dword(lut, to.code_kind, y.y, code, fl);
-            }
-          } else {
-            uint32_t lo = d(0);
-            for (int q2 = 0; q2 < nd; ++q2) {
-              const uint32_t hi = d(q2 + 1), y = __builtin_amdgcn_alignbyte(hi, lo, sh);
-              od[q2] = y;
-              if (enc) enc_dword(lut, to.code_kind, y, code, fl);
-              lo = hi;
-            }
-          }
-        } else {
-#pragma unroll 8
-          for (int j = 0; j < w; ++j) {
-            const int64_t i = sa + j;
-            const uint8_t v = i < sb ? (i < clen ? src[i] : (uint8_t)'\n') : (uint8_t)0;
-            o[j] = v;
-            if (enc) {
-              const uint32_t en = lut[v];
-              code = (code << to.code_kind) | (en & 7u);
-              fl |= en;
-            }
-          }
-        }
-        if (enc) {  // span 0's row (as written, zero-padded) -> its code
-          to.codes0[rec] = code;
-          if (to.gc0) {
-            const uint32_t g = (uint32_t)__popcll(code & to.gc_mask);
-            to.gc0[rec] = (uint8_t)(g > 255 ? 255 : g);
-          }
-          if (to.flags0) to.flags0[rec] = (uint8_t)(((fl & F_AMBIG) ? 1u : 0u) | ((fl & F_INVALID) ? 2u : 0u));
-        }
-      }
+      const int clen = (int)(cend - start), llen = clen + nl;  // < 2 TILE + max_end
+      line_spans<0>(sp, to, is_seq, rec, start, clen, llen, tile32, lut, buf, n, t0, TILE + head);
     }
 }
 
@@ -765,6 +828,9 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
     }
     {
       uint32_t bits = tbits, at = pre;
+#if SCT_FQ_ABL == 4
+      bits = 0;
+#endif
       while (bits) {
         const int j = __ffs(bits) - 1;
         bits &= bits - 1;
@@ -775,7 +841,9 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
     }
     __syncthreads();
     const int tmax = (int)(g0 + ntile <= lim_g ? ntile : (lim_g > g0 ? lim_g - g0 : 0));
+#if SCT_FQ_ABL != 1
     tile_items(as_lds16(term), tile8, tile32, lut, (int)ntile, tmax, g0, t0, nf_cur, 0, buf, n, fs, text, sp, to);
+#endif
     g0 += ntile;
     nf_cur = nf_nxt;
   }

@@ -296,9 +296,24 @@ def test_fastq_fused_one_pass_vs_indexed(fq_golden, tmp_path, text_mode, onepass
         _fused_check(fq_golden, tmp_path, text_mode)
 
 
-def _fused_check(fq_golden, tmp_path, text_mode):
+@pytest.mark.gpu
+@pytest.mark.parametrize("onepass", [0, 8])
+def test_fastq_fused_row_layouts(fq_golden, tmp_path, onepass):
+    """The fused extraction with slices of widths 9 / 8 / 12 / 33 (rows stored in 1-, 2-, 4- and
+    8-byte pieces, a slice of three 16-byte windows, a 9-base encode), against the indexed path."""
     from sctools_amd import _lib
-    spans = [(0, 16), (16, 26), (3, 9)]
+    with _lib.tuning(fastq_onepass=onepass):
+        _fused_check(fq_golden, tmp_path, 0, FUSED_SPANS[1])
+
+
+# TenXV2's CB / UMI (16 + 10) and a 6-wide slice; then widths 9 / 8 / 12 / 33 (rows written in 1-,
+# 2-, 4- and 8-byte pieces by the row layout, a slice longer than 32 bytes, a 9-base encode whose
+# last dword is partial)
+FUSED_SPANS = ([(0, 16), (16, 26), (3, 9)], [(1, 10), (0, 8), (2, 14), (0, 33)])
+
+
+def _fused_check(fq_golden, tmp_path, text_mode, spans=FUSED_SPANS[0]):
+    from sctools_amd import _lib
     for name, data, ends in _fused_cases(fq_golden, tmp_path):
         if text_mode and any(b >= 128 for b in data):
             continue
@@ -309,12 +324,13 @@ def _fused_check(fq_golden, tmp_path, text_mode):
             for a, b in zip(ref[k], got[k]):
                 assert np.array_equal(np.asarray(a), np.asarray(b)), (name, k)
         if n0:
-            codes, gc, flags = _lib.encode(2, np.ascontiguousarray(ref[0][0]), 16)
+            w0 = spans[0][1] - spans[0][0]
+            codes, gc, flags = _lib.encode(2, np.ascontiguousarray(ref[0][0]), w0)
             assert np.array_equal(enc[0], codes[:, 0]) and np.array_equal(enc[1], gc), name
             assert np.array_equal(enc[2], flags), name
             # ThreeBit (N kept as 6): the queries of the nearest-whitelist correction
             _, _, _, enc3, _ = _fused(data, ends, spans, text_mode, kind=3)
-            codes3, gc3, flags3 = _lib.encode(3, np.ascontiguousarray(ref[0][0]), 16)
+            codes3, gc3, flags3 = _lib.encode(3, np.ascontiguousarray(ref[0][0]), w0)
             assert np.array_equal(enc3[0], codes3[:, 0]) and np.array_equal(enc3[1], gc3), name
             assert np.array_equal(enc3[2], flags3), name
         # a capacity below the record count: the rows below it are the same
