@@ -579,14 +579,23 @@ __device__ __forceinline__ void store_row16(uint8_t* o, const uint4 y, int m, in
   }
 }
 
-// r (1..4) bases of the dword w, MSB-first onto code, without the LUT (lines.hip encode_line1's
-// SWAR: A/C/G/T upper case exactly; any other byte sets `bad`, and the row takes the LUT)
-__device__ __forceinline__ void swar_bases(uint32_t w, int r, int kind, uint64_t& code, uint32_t& bad) {
+// r (1..4) bases of the dword w, MSB-first onto code: lines.hip encode_line1's SWAR (A/C/G/T upper
+// case exactly), or -- when the dword holds any other byte -- its r bytes through the LUT (flags
+// into fl), from the same register
+__device__ __forceinline__ void enc_bases(uint32_t w, int r, int kind, const uint8_t* lut, uint64_t& code,
+                                          uint32_t& fl) {
   const uint32_t x = ((w >> 1) ^ (w >> 2)) & 0x03030303u;
   const uint32_t v = x ^ ((x >> 1) & 0x01010101u);
   const uint32_t keep = r >= 4 ? ~0u : (1u << (8 * r)) - 1u;
-  bad |= (__builtin_amdgcn_perm(0u, 0x47544341u, v) ^ w) & keep;  // "ACTG"[v] == the byte?
-  if (kind == 2) {
+  if ((__builtin_amdgcn_perm(0u, 0x47544341u, v) ^ w) & keep) {  // "ACTG"[v] != some byte
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (b < r) {
+        const uint32_t e = lut[(w >> (8 * b)) & 0xFFu];
+        code = (code << kind) | (e & 7u);
+        fl |= e;
+      }
+  } else if (kind == 2) {
     const uint32_t y = __builtin_amdgcn_perm(0u, v, 0x00010203u);
     const uint32_t a = (y | (y >> 6)) & 0x000F000Fu, pk = (a | (a >> 12)) & 0xFFu;
     code = (code << (2 * r)) | (pk >> (2 * (4 - r)));
@@ -602,7 +611,7 @@ __device__ __forceinline__ void swar_bases(uint32_t w, int r, int kind, uint64_t
 // llen with the '\n'.  A whole-width slice inside the content (the usual case) goes 16 bytes at a
 // time from the staged tile (lines crossing the tile end: from global memory) to its row in pieces
 // as wide as the row layout allows, span 0 of a sequence line TwoBit / ThreeBit-encoded from the
-// same registers (SWAR; the LUT only for rows with other bytes); any other slice byte by byte
+// same registers (SWAR; the LUT for the dwords holding other bytes); any other slice byte by byte
 // ('\n' past the content, zero padding past the line, as the reference's slice of the line).
 template <int NS>
 __device__ __forceinline__ void line_spans(const Spans& sp, const TileOut& to, bool is_seq, int64_t rec, int start,
@@ -632,7 +641,6 @@ __device__ __forceinline__ void line_spans(const Spans& sp, const TileOut& to, b
       const uintptr_t ob = (uintptr_t)row0;
       const int G = ((w | (int)ob) & 15) == 0 ? 16 : ((w | (int)ob) & 7) == 0 ? 8 : ((w | (int)ob) & 3) == 0 ? 4
                   : ((w | (int)ob) & 1) == 0 ? 2 : 1;
-      uint32_t bad = 0;
       for (int c = 0; c < w; c += 16) {
         const uint4 y = bytes16_at(tile32, gt, s0 + c, lds);
         const int m = w - c < 16 ? w - c : 16;
@@ -641,10 +649,9 @@ __device__ __forceinline__ void line_spans(const Spans& sp, const TileOut& to, b
           const uint32_t d[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (4 * j < m) swar_bases(d[j], m - 4 * j < 4 ? m - 4 * j : 4, to.code_kind, code, bad);
+            if (4 * j < m) enc_bases(d[j], m - 4 * j < 4 ? m - 4 * j : 4, to.code_kind, lut, code, fl);
         }
       }
-      lut_row = enc && bad != 0;
     } else {
       const uint8_t* src = buf + t0 + start;
 #pragma unroll 8
