@@ -95,3 +95,63 @@ def test_newline_count_bits():
         assert [i for i in range(4) if (hi >> (8 * i + 7)) & 1] == [i for i in range(4) if b[i] == 10]
         m4 = (((hi >> 7) * 0x10204080) & 0xFFFFFFFF) >> 28  # lines.hip lf_mask_v's gather
         assert m4 == sum(1 << i for i in range(4) if b[i] == 10)
+
+
+def _lut(kind, c):
+    """encode_common.h lut_entry: code in bits 0..2, 0x40 ambiguous / 0x80 invalid (TwoBit)."""
+    u = chr(c).upper()
+    if kind == 2:
+        if u in "ACTG":
+            return "ACTG".index(u)
+        return 0x40 if u in "MRWSYKVHDBN" else 0x80
+    return {"C": 1, "A": 2, "G": 3, "T": 4}.get(u, 6)
+
+
+def _enc_bases(w, r, kind, code, fl):
+    """fastq.hip enc_bases: r (1..4) bases of the dword w by SWAR, or -- when any of them is not an
+    upper-case base -- its r bytes through the LUT, appended to code."""
+    x = ((w >> 1) ^ (w >> 2)) & 0x03030303
+    v = x ^ ((x >> 1) & 0x01010101)
+    keep = 0xFFFFFFFF if r >= 4 else (1 << (8 * r)) - 1
+    if (perm(0, 0x47544341, v) ^ w) & keep:
+        for b in range(r):
+            e = _lut(kind, (w >> (8 * b)) & 0xFF)
+            code = (code << kind) | (e & 7)
+            fl |= e
+    else:
+        if kind == 2:
+            y = perm(0, v, 0x00010203)
+            a = (y | (y >> 6)) & 0x000F000F
+            pk = (a | (a >> 12)) & 0xFF
+        else:
+            y = perm(0, perm(0, 0x03040102, v), 0x00010203)
+            a = (y | (y >> 5)) & 0x003F003F
+            pk = (a | (a >> 10)) & 0xFFF
+        code = (code << (kind * r)) | (pk >> (kind * (4 - r)))
+    return code & ((1 << 64) - 1), fl
+
+
+def test_fastq_window_encode():
+    """fastq.hip line_spans: a slice of w <= 32 bytes encoded dword by dword from its 16-byte
+    windows (enc_bases: SWAR, the LUT for a dword holding another byte) equals the per-byte LUT
+    encode of the slice, flags included, for every width and mixes of bases, lower case, N, IUPAC
+    and other bytes."""
+    rng = np.random.default_rng(11)
+    alpha = np.frombuffer(b"ACGTACGTACGTacgtNRY\nX", np.uint8)
+    for kind, wmax in ((2, 32), (3, 21)):
+        for w in range(1, wmax + 1):
+            for trial in range(40):
+                row = rng.choice(alpha[:4] if trial % 2 else alpha, w + 16).astype(np.uint8)
+                code, fl = 0, 0
+                for c in range(0, w, 16):
+                    m = min(16, w - c)
+                    for j in range(0, m, 4):
+                        dw = int.from_bytes(bytes(row[c + j:c + j + 4]), "little")
+                        code, fl = _enc_bases(dw, min(4, m - j), kind, code, fl)
+                want, wfl = 0, 0
+                for b in row[:w]:
+                    e = _lut(kind, int(b))
+                    want = (want << kind) | (e & 7)
+                    wfl |= e
+                assert code == want, (kind, w, bytes(row[:w]))
+                assert fl & 0xC0 == wfl & 0xC0, (kind, w, bytes(row[:w]))  # the ambiguous / invalid flags

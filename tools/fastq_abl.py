@@ -14,8 +14,12 @@ if os.environ.get("FQ_CHILD"):
     import bench
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    f = bench.path_fastq(dev, 5, 6300.0)
-    print(json.dumps({"ms": f.get("ms"), "ok": bool(f.get("check", {}).get("sampled"))}))
+    if os.environ.get("FQ_PATH") == "pipeline":  # FASTQ -> ThreeBit -> nearest (bench.path_pipeline)
+        f = bench.path_pipeline(dev, 5, 6300.0, bench.host_threads()[0])
+        print(json.dumps({"ms": f.get("ms"), "extract_ms": f.get("extract_ms"), "ok": f.get("error") is None}))
+    else:
+        f = bench.path_fastq(dev, 5, 6300.0)
+        print(json.dumps({"ms": f.get("ms"), "ok": bool(f.get("check", {}).get("sampled"))}))
     sys.exit(0)
 libs = {"base": None}  # the shipped library, then sctools_amd/libsctools_hip_<arg>.so per argument
 for k in (sys.argv[1:] or ["fqabl1", "fqabl2", "fqabl3", "fqabl4"]):
