@@ -41,7 +41,7 @@ constexpr int TB = TILE / WG;  // bytes per thread
 constexpr int SEG = TB / 16;   // 16-B loads per thread
 
 #ifndef SCT_FQ_ABL
-#define SCT_FQ_ABL 0  // timing-only ablations of fastq_range_kernel (tools/gpu_fastq_abl.sh)
+#define SCT_FQ_ABL 0  // timing-only ablations of the extraction kernels (tools/build_fq_abl.sh)
 #endif
 
 struct Files {
