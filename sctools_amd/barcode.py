@@ -190,7 +190,30 @@ class Barcodes:
     @classmethod
     def from_iterable_bytes(cls, iterable, barcode_length):
         """construct an ObservedBarcodeSet from an iterable of bytes barcodes"""
-        return cls(Counter(_encode_lines([bytes(b) for b in iterable])), barcode_length=barcode_length)
+        seqs = []
+        try:
+            for b in iterable:
+                seqs.append(_item_bytes(b))
+        except Exception:
+            # the reference encodes item by item (barcode.py:114), so the items before the bad one
+            # have made their random draws when its error surfaces
+            _encode_lines(seqs)
+            raise
+        return cls(Counter(_encode_lines(seqs)), barcode_length=barcode_length)
+
+
+def _item_bytes(b):
+    """One from_iterable_bytes item as TwoBit.encode iterates it (encodings.py:85): bytes-like
+    items as they are; any other iterable of byte values through bytes(); a non-iterable raises
+    the reference's TypeError ("'int' object is not iterable"); a str raises the TypeError its
+    characters raise in the byte map (an empty str encodes to 0)."""
+    if isinstance(b, (bytes, bytearray, memoryview)):
+        return bytes(b)
+    if isinstance(b, str):
+        if b:
+            raise TypeError("'str' object cannot be interpreted as an integer")
+        return b""
+    return bytes(iter(b))
 
 
 def _encode_lines(seqs):

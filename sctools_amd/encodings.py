@@ -13,6 +13,7 @@ walked here, in order, drawing exactly the numbers the reference would draw (and
 raising its KeyError at the first invalid byte, after the draws that precede it).
 """
 
+import operator
 import random
 
 import numpy as np
@@ -101,10 +102,90 @@ def _limbs_of(values):
         if values.dtype.kind == "i" and values.size and values.min() < 0:
             raise ValueError("encoded values must be non-negative")
         return np.ascontiguousarray(values.astype(np.uint64, copy=False).reshape(values.shape[0], -1))
-    values = [int(v) for v in values]
+    values = [operator.index(v) for v in values]
     if any(v < 0 for v in values):
         raise ValueError("encoded values must be non-negative")
     return _lib.ints_to_limbs(values)
+
+
+# Negative ints.  The reference's digit loops run on Python's two's-complement ints
+# (``x & 3``, ``x >>= 2`` floor towards -inf), so where a loop ends, a negative input has an
+# answer: TwoBit decode/gc_content read sequence_length digits (the value mod 4**L,
+# encodings.py:97-99, 108-110); hamming_distance counts the digits of a ^ b, which is
+# non-negative when both operands are negative (encodings.py:115-120); ThreeBit.decode
+# reaches the all-ones top (triplet 7, not in its map) and raises KeyError at its lowest
+# 0/5/7 triplet (encodings.py:177-178).  Where a loop never ends -- a negative XOR, a
+# negative ThreeBit gc_content -- the drop-in raises ValueError instead of hanging.
+_HANG_MIXED = ("hamming_distance of a negative and a non-negative code: their XOR is negative and the "
+               "reference's `while difference:` loop (encodings.py:117, 198) never terminates on it")
+_HANG_GC3 = ("ThreeBit.gc_content of a negative code: the reference's `while integer_encoded:` loop "
+             "(encodings.py:189) never terminates on it")
+
+
+def _twos_bits(v):
+    """Bits that hold v in two's complement with its sign (non-negative: bit_length)."""
+    return v.bit_length() if v >= 0 else (~v).bit_length() + 1
+
+
+def _twos_limbs(values, words=None):
+    """ints of any sign -> (n, words) limbs of v mod 2**(64 words): a negative value keeps its
+    all-ones extension up to the top limb, so the XOR of two same-sign operands is exact."""
+    if words is None:
+        words = _lib.words_for_bits(max((_twos_bits(v) for v in values), default=0))
+    m = (1 << (64 * words)) - 1
+    return _lib.ints_to_limbs([v & m for v in values], words)
+
+
+def _codes_mod(values, bits):
+    """TwoBit decode/gc_content operands -> limbs; a negative int is read mod 2**bits."""
+    if isinstance(values, np.ndarray) and values.dtype.kind in "ui":
+        if values.dtype.kind == "i" and values.ndim == 1 and values.size and values.min() < 0:
+            if bits <= 64:  # mod 2**64 keeps every digit the loop reads
+                return values.astype(np.uint64).reshape(-1, 1)
+            values = values.tolist()
+        else:
+            return _limbs_of(values)
+    values = [operator.index(v) for v in values]
+    if any(v < 0 for v in values):
+        m = (1 << max(bits, 0)) - 1
+        values = [v & m for v in values]
+    return _lib.ints_to_limbs(values)
+
+
+def _pair_limbs(a, b):
+    """hamming_distance operands -> equal-width limbs whose XOR is a ^ b per pair."""
+    def flat_ints(x):
+        return (isinstance(x, np.ndarray) and x.dtype.kind in "ui"
+                and (x.ndim == 1 or (x.ndim == 2 and x.shape[1] == 1)))
+    if flat_ints(a) and flat_ints(b):
+        a1, b1 = a.reshape(-1), b.reshape(-1)
+        if a1.shape != b1.shape:
+            raise ValueError("operand shapes differ: %s vs %s" % (a1.shape, b1.shape))
+        na = a1 < 0 if a1.dtype.kind == "i" else np.zeros(a1.shape, bool)
+        nb = b1 < 0 if b1.dtype.kind == "i" else np.zeros(b1.shape, bool)
+        if (na != nb).any():
+            raise ValueError(_HANG_MIXED)
+        # same signs: the XOR of the uint64 views is the (non-negative) XOR of the ints
+        return a1.astype(np.uint64).reshape(-1, 1), b1.astype(np.uint64).reshape(-1, 1)
+    if isinstance(a, np.ndarray) and a.ndim == 2 or isinstance(b, np.ndarray) and b.ndim == 2:
+        la, lb = _limbs_of(a), _limbs_of(b)  # limb arrays: non-negative by construction
+        w = max(la.shape[1], lb.shape[1])
+        return _pad(la, w), _pad(lb, w)
+    a = [operator.index(v) for v in (a.tolist() if isinstance(a, np.ndarray) else a)]
+    b = [operator.index(v) for v in (b.tolist() if isinstance(b, np.ndarray) else b)]
+    if len(a) != len(b):
+        raise ValueError("operand shapes differ: (%d,) vs (%d,)" % (len(a), len(b)))
+    if any((x < 0) != (y < 0) for x, y in zip(a, b)):
+        raise ValueError(_HANG_MIXED)
+    words = _lib.words_for_bits(max((_twos_bits(v) for v in a + b), default=0))
+    return _twos_limbs(a, words), _twos_limbs(b, words)
+
+
+def _three_lift(x):
+    """A negative ThreeBit value -> the non-negative one that decodes to the same KeyError:
+    its triplets up to the first all-ones (7) triplet of the sign extension."""
+    top = -(-(~x).bit_length() // 3)  # first triplet lying wholly in the sign extension
+    return x & ((1 << (3 * (top + 1))) - 1)
 
 
 class Encoding:
@@ -170,19 +251,17 @@ class TwoBit(Encoding):
 
     def decode_array(self, codes):
         """codes -> 'S<L>' array of decoded barcodes (encodings.py:90-100)."""
-        limbs = _limbs_of(codes)
+        limbs = _codes_mod(codes, 2 * self.sequence_length)
         raw = _lib.decode2(limbs, self.sequence_length)
         return raw.view("S%d" % max(1, self.sequence_length)).reshape(-1) if self.sequence_length else \
             np.array([b""] * limbs.shape[0], dtype="S1")
 
     def gc_content_array(self, codes):
-        return _lib.gc_content(2, _limbs_of(codes), self.sequence_length)
+        return _lib.gc_content(2, _codes_mod(codes, 2 * self.sequence_length), self.sequence_length)
 
     @staticmethod
     def hamming_distance_array(a, b):
-        la, lb = _limbs_of(a), _limbs_of(b)
-        w = max(la.shape[1], lb.shape[1])
-        return _lib.hamming_pairs(2, _pad(la, w), _pad(lb, w))
+        return _lib.hamming_pairs(2, *_pair_limbs(a, b))
 
     # ------------------------------------------------------------ reference API
     @classmethod
@@ -204,19 +283,28 @@ class TwoBit(Encoding):
         return _lib.limbs_to_ints(codes)[0]
 
     def decode(self, integer_encoded):
-        """encodings.py:90-100 (batch of one)."""
-        x = int(integer_encoded)
-        if 0 <= x < _U64 and 0 < self.sequence_length <= 64:
-            return _lib.decode2_1(x, self.sequence_length)
-        limbs = _limbs_of([integer_encoded])
-        return _lib.decode2(limbs, self.sequence_length)[0].tobytes()
+        """encodings.py:90-100 (batch of one); a negative int reads mod 4**L there."""
+        x = operator.index(integer_encoded)
+        L = self.sequence_length
+        if L <= 0:  # range(L) is empty
+            return b''
+        if x < 0:
+            x &= (1 << (2 * L)) - 1
+        if x < _U64 and L <= 64:
+            return _lib.decode2_1(x, L)
+        return _lib.decode2(_lib.ints_to_limbs([x]), L)[0].tobytes()
 
     def gc_content(self, integer_encoded):
-        """encodings.py:102-111 (batch of one)."""
-        x = int(integer_encoded)
-        if 0 <= x < _U64:
-            return _lib.gc1(2, x, self.sequence_length)
-        return int(_lib.gc_content(2, _limbs_of([integer_encoded]), self.sequence_length)[0])
+        """encodings.py:102-111 (batch of one); a negative int reads mod 4**L there."""
+        x = operator.index(integer_encoded)
+        L = self.sequence_length
+        if L <= 0:
+            return 0
+        if x < 0:
+            x &= (1 << (2 * L)) - 1
+        if x < _U64:
+            return _lib.gc1(2, x, L)
+        return int(_lib.gc_content(2, _lib.ints_to_limbs([x]), L)[0])
 
     @staticmethod
     def hamming_distance(a, b):
@@ -256,7 +344,12 @@ class ThreeBit(Encoding):
 
     @classmethod
     def decode_array(cls, codes):
-        """codes -> list of bytes; raises KeyError like the reference on a bad triplet."""
+        """codes -> list of bytes; raises KeyError like the reference on a bad triplet
+        (every negative code has one: see _three_lift)."""
+        if not (isinstance(codes, np.ndarray) and (codes.dtype.kind == "u" or codes.ndim == 2
+                                                   or not codes.size or codes.min() >= 0)):
+            codes = [operator.index(v) for v in (codes.tolist() if isinstance(codes, np.ndarray) else codes)]
+            codes = [_three_lift(v) if v < 0 else v for v in codes]
         out, lengths, bad = _lib.decode3(_limbs_of(codes))
         res = []
         w = out.shape[1]
@@ -268,13 +361,15 @@ class ThreeBit(Encoding):
 
     @classmethod
     def gc_content_array(cls, codes):
-        return _lib.gc_content(3, _limbs_of(codes))
+        try:
+            limbs = _limbs_of(codes)
+        except ValueError:
+            raise ValueError(_HANG_GC3) from None
+        return _lib.gc_content(3, limbs)
 
     @staticmethod
     def hamming_distance_array(a, b):
-        la, lb = _limbs_of(a), _limbs_of(b)
-        w = max(la.shape[1], lb.shape[1])
-        return _lib.hamming_pairs(3, _pad(la, w), _pad(lb, w))
+        return _lib.hamming_pairs(3, *_pair_limbs(a, b))
 
     # ------------------------------------------------------------ reference API
     @classmethod
@@ -299,10 +394,12 @@ class ThreeBit(Encoding):
     @classmethod
     def gc_content(cls, integer_encoded):
         """encodings.py:182-192 (batch of one)."""
-        x = int(integer_encoded)
-        if 0 <= x < _U64:
+        x = operator.index(integer_encoded)
+        if x < 0:
+            raise ValueError(_HANG_GC3)
+        if x < _U64:
             return _lib.gc1(3, x)
-        return int(_lib.gc_content(3, _limbs_of([integer_encoded]))[0])
+        return int(_lib.gc_content(3, _lib.ints_to_limbs([x]))[0])
 
     @staticmethod
     def hamming_distance(a, b):
@@ -319,12 +416,13 @@ def _pad(limbs, words):
 
 
 def _hamming1(kind, a, b):
-    a, b = int(a), int(b)
+    a, b = operator.index(a), operator.index(b)
     if 0 <= a < _U64 and 0 <= b < _U64:
         return _lib.hamming1(kind, a, b)
-    if a < 0 or b < 0:
-        raise ValueError("encoded values must be non-negative")
-    words = _lib.words_for_bits(max(a.bit_length(), b.bit_length()))
-    la = _lib.ints_to_limbs([a], words)
-    lb = _lib.ints_to_limbs([b], words)
+    if (a < 0) != (b < 0):
+        raise ValueError(_HANG_MIXED)
+    words = _lib.words_for_bits(max(_twos_bits(a), _twos_bits(b)))
+    if words == 1:  # both negative within int64: the uint64 views XOR to a ^ b
+        return _lib.hamming1(kind, a & (_U64 - 1), b & (_U64 - 1))
+    la, lb = _twos_limbs([a], words), _twos_limbs([b], words)
     return int(_lib.hamming_pairs(kind, la, lb)[0])

@@ -32,6 +32,12 @@ def golden_10k():
 
 
 @pytest.fixture(scope="session")
+def golden_edges():
+    with open(os.path.join(GOLDEN_DIR, "edges.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
 def golden_wide():
     with open(os.path.join(GOLDEN_DIR, "wide_sets.json")) as f:
         return json.load(f)

@@ -125,6 +125,78 @@ def test_hamming_golden(golden):
     assert ThreeBit.hamming_distance_array(la, lb).tolist() == [r[3] for r in rows]
 
 
+def test_negative_ints_golden(golden_edges):
+    """negative ints where the reference's loops end (edges.json,
+    generated from the reference), scalar and batch; ValueError where they never end."""
+    by_L = {}
+    for rec in golden_edges["twobit_negative"]:
+        t, x = TwoBit(rec["L"]), int(rec["code"])
+        assert t.decode(x).hex() == rec["decode"]["bytes"], rec
+        assert t.gc_content(x) == int(rec["gc"]["value"]), rec
+        by_L.setdefault(rec["L"], []).append(rec)
+    for L, recs in by_L.items():
+        if L == 0:
+            continue
+        t = TwoBit(L)
+        xs = [int(r["code"]) for r in recs]
+        assert [bytes(v).hex() for v in t.decode_array(xs)] == [r["decode"]["bytes"] for r in recs]
+        assert t.gc_content_array(xs).tolist() == [int(r["gc"]["value"]) for r in recs]
+        small = [x for x in xs if x >= -(2 ** 63)]
+        want = [r for r in recs if int(r["code"]) >= -(2 ** 63)]
+        arr = np.array(small, dtype=np.int64)
+        assert [bytes(v).hex() for v in t.decode_array(arr)] == [r["decode"]["bytes"] for r in want]
+        assert t.gc_content_array(arr).tolist() == [int(r["gc"]["value"]) for r in want]
+    rows = golden_edges["hamming_negative"]
+    for a, b, d2, d3 in rows:
+        assert TwoBit.hamming_distance(int(a), int(b)) == d2, (a, b)
+        assert ThreeBit.hamming_distance(int(a), int(b)) == d3, (a, b)
+    a = [int(r[0]) for r in rows]
+    b = [int(r[1]) for r in rows]
+    assert TwoBit.hamming_distance_array(a, b).tolist() == [r[2] for r in rows]
+    assert ThreeBit.hamming_distance_array(a, b).tolist() == [r[3] for r in rows]
+    i64 = [k for k, (x, y) in enumerate(zip(a, b)) if min(x, y) >= -(2 ** 63)]
+    aa = np.array([a[k] for k in i64], dtype=np.int64)
+    bb = np.array([b[k] for k in i64], dtype=np.int64)
+    assert TwoBit.hamming_distance_array(aa, bb).tolist() == [rows[k][2] for k in i64]
+    assert ThreeBit.hamming_distance_array(aa, bb).tolist() == [rows[k][3] for k in i64]
+    for rec in golden_edges["threebit_decode_negative"]:
+        with pytest.raises(KeyError) as ei:
+            ThreeBit.decode(int(rec["code"]))
+        assert list(ei.value.args) == rec["decode"]["error"]["args"], rec
+    # where the reference never returns: ValueError, not a hang and not a made-up value
+    for x, y in golden_edges["hangs"]["hamming_mixed_signs"]:
+        for enc in (TwoBit, ThreeBit):
+            with pytest.raises(ValueError):
+                enc.hamming_distance(int(x), int(y))
+            with pytest.raises(ValueError):
+                enc.hamming_distance_array([int(x)], [int(y)])
+    with pytest.raises(ValueError):
+        TwoBit.hamming_distance_array(np.array([-1, 2], np.int64), np.array([-3, -4], np.int64))
+    for x in golden_edges["hangs"]["threebit_gc_negative"]:
+        with pytest.raises(ValueError):
+            ThreeBit.gc_content(int(x))
+    with pytest.raises(TypeError):
+        TwoBit(4).decode(1.5)  # `1.5 & 3` is a TypeError there
+
+
+def test_from_iterable_bytes_items_golden(golden_edges):
+    """barcode.py:111-114 on non-bytes items: the reference's TypeError, or its codes."""
+    items = {
+        "ints": [5, 6], "int_after_bytes": [b"ACGT", 7], "str": ["ACGT"], "empty_str": [""],
+        "list_of_ints": [[65, 67, 71, 84], [84, 84, 65, 65]],
+        "bytearray": [bytearray(b"ACGT"), memoryview(b"TTGA")], "tuple_of_ints": [(65, 67)],
+        "none": [None], "float": [1.5]}
+    for rec in golden_edges["from_iterable_bytes"]:
+        its = items[rec["name"]]
+        if "error" in rec:
+            with pytest.raises(TypeError) as ei:
+                barcode.Barcodes.from_iterable_bytes(its, rec["L"])
+            assert list(ei.value.args) == rec["error"]["args"], rec
+        else:
+            s = barcode.Barcodes.from_iterable_bytes(its, rec["L"])
+            assert [str(k) for k in s] == rec["codes"] and [s[k] for k in s] == rec["counts"]
+
+
 def test_reference_simple_barcodes(golden):
     sb = golden["simple_barcodes"]
     seqs = [bytes.fromhex(s) for s in sb["seqs"]]

@@ -125,6 +125,52 @@ def test_nearest_bruteforce(golden):
             assert dist.tolist() == want["dist"]
 
 
+def test_c_hist16_pinned(golden, golden_10k):
+    """The AVX-512 checker of every full-size all-pairs parity test (config 2, 4, 5, the
+    multisets) against the reference's own histograms: whole sets, row ranges, threads."""
+    wl = golden["whitelist_1k"]
+    codes = np.array([int(c) for c in wl["codes"]], dtype=np.uint64)
+    hist, _ = O.c_hist16(codes)
+    assert hist[:17].tolist() == wl["hist"] and not hist[17:].any()
+    parts = sum(O.c_hist16(codes, b, e, threads=t)[0] for b, e, t in ((0, 1, 1), (1, 333, 2), (333, 1000, 0)))
+    assert parts[:17].tolist() == wl["hist"]
+    c10 = synthetic.whitelist_codes(golden_10k["n"], golden_10k["L"], golden_10k["seed"])
+    hist, simd = O.c_hist16(c10)
+    assert hist[:17].tolist() == golden_10k["hist"] and not hist[17:].any()
+    # duplicates (the multiset tests): d = 0 pairs against the scalar restatement
+    dup = np.concatenate([c10[:3000], c10[:500], c10[:1]])
+    assert O.c_hist16(dup)[0].tolist() == O.c_hist_rows(dup, scalar=True).tolist()
+
+
+def test_c_nearest_pinned(golden):
+    """The OpenMP checker of the config-4 / FASTQ nearest tests against the reference's own
+    distances (golden["nearest"], composed from TwoBit/ThreeBit.hamming_distance)."""
+    for name, kind in (("three", 3), ("two", 2)):
+        rec = golden["nearest"][name]
+        wl = np.array([int(c) for c in rec["whitelist"]], dtype=np.uint64)
+        q = np.array([int(c) for c in rec["queries"]], dtype=np.uint64)
+        for md, want in rec["result"].items():
+            for threads in (1, 0):
+                idx, dist = O.c_nearest(kind, wl, q, int(md), threads=threads)
+                assert idx.tolist() == want["index"]
+                assert dist.tolist() == want["dist"]
+
+
+def test_negative_ints_oracle(golden_edges):
+    """The oracle's digit loops on negative ints against the reference's (edges.json)."""
+    for rec in golden_edges["twobit_negative"]:
+        x, L = int(rec["code"]), rec["L"]
+        assert O.two_bit_decode(x, L).hex() == rec["decode"]["bytes"]
+        assert O.two_bit_gc(x, L) == int(rec["gc"]["value"])
+    for a, b, d2, d3 in golden_edges["hamming_negative"]:
+        assert O.two_bit_hamming(int(a), int(b)) == d2
+        assert O.three_bit_hamming(int(a), int(b)) == d3
+    for rec in golden_edges["threebit_decode_negative"]:
+        with pytest.raises(KeyError) as ei:
+            O.three_bit_decode(int(rec["code"]))
+        assert list(ei.value.args) == rec["decode"]["error"]["args"]
+
+
 def test_from_whitelist_semantics_oracle(golden):
     from collections import Counter
     for rec in golden["from_whitelist"]:
