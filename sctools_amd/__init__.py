@@ -10,4 +10,16 @@ Unlike the reference's ``__init__`` this package does not import pysam.
 
 from . import encodings, barcode, stats  # noqa: F401
 
+
+def release_device_memory():
+    """Free the device workspace that all-pairs summaries keep cached between calls.
+
+    ``Barcodes.summarize_hamming_distances`` on a large set (SPECTRAL) keeps its
+    per-device workspace -- up to 4 GiB of transform intermediate -- so the next call maps nothing.
+    A process that shares the GPU with another framework can hand that memory back here; the next
+    summary call allocates it again (process exit frees it as well)."""
+    from . import _lib
+    if _lib._lib is not None:  # nothing to free before the library was loaded
+        _lib.release_plan_cache()
+
 __version__ = "0.1.0"

@@ -131,7 +131,10 @@ class Barcodes:
 
     def summarize_hamming_distances(self):
         """returns descriptive statistics on hamming distances between pairs of barcodes
-        (barcode.py:39-46)."""
+        (barcode.py:39-46).
+
+        Large sets keep a per-device workspace cached for the next call (up to 4 GiB on the GPU
+        for >= 325K 16-bp codes); ``sctools_amd.release_device_memory()`` hands it back."""
         hist = self.hamming_histogram()
         values = _lib.summary_from_hist(hist)  # IndexError for < 2 barcodes, as numpy raises
         return dict(zip(_SUMMARY_KEYS, [np.float64(v) for v in values]))

@@ -856,210 +856,6 @@ __global__ __launch_bounds__(WG) void fastq_range_kernel(
   }
 }
 
-// ---------------------------------------------------------------- one pass (round 4)
-// fastq_onepass_kernel<RT>: every byte read once.  A workgroup takes a ticket (ranges are taken
-// in ticket order, so a range only ever waits on ranges whose workgroups are already running),
-// loads its range of RT tiles into registers (RT x 32 bytes per thread), counts the range's
-// terminators and publishes that count, then looks back over its predecessors' published words
-// -- all 256 threads at once, one predecessor each -- until one holds an inclusive prefix, and
-// publishes its own inclusive prefix (one 64-bit word: flag in bits 62-63, count below).  Then
-// the range's tiles are worked from the registers as fastq_range_kernel works them, the next
-// tile's first 64 bytes staged in LDS after each tile for its last line's end.  The line total
-// is known only at the last range, so rows are written for every record < cap (those of an
-// incomplete trailing record are not meaningful) and fastq_onepass_finish_kernel drops a first
-// bad name that lies beyond the complete records.
-constexpr unsigned long long kAgg = 1ull << 62, kIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
-
-// HOLD: the range stays in registers from the count to the extraction (RT x 8 VGPRs); else the
-// extraction reads the tiles again -- from L2, where the count just brought them (the range is
-// RT x 8 KiB per workgroup) -- with the next tile's loads in flight, as fastq_range_kernel
-template <int RT, bool HOLD>
-__global__ __launch_bounds__(WG) void fastq_onepass_kernel(const uint8_t* __restrict__ buf, int64_t n, Files fs,
-                                                           int text, int64_t ntiles, int64_t nranges,
-                                                           unsigned long long* __restrict__ rstat,
-                                                           unsigned* __restrict__ ctr, Spans sp, TileOut to) {
-  __shared__ uint16_t term[MAX_TERM];
-  __shared__ uint4 tile_bytes[TILE / 16 + 4];  // the tile, then the next tile's first 64 bytes
-  __shared__ uint32_t w_cnt[WG / 64];
-  __shared__ unsigned long long w_sum[WG / 64];
-  __shared__ int w_first[WG / 64];
-  __shared__ int64_t s_r;
-  __shared__ uint8_t lut[256];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_r = (int64_t)atomicAdd(ctr, 1u);
-  if (to.codes0)
-    for (int c = tid; c < 256; c += WG) lut[c] = lut_entry(to.code_kind, c);
-  __syncthreads();
-  const int64_t r = s_r, tile0 = r * RT;
-  // the range's bytes (thread tid: bytes tid * 32 .. + 31 of each tile) and, for threads 0 and 1,
-  // the next range's first 64 bytes; without HOLD the count loads PB tiles at a time
-  constexpr int PB = HOLD ? RT : (RT < 4 ? RT : 4);
-  uint4 cur[PB + 1][SEG];
-  uint32_t c = 0, na = 0;
-  FileCursor fc1;
-#pragma unroll 1
-  for (int b0 = 0; b0 < RT; b0 += PB) {
-#pragma unroll
-    for (int i = 0; i < PB; ++i)
-#pragma unroll
-      for (int k = 0; k < SEG; ++k)
-        cur[i][k] = tile0 + b0 + i < ntiles ? load16(buf, n, (tile0 + b0 + i) * TILE + (int64_t)tid * TB + 16 * k)
-                                            : make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int k = 0; k < SEG; ++k)
-      cur[PB][k] = HOLD && tid < 2 && tile0 + RT < ntiles
-                       ? load16(buf, n, (tile0 + RT) * TILE + (int64_t)tid * TB + 16 * k)
-                       : make_uint4(0, 0, 0, 0);
-    // phase 1: the range's terminator count
-#pragma unroll
-    for (int i = 0; i < PB; ++i) {
-      if (tile0 + b0 + i >= ntiles) break;
-      const int64_t t0 = (tile0 + b0 + i) * TILE, p0 = t0 + (int64_t)tid * TB;
-      const bool ends_here = fc1.advance(fs, t0);
-      if (!text && !ends_here && p0 + TB <= n) {
-#pragma unroll
-        for (int k = 0; k < SEG; ++k) {
-          const uint32_t w[4] = {cur[i][k].x, cur[i][k].y, cur[i][k].z, cur[i][k].w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) c += __popc(eq_bytes(w[q], 0x0A0A0A0Au));
-          na |= (w[0] | w[1] | w[2] | w[3]) & 0x80808080u;
-        }
-      } else if (p0 < n) {
-        const Span spn = thread_span(buf, n, fs, text, p0, cur[i], ends_here);
-        c += __popc(spn.m | spn.vbits);
-        na |= spn.na;
-      }
-    }
-  }
-  if (na) atomicOr(reinterpret_cast<unsigned*>(to.d_status + 2), 1u);
-  unsigned long long agg = c;
-#pragma unroll
-  for (int o = 32; o; o >>= 1) agg += __shfl_xor(agg, o);
-  if (lane == 0) w_sum[wave] = agg;
-  __syncthreads();
-  agg = 0;
-#pragma unroll
-  for (int w = 0; w < WG / 64; ++w) agg += w_sum[w];
-  if (tid == 0) __hip_atomic_store(rstat + r, kAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // look-back: thread t reads predecessor base - t; the nearest inclusive one ends the walk
-  unsigned long long excl = 0;
-  for (int64_t base = r - 1;; base -= WG) {
-    const int64_t idx = base - tid;
-    unsigned long long v = kIncl;  // before range 0: an inclusive prefix of 0
-    if (idx >= 0) {
-      v = __hip_atomic_load(rstat + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // a running predecessor publishes its count without waiting on anything; the bound only
-      // guarantees an exit
-      for (int spin = 0; (v >> 62) == 0 && spin < (1 << 22); ++spin) {
-        __builtin_amdgcn_s_sleep(1);
-        v = __hip_atomic_load(rstat + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    const bool incl = (v >> 62) == 2;
-    const unsigned long long bal = __ballot(incl);
-    const int wfirst = bal ? __builtin_ctzll(bal) : 64;
-    __syncthreads();  // the previous round's readers of w_first / w_sum are done
-    if (lane == 0) w_first[wave] = wfirst;
-    __syncthreads();
-    int first = WG;  // the lowest thread (nearest predecessor) holding an inclusive prefix
-#pragma unroll
-    for (int w = 0; w < WG / 64; ++w)
-      if (first == WG && w_first[w] < 64) first = 64 * w + w_first[w];
-    unsigned long long part = tid <= first ? (v & kValMask) : 0ull;
-#pragma unroll
-    for (int o = 32; o; o >>= 1) part += __shfl_xor(part, o);
-    if (lane == 0) w_sum[wave] = part;
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < WG / 64; ++w) excl += w_sum[w];
-    if (first < WG) break;
-  }
-  if (tid == 0) {
-    __hip_atomic_store(rstat + r, kIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (r == nranges - 1) atomicMax(to.d_status, excl + agg);  // the line total
-    if (r == 0 && n > 0 && buf[0] != '@') atomicMax(to.d_status + 1, ~0ull);  // record 0's name line
-  }
-  // phase 2: the tiles from the registers (rotated down one tile per step)
-  lds_u8* tile8 = as_lds8(tile_bytes);
-  lds_u32* tile32 = as_lds32(tile_bytes);
-  int64_t g0 = (int64_t)excl;
-  FileCursor fc;
-  uint4 ca[SEG], cb[SEG];  // (!HOLD) this tile's bytes and the next tile's
-  if (!HOLD) {
-#pragma unroll
-    for (int k = 0; k < SEG; ++k) ca[k] = load16(buf, n, tile0 * TILE + (int64_t)tid * TB + 16 * k);
-  }
-#pragma unroll 1
-  for (int i = 0; i < RT; ++i) {
-    const int64_t tile = tile0 + i;
-    if (tile >= ntiles) break;
-    const int64_t t0 = tile * TILE, p0 = t0 + (int64_t)tid * TB;
-    if (!HOLD) {  // the next tile (all threads) or, after the range's last, the next range's head
-      const bool all = i + 1 < RT, need = tile + 1 < ntiles && (all || tid < 2);
-#pragma unroll
-      for (int k = 0; k < SEG; ++k)
-        cb[k] = need ? load16(buf, n, t0 + TILE + (int64_t)tid * TB + 16 * k) : make_uint4(0, 0, 0, 0);
-    }
-    const uint4* a0 = HOLD ? cur[0] : ca;
-    const uint4* a1 = HOLD ? cur[1] : cb;
-    const bool ends_here = fc.advance(fs, t0);
-    Span spn{0, 0, 0, 0};
-    if (p0 < n) spn = thread_span(buf, n, fs, text, p0, a0, ends_here);
-    __syncthreads();  // the previous tile's readers of tile_bytes / term are done
-#pragma unroll
-    for (int k = 0; k < SEG; ++k) {
-      tile_bytes[tid * SEG + k] = p0 + 16 * k < n ? a0[k] : make_uint4(0, 0, 0, 0);
-      if (tid < 2) tile_bytes[TILE / 16 + tid * SEG + k] = a1[k];  // the next tile's head
-    }
-    if (HOLD) {
-#pragma unroll
-      for (int j = 0; j < PB; ++j)
-#pragma unroll
-        for (int k = 0; k < SEG; ++k) cur[j][k] = cur[j + 1][k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < SEG; ++k) ca[k] = cb[k];
-    }
-    const uint32_t tbits = spn.m | spn.vbits, cc = __popc(tbits);
-    uint32_t ic = cc;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t x = __shfl_up(ic, d);
-      if (lane >= d) ic += x;
-    }
-    if (lane == 63) w_cnt[wave] = ic;
-    __syncthreads();
-    uint32_t pre = ic - cc, ntile = 0;
-#pragma unroll
-    for (int w = 0; w < WG / 64; ++w) {
-      if (w < wave) pre += w_cnt[w];
-      ntile += w_cnt[w];
-    }
-    {
-      uint32_t bits = tbits, at = pre;
-      while (bits) {
-        const int j = __ffs(bits) - 1;
-        bits &= bits - 1;
-        const uint32_t off = (uint32_t)(tid * TB + j);
-        term[at++] = (spn.m >> j & 1u) ? (uint16_t)(off | ((spn.crlf >> j & 1u) ? T16_CRLF : 0u))
-                                       : (uint16_t)((off + 1) | T16_VIRT);  // the file ends after byte off
-      }
-    }
-    __syncthreads();
-    // every record < cap is written (the total is not known yet); the caller reads lines / 4
-    tile_items(as_lds16(term), tile8, tile32, lut, (int)ntile, (int)ntile, g0, t0, ~0u, 64, buf, n, fs, text, sp,
-               to);
-    g0 += ntile;
-  }
-}
-
-// after fastq_onepass_kernel: a first bad name beyond the complete records is none (a kernel of
-// one thread: a completion counter in the pass cost one same-address atomic per range)
-__global__ void fastq_onepass_finish_kernel(unsigned long long* __restrict__ d_status) {
-  const unsigned long long total = d_status[0], bad = d_status[1];
-  if (bad && ~bad >= (total >> 2)) d_status[1] = 0ull;
-}
-
 // grid of the persistent tile kernels: every resident workgroup slot once (at most ntiles)
 unsigned resident_grid(const void* kernel, int64_t ntiles) {
   sct::scalar_quiesce();
@@ -1322,41 +1118,9 @@ extern "C" int sct_fastq_extract_fused(const uint8_t* d_buf, int64_t nbytes, con
   SCT_HIP(hipMemsetAsync(d_status, 0, 24, s));
   if (nbytes == 0) return SCT_OK;
   const int64_t ntiles = sct::ceil_div(nbytes, TILE);
-  SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
-  const TileOut to{d_seq, d_qual, d_seq_len, d_qual_len, d_codes0, d_gc0, d_flags0, code_kind,
-                   code_kind == 2 ? 0x5555555555555555ull : 0x9249249249249249ull, cap_records,
-                   reinterpret_cast<unsigned long long*>(d_status)};
-  // SCT_TUNE_FASTQ_ONEPASS: 4 or 8 = one pass over ranges of that many tiles, 0 = count pass first
-  const int64_t onepass = sct::tune(SCT_TUNE_FASTQ_ONEPASS, 0);
-  const bool hold = onepass < 100;
-  const int RT = (int)(hold ? onepass : onepass - 100);
-  if ((hold && (RT == 2 || RT == 4 || RT == 8)) || (!hold && (RT == 4 || RT == 8 || RT == 16 || RT == 32))) {
-    const int64_t nranges = sct::ceil_div(ntiles, RT);
-    SCT_CHECK(nranges < (1LL << 31), "buffer too large");
-    void* scr = nullptr;
-    const size_t rbytes = (size_t)nranges * 8 + 16;
-    SCT_HIP(sct::pool_alloc(&scr, rbytes, s));
-    hipError_t e1 = hipMemsetAsync(scr, 0, rbytes, s);
-    if (e1 == hipSuccess) {
-      auto* rstat = reinterpret_cast<unsigned long long*>(scr);
-      auto* ctr = reinterpret_cast<unsigned*>(rstat + nranges);
-      const Files fs{d_file_ends, nfiles};
-      auto kern = hold ? (RT == 2 ? fastq_onepass_kernel<2, true> : RT == 4 ? fastq_onepass_kernel<4, true>
-                                                                             : fastq_onepass_kernel<8, true>)
-                       : (RT == 4    ? fastq_onepass_kernel<4, false>
-                          : RT == 8  ? fastq_onepass_kernel<8, false>
-                          : RT == 16 ? fastq_onepass_kernel<16, false>
-                                     : fastq_onepass_kernel<32, false>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)nranges), dim3(WG), 0, s, d_buf, nbytes, fs, text_mode ? 1 : 0, ntiles,
-                         nranges, rstat, ctr, sp, to);
-      hipLaunchKernelGGL(fastq_onepass_finish_kernel, dim3(1), dim3(1), 0, s,
-                         reinterpret_cast<unsigned long long*>(d_status));
-      e1 = hipGetLastError();
-    }
-    sct::pool_free(scr, s);
-    if (e1 != hipSuccess) return sct::fail(SCT_E_HIP, "fastq one pass: %s", hipGetErrorString(e1));
-    return SCT_OK;
-  }
+  // fq_count_kernel runs one workgroup per tile and a launch holds < 2^32 threads
+  SCT_CHECK(ntiles * WG < (1LL << 32), "buffer too large: %lld bytes (one launch covers < %lld bytes; pass the "
+            "files in pieces, sct_fastq_stream_*)", (long long)nbytes, (long long)(((1LL << 32) / WG) * TILE));
   void* scratch = nullptr;
   const size_t sbytes = sct::tile_sums_bytes(ntiles), fbytes = (size_t)ntiles * 4;
   SCT_HIP(sct::pool_alloc(&scratch, sbytes + fbytes, s));

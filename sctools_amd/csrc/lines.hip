@@ -626,7 +626,9 @@ extern "C" int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines
   if (nbytes == 0) return SCT_OK;
   hipStream_t s = sct::as_stream(stream);
   const int64_t ntiles = sct::ceil_div(nbytes, TILE);
-  SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
+  // line_count_kernel: one workgroup per tile, < 2^32 threads per launch
+  SCT_CHECK(ntiles * WG < (1LL << 32), "buffer too large: %lld bytes (one launch covers < %lld)", (long long)nbytes,
+            (long long)(((1LL << 32) / WG) * TILE));
   size_t tb = 0;
   SCT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                            (int)(ntiles + 1), s));
@@ -686,7 +688,9 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
     return SCT_OK;
   }
   const int64_t ntiles = sct::ceil_div(nbytes, WTILE);
-  SCT_CHECK(ntiles < (1LL << 31), "buffer too large");
+  // wl_count_kernel: one workgroup per tile, < 2^32 threads per launch
+  SCT_CHECK(ntiles * WG < (1LL << 32), "buffer too large: %lld bytes (one launch covers < %lld)", (long long)nbytes,
+            (long long)(((1LL << 32) / WG) * WTILE));
   StreamBuf scratch;
   SCT_HIP(scratch.alloc(sct::tile_sums_bytes(ntiles, true), s));
   const sct::TileSums ts = sct::tile_sums_at(scratch.p, ntiles, true, true);

@@ -234,13 +234,14 @@ def _fused(data, ends, spans, text_mode, cap=None, encode=True, kind=2):
     cap = max(1, n // 6 + 2) if cap is None else cap
     widths = [e - s for s, e in spans]
     W = sum(widths)
-    seq = torch.zeros(max(1, cap * W), dtype=torch.uint8, device="cuda")
-    qual = torch.zeros_like(seq)
-    slen = torch.full((max(1, cap * len(spans)),), -9, dtype=torch.int32, device="cuda")
+    G = 64  # guard rows past the capacity: nothing may be written there
+    seq = torch.full((max(1, (cap + G) * W),), 0xEE, dtype=torch.uint8, device="cuda")
+    qual = torch.full_like(seq, 0xEE)
+    slen = torch.full((max(1, (cap + G) * len(spans)),), -9, dtype=torch.int32, device="cuda")
     qlen = torch.full_like(slen, -9)
-    codes = torch.zeros(cap, dtype=torch.int64, device="cuda")
-    gc = torch.zeros(cap, dtype=torch.uint8, device="cuda")
-    fl = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    codes = torch.full((cap + G,), -7, dtype=torch.int64, device="cuda")
+    gc = torch.full((cap + G,), 0xEE, dtype=torch.uint8, device="cuda")
+    fl = torch.full((cap + G,), 0xEE, dtype=torch.uint8, device="cuda")
     status = torch.full((3,), 77, dtype=torch.int64, device="cuda")
     sp = np.ascontiguousarray(np.array(spans, dtype=np.int32).reshape(-1, 2))
     _lib.check(_lib.lib().sct_fastq_extract_fused(
@@ -251,8 +252,10 @@ def _fused(data, ends, spans, text_mode, cap=None, encode=True, kind=2):
     torch.cuda.synchronize()
     st = status.cpu().numpy().view(np.uint64)
     nrec = int(st[0]) // 4
-    bad = int(~st[1] & np.uint64(0xFFFFFFFFFFFFFFFF)) if int(st[1]) else -1
-    bad = bad if 0 <= bad < nrec else -1
+    bad = int(~st[1] & np.uint64(0xFFFFFFFFFFFFFFFF)) if int(st[1]) else -1  # raw: no trimming here
+    for buf_, fill in ((seq[cap * W:], 0xEE), (qual[cap * W:], 0xEE), (slen[cap * len(spans):], -9),
+                       (qlen[cap * len(spans):], -9), (codes[cap:], -7), (gc[cap:], 0xEE), (fl[cap:], 0xEE)):
+        assert bool((buf_ == fill).all()), "a row at or past the capacity was written"
     out, off = [], 0
     s_h, q_h = seq.cpu().numpy(), qual.cpu().numpy()
     sl_h, ql_h = slen.cpu().numpy(), qlen.cpu().numpy()
@@ -284,26 +287,21 @@ def _fused_cases(fq_golden, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("onepass", [0, 4, 8, 108, 132])
 @pytest.mark.parametrize("text_mode", [0, 1])
-def test_fastq_fused_one_pass_vs_indexed(fq_golden, tmp_path, text_mode, onepass):
+def test_fastq_fused_vs_indexed(fq_golden, tmp_path, text_mode):
     """sct_fastq_extract_fused (no index, no scan launch, no host synchronisation; VERDICT r3
-    #6; onepass 4 / 8: every byte read once, a look-back over ranges of that many tiles) against the indexed two-pass path (itself pinned to the reference's golden outputs
-    above): record count, first bad name, every span's sequence / quality rows and lengths, and
-    the in-kernel TwoBit and ThreeBit encodes of span 0's rows against sct_encode of the same rows."""
-    from sctools_amd import _lib
-    with _lib.tuning(fastq_onepass=onepass):
-        _fused_check(fq_golden, tmp_path, text_mode)
+    #6) against the indexed two-pass path (itself pinned to the reference's golden outputs
+    above): record count, first bad name (the raw status word), every span's sequence / quality
+    rows and lengths, and the in-kernel TwoBit and ThreeBit encodes of span 0's rows against
+    sct_encode of the same rows."""
+    _fused_check(fq_golden, tmp_path, text_mode)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("onepass", [0, 8])
-def test_fastq_fused_row_layouts(fq_golden, tmp_path, onepass):
+def test_fastq_fused_row_layouts(fq_golden, tmp_path):
     """The fused extraction with slices of widths 9 / 8 / 12 / 33 (rows stored in 1-, 2-, 4- and
     8-byte pieces, a slice of three 16-byte windows, a 9-base encode), against the indexed path."""
-    from sctools_amd import _lib
-    with _lib.tuning(fastq_onepass=onepass):
-        _fused_check(fq_golden, tmp_path, 0, FUSED_SPANS[1])
+    _fused_check(fq_golden, tmp_path, 0, FUSED_SPANS[1])
 
 
 # TenXV2's CB / UMI (16 + 10) and a 6-wide slice; then widths 9 / 8 / 12 / 33 (rows written in 1-,

@@ -17,11 +17,6 @@ if os.environ.get("FQ_CHILD"):
     if os.environ.get("FQ_PATH") == "pipeline":  # FASTQ -> ThreeBit -> nearest (bench.path_pipeline)
         f = bench.path_pipeline(dev, 5, 6300.0, bench.host_threads()[0])
         print(json.dumps({"ms": f.get("ms"), "extract_ms": f.get("extract_ms"), "ok": f.get("error") is None}))
-    elif os.environ.get("FQ_ONEPASS"):  # the one-pass form (SCT_TUNE_FASTQ_ONEPASS)
-        from sctools_amd import _lib
-        with _lib.tuning(fastq_onepass=int(os.environ["FQ_ONEPASS"])):
-            f = bench.path_fastq(dev, 5, 6300.0)
-        print(json.dumps({"ms": f.get("ms"), "ok": bool(f.get("check", {}).get("sampled"))}))
     else:
         f = bench.path_fastq(dev, 5, 6300.0)
         print(json.dumps({"ms": f.get("ms"), "ok": bool(f.get("check", {}).get("sampled"))}))
