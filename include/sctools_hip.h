@@ -55,13 +55,12 @@ int sct_set_device(int device);        /* select the device for later calls (hip
 #define SCT_TUNE_ENCODE_GRID 12         /* tiled encoder grid: 1 one workgroup per tile (default), 0 resident workgroups */
 #define SCT_TUNE_INGEST_TILES 13        /* whitelist / FASTQ extraction: tiles per workgroup (0: one range per
                                            resident slot, the whitelist's default; FASTQ default 8) */
-#define SCT_TUNE_FASTQ_ONEPASS 14       /* sct_fastq_extract_fused: 0 = count pass first (default); 2 / 4 / 8 = one
-                                           pass, a look-back over ranges of that many 8 KiB tiles held in
-                                           registers; 104 / 108 / 116 / 132 = the same over 4-32 tiles, the
-                                           extraction reading them again */
+#define SCT_TUNE_FASTQ_ONEPASS 14       /* retired in round 5 (the one-pass FASTQ forms lost their A/B and were
+                                           removed); accepted and ignored, so the key numbers stay stable */
 #define SCT_TUNE_INGEST_DIRECT 15       /* whitelist ingest: up to this many 16 KiB tiles (4096) the encode pass
                                            sums the per-tile counts itself, no reduction launch */
-#define SCT_TUNE_NKEYS 16
+#define SCT_TUNE_INGEST_SPEC 16         /* whitelist ingest: 1 tries 16-base lines in one read first (default), 0 never */
+#define SCT_TUNE_NKEYS 17
 int sct_tune_set(int key, int64_t value);
 int sct_tune_get(int key, int64_t* value);  /* -1 when unset */
 
@@ -110,10 +109,13 @@ int sct_encode_var(int kind, const uint8_t* buf, const int64_t* starts, const in
 int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines, int64_t* d_starts, int32_t* d_lens,
               int64_t* nlines, int32_t* max_len, void* stream);
 /* sct_whitelist_encode (device, ASYNCHRONOUS on stream: no host synchronisation): the same
- * split, chop and encode in one pass over the file (a decoupled look-back numbers the lines);
+ * split, chop and encode: a one-read pass for files of 16-base lines (checked on the fly), else a
+ * count pass over the file's tiles and an encode pass that numbers the lines from the tile counts;
  * *d_nlines (int64) and *d_maxlen (int32, the longest chopped line) are written on the device;
- * lines g < max_lines get d_starts[g], d_lens[g], `words` limbs of d_codes, d_gc[g] (nullable)
- * and d_flags[g] (nullable: bit 0 ambiguous, bit 1 invalid byte, bit 2 too long for `words`). */
+ * lines g < min(max_lines, *d_nlines) get d_starts[g], d_lens[g], `words` limbs of d_codes,
+ * d_gc[g] (nullable) and d_flags[g] (nullable: bit 0 ambiguous, bit 1 invalid byte, bit 2 too long
+ * for `words`); rows g >= max_lines are never written, rows in [*d_nlines, max_lines) are
+ * unspecified. */
 int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int kind, int words, int64_t max_lines,
                          uint64_t* d_codes, int64_t* d_starts, int32_t* d_lens, uint8_t* d_gc, uint8_t* d_flags,
                          int64_t* d_nlines, int32_t* d_maxlen, void* stream);

@@ -33,7 +33,7 @@ TUNE_KEYS = {"spectral_chunk": 1, "spectral_min_n": 2, "allpairs_grab": 3, "allp
              "allpairs_grid": 5, "nearest_scheme": 6, "nearest_load": 7, "scalar_server": 8,
              "scalar_idle_ms": 9, "spectral_columns": 10, "plan_cache": 11,
              "encode_grid": 12, "ingest_tiles": 13, "fastq_onepass": 14,
-             "ingest_direct": 15}
+             "ingest_direct": 15, "ingest_spec": 16}
 NEAREST_AUTO, NEAREST_OA, NEAREST_CSR, NEAREST_HALVES = 0, 1, 2, 3
 
 _i32, _i64, _dbl = ctypes.c_int, ctypes.c_int64, ctypes.c_double

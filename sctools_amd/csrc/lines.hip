@@ -170,7 +170,9 @@ __device__ __forceinline__ int file_stride(const uint8_t* __restrict__ buf, int6
 }
 
 __global__ __launch_bounds__(WG) void wl_count_kernel(const uint8_t* __restrict__ buf, int64_t n, sct::TileSums ts,
-                                                      int32_t* __restrict__ d_maxlen) {
+                                                      int32_t* __restrict__ d_maxlen,
+                                                      const unsigned* __restrict__ spec_fail) {
+  if (spec_fail && *spec_fail == 0u) return;  // the one-read pass (whitelist_spec16_kernel) did it all
   const int64_t t0 = (int64_t)blockIdx.x * WTILE;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     *d_maxlen = 0;  // (the encode pass raises it; no memset launch)
@@ -340,7 +342,8 @@ __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
     const uint8_t* __restrict__ buf, int64_t n, int64_t ntiles, int64_t per_wg, sct::TileSums ts, int direct,
     int64_t cap, int words, uint64_t* __restrict__ codes, int64_t* __restrict__ starts, int32_t* __restrict__ lens,
     uint8_t* __restrict__ gc, uint8_t* __restrict__ flags, unsigned long long* __restrict__ d_nlines,
-    int32_t* __restrict__ d_maxlen) {
+    int32_t* __restrict__ d_maxlen, const unsigned* __restrict__ spec_fail) {
+  if (spec_fail && *spec_fail == 0u) return;  // the one-read pass did it all
   __shared__ uint8_t lut[256];
   __shared__ uint4 tile_bytes[WTILE / 16 + 1];  // (+16: encode_line1's dword reads stay inside)
   __shared__ uint32_t w_cnt[NSUB][WG / 64];
@@ -674,6 +677,102 @@ extern "C" int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines
 // line count and the longest chopped line go to d_nlines / d_maxlen; lines g < max_lines are
 // written (starts, lens, words limbs of codes, gc and flags nullable; flags bit 2 = a line
 // too long for `words` limbs).
+// One read of a 10x-style whitelist: the file is ASSUMED to be lines of 16 bases
+// and a '\n' (stride 17, the size a multiple of 17) -- line g is [17 g, 17 g + 16) -- and every
+// line is encoded straight from memory as the fixed-stride branch of whitelist_fused_kernel does,
+// while the assumption is CHECKED on the same bytes: the stride taken from the file's first line
+// must be 17, byte 17 g + 16 must be a '\n', and no line's 16 bytes may hold one (an A/C/G/T line
+// holds none; a line through the LUT path is searched).  Any failure sets *fail, and the count and
+// encode passes that follow in the stream (which return at once when *fail is 0) redo the file by
+// the general path, overwriting everything; so the count pass's read of the file is skipped only
+// for files where the result is already right.
+template <int KIND>
+__global__ __launch_bounds__(WG) void whitelist_spec16_kernel(const uint8_t* __restrict__ buf, int64_t n, int64_t cap,
+                                                              int words, uint64_t* __restrict__ codes,
+                                                              int64_t* __restrict__ starts, int32_t* __restrict__ lens,
+                                                              uint8_t* __restrict__ gc, uint8_t* __restrict__ flags,
+                                                              unsigned long long* __restrict__ d_nlines,
+                                                              int32_t* __restrict__ d_maxlen,
+                                                              unsigned* __restrict__ fail) {
+  constexpr int S = 17, L = 16;
+  __shared__ uint8_t lut[256];
+  __shared__ int s_stride;
+  const int t = threadIdx.x;
+  for (int c = t; c < 256; c += WG) lut[c] = lut_entry(KIND, c);
+  if (file_stride(buf, n, &s_stride) != S) {  // (its barrier also covers the LUT)
+    if (blockIdx.x == 0 && t == 0) atomicOr(fail, 1u);
+    return;
+  }
+  const int64_t nl = n / S, gend = nl < cap ? nl : (cap > 0 ? cap : 0);
+  if (blockIdx.x == 0 && t == 0) {
+    *d_nlines = (unsigned long long)nl;
+    *d_maxlen = L;
+  }
+  bool ok = true;
+  constexpr int U = 4;  // lines per thread per step, all their loads issued before any is used
+  for (int64_t g0 = (int64_t)blockIdx.x * WG + t; g0 < nl; g0 += (int64_t)U * gridDim.x * WG) {
+    uint32_t d[U][5];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t g = g0 + (int64_t)u * gridDim.x * WG, start = g * S;
+      const uint32_t o = (uint32_t)(start & 3);
+      if (g < nl && start - o + 20 <= n) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + (start - o));
+#pragma unroll
+        for (int k = 0; k < 5; ++k) d[u][k] = w[k];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t g = g0 + (int64_t)u * gridDim.x * WG, start = g * S;
+      if (g >= nl) break;
+      const uint32_t o = (uint32_t)(start & 3);
+      uint64_t code = 0;
+      uint32_t gg = 0, fl = 0;
+      bool done = false;
+      if (start - o + 20 <= n) {
+        uint32_t bad = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t x = __builtin_amdgcn_alignbyte(d[u][k + 1], d[u][k], o);
+          const uint32_t uu = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
+          const uint32_t v = uu ^ ((uu >> 1) & 0x01010101u);
+          bad |= __builtin_amdgcn_perm(0u, 0x47544341u, v) ^ x;
+          const uint32_t y =
+              __builtin_amdgcn_perm(0u, KIND == 2 ? v : __builtin_amdgcn_perm(0u, 0x03040102u, v), 0x00010203u);
+          if (KIND == 2) {
+            const uint32_t a = (y | (y >> 6)) & 0x000F000Fu;
+            code = (code << 8) | ((a | (a >> 12)) & 0xFFu);
+          } else {
+            const uint32_t a = (y | (y >> 5)) & 0x003F003Fu;
+            code = (code << 12) | ((a | (a >> 10)) & 0xFFFu);
+          }
+        }
+        ok = ok && ((d[u][4] >> (8 * o)) & 0xFFu) == 0x0Au;  // byte 16 of the line: its '\n'
+        if (!bad) {
+          gg = (uint32_t)__popcll(code & (KIND == 2 ? 0x5555555555555555ull : 0x9249249249249249ull));
+          done = true;
+        }
+      } else {
+        ok = ok && buf[start + L] == 0x0Au;
+      }
+      if (!done) {  // another byte in the line (the LUT), or the file's last line: any '\n' breaks the stride
+        for (int p = 0; p < L; ++p) ok = ok && buf[start + p] != 0x0Au;
+        encode_line<KIND>(lut, buf + start, L, 1, &code, gg, fl);
+      }
+      if (g < gend) {
+        codes[g * words] = code;  // (a 16-base code is one limb; wider rows get zero upper limbs)
+        for (int w = 1; w < words; ++w) codes[g * words + w] = 0;
+        starts[g] = start;
+        lens[g] = L;
+        if (gc) gc[g] = (uint8_t)gg;
+        if (flags) flags[g] = (uint8_t)fl;
+      }
+    }
+  }
+  if (!ok) atomicOr(fail, 1u);
+}
+
 extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int kind, int words, int64_t max_lines,
                                     uint64_t* d_codes, int64_t* d_starts, int32_t* d_lens, uint8_t* d_gc,
                                     uint8_t* d_flags, int64_t* d_nlines, int32_t* d_maxlen, void* stream) {
@@ -691,10 +790,26 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   // wl_count_kernel: one workgroup per tile, < 2^32 threads per launch
   SCT_CHECK(ntiles * WG < (1LL << 32), "buffer too large: %lld bytes (one launch covers < %lld)", (long long)nbytes,
             (long long)(((1LL << 32) / WG) * WTILE));
+  const size_t tsb = (sct::tile_sums_bytes(ntiles, true) + 255) & ~(size_t)255;
   StreamBuf scratch;
-  SCT_HIP(scratch.alloc(sct::tile_sums_bytes(ntiles, true), s));
+  SCT_HIP(scratch.alloc(tsb + 256, s));
   const sct::TileSums ts = sct::tile_sums_at(scratch.p, ntiles, true, true);
-  hipLaunchKernelGGL(wl_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, ts, d_maxlen);
+  const int64_t cap = max_lines > 0 ? max_lines : 0;
+  // 16-base lines are tried in one read first (whitelist_spec16_kernel): when the file is that
+  // layout, the passes below return at once; else they redo it (SCT_TUNE_INGEST_SPEC = 0: never)
+  unsigned* spec_fail = nullptr;
+  if (nbytes % 17 == 0 && sct::tune(SCT_TUNE_INGEST_SPEC, 1) != 0) {
+    spec_fail = reinterpret_cast<unsigned*>(reinterpret_cast<uint8_t*>(scratch.p) + tsb);
+    SCT_HIP(hipMemsetAsync(spec_fail, 0, 4, s));
+    auto spec = kind == 2 ? whitelist_spec16_kernel<2> : whitelist_spec16_kernel<3>;
+    const int64_t nl = nbytes / 17;
+    const unsigned sg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(sct::ceil_div(nl, 4 * WG), 8192));
+    hipLaunchKernelGGL(spec, dim3(sg), dim3(WG), 0, s, d_buf, nbytes, cap, words, d_codes, d_starts, d_lens, d_gc, d_flags,
+                       reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen, spec_fail);
+    SCT_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(wl_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, ts, d_maxlen,
+                     (const unsigned*)spec_fail);
   SCT_LAUNCH_CHECK();
   // up to 4,096 tiles (64 MiB) every encode workgroup reads the per-tile words itself (<= 16 per
   // thread) instead of waiting for a reduction launch
@@ -704,7 +819,6 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
                        ntiles);
     SCT_LAUNCH_CHECK();
   }
-  const int64_t cap = max_lines > 0 ? max_lines : 0;
   auto kern = kind == 2 ? whitelist_fused_kernel<2> : whitelist_fused_kernel<3>;
   // one range per resident slot (0.081 ms for config 5's whitelist; one 16 KiB tile per
   // workgroup 0.088, tools/ingest_tiles_ab.py); SCT_TUNE_INGEST_TILES > 0 fixes the range
@@ -712,7 +826,7 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   const int64_t per_wg = knob > 0 ? knob : sct::ceil_div(ntiles, resident_slots((const void*)kern, ntiles));
   hipLaunchKernelGGL(kern, dim3((unsigned)sct::ceil_div(ntiles, per_wg)), dim3(WG), 0, s, d_buf, nbytes, ntiles,
                      per_wg, ts, direct, cap, words, d_codes, d_starts, d_lens, d_gc, d_flags,
-                     reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen);
+                     reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen, (const unsigned*)spec_fail);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }

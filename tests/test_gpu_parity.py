@@ -764,6 +764,36 @@ def test_nearest_halves_edges(kind, L, max_d):
         plan.close()
 
 
+@pytest.mark.parametrize("kind", [2, 3])
+def test_nearest_halves_big_buckets(kind):
+    """Buckets of many chunks (every whitelist code sharing its high half, or its low half, with
+    hundreds of others: full chunks, a partial last chunk, empty buckets between) and buckets of
+    exactly 16 / 17 / 32 / 33 codes, against the brute force."""
+    rng = np.random.default_rng(77 + kind)
+    L = 16
+    hi = np.uint64(0x5A5A) << np.uint64(16)  # one high half (A key) for 700 codes
+    lo_codes = np.unique(rng.integers(0, 1 << 16, 1200, dtype=np.uint64))[:700]
+    wl2 = [hi | lo_codes]
+    for k, size in enumerate((16, 17, 32, 33, 1)):  # buckets of exact group multiples and one more
+        a = np.uint64(0x1000 + k) << np.uint64(16)
+        wl2.append(a | np.unique(rng.integers(0, 1 << 16, 4 * size, dtype=np.uint64))[:size])
+    b = np.uint64(0x0F0F)  # one low half (B key) for 300 codes
+    wl2.append((np.unique(rng.integers(0, 1 << 16, 600, dtype=np.uint64))[:300] << np.uint64(16)) | b)
+    wl2 = np.unique(np.concatenate(wl2))
+    wl = wl2 if kind == 2 else synthetic.two_to_three(wl2, L)
+    picks = wl[rng.integers(0, wl.size, 4000)]
+    pos = rng.integers(0, L, picks.size).astype(np.uint64)
+    w = np.uint64(kind)
+    sub = rng.integers(0, 4, picks.size).astype(np.uint64) + (np.uint64(1) if kind == 3 else np.uint64(0))
+    one = rng.random(picks.size) < 0.5
+    q = picks.copy()
+    q[one] = (q[one] & ~(np.uint64((1 << kind) - 1) << (w * pos[one]))) | (sub[one] << (w * pos[one]))
+    ridx, rdist = O.c_nearest(kind, wl, q, 1)
+    with _lib.tuning(nearest_scheme=_lib.NEAREST_HALVES):
+        idx, dist = barcode.nearest_whitelist(q, wl, max_distance=1, encoding=kind)
+    assert np.array_equal(idx, ridx) and np.array_equal(dist, rdist)
+
+
 def test_nearest_halves_falls_back_on_non_acgt_whitelists():
     """A ThreeBit whitelist holding an N (or a shorter code) cannot use the half-key tables:
     the plan takes another layout and the result is still the brute force's."""
@@ -1364,6 +1394,12 @@ def _ingest_cases():
     odd = bytearray(b"ACGTACGTACGTACGT\n" * 20_000)
     odd[170_000:170_017] = b"ACGTACGTACGTACG\nA"  # one end moved by one byte
     cases["fixed_one_off"] = bytes(odd)
+    # sizes that are multiples of 17 with a 17-byte first line, but not 16-base lines throughout: the
+    # one-read pass (whitelist_spec16_kernel) must notice and leave the file to the general path
+    split = bytearray(b"ACGTACGTACGTACGT\n" * 20_000)
+    split[85_000:85_017] = b"ACGTACG\nACGTACGT\n"  # two lines in one 17-byte slot (an inner '\n')
+    cases["fixed_split_line"] = bytes(split)
+    cases["fixed_long_line"] = b"ACGTACGTACGTACGT\n" * 9_000 + b"ACGT" * 8 + b"A\n" + b"TTTTGGGGCCCCAAAA\n" * 9_000
     return cases
 
 
@@ -1379,6 +1415,15 @@ def test_whitelist_encode_with_reduction_launch(name):
     buffers above 64 MiB take), not summed by every encode workgroup."""
     with _lib.tuning(ingest_direct=0):
         _whitelist_encode_check(name, 2, 1)
+
+
+@pytest.mark.parametrize("name", ["fixed16", "fixed_one_off", "fixed_split_line", "tiny"])
+def test_whitelist_encode_without_one_read(name):
+    """The count + encode passes on their own (SCT_TUNE_INGEST_SPEC = 0): the 16-base fixed-stride
+    branch of the encode pass, which the one-read pass otherwise takes over."""
+    with _lib.tuning(ingest_spec=0):
+        _whitelist_encode_check(name, 2, 1)
+        _whitelist_encode_check(name, 3, 1)
 
 
 def _whitelist_encode_check(name, kind, words):
