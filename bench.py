@@ -55,7 +55,8 @@ HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E (MI355X_MICROARCH.md)
 SIMDS = 256 * 4
 ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-bit code word
 METRIC = "Hamming pair-comparisons/sec, 737K 10x whitelist all-pairs, 1-8 GPUs"
-PROFILE_ROUND = "r04"  # the committed rocprof / PMC summaries the line cites (profiles/)
+PROFILE_ROUND = "r05"  # the committed rocprof / PMC summaries the line cites (profiles/)
+PROFILE_FALLBACK = ("r04",)  # a kernel not re-profiled this round cites its latest summary
 
 
 def parse(argv=None):
@@ -203,27 +204,30 @@ def cpu_baseline(codes, gpu_hist, budget_s):
 
 # ------------------------------------------------------------------ rooflines
 def _profile(name):
-    """A committed PMC summary (profiles/pmc_<name>_<round>.json, tools/summarize_profile.py)."""
-    path = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (name, PROFILE_ROUND))
-    if os.path.exists(path):
-        with open(path) as f:
-            return dict(json.load(f), file=os.path.relpath(path, ROOT))
+    """A committed PMC summary (profiles/pmc_<name>_<round>.json, tools/summarize_profile.py): this
+    round's, else the latest earlier one."""
+    for rnd in (PROFILE_ROUND,) + PROFILE_FALLBACK:
+        path = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (name, rnd))
+        if os.path.exists(path):
+            with open(path) as f:
+                return dict(json.load(f), file=os.path.relpath(path, ROOT))
     return None
 
 
-def _rocprof_avg_ms(kernel_substr):
+def _rocprof_avg_ms(kernel_substr, stats="kernel_stats"):
     """Average dispatch duration of a kernel in the committed rocprofv3 kernel trace of this
     bench command: over the timed steps' dispatches (profiles/<round>_timed_dispatches.json,
     the last K dispatches, the launches the live HIP events time) when present, else the
-    --stats average of every dispatch (profiles/<round>_kernel_stats.csv); or None."""
+    --stats average of every dispatch (profiles/<round>_<stats>.csv: the bench command's, or
+    config5_kernel_stats for config 5's path run alone); or None."""
     import csv
     win = os.path.join(ROOT, "profiles", "%s_timed_dispatches.json" % PROFILE_ROUND)
-    if os.path.exists(win):
+    if os.path.exists(win) and stats == "kernel_stats":
         with open(win) as f:
             k = json.load(f)["kernels"].get(kernel_substr)
         if k:
             return k["avg_ns"] * 1e-6, k["window"], k.get("live_vs_trace_same_run")
-    path = os.path.join(ROOT, "profiles", "%s_kernel_stats.csv" % PROFILE_ROUND)
+    path = os.path.join(ROOT, "profiles", "%s_%s.csv" % (PROFILE_ROUND, stats))
     if not os.path.exists(path):
         return None, None, None
     with open(path) as f:
@@ -297,8 +301,9 @@ def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, nam
     for k, label, prof_name, rp in kernels:
         ms, nl = kt[k]
         avg = ms / nl if nl else float("nan")
-        prof = _profile(prof_name) if elem_bytes == 1 and column_bits == 14 else None
-        rms, rcalls, same_run = _rocprof_avg_ms(rp) if elem_bytes == 1 and column_bits == 14 else (None, None, None)
+        prof = _profile(prof_name) if elem_bytes == 1 else None
+        rms, rcalls, same_run = (_rocprof_avg_ms(rp, "kernel_stats" if column_bits == 14 else "config5_kernel_stats")
+                                 if elem_bytes == 1 else (None, None, None))
         gbs = algo / (avg * 1e-3) / 1e9
         kern[k] = {"kernel": label, "ms": avg, "launches": nl, "achieved_gbs": gbs, "frac": gbs * 1e9 / HBM_PEAK_BPS,
                    "frac_of_copy_ceiling": gbs / copy_gbs if copy_gbs else None,
@@ -306,9 +311,11 @@ def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, nam
                    "issue": issue_picture(prof),
                    "rocprof": None if rms is None else {
                        "avg_ms": rms, "calls": rcalls, "frac": algo / (rms * 1e-3) / HBM_PEAK_BPS,
-                       "source": "profiles/%s_timed_dispatches.json (the timed steps' dispatches of the rocprofv3 "
-                                 "kernel trace of this command; every dispatch: profiles/%s_kernel_stats.csv)"
-                                 % (PROFILE_ROUND, PROFILE_ROUND),
+                       "source": ("profiles/%s_timed_dispatches.json (the timed steps' dispatches of the rocprofv3 "
+                                  "kernel trace of this command; every dispatch: profiles/%s_kernel_stats.csv)"
+                                  % (PROFILE_ROUND, PROFILE_ROUND)) if column_bits == 14 else
+                                 ("profiles/%s_config5_kernel_stats.csv (rocprofv3 --kernel-trace --stats of "
+                                  "tools/run_paths.py config5_allpairs: every dispatch)" % PROFILE_ROUND),
                        "live_vs_rocprof": avg / rms - 1.0,
                        "profiled_run_live_vs_rocprof": same_run,
                        "note": "live_vs_rocprof compares this run with a trace taken on another box (boxes differ "
@@ -501,8 +508,8 @@ def path_config5_allpairs(dev, steps, copy_gbs):
     return {"workload": "config 5 all-pairs: %d-code 16-bp whitelist, all %d pairs" % (n, P),
             "column_bits": info["column_bits"], "value": P / dt, "unit": "pairs/s", "ms_per_step": dt * 1e3, "steps": steps,
             "roofline": {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel", "kernel_ms",
-                                              "launches", "frac_of_copy_ceiling", "other_kernel",
-                                              "algo_bytes_per_launch")},
+                                              "launches", "frac_of_copy_ceiling", "traffic", "issue", "rocprof",
+                                              "other_kernel", "algo_bytes_per_launch")},
             "check": {"steps_agree": ok_steps, "pairs": int(hist.sum()) == P,
                       "moments_vs_oracle_marginals": m_hist == m_codes,
                       "sample": "M_1, M_2 (pairs agreeing on 1 / 2 chosen positions) from the histogram vs "
@@ -561,14 +568,27 @@ def path_config5_encode(dev, reps, copy_gbs):
 
 
 def _hip_runtime():
-    """The HIP runtime torch loaded (for hipHostRegister / hipHostUnregister from Python)."""
+    """The HIP runtime torch loaded (for hipHostMalloc / hipHostFree from Python)."""
     import ctypes
 
     from sctools_amd import _lib
     rt = ctypes.CDLL(os.environ.get("SCTOOLS_HIP_RUNTIME") or _lib._torch_hip_runtime() or "libamdhip64.so")
-    rt.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
-    rt.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    rt.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    rt.hipHostFree.argtypes = [ctypes.c_void_p]
     return rt
+
+
+def _pinned_array(rt, shape, dtype, keep):
+    """A numpy array over a fresh hipHostMalloc block (page-locked from the start, as a long-running
+    ingest would allocate its buffers); the block's pointer is appended to `keep` for hipHostFree."""
+    import ctypes
+    nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    p = ctypes.c_void_p()
+    if rt.hipHostMalloc(ctypes.byref(p), nbytes, 0) != 0 or not p.value:
+        raise RuntimeError("hipHostMalloc of %d bytes failed" % nbytes)
+    keep.append(p)
+    buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
+    return np.frombuffer(buf, dtype=dtype).reshape(shape)
 
 
 def pcie_ceiling_gbs(dev, gib=2, reps=3):
@@ -588,25 +608,22 @@ def path_config5_encode_stream(dev, reps, pcie):
     """Config 5's read stream HOST-resident (SURVEY §8(d) "report both"): 1e9 28-bp reads in host
     memory (1 % with one N), TwoBit encode + GC + flags through sct_encode_stream_host (pinned,
     three stages in flight: H2D, encode, D2H), codes / GC / flags back in host memory.  The host
-    buffers are page-locked before the timed calls (as a long-running ingest would keep them)."""
+    buffers are page-locked allocations (hipHostMalloc, as a long-running ingest would keep them),
+    which the stream copies by DMA in place."""
     import ctypes
 
     import torch
     from oracle import oracle as O
     from sctools_amd import _lib, synthetic
     n, L = synthetic.CONFIG5_READS, synthetic.CONFIG5_READ_LENGTH
-    seqs = np.empty((n, L), dtype=np.uint8)
-    codes = np.empty(n, dtype=np.uint64)
-    gc = np.empty(n, dtype=np.uint8)
-    flags = np.empty(n, dtype=np.uint8)
     rt = _hip_runtime()
-    bufs = [seqs, codes, gc, flags]
-    reg = []
+    blocks = []
     try:
-        for a in bufs:
-            if rt.hipHostRegister(a.ctypes.data, a.nbytes, 0) != 0:
-                raise RuntimeError("hipHostRegister of %d bytes failed" % a.nbytes)
-            reg.append(a)
+        seqs = _pinned_array(rt, (n, L), np.uint8, blocks)
+        codes = _pinned_array(rt, (n,), np.uint64, blocks)
+        gc = _pinned_array(rt, (n,), np.uint8, blocks)
+        flags = _pinned_array(rt, (n,), np.uint8, blocks)
+        direct = all(_lib.host_pinned(a) for a in (seqs, codes, gc, flags))
         # the reads: a 2^25-read random block made on the device (ASCII A/C/G/T, one N in every 100th
         # read), copied into every block of the host array
         blk = 1 << 25
@@ -646,12 +663,12 @@ def path_config5_encode_stream(dev, reps, pcie):
                 and bool(flags[r]) == has_n
         nflag = int(flags.sum(dtype=np.int64))
         want_flags = sum(len(range(0, min(blk, n - r0), 100)) for r0 in range(0, n, blk))
+        del seqs, codes, gc, flags, hs
     finally:
-        for a in reg:
-            rt.hipHostUnregister(a.ctypes.data)
+        for p in blocks:
+            rt.hipHostFree(p)
     in_bytes, out_bytes = n * L, n * 10
     gbs_in = in_bytes / dt / 1e9
-    del seqs, codes, gc, flags
     return {"workload": "config 5 read stream, host-resident: %d random %d-bp reads (1%% with one N) in host "
                         "memory -> TwoBit codes + GC + flags in host memory (sct_encode_stream_host)" % (n, L),
             "value": n / dt, "unit": "reads/s", "ms": dt * 1e3, "ms_all": [t * 1e3 for t in ts], "reps": reps,
@@ -661,6 +678,7 @@ def path_config5_encode_stream(dev, reps, pcie):
                          "d2h_peak": pcie["d2h_gbs"],
                          "note": "%d bytes in and %d out per pass; the device side (paths.config5_encode) runs "
                                  "the same reads at HBM speed, so the host link bounds this path" % (in_bytes, out_bytes)},
+            "dma_in_place": direct,
             "check": {"sampled_vs_oracle": ok, "flagged_reads": nflag == want_flags,
                       "sample": "the first 4096 reads byte for byte; 46 reads (every 97th of the first block, the "
                                 "last, the middle, one N read) vs oracle.two_bit_encode (N as A), their GC and flag; one "
@@ -708,18 +726,34 @@ def path_fastq_stream_to_nearest(dev, threads):
         nbytes = os.path.getsize(path)
         eb = fastq.EmbeddedBarcode(0, 16, "CR", "CY")
 
+        parts_s = {"pieces": 0.0, "encode": 0.0, "nearest": 0.0}
+
         def run():
             idx_parts, dist_parts, code_parts = [], [], []
             gen = fastq.EmbeddedBarcodeGenerator([eb], [path], mode="rb")
-            for arrays in gen.iter_arrays(qualities=False):
+            it = gen.iter_arrays(qualities=False)
+            while True:
+                t0 = time.perf_counter()
+                arrays = next(it, None)
+                t1 = time.perf_counter()
+                if arrays is None:
+                    parts_s["pieces"] += t1 - t0
+                    break
                 cb = arrays["CR"][0]
                 codes = encodings.ThreeBit.encode_array(cb)
+                t2 = time.perf_counter()
                 idx, dist = barcode.nearest_whitelist(codes, wl, max_distance=1, encoding="ThreeBit")
+                t3 = time.perf_counter()
+                parts_s["pieces"] += t1 - t0
+                parts_s["encode"] += t2 - t1
+                parts_s["nearest"] += t3 - t2
                 idx_parts.append(idx)
                 dist_parts.append(dist)
                 code_parts.append(codes)
             return np.concatenate(idx_parts), np.concatenate(dist_parts), np.concatenate(code_parts)
         run()  # warm (and the file in the page cache)
+        for k in parts_s:
+            parts_s[k] = 0.0
         t = time.perf_counter()
         idx, dist, codes = run()
         dt = time.perf_counter() - t
@@ -742,7 +776,7 @@ def path_fastq_stream_to_nearest(dev, threads):
                         "(sct_fastq_stream_*) -> ThreeBit.encode_array -> nearest_whitelist vs the %d-code whitelist "
                         "at Hamming <= 1, host arrays between the calls" % (n_rec, nbytes, n),
             "value": n_rec / dt, "unit": "records/s", "ms": dt * 1e3, "file_bytes": nbytes,
-            "file_gbs": nbytes / dt / 1e9,
+            "file_gbs": nbytes / dt / 1e9, "breakdown_ms": {k: v * 1e3 for k, v in parts_s.items()},
             "roofline": {"bound": "file read", "achieved": nbytes / dt / 1e9, "unit": "GB/s of FASTQ",
                          "peak": nbytes / read_dt / 1e9, "frac": read_dt / dt,
                          "peak_source": "the same file read in the same pieces (page cache), nothing else, this run"},

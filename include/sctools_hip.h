@@ -86,11 +86,19 @@ int sct_encode_host(int kind, const uint8_t* seqs, int64_t n, int64_t stride, in
                     uint64_t* codes, uint8_t* gc, uint8_t* flags);
 
 /* Host-resident stream of n records (stride L, one limb: L <= 32 TwoBit / 21 ThreeBit):
- * chunks of `chunk` records (<= 0: 16M) pipeline H2D / encode / D2H over 3 streams; the
- * caller's buffers are page-locked in place for the call unless already pinned.  gc and
- * flags are required.  Returns when all outputs are in host memory. */
+ * chunks of `chunk` records (<= 0: 16M) pipeline H2D / encode / D2H over 3 streams.  Buffers
+ * already page-locked (sct_host_pinned) are copied by DMA in place; pageable ones go through
+ * the library's own pinned stage in chunks of <= 2M records (the library never registers
+ * caller memory).  gc and flags are required.  Returns when all outputs are in host memory.
+ * Replaces the per-record loop of encodings.py:60-71 / 140-147 for a batch of records. */
 int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, int L, uint64_t* codes,
                            uint8_t* gc, uint8_t* flags, int64_t chunk);
+
+/* *pinned = 1 when all of [p, p + bytes) lies in one page-locked host allocation the HIP
+ * runtime knows (hipHostMalloc, torch pin_memory, hipHostRegister): the host-stream entry
+ * points then DMA to / from it in place; 0 otherwise (pageable memory, or a range that
+ * runs past its allocation). */
+int sct_host_pinned(const void* p, int64_t bytes, int* pinned);
 
 /* Variable-length records (device): record r = starts[r] .. starts[r] + lens[r] of buf,
  * encoded as encodings.py:75-88 / :155-167 do into `words` limbs (words >= ceil(kind*len/64)

@@ -51,6 +51,7 @@ SIGNATURES = {
     "sct_encode": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
     "sct_encode_host": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp],
     "sct_encode_stream_host": [_i32, _vp, _i64, _i32, _vp, _vp, _vp, _i64],
+    "sct_host_pinned": [_vp, _i64, _vp],
     "sct_encode_var": [_i32, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp],
     "sct_lines": [_vp, _i64, _i64, _vp, _vp, ctypes.POINTER(_i64), ctypes.POINTER(_i32), _vp],
     "sct_whitelist_encode": [_vp, _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -313,6 +314,13 @@ def encode_stream(kind, seqs, chunk=0):
     flags = np.empty(n, dtype=np.uint8)
     check(lib().sct_encode_stream_host(kind, _ptr(seqs), n, L, _ptr(codes), _ptr(gc), _ptr(flags), chunk))
     return codes, gc, flags
+
+
+def host_pinned(arr):
+    """True when the numpy array's bytes lie in one page-locked allocation (DMA in place)."""
+    out = _i32(0)
+    check(lib().sct_host_pinned(_vp(arr.ctypes.data), arr.nbytes, ctypes.byref(out)))
+    return bool(out.value)
 
 
 def whitelist_encode(data, kind=2):

@@ -1048,6 +1048,7 @@ extern "C" int sct_allpairs_plan_create_ex2(const uint64_t* d_codes, int64_t n, 
 
 extern "C" int sct_allpairs_plan_destroy(sct_allpairs_plan* plan) {
   if (!plan) return SCT_OK;
+  sct_spectral::wait_idle(plan->spec);  // (every scheme's work is recorded there) before any buffer goes
   if (plan->d_codes) sct_spectral::ws_put(plan->spec.ws, plan->d_codes);  // (the workspace: kept)
   if (plan->d_sorted) (void)hipFree(plan->d_sorted);
   if (plan->d_sort_tmp) (void)hipFree(plan->d_sort_tmp);

@@ -1128,7 +1128,11 @@ extern "C" int sct_base_frequency_host(const uint64_t* codes, int64_t n, int L, 
 // Host-resident stream (config 5): records live in host memory; chunks flow through
 // NSTAGE device buffers on NSTAGE streams so that the H2D copy of one chunk, the encode
 // of another and the D2H copy of a third overlap (PCIe-bound: L + 10 bytes per read cross
-// the link).  Caller buffers are page-locked in place for the call unless already pinned.
+// the link).  Caller buffers the runtime already page-locks (hipHostMalloc, torch pin_memory, the
+// caller's own hipHostRegister) are copied by DMA in place; pageable ones go through the thread's
+// pinned stage, filled and emptied on the CPU while the other stages' copies and kernels run.  The
+// library never page-locks caller memory itself (registering and unregistering ranges the runtime
+// may also lock for its own pageable copies is not something to do behind the caller's back).
 extern "C" int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, int L,
                                       uint64_t* codes, uint8_t* gc, uint8_t* flags,
                                       int64_t chunk) {
@@ -1137,35 +1141,32 @@ extern "C" int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, 
   SCT_CHECK(gc != nullptr && flags != nullptr && codes != nullptr && seqs != nullptr, "NULL pointer");
   if (n == 0) return SCT_OK;
   if (chunk <= 0) chunk = 1 << 24;
-  chunk = std::min<int64_t>(chunk, n);
   constexpr int NSTAGE = 3;
-  struct Reg {
-    void* p = nullptr;
-    ~Reg() {
-      if (p) (void)hipHostUnregister(p);
-    }
-  } reg[4];
-  auto pin = [&](Reg& r, const void* ptr, size_t bytes) -> int {
-    hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, ptr) == hipSuccess && at.type != hipMemoryTypeUnregistered)
-      return SCT_OK;  // already pinned or device-visible
-    (void)hipGetLastError();
-    SCT_HIP(hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault));
-    r.p = const_cast<void*>(ptr);
-    return SCT_OK;
-  };
-  int rc;
-  if ((rc = pin(reg[0], seqs, (size_t)n * L)) != SCT_OK) return rc;
-  if ((rc = pin(reg[1], codes, (size_t)n * 8)) != SCT_OK) return rc;
-  if ((rc = pin(reg[2], gc, (size_t)n)) != SCT_OK) return rc;
-  if ((rc = pin(reg[3], flags, (size_t)n)) != SCT_OK) return rc;
+  const bool pin_in = sct::host_range_pinned(seqs, (size_t)n * L);
+  const bool pin_out = sct::host_range_pinned(codes, (size_t)n * 8) && sct::host_range_pinned(gc, (size_t)n) &&
+                       sct::host_range_pinned(flags, (size_t)n);
+  const bool staged = !pin_in || !pin_out;
+  if (staged) chunk = std::min<int64_t>(chunk, 1 << 21);  // (a staged chunk: 2M reads, <= 2M * (L + 10) B)
+  chunk = std::min<int64_t>(chunk, n);
+  const size_t in_b = pin_in ? 0 : (((size_t)chunk * L + 255) & ~(size_t)255);
+  const size_t out_b = pin_out ? 0 : (size_t)chunk * 10;
+  uint8_t* stage = nullptr;
+  if (staged) {
+    sct::HostStage* hs = sct::host_stage();
+    if (!hs) return SCT_E_HIP;
+    SCT_TRY(sct::stage_reserve(hs, NSTAGE * (in_b + out_b), 0));
+    stage = hs->pinned;
+  }
   sct::DevBuf din[NSTAGE], dcode[NSTAGE], dgc[NSTAGE], dfl[NSTAGE];
   hipStream_t st[NSTAGE] = {};
   struct Streams {
     hipStream_t* s;
-    ~Streams() {
+    ~Streams() {  // (an early return leaves nothing in flight on the stage or the device buffers)
       for (int k = 0; k < NSTAGE; ++k)
-        if (s[k]) (void)hipStreamDestroy(s[k]);
+        if (s[k]) {
+          (void)hipStreamSynchronize(s[k]);
+          (void)hipStreamDestroy(s[k]);
+        }
     }
   } guard{st};
   for (int k = 0; k < NSTAGE; ++k) {
@@ -1175,19 +1176,45 @@ extern "C" int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, 
     SCT_HIP(dgc[k].alloc((size_t)chunk));
     SCT_HIP(dfl[k].alloc((size_t)chunk));
   }
+  // stage k's pinned buffers: the input chunk, then codes / GC / flags of the chunk in flight
+  auto h_in = [&](int k) { return stage + (size_t)k * (in_b + out_b); };
+  auto h_out = [&](int k) { return stage + (size_t)k * (in_b + out_b) + in_b; };
+  int64_t pend_r0[NSTAGE] = {}, pend_m[NSTAGE] = {};
+  auto drain = [&](int k) -> int {  // wait for stage k's chunk; pageable outputs copied out
+    if (pend_m[k] == 0) return SCT_OK;
+    SCT_HIP(hipStreamSynchronize(st[k]));
+    const int64_t r0 = pend_r0[k], m = pend_m[k];
+    if (!pin_out) {
+      memcpy(codes + r0, h_out(k), (size_t)m * 8);
+      memcpy(gc + r0, h_out(k) + (size_t)chunk * 8, (size_t)m);
+      memcpy(flags + r0, h_out(k) + (size_t)chunk * 9, (size_t)m);
+    }
+    pend_m[k] = 0;
+    return SCT_OK;
+  };
   int64_t c = 0;
   for (int64_t r0 = 0; r0 < n; r0 += chunk, ++c) {
     const int k = (int)(c % NSTAGE);  // stage k's previous chunk is ordered before on st[k]
     const int64_t m = std::min<int64_t>(chunk, n - r0);
-    SCT_HIP(hipMemcpyAsync(din[k].p, seqs + r0 * L, (size_t)m * L, hipMemcpyHostToDevice, st[k]));
-    rc = sct_encode(kind, (const uint8_t*)din[k].p, m, L, L, (uint64_t*)dcode[k].p, (uint8_t*)dgc[k].p,
-                    (uint8_t*)dfl[k].p, st[k]);
-    if (rc != SCT_OK) return rc;
-    SCT_HIP(hipMemcpyAsync(codes + r0, dcode[k].p, (size_t)m * 8, hipMemcpyDeviceToHost, st[k]));
-    SCT_HIP(hipMemcpyAsync(gc + r0, dgc[k].p, (size_t)m, hipMemcpyDeviceToHost, st[k]));
-    SCT_HIP(hipMemcpyAsync(flags + r0, dfl[k].p, (size_t)m, hipMemcpyDeviceToHost, st[k]));
+    if (staged) SCT_TRY(drain(k));  // (its pinned buffers are about to be refilled)
+    const uint8_t* src = seqs + r0 * L;
+    if (!pin_in) {
+      memcpy(h_in(k), src, (size_t)m * L);
+      src = h_in(k);
+    }
+    SCT_HIP(hipMemcpyAsync(din[k].p, src, (size_t)m * L, hipMemcpyHostToDevice, st[k]));
+    SCT_TRY(sct_encode(kind, (const uint8_t*)din[k].p, m, L, L, (uint64_t*)dcode[k].p, (uint8_t*)dgc[k].p,
+                       (uint8_t*)dfl[k].p, st[k]));
+    uint8_t* oc = pin_out ? reinterpret_cast<uint8_t*>(codes + r0) : h_out(k);
+    uint8_t* og = pin_out ? gc + r0 : h_out(k) + (size_t)chunk * 8;
+    uint8_t* of = pin_out ? flags + r0 : h_out(k) + (size_t)chunk * 9;
+    SCT_HIP(hipMemcpyAsync(oc, dcode[k].p, (size_t)m * 8, hipMemcpyDeviceToHost, st[k]));
+    SCT_HIP(hipMemcpyAsync(og, dgc[k].p, (size_t)m, hipMemcpyDeviceToHost, st[k]));
+    SCT_HIP(hipMemcpyAsync(of, dfl[k].p, (size_t)m, hipMemcpyDeviceToHost, st[k]));
+    pend_r0[k] = r0;
+    pend_m[k] = m;
   }
-  for (int k = 0; k < NSTAGE; ++k) SCT_HIP(hipStreamSynchronize(st[k]));
+  for (int k = 0; k < NSTAGE; ++k) SCT_TRY(drain(k));
   return SCT_OK;
 }
 

@@ -905,7 +905,7 @@ namespace {
 // One spare index allocation per device, kept when an index is destroyed and taken by the
 // next create that fits: a stream of pieces (one index per piece) or repeated extractions pay
 // no hipMalloc / hipFree per call.  Every user of an index synchronises its stream before the
-// index is destroyed, so a cached block is idle.
+// index is destroyed (sct_fastq_extract_spans ends with one), so a cached or freed block is idle.
 constexpr int kMaxDev = 16;
 std::mutex g_ix_mu;
 struct Spare {
@@ -1210,6 +1210,7 @@ struct sct_fastq_stream {
 
 extern "C" int sct_fastq_stream_destroy(sct_fastq_stream* s) {
   if (!s) return SCT_OK;
+  if (s->st) (void)hipStreamSynchronize(s->st->stream);  // nothing of the stream's still reads its buffers
   if (s->d_buf) (void)hipFree(s->d_buf);
   if (s->d_out) (void)hipFree(s->d_out);
   if (s->d_end) (void)hipFree(s->d_end);

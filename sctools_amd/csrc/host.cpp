@@ -44,6 +44,24 @@ HostStage* host_stage() {
   return stages[dev];
 }
 
+bool host_range_pinned(const void* p, size_t bytes) {
+  if (!p || !bytes) return false;
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (a.type != hipMemoryTypeHost) return false;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const uintptr_t b = reinterpret_cast<uintptr_t>(base), q = reinterpret_cast<uintptr_t>(p);
+  return q >= b && q - b <= size && bytes <= size - (q - b);
+}
+
 int stage_reserve(HostStage* st, size_t pinned_bytes, size_t dev_bytes) {
   auto grow = [](size_t have, size_t need) {
     size_t c = have ? have : (size_t)1 << 16;
@@ -135,6 +153,12 @@ extern "C" int sct_tune_get(int key, int64_t* value) {
   SCT_CHECK(key > 0 && key < SCT_TUNE_NKEYS, "unknown tuning key %d", key);
   SCT_CHECK(value != nullptr, "value is NULL");
   *value = sct::tune(key, -1);
+  return SCT_OK;
+}
+
+extern "C" int sct_host_pinned(const void* p, int64_t bytes, int* pinned) {
+  SCT_CHECK(pinned != nullptr && bytes >= 0, "bad arguments");
+  *pinned = sct::host_range_pinned(p, (size_t)bytes) ? 1 : 0;
   return SCT_OK;
 }
 

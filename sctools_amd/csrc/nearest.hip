@@ -647,10 +647,17 @@ struct sct_nearest_plan {
   uint32_t* d_off[MAX_PARTS] = {};
   uint64_t* d_code[MAX_PARTS] = {};
   uint32_t* d_index[MAX_PARTS] = {};
+  // recorded after every query on its stream: destroy waits on it, so freeing the tables never
+  // races a query still in flight (a caller may destroy right after enqueueing one)
+  hipEvent_t last_query = nullptr;
 };
 
 extern "C" int sct_nearest_plan_destroy(sct_nearest_plan* p) {
   if (!p) return SCT_OK;
+  if (p->last_query) {
+    (void)hipEventSynchronize(p->last_query);
+    (void)hipEventDestroy(p->last_query);
+  }
   for (void* m : p->hv_mem)
     if (m) (void)hipFree(m);
   for (int k = 0; k < MAX_KEYS; ++k)
@@ -911,8 +918,21 @@ extern "C" int sct_nearest_plan_info(const sct_nearest_plan* p, int* scheme, int
   return SCT_OK;
 }
 
+static int nearest_query_launch(sct_nearest_plan* p, const uint64_t* d_queries, int64_t nq, int32_t* d_index,
+                                uint8_t* d_dist, void* stream);
+
 extern "C" int sct_nearest_query(sct_nearest_plan* p, const uint64_t* d_queries, int64_t nq,
                                  int32_t* d_index, uint8_t* d_dist, void* stream) {
+  const int rc = nearest_query_launch(p, d_queries, nq, d_index, d_dist, stream);
+  if (rc == SCT_OK && p && nq > 0) {
+    if (!p->last_query) SCT_HIP(hipEventCreateWithFlags(&p->last_query, hipEventDisableTiming));
+    SCT_HIP(hipEventRecord(p->last_query, sct::as_stream(stream)));
+  }
+  return rc;
+}
+
+static int nearest_query_launch(sct_nearest_plan* p, const uint64_t* d_queries, int64_t nq, int32_t* d_index,
+                                uint8_t* d_dist, void* stream) {
   SCT_CHECK(p != nullptr, "plan is NULL");
   SCT_CHECK(nq >= 0, "nq must be >= 0");
   if (nq == 0) return SCT_OK;
@@ -966,11 +986,11 @@ extern "C" int sct_nearest_host(int kind, const uint64_t* whitelist, int64_t nw,
   int rc = sct_nearest_plan_create(kind, (const uint64_t*)dw.p, nw, code_bits, max_d, nullptr, &plan);
   if (rc != SCT_OK) return rc;
   rc = sct_nearest_query(plan, (const uint64_t*)dq.p, nq, (int32_t*)di.p, (uint8_t*)dd.p, nullptr);
-  sct_nearest_plan_destroy(plan);
-  if (rc != SCT_OK) return rc;
-  if (nq) {
-    SCT_HIP(hipMemcpy(index, di.p, (size_t)nq * 4, hipMemcpyDeviceToHost));
-    SCT_HIP(hipMemcpy(dist, dd.p, (size_t)nq, hipMemcpyDeviceToHost));
+  if (rc == SCT_OK && nq) {  // (the copies wait for the query; the plan's tables are freed after)
+    hipError_t e = hipMemcpy(index, di.p, (size_t)nq * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(dist, dd.p, (size_t)nq, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = sct::fail(SCT_E_HIP, "nearest: %s", hipGetErrorString(e));
   }
-  return SCT_OK;
+  sct_nearest_plan_destroy(plan);
+  return rc;
 }

@@ -54,6 +54,11 @@ struct HostStage {
 };
 // nullptr (with the error set) if the stage cannot be created.
 HostStage* host_stage();
+// True when all of [p, p + bytes) lies in ONE page-locked host allocation the HIP runtime knows
+// (hipHostMalloc, torch pin_memory, a caller's own hipHostRegister): DMA may then use the caller's
+// memory directly.  The library itself never registers or unregisters caller memory -- pageable
+// arrays are copied through the stage's own pinned buffer instead.
+bool host_range_pinned(const void* p, size_t bytes);
 int stage_reserve(HostStage* st, size_t pinned_bytes, size_t dev_bytes);
 // Calls of at most this many bytes (inputs + outputs) run zero-copy on the pinned buffer.
 constexpr size_t kZeroCopyBytes = 64 << 10;

@@ -169,6 +169,8 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
 // (host; one synchronisation); scratch from the plan's workspace slot W_PROBE
 int probe(Workspace* ws, const uint64_t* d_codes, int64_t n, unsigned long long* out);
 void destroy(State& st);
+// wait for every piece of work the plan enqueued (its recorded streams' events)
+void wait_idle(State& st);
 // group the codes by column + bit planes (any slice range needs all of them)
 int build(State& st, const uint64_t* d_codes, hipStream_t s);
 // add the counts of slices [z_begin, z_end): d_counts[1 + w] += S_w over those slices,

@@ -1200,12 +1200,17 @@ int create(State& st, const uint64_t* d_codes, int64_t n, int64_t chunk, int cus
   return SCT_OK;
 }
 
-void destroy(State& st) {
-  // the plan's work has to be done before its buffers serve another plan (or are freed)
+void wait_idle(State& st) {
   for (auto& u : st.used) {
     (void)hipEventSynchronize(u.second);
     (void)hipEventDestroy(u.second);
   }
+  st.used.clear();
+}
+
+void destroy(State& st) {
+  // the plan's work has to be done before its buffers serve another plan (or are freed)
+  wait_idle(st);
   for (void* p : {(void*)st.d_hi, (void*)st.d_off, (void*)st.d_cnt, (void*)st.d_gofs, (void*)st.d_planes,
                   (void*)st.d_hist, st.d_buf, (void*)st.d_order, (void*)st.d_sumsq, st.d_sumsq_tmp})
     ws_put(st.ws, p);

@@ -916,6 +916,46 @@ def test_encode_stream_pipeline():
 
 
 # ---------------------------------------------------------------- headline sizes vs the oracle
+def test_encode_stream_pinned_and_pageable():
+    """The host stream copies page-locked buffers in place and pageable ones through its own pinned
+    stage (it never registers caller memory): both give the same codes, GC and flags, for inputs
+    and outputs pinned or not, a view into a larger block, and ranges that run past a pinned block."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(57)
+    n, L = 2_500_003, 16
+    seqs = np.frombuffer(b"ACGTN", np.uint8)[rng.integers(0, 5, (n, L))]
+    want = _lib.encode_stream(2, seqs, chunk=1 << 20)
+    assert not _lib.host_pinned(seqs)
+    pin = torch.empty((n + 5, L), dtype=torch.uint8, pin_memory=True).numpy()
+    pin[:n] = seqs
+    assert _lib.host_pinned(pin) and _lib.host_pinned(pin[3:n])
+    big = torch.empty((n + 5) * L + 4096, dtype=torch.uint8, pin_memory=True).numpy()
+    base = big.ctypes.data
+    assert _lib.host_pinned(big)
+    # a range that starts inside the block and runs past its end (1 TiB) is not in place
+    import ctypes
+    out = ctypes.c_int(7)
+    _lib.check(_lib.lib().sct_host_pinned(ctypes.c_void_p(base + 64), 1 << 40, ctypes.byref(out)))
+    assert out.value == 0
+    codes = torch.empty(n, dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+    gc = torch.empty(n, dtype=torch.uint8, pin_memory=True).numpy()
+    fl = torch.empty(n, dtype=torch.uint8, pin_memory=True).numpy()
+    f = _lib.lib().sct_encode_stream_host
+    for src in (pin[:n], seqs):
+        for outs in ((codes, gc, fl), tuple(np.zeros_like(a) for a in (codes, gc, fl))):
+            for a in outs:
+                a[:] = 0
+            _lib.check(f(2, _lib._ptr(src), n, L, _lib._ptr(outs[0]), _lib._ptr(outs[1]), _lib._ptr(outs[2]), 0))
+            for a, b in zip(outs, want):
+                assert np.array_equal(a, b)
+    # a pinned input view that is not at its block's start; a one-record and a two-chunk stream
+    got = _lib.encode_stream(2, pin[3:n], chunk=1 << 19)
+    for a, b in zip(got, want):
+        assert np.array_equal(a, b[3:])
+    one = _lib.encode_stream(2, seqs[:1])
+    assert int(one[0][0]) == int(want[0][0])
+
+
 def test_allpairs_737k_spectral_bin_for_bin():
     """Config 2 at full size: AUTO (= SPECTRAL) histogram of all 271,790,530,560 pairs,
     bin for bin against the C oracle's AVX-512 popcount loop over every pair."""
