@@ -100,6 +100,13 @@ int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, int L, uint
  * runs past its allocation). */
 int sct_host_pinned(const void* p, int64_t bytes, int* pinned);
 
+/* Page-locked host blocks (hipHostMalloc) for the Python layer's pinned array pool: the host
+ * stream paths (FASTQ pieces read from files, their extracted rows, stream-encoded codes,
+ * nearest results) then cross PCIe by DMA in place, and a block handed back to the pool is
+ * reused without new page faults.  sct_host_free(NULL) is a no-op. */
+int sct_host_alloc(int64_t bytes, void** ptr);
+int sct_host_free(void* ptr);
+
 /* Variable-length records (device): record r = starts[r] .. starts[r] + lens[r] of buf,
  * encoded as encodings.py:75-88 / :155-167 do into `words` limbs (words >= ceil(kind*len/64)
  * for every record); gc (nullable, saturating at 255) and flags as sct_encode. */

@@ -17,9 +17,11 @@ def release_device_memory():
     ``Barcodes.summarize_hamming_distances`` on a large set (SPECTRAL) keeps its
     per-device workspace -- up to 4 GiB of transform intermediate -- so the next call maps nothing.
     A process that shares the GPU with another framework can hand that memory back here; the next
-    summary call allocates it again (process exit frees it as well)."""
+    summary call allocates it again (process exit frees it as well).  The idle page-locked host
+    blocks the streaming paths keep for their next arrays (``_lib.pinned``) are freed too."""
     from . import _lib
     if _lib._lib is not None:  # nothing to free before the library was loaded
         _lib.release_plan_cache()
+        _lib.pinned.trim()
 
 __version__ = "0.1.0"

@@ -10,6 +10,7 @@ as ``RuntimeError`` with the library's message.
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -52,6 +53,8 @@ SIGNATURES = {
     "sct_encode_host": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp],
     "sct_encode_stream_host": [_i32, _vp, _i64, _i32, _vp, _vp, _vp, _i64],
     "sct_host_pinned": [_vp, _i64, _vp],
+    "sct_host_alloc": [_i64, _vp],
+    "sct_host_free": [_vp],
     "sct_encode_var": [_i32, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp],
     "sct_lines": [_vp, _i64, _i64, _vp, _vp, ctypes.POINTER(_i64), ctypes.POINTER(_i32), _vp],
     "sct_whitelist_encode": [_vp, _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -309,9 +312,9 @@ def encode_stream(kind, seqs, chunk=0):
     pipelined H2D/encode/D2H stream (one limb per code)."""
     seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
     n, L = seqs.shape
-    codes = np.empty(n, dtype=np.uint64)
-    gc = np.empty(n, dtype=np.uint8)
-    flags = np.empty(n, dtype=np.uint8)
+    codes = pinned.empty(n, np.uint64)
+    gc = pinned.empty(n, np.uint8)
+    flags = pinned.empty(n, np.uint8)
     check(lib().sct_encode_stream_host(kind, _ptr(seqs), n, L, _ptr(codes), _ptr(gc), _ptr(flags), chunk))
     return codes, gc, flags
 
@@ -321,6 +324,79 @@ def host_pinned(arr):
     out = _i32(0)
     check(lib().sct_host_pinned(_vp(arr.ctypes.data), arr.nbytes, ctypes.byref(out)))
     return bool(out.value)
+
+
+class PinnedPool:
+    """Page-locked host blocks (sct_host_alloc) behind numpy arrays: the host stream paths read
+    files into them and copy device results into them, so every PCIe crossing is a DMA in place
+    and a reused block takes no page faults.  An array (with every view of it) hands its block
+    back when it is freed; up to ``keep_bytes`` of idle blocks stay for the next arrays, the rest
+    are freed.  Small arrays, and every array once page-locked memory is refused (no GPU, or the
+    allocation fails), are plain numpy arrays."""
+
+    MIN_BYTES = 1 << 20
+
+    def __init__(self, keep_bytes=2 << 30):
+        self.keep_bytes = int(keep_bytes)
+        self._free = {}  # size class -> [pointer]
+        self._idle = 0
+        self._mu = threading.Lock()
+        self._ok = True
+        self._types = {}
+
+    @staticmethod
+    def _class(nbytes):
+        c = PinnedPool.MIN_BYTES
+        while c < nbytes:
+            c <<= 1
+        return c
+
+    def empty(self, shape, dtype=np.uint8):
+        shape = (shape,) if isinstance(shape, (int, np.integer)) else tuple(shape)
+        dtype = np.dtype(dtype)
+        count = int(np.prod(shape, dtype=np.int64)) if shape else 1
+        nbytes = count * dtype.itemsize
+        if nbytes < self.MIN_BYTES or not self._ok:
+            return np.empty(shape, dtype)
+        c = self._class(nbytes)
+        with self._mu:
+            blocks = self._free.get(c)
+            ptr = blocks.pop() if blocks else None
+            if ptr is not None:
+                self._idle -= c
+        if ptr is None:
+            p = _vp()
+            if lib().sct_host_alloc(c, ctypes.byref(p)) != SCT_OK or not p.value:
+                self._ok = False  # (no GPU, or page-locked memory refused: plain arrays from now on)
+                return np.empty(shape, dtype)
+            ptr = p.value
+        t = self._types.get(c)
+        if t is None:
+            t = self._types[c] = ctypes.c_uint8 * c
+        buf = t.from_address(ptr)
+        fin = weakref.finalize(buf, self._release, ptr, c)
+        fin.atexit = False  # (at interpreter exit the process returns the memory)
+        return np.frombuffer(buf, dtype=dtype, count=count).reshape(shape)
+
+    def _release(self, ptr, c):
+        with self._mu:
+            if self._idle + c <= self.keep_bytes:
+                self._free.setdefault(c, []).append(ptr)
+                self._idle += c
+                return
+        lib().sct_host_free(_vp(ptr))
+
+    def trim(self):
+        """Free every idle block."""
+        with self._mu:
+            ptrs = [p for blocks in self._free.values() for p in blocks]
+            self._free.clear()
+            self._idle = 0
+        for p in ptrs:
+            lib().sct_host_free(_vp(p))
+
+
+pinned = PinnedPool()
 
 
 def whitelist_encode(data, kind=2):
@@ -514,10 +590,11 @@ class FastqStream:
         del data
         nr = n.value
         widths = [b - a for a, b in self.spans]
-        seq = np.zeros(max(1, nr * sum(widths)), dtype=np.uint8)
-        qual = np.zeros_like(seq) if self.qualities else None
-        slen = np.zeros(max(1, nr * len(widths)), dtype=np.int32)
-        qlen = np.zeros_like(slen) if self.qualities else None
+        # (the fetch fills every element; page-locked rows come back by DMA in place)
+        seq = pinned.empty(max(1, nr * sum(widths)), np.uint8)
+        qual = pinned.empty(seq.size, np.uint8) if self.qualities else None
+        slen = pinned.empty(max(1, nr * len(widths)), np.int32)
+        qlen = pinned.empty(slen.size, np.int32) if self.qualities else None
         check(self._lib.sct_fastq_stream_fetch(self._h, _ptr(seq), _ptr(qual), _ptr(slen), _ptr(qlen)))
         out, off = [], 0
         for k, w in enumerate(widths):
@@ -589,8 +666,8 @@ def nearest(kind, whitelist, queries, max_d=1, code_bits=None):
     q = np.ascontiguousarray(queries, dtype=np.uint64).reshape(-1)
     if code_bits is None:
         code_bits = max(1, int(np.bitwise_or.reduce(wl)).bit_length() if wl.size else 1)
-    index = np.zeros(q.size, dtype=np.int32)
-    dist = np.zeros(q.size, dtype=np.uint8)
+    index = pinned.empty(q.size, np.int32)
+    dist = pinned.empty(q.size, np.uint8)
     check(lib().sct_nearest_host(kind, _ptr(wl), wl.size, _ptr(q), q.size, code_bits, max_d,
                                  _ptr(index), _ptr(dist)))
     return index, dist

@@ -1261,14 +1261,20 @@ extern "C" int sct_fastq_stream_chunk(sct_fastq_stream* s, const uint8_t* buf, i
     SCT_HIP(hipMalloc(&s->d_buf, (size_t)nbytes));
     s->buf_cap = nbytes;
   }
-  // through the stage's pinned buffer in 64 MB pieces: page-locked copies, no per-call pinning
-  constexpr size_t kPiece = 64ull << 20;
-  SCT_TRY(sct::stage_reserve(s->st, std::min<size_t>((size_t)nbytes, kPiece), 0));
-  for (int64_t o = 0; o < nbytes; o += (int64_t)kPiece) {
-    const size_t len = (size_t)std::min<int64_t>((int64_t)kPiece, nbytes - o);
-    SCT_HIP(hipStreamSynchronize(hs));  // the previous piece's copy has left the pinned buffer
-    memcpy(s->st->pinned, buf + o, len);
-    SCT_HIP(hipMemcpyAsync((uint8_t*)s->d_buf + o, s->st->pinned, len, hipMemcpyHostToDevice, hs));
+  if (sct::host_range_pinned(buf, (size_t)nbytes)) {
+    // a page-locked piece (the Python layer reads the files into one): one DMA in place; the
+    // call returns only after a synchronisation of `hs`, so the caller may refill it afterwards
+    if (nbytes) SCT_HIP(hipMemcpyAsync(s->d_buf, buf, (size_t)nbytes, hipMemcpyHostToDevice, hs));
+  } else {
+    // through the stage's pinned buffer in 64 MB pieces: page-locked copies, no per-call pinning
+    constexpr size_t kPiece = 64ull << 20;
+    SCT_TRY(sct::stage_reserve(s->st, std::min<size_t>((size_t)nbytes, kPiece), 0));
+    for (int64_t o = 0; o < nbytes; o += (int64_t)kPiece) {
+      const size_t len = (size_t)std::min<int64_t>((int64_t)kPiece, nbytes - o);
+      SCT_HIP(hipStreamSynchronize(hs));  // the previous piece's copy has left the pinned buffer
+      memcpy(s->st->pinned, buf + o, len);
+      SCT_HIP(hipMemcpyAsync((uint8_t*)s->d_buf + o, s->st->pinned, len, hipMemcpyHostToDevice, hs));
+    }
   }
   sct_fastq_index* ix = nullptr;
   SCT_TRY(sct_fastq_index_create((const uint8_t*)s->d_buf, nbytes, file_ends, nfiles, s->text, hs, &ix));
@@ -1307,6 +1313,7 @@ extern "C" int sct_fastq_stream_chunk(sct_fastq_stream* s, const uint8_t* buf, i
       used = e;
     }
   }
+  if (final) SCT_HIP(hipStreamSynchronize(hs));  // (the piece's buffer is the caller's again)
   s->nrec = nrec;
   s->first_bad = bad;
   s->consumed = used;

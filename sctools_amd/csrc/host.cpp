@@ -162,6 +162,23 @@ extern "C" int sct_host_pinned(const void* p, int64_t bytes, int* pinned) {
   return SCT_OK;
 }
 
+extern "C" int sct_host_alloc(int64_t bytes, void** ptr) {
+  SCT_CHECK(ptr != nullptr && bytes > 0, "bad arguments");
+  *ptr = nullptr;
+  const hipError_t e = hipHostMalloc(ptr, (size_t)bytes, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *ptr = nullptr;
+    return sct::fail(SCT_E_NOMEM, "hipHostMalloc(%lld): %s", (long long)bytes, hipGetErrorString(e));
+  }
+  return SCT_OK;
+}
+
+extern "C" int sct_host_free(void* ptr) {
+  if (ptr) SCT_HIP(hipHostFree(ptr));
+  return SCT_OK;
+}
+
 extern "C" int sct_version(void) { return 1; }
 
 extern "C" const char* sct_last_error(void) { return sct::last_error(); }

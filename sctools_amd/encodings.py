@@ -39,9 +39,9 @@ def _as_bytes(seq):
 def _records(seqs):
     """Batch input -> (n, L) uint8 array of equal-length records."""
     if isinstance(seqs, np.ndarray):
-        if seqs.dtype.kind == "S":
+        if seqs.dtype.kind == "S":  # (a view of the rows: no copy)
             L = seqs.dtype.itemsize
-            return np.frombuffer(np.ascontiguousarray(seqs).tobytes(), dtype=np.uint8).reshape(-1, L)
+            return np.ascontiguousarray(seqs).reshape(-1).view(np.uint8).reshape(-1, L)
         if seqs.dtype == np.uint8 and seqs.ndim == 2:
             return np.ascontiguousarray(seqs)
         raise TypeError("expected an 'S<L>' array or an (n, L) uint8 array")

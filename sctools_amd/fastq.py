@@ -58,6 +58,21 @@ def _open_binary(name):
 CHUNK_BYTES = 256 << 20
 
 
+def _last_line_end(buf, have):
+    """1 + the position of the last '\\n' in buf[:have] (0 if none), searching back from the end
+    in growing windows (a piece's last line end is normally within its last record)."""
+    w = 1 << 16
+    hi = have
+    while hi > 0:
+        lo = max(0, hi - w)
+        hits = np.flatnonzero(buf[lo:hi] == 10)
+        if hits.size:
+            return lo + int(hits[-1]) + 1
+        hi = lo
+        w <<= 1
+    return 0
+
+
 class EmbeddedBarcodeGenerator:
     """fastq.py:165-200 on the device.  ``embedded_barcodes``: EmbeddedBarcode tuples with
     non-negative int start <= end."""
@@ -82,36 +97,47 @@ class EmbeddedBarcodeGenerator:
         their last '\\n'; the device extracts each piece's complete records and says where
         the next piece starts (a record cut by the piece end is carried over, also across a
         file boundary).  Yields (first record number, nrecords, first bad-name record of the
-        piece or -1, per-span arrays)."""
-        chunk_bytes = int(chunk_bytes or CHUNK_BYTES)
+        piece or -1, per-span arrays).
+
+        The files are read (``readinto``) straight into one page-locked buffer that the device
+        copies by DMA in place; the carried-over tail moves to its front.  A piece with no
+        complete record (one record longer than the buffer) doubles the buffer."""
+        chunk_bytes = max(1, int(chunk_bytes or CHUNK_BYTES))
         st = _lib.FastqStream([(eb.start, eb.end) for eb in self.embedded_barcodes], self._mode == 'r', qualities)
-        pending = bytearray()
-        ends = []  # file ends inside `pending`
+        buf = _lib.pinned.empty(chunk_bytes, np.uint8)
+        have = 0   # bytes of buf holding file data (the carried tail first)
+        ends = []  # file ends inside buf[:have]
         done = 0
         try:
             for name in self._files:
                 with _open_binary(name) as f:
                     while True:
-                        data = f.read(chunk_bytes)
-                        if not data:
+                        if have == buf.size:  # a record longer than the buffer: grow it
+                            bigger = _lib.pinned.empty(2 * buf.size, np.uint8)
+                            bigger[:have] = buf[:have]
+                            buf = bigger
+                        got = f.readinto(memoryview(buf)[have:])
+                        if not got:
                             break
-                        pending += data
-                        while len(pending) >= chunk_bytes:
-                            cut = pending.rfind(b'\n') + 1
-                            if cut <= 0:
-                                break  # no line ends yet: read on
-                            n, used, bad, parts = st.chunk(pending, cut, [e for e in ends if e < cut] + [cut],
-                                                           final=False)
-                            yield done, n, bad, parts
-                            if bad >= 0:
-                                return
-                            done += n
-                            del pending[:used]
+                        have += got
+                        if have < buf.size:
+                            continue  # fill the piece
+                        cut = _last_line_end(buf, have)
+                        if cut <= 0:
+                            continue  # no line ends yet: read on (the buffer grows)
+                        n, used, bad, parts = st.chunk(buf, cut, [e for e in ends if e < cut] + [cut],
+                                                       final=False)
+                        yield done, n, bad, parts
+                        if bad >= 0:
+                            return
+                        done += n
+                        if used:
+                            rest = have - used
+                            buf[:rest] = buf[used:have]  # (numpy copies overlapping ranges safely)
+                            have = rest
                             ends = [e - used for e in ends if e > used]
-                            if used == 0:
-                                break  # no complete record in the piece: read on
-                ends.append(len(pending))
-            n, _, bad, parts = st.chunk(pending, len(pending), ends or [0], final=True)
+                ends.append(have)
+            n, _, bad, parts = st.chunk(buf, have, ends or [0], final=True)
             yield done, n, bad, parts
         finally:
             st.close()
@@ -181,10 +207,10 @@ class EmbeddedBarcodeGenerator:
             for eb, (seq, slen, qual, qlen) in zip(self.embedded_barcodes, parts):
                 w = eb.end - eb.start
                 out[eb.sequence_tag] = (np.ascontiguousarray(seq[:stop]).view('S%d' % w).reshape(stop) if w else
-                                        np.zeros(stop, dtype='S1'), slen[:stop].copy())
+                                        np.zeros(stop, dtype='S1'), slen[:stop])
                 if qualities:
                     out[eb.quality_tag] = (np.ascontiguousarray(qual[:stop]).view('S%d' % w).reshape(stop) if w else
-                                           np.zeros(stop, dtype='S1'), qlen[:stop].copy())
+                                           np.zeros(stop, dtype='S1'), qlen[:stop])
             yield out
             if bad >= 0:
                 raise ValueError('fastq name must start with @')

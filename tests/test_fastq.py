@@ -128,6 +128,18 @@ def test_fastq_synthetic_large_text_vs_python(tmp_path):
 
 
 # ---------------------------------------------------------------- streaming (pieces)
+def test_last_line_end_windows():
+    """The piece cut: 1 + the last '\\n' in buf[:have], found back from the end in growing windows."""
+    buf = np.full(300_000, ord("A"), np.uint8)
+    assert fastq._last_line_end(buf, buf.size) == 0
+    buf[5] = 10
+    assert fastq._last_line_end(buf, buf.size) == 6  # (found in the widest window)
+    buf[250_000] = 10
+    assert fastq._last_line_end(buf, buf.size) == 250_001
+    assert fastq._last_line_end(buf, 250_000) == 6  # (a '\\n' at or past `have` is not seen)
+    assert fastq._last_line_end(buf, 0) == 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("chunk", [7, 64, 333])
 def test_fastq_golden_cases_in_small_pieces(fq_golden, tmp_path, monkeypatch, chunk):

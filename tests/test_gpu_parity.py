@@ -916,6 +916,33 @@ def test_encode_stream_pipeline():
 
 
 # ---------------------------------------------------------------- headline sizes vs the oracle
+def test_pinned_pool_blocks_reused_after_last_view():
+    """_lib.pinned: arrays over page-locked blocks (DMA in place); a block goes back to the pool
+    only when the last view of its array is freed, and the next array of its size class reuses it."""
+    import gc as _gc
+    pool = _lib.PinnedPool(keep_bytes=64 << 20)
+    a = pool.empty((3 << 20,), np.uint8)
+    assert _lib.host_pinned(a)
+    p0 = a.ctypes.data
+    a[:] = 7
+    v = a[1000:2000]
+    del a
+    _gc.collect()
+    b = pool.empty(3 << 20, np.uint8)
+    assert b.ctypes.data != p0  # the view still holds the first block
+    assert int(v.sum()) == 7 * 1000
+    del v
+    _gc.collect()
+    c = pool.empty((2 << 20, 2), np.uint8)  # same 4 MiB class: the first block again
+    assert c.ctypes.data == p0 and _lib.host_pinned(c)
+    small = pool.empty(100, np.int32)  # below MIN_BYTES: plain numpy
+    assert small.shape == (100,) and not _lib.host_pinned(small)
+    del b, c
+    _gc.collect()
+    pool.trim()
+    assert pool._idle == 0 and not pool._free
+
+
 def test_encode_stream_pinned_and_pageable():
     """The host stream copies page-locked buffers in place and pageable ones through its own pinned
     stage (it never registers caller memory): both give the same codes, GC and flags, for inputs

@@ -1,9 +1,9 @@
-# Round 5: the host stream no longer registers caller memory (pageable buffers go through the
-# library's pinned stage): the FASTQ -> nearest flow, the whole GPU suite (any failure ends the
-# call), then one default bench line.
+# Round 5: host stream paths on page-locked pool arrays (FASTQ pieces read into a pinned buffer and
+# DMAed in place, rows / codes / nearest results in pool blocks): the FASTQ -> nearest flow, the
+# whole GPU suite (any failure ends the call), then one default bench line.
 set -u
 cd "$GRAFT_REPO_ROOT"
-P=gpurun_out/r5h
+P=gpurun_out/r5i
 mkdir -p $P
 export TMPDIR=/tmp
 timeout -k 10 300 python3 tools/fastq_flow_breakdown.py > $P/fastq_flow.json 2> $P/fastq_flow.err || exit 3
