@@ -19,6 +19,8 @@ filenames, modes 'r' (text: universal newlines, str fields) and 'rb' (bytes fiel
 
 import bz2
 import gzip
+import queue
+import threading
 from collections import namedtuple
 from collections.abc import Iterable
 
@@ -56,6 +58,67 @@ def _open_binary(name):
 
 #: bytes per piece handed to the device (the files are read lazily, piece by piece)
 CHUNK_BYTES = 256 << 20
+
+
+#: bytes in front of every piece buffer for the tail carried over from the previous piece
+_HEADROOM = 1 << 20
+
+
+class _PieceReader(threading.Thread):
+    """Fills page-locked piece buffers from the files, one buffer ahead of the consumer: each
+    buffer in `free` comes back through `full` as (buffer, bytes read at [head, head + n), the
+    file ends among them, whether every file is exhausted), or an exception raised while
+    opening or reading (raised by the consumer in its turn).  The read releases the GIL."""
+
+    def __init__(self, files, buffers, head):
+        super().__init__(name="sctools-fastq-reader", daemon=True)
+        self._files = list(files)
+        self._head = head
+        self._halt = False
+        self.free = queue.Queue()
+        self.full = queue.Queue()
+        for b in buffers:
+            self.free.put(b)
+
+    def run(self):
+        f = None
+        names = iter(self._files)
+        try:
+            last = False
+            while not last:
+                buf = self.free.get()
+                if buf is None or self._halt:
+                    return
+                mv = memoryview(buf)[self._head:]
+                n, ends, cap = 0, [], buf.size - self._head
+                while n < cap:
+                    if f is None:
+                        name = next(names, None)
+                        if name is None:
+                            last = True
+                            break
+                        f = _open_binary(name)
+                    got = f.readinto(mv[n:])
+                    if not got:
+                        f.close()
+                        f = None
+                        ends.append(n)
+                        continue
+                    n += got
+                del mv
+                self.full.put((buf, n, ends, last))
+        except BaseException as e:  # (handed to the consumer)
+            self.full.put(e)
+        finally:
+            if f is not None:
+                f.close()
+
+    def close(self):
+        """Stop after the current read (a consumer that stops early): the thread holds its own
+        references to any buffer it is still filling, so a block is never reused under it."""
+        self._halt = True
+        self.free.put(None)
+        self.join(timeout=10.0)
 
 
 def _last_line_end(buf, have):
@@ -99,47 +162,56 @@ class EmbeddedBarcodeGenerator:
         file boundary).  Yields (first record number, nrecords, first bad-name record of the
         piece or -1, per-span arrays).
 
-        The files are read (``readinto``) straight into one page-locked buffer that the device
-        copies by DMA in place; the carried-over tail moves to its front.  A piece with no
-        complete record (one record longer than the buffer) doubles the buffer."""
+        A reader thread (`_PieceReader`) fills one page-locked buffer while the device and the
+        caller work on the other, so the file reads overlap everything else; the device copies
+        each piece by DMA in place.  The carried-over tail goes into the headroom in front of
+        the next piece (a tail longer than the headroom -- a record longer than a megabyte --
+        is merged with the next piece in a new buffer)."""
         chunk_bytes = max(1, int(chunk_bytes or CHUNK_BYTES))
+        head = _HEADROOM
         st = _lib.FastqStream([(eb.start, eb.end) for eb in self.embedded_barcodes], self._mode == 'r', qualities)
-        buf = _lib.pinned.empty(chunk_bytes, np.uint8)
-        have = 0   # bytes of buf holding file data (the carried tail first)
-        ends = []  # file ends inside buf[:have]
+        reader = _PieceReader(self._files, [_lib.pinned.empty(head + chunk_bytes, np.uint8) for _ in range(2)], head)
+        reader.start()
+        carry = np.zeros(0, np.uint8)  # the unconsumed tail of the last piece (a copy)
+        carry_ends = []                # file ends inside it
         done = 0
         try:
-            for name in self._files:
-                with _open_binary(name) as f:
-                    while True:
-                        if have == buf.size:  # a record longer than the buffer: grow it
-                            bigger = _lib.pinned.empty(2 * buf.size, np.uint8)
-                            bigger[:have] = buf[:have]
-                            buf = bigger
-                        got = f.readinto(memoryview(buf)[have:])
-                        if not got:
-                            break
-                        have += got
-                        if have < buf.size:
-                            continue  # fill the piece
-                        cut = _last_line_end(buf, have)
-                        if cut <= 0:
-                            continue  # no line ends yet: read on (the buffer grows)
-                        n, used, bad, parts = st.chunk(buf, cut, [e for e in ends if e < cut] + [cut],
-                                                       final=False)
-                        yield done, n, bad, parts
-                        if bad >= 0:
-                            return
-                        done += n
-                        if used:
-                            rest = have - used
-                            buf[:rest] = buf[used:have]  # (numpy copies overlapping ranges safely)
-                            have = rest
-                            ends = [e - used for e in ends if e > used]
-                ends.append(have)
-            n, _, bad, parts = st.chunk(buf, have, ends or [0], final=True)
-            yield done, n, bad, parts
+            while True:
+                got = reader.full.get()
+                if isinstance(got, BaseException):
+                    raise got
+                buf, n, seg_ends, last = got
+                c = carry.size
+                if c <= head:  # the tail goes in front of the segment, in the same buffer
+                    buf[head - c:head] = carry
+                    piece = buf[head - c:head + n]
+                    release = buf
+                else:  # (a tail longer than the headroom: one merged buffer)
+                    piece = _lib.pinned.empty(c + n, np.uint8)
+                    piece[:c] = carry
+                    piece[c:] = buf[head:head + n]
+                    reader.free.put(buf)
+                    release = None
+                ends = carry_ends + [c + e for e in seg_ends]
+                if last:
+                    nrec, _, bad, parts = st.chunk(piece, piece.size, ends or [0], final=True)
+                    yield done, nrec, bad, parts
+                    return
+                cut = _last_line_end(piece, piece.size)
+                used = 0
+                if cut > 0:
+                    nrec, used, bad, parts = st.chunk(piece, cut, [e for e in ends if e < cut] + [cut], final=False)
+                    yield done, nrec, bad, parts
+                    if bad >= 0:
+                        return
+                    done += nrec
+                carry = piece[used:].copy()  # (no line end, or no complete record yet: all of it)
+                carry_ends = [e - used for e in ends if e > used]
+                del piece
+                if release is not None:
+                    reader.free.put(release)
         finally:
+            reader.close()
             st.close()
 
     def _run(self, qualities=True):

@@ -128,6 +128,108 @@ def test_fastq_synthetic_large_text_vs_python(tmp_path):
 
 
 # ---------------------------------------------------------------- streaming (pieces)
+class _FakeStream:
+    """A host stand-in for sct_fastq_stream with the device's record rules (lines end at '\\n'
+    and at file ends; records are 4 lines over all files; a non-final piece reports the bytes
+    of its complete records), so the piece logic of _pieces -- the read-ahead thread, the
+    carried tail, the file ends -- is checked on the CPU against one whole-input call."""
+
+    def __init__(self, spans, text_mode, qualities=True):
+        self.spans, self.qualities = [tuple(x) for x in spans], qualities
+
+    def chunk(self, buf, nbytes, file_ends, final):
+        data = bytes(np.asarray(buf)[:nbytes])
+        cuts = sorted(set([e for e in file_ends if 0 < e <= nbytes]))
+        lines, pos = [], 0  # (start, end without '\\n', next start)
+        while pos < nbytes:
+            nl = data.find(b"\n", pos)
+            stop = min([c for c in cuts if c > pos] + [nbytes])
+            if nl < 0 or nl >= stop:
+                if stop < nbytes or final or stop in cuts:
+                    lines.append((pos, stop, stop))
+                pos = stop
+                continue
+            lines.append((pos, nl, nl + 1))
+            pos = nl + 1
+        nrec = len(lines) // 4
+        used = lines[4 * nrec - 1][2] if nrec else 0
+        bad = next((r for r in range(nrec) if data[lines[4 * r][0]:lines[4 * r][0] + 1] != b"@"), -1)
+        parts = []
+        for a, b in self.spans:
+            w = b - a
+            seq = np.zeros((nrec, w), np.uint8)
+            qual = np.zeros((nrec, w), np.uint8)
+            sl = np.zeros(nrec, np.int32)
+            ql = np.zeros(nrec, np.int32)
+            for r in range(nrec):
+                for li, arr, ln in ((1, seq, sl), (3, qual, ql)):
+                    st, en, _ = lines[4 * r + li]
+                    x = data[st:en][a:b]
+                    arr[r, :len(x)] = np.frombuffer(x, np.uint8)
+                    ln[r] = len(x)
+            parts.append((seq, sl, qual if self.qualities else None, ql if self.qualities else None))
+        return nrec, (nbytes if final else used), bad, parts
+
+    def close(self):
+        pass
+
+
+@pytest.mark.parametrize("chunk", [5, 23, 64, 1000, 1 << 16])
+def test_pieces_reader_carry_and_file_ends(tmp_path, monkeypatch, chunk):
+    """_pieces in pieces of `chunk` bytes (tails longer than the headroom when the headroom is
+    shrunk below a record) across files that cut records between any two lines, an empty file and a last file
+    with no final newline: the records, their order and the per-piece counts equal one call over
+    the whole input (host stand-in for the device: see _FakeStream)."""
+    rng = np.random.default_rng(chunk)
+    recs = []
+    for r in range(400):
+        L = int(rng.integers(0, 40))
+        recs += [b"@r%d\n" % r, bytes(rng.choice(list(b"ACGTN"), size=L).tolist()) + b"\n", b"+\n",
+                 bytes([70] * L) + b"\n"]
+    blob = b"".join(recs)
+    starts = np.cumsum([len(x) for x in recs])[:-1]  # files end between lines (inside records)
+    bounds = sorted(set(rng.choice(starts, 4).tolist()))
+    parts = [blob[i:j] for i, j in zip([0] + bounds, bounds + [len(blob)])]
+    parts.insert(2, b"")  # an empty file
+    parts[-1] = parts[-1][:-1]  # the last file has no final newline
+    paths = []
+    for k, part in enumerate(parts):
+        p = tmp_path / ("p%d.fastq" % k)
+        p.write_bytes(part)
+        paths.append(str(p))
+    monkeypatch.setattr(fastq._lib, "FastqStream", _FakeStream)
+    if chunk <= 64:
+        monkeypatch.setattr(fastq, "_HEADROOM", 8)  # tails outgrow the headroom: merged buffers
+    eb = [fastq.EmbeddedBarcode(0, 16, "CR", "CY"), fastq.EmbeddedBarcode(4, 9, "UR", "UY")]
+    gen = fastq.EmbeddedBarcodeGenerator(eb, paths, "rb")
+    got = list(gen._pieces(True, chunk))
+    # the whole input in one call, file ends at the files' ends
+    ends, acc = [], 0
+    for part in parts:
+        acc += len(part)
+        ends.append(acc)
+    whole = np.frombuffer(b"".join(parts), np.uint8)
+    n, _, bad, want = _FakeStream([(0, 16), (4, 9)], False).chunk(whole, whole.size, ends, True)
+    assert bad == -1 and n >= 399  # (399 when the last record's empty quality line was its final newline)
+    assert sum(g[1] for g in got) == n
+    assert [g[0] for g in got] == list(np.cumsum([0] + [g[1] for g in got[:-1]]))
+    for k in range(2):
+        for i in range(4):
+            cat = np.concatenate([g[3][k][i] for g in got])
+            assert np.array_equal(cat, want[k][i]), (k, i)
+
+
+def test_pieces_reader_propagates_open_errors(tmp_path, monkeypatch):
+    """A missing file raises FileNotFoundError from the generator (after the pieces before it)."""
+    p = tmp_path / "a.fastq"
+    p.write_bytes(b"@a\nACGT\n+\nFFFF\n" * 100)
+    monkeypatch.setattr(fastq._lib, "FastqStream", _FakeStream)
+    gen = fastq.EmbeddedBarcodeGenerator([fastq.EmbeddedBarcode(0, 4, "CR", "CY")],
+                                         [str(p), str(tmp_path / "missing.fastq")], "rb")
+    with pytest.raises(FileNotFoundError):
+        list(gen._pieces(True, 64))
+
+
 def test_last_line_end_windows():
     """The piece cut: 1 + the last '\\n' in buf[:have], found back from the end in growing windows."""
     buf = np.full(300_000, ord("A"), np.uint8)
