@@ -333,7 +333,9 @@ int sct_hamming_hist_allpairs_host_ex(const uint64_t* codes, int64_t n, int code
  * them allocated when destroyed, so repeated one-shot calls map no device memory (the
  * drop-in's summarize_hamming_distances, barcode.py:39-46, is one such call).  This frees
  * every idle cache (all devices); a cache lent to a live plan is freed when that plan is
- * destroyed.  sct_tune_set(SCT_TUNE_PLAN_CACHE, 0) turns the cache off. */
+ * destroyed.  sct_tune_set(SCT_TUNE_PLAN_CACHE, 0) turns the cache off.  The idle memory of
+ * the library's stream-ordered scratch pool (host-stream stages, ingest scratch) is trimmed
+ * too, after a synchronisation of the current device. */
 int sct_allpairs_cache_release(void);
 
 /* ---------------------------------------------------------------- all-pairs, wide codes

@@ -1368,5 +1368,7 @@ extern "C" int sct_hamming_hist_allpairs_host_ex(const uint64_t* codes, int64_t 
 
 extern "C" int sct_allpairs_cache_release(void) {
   sct_spectral::ws_release_all();
+  (void)hipDeviceSynchronize();  // (the stream-ordered frees have completed)
+  sct::pool_trim();
   return SCT_OK;
 }

@@ -1147,6 +1147,9 @@ extern "C" int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, 
                        sct::host_range_pinned(flags, (size_t)n);
   const bool staged = !pin_in || !pin_out;
   if (staged) chunk = std::min<int64_t>(chunk, 1 << 21);  // (a staged chunk: 2M reads, <= 2M * (L + 10) B)
+  // at least four chunks when there are enough records, so the three stages overlap even for one
+  // piece of a stream (a few million records)
+  chunk = std::min<int64_t>(chunk, std::max<int64_t>(1 << 18, sct::ceil_div(n, 4)));
   chunk = std::min<int64_t>(chunk, n);
   const size_t in_b = pin_in ? 0 : (((size_t)chunk * L + 255) & ~(size_t)255);
   const size_t out_b = pin_out ? 0 : (size_t)chunk * 10;
@@ -1157,7 +1160,6 @@ extern "C" int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, 
     SCT_TRY(sct::stage_reserve(hs, NSTAGE * (in_b + out_b), 0));
     stage = hs->pinned;
   }
-  sct::DevBuf din[NSTAGE], dcode[NSTAGE], dgc[NSTAGE], dfl[NSTAGE];
   hipStream_t st[NSTAGE] = {};
   struct Streams {
     hipStream_t* s;
@@ -1169,12 +1171,29 @@ extern "C" int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, 
         }
     }
   } guard{st};
+  // one device block per stage from the library's stream-ordered pool (records, then codes, GC,
+  // flags), freed on its stage's stream before the streams go (declared after the guard)
+  struct Blocks {
+    void* p[NSTAGE] = {};
+    hipStream_t* s;
+    ~Blocks() {
+      for (int k = 0; k < NSTAGE; ++k) sct::pool_free(p[k], s[k]);
+    }
+  } blk{{}, st};
+  const size_t rec_b = ((size_t)chunk * L + 255) & ~(size_t)255;
   for (int k = 0; k < NSTAGE; ++k) {
     SCT_HIP(hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking));
-    SCT_HIP(din[k].alloc((size_t)chunk * L));
-    SCT_HIP(dcode[k].alloc((size_t)chunk * 8));
-    SCT_HIP(dgc[k].alloc((size_t)chunk));
-    SCT_HIP(dfl[k].alloc((size_t)chunk));
+    SCT_HIP(sct::pool_alloc(&blk.p[k], rec_b + (size_t)chunk * 10, st[k]));
+  }
+  struct StageDev {
+    uint8_t* p;
+  } din[NSTAGE], dcode[NSTAGE], dgc[NSTAGE], dfl[NSTAGE];
+  for (int k = 0; k < NSTAGE; ++k) {
+    uint8_t* b = static_cast<uint8_t*>(blk.p[k]);
+    din[k].p = b;
+    dcode[k].p = b + rec_b;
+    dgc[k].p = b + rec_b + (size_t)chunk * 8;
+    dfl[k].p = b + rec_b + (size_t)chunk * 9;
   }
   // stage k's pinned buffers: the input chunk, then codes / GC / flags of the chunk in flight
   auto h_in = [&](int k) { return stage + (size_t)k * (in_b + out_b); };

@@ -103,12 +103,19 @@ int64_t tune(int key, int64_t dflt) {
 // pool, which PyTorch and other libraries share, is left alone).  Its release threshold is
 // raised once, so per-call scratch is reused from the pool instead of being mapped and unmapped
 // around every stream synchronisation.
+static std::mutex g_pool_mu;
+static hipMemPool_t g_pools[64] = {};
+
+static hipMemPool_t existing_pool(int dev) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  return dev >= 0 && dev < 64 ? g_pools[dev] : nullptr;
+}
+
 static hipMemPool_t private_pool(int dev) {
-  static std::mutex mu;
-  static hipMemPool_t pools[64] = {};
   static bool tried[64] = {};
+  hipMemPool_t* pools = g_pools;
   if (dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
+  std::lock_guard<std::mutex> lk(g_pool_mu);
   if (!tried[dev]) {
     tried[dev] = true;
     hipMemPoolProps props = {};
@@ -139,6 +146,13 @@ hipError_t pool_alloc(void** p, size_t bytes, hipStream_t s) {
 
 void pool_free(void* p, hipStream_t s) {
   if (p) (void)hipFreeAsync(p, s);
+}
+
+// hands the idle memory of every pool created so far back to the device (the callers have
+// synchronised the work that freed it)
+void pool_trim() {
+  for (int dev = 0; dev < 64; ++dev)
+    if (hipMemPool_t pool = existing_pool(dev)) (void)hipMemPoolTrimTo(pool, 0);
 }
 
 }  // namespace sct

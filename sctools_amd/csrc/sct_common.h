@@ -69,6 +69,8 @@ constexpr size_t kStageBytes = 256ull << 20;
 // Stream-ordered scratch from the library's private memory pool of the current device (host.cpp;
 // the device's default pool is not touched): released memory stays in the pool for the next call.
 hipError_t pool_alloc(void** p, size_t bytes, hipStream_t s);
+// every pool's idle memory back to the device (sct_allpairs_cache_release)
+void pool_trim();
 void pool_free(void* p, hipStream_t s);
 
 // sct_tune_set value of `key`, or dflt when unset (host.cpp).
