@@ -386,6 +386,15 @@ int sct_nearest_query(sct_nearest_plan* plan, const uint64_t* d_queries, int64_t
 int sct_nearest_plan_info(const sct_nearest_plan* plan, int* scheme, int64_t* index_bytes);
 int sct_nearest_host(int kind, const uint64_t* whitelist, int64_t nw, const uint64_t* queries,
                      int64_t nq, int code_bits, int max_d, int32_t* index, uint8_t* dist);
+/* A plan from a HOST whitelist (copied for the build, not kept), and queries from host memory
+ * against it: a stream of batches builds the index once (barcode.WhitelistCorrector).  The
+ * query call copies the queries in, runs sct_nearest_query on the thread's stream with scratch
+ * from the library's stream-ordered pool, and returns with index / dist in host memory
+ * (page-locked buffers are copied by DMA in place). */
+int sct_nearest_plan_create_host(int kind, const uint64_t* whitelist, int64_t nw, int code_bits, int max_d,
+                                 sct_nearest_plan** plan);
+int sct_nearest_query_host(sct_nearest_plan* plan, const uint64_t* queries, int64_t nq, int32_t* index,
+                           uint8_t* dist);
 
 /* ---------------------------------------------------------------- FASTQ barcode extraction
  * Replaces the per-record path reader.Reader.__iter__ (src/sctools/reader.py:56-85) ->

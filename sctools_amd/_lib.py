@@ -53,6 +53,8 @@ SIGNATURES = {
     "sct_encode_host": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp],
     "sct_encode_stream_host": [_i32, _vp, _i64, _i32, _vp, _vp, _vp, _i64],
     "sct_host_pinned": [_vp, _i64, _vp],
+    "sct_nearest_plan_create_host": [_i32, _vp, _i64, _i32, _i32, _vp],
+    "sct_nearest_query_host": [_vp, _vp, _i64, _vp, _vp],
     "sct_host_alloc": [_i64, _vp],
     "sct_host_free": [_vp],
     "sct_encode_var": [_i32, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp],
@@ -671,6 +673,37 @@ def nearest(kind, whitelist, queries, max_d=1, code_bits=None):
     check(lib().sct_nearest_host(kind, _ptr(wl), wl.size, _ptr(q), q.size, code_bits, max_d,
                                  _ptr(index), _ptr(dist)))
     return index, dist
+
+
+class HostNearestPlan:
+    """A nearest-whitelist plan built once from a host whitelist, queried with host arrays
+    (sct_nearest_plan_create_host / sct_nearest_query_host): results in page-locked pool arrays."""
+
+    def __init__(self, kind, whitelist, code_bits, max_d):
+        self._lib = lib()
+        self._h = _vp()
+        wl = np.ascontiguousarray(whitelist, dtype=np.uint64).reshape(-1)
+        self.kind, self.nw, self.max_d = kind, wl.size, max_d
+        check(self._lib.sct_nearest_plan_create_host(kind, _ptr(wl), wl.size, code_bits, max_d, ctypes.byref(self._h)))
+
+    def query(self, queries):
+        q = np.ascontiguousarray(queries, dtype=np.uint64).reshape(-1)
+        index = pinned.empty(q.size, np.int32)
+        dist = pinned.empty(q.size, np.uint8)
+        if q.size:
+            check(self._lib.sct_nearest_query_host(self._h, _ptr(q), q.size, _ptr(index), _ptr(dist)))
+        return index, dist
+
+    def close(self):
+        if self._h:
+            self._lib.sct_nearest_plan_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class NearestPlan:

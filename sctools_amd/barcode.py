@@ -19,7 +19,7 @@ from . import _lib, _pykeys
 from .encodings import TwoBit
 from .stats import base4_entropy
 
-__all__ = ["Barcodes", "ObservedBarcodeSet", "PriorBarcodeSet", "nearest_whitelist"]
+__all__ = ["Barcodes", "ObservedBarcodeSet", "PriorBarcodeSet", "WhitelistCorrector", "nearest_whitelist"]
 
 _MIXED_SIGNS = ('barcode codes mix negative and non-negative integers: their XOR is negative and the '
                 'reference\'s distance loop (encodings.py:118, `while difference:`) never terminates on it')
@@ -246,6 +246,38 @@ def _encode_lines(seqs):
     for i in sorted(pending):
         out[i] = TwoBit.encode(seqs[i])  # batch of one: draws in record order
     return out
+
+
+class WhitelistCorrector:
+    """``nearest_whitelist`` against one whitelist for a stream of query batches: the device
+    index of the whitelist is built once, here, and every ``nearest(queries)`` call only copies
+    its queries in and the results out (no reference counterpart).  The
+    whitelist is copied at construction: changing the caller's array afterwards changes nothing.
+
+    :return of nearest (np.ndarray[int32], np.ndarray[uint8]): index, distance -- as
+        ``nearest_whitelist``
+    """
+
+    def __init__(self, whitelist, max_distance=1, encoding='ThreeBit'):
+        self.kind = {'ThreeBit': 3, 'TwoBit': 2, 3: 3, 2: 2}[encoding]
+        self.max_distance = max_distance
+        wl = np.ascontiguousarray(np.asarray(whitelist, dtype=np.uint64)).reshape(-1)
+        self.size = wl.size
+        self._plan = None
+        if wl.size:
+            bits = max(int(np.bitwise_or.reduce(wl)).bit_length(), self.kind * (max_distance + 1))
+            self._plan = _lib.HostNearestPlan(self.kind, wl, min(64, bits), max_distance)
+
+    def nearest(self, queries):
+        q = np.ascontiguousarray(np.asarray(queries, dtype=np.uint64)).reshape(-1)
+        if self._plan is None:
+            return np.full(q.size, -1, np.int32), np.full(q.size, 255, np.uint8)
+        return self._plan.query(q)
+
+    def close(self):
+        if self._plan is not None:
+            self._plan.close()
+            self._plan = None
 
 
 def nearest_whitelist(queries, whitelist, max_distance=1, encoding='ThreeBit'):

@@ -994,3 +994,43 @@ extern "C" int sct_nearest_host(int kind, const uint64_t* whitelist, int64_t nw,
   sct_nearest_plan_destroy(plan);
   return rc;
 }
+
+extern "C" int sct_nearest_plan_create_host(int kind, const uint64_t* whitelist, int64_t nw, int code_bits, int max_d,
+                                            sct_nearest_plan** out) {
+  SCT_CHECK(out != nullptr, "plan is NULL");
+  SCT_CHECK(nw >= 0 && (nw == 0 || whitelist), "bad whitelist");
+  sct::DevBuf dw;
+  SCT_HIP(dw.alloc((size_t)nw * 8));
+  if (nw) SCT_HIP(hipMemcpy(dw.p, whitelist, (size_t)nw * 8, hipMemcpyHostToDevice));
+  const int rc = sct_nearest_plan_create(kind, (const uint64_t*)dw.p, nw, code_bits, max_d, nullptr, out);
+  SCT_HIP(hipStreamSynchronize(nullptr));  // (the build has read the whitelist before it is freed)
+  return rc;
+}
+
+extern "C" int sct_nearest_query_host(sct_nearest_plan* p, const uint64_t* queries, int64_t nq, int32_t* index,
+                                      uint8_t* dist) {
+  SCT_CHECK(p != nullptr, "plan is NULL");
+  SCT_CHECK(nq >= 0 && (nq == 0 || (queries && index && dist)), "bad arguments");
+  if (nq == 0) return SCT_OK;
+  sct::HostStage* hs = sct::host_stage();
+  if (!hs) return SCT_E_HIP;
+  hipStream_t s = hs->stream;
+  const size_t qb = ((size_t)nq * 8 + 255) & ~(size_t)255, ib = ((size_t)nq * 4 + 255) & ~(size_t)255;
+  void* blk = nullptr;
+  SCT_HIP(sct::pool_alloc(&blk, qb + ib + (size_t)nq, s));
+  uint8_t* b = static_cast<uint8_t*>(blk);
+  int rc = SCT_OK;
+  hipError_t e = hipMemcpyAsync(b, queries, (size_t)nq * 8, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) {
+    rc = sct_nearest_query(p, (const uint64_t*)b, nq, (int32_t*)(b + qb), b + qb + ib, s);
+    if (rc == SCT_OK) {
+      e = hipMemcpyAsync(index, b + qb, (size_t)nq * 4, hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipMemcpyAsync(dist, b + qb + ib, (size_t)nq, hipMemcpyDeviceToHost, s);
+    }
+  }
+  sct::pool_free(blk, s);
+  const hipError_t se = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = se;
+  if (rc == SCT_OK && e != hipSuccess) rc = sct::fail(SCT_E_HIP, "nearest query: %s", hipGetErrorString(e));
+  return rc;
+}

@@ -794,6 +794,43 @@ def test_nearest_halves_big_buckets(kind):
     assert np.array_equal(idx, ridx) and np.array_equal(dist, rdist)
 
 
+@pytest.mark.parametrize("kind,max_d", [(3, 1), (2, 1), (3, 0), (3, 2), (2, 2)])
+def test_whitelist_corrector_batches(kind, max_d):
+    """WhitelistCorrector (one device index, many host batches) against nearest_whitelist and
+    the brute force: several batches, an empty one, a page-locked one; the caller's whitelist
+    changed after construction changes nothing; an empty whitelist finds nothing."""
+    rng = np.random.default_rng(90 + 10 * kind + max_d)
+    L = 16
+    wl2 = synthetic.whitelist_codes(6000, L, seed=31 + kind)
+    wl = wl2 if kind == 2 else synthetic.two_to_three(wl2, L)
+    wl = np.concatenate([wl, wl[:5]])  # duplicates: ties
+    keep = wl.copy()
+    corr = barcode.WhitelistCorrector(wl, max_distance=max_d, encoding=kind)
+    wl[:] = 0  # (the corrector holds its own copy)
+    batches = []
+    for size in (5000, 0, 1, 12345):
+        q = keep[rng.integers(0, keep.size, size)]
+        pos = rng.integers(0, L, size).astype(np.uint64)
+        one = rng.random(size) < 0.5
+        w = np.uint64(kind)
+        sub = rng.integers(0, 4, size).astype(np.uint64) + (np.uint64(1) if kind == 3 else np.uint64(0))
+        q[one] = (q[one] & ~(np.uint64((1 << kind) - 1) << (w * pos[one]))) | (sub[one] << (w * pos[one]))
+        batches.append(q)
+    pin = _lib.pinned.empty(batches[3].size, np.uint64)
+    pin[:] = batches[3]
+    batches.append(pin)
+    for q in batches:
+        idx, dist = corr.nearest(q)
+        ridx, rdist = O.c_nearest(kind, keep, q, max_d)
+        assert np.array_equal(idx, ridx) and np.array_equal(dist, rdist)
+        idx2, dist2 = barcode.nearest_whitelist(q, keep, max_distance=max_d, encoding=kind)
+        assert np.array_equal(idx, idx2) and np.array_equal(dist, dist2)
+    corr.close()
+    empty = barcode.WhitelistCorrector(np.zeros(0, np.uint64), max_distance=max_d, encoding=kind)
+    idx, dist = empty.nearest(batches[0][:10])
+    assert (idx == -1).all() and (dist == 255).all()
+
+
 def test_nearest_halves_falls_back_on_non_acgt_whitelists():
     """A ThreeBit whitelist holding an N (or a shorter code) cannot use the half-key tables:
     the plan takes another layout and the result is still the brute force's."""

@@ -1,6 +1,6 @@
 """Where the drop-in FASTQ -> nearest flow (bench.path_fastq_stream_to_nearest) spends its time:
 the file pieces split into the read / carry-over in Python, the C chunk call (staging copies, H2D,
-index, extraction) and the fetch (D2H), then ThreeBit.encode_array and nearest_whitelist, each
+index, extraction) and the fetch (D2H), then ThreeBit.encode_array and the WhitelistCorrector build and queries, each
 wrapped with a wall-clock timer.  One JSON line.  (GPU box; writes a 1.38 GB file under /tmp.)"""
 import json
 import os
@@ -33,8 +33,8 @@ wrap(_lib.lib(), "sct_fastq_stream_chunk", "  sct_fastq_stream_chunk")
 wrap(_lib.lib(), "sct_fastq_stream_fetch", "  sct_fastq_stream_fetch")
 wrap(encodings.ThreeBit, "encode_array", "ThreeBit.encode_array")
 wrap(_lib, "encode_stream", "  _lib.encode_stream")
-wrap(barcode, "nearest_whitelist", "nearest_whitelist")
-wrap(_lib, "nearest", "  _lib.nearest")
+wrap(barcode.WhitelistCorrector, "__init__", "WhitelistCorrector (index build)")
+wrap(barcode.WhitelistCorrector, "nearest", "WhitelistCorrector.nearest")
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
 r = bench.path_fastq_stream_to_nearest(dev, bench.host_threads()[0])
