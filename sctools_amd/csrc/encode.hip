@@ -598,7 +598,9 @@ extern "C" int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint6
     SCT_HIP(hipMemsetAsync(out, 0, (size_t)L * 4 * 8, s));  // no code: every count 0
     return SCT_OK;
   }
-  const int blocks = (int)std::min<int64_t>(sct::ceil_div(n, 8 * WG), 1024);
+  // >= 32 codes per lane before the wave / workgroup reduction (at 8 per lane, 3.7M codes on 1,024
+  // workgroups, that epilogue -- 24 64-bit wave reductions per wave -- was most of the kernel)
+  const int blocks = (int)std::min<int64_t>(sct::ceil_div(n, 32 * WG), 512);
   void* part = nullptr;
   SCT_HIP(sct::pool_alloc(&part, (size_t)128 * blocks * 8, s));
   hipLaunchKernelGGL(base_frequency_kernel, dim3(blocks), dim3(WG), 0, s, codes, n, (unsigned long long*)part);
