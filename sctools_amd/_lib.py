@@ -333,15 +333,25 @@ class PinnedPool:
     files into them and copy device results into them, so every PCIe crossing is a DMA in place
     and a reused block takes no page faults.  An array (with every view of it) hands its block
     back when it is freed; up to ``keep_bytes`` of idle blocks stay for the next arrays, the rest
-    are freed.  Small arrays, and every array once page-locked memory is refused (no GPU, or the
-    allocation fails), are plain numpy arrays."""
+    are freed.  At most ``max_bytes`` are page-locked at a time (default: a quarter of the host's
+    memory, at most 16 GiB): past that -- a caller keeping every piece of a long stream -- new
+    arrays are plain numpy arrays again.  Small arrays, and every array once page-locked memory
+    is refused (no GPU, or the allocation fails), are plain numpy arrays."""
 
     MIN_BYTES = 1 << 20
 
-    def __init__(self, keep_bytes=2 << 30):
+    def __init__(self, keep_bytes=2 << 30, max_bytes=None):
         self.keep_bytes = int(keep_bytes)
+        if max_bytes is None:
+            try:
+                phys = os.sysconf("SC_PHYS_PAGES") * os.sysconf("SC_PAGE_SIZE")
+            except (ValueError, OSError, AttributeError):
+                phys = 64 << 30
+            max_bytes = min(16 << 30, phys // 4)
+        self.max_bytes = int(max_bytes)
         self._free = {}  # size class -> [pointer]
         self._idle = 0
+        self._held = 0  # page-locked bytes: blocks behind live arrays + idle blocks
         self._mu = threading.Lock()
         self._ok = True
         self._types = {}
@@ -367,8 +377,14 @@ class PinnedPool:
             if ptr is not None:
                 self._idle -= c
         if ptr is None:
+            with self._mu:
+                if self._held + c > self.max_bytes:
+                    return np.empty(shape, dtype)
+                self._held += c
             p = _vp()
             if lib().sct_host_alloc(c, ctypes.byref(p)) != SCT_OK or not p.value:
+                with self._mu:
+                    self._held -= c
                 self._ok = False  # (no GPU, or page-locked memory refused: plain arrays from now on)
                 return np.empty(shape, dtype)
             ptr = p.value
@@ -386,6 +402,7 @@ class PinnedPool:
                 self._free.setdefault(c, []).append(ptr)
                 self._idle += c
                 return
+            self._held -= c
         lib().sct_host_free(_vp(ptr))
 
     def trim(self):
@@ -393,6 +410,7 @@ class PinnedPool:
         with self._mu:
             ptrs = [p for blocks in self._free.values() for p in blocks]
             self._free.clear()
+            self._held -= self._idle
             self._idle = 0
         for p in ptrs:
             lib().sct_host_free(_vp(p))

@@ -977,7 +977,16 @@ def test_pinned_pool_blocks_reused_after_last_view():
     del b, c
     _gc.collect()
     pool.trim()
-    assert pool._idle == 0 and not pool._free
+    assert pool._idle == 0 and not pool._free and pool._held == 0
+    capped = _lib.PinnedPool(keep_bytes=0, max_bytes=4 << 20)  # one 4 MiB block at a time
+    x = capped.empty(3 << 20, np.uint8)
+    y = capped.empty(3 << 20, np.uint8)  # over the cap: plain numpy
+    assert _lib.host_pinned(x) and not _lib.host_pinned(y)
+    del x
+    _gc.collect()
+    assert capped._held == 0  # (keep_bytes = 0: freed at once)
+    z = capped.empty(3 << 20, np.uint8)
+    assert _lib.host_pinned(z)
 
 
 def test_encode_stream_pinned_and_pageable():
