@@ -132,15 +132,21 @@ class ShardedAllPairs:
                 self._t["moments_ms"].append(ev["m0"].elapsed_time(ev["m1"]))
         return hist
 
+    #: where run() builds: "side" -- a build stream beside the previous step's count (and the
+    #: count buffer zeroed there too), "main" -- in line on the main stream before the count
+    build_on = "side"
+
     def run(self, steps, timing=False):
         """``steps`` whole steps, software-pipelined two deep; returns their histograms.
 
         Every step does all of ``step()``'s work -- zero, build, count, all-reduce, D2H,
         exact inversion -- with one of two plans and count buffers: step k + 1's build runs
         on a build stream as soon as its plan's count of step k - 1 is done (beside step k's
-        count), its count is queued on the main stream before the host waits for step k, and
-        step k's all-reduce and read-back run on a tail stream, so they and the host's
-        inversion overlap the next step's kernels instead of leaving the GPU idle."""
+        count; ``build_on = "main"`` keeps it in line instead), its count is queued on the main
+        stream before the host waits for step k, and step k's all-reduce and read-back run on a
+        tail stream, so they and the host's inversion overlap the next step's kernels instead of
+        leaving the GPU idle.  The main stream waits on one other stream per step at most (a
+        cross-queue wait costs the count ≈10-20 µs of idle GPU, rocprof trace)."""
         import torch
         import torch.distributed as dist
         if steps <= 0:
@@ -172,19 +178,27 @@ class ShardedAllPairs:
         s, side, tail, sptr = self.stream, self.side, pp["tail"], self.stream.cuda_stream
         moments = self.plan.scheme == _lib.SCHEME_MOMENTS
 
-        bs = pp["build"]
+        side_build = self.build_on == "side" and not moments
+        bs = pp["build"] if side_build else s
 
         def issue(b):
             counts, ev, plan = pp["counts"][b], pp["ev"][b], pp["plans"][b]
-            bs.wait_event(ev["c1"])  # this plan's count two steps ago no longer reads its tables
+            if side_build:
+                bs.wait_event(ev["c1"])  # this plan's count two steps ago no longer reads its tables
+                bs.wait_event(pp["done"][b])  # this buffer's read-back two steps ago has finished
+                with torch.cuda.stream(bs):
+                    counts.zero_()
             if timing:
                 ev["b0"].record(bs)
             plan.build(bs.cuda_stream, self.begin, self.end)
             if timing:
                 ev["b1"].record(bs)
-            pp["built"][b].record(bs)
-            s.wait_event(pp["done"][b])  # this buffer's read-back two steps ago has finished
-            counts.zero_()
+            if side_build:
+                pp["built"][b].record(bs)
+            else:
+                # (no GPU wait: this buffer's read-back two steps ago was waited for on the host,
+                # in finish(), before this issue() -- the loop below alternates them)
+                counts.zero_()
             if moments:
                 pp["zero"][b].record(s)
                 side.wait_event(pp["zero"][b])
@@ -195,7 +209,8 @@ class ShardedAllPairs:
                     ev["m1"].record(side)
                 pp["mom"][b].record(side)
                 s.wait_event(pp["mom"][b])
-            s.wait_event(pp["built"][b])
+            if side_build:
+                s.wait_event(pp["built"][b])
             if timing:
                 ev["c0"].record(s)
             plan.count(counts.data_ptr(), self.begin, self.end, 0, sptr)

@@ -1335,13 +1335,16 @@ def test_nearest_max_d_near_limit(kind, max_d):
 
 
 @pytest.mark.parametrize("scheme", [0, 1, 2])
-def test_sharded_run_pipelined_steps_match_oracle(scheme):
+@pytest.mark.parametrize("build_on", ["side", "main"])
+def test_sharded_run_pipelined_steps_match_oracle(scheme, build_on):
     """ShardedAllPairs.run (what bench.py times): steps pipelined two deep over two count
-    buffers; every step's histogram equals step()'s and the oracle's (barcode.py:39-46)."""
+    buffers, the build beside the previous count or in line; every step's histogram equals
+    step()'s and the oracle's (barcode.py:39-46)."""
     n = 6_000 if scheme == 0 else 20_000
     codes = synthetic.whitelist_codes(n, 16, 77 + scheme)
     ref = O.c_hist16(codes)[0][:17].tolist()
     with sharding.ShardedAllPairs(codes, 32, scheme) as job:
+        job.build_on = build_on
         assert job.step().tolist() == ref
         for steps in (1, 2, 5):
             hists = job.run(steps, timing=True)
