@@ -40,20 +40,22 @@ KERNELS = (
 )
 
 
-def timed_window(src, trace, kernel_substr, last):
-    """Mean duration of the LAST `last` dispatches of a kernel in a kernel trace: the dispatches
-    of the bench's timed steps (the warm-up steps and a plan's first launch into a fresh
-    intermediate come first), i.e. the launches the bench line's HIP events time."""
+def timed_window(src, trace, kernel_substr, last, skip=5):
+    """Mean duration of the bench's timed dispatches of a kernel in a kernel trace: in start
+    order, the headline job's `skip` warm-up dispatches come first and its `last` timed ones
+    next (the side paths -- the drop-in summary too -- run after the headline and are not
+    counted), i.e. the launches the bench line's HIP events time."""
     path = os.path.join(src, trace, "run_kernel_trace.csv")
     if not os.path.exists(path):
         return None
-    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(path))
-         if kernel_substr in r["Kernel_Name"]]
+    rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(path))
+                  if kernel_substr in r["Kernel_Name"])
+    d = [e - b for b, e in rows]
     if not d:
         return None
-    w = d[-last:]
-    return {"kernel": kernel_substr, "dispatches": len(d), "window": len(w), "avg_ns": sum(w) / len(w),
-            "all_avg_ns": sum(d) / len(d)}
+    w = d[skip:skip + last] or d[-last:]
+    return {"kernel": kernel_substr, "dispatches": len(d), "window": len(w), "window_first": skip,
+            "avg_ns": sum(w) / len(w), "all_avg_ns": sum(d) / len(d)}
 
 
 def pmc_means(src, prefix, kernel_substr):
@@ -126,7 +128,8 @@ def main():
         if os.path.exists(src):
             shutil.copy(src, os.path.join(dst, fn % a.round))
     ap_steps = int(os.environ.get("BENCH_STEPS", "20"))
-    win = {k: timed_window(a.src, "trace", k, ap_steps) for k in ("tile_reg_kernel", "seed_sm_kernel")}
+    ap_warm = int(os.environ.get("BENCH_WARMUP", "5"))
+    win = {k: timed_window(a.src, "trace", k, ap_steps, ap_warm) for k in ("tile_reg_kernel", "seed_sm_kernel")}
     # the profiled command's own bench line: its live HIP-event kernel times, same box and run
     live = {}
     log = os.path.join(a.src, "trace.log")
