@@ -143,9 +143,10 @@ def main():
             w["live_ms_same_run"] = live[k]
             w["live_vs_trace_same_run"] = live[k] / (w["avg_ns"] * 1e-6) - 1.0
     with open(os.path.join(dst, "%s_timed_dispatches.json" % a.round), "w") as f:
-        json.dump({"command": "python3 bench.py --gpus 1 --steps %d --warmup 5" % ap_steps, "kernels": win,
-                   "note": "rocprofv3 kernel trace of the command; avg_ns = the last `window` dispatches of "
-                           "the kernel (the timed steps), all_avg_ns = every dispatch; live_ms_same_run = "
+        json.dump({"command": "python3 bench.py --gpus 1 --steps %d --warmup %d" % (ap_steps, ap_warm), "kernels": win,
+                   "note": "rocprofv3 kernel trace of the command; avg_ns = the kernel's dispatches "
+                           "[window_first, window_first + window) in start order (the headline's timed steps, "
+                           "after its warm-up), all_avg_ns = every dispatch; live_ms_same_run = "
                            "the HIP-event kernel time the same profiled command printed (same box, same run)"},
                   f, indent=1)
     print("timed window", json.dumps(win))
