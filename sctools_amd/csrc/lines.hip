@@ -18,6 +18,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 
 #include "sct_common.h"
 #include "encode_common.h"
@@ -169,73 +170,81 @@ __device__ __forceinline__ int file_stride(const uint8_t* __restrict__ buf, int6
   return *s_stride;
 }
 
-__global__ __launch_bounds__(WG) void wl_count_kernel(const uint8_t* __restrict__ buf, int64_t n, sct::TileSums ts,
-                                                      int32_t* __restrict__ d_maxlen,
-                                                      const unsigned* __restrict__ spec_fail) {
-  if (spec_fail && *spec_fail == 0u) return;  // the one-read pass (whitelist_spec16_kernel) did it all
-  const int64_t t0 = (int64_t)blockIdx.x * WTILE;
+// spec_fail / spec_gen: when the one-read pass ran, it stored spec_gen in *spec_fail if the file is
+// not its layout; any other value (the scratch word is not cleared: it may hold anything but
+// this call's generation) means the one-read pass did it all and this pass returns at once.
+// A grid of at most a few resident slots walks the tiles (a no-op launch then costs ~2 us less
+// than one workgroup per tile).
+__global__ __launch_bounds__(WG) void wl_count_kernel(const uint8_t* __restrict__ buf, int64_t n, int64_t ntiles,
+                                                      sct::TileSums ts, int32_t* __restrict__ d_maxlen,
+                                                      const unsigned* __restrict__ spec_fail, unsigned spec_gen) {
+  if (spec_fail && *spec_fail != spec_gen) return;  // the one-read pass (whitelist_spec16_kernel) did it all
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     *d_maxlen = 0;  // (the encode pass raises it; no memset launch)
     *ts.fany = 0u;  // (the reduction ORs the tile flags into it)
   }
-  uint4 v[NSUB];
-#pragma unroll
-  for (int j = 0; j < NSUB; ++j) v[j] = load16(buf, n, t0 + j * TILE + threadIdx.x * 16);
   __shared__ int s_stride;
   __shared__ uint32_t s_t0mod;
-  const int S = file_stride(buf, n, &s_stride);
-  if (threadIdx.x == 0 && S) s_t0mod = (uint32_t)(t0 % S);
-  __syncthreads();
-  const uint32_t t0mod = S ? s_t0mod : 0u;
-  const float invS = S ? 1.0f / (float)S : 0.0f;
-  unsigned long long c = 0;
-  long long last = -1;
-  uint32_t odd = S ? 0u : 1u;  // a line end off the stride
-#pragma unroll
-  for (int j = 0; j < NSUB; ++j) {
-    const int64_t p0 = t0 + j * TILE + threadIdx.x * 16;
-    const uint32_t m = p0 < n ? lf_mask_v(v[j], n, p0) : 0u;
-    c += __popc(m);
-    if (m) last = p0 + 31 - __clz(m);  // (sub-tiles in byte order)
-    if (S && p0 < n) {
-      // p0 mod S from the tile's t0 mod S and the in-tile offset r < 2^14 (float quotient: off by
-      // at most one below, fixed by one compare)
-      const uint32_t r = (uint32_t)(j * TILE + threadIdx.x * 16);
-      const uint32_t q = (uint32_t)((float)r * invS);
-      uint32_t ph = r - q * (uint32_t)S;
-      if (ph >= (uint32_t)S) ph -= S;
-      ph += t0mod;
-      if (ph >= (uint32_t)S) ph -= S;
-      uint32_t e = 0;  // the ends a stride-S file has in these bytes
-      for (uint32_t b = (uint32_t)S - 1u - ph; b < 16u; b += (uint32_t)S) e |= 1u << b;
-      const uint32_t valid = p0 + 16 <= n ? 0xFFFFu : (1u << (n - p0)) - 1u;
-      odd |= (m ^ e) & valid;
-    }
-  }
-#pragma unroll
-  for (int o = 32; o; o >>= 1) {
-    c += __shfl_xor(c, o);
-    last = max(last, __shfl_xor(last, o));
-  }
   __shared__ unsigned long long wc[WG / 64];
   __shared__ long long wl[WG / 64];
   __shared__ uint32_t wodd[WG / 64];
-  const uint64_t oddw = __ballot(odd != 0u);
-  if ((threadIdx.x & 63) == 0) {
-    wc[threadIdx.x >> 6] = c;
-    wl[threadIdx.x >> 6] = last;
-    wodd[threadIdx.x >> 6] = oddw ? 1u : 0u;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t f = wodd[0];
-    for (int w = 1; w < WG / 64; ++w) {
-      c += wc[w];
-      last = max(last, wl[w]);
-      f |= wodd[w];
+  const int S = file_stride(buf, n, &s_stride);
+  const float invS = S ? 1.0f / (float)S : 0.0f;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t t0 = tile * WTILE;
+    uint4 v[NSUB];
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) v[j] = load16(buf, n, t0 + j * TILE + threadIdx.x * 16);
+    __syncthreads();  // (the previous tile's readers of the shared words are done)
+    if (threadIdx.x == 0 && S) s_t0mod = (uint32_t)(t0 % S);
+    __syncthreads();
+    const uint32_t t0mod = S ? s_t0mod : 0u;
+    unsigned long long c = 0;
+    long long last = -1;
+    uint32_t odd = S ? 0u : 1u;  // a line end off the stride
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) {
+      const int64_t p0 = t0 + j * TILE + threadIdx.x * 16;
+      const uint32_t m = p0 < n ? lf_mask_v(v[j], n, p0) : 0u;
+      c += __popc(m);
+      if (m) last = p0 + 31 - __clz(m);  // (sub-tiles in byte order)
+      if (S && p0 < n) {
+        // p0 mod S from the tile's t0 mod S and the in-tile offset r < 2^14 (float quotient: off by
+        // at most one below, fixed by one compare)
+        const uint32_t r = (uint32_t)(j * TILE + threadIdx.x * 16);
+        const uint32_t q = (uint32_t)((float)r * invS);
+        uint32_t ph = r - q * (uint32_t)S;
+        if (ph >= (uint32_t)S) ph -= S;
+        ph += t0mod;
+        if (ph >= (uint32_t)S) ph -= S;
+        uint32_t e = 0;  // the ends a stride-S file has in these bytes
+        for (uint32_t b = (uint32_t)S - 1u - ph; b < 16u; b += (uint32_t)S) e |= 1u << b;
+        const uint32_t valid = p0 + 16 <= n ? 0xFFFFu : (1u << (n - p0)) - 1u;
+        odd |= (m ^ e) & valid;
+      }
     }
-    sct::tile_publish(ts, blockIdx.x, c, last);
-    ts.f0[blockIdx.x] = f;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+      c += __shfl_xor(c, o);
+      last = max(last, __shfl_xor(last, o));
+    }
+    const uint64_t oddw = __ballot(odd != 0u);
+    if ((threadIdx.x & 63) == 0) {
+      wc[threadIdx.x >> 6] = c;
+      wl[threadIdx.x >> 6] = last;
+      wodd[threadIdx.x >> 6] = oddw ? 1u : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t f = wodd[0];
+      for (int w = 1; w < WG / 64; ++w) {
+        c += wc[w];
+        last = max(last, wl[w]);
+        f |= wodd[w];
+      }
+      sct::tile_publish(ts, tile, c, last);
+      ts.f0[tile] = f;
+    }
   }
 }
 
@@ -342,8 +351,8 @@ __global__ __launch_bounds__(WG) void whitelist_fused_kernel(
     const uint8_t* __restrict__ buf, int64_t n, int64_t ntiles, int64_t per_wg, sct::TileSums ts, int direct,
     int64_t cap, int words, uint64_t* __restrict__ codes, int64_t* __restrict__ starts, int32_t* __restrict__ lens,
     uint8_t* __restrict__ gc, uint8_t* __restrict__ flags, unsigned long long* __restrict__ d_nlines,
-    int32_t* __restrict__ d_maxlen, const unsigned* __restrict__ spec_fail) {
-  if (spec_fail && *spec_fail == 0u) return;  // the one-read pass did it all
+    int32_t* __restrict__ d_maxlen, const unsigned* __restrict__ spec_fail, unsigned spec_gen) {
+  if (spec_fail && *spec_fail != spec_gen) return;  // the one-read pass did it all
   __shared__ uint8_t lut[256];
   __shared__ uint4 tile_bytes[WTILE / 16 + 1];  // (+16: encode_line1's dword reads stay inside)
   __shared__ uint32_t w_cnt[NSUB][WG / 64];
@@ -682,10 +691,13 @@ extern "C" int sct_lines(const uint8_t* d_buf, int64_t nbytes, int64_t max_lines
 // line is encoded straight from memory as the fixed-stride branch of whitelist_fused_kernel does,
 // while the assumption is CHECKED on the same bytes: the stride taken from the file's first line
 // must be 17, byte 17 g + 16 must be a '\n', and no line's 16 bytes may hold one (an A/C/G/T line
-// holds none; a line through the LUT path is searched).  Any failure sets *fail, and the count and
-// encode passes that follow in the stream (which return at once when *fail is 0) redo the file by
-// the general path, overwriting everything; so the count pass's read of the file is skipped only
-// for files where the result is already right.
+// holds none; a line through the LUT path is searched).  Any failure stores this call's generation
+// `gen` in *fail, and the count and encode passes that follow in the stream (which return at once
+// unless *fail holds gen -- the word is never cleared, so no memset launch precedes the pass: a
+// stale value can only be another call's generation, or garbage that happens to equal gen, which
+// merely runs the general path for nothing) redo the file by the general path, overwriting
+// everything; so the count pass's read of the file is skipped only for files where the result is
+// already right.
 template <int KIND>
 __global__ __launch_bounds__(WG) void whitelist_spec16_kernel(const uint8_t* __restrict__ buf, int64_t n, int64_t cap,
                                                               int words, uint64_t* __restrict__ codes,
@@ -693,14 +705,14 @@ __global__ __launch_bounds__(WG) void whitelist_spec16_kernel(const uint8_t* __r
                                                               uint8_t* __restrict__ gc, uint8_t* __restrict__ flags,
                                                               unsigned long long* __restrict__ d_nlines,
                                                               int32_t* __restrict__ d_maxlen,
-                                                              unsigned* __restrict__ fail) {
+                                                              unsigned* __restrict__ fail, unsigned gen) {
   constexpr int S = 17, L = 16;
   __shared__ uint8_t lut[256];
   __shared__ int s_stride;
   const int t = threadIdx.x;
   for (int c = t; c < 256; c += WG) lut[c] = lut_entry(KIND, c);
   if (file_stride(buf, n, &s_stride) != S) {  // (its barrier also covers the LUT)
-    if (blockIdx.x == 0 && t == 0) atomicOr(fail, 1u);
+    if (blockIdx.x == 0 && t == 0) atomicExch(fail, gen);
     return;
   }
   const int64_t nl = n / S, gend = nl < cap ? nl : (cap > 0 ? cap : 0);
@@ -770,7 +782,7 @@ __global__ __launch_bounds__(WG) void whitelist_spec16_kernel(const uint8_t* __r
       }
     }
   }
-  if (!ok) atomicOr(fail, 1u);
+  if (!ok) atomicExch(fail, gen);
 }
 
 extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int kind, int words, int64_t max_lines,
@@ -787,7 +799,7 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
     return SCT_OK;
   }
   const int64_t ntiles = sct::ceil_div(nbytes, WTILE);
-  // wl_count_kernel: one workgroup per tile, < 2^32 threads per launch
+  // tile numbers stay below 2^32 / WG (the guard of ADVICE r4, kept for the encode pass's grid)
   SCT_CHECK(ntiles * WG < (1LL << 32), "buffer too large: %lld bytes (one launch covers < %lld)", (long long)nbytes,
             (long long)(((1LL << 32) / WG) * WTILE));
   const size_t tsb = (sct::tile_sums_bytes(ntiles, true) + 255) & ~(size_t)255;
@@ -798,18 +810,30 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   // 16-base lines are tried in one read first (whitelist_spec16_kernel): when the file is that
   // layout, the passes below return at once; else they redo it (SCT_TUNE_INGEST_SPEC = 0: never)
   unsigned* spec_fail = nullptr;
+  static std::atomic<unsigned> g_spec_gen{0};
+  unsigned gen = 0;
   if (nbytes % 17 == 0 && sct::tune(SCT_TUNE_INGEST_SPEC, 1) != 0) {
     spec_fail = reinterpret_cast<unsigned*>(reinterpret_cast<uint8_t*>(scratch.p) + tsb);
-    SCT_HIP(hipMemsetAsync(spec_fail, 0, 4, s));
+    gen = ++g_spec_gen;  // (a new value per call: the scratch word is not cleared)
     auto spec = kind == 2 ? whitelist_spec16_kernel<2> : whitelist_spec16_kernel<3>;
     const int64_t nl = nbytes / 17;
     const unsigned sg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(sct::ceil_div(nl, 4 * WG), 8192));
     hipLaunchKernelGGL(spec, dim3(sg), dim3(WG), 0, s, d_buf, nbytes, cap, words, d_codes, d_starts, d_lens, d_gc, d_flags,
-                       reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen, spec_fail);
+                       reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen, spec_fail, gen);
     SCT_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(wl_count_kernel, dim3((unsigned)ntiles), dim3(WG), 0, s, d_buf, nbytes, ts, d_maxlen,
-                     (const unsigned*)spec_fail);
+  // (no work depends on another workgroup here: a grid of resident slots without stopping the
+  // scalar server, the occupancy looked up once)
+  static const int64_t count_slots = [] {
+    int dev = 0, cus = 256, per_cu = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wl_count_kernel, WG, 0) != hipSuccess || per_cu <= 0)
+      per_cu = 4;
+    return (int64_t)cus * per_cu;
+  }();
+  const unsigned cg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ntiles, count_slots));
+  hipLaunchKernelGGL(wl_count_kernel, dim3(cg), dim3(WG), 0, s, d_buf, nbytes, ntiles, ts, d_maxlen,
+                     (const unsigned*)spec_fail, gen);
   SCT_LAUNCH_CHECK();
   // up to 4,096 tiles (64 MiB) every encode workgroup reads the per-tile words itself (<= 16 per
   // thread) instead of waiting for a reduction launch
@@ -826,7 +850,7 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   const int64_t per_wg = knob > 0 ? knob : sct::ceil_div(ntiles, resident_slots((const void*)kern, ntiles));
   hipLaunchKernelGGL(kern, dim3((unsigned)sct::ceil_div(ntiles, per_wg)), dim3(WG), 0, s, d_buf, nbytes, ntiles,
                      per_wg, ts, direct, cap, words, d_codes, d_starts, d_lens, d_gc, d_flags,
-                     reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen, (const unsigned*)spec_fail);
+                     reinterpret_cast<unsigned long long*>(d_nlines), d_maxlen, (const unsigned*)spec_fail, gen);
   SCT_LAUNCH_CHECK();
   return SCT_OK;
 }
