@@ -912,7 +912,7 @@ def path_dropin(dev, reps, want_summary):
             "note": "hist_call = sct_hamming_hist_allpairs_host: H2D of the codes, plan on the cached workspace "
                     "(probe + one sync), build, count (SPECTRAL), D2H, exact inversion; codes_array = the "
                     "mapping's keys -> uint64 with the reference's type semantics (host)",
-            "check": {"summary_equals_headline": got == [float(x) for x in want_summary]
+            "check": {"summary_equals_headline": (want_summary is None or got == [float(x) for x in want_summary])
                       and [float(first[k]) for k in first] == got}}
 
 

@@ -892,6 +892,45 @@ __global__ __launch_bounds__(256) void probe_kernel(const uint64_t* __restrict__
   for (int s = 32; s; s >>= 1) o |= __shfl_xor(o, s);
   if ((threadIdx.x & 63) == 0 && o) atomicOr(out, o);
 }
+// The 14-bit column counts without global atomics (sets of >= kProbeHistMin codes): workgroup g
+// counts its contiguous share in LDS (as column_hist_wg_kernel) and writes H[g][.], ORing the
+// codes on the way; probe_max14_kernel sums each column over the workgroups and takes the max.
+// The 16-bit counts (only asked for when 14-bit columns would need int16 seeds, or forced) keep
+// the atomic probe_kernel below.
+constexpr int64_t kProbeHistMin = 1 << 17;
+__global__ __launch_bounds__(kSortThreads) void probe_hist14_kernel(const uint64_t* __restrict__ codes, int64_t n,
+                                                                    uint32_t* __restrict__ H,
+                                                                    unsigned long long* __restrict__ out) {
+  __shared__ uint32_t h[kLo];
+  for (int c = threadIdx.x; c < kLo; c += kSortThreads) h[c] = 0;
+  __syncthreads();
+  int64_t b, e;
+  wg_range(n, b, e);
+  unsigned long long o = 0;
+  for (int64_t i = b + threadIdx.x; i < e; i += kSortThreads) {
+    const uint64_t x = codes[i];
+    o |= x;
+    atomicAdd(&h[x & (kLo - 1)], 1u);
+  }
+#pragma unroll
+  for (int s = 32; s; s >>= 1) o |= __shfl_xor(o, s);
+  if ((threadIdx.x & 63) == 0 && o) atomicOr(out, o);
+  __syncthreads();
+  uint32_t* row = H + (int64_t)blockIdx.x * kLo;
+  for (int c = threadIdx.x; c < kLo; c += kSortThreads) row[c] = h[c];
+}
+
+__global__ __launch_bounds__(256) void probe_max14_kernel(const uint32_t* __restrict__ H, int wgs,
+                                                          unsigned long long* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  uint32_t m = 0;
+#pragma unroll 8
+  for (int g = 0; g < wgs; ++g) m += H[(int64_t)g * kLo + c];
+#pragma unroll
+  for (int s = 32; s; s >>= 1) m = max(m, (uint32_t)__shfl_xor(m, s));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(out + 1, (unsigned long long)m);
+}
+
 // out[1] = max cnt14, out[2] = max cnt16 (grid covers the 2^16 counters)
 __global__ __launch_bounds__(256) void probe_max_kernel(const uint32_t* __restrict__ cnt14,
                                                         const uint32_t* __restrict__ cnt16,
@@ -1122,17 +1161,31 @@ int make_order_table(State& st) {
 int probe(Workspace* ws, const uint64_t* d_codes, int64_t n, unsigned long long* out) {
   void* p = nullptr;
   constexpr size_t kWords = (size_t)kLo + (1u << 16);
-  if (int rc = ws_get(ws, W_PROBE, kWords * 4 + 32, &p); rc != SCT_OK) return rc;
+  const bool hist = n >= kProbeHistMin;  // (smaller sets: the atomic counts are as quick)
+  const size_t hbytes = hist ? (size_t)kSortWGs * kLo * 4 : 0;
+  if (int rc = ws_get(ws, W_PROBE, hbytes + kWords * 4 + 32, &p); rc != SCT_OK) return rc;
   struct Put {
     Workspace* ws;
     void* p;
     ~Put() { ws_put(ws, p); }
   } put{ws, p};
-  uint32_t* cnt14 = reinterpret_cast<uint32_t*>(p);
+  uint32_t* H = reinterpret_cast<uint32_t*>(p);
+  uint32_t* cnt14 = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p) + hbytes);
   uint32_t* cnt16 = cnt14 + kLo;
   unsigned long long* res = reinterpret_cast<unsigned long long*>(cnt16 + (1u << 16));
-  SCT_HIP(hipMemsetAsync(p, 0, kWords * 4 + 32, 0));
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(1024, sct::ceil_div(n, 256)));
+  if (hist) {
+    // OR and the 14-bit counts first; the 16-bit ones only when the 14-bit layout cannot take
+    // int8 seeds (or 16-bit columns are forced: SCT_TUNE_SPECTRAL_COLUMNS)
+    SCT_HIP(hipMemsetAsync(res, 0, 32, 0));
+    hipLaunchKernelGGL(probe_hist14_kernel, dim3(kSortWGs), dim3(kSortThreads), 0, 0, d_codes, n, H, res);
+    SCT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(probe_max14_kernel, dim3(kLo / 256), dim3(256), 0, 0, H, kSortWGs, res);
+    SCT_LAUNCH_CHECK();
+    SCT_HIP(hipMemcpy(out, res, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (out[1] <= 127 && sct::tune(SCT_TUNE_SPECTRAL_COLUMNS, 0) != kLoBits16) return SCT_OK;  // (out[2] = 0: unused)
+  }
+  SCT_HIP(hipMemsetAsync(cnt14, 0, kWords * 4 + 32, 0));
   if (n > 0) {
     hipLaunchKernelGGL(probe_kernel, dim3(blocks), dim3(256), 0, 0, d_codes, n, cnt14, cnt16, res);
     SCT_LAUNCH_CHECK();

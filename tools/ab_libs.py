@@ -27,13 +27,16 @@ def child(path, knobs):
           "pipeline": lambda: bench.path_pipeline(dev, 5, copy, threads),
           "fastq": lambda: bench.path_fastq(dev, 5, copy),
           "whitelist": lambda: bench.path_whitelist(dev, 5, copy),
-          "config5_allpairs": lambda: bench.path_config5_allpairs(dev, 5, copy)}[path]
+          "config5_allpairs": lambda: bench.path_config5_allpairs(dev, 5, copy),
+          "dropin": lambda: bench.path_dropin(dev, 10, None)}[path]
     with _lib.tuning(**knobs):
         r = fn()
     keep = {k: r.get(k) for k in ("ms", "ms_per_step", "extract_ms", "query_ms", "index_build_ms", "check")}
     if path == "whitelist":
         keep = {"ms": r["whitelist_ingest"].get("ms"), "check": r["whitelist_ingest"].get("check"),
                 "base_frequency_ms": r["base_frequency"].get("ms")}
+    if path == "dropin":
+        keep["breakdown_ms"] = r.get("breakdown_ms")
     if path == "config5_allpairs":
         keep["kernels"] = {"tile_ms": r["roofline"]["kernel_ms"], "seed_ms": r["roofline"]["other_kernel"]["ms"]}
     print(json.dumps(keep), flush=True)
