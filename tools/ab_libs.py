@@ -14,6 +14,31 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def headline(dev, steps=20):
+    """Config 2's pipelined step (ShardedAllPairs.run, what bench.py times) at W = 1 and for rank
+    0's share at W = 8 (emulated: the rank's slice range, no all-reduce): ms per step."""
+    import time
+    import torch
+    from sctools_amd import _lib, sharding, synthetic
+    n, L, seed = synthetic.CONFIGS[2]
+    codes = synthetic.whitelist_codes(n, L, seed)
+    out = {}
+    inv = _lib.counts_to_hist
+    for world in (1, 8):
+        with sharding.ShardedAllPairs(codes, 2 * L) as job:
+            job.begin, job.end = sharding.item_range(job.plan.items, 0, world)
+            _lib.counts_to_hist = inv if world == 1 else (lambda host, scheme, nbins: host)
+            job.run(3)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            hists = job.run(steps)
+            torch.cuda.synchronize()
+            out["w%d_ms" % world] = (time.perf_counter() - t0) / steps * 1e3
+            out["w%d_agree" % world] = all((h == hists[0]).all() for h in hists)
+    _lib.counts_to_hist = inv
+    return {"ms": out["w1_ms"], "ms_per_step": out, "check": {"steps_agree": out["w1_agree"] and out["w8_agree"]}}
+
+
 def child(path, knobs):
     sys.path.insert(0, ROOT)
     import torch
@@ -28,7 +53,8 @@ def child(path, knobs):
           "fastq": lambda: bench.path_fastq(dev, 5, copy),
           "whitelist": lambda: bench.path_whitelist(dev, 5, copy),
           "config5_allpairs": lambda: bench.path_config5_allpairs(dev, 5, copy),
-          "dropin": lambda: bench.path_dropin(dev, 10, None)}[path]
+          "dropin": lambda: bench.path_dropin(dev, 10, None),
+          "headline": lambda: headline(dev)}[path]
     with _lib.tuning(**knobs):
         r = fn()
     keep = {k: r.get(k) for k in ("ms", "ms_per_step", "extract_ms", "query_ms", "index_build_ms", "check")}
