@@ -65,6 +65,36 @@ __device__ __forceinline__ uint32_t popc_add(uint32_t x, uint32_t a) {
   asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(a));
   return r;
 }
+
+// The column (offset in the block of 256) lane `tid` walks: the block's columns in three classes by
+// group count -- >= 3, 2, <= 1 -- each class in column order (a stable partition: ballots within a
+// wave, counts across the 4 waves), so the columns of more than 64 codes share waves instead of
+// raising every wave's walk to 3 groups, and the stage bytes a 32-lane group stores stay mostly
+// increasing (2-way bank conflicts at most, free for a byte store).  Each column's result still goes
+// to its own stage byte: only which lane walks which column changes.  Two barriers.
+__device__ __forceinline__ int seed_lane_column(const uint32_t* __restrict__ gofs, int c0, int tid) {
+  __shared__ uint32_t s_wcnt[4][3];
+  __shared__ uint8_t s_col[256];
+  const uint32_t ng = gofs[c0 + tid + 1] - gofs[c0 + tid];
+  const int cls = ng >= 3u ? 0 : (ng == 2u ? 1 : 2);
+  const int lane = tid & 63, wave = tid >> 6;
+  const uint64_t b0 = __ballot(cls == 0), b1 = __ballot(cls == 1), b2 = __ballot(cls == 2);
+  const uint64_t mine = cls == 0 ? b0 : (cls == 1 ? b1 : b2);
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;  // the lanes before this one
+  if (lane == 0) {
+    s_wcnt[wave][0] = (uint32_t)__popcll(b0);
+    s_wcnt[wave][1] = (uint32_t)__popcll(b1);
+    s_wcnt[wave][2] = (uint32_t)__popcll(b2);
+  }
+  __syncthreads();
+  uint32_t pos = (uint32_t)__popcll(mine & below);
+  for (int k = 0; k < cls; ++k)
+    for (int w = 0; w < 4; ++w) pos += s_wcnt[w][k];
+  for (int w = 0; w < wave; ++w) pos += s_wcnt[w][cls];
+  s_col[pos] = (uint8_t)tid;
+  __syncthreads();
+  return (int)s_col[tid];
+}
 constexpr int ctz_c(int i) {
   int k = 0;
   while (!(i & 1)) {

@@ -433,8 +433,8 @@ constexpr int kMaxWalkBlockBits = 4;  // walks per Gray-ordered block: <= 16
 // after the register groups' walk of slices zblk..zblk + 63: the groups beyond them (columns of
 // > 96 codes) from L2 into the lane's stage bytes, then the stage to HBM as int8 m - 2 * sum
 __device__ __forceinline__ void seed_finish(const uint32_t* __restrict__ planes, uint32_t g0, int ng, int wng,
-                                            uint8_t* st8, int tid, const uint32_t* mx, int mcb, int c0, int zblk,
-                                            int z0, int z1, int8_t* __restrict__ buf) {
+                                            uint8_t* st8, int tid, int co, const uint32_t* mx, int mcb, int c0,
+                                            int zblk, int z0, int z1, int8_t* __restrict__ buf) {
   constexpr int NT = 256;
   for (int g = kRegGroupsSM; g < wng; ++g) {
     uint32_t p[kHiBits];
@@ -451,7 +451,7 @@ __device__ __forceinline__ void seed_finish(const uint32_t* __restrict__ planes,
 #pragma unroll
     for (int i = 0; i < kWalk; ++i) {
       if (i) x ^= p[ctz_c(i)];
-      st8[gray(i) * NT + tid] += (uint8_t)__popc(x);
+      st8[gray(i) * NT + co] += (uint8_t)__popc(x);
       if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -472,8 +472,9 @@ __device__ __forceinline__ void seed_finish(const uint32_t* __restrict__ planes,
 // flipped: two XORs per group instead of the start state's twelve planes
 template <int G>
 __device__ __forceinline__ void seed_walks(const uint32_t (*pr)[kHiBits], const uint32_t* __restrict__ planes,
-                                           uint32_t g0, int ng, int wng, uint8_t* st8, int tid, const uint32_t* mx,
-                                           int mcb, int c0, int z0, int z1, int8_t* __restrict__ buf, int lp) {
+                                           uint32_t g0, int ng, int wng, uint8_t* st8, int tid, int co,
+                                           const uint32_t* mx, int mcb, int c0, int z0, int z1,
+                                           int8_t* __restrict__ buf, int lp) {
   const int wa = (z0 & ~(kWalk - 1)) >> kWalkBits, we = (z1 + kWalk - 1) >> kWalkBits, P = 1 << lp;
   const int b1 = (we + P - 1) >> lp;
   for (int b = (wa >> lp) + blockIdx.y; b < b1; b += gridDim.y) {
@@ -498,8 +499,8 @@ __device__ __forceinline__ void seed_walks(const uint32_t (*pr)[kHiBits], const 
         continue;
       }
       __syncthreads();  // the previous walk's store-out reads of `stage` are done
-      walk_from<G>(pr, x, st8, tid);
-      seed_finish(planes, g0, ng, wng, st8, tid, mx, mcb, c0, w << kWalkBits, z0, z1, buf);
+      walk_from<G>(pr, x, st8, co);
+      seed_finish(planes, g0, ng, wng, st8, tid, co, mx, mcb, c0, w << kWalkBits, z0, z1, buf);
     }
   }
 }
@@ -513,7 +514,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void s
   __shared__ uint32_t stage[kWalk * NT / 4];
   uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
   const int tid = threadIdx.x;
-  const int c0 = blockIdx.x * NT, c = c0 + tid;
+  const int c0 = blockIdx.x * NT;
+  // columns to lanes by group count (seed_lane_column); the stage rows and the store-out stay in
+  // column order
+  const int co = seed_lane_column(gofs, c0, tid);
+  const int c = c0 + co;
   const uint32_t g0 = gofs[c];
   const int ng = (int)(gofs[c + 1] - g0);
   int wng = ng;
@@ -544,9 +549,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void s
     if (ph >= 1) __builtin_amdgcn_s_sleep(24);
     if (ph == 2) __builtin_amdgcn_s_sleep(24);
   }
-  if (wng <= 1) seed_walks<1>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
-  else if (wng == 2) seed_walks<2>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
-  else seed_walks<3>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
+  if (wng <= 1) seed_walks<1>(pr, planes, g0, ng, wng, st8, tid, co, mx, mcb, c0, z0, z1, buf, lp);
+  else if (wng == 2) seed_walks<2>(pr, planes, g0, ng, wng, st8, tid, co, mx, mcb, c0, z0, z1, buf, lp);
+  else seed_walks<3>(pr, planes, g0, ng, wng, st8, tid, co, mx, mcb, c0, z0, z1, buf, lp);
 }
 
 template <typename T>

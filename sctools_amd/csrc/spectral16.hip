@@ -220,8 +220,8 @@ constexpr int kMaxWalkBlockBits16 = 4;    // walks per Gray-ordered block: <= 16
 // after the register groups' walk of slices zblk..zblk + 63: the groups past them from L2, then
 // the stage to HBM
 __device__ __forceinline__ void seed16_finish(const uint32_t* __restrict__ planes, uint32_t g0, int ng, int wng,
-                                              uint8_t* st8, int tid, const uint32_t* mx, int mcb, int c0, int zblk,
-                                              int z0, int z1, int8_t* __restrict__ buf) {
+                                              uint8_t* st8, int tid, int co, const uint32_t* mx, int mcb, int c0,
+                                              int zblk, int z0, int z1, int8_t* __restrict__ buf) {
   constexpr int NT = 256;
   for (int g = kRegGroups16; g < wng; ++g) {  // the groups past the register-resident ones, from L2
     uint32_t p[kHi16];
@@ -238,7 +238,7 @@ __device__ __forceinline__ void seed16_finish(const uint32_t* __restrict__ plane
 #pragma unroll
     for (int i = 0; i < kWalk16; ++i) {
       if (i) x ^= p[ctz_c(i)];
-      st8[gray(i) * NT + tid] += (uint8_t)__popc(x);
+      st8[gray(i) * NT + co] += (uint8_t)__popc(x);
       if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -256,8 +256,9 @@ __device__ __forceinline__ void seed16_finish(const uint32_t* __restrict__ plane
 // the walks in Gray-ordered blocks of 2^lp, as seed_walks in spectral.hip
 template <int G>
 __device__ __forceinline__ void seed16_walks(const uint32_t (*pr)[kHi16], const uint32_t* __restrict__ planes,
-                                             uint32_t g0, int ng, int wng, uint8_t* st8, int tid, const uint32_t* mx,
-                                             int mcb, int c0, int z0, int z1, int8_t* __restrict__ buf, int lp) {
+                                             uint32_t g0, int ng, int wng, uint8_t* st8, int tid, int co,
+                                             const uint32_t* mx, int mcb, int c0, int z0, int z1,
+                                             int8_t* __restrict__ buf, int lp) {
   const int wa = (z0 & ~(kWalk16 - 1)) >> kWalkBits16, we = (z1 + kWalk16 - 1) >> kWalkBits16, P = 1 << lp;
   const int b1 = (we + P - 1) >> lp;
   for (int b = (wa >> lp) + blockIdx.y; b < b1; b += gridDim.y) {
@@ -282,8 +283,8 @@ __device__ __forceinline__ void seed16_walks(const uint32_t (*pr)[kHi16], const 
         continue;
       }
       __syncthreads();  // the previous walk's store-out reads of `stage` are done
-      walk_from16<G>(pr, x, st8, tid);
-      seed16_finish(planes, g0, ng, wng, st8, tid, mx, mcb, c0, w << kWalkBits16, z0, z1, buf);
+      walk_from16<G>(pr, x, st8, co);
+      seed16_finish(planes, g0, ng, wng, st8, tid, co, mx, mcb, c0, w << kWalkBits16, z0, z1, buf);
     }
   }
 }
@@ -295,7 +296,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void s
   __shared__ uint32_t stage[kWalk16 * NT / 4];
   uint8_t* st8 = reinterpret_cast<uint8_t*>(stage);
   const int tid = threadIdx.x;
-  const int c0 = blockIdx.x * NT, c = c0 + tid;
+  const int c0 = blockIdx.x * NT;
+  // columns to lanes by group count (seed_lane_column, spectral.h): at config 5's density 1 in 8
+  // columns holds more than 64 codes, so in column order nearly every wave walks 3 groups
+  const int co = seed_lane_column(gofs, c0, tid);
+  const int c = c0 + co;
   const uint32_t g0 = gofs[c];
   const int ng = (int)(gofs[c + 1] - g0);
   int wng = ng;
@@ -326,9 +331,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void s
     if (ph >= 1) __builtin_amdgcn_s_sleep(24);
     if (ph == 2) __builtin_amdgcn_s_sleep(24);
   }
-  if (wng <= 1) seed16_walks<1>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
-  else if (wng == 2) seed16_walks<2>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
-  else seed16_walks<3>(pr, planes, g0, ng, wng, st8, tid, mx, mcb, c0, z0, z1, buf, lp);
+  if (wng <= 1) seed16_walks<1>(pr, planes, g0, ng, wng, st8, tid, co, mx, mcb, c0, z0, z1, buf, lp);
+  else if (wng == 2) seed16_walks<2>(pr, planes, g0, ng, wng, st8, tid, co, mx, mcb, c0, z0, z1, buf, lp);
+  else seed16_walks<3>(pr, planes, g0, ng, wng, st8, tid, co, mx, mcb, c0, z0, z1, buf, lp);
 }
 
 // ---------------------------------------------------------------- tile
