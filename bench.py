@@ -761,15 +761,21 @@ def path_fastq_stream_to_nearest(dev, threads):
         t = time.perf_counter()
         idx, dist, codes = run()
         dt = time.perf_counter() - t
-        # the ceiling this flow runs against: reading the same file into one page-locked buffer of
-        # the same piece size (readinto, as the generator does), nothing else
-        from sctools_amd import _lib
-        rbuf = _lib.pinned.empty(fastq.CHUNK_BYTES, np.uint8)
-        mv = memoryview(rbuf)
+        # the ceiling this flow runs against: the generator's own piece reader reading the same file
+        # (page cache) into its page-locked buffers, nothing else
         t = time.perf_counter()
-        with open(path, "rb") as f:
-            while f.readinto(mv):
-                pass
+        rd = fastq._piece_reader([path], fastq.CHUNK_BYTES, fastq._HEADROOM)
+        rd.start()
+        try:
+            while True:
+                got = rd.get()
+                if isinstance(got, BaseException):
+                    raise got
+                rd.free.put(got[0])
+                if got[3]:
+                    break
+        finally:
+            rd.close()
         read_dt = time.perf_counter() - t
     finally:
         os.unlink(path)
@@ -787,8 +793,9 @@ def path_fastq_stream_to_nearest(dev, threads):
             "file_gbs": nbytes / dt / 1e9, "breakdown_ms": {k: v * 1e3 for k, v in parts_s.items()},
             "roofline": {"bound": "file read", "achieved": nbytes / dt / 1e9, "unit": "GB/s of FASTQ",
                          "peak": nbytes / read_dt / 1e9, "frac": read_dt / dt,
-                         "peak_source": "the same file read (page cache) into one page-locked buffer of the same "
-                                        "piece size, nothing else, this run"},
+                         "peak_source": "the same file read (page cache) by the generator's own piece reader "
+                                        "(parallel positional reads into its page-locked buffers), nothing "
+                                        "else, this run"},
             "note": "the drop-in Python flow end to end (file reads, four host<->device crossings per piece); "
                     "paths.fastq_to_nearest is the same work device-resident",
             "check": {"codes_equal_queries": ok_codes, "exact_draws_own_index": ok_exact,

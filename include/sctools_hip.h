@@ -461,6 +461,13 @@ int sct_fastq_stream_chunk(sct_fastq_stream* stream, const uint8_t* buf, int64_t
                            int nfiles, int final, int64_t* nrecords, int64_t* consumed, int64_t* first_bad_name);
 int sct_fastq_stream_fetch(sct_fastq_stream* stream, uint8_t* seq_out, uint8_t* qual_out, int32_t* seq_len,
                            int32_t* qual_len);
+/* Copy the NEXT piece to the device ahead of its chunk call (asynchronous, on a copy stream of
+ * the stream's own): a caller that knows the next piece while it works on this one's results
+ * overlaps the piece's PCIe copy with that work.  Only a page-locked piece (sct_host_pinned) is
+ * staged (anything else: a no-op); the piece's bytes must stay unchanged until the chunk call
+ * for exactly (buf, nbytes) -- which then skips its own copy -- or the next stage call, or
+ * the stream's destruction (each waits for the copy). */
+int sct_fastq_stream_stage(sct_fastq_stream* stream, const uint8_t* buf, int64_t nbytes);
 
 /* ---------------------------------------------------------------- bench aid
  * Streaming device copy (16 B per lane, nontemporal, resident grid) of `bytes` (a multiple

@@ -53,6 +53,7 @@ SIGNATURES = {
     "sct_encode_host": [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp],
     "sct_encode_stream_host": [_i32, _vp, _i64, _i32, _vp, _vp, _vp, _i64],
     "sct_host_pinned": [_vp, _i64, _vp],
+    "sct_fastq_stream_stage": [_vp, _vp, _i64],
     "sct_nearest_plan_create_host": [_i32, _vp, _i64, _i32, _i32, _vp],
     "sct_nearest_query_host": [_vp, _vp, _i64, _vp, _vp],
     "sct_host_alloc": [_i64, _vp],
@@ -623,6 +624,13 @@ class FastqStream:
             out.append((rows, slen[k * nr:(k + 1) * nr], q, qlen[k * nr:(k + 1) * nr] if self.qualities else None))
             off += nr * w
         return nr, used.value, bad.value, out
+
+    def stage(self, buf, nbytes):
+        """Copy the next piece buf[:nbytes] to the device now (page-locked buffers only); the
+        chunk call for the same buffer and size then skips its copy.  buf must stay unchanged
+        until that call."""
+        data = np.frombuffer(buf, dtype=np.uint8, count=nbytes) if nbytes else np.zeros(1, np.uint8)
+        check(self._lib.sct_fastq_stream_stage(self._h, _ptr(data), nbytes))
 
     def close(self):
         if self._h:

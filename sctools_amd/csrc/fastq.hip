@@ -26,6 +26,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <utility>
 #include <mutex>
 #include <vector>
 
@@ -1206,10 +1207,24 @@ struct sct_fastq_stream {
   int64_t rec_cap = 0;
   long long* d_end = nullptr;
   int64_t nrec = 0, first_bad = -1, consumed = 0;
+  // the next piece copied ahead (sct_fastq_stream_stage): into d_next on copy_stream, `staged`
+  // recorded after it; the chunk call for (staged_ptr, staged_n) swaps d_next in
+  void* d_next = nullptr;
+  int64_t next_cap = 0;
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t staged = nullptr;
+  const uint8_t* staged_ptr = nullptr;
+  int64_t staged_n = -1;
 };
 
 extern "C" int sct_fastq_stream_destroy(sct_fastq_stream* s) {
   if (!s) return SCT_OK;
+  if (s->copy_stream) {
+    (void)hipStreamSynchronize(s->copy_stream);
+    (void)hipStreamDestroy(s->copy_stream);
+  }
+  if (s->staged) (void)hipEventDestroy(s->staged);
+  if (s->d_next) (void)hipFree(s->d_next);
   if (s->st) (void)hipStreamSynchronize(s->st->stream);  // nothing of the stream's still reads its buffers
   if (s->d_buf) (void)hipFree(s->d_buf);
   if (s->d_out) (void)hipFree(s->d_out);
@@ -1254,6 +1269,16 @@ extern "C" int sct_fastq_stream_chunk(sct_fastq_stream* s, const uint8_t* buf, i
   SCT_CHECK(s && nrecords && consumed && first_bad_name, "NULL pointer");
   SCT_CHECK(nbytes >= 0 && (nbytes == 0 || buf), "bad buffer");
   hipStream_t hs = s->st->stream;
+  const bool was_staged = s->staged_n >= 0 && s->staged_ptr == buf && s->staged_n == nbytes;
+  if (s->staged_n >= 0) {  // (a staged copy is complete before anything else touches its buffers)
+    SCT_HIP(hipStreamWaitEvent(hs, s->staged, 0));
+    s->staged_n = -1;
+    s->staged_ptr = nullptr;
+    if (was_staged) {  // the piece is on the device already: its buffer becomes this chunk's
+      std::swap(s->d_buf, s->d_next);
+      std::swap(s->buf_cap, s->next_cap);
+    }
+  }
   if (nbytes > s->buf_cap) {
     if (s->d_buf) (void)hipFree(s->d_buf);
     s->d_buf = nullptr;
@@ -1261,7 +1286,9 @@ extern "C" int sct_fastq_stream_chunk(sct_fastq_stream* s, const uint8_t* buf, i
     SCT_HIP(hipMalloc(&s->d_buf, (size_t)nbytes));
     s->buf_cap = nbytes;
   }
-  if (sct::host_range_pinned(buf, (size_t)nbytes)) {
+  if (was_staged) {
+    // (copied by sct_fastq_stream_stage)
+  } else if (sct::host_range_pinned(buf, (size_t)nbytes)) {
     // a page-locked piece (the Python layer reads the files into one): one DMA in place; the
     // call returns only after a synchronisation of `hs`, so the caller may refill it afterwards
     if (nbytes) SCT_HIP(hipMemcpyAsync(s->d_buf, buf, (size_t)nbytes, hipMemcpyHostToDevice, hs));
@@ -1320,6 +1347,39 @@ extern "C" int sct_fastq_stream_chunk(sct_fastq_stream* s, const uint8_t* buf, i
   *nrecords = nrec;
   *consumed = used;
   *first_bad_name = bad;
+  return SCT_OK;
+}
+
+extern "C" int sct_fastq_stream_stage(sct_fastq_stream* s, const uint8_t* buf, int64_t nbytes) {
+  SCT_CHECK(s != nullptr, "stream is NULL");
+  SCT_CHECK(nbytes >= 0 && (nbytes == 0 || buf), "bad buffer");
+  if (s->staged_n >= 0) {  // a previous stage never used: its copy must end before d_next is reused
+    SCT_HIP(hipEventSynchronize(s->staged));
+    s->staged_n = -1;
+    s->staged_ptr = nullptr;
+  }
+  if (nbytes == 0 || !sct::host_range_pinned(buf, (size_t)nbytes)) return SCT_OK;  // (the chunk call copies)
+  if (!s->copy_stream) SCT_HIP(hipStreamCreateWithFlags(&s->copy_stream, hipStreamNonBlocking));
+  if (!s->staged) SCT_HIP(hipEventCreateWithFlags(&s->staged, hipEventDisableTiming));
+  if (nbytes > s->next_cap) {
+    if (s->d_next) {
+      SCT_HIP(hipStreamSynchronize(s->st->stream));  // (no chunk kernel reads the old buffer)
+      (void)hipFree(s->d_next);
+    }
+    s->d_next = nullptr;
+    s->next_cap = 0;
+    SCT_HIP(hipMalloc(&s->d_next, (size_t)nbytes));
+    s->next_cap = nbytes;
+  }
+  // d_next was the previous chunk's buffer two pieces ago at most: the copy waits for the chunk
+  // work queued so far on the stream (its index and extraction read d_buf, not d_next, but a
+  // swapped-out buffer may still be read by the last chunk's kernels)
+  SCT_HIP(hipEventRecord(s->staged, s->st->stream));
+  SCT_HIP(hipStreamWaitEvent(s->copy_stream, s->staged, 0));
+  SCT_HIP(hipMemcpyAsync(s->d_next, buf, (size_t)nbytes, hipMemcpyHostToDevice, s->copy_stream));
+  SCT_HIP(hipEventRecord(s->staged, s->copy_stream));
+  s->staged_ptr = buf;
+  s->staged_n = nbytes;
   return SCT_OK;
 }
 

@@ -19,6 +19,8 @@ filenames, modes 'r' (text: universal newlines, str fields) and 'rb' (bytes fiel
 
 import bz2
 import gzip
+import itertools
+import os
 import queue
 import threading
 from collections import namedtuple
@@ -66,9 +68,11 @@ _HEADROOM = 1 << 20
 
 class _PieceReader(threading.Thread):
     """Fills page-locked piece buffers from the files, one buffer ahead of the consumer: each
-    buffer in `free` comes back through `full` as (buffer, bytes read at [head, head + n), the
+    buffer in `free` comes back through get() as (buffer, bytes read at [head, head + n), the
     file ends among them, whether every file is exhausted), or an exception raised while
-    opening or reading (raised by the consumer in its turn).  The read releases the GIL."""
+    opening or reading (raised by the consumer in its turn).  The read releases the GIL.  The
+    files are read in sequence, so a missing or unreadable file surfaces after the pieces of
+    the files before it (reader.py:64-71 opens each file when it gets there)."""
 
     def __init__(self, files, buffers, head):
         super().__init__(name="sctools-fastq-reader", daemon=True)
@@ -79,6 +83,9 @@ class _PieceReader(threading.Thread):
         self.full = queue.Queue()
         for b in buffers:
             self.free.put(b)
+
+    def get(self, block=True):
+        return self.full.get(block)
 
     def run(self):
         f = None
@@ -119,6 +126,125 @@ class _PieceReader(threading.Thread):
         self._halt = True
         self.free.put(None)
         self.join(timeout=10.0)
+
+
+class _ParallelPieceReader:
+    """The same pieces as _PieceReader, for plain (uncompressed, existing) files: segment k of the
+    concatenated files -- bytes [k cap, (k + 1) cap) -- is read with os.preadv by one of W workers
+    (page-cache copies on W cores at once: one reading thread was the FASTQ -> nearest flow's
+    ceiling), and get() hands the segments back in order.  Buffers go to segments in segment
+    order (one worker at a time takes the next free buffer and the next segment number), so the
+    segment the consumer waits for always holds a buffer.  File ends as _PieceReader reports
+    them: a file ending exactly at a segment's end is that of the next segment, at 0."""
+
+    def __init__(self, files, buffers, head, workers):
+        self._head = head
+        self._halt = False
+        self._cap = buffers[0].size - head
+        self._fds = []
+        try:
+            for name in files:
+                self._fds.append(os.open(name, os.O_RDONLY))
+        except BaseException:
+            self._close_fds()
+            raise
+        sizes = [os.fstat(fd).st_size for fd in self._fds]
+        self._bounds = list(itertools.accumulate(sizes))  # the files' ends in the concatenation
+        self._starts = [b - z for b, z in zip(self._bounds, sizes)]
+        total = self._bounds[-1] if self._bounds else 0
+        self._nseg = total // self._cap + 1  # (the last one short, possibly empty)
+        self.free = queue.Queue()
+        for b in buffers:
+            self.free.put(b)
+        self._take = threading.Lock()  # (a free buffer and the next segment number, together)
+        self._k_next = 0
+        self._cv = threading.Condition()
+        self._done = {}
+        self._next = 0
+        self._threads = [threading.Thread(target=self._work, name="sctools-fastq-reader-%d" % w, daemon=True)
+                         for w in range(max(1, min(workers, self._nseg)))]
+
+    def start(self):
+        for t in self._threads:
+            t.start()
+
+    def get(self, block=True):
+        with self._cv:
+            while self._next not in self._done:
+                if not block:
+                    raise queue.Empty
+                self._cv.wait()
+            item = self._done.pop(self._next)
+            self._next += 1
+            return item
+
+    def _fill(self, buf, k):
+        lo = k * self._cap
+        hi = min(lo + self._cap, self._bounds[-1] if self._bounds else 0)
+        mv = memoryview(buf)
+        for fd, fs, fe in zip(self._fds, self._starts, self._bounds):
+            a, b = max(lo, fs), min(hi, fe)
+            while a < b:  # (preadv may return short)
+                got = os.preadv(fd, [mv[self._head + a - lo:self._head + b - lo]], a - fs)
+                if got <= 0:
+                    raise OSError("short read of a FASTQ file (it changed while being read?)")
+                a += got
+        ends = [e - lo for e in self._bounds if lo <= e < lo + self._cap]
+        return buf, hi - lo, ends, k == self._nseg - 1
+
+    def _work(self):
+        while True:
+            with self._take:
+                buf = self.free.get()
+                if buf is None or self._halt or self._k_next >= self._nseg:
+                    return
+                k = self._k_next
+                self._k_next += 1
+            try:
+                item = self._fill(buf, k)
+            except BaseException as e:  # (handed to the consumer in its turn)
+                item = e
+            with self._cv:
+                self._done[k] = item
+                self._cv.notify_all()
+            if isinstance(item, BaseException):
+                return
+
+    def _close_fds(self):
+        for fd in self._fds:
+            os.close(fd)
+        self._fds = []
+
+    def close(self):
+        self._halt = True
+        for _ in self._threads:
+            self.free.put(None)
+        for t in self._threads:
+            t.join(timeout=10.0)
+        if not any(t.is_alive() for t in self._threads):
+            self._close_fds()
+
+
+#: worker threads of the parallel piece reader (plain files)
+READ_WORKERS = 3
+
+
+def _piece_reader(files, chunk_bytes, head):
+    """The reader for these files: parallel positional reads for plain files that all exist,
+    else one thread reading them in order (compressed files, stdin, or a missing file, whose
+    error then comes after the pieces before it)."""
+    files = list(files)
+    plain = files and all(not f.endswith(('.gz', '.bz2')) and os.path.isfile(f) for f in files)
+    if plain and READ_WORKERS > 1 and hasattr(os, "preadv"):
+        try:
+            # W + 2 buffers (W filling, one ready, one with the consumer) of half-size pieces: the
+            # page-locked footprint stays near the sequential reader's two full-size buffers
+            seg = chunk_bytes // 2 if chunk_bytes >= (2 << 20) else chunk_bytes
+            bufs = [_lib.pinned.empty(head + seg, np.uint8) for _ in range(READ_WORKERS + 2)]
+            return _ParallelPieceReader(files, bufs, head, READ_WORKERS)
+        except OSError:
+            pass  # (the sequential reader reports it in order)
+    return _PieceReader(files, [_lib.pinned.empty(head + chunk_bytes, np.uint8) for _ in range(2)], head)
 
 
 def _last_line_end(buf, have):
@@ -164,52 +290,80 @@ class EmbeddedBarcodeGenerator:
 
         A reader thread (`_PieceReader`) fills one page-locked buffer while the device and the
         caller work on the other, so the file reads overlap everything else; the device copies
-        each piece by DMA in place.  The carried-over tail goes into the headroom in front of
+        each piece by DMA in place, the next one (when read already) while the caller works on
+        this one's results (sct_fastq_stream_stage).  The carried-over tail goes into the headroom in front of
         the next piece (a tail longer than the headroom -- a record longer than a megabyte --
         is merged with the next piece in a new buffer)."""
         chunk_bytes = max(1, int(chunk_bytes or CHUNK_BYTES))
         head = _HEADROOM
         st = _lib.FastqStream([(eb.start, eb.end) for eb in self.embedded_barcodes], self._mode == 'r', qualities)
-        reader = _PieceReader(self._files, [_lib.pinned.empty(head + chunk_bytes, np.uint8) for _ in range(2)], head)
+        reader = _piece_reader(self._files, chunk_bytes, head)
         reader.start()
         carry = np.zeros(0, np.uint8)  # the unconsumed tail of the last piece (a copy)
         carry_ends = []                # file ends inside it
+
+        def prepare(got):
+            """A segment from the reader -> (piece, file ends in it, last?, buffer to hand back,
+            bytes of the chunk call to come: the cut after the last '\\n', the whole final piece)."""
+            buf, n, seg_ends, last = got
+            c = carry.size
+            if c <= head:  # the tail goes in front of the segment, in the same buffer
+                buf[head - c:head] = carry
+                piece = buf[head - c:head + n]
+                release = buf
+            else:  # (a tail longer than the headroom: one merged buffer)
+                piece = _lib.pinned.empty(c + n, np.uint8)
+                piece[:c] = carry
+                piece[c:] = buf[head:head + n]
+                reader.free.put(buf)
+                release = None
+            ends = carry_ends + [c + e for e in seg_ends]
+            return piece, ends, last, release, (piece.size if last else _last_line_end(piece, piece.size))
+
         done = 0
+        nxt, pending = None, None
         try:
             while True:
-                got = reader.full.get()
-                if isinstance(got, BaseException):
-                    raise got
-                buf, n, seg_ends, last = got
-                c = carry.size
-                if c <= head:  # the tail goes in front of the segment, in the same buffer
-                    buf[head - c:head] = carry
-                    piece = buf[head - c:head + n]
-                    release = buf
-                else:  # (a tail longer than the headroom: one merged buffer)
-                    piece = _lib.pinned.empty(c + n, np.uint8)
-                    piece[:c] = carry
-                    piece[c:] = buf[head:head + n]
-                    reader.free.put(buf)
-                    release = None
-                ends = carry_ends + [c + e for e in seg_ends]
+                if nxt is None:
+                    got = reader.get()
+                    if isinstance(got, BaseException):
+                        raise got
+                    nxt = prepare(got)
+                piece, ends, last, release, cut = nxt
+                nxt = None
                 if last:
                     nrec, _, bad, parts = st.chunk(piece, piece.size, ends or [0], final=True)
                     yield done, nrec, bad, parts
                     return
-                cut = _last_line_end(piece, piece.size)
-                used = 0
+                used, out = 0, None
                 if cut > 0:
                     nrec, used, bad, parts = st.chunk(piece, cut, [e for e in ends if e < cut] + [cut], final=False)
-                    yield done, nrec, bad, parts
-                    if bad >= 0:
-                        return
-                    done += nrec
+                    out = (done, nrec, bad, parts)
                 carry = piece[used:].copy()  # (no line end, or no complete record yet: all of it)
                 carry_ends = [e - used for e in ends if e > used]
                 del piece
                 if release is not None:
                     reader.free.put(release)
+                if out is not None and out[2] < 0:
+                    # the next piece, when the reader has it, goes to the device now: its copy then
+                    # overlaps the caller's work on this piece's results
+                    try:
+                        got = reader.get(block=False)
+                    except queue.Empty:
+                        got = None
+                    if isinstance(got, BaseException):
+                        pending = got
+                    elif got is not None:
+                        nxt = prepare(got)
+                        if nxt[4] > 0:
+                            st.stage(nxt[0], nxt[4])
+                if out is not None:
+                    yield out
+                    if out[2] >= 0:
+                        return
+                    done += out[1]
+                if pending is not None:
+                    raise pending
         finally:
             reader.close()
             st.close()

@@ -134,11 +134,25 @@ class _FakeStream:
     of its complete records), so the piece logic of _pieces -- the read-ahead thread, the
     carried tail, the file ends -- is checked on the CPU against one whole-input call."""
 
+    staged_hits = 0
+
     def __init__(self, spans, text_mode, qualities=True):
         self.spans, self.qualities = [tuple(x) for x in spans], qualities
+        self.staged = None
+
+    def stage(self, buf, nbytes):
+        """sct_fastq_stream_stage's contract, checked: the staged bytes must be unchanged when the
+        chunk call for the same buffer and size comes."""
+        a = np.asarray(buf)
+        self.staged = (a.ctypes.data, nbytes, bytes(a[:nbytes]))
 
     def chunk(self, buf, nbytes, file_ends, final):
         data = bytes(np.asarray(buf)[:nbytes])
+        if self.staged is not None:
+            if self.staged[:2] == (np.asarray(buf).ctypes.data, nbytes):
+                assert self.staged[2] == data, "a staged piece changed before its chunk call"
+                _FakeStream.staged_hits += 1
+            self.staged = None
         cuts = sorted(set([e for e in file_ends if 0 < e <= nbytes]))
         lines, pos = [], 0  # (start, end without '\\n', next start)
         while pos < nbytes:
@@ -210,6 +224,8 @@ def test_pieces_reader_carry_and_file_ends(tmp_path, monkeypatch, chunk):
         ends.append(acc)
     whole = np.frombuffer(b"".join(parts), np.uint8)
     n, _, bad, want = _FakeStream([(0, 16), (4, 9)], False).chunk(whole, whole.size, ends, True)
+    if chunk <= 1000 and chunk != 64:
+        assert _FakeStream.staged_hits > 0  # (the reader runs ahead: most pieces were staged)
     assert bad == -1 and n >= 399  # (399 when the last record's empty quality line was its final newline)
     assert sum(g[1] for g in got) == n
     assert [g[0] for g in got] == list(np.cumsum([0] + [g[1] for g in got[:-1]]))
