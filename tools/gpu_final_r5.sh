@@ -1,6 +1,7 @@
 # Round 5, final box: the whole GPU suite, the rocprofv3 kernel trace + stats of the EXACT driver
 # command (python3 bench.py --gpus 1 --steps 20 --warmup 5), PMC passes of a short headline-only
-# run (each pass its own run, within the per-block counter limits), the FASTQ flow breakdown.
+# run (each pass its own run, within the per-block counter limits), config 5's all-pairs path under
+# the kernel trace and the same PMC passes, the FASTQ flow breakdown, one plain bench line.
 # Summarise with: python tools/summarize_profile.py --round r05 --src gpurun_out/prof5z
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -20,6 +21,15 @@ for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES 
            "SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $pmc -d $P/pmc$i -o run --output-format csv -- $B > $P/pmc$i.log 2>&1 || echo "pmc pass $i failed"
+done
+C="python3 tools/run_paths.py config5_allpairs"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $P/s5trace -o run --output-format csv -- $C > $P/s5trace.log 2>&1 || exit 3
+i=0
+for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \
+           "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES"; do
+  i=$((i+1))
+  timeout -s KILL 150 rocprofv3 --pmc $pmc -d $P/s5pmc$i -o run --output-format csv -- $C > $P/s5pmc$i.log 2>&1 || echo "s5 pmc pass $i failed"
 done
 timeout -k 10 300 python3 tools/fastq_flow_breakdown.py > $P/fastq_flow.json 2> $P/fastq_flow.err || exit 3
 timeout -k 10 500 python3 bench.py > $P/bench.log 2> $P/bench.err || exit 3
