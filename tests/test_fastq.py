@@ -235,6 +235,25 @@ def test_pieces_reader_carry_and_file_ends(tmp_path, monkeypatch, chunk):
             assert np.array_equal(cat, want[k][i]), (k, i)
 
 
+def test_pieces_reader_stops_when_abandoned(tmp_path, monkeypatch):
+    """A consumer that stops after the first piece: closing the generator stops the reader
+    threads (no thread left reading, the files closed), for the parallel and the in-order reader."""
+    import threading
+    p = tmp_path / "a.fastq"
+    p.write_bytes(b"@a\nACGTACGTAC\n+\nFFFFFFFFFF\n" * 5000)
+    gz = tmp_path / "a.fastq.gz"
+    gz.write_bytes(gzip.compress(p.read_bytes()))
+    monkeypatch.setattr(fastq._lib, "FastqStream", _FakeStream)
+    for path in (p, gz):
+        gen = fastq.EmbeddedBarcodeGenerator([fastq.EmbeddedBarcode(0, 4, "CR", "CY")], [str(path)], "rb")
+        it = gen._pieces(True, 4096)
+        first = next(it)
+        assert first[1] > 0
+        it.close()
+        alive = [t for t in threading.enumerate() if t.name.startswith("sctools-fastq-reader")]
+        assert not alive, alive
+
+
 def test_pieces_reader_propagates_open_errors(tmp_path, monkeypatch):
     """A missing file raises FileNotFoundError from the generator (after the pieces before it)."""
     p = tmp_path / "a.fastq"
