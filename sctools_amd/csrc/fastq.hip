@@ -42,7 +42,8 @@ constexpr int TB = TILE / WG;  // bytes per thread
 constexpr int SEG = TB / 16;   // 16-B loads per thread
 
 #ifndef SCT_FQ_ABL
-#define SCT_FQ_ABL 0  // timing-only ablations of the extraction kernels (tools/build_fq_abl.sh)
+#define SCT_FQ_ABL 0  // timing-only ablations of the extraction kernels (tools/build_fq_abl.sh; 5 = the
+                      // per-line row / length / code stores into an LDS sink instead of memory)
 #endif
 
 struct Files {
@@ -558,7 +559,18 @@ __device__ __forceinline__ uint4 bytes16_at(lds_u32* tile32, const uint32_t* __r
 
 // the first m (1..16) bytes of y to o in pieces of G bytes (G: the largest of 16 / 8 / 4 / 2 / 1
 // dividing the row width and the rows' base address; m is a multiple of G; both uniform)
+#if SCT_FQ_ABL == 5  // the per-line stores into an LDS sink: the same work, no global stores
+__device__ __forceinline__ void abl_sink(uint4 y) {
+  __shared__ uint4 sink[64];
+  sink[threadIdx.x & 63] = y;
+}
+#endif
+
 __device__ __forceinline__ void store_row16(uint8_t* o, const uint4 y, int m, int G) {
+#if SCT_FQ_ABL == 5
+  abl_sink(make_uint4(y.x ^ (uint32_t)(uintptr_t)o, y.y ^ (uint32_t)m, y.z ^ (uint32_t)G, y.w));
+  return;
+#endif
   const uint32_t d[4] = {y.x, y.y, y.z, y.w};
   if (G == 16) {
     *reinterpret_cast<uint4*>(o) = y;
@@ -627,7 +639,11 @@ __device__ __forceinline__ void line_spans(const Spans& sp, const TileOut& to, b
   for (int k = 0; k < nsp; ++k) {
     const int s_k = sp.start[k], e_k = sp.end[k], w = e_k - s_k;
     const int sa = s_k < llen ? s_k : llen, sb = e_k < llen ? e_k : llen;
+#if SCT_FQ_ABL == 5
+    if (len) abl_sink(make_uint4((uint32_t)(sb - sa), (uint32_t)(k * to.cap + rec), 0u, 0u));
+#else
     if (len) len[k * to.cap + rec] = sb - sa;
+#endif
     if (!out) continue;
     const bool enc = SCT_FQ_ABL != 3 && k == 0 && is_seq && to.codes0 != nullptr;
     uint8_t* row0 = out + sp.prefix[k] * to.cap;
@@ -673,6 +689,10 @@ __device__ __forceinline__ void line_spans(const Spans& sp, const TileOut& to, b
         fl |= en;
       }
     }
+#if SCT_FQ_ABL == 5
+    if (enc) abl_sink(make_uint4((uint32_t)code, (uint32_t)(code >> 32), fl, (uint32_t)rec));
+    continue;
+#endif
     if (enc) {
       to.codes0[rec] = code;
       if (to.gc0) {

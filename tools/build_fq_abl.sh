@@ -1,6 +1,6 @@
 #!/bin/bash
 # Timing-only ablation libraries of fastq_range_kernel (SCT_FQ_ABL = 1 no per-tile items, 2 name
-# checks only, 3 no CB encode, 4 no terminator list): sctools_amd/libsctools_hip_fqabl<k>.so,
+# checks only, 3 no CB encode, 4 no terminator list, 5 per-line stores into an LDS sink): sctools_amd/libsctools_hip_fqabl<k>.so,
 # loaded through SCTOOLS_HIP_LIB by tools/fastq_abl.py.  Wrong results by design.
 set -eu
 cd "$(dirname "$0")/../sctools_amd/csrc"
