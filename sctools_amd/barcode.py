@@ -71,27 +71,35 @@ class Barcodes:
         difference:`` never ends; that raises ValueError here instead of hanging.  The masking
         only preserves XORs WITHIN the set, so callers comparing the codes with outside values
         (``nearest``) pass ``mask_negative=False`` and get ValueError for any negative key."""
+        return self._codes_and_bits(mask_negative)[0]
+
+    def _codes_and_bits(self, mask_negative=True):
+        """codes_array() and, when the C key loop gave it for free, the bit length of the
+        largest code (None otherwise: the library takes it from the codes)."""
         keys = self._data.keys()
         n = len(self._data)
         # the common case (Python-int keys within int64) in one C loop (csrc/pykeys.c): the type
-        # check and the conversion together; every other case takes the general path below
+        # check, the conversion and the keys' min / max together (no numpy pass over the codes
+        # for the sign check or the width); every other case takes the general path below
         arr = np.empty(n, dtype=np.int64)
-        status, got = _pykeys.keys_to_int64(self._data if type(self._data) in (dict, Counter) else keys, arr)
+        status, got, lo, hi = _pykeys.keys_to_int64(self._data if type(self._data) in (dict, Counter) else keys, arr)
         if status == 0 and got == n:
-            return self._finish_int64(arr, mask_negative)
+            if lo >= 0:
+                return arr.view(np.uint64), int(hi).bit_length()
+            return self._finish_int64(arr, mask_negative), None
         if not all(issubclass(t, (int, np.integer)) for t in set(map(type, keys))):
             # the reference's pair loop dies at its first ``a ^ b`` on a non-integer key
             # (encodings.py:117 via barcode.py:42-43): raise exactly that TypeError
             for a, b in itertools.combinations(self._data, 2):
                 a ^ b
-            return np.zeros(n, dtype=np.uint64)  # < 2 keys: no pair, nothing to compare
+            return np.zeros(n, dtype=np.uint64), None  # < 2 keys: no pair, nothing to compare
         try:  # numpy integer keys within int64
-            return self._finish_int64(np.fromiter(keys, dtype=np.int64, count=n), mask_negative)
+            return self._finish_int64(np.fromiter(keys, dtype=np.int64, count=n), mask_negative), None
         except OverflowError:
             pass
         if not any(isinstance(k, np.signedinteger) and k < 0 for k in keys):  # (numpy would wrap those)
             try:
-                return np.fromiter(keys, dtype=np.uint64, count=n)
+                return np.fromiter(keys, dtype=np.uint64, count=n), None
             except OverflowError:
                 pass
         ints = [int(k) for k in keys]
@@ -103,7 +111,7 @@ class Barcodes:
                 raise ValueError(_MIXED_SIGNS)
             mask = (1 << max((~v).bit_length() for v in ints)) - 1
             ints = [v & mask for v in ints]
-        return _lib.ints_to_limbs(ints)
+        return _lib.ints_to_limbs(ints), None
 
     @staticmethod
     def _finish_int64(arr, mask_negative):
@@ -119,11 +127,11 @@ class Barcodes:
 
     def hamming_histogram(self):
         """np.uint64 histogram H[d] of TwoBit distances over all unordered pairs."""
-        codes = self.codes_array()
+        codes, bits = self._codes_and_bits()
         if codes.ndim == 2:  # keys >= 2^64: the multi-limb pair kernel
             hist = _lib.hamming_hist_allpairs_wide(codes)
         else:
-            hist = _lib.hamming_hist_allpairs(codes, distinct=True)  # mapping keys: distinct
+            hist = _lib.hamming_hist_allpairs(codes, bits, distinct=True)  # mapping keys: distinct
         want = (self._barcode_length + 1) if isinstance(self._barcode_length, int) else 0
         if want > hist.size:  # bins up to the barcode length, as np.bincount(minlength=L+1)
             hist = np.concatenate([hist, np.zeros(want - hist.size, dtype=hist.dtype)])
