@@ -214,6 +214,20 @@ def _profile(name):
     return None
 
 
+def _pmc_traffic(names, algo_per_unit):
+    """The committed PMC summaries of a path's kernels (_profile): HBM bytes per unit of each, their
+    sum and its ratio to the path's algorithmic bytes per unit (the 'traffic' of a side path)."""
+    ks = {}
+    for name in names:
+        pr = _profile(name)
+        if pr:
+            ks[name] = {k: pr.get(k) for k in ("file", "trace_avg_ns", "hbm_bytes_per_unit", "valu_busy_frac")}
+    if not ks or any(v["hbm_bytes_per_unit"] is None for v in ks.values()):
+        return None
+    tot = sum(v["hbm_bytes_per_unit"] for v in ks.values())
+    return {"kernels": ks, "bytes_per_unit": tot, "vs_algorithmic": tot / algo_per_unit}
+
+
 def _rocprof_avg_ms(kernel_substr, stats="kernel_stats"):
     """Average dispatch duration of a kernel in the committed rocprofv3 kernel trace of this
     bench command: over the timed steps' dispatches (profiles/<round>_timed_dispatches.json,
@@ -865,10 +879,12 @@ def path_whitelist(dev, reps, copy_gbs):
                 "workload": "config 5's whitelist file: %d lines of 16 bases + LF (%d bytes, device-resident): "
                             "line split (line[:-1]) + TwoBit encode + GC" % (n, nbytes),
                 "value": n / (ms_in * 1e-3), "unit": "lines/s", "ms": ms_in, "reps": reps,
-                "roofline": roof(algo_in, ms_in, "sct_whitelist_encode (wl_count_kernel + whitelist_fused_kernel)",
-                                 "algorithmic bytes: the file once + codes / starts / lens / GC / flags; a count "
-                                 "pass, a one-wave reduction of the tile counts and the encode pass (no scan "
-                                 "launch, no host sync)"),
+                "roofline": dict(roof(algo_in, ms_in, "sct_whitelist_encode (whitelist_spec16_kernel: one read of "
+                                      "a file of 16-base lines; wl_count_kernel + whitelist_fused_kernel otherwise)",
+                                      "algorithmic bytes: the file once + codes / starts / lens / GC / flags; 16-base "
+                                      "files in one pass that also checks the layout, the count and encode passes "
+                                      "returning at once (no scan launch, no host sync)"),
+                                 traffic=_pmc_traffic(("whitelist_spec16",), algo_in / n)),
                 "check": {"every_line": ok_in, "sample": "all %d codes, GC counts, starts and lengths vs the "
                                                          "generating codes, no flags" % n}},
             "base_frequency": {
@@ -989,6 +1005,7 @@ def path_fastq(dev, reps, copy_gbs):
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
                          "frac": gbs * 1e9 / HBM_PEAK_BPS, "frac_of_copy_ceiling": gbs / copy_gbs,
                          "algo_bytes_per_record": algo / n_rec, "kernel": "fastq_range_kernel (sct_fastq_extract_fused)",
+                         "traffic": _pmc_traffic(("fastq_count", "fastq_range"), algo / n_rec),
                          "note": "algorithmic bytes: the FASTQ once + the slices + codes; a count pass, a "
                                  "one-wave reduction of the tile counts, and the extraction (contiguous tile "
                                  "ranges carrying the line numbers, the CB encode fused); no scan launch, no "

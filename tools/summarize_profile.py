@@ -33,6 +33,7 @@ KERNELS = (
     ("spectral16", "tile16_kernel", "s5pmc", "s5trace", 65536, "slices of 2^16"),
     ("nearest", "halves_query_kernel", "npmc", "ntrace", 100_000_000, "queries"),
     ("nearest_index", "halves_index_kernel", "npmc", "ntrace", 100_000_000, "queries"),
+    ("whitelist_spec16", "whitelist_spec16_kernel", "ipmc", "itrace", 3_686_400, "lines"),
     ("whitelist_fused", "whitelist_fused_kernel", "ipmc", "itrace", 3_686_400, "lines"),
     ("fastq_range", "fastq_range_kernel", "ipmc", "itrace", 20_000_000, "records"),
     ("whitelist_count", "wl_count_kernel", "ipmc", "itrace", 3_686_400, "lines"),
