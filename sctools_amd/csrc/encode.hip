@@ -1156,21 +1156,23 @@ extern "C" int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, 
   const size_t in_b = pin_in ? 0 : (((size_t)chunk * L + 255) & ~(size_t)255);
   const size_t out_b = pin_out ? 0 : (size_t)chunk * 10;
   uint8_t* stage = nullptr;
+  sct::HostStage* hs = sct::host_stage();
+  if (!hs) return SCT_E_HIP;
   if (staged) {
-    sct::HostStage* hs = sct::host_stage();
-    if (!hs) return SCT_E_HIP;
     SCT_TRY(sct::stage_reserve(hs, NSTAGE * (in_b + out_b), 0));
     stage = hs->pinned;
   }
+  static_assert(NSTAGE <= 3, "HostStage::pipe holds three streams");
   hipStream_t st[NSTAGE] = {};
+  for (int k = 0; k < NSTAGE; ++k) {  // the thread's pipeline streams (kept across calls)
+    if (!hs->pipe[k]) SCT_HIP(hipStreamCreateWithFlags(&hs->pipe[k], hipStreamNonBlocking));
+    st[k] = hs->pipe[k];
+  }
   struct Streams {
     hipStream_t* s;
     ~Streams() {  // (an early return leaves nothing in flight on the stage or the device buffers)
       for (int k = 0; k < NSTAGE; ++k)
-        if (s[k]) {
-          (void)hipStreamSynchronize(s[k]);
-          (void)hipStreamDestroy(s[k]);
-        }
+        if (s[k]) (void)hipStreamSynchronize(s[k]);
     }
   } guard{st};
   // one device block per stage from the library's stream-ordered pool (records, then codes, GC,
@@ -1183,10 +1185,7 @@ extern "C" int sct_encode_stream_host(int kind, const uint8_t* seqs, int64_t n, 
     }
   } blk{{}, st};
   const size_t rec_b = ((size_t)chunk * L + 255) & ~(size_t)255;
-  for (int k = 0; k < NSTAGE; ++k) {
-    SCT_HIP(hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking));
-    SCT_HIP(sct::pool_alloc(&blk.p[k], rec_b + (size_t)chunk * 10, st[k]));
-  }
+  for (int k = 0; k < NSTAGE; ++k) SCT_HIP(sct::pool_alloc(&blk.p[k], rec_b + (size_t)chunk * 10, st[k]));
   struct StageDev {
     uint8_t* p;
   } din[NSTAGE], dcode[NSTAGE], dgc[NSTAGE], dfl[NSTAGE];

@@ -51,6 +51,9 @@ struct HostStage {
   size_t pinned_cap = 0;
   uint8_t* dev = nullptr;
   size_t dev_cap = 0;
+  // the host stream paths' pipeline streams (sct_encode_stream_host), created on first use and
+  // kept: a stream's creation and destruction cost more than a piece's copies (round 5)
+  hipStream_t pipe[3] = {nullptr, nullptr, nullptr};
 };
 // nullptr (with the error set) if the stage cannot be created.
 HostStage* host_stage();
