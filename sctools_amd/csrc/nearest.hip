@@ -999,11 +999,20 @@ extern "C" int sct_nearest_plan_create_host(int kind, const uint64_t* whitelist,
                                             sct_nearest_plan** out) {
   SCT_CHECK(out != nullptr, "plan is NULL");
   SCT_CHECK(nw >= 0 && (nw == 0 || whitelist), "bad whitelist");
-  sct::DevBuf dw;
-  SCT_HIP(dw.alloc((size_t)nw * 8));
-  if (nw) SCT_HIP(hipMemcpy(dw.p, whitelist, (size_t)nw * 8, hipMemcpyHostToDevice));
-  const int rc = sct_nearest_plan_create(kind, (const uint64_t*)dw.p, nw, code_bits, max_d, nullptr, out);
-  SCT_HIP(hipStreamSynchronize(nullptr));  // (the build has read the whitelist before it is freed)
+  // the whitelist through the library's stream-ordered pool on the thread's stream (no per-call
+  // hipMalloc / hipFree: a stream of batches builds its index once, but the flows that build
+  // one per file set pay it each time)
+  sct::HostStage* hs = sct::host_stage();
+  if (!hs) return SCT_E_HIP;
+  hipStream_t s = hs->stream;
+  void* dw = nullptr;
+  SCT_HIP(sct::pool_alloc(&dw, std::max<size_t>((size_t)nw * 8, 8), s));
+  hipError_t e = nw ? hipMemcpyAsync(dw, whitelist, (size_t)nw * 8, hipMemcpyHostToDevice, s) : hipSuccess;
+  int rc = e == hipSuccess ? sct_nearest_plan_create(kind, (const uint64_t*)dw, nw, code_bits, max_d, s, out)
+                           : sct::fail(SCT_E_HIP, "whitelist copy: %s", hipGetErrorString(e));
+  sct::pool_free(dw, s);  // (ordered after the build's reads of it)
+  e = hipStreamSynchronize(s);
+  if (rc == SCT_OK && e != hipSuccess) rc = sct::fail(SCT_E_HIP, "nearest plan: %s", hipGetErrorString(e));
   return rc;
 }
 
