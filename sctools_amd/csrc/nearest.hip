@@ -975,22 +975,13 @@ static int nearest_query_launch(sct_nearest_plan* p, const uint64_t* d_queries, 
 extern "C" int sct_nearest_host(int kind, const uint64_t* whitelist, int64_t nw, const uint64_t* queries,
                                 int64_t nq, int code_bits, int max_d, int32_t* index, uint8_t* dist) {
   SCT_CHECK(nw >= 0 && nq >= 0, "bad sizes");
-  sct::DevBuf dw, dq, di, dd;
-  SCT_HIP(dw.alloc((size_t)nw * 8));
-  if (nw) SCT_HIP(hipMemcpy(dw.p, whitelist, (size_t)nw * 8, hipMemcpyHostToDevice));
-  SCT_HIP(dq.alloc((size_t)nq * 8));
-  if (nq) SCT_HIP(hipMemcpy(dq.p, queries, (size_t)nq * 8, hipMemcpyHostToDevice));
-  SCT_HIP(di.alloc((size_t)nq * 4));
-  SCT_HIP(dd.alloc((size_t)nq));
+  // a host-whitelist plan and one host query pass (both through the library's stream-ordered
+  // pool on the thread's stream: no per-call hipMalloc / hipFree); the results are read back
+  // before the plan goes
   sct_nearest_plan* plan = nullptr;
-  int rc = sct_nearest_plan_create(kind, (const uint64_t*)dw.p, nw, code_bits, max_d, nullptr, &plan);
+  int rc = sct_nearest_plan_create_host(kind, whitelist, nw, code_bits, max_d, &plan);
   if (rc != SCT_OK) return rc;
-  rc = sct_nearest_query(plan, (const uint64_t*)dq.p, nq, (int32_t*)di.p, (uint8_t*)dd.p, nullptr);
-  if (rc == SCT_OK && nq) {  // (the copies wait for the query; the plan's tables are freed after)
-    hipError_t e = hipMemcpy(index, di.p, (size_t)nq * 4, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(dist, dd.p, (size_t)nq, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) rc = sct::fail(SCT_E_HIP, "nearest: %s", hipGetErrorString(e));
-  }
+  rc = sct_nearest_query_host(plan, queries, nq, index, dist);
   sct_nearest_plan_destroy(plan);
   return rc;
 }
