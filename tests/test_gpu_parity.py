@@ -825,6 +825,19 @@ def test_whitelist_corrector_batches(kind, max_d):
         assert np.array_equal(idx, ridx) and np.array_equal(dist, rdist)
         idx2, dist2 = barcode.nearest_whitelist(q, keep, max_distance=max_d, encoding=kind)
         assert np.array_equal(idx, idx2) and np.array_equal(dist, dist2)
+    # a flow-piece-sized batch (1.1M queries), page-locked and pageable: equal to the same
+    # queries sent as smaller batches, and to the brute force on a sample
+    big = batches[0][rng.integers(0, batches[0].size, 1_100_003)]
+    parts = [corr.nearest(big[s:s + 300_000]) for s in range(0, big.size, 300_000)]
+    pidx, pdist = np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
+    bigp = _lib.pinned.empty(big.size, np.uint64)
+    bigp[:] = big
+    samp = rng.integers(0, big.size, 3000)
+    ridx, rdist = O.c_nearest(kind, keep, big[samp], max_d)
+    for q in (big, bigp):
+        idx, dist = corr.nearest(q)
+        assert np.array_equal(idx, pidx) and np.array_equal(dist, pdist)
+        assert np.array_equal(idx[samp], ridx) and np.array_equal(dist[samp], rdist)
     corr.close()
     empty = barcode.WhitelistCorrector(np.zeros(0, np.uint64), max_distance=max_d, encoding=kind)
     idx, dist = empty.nearest(batches[0][:10])
