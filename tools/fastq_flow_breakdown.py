@@ -1,7 +1,9 @@
 """Where the drop-in FASTQ -> nearest flow (bench.path_fastq_stream_to_nearest) spends its time:
 the file pieces split into the read / carry-over in Python, the C chunk call (staging copies, H2D,
 index, extraction) and the fetch (D2H), then ThreeBit.encode_array and the WhitelistCorrector build and queries, each
-wrapped with a wall-clock timer.  One JSON line.  (GPU box; writes a 1.38 GB file under /tmp.)"""
+wrapped with a wall-clock timer.  One JSON line.  (GPU box; writes a 1.38 GB file under /tmp.)
+--no-stage: the next piece is not copied ahead (FastqStream.stage a no-op), to see what the
+caller's copies pay for sharing the link with it."""
 import json
 import os
 import sys
@@ -28,6 +30,8 @@ def wrap(obj, name, key):
     setattr(obj, name, timed)
 
 
+if "--no-stage" in sys.argv:
+    _lib.FastqStream.stage = lambda self, *a, **k: None
 wrap(_lib.FastqStream, "chunk", "stream.chunk (C chunk + fetch)")
 wrap(_lib.lib(), "sct_fastq_stream_chunk", "  sct_fastq_stream_chunk")
 wrap(_lib.lib(), "sct_fastq_stream_fetch", "  sct_fastq_stream_fetch")
@@ -39,5 +43,5 @@ dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
 r = bench.path_fastq_stream_to_nearest(dev, bench.host_threads()[0])
 T = {k: v for k, v in T.items()}  # both runs (warm + timed): halve for one
-print(json.dumps({"flow_ms": r.get("ms"), "breakdown_ms": r.get("breakdown_ms"),
+print(json.dumps({"no_stage": "--no-stage" in sys.argv, "flow_ms": r.get("ms"), "breakdown_ms": r.get("breakdown_ms"),
                   "wrapped_ms_two_runs": {k: v * 1e3 for k, v in T.items()}, "check": r.get("check")}))
