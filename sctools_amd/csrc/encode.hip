@@ -442,6 +442,110 @@ __global__ __launch_bounds__(WG) void base_frequency_kernel(const uint64_t* __re
   }
 }
 
+// L <= 16 (every output field j < 16 lies in a code's low 32 bits; the bits above are never
+// read): the same partials from 32-bit words at a third of the instructions.  Per code the
+// indicator masks m_v (bit 2j set when field j holds v = 1..3) come from x and x >> 1 by one
+// bitop3 each; three codes' masks add in one v_add3_u32 (2-bit fields, <= 3), five such sums
+// into nibble counters (fields 2i / 2i + 1 in nibble i of two words, <= 15), then into byte
+// counters (field 4k + {0, 2, 1, 3}[w] in byte k of word w).  The host sizes the grid so no
+// lane sees more than 255 codes.  The workgroup's 12 x 256 byte-counter words meet in LDS and
+// 192 threads sum them (byte pairs widened to 16-bit lanes, <= 256 * 255), so the epilogue is
+// 16 LDS reads and 8 shuffles per thread instead of 24 64-bit wave reductions per wave.
+__global__ __launch_bounds__(WG) void base_frequency16_kernel(const uint64_t* __restrict__ codes, int64_t n,
+                                                              unsigned long long* __restrict__ part) {
+  constexpr uint32_t K5 = 0x55555555u, K3 = 0x33333333u, KF = 0x0F0F0F0Fu;
+  __shared__ uint32_t xch[WG / 64][12][64];
+  __shared__ uint32_t cnt[16][4];  // [field j][value v]
+  __shared__ uint32_t seen_w[WG / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t G = (int64_t)gridDim.x * WG;
+  const uint32_t* lo32 = reinterpret_cast<const uint32_t*>(codes);  // (little endian: word 2r = low half)
+  uint32_t B[3][4] = {};
+  uint32_t seen = 0;
+  for (int64_t c0 = (int64_t)blockIdx.x * WG + tid; c0 - tid < n; c0 += 15 * G) {  // rounds of 15 codes
+    uint32_t xs[15];
+#pragma unroll
+    for (int u = 0; u < 15; ++u) {  // all 15 loads issued first (clamped, then zeroed: a zero adds no mask)
+      const int64_t r = c0 + u * G;
+      xs[u] = lo32[2 * (r < n ? r : n - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < 15; ++u) {
+      const bool in = c0 + u * G < n;
+      xs[u] = in ? xs[u] : 0u;
+      seen += in ? 1u : 0u;
+    }
+    uint32_t Ne[3] = {0, 0, 0}, No[3] = {0, 0, 0};
+#pragma unroll
+    for (int g = 0; g < 5; ++g) {
+      uint32_t m[3][3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const uint32_t x = xs[3 * g + t], y = x >> 1;
+        m[0][t] = x & ~y & K5;  // 01: value 1
+        m[1][t] = ~x & y & K5;  // 10: value 2
+        m[2][t] = x & y & K5;   // 11: value 3
+      }
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        const uint32_t S = m[v][0] + m[v][1] + m[v][2];
+        Ne[v] += S & K3;
+        No[v] += (S >> 2) & K3;
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+      B[v][0] += Ne[v] & KF;         // fields 4k
+      B[v][1] += (Ne[v] >> 4) & KF;  // fields 4k + 2
+      B[v][2] += No[v] & KF;         // fields 4k + 1
+      B[v][3] += (No[v] >> 4) & KF;  // fields 4k + 3
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < 3; ++v)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) xch[wave][4 * v + w][lane] = B[v][w];
+  for (int o = 32; o; o >>= 1) seen += __shfl_xor(seen, o);
+  if (lane == 0) seen_w[wave] = seen;
+  __syncthreads();
+  if (tid < 192) {  // word w = 4 v + q of all 256 lanes: 16 threads (one 16-lane group of a wave) per word
+    const int w = tid >> 4, sub = tid & 15;
+    uint32_t e = 0, o = 0;  // bytes 0, 2 / 1, 3 as 16-bit lanes
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int l = sub + 16 * i;
+      const uint32_t x = xch[l >> 6][w][l & 63];
+      e += x & 0x00FF00FFu;
+      o += (x >> 8) & 0x00FF00FFu;
+    }
+#pragma unroll
+    for (int s = 8; s; s >>= 1) {
+      e += __shfl_xor(e, s);
+      o += __shfl_xor(o, s);
+    }
+    if (sub == 0) {
+      const int v = w >> 2, q = w & 3, off = q == 0 ? 0 : (q == 1 ? 2 : (q == 2 ? 1 : 3));
+      cnt[off][v + 1] = e & 0xFFFFu;         // byte 0: field off
+      cnt[4 + off][v + 1] = o & 0xFFFFu;     // byte 1: field 4 + off
+      cnt[8 + off][v + 1] = e >> 16;         // byte 2
+      cnt[12 + off][v + 1] = o >> 16;        // byte 3
+    }
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const int j = tid >> 2, v = tid & 3;
+    uint32_t all = 0;
+#pragma unroll
+    for (int k = 0; k < WG / 64; ++k) all += seen_w[k];
+    uint32_t t = 0;
+    if (j < 16)
+      t = v ? cnt[j][v] : all - cnt[j][1] - cnt[j][2] - cnt[j][3];
+    else
+      t = v ? 0u : all;  // (fields 16..31 are not output for L <= 16)
+    part[(size_t)tid * gridDim.x + blockIdx.x] = t;
+  }
+}
+
 // out[4 (L - 1 - j) + v] = the sum of the workgroups' partials of (j, v) (one workgroup per
 // bin); bases p < L - 32 are all 0: n of value 0
 __global__ __launch_bounds__(WG) void base_frequency_reduce_kernel(const unsigned long long* __restrict__ part,
@@ -598,12 +702,21 @@ extern "C" int sct_base_frequency(const uint64_t* codes, int64_t n, int L, uint6
     SCT_HIP(hipMemsetAsync(out, 0, (size_t)L * 4 * 8, s));  // no code: every count 0
     return SCT_OK;
   }
-  // >= 32 codes per lane before the wave / workgroup reduction (at 8 per lane, 3.7M codes on 1,024
-  // workgroups, that epilogue -- 24 64-bit wave reductions per wave -- was most of the kernel)
-  const int blocks = (int)std::min<int64_t>(sct::ceil_div(n, 32 * WG), 512);
+  // 64-bit form: >= 32 codes per lane before the wave / workgroup reduction (at 8 per lane, 3.7M
+  // codes on 1,024 workgroups, that epilogue -- 24 64-bit wave reductions per wave -- was most of
+  // the kernel).  32-bit form (L <= 16): rounds of 15 codes per lane, never more than 255
+  int blocks = (int)std::min<int64_t>(sct::ceil_div(n, 32 * WG), 512);
+  if (L <= 16) {
+    // one round per lane (15 codes) measured best: 3.69M codes 15.6-17.7 us, two rounds 13.2-21.4,
+    // three 17.5-19.4, the 64-bit kernel 23.2-27.6 (profiles/ab_basefreq16_r05.jsonl)
+    blocks = (int)std::max<int64_t>(std::min<int64_t>(sct::ceil_div(n, 15 * WG), 4096), sct::ceil_div(n, 255 * WG));
+  }
   void* part = nullptr;
   SCT_HIP(sct::pool_alloc(&part, (size_t)128 * blocks * 8, s));
-  hipLaunchKernelGGL(base_frequency_kernel, dim3(blocks), dim3(WG), 0, s, codes, n, (unsigned long long*)part);
+  if (L <= 16)
+    hipLaunchKernelGGL(base_frequency16_kernel, dim3(blocks), dim3(WG), 0, s, codes, n, (unsigned long long*)part);
+  else
+    hipLaunchKernelGGL(base_frequency_kernel, dim3(blocks), dim3(WG), 0, s, codes, n, (unsigned long long*)part);
   hipError_t le = hipGetLastError();
   if (le == hipSuccess)
     hipLaunchKernelGGL(base_frequency_reduce_kernel, dim3(128), dim3(WG), 0, s, (const unsigned long long*)part,

@@ -1448,6 +1448,25 @@ def test_base_frequency_lengths(L):
         assert np.array_equal(got, want), (L, n)
 
 
+@pytest.mark.parametrize("L", [1, 5, 12, 16])
+def test_base_frequency_short_codes(L):
+    """The 32-bit form (L <= 16: base_frequency16_kernel) vs oracle.base_frequency_numpy: bits
+    above 2L set (never read), one and two rounds of 15 codes per lane, ragged n; and the byte
+    counters at their bound: a constant code repeated so that lanes see exactly 255 codes."""
+    rng = np.random.default_rng(100 + L)
+    for n in (15 * 256 * 7 + 3, 3_000_017) + ((20_000_003,) if L == 16 else ()):
+        codes = rng.integers(0, 1 << 63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+        assert np.array_equal(_lib.base_frequency(codes, L), O.base_frequency_numpy(codes, L)), (L, n)
+    if L == 16:
+        n = 4096 * 255 * 256 + 1  # the grid's 255-codes-per-lane bound
+        c = 0xDEADBEEF00000000 | 0b11100100_01001110_10110001_00011011
+        got = _lib.base_frequency(np.full(n, c, np.uint64), L)
+        want = np.zeros((L, 4), np.uint64)
+        for p in range(L):
+            want[p, (c >> (2 * (L - 1 - p))) & 3] = n
+        assert np.array_equal(got.reshape(L, 4), want)
+
+
 def test_lines_capacity_short_fills_nothing():
     """sct_lines with room for fewer lines than the buffer holds reports the count, a longest
     line of 0 and leaves the outputs untouched; with room for all of them it fills them
