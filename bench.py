@@ -895,7 +895,9 @@ def path_whitelist(dev, reps, copy_gbs):
             "base_frequency": {
                 "workload": "base_frequency over config 5's %d 16-bp codes (device-resident)" % n,
                 "value": n / (ms_bf * 1e-3), "unit": "codes/s", "ms": ms_bf, "reps": reps,
-                "roofline": roof(algo_bf, ms_bf, "base_frequency_kernel", "algorithmic bytes: the codes once"),
+                "roofline": dict(roof(algo_bf, ms_bf, "base_frequency16_kernel (L <= 16: 32-bit SWAR) + "
+                                      "base_frequency_reduce_kernel", "algorithmic bytes: the codes once"),
+                                 traffic=_pmc_traffic(("base_frequency16", "base_frequency_reduce"), algo_bf / n)),
                 "check": {"vs_oracle": ok_bf, "sample": "the whole table vs oracle.base_frequency_numpy"}}}
 
 

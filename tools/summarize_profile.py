@@ -38,6 +38,8 @@ KERNELS = (
     ("fastq_range", "fastq_range_kernel", "ipmc", "itrace", 20_000_000, "records"),
     ("whitelist_count", "wl_count_kernel", "ipmc", "itrace", 3_686_400, "lines"),
     ("fastq_count", "fq_count_kernel", "ipmc", "itrace", 20_000_000, "records"),
+    ("base_frequency16", "base_frequency16_kernel", "ipmc", "itrace", 3_686_400, "codes"),
+    ("base_frequency_reduce", "base_frequency_reduce_kernel", "ipmc", "itrace", 3_686_400, "codes"),
 )
 
 
