@@ -79,3 +79,54 @@ def test_base4_entropy_golden(golden):
     wl = golden["whitelist_1k"]
     got = base4_entropy(np.array(wl["base_frequency"]))
     assert [float(v) for v in got] == [float.fromhex(v) for v in wl["effective_diversity"]]
+
+
+def _keys_seq(keys):
+    """The key loop's contract (csrc/pykeys.c) restated in Python: (status, count, min, max)."""
+    out, lo, hi = [], None, None
+    for k in keys:
+        if not isinstance(k, int):
+            return 1, len(out), lo, hi
+        if not -(1 << 63) <= k < (1 << 63):
+            return 2, len(out), lo, hi
+        out.append(int(k))
+        lo = k if lo is None else min(lo, k)
+        hi = k if hi is None else max(hi, k)
+    return 0, len(out), lo, hi
+
+
+@pytest.mark.parametrize("case", ["plain", "negative", "bool_and_limits", "str_late", "float_early", "big_mid",
+                                  "deleted", "counter"])
+def test_parallel_key_loop_matches_sequential(case):
+    """Dicts of >= 2^17 keys take the threaded key loop (csrc/pykeys.c, four runs of the
+    entries array): the same keys, order, min / max, and the same stop status and count as
+    the sequential contract, wherever in the runs a non-int or a too-wide int sits."""
+    from collections import Counter
+
+    from sctools_amd import _pykeys
+    rng = np.random.default_rng(7)
+    n = 300_001
+    keys = [int(v) for v in rng.integers(0, 1 << 62, n)]
+    if case == "negative":
+        keys = [-k for k in keys]
+    elif case == "bool_and_limits":
+        keys[0], keys[1], keys[n // 2], keys[-1] = True, False, (1 << 63) - 1, -(1 << 63) + 1
+    elif case == "str_late":
+        keys[n - 5] = "ACGT"
+    elif case == "float_early":
+        keys[3] = 1.5
+    elif case == "big_mid":
+        keys[n // 4 + 3] = 1 << 70
+    keys = list(dict.fromkeys(keys))  # (unique, insertion order)
+    d = Counter(dict.fromkeys(keys, 1)) if case == "counter" else dict.fromkeys(keys, 1)
+    if case == "deleted":
+        for k in keys[10:20]:
+            del d[k]
+        keys = keys[:10] + keys[20:]
+    arr = np.zeros(len(keys), np.int64)
+    status, count, lo, hi = _pykeys.keys_to_int64(d, arr)
+    want = _keys_seq(keys)
+    assert (status, count) == want[:2]
+    assert arr[:count].tolist() == [int(k) for k in keys[:count]]
+    if status == 0:
+        assert (lo, hi) == want[2:]
