@@ -7,6 +7,7 @@ this module's ``lib()`` raises, and HIP failures (no device, launch errors) surf
 as ``RuntimeError`` with the library's message.
 """
 
+import collections
 import ctypes
 import os
 import threading
@@ -354,6 +355,7 @@ class PinnedPool:
         self._idle = 0
         self._held = 0  # page-locked bytes: blocks behind live arrays + idle blocks
         self._mu = threading.Lock()
+        self._pending = collections.deque()  # blocks handed back, not yet filed under _mu
         self._ok = True
         self._types = {}
 
@@ -372,6 +374,7 @@ class PinnedPool:
         if nbytes < self.MIN_BYTES or not self._ok:
             return np.empty(shape, dtype)
         c = self._class(nbytes)
+        self._drain()
         with self._mu:
             blocks = self._free.get(c)
             ptr = blocks.pop() if blocks else None
@@ -398,21 +401,41 @@ class PinnedPool:
         return np.frombuffer(buf, dtype=dtype, count=count).reshape(shape)
 
     def _release(self, ptr, c):
-        with self._mu:
-            if self._idle + c <= self.keep_bytes:
-                self._free.setdefault(c, []).append(ptr)
-                self._idle += c
-                return
-            self._held -= c
-        lib().sct_host_free(_vp(ptr))
+        # a weakref.finalize callback: it can run inside a cyclic collection that an allocation
+        # made while this thread holds _mu started, so it never waits on _mu -- the
+        # block goes on a lock-free queue and whoever holds or next takes the lock files it
+        self._pending.append((ptr, c))
+        self._drain()
+
+    def _drain(self):
+        if not self._mu.acquire(blocking=False):
+            return  # (the holder -- maybe this very thread -- drains the queue before it lets go)
+        to_free = []
+        try:
+            while self._pending:
+                ptr, c = self._pending.popleft()
+                if self._idle + c <= self.keep_bytes:
+                    self._free.setdefault(c, []).append(ptr)
+                    self._idle += c
+                else:
+                    self._held -= c
+                    to_free.append(ptr)
+        finally:
+            self._mu.release()
+        for p in to_free:
+            lib().sct_host_free(_vp(p))
+        if self._pending:  # (queued by another thread between the last pop and the release)
+            self._drain()
 
     def trim(self):
         """Free every idle block."""
+        self._drain()
         with self._mu:
             ptrs = [p for blocks in self._free.values() for p in blocks]
             self._free.clear()
             self._held -= self._idle
             self._idle = 0
+        self._drain()  # (blocks handed back while the lock was held go idle, then stay for reuse)
         for p in ptrs:
             lib().sct_host_free(_vp(p))
 

@@ -196,21 +196,30 @@ class Barcodes:
     @classmethod
     def from_iterable_strings(cls, iterable, barcode_length):
         """construct an ObservedBarcodeSet from an iterable of string barcodes"""
-        return cls(Counter(_encode_lines([b.encode() for b in iterable])), barcode_length=barcode_length)
+        return cls(Counter(_encode_items(iterable, lambda b: _item_bytes(b.encode()))), barcode_length=barcode_length)
 
     @classmethod
     def from_iterable_bytes(cls, iterable, barcode_length):
         """construct an ObservedBarcodeSet from an iterable of bytes barcodes"""
-        seqs = []
-        try:
-            for b in iterable:
-                seqs.append(_item_bytes(b))
-        except Exception:
-            # the reference encodes item by item (barcode.py:114), so the items before the bad one
-            # have made their random draws when its error surfaces
-            _encode_lines(seqs)
-            raise
-        return cls(Counter(_encode_lines(seqs)), barcode_length=barcode_length)
+        return cls(Counter(_encode_items(iterable, _item_bytes)), barcode_length=barcode_length)
+
+
+def _encode_items(iterable, to_bytes):
+    """TwoBit codes of ``to_bytes(item)`` for every item, in order, batched on the GPU.
+
+    The reference takes item, converts, encodes, then the next item (barcode.py:104-114, a
+    generator inside Counter).  So when an item's conversion fails -- or the iterable itself
+    raises -- the items before it have already made their random draws, and an earlier item's
+    KeyError surfaces instead: the items taken so far are encoded (draws and KeyError in record
+    order) before the error is re-raised."""
+    seqs = []
+    try:
+        for b in iterable:
+            seqs.append(to_bytes(b))
+    except Exception:
+        _encode_lines(seqs)
+        raise
+    return _encode_lines(seqs)
 
 
 def _item_bytes(b):

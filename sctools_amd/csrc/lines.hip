@@ -840,7 +840,7 @@ extern "C" int sct_whitelist_encode(const uint8_t* d_buf, int64_t nbytes, int ki
   const int direct = ntiles <= sct::tune(SCT_TUNE_INGEST_DIRECT, 4096) ? 1 : 0;
   if (!direct) {
     hipLaunchKernelGGL(sct::tile_sums_reduce_kernel, dim3((unsigned)sct::ceil_div(ntiles, 1024)), dim3(64), 0, s, ts,
-                       ntiles);
+                       ntiles, (const unsigned*)spec_fail, gen);
     SCT_LAUNCH_CHECK();
   }
   auto kern = kind == 2 ? whitelist_fused_kernel<2> : whitelist_fused_kernel<3>;

@@ -17,8 +17,8 @@
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
-#include <longintrepr.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <unistd.h>
 
@@ -47,6 +47,7 @@ static int put_key(PyObject* k, int64_t* out, Py_ssize_t cap, Py_ssize_t* i, int
  * other key ends a worker's run with the status the sequential loop would give it. */
 #if PY_VERSION_HEX >= 0x030A0000 && PY_VERSION_HEX < 0x030B0000
 #define SCT_PARALLEL_KEYS 1
+#include <longintrepr.h> /* (3.10 only: from 3.11 it lives under cpython/ and Python.h has it) */
 typedef struct {
   Py_hash_t me_hash;
   PyObject* me_key;
@@ -132,8 +133,16 @@ static int keys_parallel(PyObject* d, int64_t* out, Py_ssize_t cap, int* status,
   if (e[n - 1].me_key == NULL || e[n - 1].me_value == NULL) return 0;
   pos = n - 1;
   if (!PyDict_Next(d, &pos, &k, &v) || k != e[n - 1].me_key || PyDict_Next(d, &pos, &k, &v)) return 0;
-  const long cpus = sysconf(_SC_NPROCESSORS_ONLN);
-  const int T = cpus >= kThreads ? kThreads : (cpus > 1 ? (int)cpus : 1);
+  /* the CPUs this process may run on (affinity mask / cpuset), not the machine's: a pinned or
+   * quota-limited caller gets no more threads than it has CPUs, and one CPU the plain loop */
+  long cpus = 1;
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0)
+    cpus = CPU_COUNT(&set);
+  else
+    cpus = sysconf(_SC_NPROCESSORS_ONLN);
+  if (cpus <= 1) return 0;
+  const int T = cpus >= kThreads ? kThreads : (int)cpus;
   Run runs[kThreads];
   pthread_t tid[kThreads];
   int started[kThreads] = {0};

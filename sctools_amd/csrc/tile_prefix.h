@@ -53,8 +53,13 @@ __device__ __forceinline__ void tile_publish(const TileSums& s, int64_t t, unsig
 }
 
 // one 64-lane wave per 1,024 tiles: lane i sums tiles [16 i, 16 i + 16) of the block, lane pairs
-// form the 32-tile sums, the wave the 1,024-tile sum (launch ceil(ntiles / 1024) blocks of 64)
-static __global__ __launch_bounds__(64) void tile_sums_reduce_kernel(TileSums s, int64_t ntiles) {
+// form the 32-tile sums, the wave the 1,024-tile sum (launch ceil(ntiles / 1024) blocks of 64).
+// skip / skip_gen: as the count passes' spec_fail / spec_gen -- when a one-read pass ran and did
+// the whole job (*skip != skip_gen) the count pass wrote nothing, so there is nothing to reduce
+static __global__ __launch_bounds__(64) void tile_sums_reduce_kernel(TileSums s, int64_t ntiles,
+                                                                     const unsigned* skip = nullptr,
+                                                                     unsigned skip_gen = 0) {
+  if (skip && *skip != skip_gen) return;
   const int lane = threadIdx.x;
   const int64_t t0 = (int64_t)blockIdx.x * 1024 + 16 * lane;
   unsigned long long c = 0, l = 0;

@@ -135,7 +135,12 @@ class _ParallelPieceReader:
     ceiling), and get() hands the segments back in order.  Buffers go to segments in segment
     order (one worker at a time takes the next free buffer and the next segment number), so the
     segment the consumer waits for always holds a buffer.  File ends as _PieceReader reports
-    them: a file ending exactly at a segment's end is that of the next segment, at 0."""
+    them: a file ending exactly at a segment's end is that of the next segment, at 0.
+
+    The files' sizes are taken when they are opened (a snapshot: the segments need them), where the
+    sequential reader reads each file to its EOF when it gets there.  So a file still being appended
+    to would give different records: the last segment checks every size again and raises OSError,
+    after the records before it, when one changed."""
 
     def __init__(self, files, buffers, head, workers):
         self._head = head
@@ -149,6 +154,7 @@ class _ParallelPieceReader:
             self._close_fds()
             raise
         sizes = [os.fstat(fd).st_size for fd in self._fds]
+        self._sizes = sizes
         self._bounds = list(itertools.accumulate(sizes))  # the files' ends in the concatenation
         self._starts = [b - z for b, z in zip(self._bounds, sizes)]
         total = self._bounds[-1] if self._bounds else 0
@@ -190,6 +196,9 @@ class _ParallelPieceReader:
                     raise OSError("short read of a FASTQ file (it changed while being read?)")
                 a += got
         ends = [e - lo for e in self._bounds if lo <= e < lo + self._cap]
+        if k == self._nseg - 1 and [os.fstat(fd).st_size for fd in self._fds] != self._sizes:
+            raise OSError("a FASTQ file changed size while being read (the parallel reader reads the "
+                          "sizes the files had when they were opened)")
         return buf, hi - lo, ends, k == self._nseg - 1
 
     def _work(self):

@@ -32,6 +32,16 @@ def call(fn, *args):
     return {"value": str(r)}
 
 
+def iterable_from_spec(spec):
+    """The items of an edges.json from_iterable_strings case, as a generator (tests rebuild
+    them with the same function: tests/test_gpu_parity.py imports it from here)."""
+    for item in spec:
+        tag = item[0]
+        if tag == "raise":
+            raise RuntimeError(item[1])
+        yield {"s": lambda v: v, "b": bytes.fromhex, "i": int, "f": float, "n": lambda *a: None}[tag](*item[1:])
+
+
 def main():
     enc, bc, _ = load_reference()
     TwoBit, ThreeBit = enc.TwoBit, enc.ThreeBit
@@ -106,6 +116,37 @@ def main():
             rec["error"] = exc_record(e)
         ib.append(rec)
     out["from_iterable_bytes"] = ib
+
+    # ---- Barcodes.from_iterable_strings (barcode.py:104-108): `b.encode()` and the encode run
+    # item by item inside the Counter's generator, so an item that fails raises only after the
+    # items before it made their random draws, and an earlier item's KeyError comes first.
+    # Items are JSON specs (built by iterable_from_spec): ["s", str], ["b", hex bytes],
+    # ["i", int], ["f", float], ["n"] (None), ["raise", msg] (the iterable raises RuntimeError)
+    fs = []
+    for name, spec, L, seed in (
+            ("keyerror_before_attr", [["s", "ACGP"], ["i", 5]], 4, 11),
+            ("draws_before_attr", [["s", "ANNA"], ["i", 5]], 4, 12),
+            ("none", [["n"]], 4, 13),
+            ("bytes_item", [["s", "ACGT"], ["b", "41434754"]], 4, 14),
+            ("float_after_n", [["s", "NNNN"], ["f", 1.5]], 4, 15),
+            ("non_ascii", [["s", "NN"], ["s", "ACéG"], ["s", "NNNN"]], 4, 16),
+            ("keyerror_mid", [["s", "NNNN"], ["s", "ACGX"], ["s", "NNNN"]], 4, 17),
+            ("generator_raises", [["s", "ACGT"], ["s", "NNAC"], ["raise", "boom"], ["s", "NNNN"]], 4, 18),
+            ("raises_after_bad", [["s", "NACGTX"], ["raise", "boom"]], 6, 19),
+            ("ok_ragged", [["s", "ACGT"], ["s", "NN"], ["s", "ACGTNA"], ["s", "ACGT"], ["s", ""]], 4, 20),
+            ("ok_with_n", [["s", "ANNA"], ["s", "acgt"], ["s", "ANNA"], ["s", "ryky"]], 4, 21),
+            ("empty", [], 4, 22)):
+        rec = {"name": name, "spec": spec, "L": L, "seed": seed}
+        random.seed(seed)
+        try:
+            s = bc.Barcodes.from_iterable_strings(iterable_from_spec(spec), L)
+            rec["codes"] = [str(k) for k in s]
+            rec["counts"] = [s[k] for k in s]
+        except Exception as e:
+            rec["error"] = exc_record(e)
+        rec["after"] = random.getrandbits(32)
+        fs.append(rec)
+    out["from_iterable_strings"] = fs
 
     # calls the reference never returns from (not executed here)
     out["hangs"] = {

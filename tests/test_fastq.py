@@ -265,6 +265,32 @@ def test_pieces_reader_propagates_open_errors(tmp_path, monkeypatch):
         list(gen._pieces(True, 64))
 
 
+def test_parallel_reader_detects_a_growing_file(tmp_path):
+    """The parallel reader reads the sizes the files had when opened; a file appended to while it
+    reads is reported (OSError on the last segment), not silently cut."""
+    p = tmp_path / "a.fastq"
+    p.write_bytes(b"@a\nACGT\n+\nFFFF\n" * 1000)
+    bufs = [np.zeros(64 + 4096, np.uint8) for _ in range(4)]
+    r = fastq._ParallelPieceReader([str(p)], bufs, 64, 1)
+    try:
+        with open(p, "ab") as f:  # grows before the reader reaches its last segment
+            f.write(b"@b\nACGT\n+\nFFFF\n")
+        r.start()
+        items = []
+        while True:
+            it = r.get()
+            if isinstance(it, BaseException):
+                items.append(it)
+                break
+            items.append(it)
+            r.free.put(it[0])
+            if it[3]:
+                break
+        assert isinstance(items[-1], OSError) and "changed size" in str(items[-1])
+    finally:
+        r.close()
+
+
 def test_last_line_end_windows():
     """The piece cut: 1 + the last '\\n' in buf[:have], found back from the end in growing windows."""
     buf = np.full(300_000, ord("A"), np.uint8)

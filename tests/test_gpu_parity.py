@@ -197,6 +197,29 @@ def test_from_iterable_bytes_items_golden(golden_edges):
             assert [str(k) for k in s] == rec["codes"] and [s[k] for k in s] == rec["counts"]
 
 
+def test_from_iterable_strings_items_golden(golden_edges):
+    """barcode.py:104-108 item by item: the first failing item's error (or an earlier item's
+    KeyError) after exactly the draws the reference makes, or its codes; the RNG state after
+    the call matches the reference's (VERDICT r5 weak #1)."""
+    import builtins
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from gen_golden_edges import iterable_from_spec
+    for rec in golden_edges["from_iterable_strings"]:
+        random.seed(rec["seed"])
+        its = iterable_from_spec(rec["spec"])
+        if "error" in rec:
+            with pytest.raises(getattr(builtins, rec["error"]["type"])) as ei:
+                barcode.Barcodes.from_iterable_strings(its, rec["L"])
+            assert type(ei.value).__name__ == rec["error"]["type"], rec["name"]
+            assert list(ei.value.args) == rec["error"]["args"], rec["name"]
+        else:
+            s = barcode.Barcodes.from_iterable_strings(its, rec["L"])
+            assert [str(k) for k in s] == rec["codes"] and [s[k] for k in s] == rec["counts"], rec["name"]
+        assert random.getrandbits(32) == rec["after"], rec["name"]
+
+
 def test_reference_simple_barcodes(golden):
     sb = golden["simple_barcodes"]
     seqs = [bytes.fromhex(s) for s in sb["seqs"]]
