@@ -914,11 +914,24 @@ def path_dropin(dev, reps, want_summary):
     b = barcode.Barcodes(dict.fromkeys((int(c) for c in codes), 1), L)
     first = b.summarize_hamming_distances()
     torch.cuda.synchronize()
-    ts = []
-    for _ in range(reps):
-        t = time.perf_counter()
-        r = b.summarize_hamming_distances()
-        ts.append((time.perf_counter() - t) * 1e3)
+
+    def timed():
+        out = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            r = b.summarize_hamming_distances()
+            out.append((time.perf_counter() - t) * 1e3)
+        return out, r
+    # the default policy (every call maps and frees its own device memory), then the opt-in
+    # workspace cache (sctools_amd.keep_workspace(True): nothing mapped after the first call)
+    prev = _lib.keep_workspace(False)
+    free0 = torch.cuda.mem_get_info()[0]
+    ts, r = timed()
+    leaked = free0 - torch.cuda.mem_get_info()[0]
+    _lib.keep_workspace(True)
+    b.summarize_hamming_distances()
+    ts_keep, r_keep = timed()
+    kept = free0 - torch.cuda.mem_get_info()[0]
     parts = {"codes_array_ms": [], "hist_call_ms": [], "summary_ms": []}
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -931,19 +944,27 @@ def path_dropin(dev, reps, want_summary):
         parts["codes_array_ms"].append((t1 - t0) * 1e3)
         parts["hist_call_ms"].append((t2 - t1) * 1e3)
         parts["summary_ms"].append((t3 - t2) * 1e3)
+    _lib.keep_workspace(prev)
+    _lib.release_plan_cache()
     med = lambda v: float(sorted(v)[len(v) // 2])  # noqa: E731
     ms = med(ts)
     P = n * (n - 1) // 2
-    got = [float(r[k]) for k in ("minimum", "25th percentile", "median", "75th percentile", "maximum", "average")]
+    keys = ("minimum", "25th percentile", "median", "75th percentile", "maximum", "average")
+    got = [float(r[k]) for k in keys]
     return {"workload": "Barcodes(dict of the %d config-2 codes, L=%d).summarize_hamming_distances(): host keys in, "
                         "summary dict out, one call at a time" % (n, L),
             "value": P / (ms * 1e-3), "unit": "pair-equivalents/s", "ms": ms, "ms_all": ts, "reps": reps,
+            "device_bytes_left_after_calls": int(leaked),
+            "keep_workspace": {"ms": med(ts_keep), "ms_all": ts_keep, "device_bytes_held": int(kept)},
             "breakdown_ms": {k: med(v) for k, v in parts.items()},
-            "note": "hist_call = sct_hamming_hist_allpairs_host: H2D of the codes, plan on the cached workspace "
-                    "(probe + one sync), build, count (SPECTRAL), D2H, exact inversion; codes_array = the "
-                    "mapping's keys -> uint64 with the reference's type semantics (host)",
+            "note": "ms: the default policy, every call maps and frees its own device memory (4 GiB transform "
+                    "intermediate + codes); keep_workspace: sctools_amd.keep_workspace(True), the buffers cached "
+                    "per device between calls (breakdown under this setting).  hist_call = "
+                    "sct_hamming_hist_allpairs_host_ex: H2D of the codes, plan (probe + one sync), build, count "
+                    "(SPECTRAL), D2H, exact inversion; codes_array = the mapping's keys -> uint64 with the "
+                    "reference's type semantics (host)",
             "check": {"summary_equals_headline": (want_summary is None or got == [float(x) for x in want_summary])
-                      and [float(first[k]) for k in first] == got}}
+                      and [float(first[k]) for k in first] == got and [float(r_keep[k]) for k in keys] == got}}
 
 
 def _guarded(fn, *a):

@@ -244,6 +244,9 @@ typedef struct sct_allpairs_plan sct_allpairs_plan;
  *   sum f^2 = n instead of sorting the codes; a broken promise fails the host's exact check
  *   (SCT_E_RANGE), it never yields a histogram. */
 #define SCT_ALLPAIRS_DISTINCT 1
+/* SCT_ALLPAIRS_NO_CACHE  the plan allocates its own device buffers and frees them when destroyed,
+ *   instead of borrowing its device's cached workspace (see sct_allpairs_cache_release). */
+#define SCT_ALLPAIRS_NO_CACHE 2
 
 /* = sct_allpairs_plan_create_ex(..., SCT_ALLPAIRS_AUTO, plan) */
 int sct_allpairs_plan_create(const uint64_t* d_codes, int64_t n, int code_bits,
@@ -324,9 +327,42 @@ int sct_counts_to_hist_ex(int scheme, const uint64_t* counts, int ncounts, uint6
  * unordered pairs of the n codes.  hist must hold nbins = 2*ceil(code_bits/4)+1. */
 int sct_hamming_hist_allpairs_host(const uint64_t* codes, int64_t n, int code_bits,
                                    uint64_t* hist, int nbins);
-/* the same with SCT_ALLPAIRS_* plan flags */
+/* the same with SCT_ALLPAIRS_DISTINCT.  By default a one-shot call leaves no device memory
+ * behind: its plan and staging buffers are its own and freed before it returns (4 GiB for a
+ * 16-base set from 325K codes).  sct_keep_workspace(1) keeps them cached per device instead, so
+ * repeated calls map nothing (previous: the setting before the call; keep < 0 only reads it). */
 int sct_hamming_hist_allpairs_host_ex(const uint64_t* codes, int64_t n, int code_bits, int flags,
                                       uint64_t* hist, int nbins);
+int sct_keep_workspace(int keep, int* previous);
+
+/* ---------------------------------------------------------------- several devices, one process
+ * SURVEY §8(b) `n_gpus` (sct_init(n_gpus) / an n_gpus argument in the survey's sketch): the
+ * one-shot and host-stream calls split across devices[0..ndev) of this process (HIP ordinals;
+ * repeats are logical shards of one GPU).  Slot r runs on a persistent worker thread of its own
+ * with devices[r] current; the calling thread's current device is not changed.  devices == NULL
+ * or ndev == 1: the single-device call on the current device (or devices[0]).  One multi-device
+ * call runs at a time per process (calls from several threads queue).
+ *
+ * All-pairs (replaces barcode.py:42-43 like sct_hamming_hist_allpairs_host_ex): every slot holds
+ * a replica of the codes and counts the item range items*r/ndev .. items*(r+1)/ndev (SPECTRAL:
+ * transform slices) plus moment part r of ndev; the 53 / 17 / nbins counts of the slots are summed
+ * on the host -- where they are needed anyway -- and inverted once.  Bit-identical for any ndev. */
+int sct_hamming_hist_allpairs_host_devices(const uint64_t* codes, int64_t n, int code_bits, int flags,
+                                           const int* devices, int ndev, uint64_t* hist, int nbins);
+/* Nearest whitelist: contiguous query ranges per slot, the whitelist indexed on every device
+ * (no exchange).  The multi plan keeps one index per slot for a stream of query batches. */
+int sct_nearest_host_devices(int kind, const uint64_t* whitelist, int64_t nw, const uint64_t* queries, int64_t nq,
+                             int code_bits, int max_d, const int* devices, int ndev, int32_t* index,
+                             uint8_t* dist);
+typedef struct sct_nearest_multi sct_nearest_multi;
+int sct_nearest_multi_create_host(int kind, const uint64_t* whitelist, int64_t nw, int code_bits, int max_d,
+                                  const int* devices, int ndev, sct_nearest_multi** plan);
+int sct_nearest_multi_query_host(sct_nearest_multi* plan, const uint64_t* queries, int64_t nq, int32_t* index,
+                                 uint8_t* dist);
+int sct_nearest_multi_destroy(sct_nearest_multi* plan);
+/* Host encode stream (sct_encode_stream_host) over contiguous record ranges, one per slot. */
+int sct_encode_stream_host_devices(int kind, const uint8_t* seqs, int64_t n, int L, uint64_t* codes, uint8_t* gc,
+                                   uint8_t* flags, int64_t chunk, const int* devices, int ndev);
 
 /* Plan cache: a plan created while no other plan holds its device's cached buffers borrows
  * them (the SPECTRAL intermediate of up to 4 GiB, codes, bit planes, order table) and leaves
@@ -335,7 +371,8 @@ int sct_hamming_hist_allpairs_host_ex(const uint64_t* codes, int64_t n, int code
  * every idle cache (all devices); a cache lent to a live plan is freed when that plan is
  * destroyed.  sct_tune_set(SCT_TUNE_PLAN_CACHE, 0) turns the cache off.  The idle memory of
  * the library's stream-ordered scratch pool (host-stream stages, ingest scratch) is trimmed
- * too, after a synchronisation of the current device. */
+ * too, after a synchronisation of the current device, and the calling thread's staging buffer
+ * on the current device is freed. */
 int sct_allpairs_cache_release(void);
 
 /* ---------------------------------------------------------------- all-pairs, wide codes

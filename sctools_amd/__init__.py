@@ -24,4 +24,21 @@ def release_device_memory():
         _lib.release_plan_cache()
         _lib.pinned.trim()
 
+
+def set_devices(devices):
+    """GPUs the drop-in's large calls split over inside the library (the all-pairs summary,
+    nearest-whitelist correction, the host encode stream): HIP ordinals, a repeated ordinal being
+    a logical shard of one GPU; ``None`` (the default) = every visible device."""
+    from . import _lib
+    _lib.set_devices(devices)
+
+
+def keep_workspace(keep=None):
+    """False (default): a one-shot all-pairs summary frees all the device memory it mapped before it
+    returns.  True: it stays cached per device for the next call (``release_device_memory()``
+    hands it back).  Returns the previous setting; ``None`` only reads it."""
+    from . import _lib
+    return _lib.keep_workspace(keep)
+
+
 __version__ = "0.1.0"

@@ -122,6 +122,13 @@ SIGNATURES = {
     "sct_scalar_server_stop": [],
     "sct_stream_copy": [_vp, _vp, _i64, _vp],
     "sct_scalar_server_status": [ctypes.POINTER(_i64), ctypes.POINTER(_i32)],
+    "sct_keep_workspace": [_i32, ctypes.POINTER(_i32)],
+    "sct_hamming_hist_allpairs_host_devices": [_vp, _i64, _i32, _i32, _vp, _i32, _vp, _i32],
+    "sct_nearest_host_devices": [_i32, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _i32, _vp, _vp],
+    "sct_nearest_multi_create_host": [_i32, _vp, _i64, _i32, _i32, _vp, _i32, ctypes.POINTER(_vp)],
+    "sct_nearest_multi_query_host": [_vp, _vp, _i64, _vp, _vp],
+    "sct_nearest_multi_destroy": [_vp],
+    "sct_encode_stream_host_devices": [_i32, _vp, _i64, _i32, _vp, _vp, _vp, _i64, _vp, _i32],
 }
 _RESTYPES = {"sct_last_error": ctypes.c_char_p}
 
@@ -225,6 +232,66 @@ def _ptr(a):
     return a.ctypes.data_as(_vp) if a is not None else None
 
 
+# ------------------------------------------------------------------ devices
+# The drop-in's large calls split over these devices inside the library (devices.cpp: one worker
+# thread per slot, no torch.distributed): the all-pairs summary from the SPECTRAL threshold, nearest
+# and the host encode stream from MULTI_MIN_RECORDS.  None = every visible device.
+_devices = None
+MULTI_MIN_RECORDS = 1 << 22
+
+
+def set_devices(devices):
+    """Use ``devices`` (HIP ordinals; a repeated ordinal is a logical shard of one GPU) for the
+    drop-in's multi-device calls; ``None`` restores the default, every visible device."""
+    global _devices
+    if devices is None:
+        _devices = None
+        return
+    devs = [int(d) for d in devices]
+    if not devs:
+        raise ValueError("set_devices needs at least one device")
+    _devices = devs
+
+
+def get_devices():
+    """The devices multi-device calls split over (default: every visible device)."""
+    if _devices is not None:
+        return list(_devices)
+    n = device_count()
+    return list(range(n)) if n > 1 else [0]
+
+
+def _devs(devices, size, threshold):
+    """The device list a call of ``size`` records uses: the explicit one, else the configured
+    devices when the call is large enough to split; None = the current device alone."""
+    if devices is not None:
+        devs = [int(d) for d in devices]
+        return devs if len(devs) > 1 else None
+    if size < threshold:
+        return None
+    devs = get_devices()
+    return devs if len(devs) > 1 else None
+
+
+def _dev_array(devs):
+    return (ctypes.c_int * len(devs))(*devs)
+
+
+def keep_workspace(keep=None):
+    """The all-pairs one-shot's device memory policy; returns the previous setting.  False (the
+    default): a call frees every device buffer it allocated before it returns (a 737K summary maps
+    and unmaps its 4 GiB transform intermediate each time).  True: the buffers stay cached per
+    device, so repeated calls map nothing (``release_device_memory()`` frees them).  None: read."""
+    prev = _i32(0)
+    check(lib().sct_keep_workspace(-1 if keep is None else int(bool(keep)), ctypes.byref(prev)))
+    return bool(prev.value)
+
+
+def _spectral_min_n():
+    v = tune_get("spectral_min_n")
+    return 325000 if v < 0 else v
+
+
 # ------------------------------------------------------------------ int <-> limbs
 def words_for_bits(bits):
     return max(1, -(-int(bits) // 64))
@@ -311,15 +378,21 @@ def encode(kind, seqs, L):
     return codes, gc, flags
 
 
-def encode_stream(kind, seqs, chunk=0):
+def encode_stream(kind, seqs, chunk=0, devices=None):
     """Host (n, L) uint8 records -> (codes uint64[n], gc uint8[n], flags uint8[n]) through the
-    pipelined H2D/encode/D2H stream (one limb per code)."""
+    pipelined H2D/encode/D2H stream (one limb per code); large batches split over the devices
+    (contiguous record ranges, see set_devices)."""
     seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
     n, L = seqs.shape
     codes = pinned.empty(n, np.uint64)
     gc = pinned.empty(n, np.uint8)
     flags = pinned.empty(n, np.uint8)
-    check(lib().sct_encode_stream_host(kind, _ptr(seqs), n, L, _ptr(codes), _ptr(gc), _ptr(flags), chunk))
+    devs = _devs(devices, n, MULTI_MIN_RECORDS)
+    if devs:
+        check(lib().sct_encode_stream_host_devices(kind, _ptr(seqs), n, L, _ptr(codes), _ptr(gc), _ptr(flags), chunk,
+                                                   _dev_array(devs), len(devs)))
+    else:
+        check(lib().sct_encode_stream_host(kind, _ptr(seqs), n, L, _ptr(codes), _ptr(gc), _ptr(flags), chunk))
     return codes, gc, flags
 
 
@@ -509,19 +582,25 @@ def nbins_for_bits(code_bits):
 ALLPAIRS_DISTINCT = 1  # plan flag: the caller promises pairwise-distinct codes
 
 
-def hamming_hist_allpairs(codes, code_bits=None, distinct=False):
+def hamming_hist_allpairs(codes, code_bits=None, distinct=False, devices=None):
     """Histogram (uint64[nbins]) of TwoBit distances over all unordered pairs of codes.
     distinct=True promises pairwise-distinct codes (mapping keys): SPECTRAL then skips its
     sort for sum f^2; a broken promise raises ValueError (the host's exact check), never a
-    wrong histogram."""
+    wrong histogram.  devices: the device slots to split over (default: every device of
+    set_devices() once the set reaches the SPECTRAL threshold; one device below it)."""
     codes = np.ascontiguousarray(codes, dtype=np.uint64).reshape(-1)
     if code_bits is None:  # bit_length(max) = bit_length(OR) for non-negative codes
         code_bits = int(codes.max()).bit_length() if codes.size else 1
     code_bits = max(1, code_bits)
     nbins = nbins_for_bits(code_bits)
     hist = np.zeros(nbins, dtype=np.uint64)
-    check(lib().sct_hamming_hist_allpairs_host_ex(_ptr(codes), codes.size, code_bits,
-                                                  ALLPAIRS_DISTINCT if distinct else 0, _ptr(hist), nbins))
+    flags = ALLPAIRS_DISTINCT if distinct else 0
+    devs = _devs(devices, codes.size, _spectral_min_n())
+    if devs:
+        check(lib().sct_hamming_hist_allpairs_host_devices(_ptr(codes), codes.size, code_bits, flags, _dev_array(devs),
+                                                           len(devs), _ptr(hist), nbins))
+    else:
+        check(lib().sct_hamming_hist_allpairs_host_ex(_ptr(codes), codes.size, code_bits, flags, _ptr(hist), nbins))
     return hist
 
 
@@ -711,41 +790,58 @@ def allpairs_geometry(n, code_bits):
     return {"nbins": nb.value, "items": it.value, "rows_per_item": rb.value, "cols_per_item": cb.value}
 
 
-def nearest(kind, whitelist, queries, max_d=1, code_bits=None):
-    """Brute-force-equivalent nearest whitelist entry -> (index int32, dist uint8)."""
+def nearest(kind, whitelist, queries, max_d=1, code_bits=None, devices=None):
+    """Brute-force-equivalent nearest whitelist entry -> (index int32, dist uint8); large query
+    sets split over the devices (contiguous ranges, the whitelist indexed on each)."""
     wl = np.ascontiguousarray(whitelist, dtype=np.uint64).reshape(-1)
     q = np.ascontiguousarray(queries, dtype=np.uint64).reshape(-1)
     if code_bits is None:
         code_bits = max(1, int(np.bitwise_or.reduce(wl)).bit_length() if wl.size else 1)
     index = pinned.empty(q.size, np.int32)
     dist = pinned.empty(q.size, np.uint8)
-    check(lib().sct_nearest_host(kind, _ptr(wl), wl.size, _ptr(q), q.size, code_bits, max_d,
-                                 _ptr(index), _ptr(dist)))
+    devs = _devs(devices, q.size, MULTI_MIN_RECORDS)
+    if devs:
+        check(lib().sct_nearest_host_devices(kind, _ptr(wl), wl.size, _ptr(q), q.size, code_bits, max_d,
+                                             _dev_array(devs), len(devs), _ptr(index), _ptr(dist)))
+    else:
+        check(lib().sct_nearest_host(kind, _ptr(wl), wl.size, _ptr(q), q.size, code_bits, max_d,
+                                     _ptr(index), _ptr(dist)))
     return index, dist
 
 
 class HostNearestPlan:
     """A nearest-whitelist plan built once from a host whitelist, queried with host arrays
-    (sct_nearest_plan_create_host / sct_nearest_query_host): results in page-locked pool arrays."""
+    (sct_nearest_plan_create_host / sct_nearest_query_host): results in page-locked pool arrays.
+    With several devices (``devices``, default set_devices()'s) the index is built on each and
+    every query batch splits over them (sct_nearest_multi_*)."""
 
-    def __init__(self, kind, whitelist, code_bits, max_d):
+    def __init__(self, kind, whitelist, code_bits, max_d, devices=None):
         self._lib = lib()
         self._h = _vp()
         wl = np.ascontiguousarray(whitelist, dtype=np.uint64).reshape(-1)
         self.kind, self.nw, self.max_d = kind, wl.size, max_d
-        check(self._lib.sct_nearest_plan_create_host(kind, _ptr(wl), wl.size, code_bits, max_d, ctypes.byref(self._h)))
+        devs = _devs(devices, 0, 0)
+        self.devices = devs or [None]
+        self._multi = bool(devs)
+        if self._multi:
+            check(self._lib.sct_nearest_multi_create_host(kind, _ptr(wl), wl.size, code_bits, max_d, _dev_array(devs),
+                                                          len(devs), ctypes.byref(self._h)))
+        else:
+            check(self._lib.sct_nearest_plan_create_host(kind, _ptr(wl), wl.size, code_bits, max_d,
+                                                         ctypes.byref(self._h)))
 
     def query(self, queries):
         q = np.ascontiguousarray(queries, dtype=np.uint64).reshape(-1)
         index = pinned.empty(q.size, np.int32)
         dist = pinned.empty(q.size, np.uint8)
         if q.size:
-            check(self._lib.sct_nearest_query_host(self._h, _ptr(q), q.size, _ptr(index), _ptr(dist)))
+            f = self._lib.sct_nearest_multi_query_host if self._multi else self._lib.sct_nearest_query_host
+            check(f(self._h, _ptr(q), q.size, _ptr(index), _ptr(dist)))
         return index, dist
 
     def close(self):
         if self._h:
-            self._lib.sct_nearest_plan_destroy(self._h)
+            (self._lib.sct_nearest_multi_destroy if self._multi else self._lib.sct_nearest_plan_destroy)(self._h)
             self._h = _vp()
 
     def __del__(self):

@@ -141,8 +141,10 @@ class Barcodes:
         """returns descriptive statistics on hamming distances between pairs of barcodes
         (barcode.py:39-46).
 
-        Large sets keep a per-device workspace cached for the next call (up to 4 GiB on the GPU
-        for >= 325K 16-bp codes); ``sctools_amd.release_device_memory()`` hands it back."""
+        From the SPECTRAL threshold (325K 16-bp codes) the count splits over every device of
+        ``sctools_amd.set_devices()`` (default: all visible GPUs).  The call frees all the device
+        memory it mapped before it returns (up to 4 GiB per device); with
+        ``sctools_amd.keep_workspace(True)`` it stays cached for the next call instead."""
         hist = self.hamming_histogram()
         values = _lib.summary_from_hist(hist)  # IndexError for < 2 barcodes, as numpy raises
         return dict(zip(_SUMMARY_KEYS, [np.float64(v) for v in values]))
@@ -270,12 +272,14 @@ class WhitelistCorrector:
     index of the whitelist is built once, here, and every ``nearest(queries)`` call only copies
     its queries in and the results out (no reference counterpart).  The
     whitelist is copied at construction: changing the caller's array afterwards changes nothing.
+    The index is built on every device of ``devices`` (default: ``sctools_amd.set_devices()``'s,
+    every visible GPU) and each batch splits over them.
 
     :return of nearest (np.ndarray[int32], np.ndarray[uint8]): index, distance -- as
         ``nearest_whitelist``
     """
 
-    def __init__(self, whitelist, max_distance=1, encoding='ThreeBit'):
+    def __init__(self, whitelist, max_distance=1, encoding='ThreeBit', devices=None):
         self.kind = {'ThreeBit': 3, 'TwoBit': 2, 3: 3, 2: 2}[encoding]
         self.max_distance = max_distance
         wl = np.ascontiguousarray(np.asarray(whitelist, dtype=np.uint64)).reshape(-1)
@@ -283,7 +287,7 @@ class WhitelistCorrector:
         self._plan = None
         if wl.size:
             bits = max(int(np.bitwise_or.reduce(wl)).bit_length(), self.kind * (max_distance + 1))
-            self._plan = _lib.HostNearestPlan(self.kind, wl, min(64, bits), max_distance)
+            self._plan = _lib.HostNearestPlan(self.kind, wl, min(64, bits), max_distance, devices=devices)
 
     def nearest(self, queries):
         q = np.ascontiguousarray(np.asarray(queries, dtype=np.uint64)).reshape(-1)
@@ -297,7 +301,7 @@ class WhitelistCorrector:
             self._plan = None
 
 
-def nearest_whitelist(queries, whitelist, max_distance=1, encoding='ThreeBit'):
+def nearest_whitelist(queries, whitelist, max_distance=1, encoding='ThreeBit', devices=None):
     """Whitelist error correction (no reference counterpart).
 
     Same result as the brute force over the reference's distance
@@ -314,7 +318,7 @@ def nearest_whitelist(queries, whitelist, max_distance=1, encoding='ThreeBit'):
     if wl.size == 0:
         return np.full(q.size, -1, np.int32), np.full(q.size, 255, np.uint8)
     bits = max(int(np.bitwise_or.reduce(wl)).bit_length(), kind * (max_distance + 1))
-    return _lib.nearest(kind, wl, q, max_d=max_distance, code_bits=min(64, bits))
+    return _lib.nearest(kind, wl, q, max_d=max_distance, code_bits=min(64, bits), devices=devices)
 
 
 class ObservedBarcodeSet(Barcodes):

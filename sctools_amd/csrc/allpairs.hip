@@ -36,6 +36,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include <hipcub/hipcub.hpp>
@@ -913,7 +914,7 @@ extern "C" int sct_allpairs_plan_create_ex(const uint64_t* d_codes, int64_t n, i
 extern "C" int sct_allpairs_plan_create_ex2(const uint64_t* d_codes, int64_t n, int code_bits, int scheme,
                                             int flags, sct_allpairs_plan** plan) {
   SCT_CHECK(plan != nullptr, "plan is NULL");
-  SCT_CHECK((flags & ~SCT_ALLPAIRS_DISTINCT) == 0, "unknown plan flags 0x%x", flags);
+  SCT_CHECK((flags & ~(SCT_ALLPAIRS_DISTINCT | SCT_ALLPAIRS_NO_CACHE)) == 0, "unknown plan flags 0x%x", flags);
   SCT_CHECK(scheme == SCT_ALLPAIRS_AUTO || scheme == SCT_ALLPAIRS_SUBSETS ||
                 scheme == SCT_ALLPAIRS_MOMENTS || scheme == SCT_ALLPAIRS_SPECTRAL,
             "unknown scheme %d", scheme);
@@ -931,7 +932,7 @@ extern "C" int sct_allpairs_plan_create_ex2(const uint64_t* d_codes, int64_t n, 
   if (e != hipSuccess) return cleanup(sct::fail(SCT_E_HIP, "hipGetDevice: %s", hipGetErrorString(e)));
   p->n = n;
   // the device's cached buffers (plan cache, spectral.h) when no other plan holds them
-  p->spec.ws = sct_spectral::ws_acquire();
+  p->spec.ws = (flags & SCT_ALLPAIRS_NO_CACHE) ? nullptr : sct_spectral::ws_acquire();
   // one probe of the codes: their OR (code width) and the densest transform columns (SPECTRAL's
   // seed width), one synchronisation
   unsigned long long probe[3] = {0, 0, 0};
@@ -1326,49 +1327,113 @@ extern "C" int sct_hamming_hist_allpairs_host(const uint64_t* codes, int64_t n, 
   return sct_hamming_hist_allpairs_host_ex(codes, n, code_bits, 0, hist, nbins);
 }
 
+namespace {
+// one device's share of a one-shot all-pairs job (sct_hamming_hist_allpairs_host*): a plan on the
+// current device over the n host codes, built, then moment part `part` of `nparts` and item range
+// items * part / nparts .. items * (part + 1) / nparts counted; the raw counts come back to `counts`
+// (129 words) with the plan's scheme / counts length / bins.  Without the keep-workspace setting
+// (sct_keep_workspace) every device buffer of the call is its own and freed before it returns.
+struct Share {
+  uint64_t counts[129] = {};
+  int scheme = 0, ncounts = 0, nbins = 0;
+};
+std::atomic<int> g_keep_ws{0};
+
+int allpairs_share_host(const uint64_t* codes, int64_t n, int code_bits, int flags, int part, int nparts,
+                        Share* out) {
+  const bool keep = g_keep_ws.load(std::memory_order_relaxed) != 0;
+  // codes and counts: the thread's cached staging buffer when the workspace is kept (no per-call
+  // hipMalloc), else a buffer of the call's own
+  const size_t cbytes = ((size_t)n * 8 + 255) & ~(size_t)255, need = cbytes + 129 * 8;
+  sct::DevBuf own;
+  uint8_t* base = nullptr;
+  if (keep) {
+    sct::HostStage* hs = sct::host_stage();
+    if (!hs) return SCT_E_HIP;
+    if (int rc = sct::stage_reserve(hs, 0, need); rc != SCT_OK) return rc;
+    base = hs->dev;
+  } else {
+    SCT_HIP(own.alloc(need));
+    base = static_cast<uint8_t*>(own.p);
+  }
+  uint64_t* d_codes = reinterpret_cast<uint64_t*>(base);
+  uint64_t* d_counts = reinterpret_cast<uint64_t*>(base + cbytes);
+  if (n) SCT_HIP(hipMemcpyAsync(d_codes, codes, (size_t)n * 8, hipMemcpyHostToDevice, 0));
+  sct_allpairs_plan* plan = nullptr;
+  int rc = sct_allpairs_plan_create_ex2(d_codes, n, code_bits, SCT_ALLPAIRS_AUTO,
+                                        flags | (keep ? 0 : SCT_ALLPAIRS_NO_CACHE), &plan);
+  if (rc != SCT_OK) return rc;
+  struct Guard {
+    sct_allpairs_plan* p;
+    ~Guard() { sct_allpairs_plan_destroy(p); }  // (waits for the plan's work: before `own` is freed)
+  } guard{plan};
+  out->scheme = plan->scheme;
+  out->ncounts = plan->ncounts;
+  out->nbins = plan->nbins;
+  const int64_t b = plan->items * part / nparts, e = plan->items * (part + 1) / nparts;
+  SCT_HIP(hipMemsetAsync(d_counts, 0, (size_t)plan->ncounts * 8, 0));
+  rc = sct_allpairs_build_items(plan, b, e, nullptr);
+  if (rc != SCT_OK) return rc;
+  rc = sct_allpairs_moments(plan, part, nparts, d_counts, nullptr);
+  if (rc != SCT_OK) return rc;
+  rc = sct_allpairs_count(plan, b, e, d_counts, 0, nullptr);
+  if (rc != SCT_OK) return rc;
+  SCT_HIP(hipMemcpy(out->counts, d_counts, (size_t)plan->ncounts * 8, hipMemcpyDeviceToHost));
+  return SCT_OK;
+}
+
+// the shares' counts summed (mod 2^64, as an int64 all-reduce sums them), checked and inverted
+int allpairs_finish(const Share* sh, int nshares, int64_t n, uint64_t* hist, int nbins) {
+  uint64_t counts[129] = {};
+  for (int r = 0; r < nshares; ++r) {
+    if (sh[r].scheme != sh[0].scheme || sh[r].ncounts != sh[0].ncounts || sh[r].nbins != sh[0].nbins)
+      return sct::fail(SCT_E_HIP, "device shares disagree on the plan (scheme %d / %d)", sh[0].scheme, sh[r].scheme);
+    for (int k = 0; k < sh[r].ncounts; ++k) counts[k] += sh[r].counts[k];
+  }
+  if (sh[0].nbins != nbins) return sct::fail(SCT_E_INVALID, "hist holds %d bins, plan needs %d", nbins, sh[0].nbins);
+  // counts[0]: pairs counted (SUBSETS, MOMENTS) or the code count (SPECTRAL)
+  const int64_t expect = sh[0].scheme == SCT_ALLPAIRS_SPECTRAL ? n : n * (n - 1) / 2;
+  if ((int64_t)counts[0] != (n >= 2 ? expect : 0))
+    return sct::fail(SCT_E_HIP, "pair count mismatch: counted %llu, expected %lld", (unsigned long long)counts[0],
+                     (long long)expect);
+  return sct_counts_to_hist_ex(sh[0].scheme, counts, sh[0].ncounts, hist, nbins);
+}
+}  // namespace
+
 extern "C" int sct_hamming_hist_allpairs_host_ex(const uint64_t* codes, int64_t n, int code_bits, int flags,
                                                  uint64_t* hist, int nbins) {
   SCT_CHECK(hist != nullptr, "hist is NULL");
   SCT_CHECK(n >= 0 && (n == 0 || codes != nullptr), "bad codes");
-  // codes and counts through the thread's cached staging buffer (no per-call hipMalloc); the
-  // plan borrows the device's cached workspace, so after the first call nothing is mapped
-  sct::HostStage* hs = sct::host_stage();
-  if (!hs) return SCT_E_HIP;
-  const size_t cbytes = ((size_t)n * 8 + 255) & ~(size_t)255;
-  if (int rc = sct::stage_reserve(hs, 0, cbytes + 129 * 8); rc != SCT_OK) return rc;
-  uint64_t* d_codes = reinterpret_cast<uint64_t*>(hs->dev);
-  uint64_t* d_counts = reinterpret_cast<uint64_t*>(hs->dev + cbytes);
-  if (n) SCT_HIP(hipMemcpyAsync(d_codes, codes, (size_t)n * 8, hipMemcpyHostToDevice, 0));
-  sct_allpairs_plan* plan = nullptr;
-  int rc = sct_allpairs_plan_create_ex2(d_codes, n, code_bits, SCT_ALLPAIRS_AUTO, flags, &plan);
+  SCT_CHECK((flags & ~SCT_ALLPAIRS_DISTINCT) == 0, "unknown flags 0x%x", flags);
+  Share sh;
+  if (int rc = allpairs_share_host(codes, n, code_bits, flags, 0, 1, &sh); rc != SCT_OK) return rc;
+  return allpairs_finish(&sh, 1, n, hist, nbins);
+}
+
+extern "C" int sct_hamming_hist_allpairs_host_devices(const uint64_t* codes, int64_t n, int code_bits, int flags,
+                                                      const int* devices, int ndev, uint64_t* hist, int nbins) {
+  SCT_CHECK(hist != nullptr, "hist is NULL");
+  SCT_CHECK(n >= 0 && (n == 0 || codes != nullptr), "bad codes");
+  SCT_CHECK((flags & ~SCT_ALLPAIRS_DISTINCT) == 0, "unknown flags 0x%x", flags);
+  std::vector<Share> sh((size_t)std::max(ndev, 1));
+  const int rc = sct::run_on_devices(devices, ndev, [&](int r) {
+    return allpairs_share_host(codes, n, code_bits, flags, r, ndev, &sh[(size_t)r]);
+  });
   if (rc != SCT_OK) return rc;
-  struct Guard {
-    sct_allpairs_plan* p;
-    ~Guard() { sct_allpairs_plan_destroy(p); }
-  } guard{plan};
-  if (plan->nbins != nbins)
-    return sct::fail(SCT_E_INVALID, "hist holds %d bins, plan needs %d", nbins, plan->nbins);
-  const int nc = plan->ncounts;
-  SCT_HIP(hipMemsetAsync(d_counts, 0, (size_t)nc * 8, 0));
-  rc = sct_allpairs_build(plan, nullptr);
-  if (rc != SCT_OK) return rc;
-  rc = sct_allpairs_moments(plan, 0, 1, d_counts, nullptr);
-  if (rc != SCT_OK) return rc;
-  rc = sct_allpairs_count(plan, 0, plan->items, d_counts, 0, nullptr);
-  if (rc != SCT_OK) return rc;
-  uint64_t counts[129];
-  SCT_HIP(hipMemcpy(counts, d_counts, (size_t)nc * 8, hipMemcpyDeviceToHost));
-  // counts[0]: pairs counted (SUBSETS, MOMENTS) or the code count (SPECTRAL)
-  const int64_t expect = plan->scheme == SCT_ALLPAIRS_SPECTRAL ? n : n * (n - 1) / 2;
-  if ((int64_t)counts[0] != (n >= 2 ? expect : 0))
-    return sct::fail(SCT_E_HIP, "pair count mismatch: counted %llu, expected %lld",
-                     (unsigned long long)counts[0], (long long)expect);
-  return sct_counts_to_hist_ex(plan->scheme, counts, nc, hist, nbins);
+  return allpairs_finish(sh.data(), ndev, n, hist, nbins);
+}
+
+extern "C" int sct_keep_workspace(int keep, int* previous) {
+  const int was = g_keep_ws.load();
+  if (previous) *previous = was;
+  if (keep >= 0) g_keep_ws.store(keep ? 1 : 0);
+  return SCT_OK;
 }
 
 extern "C" int sct_allpairs_cache_release(void) {
   sct_spectral::ws_release_all();
   (void)hipDeviceSynchronize();  // (the stream-ordered frees have completed)
   sct::pool_trim();
+  sct::stage_release_device();
   return SCT_OK;
 }

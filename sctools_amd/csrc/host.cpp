@@ -44,6 +44,17 @@ HostStage* host_stage() {
   return stages[dev];
 }
 
+void stage_release_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  HostStage* st = host_stage();
+  if (!st || !st->dev) return;
+  (void)hipStreamSynchronize(st->stream);
+  (void)hipFree(st->dev);
+  st->dev = nullptr;
+  st->dev_cap = 0;
+}
+
 bool host_range_pinned(const void* p, size_t bytes) {
   if (!p || !bytes) return false;
   hipPointerAttribute_t a{};

@@ -6,6 +6,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <functional>
 #include <vector>
 
 #include "../../include/sctools_hip.h"
@@ -63,6 +64,9 @@ HostStage* host_stage();
 // arrays are copied through the stage's own pinned buffer instead.
 bool host_range_pinned(const void* p, size_t bytes);
 int stage_reserve(HostStage* st, size_t pinned_bytes, size_t dev_bytes);
+// the calling thread's stage on the current device gives its device buffer back (the next call
+// that needs one maps it again)
+void stage_release_device();
 // Calls of at most this many bytes (inputs + outputs) run zero-copy on the pinned buffer.
 constexpr size_t kZeroCopyBytes = 64 << 10;
 // Larger calls up to this size go through the pinned + device buffers (two copies); beyond
@@ -75,6 +79,13 @@ hipError_t pool_alloc(void** p, size_t bytes, hipStream_t s);
 // every pool's idle memory back to the device (sct_allpairs_cache_release)
 void pool_trim();
 void pool_free(void* p, hipStream_t s);
+
+// Several devices from one process (devices.cpp): fn(r) for every slot r in [0, ndev) on a
+// persistent worker thread of its own (slot r is always the same thread, so its thread-local host
+// stages and pipeline streams are reused from call to call) with devices[r] its current device;
+// devices == NULL or ndev <= 1 runs fn(0) on the calling thread and its current device.
+// Returns the first failing slot's status with its message.  One such call at a time per process.
+int run_on_devices(const int* devices, int ndev, const std::function<int(int)>& fn);
 
 // sct_tune_set value of `key`, or dflt when unset (host.cpp).
 int64_t tune(int key, int64_t dflt);
