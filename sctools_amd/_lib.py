@@ -535,10 +535,12 @@ def whitelist_encode(data, kind=2):
     return codes, starts, lens, flags
 
 
+# Element-wise batch outputs come from the page-locked pool (large calls then DMA their results
+# in place: the library streams them in chunks, include/sctools_hip.h); every element is written.
 def decode2(codes, L):
     codes = np.ascontiguousarray(codes, dtype=np.uint64)
     codes2 = codes.reshape(codes.shape[0], -1)
-    out = np.zeros((codes2.shape[0], L), dtype=np.uint8)
+    out = pinned.empty((codes2.shape[0], L), np.uint8)
     check(lib().sct_decode2_host(_ptr(codes2), codes2.shape[0], codes2.shape[1], L, _ptr(out)))
     return out
 
@@ -548,9 +550,9 @@ def decode3(codes):
     codes2 = codes.reshape(codes.shape[0], -1)
     n, words = codes2.shape
     maxlen = (64 * words + 2) // 3
-    out = np.zeros((n, maxlen), dtype=np.uint8)
-    lengths = np.zeros(n, dtype=np.int32)
-    bad = np.zeros(n, dtype=np.int32)
+    out = pinned.empty((n, maxlen), np.uint8)  # (row r's bytes before its right-aligned sequence: unset)
+    lengths = pinned.empty(n, np.int32)
+    bad = pinned.empty(n, np.int32)
     check(lib().sct_decode3_host(_ptr(codes2), n, words, maxlen, _ptr(out), _ptr(lengths), _ptr(bad)))
     return out, lengths, bad
 
@@ -558,7 +560,7 @@ def decode3(codes):
 def gc_content(kind, codes, L=0):
     codes = np.ascontiguousarray(codes, dtype=np.uint64)
     codes2 = codes.reshape(codes.shape[0], -1)
-    out = np.zeros(codes2.shape[0], dtype=np.int32)
+    out = pinned.empty(codes2.shape[0], np.int32)
     check(lib().sct_gc_content_host(kind, _ptr(codes2), codes2.shape[0], codes2.shape[1], L, _ptr(out)))
     return out
 
@@ -570,7 +572,7 @@ def hamming_pairs(kind, a, b):
     b2 = b.reshape(b.shape[0], -1)
     if a2.shape != b2.shape:
         raise ValueError("operand shapes differ: %s vs %s" % (a2.shape, b2.shape))
-    out = np.zeros(a2.shape[0], dtype=np.int32)
+    out = pinned.empty(a2.shape[0], np.int32)
     check(lib().sct_hamming_pairs_host(kind, _ptr(a2), _ptr(b2), a2.shape[0], a2.shape[1], _ptr(out)))
     return out
 

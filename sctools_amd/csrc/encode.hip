@@ -1211,6 +1211,120 @@ int host_call(const In (&ins)[NI], const Out (&outs)[NO], bool zero_copy, F&& la
   SCT_HIP(hipStreamSynchronize(st->stream));
   return SCT_OK;
 }
+// Large element-wise calls (the *_array forms on host arrays): n items, item r of input k at
+// ins[k].p + r * ins[k].bytes (bytes = PER ITEM here), likewise the outputs.  Chunks of items flow
+// through NSTAGE device blocks on the thread's NSTAGE pipeline streams, so one chunk's H2D copy,
+// another's kernel and a third's D2H copy overlap: the call runs at the PCIe rate of its larger
+// direction.  Page-locked caller arrays (sct_host_pinned: the pool arrays the drop-in returns, torch
+// pin_memory) are copied by DMA in place; pageable ones through the thread's pinned stage, filled
+// and emptied by par_memcpy while the other stages' copies run.  launch(ptrs, m, stream) runs the
+// kernel on m items at the device pointers.
+constexpr size_t kStreamMinBytes = (size_t)8 << 20;  // below: one staged round trip (host_call)
+
+template <int NI, int NO, class F>
+int host_items(int64_t n, const In (&ins)[NI], const Out (&outs)[NO], F&& launch) {
+  constexpr int NSTAGE = 3;
+  size_t per = 0;
+  for (int k = 0; k < NI; ++k) per += ins[k].bytes;
+  for (int k = 0; k < NO; ++k) per += outs[k].p ? outs[k].bytes : 0;
+  bool pin_in[NI > 0 ? NI : 1], pin_out[NO > 0 ? NO : 1];
+  size_t stage_item = 0;  // pinned stage bytes per item (pageable arrays only)
+  for (int k = 0; k < NI; ++k) {
+    pin_in[k] = sct::host_range_pinned(ins[k].p, (size_t)n * ins[k].bytes);
+    if (!pin_in[k]) stage_item += ins[k].bytes;
+  }
+  for (int k = 0; k < NO; ++k) {
+    pin_out[k] = !outs[k].p || sct::host_range_pinned(outs[k].p, (size_t)n * outs[k].bytes);
+    if (!pin_out[k]) stage_item += outs[k].bytes;
+  }
+  // ~16 MB of traffic per chunk, at least four chunks when there are enough items
+  int64_t chunk = std::max<int64_t>(1 << 16, (int64_t)(((size_t)16 << 20) / std::max<size_t>(per, 1)));
+  chunk = std::min<int64_t>(chunk, std::max<int64_t>(1 << 16, sct::ceil_div(n, 4)));
+  chunk = std::min<int64_t>(chunk, n);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t doff[NI + NO], dtot = 0, hoff[NI + NO], htot = 0;
+  for (int k = 0; k < NI + NO; ++k) {
+    const size_t b = k < NI ? ins[k].bytes : (outs[k - NI].p ? outs[k - NI].bytes : 0);
+    doff[k] = dtot;
+    dtot += al((size_t)chunk * b);
+    const bool staged = k < NI ? !pin_in[k] : !pin_out[k - NI];
+    hoff[k] = htot;
+    if (staged) htot += al((size_t)chunk * b);
+  }
+  sct::HostStage* hs = sct::host_stage();
+  if (!hs) return SCT_E_HIP;
+  if (htot) SCT_TRY(sct::stage_reserve(hs, NSTAGE * htot, 0));
+  hipStream_t st[NSTAGE] = {};
+  for (int k = 0; k < NSTAGE; ++k) {
+    if (!hs->pipe[k]) SCT_HIP(hipStreamCreateWithFlags(&hs->pipe[k], hipStreamNonBlocking));
+    st[k] = hs->pipe[k];
+  }
+  struct Streams {
+    hipStream_t* s;
+    ~Streams() {
+      for (int k = 0; k < NSTAGE; ++k)
+        if (s[k]) (void)hipStreamSynchronize(s[k]);
+    }
+  } guard{st};
+  struct Blocks {
+    void* p[NSTAGE] = {};
+    hipStream_t* s;
+    ~Blocks() {
+      for (int k = 0; k < NSTAGE; ++k) sct::pool_free(p[k], s[k]);
+    }
+  } blk{{}, st};
+  for (int k = 0; k < NSTAGE; ++k) SCT_HIP(sct::pool_alloc(&blk.p[k], dtot, st[k]));
+  auto hstage = [&](int k, int a) { return hs->pinned + (size_t)k * htot + hoff[a]; };
+  int64_t pend_r0[NSTAGE] = {}, pend_m[NSTAGE] = {};
+  auto drain = [&](int k) -> int {
+    if (pend_m[k] == 0) return SCT_OK;
+    SCT_HIP(hipStreamSynchronize(st[k]));
+    for (int o = 0; o < NO; ++o)
+      if (outs[o].p && !pin_out[o])
+        sct::par_memcpy(static_cast<uint8_t*>(outs[o].p) + (size_t)pend_r0[k] * outs[o].bytes, hstage(k, NI + o),
+                        (size_t)pend_m[k] * outs[o].bytes);
+    pend_m[k] = 0;
+    return SCT_OK;
+  };
+  int64_t c = 0;
+  for (int64_t r0 = 0; r0 < n; r0 += chunk, ++c) {
+    const int k = (int)(c % NSTAGE);
+    const int64_t m = std::min<int64_t>(chunk, n - r0);
+    SCT_TRY(drain(k));  // (stage k's buffers are about to be reused)
+    void* ptr[NI + NO];
+    uint8_t* dev = static_cast<uint8_t*>(blk.p[k]);
+    for (int a = 0; a < NI; ++a) {
+      const uint8_t* src = static_cast<const uint8_t*>(ins[a].p) + (size_t)r0 * ins[a].bytes;
+      const size_t b = (size_t)m * ins[a].bytes;
+      if (!pin_in[a]) {
+        sct::par_memcpy(hstage(k, a), src, b);
+        src = hstage(k, a);
+      }
+      SCT_HIP(hipMemcpyAsync(dev + doff[a], src, b, hipMemcpyHostToDevice, st[k]));
+      ptr[a] = dev + doff[a];
+    }
+    for (int o = 0; o < NO; ++o) ptr[NI + o] = outs[o].p ? dev + doff[NI + o] : nullptr;
+    SCT_TRY(launch(ptr, m, st[k]));
+    for (int o = 0; o < NO; ++o) {
+      if (!outs[o].p) continue;
+      uint8_t* dst = pin_out[o] ? static_cast<uint8_t*>(outs[o].p) + (size_t)r0 * outs[o].bytes : hstage(k, NI + o);
+      SCT_HIP(hipMemcpyAsync(dst, dev + doff[NI + o], (size_t)m * outs[o].bytes, hipMemcpyDeviceToHost, st[k]));
+    }
+    pend_r0[k] = r0;
+    pend_m[k] = m;
+  }
+  for (int k = 0; k < NSTAGE; ++k) SCT_TRY(drain(k));
+  return SCT_OK;
+}
+
+// total bytes of an element-wise call
+template <int NI, int NO>
+size_t items_bytes(int64_t n, const In (&ins)[NI], const Out (&outs)[NO]) {
+  size_t per = 0;
+  for (int k = 0; k < NI; ++k) per += ins[k].bytes;
+  for (int k = 0; k < NO; ++k) per += outs[k].p ? outs[k].bytes : 0;
+  return (size_t)n * per;
+}
 }  // namespace
 
 extern "C" int sct_encode_host(int kind, const uint8_t* seqs, int64_t n, int64_t stride, int L,
@@ -1358,6 +1472,12 @@ extern "C" int sct_decode2_host(const uint64_t* codes, int64_t n, int words, int
     const int rc = srv_call<1, 1>(OP_DECODE2, 2, n, words, L, 0, 0, {{codes, (size_t)n * words * 8}}, {{out, (size_t)n * L}});
     if (rc != 1) return rc;
   }
+  const In ii[1] = {{codes, (size_t)words * 8}};
+  const Out oo[1] = {{out, (size_t)L}};
+  if (codes && out && items_bytes(n, ii, oo) >= kStreamMinBytes)
+    return host_items(n, ii, oo, [&](void** p, int64_t m, hipStream_t s) {
+      return sct_decode2((const uint64_t*)p[0], m, words, L, (uint8_t*)p[1], s);
+    });
   return host_call<1, 1>({{codes, (size_t)n * words * 8}}, {{out, (size_t)n * L}}, true,
                          [&](void** p, hipStream_t s) {
                            return sct_decode2((const uint64_t*)p[0], n, words, L, (uint8_t*)p[1], s);
@@ -1373,6 +1493,12 @@ extern "C" int sct_decode3_host(const uint64_t* codes, int64_t n, int words, int
                                   {{out, (size_t)n * maxlen}, {lengths, (size_t)n * 4}, {bad, (size_t)n * 4}});
     if (rc != 1) return rc;
   }
+  const In ii[1] = {{codes, (size_t)words * 8}};
+  const Out oo[3] = {{out, (size_t)maxlen}, {lengths, 4}, {bad, 4}};
+  if (codes && out && lengths && bad && items_bytes(n, ii, oo) >= kStreamMinBytes)
+    return host_items(n, ii, oo, [&](void** p, int64_t m, hipStream_t s) {
+      return sct_decode3((const uint64_t*)p[0], m, words, maxlen, (uint8_t*)p[1], (int32_t*)p[2], (int32_t*)p[3], s);
+    });
   return host_call<1, 3>({{codes, (size_t)n * words * 8}},
                          {{out, (size_t)n * maxlen}, {lengths, (size_t)n * 4}, {bad, (size_t)n * 4}}, true,
                          [&](void** p, hipStream_t s) {
@@ -1389,6 +1515,12 @@ extern "C" int sct_gc_content_host(int kind, const uint64_t* codes, int64_t n, i
     const int rc = srv_call<1, 1>(OP_GC, kind, n, words, L, 0, 0, {{codes, (size_t)n * words * 8}}, {{out, (size_t)n * 4}});
     if (rc != 1) return rc;
   }
+  const In ii[1] = {{codes, (size_t)words * 8}};
+  const Out oo[1] = {{out, 4}};
+  if (codes && out && items_bytes(n, ii, oo) >= kStreamMinBytes)
+    return host_items(n, ii, oo, [&](void** p, int64_t m, hipStream_t s) {
+      return sct_gc_content(kind, (const uint64_t*)p[0], m, words, L, (int32_t*)p[1], s);
+    });
   return host_call<1, 1>({{codes, (size_t)n * words * 8}}, {{out, (size_t)n * 4}}, true,
                          [&](void** p, hipStream_t s) {
                            return sct_gc_content(kind, (const uint64_t*)p[0], n, words, L, (int32_t*)p[1], s);
@@ -1404,6 +1536,12 @@ extern "C" int sct_hamming_pairs_host(int kind, const uint64_t* a, const uint64_
                                   {{a, (size_t)n * words * 8}, {b, (size_t)n * words * 8}}, {{out, (size_t)n * 4}});
     if (rc != 1) return rc;
   }
+  const In ii[2] = {{a, (size_t)words * 8}, {b, (size_t)words * 8}};
+  const Out oo[1] = {{out, 4}};
+  if (a && b && out && items_bytes(n, ii, oo) >= kStreamMinBytes)
+    return host_items(n, ii, oo, [&](void** p, int64_t m, hipStream_t s) {
+      return sct_hamming_pairs(kind, (const uint64_t*)p[0], (const uint64_t*)p[1], m, words, (int32_t*)p[2], s);
+    });
   return host_call<2, 1>({{a, (size_t)n * words * 8}, {b, (size_t)n * words * 8}}, {{out, (size_t)n * 4}}, true,
                          [&](void** p, hipStream_t s) {
                            return sct_hamming_pairs(kind, (const uint64_t*)p[0], (const uint64_t*)p[1], n, words,

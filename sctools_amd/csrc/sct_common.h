@@ -64,6 +64,9 @@ HostStage* host_stage();
 // arrays are copied through the stage's own pinned buffer instead.
 bool host_range_pinned(const void* p, size_t bytes);
 int stage_reserve(HostStage* st, size_t pinned_bytes, size_t dev_bytes);
+// memcpy split over the library's copy helper threads for large pageable <-> page-locked copies
+// (host.cpp); small copies, or one while another thread's is running, stay on the calling thread
+void par_memcpy(void* dst, const void* src, size_t bytes);
 // the calling thread's stage on the current device gives its device buffer back (the next call
 // that needs one maps it again)
 void stage_release_device();

@@ -761,10 +761,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     for (int q2 = 0; q2 < 4; ++q2)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+#ifdef SCT_TILE_SQ_ABL
+        // timing-only ablation (wrong results): the squares replaced by one full-rate XOR, the floor
+        // of any exact F^2 accumulate (ab_tile_squares_r06)
+        acc[digit_weight_c((uint32_t)qa) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] ^=
+            (uint32_t)ca[q2][i];
+        acc2[digit_weight_c((uint32_t)qb) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] ^=
+            (uint32_t)cb[q2][i];
+#else
         acc[digit_weight_c((uint32_t)qa) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
             (unsigned long long)((int64_t)ca[q2][i] * ca[q2][i]);
         acc2[digit_weight_c((uint32_t)qb) + digit_weight_c((uint32_t)q2) + digit_weight_c((uint32_t)i)] +=
             (unsigned long long)((int64_t)cb[q2][i] * cb[q2][i]);
+#endif
       }
   };
   // int16 pairs (v + 128 of stage 1, |.| < 2^15) -> the high / low byte operands

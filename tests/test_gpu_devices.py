@@ -183,3 +183,35 @@ def test_plan_destroy_waits_for_enqueued_work():
     samp = np.random.default_rng(8).integers(0, q.numel(), 5000)
     ridx, rdist = O.c_nearest(3, wl, q.cpu().numpy().view(np.uint64)[samp], 1)
     assert np.array_equal(idx.cpu().numpy()[samp], ridx) and np.array_equal(dist.cpu().numpy()[samp], rdist)
+
+
+@pytest.mark.parametrize("pinned_inputs", [True, False])
+def test_batch_arrays_streamed(pinned_inputs):
+    """Element-wise batch calls above the stream threshold (8 MB) run chunked over the pipeline
+    streams (host_items): hamming_distance_array (both kinds), decode_array, gc_content_array on
+    3,000,017 items from page-locked or pageable inputs equal the same calls made in small pieces
+    (one staged round trip each) and the numpy formulas on a sample."""
+    rng = np.random.default_rng(17 + pinned_inputs)
+    n = 3_000_017
+    a = rng.integers(0, 1 << 32, n, dtype=np.uint64)
+    b = a ^ (rng.integers(0, 1 << 32, n, dtype=np.uint64) & np.uint64(0x00F0000F))
+    if pinned_inputs:
+        pa, pb = _lib.pinned.empty(n, np.uint64), _lib.pinned.empty(n, np.uint64)
+        pa[:], pb[:] = a, b
+        assert _lib.host_pinned(pa) and _lib.host_pinned(pb)
+        a, b = pa, pb
+    T2, T3, t16 = encodings.TwoBit, encodings.ThreeBit, encodings.TwoBit(16)
+    full = [T2.hamming_distance_array(a, b), T3.hamming_distance_array(a, b), t16.decode_array(a),
+            t16.gc_content_array(a)]
+    step = 200_000  # pieces of 2.4-4.8 MB: below the threshold
+    pieces = [np.concatenate([f(a[i:i + step], b[i:i + step]) for i in range(0, n, step)])
+              for f in (T2.hamming_distance_array, T3.hamming_distance_array, lambda x, y: t16.decode_array(x),
+                        lambda x, y: t16.gc_content_array(x))]
+    for f, p in zip(full, pieces):
+        assert np.array_equal(f, p)
+    s = rng.integers(0, n, 20_000)
+    x = a[s] ^ b[s]
+    w2 = [bin(int(v)).count("1") for v in (x | (x >> np.uint64(1))) & np.uint64(0x5555555555555555)]
+    assert full[0][s].tolist() == w2
+    assert full[3][s].tolist() == [bin(int(v) & 0x55555555).count("1") for v in a[s]]
+    assert [bytes(v) for v in full[2][s[:500]]] == [O.two_bit_decode(int(v), 16) for v in a[s[:500]]]

@@ -30,6 +30,8 @@ for name in names:
         out[name] = bench._guarded(bench.path_pipeline, dev, 5, copy, threads)
     elif name == "config5_encode":
         out[name] = bench._guarded(bench.path_config5_encode, dev, 3, copy)
+    elif name == "host_arrays":
+        out[name] = bench._guarded(bench.path_host_arrays, dev, bench.pcie_ceiling_gbs(dev))
     elif name == "config5_allpairs":
         out[name] = bench._guarded(bench.path_config5_allpairs, dev, 5, copy)
     print(json.dumps({name: out.get(name)}), file=sys.stderr, flush=True)
