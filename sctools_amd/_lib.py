@@ -429,6 +429,7 @@ class PinnedPool:
         self._held = 0  # page-locked bytes: blocks behind live arrays + idle blocks
         self._mu = threading.Lock()
         self._pending = collections.deque()  # blocks handed back, not yet filed under _mu
+        self._order = collections.deque()  # idle (size class, pointer) in the order they went idle
         self._ok = True
         self._types = {}
 
@@ -453,6 +454,7 @@ class PinnedPool:
             ptr = blocks.pop() if blocks else None
             if ptr is not None:
                 self._idle -= c
+                self._order.remove((c, ptr))
         if ptr is None:
             with self._mu:
                 if self._held + c > self.max_bytes:
@@ -487,12 +489,21 @@ class PinnedPool:
         try:
             while self._pending:
                 ptr, c = self._pending.popleft()
-                if self._idle + c <= self.keep_bytes:
-                    self._free.setdefault(c, []).append(ptr)
-                    self._idle += c
-                else:
+                if c > self.keep_bytes:
                     self._held -= c
                     to_free.append(ptr)
+                    continue
+                # the block just handed back stays; the longest-idle ones make room for it (a
+                # stream of equal calls then reuses its blocks instead of page-locking anew)
+                while self._idle + c > self.keep_bytes:
+                    oc, op = self._order.popleft()
+                    self._free[oc].remove(op)
+                    self._idle -= oc
+                    self._held -= oc
+                    to_free.append(op)
+                self._free.setdefault(c, []).append(ptr)
+                self._order.append((c, ptr))
+                self._idle += c
         finally:
             self._mu.release()
         for p in to_free:
@@ -506,6 +517,7 @@ class PinnedPool:
         with self._mu:
             ptrs = [p for blocks in self._free.values() for p in blocks]
             self._free.clear()
+            self._order.clear()
             self._held -= self._idle
             self._idle = 0
         self._drain()  # (blocks handed back while the lock was held go idle, then stay for reuse)

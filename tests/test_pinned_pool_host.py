@@ -46,3 +46,31 @@ def test_trim_files_pending_blocks_first():
     finally:
         _lib.lib = real
     assert freed == [0x3000] and pool._held == 0 and pool._idle == 0 and not pool._pending
+
+
+def test_idle_blocks_make_room_for_the_latest():
+    """A block handed back stays idle when it fits keep_bytes on its own; the longest-idle blocks are
+    freed to make room for it (so a repeated large call reuses its block instead of page-locking a
+    new one), and a block larger than keep_bytes is freed at once."""
+    MB = _lib.PinnedPool.MIN_BYTES
+    pool = _lib.PinnedPool(keep_bytes=4 * MB, max_bytes=1 << 30)
+    pool._held = 1 * MB + 2 * MB + 4 * MB + 8 * MB
+    freed = []
+
+    class FakeLib:
+        def sct_host_free(self, p):
+            freed.append(p.value)
+
+    real = _lib.lib
+    _lib.lib = lambda: FakeLib()
+    try:
+        pool._release(0x10, MB)
+        pool._release(0x20, 2 * MB)
+        assert pool._idle == 3 * MB and not freed
+        pool._release(0x40, 4 * MB)  # both older blocks go
+        assert sorted(freed) == [0x10, 0x20] and pool._idle == 4 * MB and pool._free[4 * MB] == [0x40]
+        pool._release(0x80, 8 * MB)  # larger than keep_bytes: freed, the idle one stays
+        assert freed[-1] == 0x80 and pool._free[4 * MB] == [0x40]
+        assert pool._held == 4 * MB and list(pool._order) == [(4 * MB, 0x40)]
+    finally:
+        _lib.lib = real
