@@ -932,7 +932,16 @@ extern "C" int sct_allpairs_plan_create_ex2(const uint64_t* d_codes, int64_t n, 
   if (e != hipSuccess) return cleanup(sct::fail(SCT_E_HIP, "hipGetDevice: %s", hipGetErrorString(e)));
   p->n = n;
   // the device's cached buffers (plan cache, spectral.h) when no other plan holds them
-  p->spec.ws = (flags & SCT_ALLPAIRS_NO_CACHE) ? nullptr : sct_spectral::ws_acquire();
+  if (flags & SCT_ALLPAIRS_NO_CACHE) {
+    // the plan's own buffers, carved from one block: the codes, the probe's scratch and (for a
+    // set AUTO sends to SPECTRAL) the transform's buffers with its 4 GiB intermediate
+    size_t est = ((size_t)n * 8 + 255) + ((size_t)36 << 20);
+    if (n >= 2 && n >= sct::tune(SCT_TUNE_SPECTRAL_MIN_N, 325000))
+      est += (size_t)n * 4 + ((size_t)n / 32 + 65536) * 80 + ((size_t)4 << 30) + ((size_t)16 << 20);
+    p->spec.ws = sct_spectral::ws_arena(est);
+  } else {
+    p->spec.ws = sct_spectral::ws_acquire();
+  }
   // one probe of the codes: their OR (code width) and the densest transform columns (SPECTRAL's
   // seed width), one synchronisation
   unsigned long long probe[3] = {0, 0, 0};

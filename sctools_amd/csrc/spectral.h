@@ -117,8 +117,11 @@ enum WsSlot {
 struct Workspace;
 // the current device's workspace, lent to the caller, or nullptr when it is lent out already
 Workspace* ws_acquire();
-// give it back (its buffers stay allocated unless a release was asked for meanwhile)
+// give it back (its buffers stay allocated unless a release was asked for meanwhile; a private
+// arena is freed)
 void ws_release(Workspace* ws);
+// a private arena of one `bytes` block for one plan (never shared; freed by ws_release)
+Workspace* ws_arena(size_t bytes);
 // slot `slot` of at least `bytes` (grow-only); ws == nullptr: a plain hipMalloc
 int ws_get(Workspace* ws, int slot, size_t bytes, void** p);
 // free p unless it came from a workspace

@@ -1055,6 +1055,13 @@ struct Workspace {
   bool order_ready = false;
   void* p[W_NSLOTS] = {};
   size_t cap[W_NSLOTS] = {};
+  // a plan's private arena (SCT_ALLPAIRS_NO_CACHE): one block, the slots carved from it in turn,
+  // freed whole when the plan goes -- one hipMalloc / hipFree per call instead of one per slot
+  // (a hipFree costs ~110 us, profiles/dropin_hip_api_r06.csv); slots that do not fit get their own
+  bool arena = false;
+  uint8_t* base = nullptr;
+  size_t size = 0, used = 0;
+  std::vector<void*> extra;
 };
 
 namespace {
@@ -1062,11 +1069,29 @@ std::mutex g_ws_mu;
 Workspace* g_ws[64] = {};
 
 void ws_free(Workspace* ws) {
-  for (int k = 0; k < W_NSLOTS; ++k)
-    if (ws->p[k]) (void)hipFree(ws->p[k]);
+  if (ws->arena) {
+    if (ws->base) (void)hipFree(ws->base);
+    for (void* q : ws->extra) (void)hipFree(q);
+  } else {
+    for (int k = 0; k < W_NSLOTS; ++k)
+      if (ws->p[k]) (void)hipFree(ws->p[k]);
+  }
   delete ws;
 }
 }  // namespace
+
+Workspace* ws_arena(size_t bytes) {
+  auto* ws = new Workspace();
+  ws->arena = true;
+  ws->busy = true;
+  if (hipGetDevice(&ws->device) != hipSuccess || hipMalloc((void**)&ws->base, bytes) != hipSuccess) {
+    (void)hipGetLastError();  // (no block: every slot its own allocation, as without an arena)
+    ws->base = nullptr;
+    bytes = 0;
+  }
+  ws->size = bytes;
+  return ws;
+}
 
 Workspace* ws_acquire() {
   if (sct::tune(SCT_TUNE_PLAN_CACHE, 1) == 0) return nullptr;
@@ -1086,6 +1111,10 @@ Workspace* ws_acquire() {
 
 void ws_release(Workspace* ws) {
   if (!ws) return;
+  if (ws->arena) {
+    ws_free(ws);
+    return;
+  }
   std::lock_guard<std::mutex> lk(g_ws_mu);
   ws->busy = false;
   if (ws->release) {
@@ -1098,6 +1127,24 @@ int ws_get(Workspace* ws, int slot, size_t bytes, void** p) {
   bytes = std::max<size_t>(bytes, 256);
   if (!ws) {
     SCT_HIP(hipMalloc(p, bytes));
+    return SCT_OK;
+  }
+  if (ws->arena) {
+    if (ws->cap[slot] < bytes) {
+      const size_t at = (ws->used + 255) & ~(size_t)255;
+      if (ws->base && at + bytes <= ws->size) {
+        ws->p[slot] = ws->base + at;
+        ws->used = at + bytes;
+      } else {
+        void* q = nullptr;
+        SCT_HIP(hipMalloc(&q, bytes));
+        ws->extra.push_back(q);
+        ws->p[slot] = q;
+      }
+      ws->cap[slot] = bytes;
+      if (slot == W_ORDER) ws->order_ready = false;
+    }
+    *p = ws->p[slot];
     return SCT_OK;
   }
   if (ws->cap[slot] < bytes) {  // grow (rare: a larger set than any before on this device)
