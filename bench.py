@@ -55,8 +55,8 @@ HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E (MI355X_MICROARCH.md)
 SIMDS = 256 * 4
 ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-bit code word
 METRIC = "Hamming pair-comparisons/sec, 737K 10x whitelist all-pairs, 1-8 GPUs"
-PROFILE_ROUND = "r05"  # the committed rocprof / PMC summaries the line cites (profiles/)
-PROFILE_FALLBACK = ("r04",)  # a kernel not re-profiled this round cites its latest summary
+PROFILE_ROUND = "r06"  # the committed rocprof / PMC summaries the line cites (profiles/)
+PROFILE_FALLBACK = ("r05", "r04")  # a kernel not re-profiled this round cites its latest summary
 
 
 def parse(argv=None):
