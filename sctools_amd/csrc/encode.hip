@@ -831,9 +831,12 @@ __global__ __launch_bounds__(64) void scalar_server_kernel(SrvMailbox* mb, uint3
       const int in_words = ((int)(h4 & 0xFFFFu) + 3) / 4, out_words = ((int)(h4 >> 16) + 3) / 4;
       const int io[2] = {off16(h5 & 0xFFFFu), off16(h5 >> 16)};
       const int oo[3] = {off16(h6 & 0xFFFFu), off16(h6 >> 16), off16(h7 & 0xFFFFu)};
-      // payload: the first 7 dwords came with the line; the rest (if any) in one more round trip
+      // payload: the first 7 dwords came with the line; the rest (if any) in one more round trip.
+      // No acquire fence: the rest is read with system-scope loads (they bypass the caches) issued
+      // only after this wave saw the sequence number the host stored after the payload, so they
+      // return the new bytes; a system-scope acquire here was a whole-L2 invalidate
+      // (buffer_inv sc0 sc1) on every request (round 6)
       if (lane >= 8 && lane < 15 && lane - 8 < in_words) in_l[lane - 8] = line;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       for (int k = kSrvInline / 4 + lane; k < in_words; k += 64) in_l[k] = sys_load(&mb->more[k - kSrvInline / 4]);
       for (int k = lane; k < out_words; k += 64) out_l[k] = 0u;
       __syncthreads();
@@ -1030,7 +1033,10 @@ template <int NI, int NO>
 int srv_call(uint32_t op, int kind, int64_t n, int words, int L, int64_t stride, int maxlen, const SrvIn (&ins)[NI],
              const SrvOut (&outs)[NO]) {
   if (!server_enabled() || n > kSrvMaxN || stride > kSrvIn || L > kSrvOut || maxlen > kSrvOut || words > 255) return 1;
-  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  // 8-byte aligned pieces (the widest element is a uint64 code): a pair of one-limb codes is 16 B
+  // and rides in the request line; 16-byte alignment made it 32 B, past the 28 inline bytes, and
+  // cost every hamming_distance call a second PCIe round trip for the rest (round 6)
+  auto al = [](size_t x) { return (x + 7) & ~(size_t)7; };
   int32_t io[2] = {-1, -1}, oo[3] = {-1, -1, -1};
   size_t tin = 0, tout = 0;
   for (int k = 0; k < NI; ++k) {
