@@ -15,6 +15,8 @@ import weakref
 
 import numpy as np
 
+from . import _scalar
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SCTOOLS_HIP_LIB") or os.path.join(_HERE, "libsctools_hip.so")
 
@@ -178,6 +180,10 @@ def lib():
                 fn = getattr(handle, name)
                 fn.argtypes = args
                 fn.restype = _RESTYPES.get(name, _i32)
+            # the scalar methods' CPython entry points call these directly (csrc/pyscalar.c)
+            _scalar.bind(*(ctypes.cast(getattr(handle, name), ctypes.c_void_p).value
+                           for name in ("sct_hamming_pairs_host", "sct_gc_content_host", "sct_decode2_host",
+                                        "sct_encode_host")))
             _lib = handle
     return _lib
 

@@ -252,7 +252,9 @@ __device__ __forceinline__ void decode2_record(const uint64_t* w, int words, int
   for (int p = 0; p < L; ++p) {
     const int64_t pos = 2LL * (L - 1 - p);
     const uint32_t v = pos < 64LL * words ? group_at(w, words, pos, 2) : 0u;
-    o[p] = (uint8_t)("ACTG"[v]);
+    // "ACTG"[v] from a register (the string literal was a global load per base: ~2 us of a
+    // 16-base scalar decode)
+    o[p] = (uint8_t)(0x47544341u >> (8 * v));
   }
 }
 
@@ -752,17 +754,27 @@ enum : uint32_t { OP_ENCODE = 1, OP_DECODE2 = 2, OP_DECODE3 = 3, OP_GC = 4, OP_H
 constexpr int kSrvIn = 1024, kSrvOut = 1024, kSrvMaxN = 64;
 
 constexpr int kSrvInline = 28;  // payload bytes that ride in the request line itself
+#ifndef SCT_SRV_COPIES
+#define SCT_SRV_COPIES 4  // copies of the request line, one poll in flight on each
+#endif
+constexpr int kSrvCopies = SCT_SRV_COPIES;
+static_assert(kSrvCopies >= 1 && kSrvCopies <= 8, "copies of the request line");
 
 // One request line of 64 B: req[0] = seq (written last), req[1..7] = the packed fields,
 // req[8..14] = the first 28 payload bytes, req[15] = line_check(req[0..14]); payload bytes
-// 28.. follow in `more`.  The wave reads the whole line with one 64-B load
-// per poll, so a scalar call (payload <= 28 B: a pair of one-limb codes, a 28-base record)
-// costs one PCIe read.  Nothing guarantees that the 16 dwords of one poll are one snapshot,
-// so the wave takes a new sequence number only with a matching check word: a line mixing
-// this request's seq with the previous request's fields is not accepted, only polled again.
+// 28.. follow in `more`.  The host writes the line kSrvCopies times (req, req_copy[..]) and the
+// wave keeps one 64-B load in flight on each copy, so a scalar call (payload <= 28 B: a pair of
+// one-limb codes, a 28-base record) is seen a fraction of a PCIe round trip after it lands
+// (two loads in flight on the SAME line were slower than one: tools/scalar_floor_probe.hip).
+// Nothing guarantees that the 16 dwords of one poll are one
+// snapshot, so the wave takes a sequence number only when it is newer than the last served
+// one (a copy not yet rewritten still shows the previous request) and the check word matches:
+// a line mixing this request's seq with the previous request's fields is only polled again.
 struct SrvMailbox {
   alignas(64) uint32_t req[16];
   uint32_t more[(kSrvIn - kSrvInline) / 4];
+  // the other copies of the request line (dwords 0..15 of each row), 256 B apart
+  alignas(256) uint32_t req_copy[kSrvCopies > 1 ? kSrvCopies - 1 : 1][64];
   // control (host)
   alignas(64) uint32_t stop;
   // response line (device), written by one 16-lane store: resp[0] = the served seq,
@@ -777,13 +789,33 @@ struct SrvMailbox {
 };
 constexpr int kSrvInlineOut = 52;
 
-__host__ __device__ inline uint32_t line_check(const uint32_t* w) {
-  uint32_t h = 0x9E3779B9u;
-  for (int k = 0; k < 15; ++k) {
-    h = (h ^ w[k]) * 0x01000193u;
-    h ^= h >> 15;
-  }
+// The check word of a 64-B line: the XOR of a hash of each of its first 15 dwords and their
+// positions -- on the device one hash per lane and a 4-step XOR across the lanes of a DPP row,
+// where a chained hash cost 15 dependent readlanes and multiplies on the request path (twice:
+// request and response)
+__host__ __device__ inline uint32_t word_mix(uint32_t w, uint32_t k) {
+  uint32_t h = w ^ (0x9E3779B9u * (k + 1u));
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  h *= 0x846CA68Bu;
+  h ^= h >> 16;
   return h;
+}
+inline uint32_t line_check(const uint32_t* w) {
+  uint32_t h = 0;
+  for (uint32_t k = 0; k < 15; ++k) h ^= word_mix(w[k], k);
+  return h;
+}
+// every lane: line_check of the 16-lane row holding it (lane r of the row holds dword r)
+__device__ __forceinline__ uint32_t line_check_row(uint32_t v, int lane) {
+  const int r = lane & 15;
+  int h = (int)(r < 15 ? word_mix(v, (uint32_t)r) : 0u);
+  h ^= __builtin_amdgcn_update_dpp(0, h, 0x128, 0xF, 0xF, false);  // row_ror:8
+  h ^= __builtin_amdgcn_update_dpp(0, h, 0x124, 0xF, 0xF, false);  // row_ror:4
+  h ^= __builtin_amdgcn_update_dpp(0, h, 0x122, 0xF, 0xF, false);  // row_ror:2
+  h ^= __builtin_amdgcn_update_dpp(0, h, 0x121, 0xF, 0xF, false);  // row_ror:1
+  return (uint32_t)h;
 }
 static_assert(offsetof(SrvMailbox, more) == 64, "the payload continues after the request line");
 
@@ -804,103 +836,124 @@ __global__ __launch_bounds__(64) void scalar_server_kernel(SrvMailbox* mb, uint3
     lut[1][c] = lut_entry(3, c);
   }
   __syncthreads();
+  // One poll in flight on each copy of the request line, and the wall clock read only every 32nd
+  // round of polls (the idle exit).  Round-6 A/B of the library's C call (one TwoBit pair,
+  // tools/scalar_floor_probe.hip, profiles/scalar_floor_r06/): two loads in flight on the same
+  // line 4.81-4.84 us, one poll at a time 3.47-3.49 (the clock read on every poll +0.02-0.03),
+  // one poll on each of two copies and the lane-parallel check word 2.09-2.22, on each of four
+  // 1.98.  A polled mailbox answers in steps of its polls, so the time also depends on the host's
+  // own time between calls: averaged over 0-2 us of it, 2.23-2.25 us with four copies, 2.5 with
+  // two, 4.2 before round 6.  Sleeping a calibrated quarter round trip after each reload (to
+  // spread the four polls evenly) made it worse: 2.81-3.04.
   uint64_t t_last = wall_clock64();
-  // two polls in flight: the next line's load is issued before this one is examined, so a
-  // request is seen about half a PCIe round trip sooner than with one poll at a time
-  uint32_t line = lane < 16 ? sys_load(&mb->req[lane]) : 0u;
-  for (uint32_t it = 1;; ++it) {
-    const uint32_t ahead = lane < 16 ? sys_load(&mb->req[lane]) : 0u;
+  bool served_since = false;  // t_last is refreshed at the next clock read, off the request path
+  // Serves the request `line` holds (lane r of each row holds dword r; a new seq, check word
+  // matched).
+  auto serve = [&](const uint32_t line) {
     const uint32_t seq = __builtin_amdgcn_readlane(line, 0);
-    bool arrived = seq != served;
-    if (arrived) {
-      uint32_t w[15];
-#pragma unroll
-      for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_readlane(line, k);
-      arrived = line_check(w) == __builtin_amdgcn_readlane(line, 15);
-    }
-    if (arrived) {
-      const uint32_t h1 = __builtin_amdgcn_readlane(line, 1), h2 = __builtin_amdgcn_readlane(line, 2),
-                     h3 = __builtin_amdgcn_readlane(line, 3), h4 = __builtin_amdgcn_readlane(line, 4),
-                     h5 = __builtin_amdgcn_readlane(line, 5), h6 = __builtin_amdgcn_readlane(line, 6),
-                     h7 = __builtin_amdgcn_readlane(line, 7);
-      auto off16 = [](uint32_t v) { return v == 0xFFFFu ? -1 : (int)v; };
-      const uint32_t op = h1 & 0xFFu;
-      const int kind = (int)((h1 >> 8) & 0xFFu), words = (int)(h1 >> 16);
-      const int n = (int)(h2 & 0xFFFFu), L = (int)(h2 >> 16);
-      const int stride = (int)(h3 & 0xFFFFu), maxlen = (int)(h3 >> 16);
-      const int in_words = ((int)(h4 & 0xFFFFu) + 3) / 4, out_words = ((int)(h4 >> 16) + 3) / 4;
-      const int io[2] = {off16(h5 & 0xFFFFu), off16(h5 >> 16)};
-      const int oo[3] = {off16(h6 & 0xFFFFu), off16(h6 >> 16), off16(h7 & 0xFFFFu)};
-      // payload: the first 7 dwords came with the line; the rest (if any) in one more round trip.
-      // No acquire fence: the rest is read with system-scope loads (they bypass the caches) issued
-      // only after this wave saw the sequence number the host stored after the payload, so they
-      // return the new bytes; a system-scope acquire here was a whole-L2 invalidate
-      // (buffer_inv sc0 sc1) on every request (round 6)
-      if (lane >= 8 && lane < 15 && lane - 8 < in_words) in_l[lane - 8] = line;
-      for (int k = kSrvInline / 4 + lane; k < in_words; k += 64) in_l[k] = sys_load(&mb->more[k - kSrvInline / 4]);
-      for (int k = lane; k < out_words; k += 64) out_l[k] = 0u;
-      __syncthreads();
-      const uint8_t* in8 = reinterpret_cast<const uint8_t*>(in_l);
-      uint8_t* out8 = reinterpret_cast<uint8_t*>(out_l);
-      const int r = lane;
-      if (r < n) {
-        switch (op) {
-          case OP_ENCODE: {
-            RecordReader rd{in8 + io[0] + r * stride, false, 0u, -1};
-            uint32_t g, fl;
-            encode_record(lut[kind == 2 ? 0 : 1], kind, rd, L, words,
-                          reinterpret_cast<uint64_t*>(out8 + oo[0]) + r * words, g, fl);
-            if (oo[1] >= 0) out8[oo[1] + r] = (uint8_t)(g > 255 ? 255 : g);
-            if (oo[2] >= 0) out8[oo[2] + r] = (uint8_t)fl;
-            break;
-          }
-          case OP_DECODE2:
-            decode2_record(reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words, words, L, out8 + oo[0] + r * L);
-            break;
-          case OP_DECODE3: {
-            int32_t err;
-            const int32_t len = decode3_record(reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words, words, maxlen,
-                                               out8 + oo[0] + r * maxlen, err);
-            reinterpret_cast<int32_t*>(out8 + oo[1])[r] = len;
-            reinterpret_cast<int32_t*>(out8 + oo[2])[r] = err;
-            break;
-          }
-          case OP_GC:
-            reinterpret_cast<int32_t*>(out8 + oo[0])[r] =
-                gc_record(kind, reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words, words, L);
-            break;
-          case OP_HAMMING:
-            reinterpret_cast<int32_t*>(out8 + oo[0])[r] =
-                hamming_record(kind, reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words,
-                               reinterpret_cast<const uint64_t*>(in8 + io[1]) + r * words, words);
-            break;
-          default:
-            break;
+    const uint32_t h1 = __builtin_amdgcn_readlane(line, 1), h2 = __builtin_amdgcn_readlane(line, 2),
+                   h3 = __builtin_amdgcn_readlane(line, 3), h4 = __builtin_amdgcn_readlane(line, 4),
+                   h5 = __builtin_amdgcn_readlane(line, 5), h6 = __builtin_amdgcn_readlane(line, 6),
+                   h7 = __builtin_amdgcn_readlane(line, 7);
+    auto off16 = [](uint32_t v) { return v == 0xFFFFu ? -1 : (int)v; };
+    const uint32_t op = h1 & 0xFFu;
+    const int kind = (int)((h1 >> 8) & 0xFFu), words = (int)(h1 >> 16);
+    const int n = (int)(h2 & 0xFFFFu), L = (int)(h2 >> 16);
+    const int stride = (int)(h3 & 0xFFFFu), maxlen = (int)(h3 >> 16);
+    const int in_words = ((int)(h4 & 0xFFFFu) + 3) / 4, out_words = ((int)(h4 >> 16) + 3) / 4;
+    const int io[2] = {off16(h5 & 0xFFFFu), off16(h5 >> 16)};
+    const int oo[3] = {off16(h6 & 0xFFFFu), off16(h6 >> 16), off16(h7 & 0xFFFFu)};
+    // payload: the first 7 dwords came with the line; the rest (if any) in one more round trip.
+    // No acquire fence: the rest is read with system-scope loads (they bypass the caches) issued
+    // only after this wave saw the sequence number the host stored after the payload, so they
+    // return the new bytes; a system-scope acquire here was a whole-L2 invalidate
+    // (buffer_inv sc0 sc1) on every request (round 6)
+    if (lane >= 8 && lane < 15 && lane - 8 < in_words) in_l[lane - 8] = line;
+    for (int k = kSrvInline / 4 + lane; k < in_words; k += 64) in_l[k] = sys_load(&mb->more[k - kSrvInline / 4]);
+    for (int k = lane; k < out_words; k += 64) out_l[k] = 0u;
+    __syncthreads();
+    const uint8_t* in8 = reinterpret_cast<const uint8_t*>(in_l);
+    uint8_t* out8 = reinterpret_cast<uint8_t*>(out_l);
+    const int r = lane;
+    if (r < n) {
+      switch (op) {
+        case OP_ENCODE: {
+          RecordReader rd{in8 + io[0] + r * stride, false, 0u, -1};
+          uint32_t g, fl;
+          encode_record(lut[kind == 2 ? 0 : 1], kind, rd, L, words,
+                        reinterpret_cast<uint64_t*>(out8 + oo[0]) + r * words, g, fl);
+          if (oo[1] >= 0) out8[oo[1] + r] = (uint8_t)(g > 255 ? 255 : g);
+          if (oo[2] >= 0) out8[oo[2] + r] = (uint8_t)fl;
+          break;
         }
+        case OP_DECODE2:
+          decode2_record(reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words, words, L, out8 + oo[0] + r * L);
+          break;
+        case OP_DECODE3: {
+          int32_t err;
+          const int32_t len = decode3_record(reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words, words, maxlen,
+                                             out8 + oo[0] + r * maxlen, err);
+          reinterpret_cast<int32_t*>(out8 + oo[1])[r] = len;
+          reinterpret_cast<int32_t*>(out8 + oo[2])[r] = err;
+          break;
+        }
+        case OP_GC:
+          reinterpret_cast<int32_t*>(out8 + oo[0])[r] =
+              gc_record(kind, reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words, words, L);
+          break;
+        case OP_HAMMING:
+          reinterpret_cast<int32_t*>(out8 + oo[0])[r] =
+              hamming_record(kind, reinterpret_cast<const uint64_t*>(in8 + io[0]) + r * words,
+                             reinterpret_cast<const uint64_t*>(in8 + io[1]) + r * words, words);
+          break;
+        default:
+          break;
       }
-      __syncthreads();
-      const bool inline_out = out_words * 4 <= kSrvInlineOut;
-      if (!inline_out) {
-        for (int k = lane; k < out_words; k += 64)
-          __hip_atomic_store(&mb->out[k], out_l[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      }
-      const uint32_t status = op >= OP_ENCODE && op <= OP_HAMMING ? 0u : 1u;
-      uint32_t v = lane == 0 ? seq : lane == 1 ? status : (lane < 15 && inline_out && lane - 2 < out_words) ? out_l[lane - 2] : 0u;
-      uint32_t w[15];
-#pragma unroll
-      for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_readlane(v, k);
-      if (lane == 15) v = line_check(w);
-      if (lane < 16) __hip_atomic_store(&mb->resp[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      served = seq;
-      t_last = wall_clock64();
-      line = ahead;
-      continue;
     }
-    // the stop word costs a round trip of its own: looked at every 256th poll (~0.2 ms)
-    if ((it & 255) == 0 && sys_load(&mb->stop) != 0u) break;
-    if (wall_clock64() - t_last > idle_ticks) break;
-    line = ahead;
+    __syncthreads();
+    const bool inline_out = out_words * 4 <= kSrvInlineOut;
+    if (!inline_out) {
+      for (int k = lane; k < out_words; k += 64)
+        __hip_atomic_store(&mb->out[k], out_l[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    }
+    const uint32_t status = op >= OP_ENCODE && op <= OP_HAMMING ? 0u : 1u;
+    uint32_t v = lane == 0 ? seq : lane == 1 ? status : (lane < 15 && inline_out && lane - 2 < out_words) ? out_l[lane - 2] : 0u;
+    const uint32_t check = line_check_row(v, lane);
+    if (lane == 15) v = check;
+    if (lane < 16) __hip_atomic_store(&mb->resp[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    served = seq;
+    served_since = true;
+  };
+  // Every lane loads dword (lane & 15), so no lane branch surrounds the loads, and a copy's next
+  // load is issued only after its line was examined (into the same register): the wait for the
+  // oldest poll is then vmcnt(kSrvCopies - 1) and the other copies' loads stay in flight.  (An
+  // array of copies in a loop over j was compiled with a full drain every round: the registers
+  // rotated.)
+  auto line_at = [&](int j) { return j == 0 ? mb->req + (lane & 15) : mb->req_copy[j - 1] + (lane & 15); };
+  auto step = [&](uint32_t& v, int j) {
+    if ((int32_t)(__builtin_amdgcn_readlane(v, 0) - served) > 0 &&
+        __builtin_amdgcn_readlane(line_check_row(v, lane), 0) == __builtin_amdgcn_readlane(v, 15))
+      serve(v);
+    v = sys_load(line_at(j));
+  };
+  static_assert(kSrvCopies == 2 || kSrvCopies == 4, "2 or 4 copies of the request line");
+  uint32_t v0 = sys_load(line_at(0)), v1 = sys_load(line_at(1));
+  uint32_t v2 = kSrvCopies > 2 ? sys_load(line_at(2)) : 0u, v3 = kSrvCopies > 2 ? sys_load(line_at(3)) : 0u;
+  for (uint32_t it = 1;; ++it) {
+    step(v0, 0);
+    step(v1, 1);
+    if constexpr (kSrvCopies > 2) {
+      step(v2, 2);
+      step(v3, 3);
+    }
+    // the stop word costs a round trip of its own: looked at every 128th round of polls (~0.2 ms)
+    if ((it & 127) == 0 && sys_load(&mb->stop) != 0u) break;
+    if ((it & 31) == 0) {
+      const uint64_t now = wall_clock64();
+      if (served_since) t_last = now, served_since = false;
+      else if (now - t_last > idle_ticks) break;
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if (lane == 0) __hip_atomic_store(&mb->exit_gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1052,29 +1105,30 @@ int srv_call(uint32_t op, int kind, int64_t n, int words, int L, int64_t stride,
   Server* sv = server();
   if (!sv) return 1;
   SrvMailbox* mb = sv->mb;
+  uint32_t req[16] = {};  // the request line, written to both copies; seq last in each
   {  // payload bytes [0, 28) into req[8..14], the rest into `more`
     uint8_t pay[kSrvIn];
     for (int k = 0; k < NI; ++k)
       if (ins[k].bytes) memcpy(pay + io[k], ins[k].p, ins[k].bytes);
-    memcpy(&mb->req[8], pay, std::min<size_t>(tin, kSrvInline));
+    memcpy(&req[8], pay, std::min<size_t>(tin, kSrvInline));
     if (tin > (size_t)kSrvInline) memcpy(mb->more, pay + kSrvInline, tin - kSrvInline);
   }
   auto o16 = [](int32_t v) { return v < 0 ? 0xFFFFu : (uint32_t)v; };
-  mb->req[1] = op | (uint32_t)kind << 8 | (uint32_t)words << 16;
-  mb->req[2] = (uint32_t)n | (uint32_t)L << 16;
-  mb->req[3] = (uint32_t)stride | (uint32_t)maxlen << 16;
-  mb->req[4] = (uint32_t)tin | (uint32_t)tout << 16;
-  mb->req[5] = o16(io[0]) | o16(io[1]) << 16;
-  mb->req[6] = o16(oo[0]) | o16(oo[1]) << 16;
-  mb->req[7] = o16(oo[2]);
+  req[1] = op | (uint32_t)kind << 8 | (uint32_t)words << 16;
+  req[2] = (uint32_t)n | (uint32_t)L << 16;
+  req[3] = (uint32_t)stride | (uint32_t)maxlen << 16;
+  req[4] = (uint32_t)tin | (uint32_t)tout << 16;
+  req[5] = o16(io[0]) | o16(io[1]) << 16;
+  req[6] = o16(oo[0]) | o16(oo[1]) << 16;
+  req[7] = o16(oo[2]);
   const uint32_t seq = ++sv->seq;
-  {
-    uint32_t w[15];
-    w[0] = seq;
-    for (int k = 1; k < 15; ++k) w[k] = mb->req[k];
-    mb->req[15] = line_check(w);
+  req[0] = seq;
+  req[15] = line_check(req);
+  for (int j = 0; j < kSrvCopies; ++j) {
+    uint32_t* line = j == 0 ? mb->req : mb->req_copy[j - 1];
+    memcpy(line + 1, req + 1, 15 * 4);
+    __atomic_store_n(&line[0], seq, __ATOMIC_RELEASE);
   }
-  __atomic_store_n(&mb->req[0], seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
   uint32_t line[16];
   auto answered = [&]() {  // the whole response line of this request, check included

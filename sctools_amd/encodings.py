@@ -18,7 +18,7 @@ import random
 
 import numpy as np
 
-from . import _lib
+from . import _lib, _scalar
 
 __all__ = ["Encoding", "TwoBit", "ThreeBit"]
 
@@ -271,6 +271,9 @@ class TwoBit(Encoding):
     @classmethod
     def encode(cls, bytes_encoded):
         """encodings.py:75-88 (batch of one)."""
+        code = _scalar.encode(2, bytes_encoded)  # a bytes record of one limb, no ambiguous base
+        if code is not NotImplemented:
+            return code
         if isinstance(bytes_encoded, str):
             if not bytes_encoded:
                 return 0
@@ -288,6 +291,9 @@ class TwoBit(Encoding):
 
     def decode(self, integer_encoded):
         """encodings.py:90-100 (batch of one); a negative int reads mod 4**L there."""
+        out = _scalar.decode2(integer_encoded, self.sequence_length)  # an int in [0, 2^64), 1 <= L <= 64
+        if out is not NotImplemented:
+            return out
         x = operator.index(integer_encoded)
         L = self.sequence_length
         if L <= 0:  # range(L) is empty
@@ -300,6 +306,9 @@ class TwoBit(Encoding):
 
     def gc_content(self, integer_encoded):
         """encodings.py:102-111 (batch of one); a negative int reads mod 4**L there."""
+        gc = _scalar.gc(2, integer_encoded, self.sequence_length)  # an int in [0, 2^64), L >= 1
+        if gc is not NotImplemented:
+            return gc
         x = operator.index(integer_encoded)
         L = self.sequence_length
         if L <= 0:
@@ -313,7 +322,8 @@ class TwoBit(Encoding):
     @staticmethod
     def hamming_distance(a, b):
         """encodings.py:113-121 (batch of one)."""
-        return _hamming1(2, a, b)
+        d = _scalar.hamming(2, a, b)  # two ints in [0, 2^64)
+        return _hamming1(2, a, b) if d is NotImplemented else d
 
 
 class ThreeBit(Encoding):
@@ -379,6 +389,9 @@ class ThreeBit(Encoding):
     @classmethod
     def encode(cls, bytes_encoded):
         """encodings.py:155-167 (batch of one)."""
+        code = _scalar.encode(3, bytes_encoded)  # a bytes record of one limb
+        if code is not NotImplemented:
+            return code
         if isinstance(bytes_encoded, str):
             # iterating a str yields str characters: none is in the byte map -> all N (6)
             seq = b"N" * len(bytes_encoded)
@@ -398,6 +411,9 @@ class ThreeBit(Encoding):
     @classmethod
     def gc_content(cls, integer_encoded):
         """encodings.py:182-192 (batch of one)."""
+        gc = _scalar.gc(3, integer_encoded, 0)  # an int in [0, 2^64)
+        if gc is not NotImplemented:
+            return gc
         x = operator.index(integer_encoded)
         if x < 0:
             raise ValueError(_HANG_GC3)
@@ -408,7 +424,8 @@ class ThreeBit(Encoding):
     @staticmethod
     def hamming_distance(a, b):
         """encodings.py:194-202 (batch of one)."""
-        return _hamming1(3, a, b)
+        d = _scalar.hamming(3, a, b)  # two ints in [0, 2^64)
+        return _hamming1(3, a, b) if d is NotImplemented else d
 
 
 def _pad(limbs, words):

@@ -141,3 +141,33 @@ def test_one_server_per_thread():
         t.join(timeout=60)
     assert not errors
     assert not any(t.is_alive() for t in ts)
+
+
+def test_cpython_entry_points_take_the_common_case():
+    """The scalar methods' C entry points (csrc/pyscalar.c) answer ints in [0, 2^64) and one-limb
+    bytes records themselves, equal to the ctypes path, and leave every other case (negative or
+    multi-limb ints, numpy scalars, str, ambiguous bases, L = 0 or > 64) to the Python path."""
+    from sctools_amd import _scalar
+    _lib.lib()  # binds the entry points
+    rng = random.Random(17)
+    for kind in (2, 3):
+        for _ in range(200):
+            a, b = rng.getrandbits(64), rng.getrandbits(rng.choice((1, 20, 63, 64)))
+            assert _scalar.hamming(kind, a, b) == _lib.hamming1(kind, a, b)
+            assert _scalar.gc(kind, a, 32 if kind == 2 else 0) == _lib.gc1(kind, a, 32 if kind == 2 else 0)
+        for L in (1, 7, 16, 21):
+            s = bytes(rng.choice(b"ACGT") for _ in range(L))
+            assert _scalar.encode(kind, s) == _lib.encode1(kind, s)[0]
+    for L in (1, 16, 33, 64):
+        x = rng.getrandbits(2 * L) & ((1 << 64) - 1)
+        assert _scalar.decode2(x, L) == _lib.decode2_1(x, L)
+    assert _scalar.hamming(2, True, False) == 1
+    for args in ((2, -1, 3), (2, 1 << 64, 3), (2, np.uint64(3), 1), (2, 1.0, 1)):
+        assert _scalar.hamming(*args) is NotImplemented
+    assert _scalar.gc(2, 5, 0) is NotImplemented and _scalar.gc(2, -5, 8) is NotImplemented
+    assert _scalar.decode2(5, 0) is NotImplemented and _scalar.decode2(5, 65) is NotImplemented
+    assert _scalar.encode(2, b"ACNT") is NotImplemented  # ambiguous: drawn in order by the Python path
+    assert _scalar.encode(3, b"ACNT") == _lib.encode1(3, b"ACNT")[0]  # ThreeBit keeps N
+    for seq in ("ACGT", bytearray(b"ACGT"), b"", b"A" * 33):
+        assert _scalar.encode(2, seq) is NotImplemented
+    assert _scalar.encode(3, b"A" * 22) is NotImplemented
