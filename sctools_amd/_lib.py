@@ -183,7 +183,7 @@ def lib():
             # the scalar methods' CPython entry points call these directly (csrc/pyscalar.c)
             _scalar.bind(*(ctypes.cast(getattr(handle, name), ctypes.c_void_p).value
                            for name in ("sct_hamming_pairs_host", "sct_gc_content_host", "sct_decode2_host",
-                                        "sct_encode_host")))
+                                        "sct_encode_host", "sct_decode3_host")))
             _lib = handle
     return _lib
 

@@ -248,13 +248,24 @@ __device__ __forceinline__ uint32_t group_at(const uint64_t* w, int words, int64
   return (uint32_t)(v & ((1u << width) - 1u));
 }
 
-__device__ __forceinline__ void decode2_record(const uint64_t* w, int words, int L, uint8_t* o) {
+__device__ __forceinline__ void decode2_limbs(const uint64_t* w, int words, int L, uint8_t* o) {
   for (int p = 0; p < L; ++p) {
     const int64_t pos = 2LL * (L - 1 - p);
     const uint32_t v = pos < 64LL * words ? group_at(w, words, pos, 2) : 0u;
     // "ACTG"[v] from a register (the string literal was a global load per base: ~2 us of a
     // 16-base scalar decode)
     o[p] = (uint8_t)(0x47544341u >> (8 * v));
+  }
+}
+
+// A one-limb code is read once into a register: the byte stores to o may alias w, so the
+// compiler reloaded it for every base (16 dependent LDS reads of a scalar-server decode)
+__device__ __forceinline__ void decode2_record(const uint64_t* w, int words, int L, uint8_t* o) {
+  if (words == 1) {
+    const uint64_t c = w[0];
+    decode2_limbs(&c, 1, L, o);
+  } else {
+    decode2_limbs(w, words, L, o);
   }
 }
 
@@ -266,8 +277,8 @@ __global__ __launch_bounds__(WG) void decode2_kernel(const uint64_t* __restrict_
 
 // o[maxlen - 1 - t] = base of triplet t for t <= the top non-zero triplet; returns that
 // count, and in err the first invalid triplet value (0 / 5 / 7) or -1
-__device__ __forceinline__ int32_t decode3_record(const uint64_t* w, int words, int maxlen, uint8_t* o,
-                                                  int32_t& err) {
+__device__ __forceinline__ int32_t decode3_limbs(const uint64_t* w, int words, int maxlen, uint8_t* o,
+                                                 int32_t& err) {
   const int ntrip = (64 * words + 2) / 3;
   int top = -1;
   for (int t = ntrip - 1; t >= 0; --t)
@@ -292,6 +303,15 @@ __device__ __forceinline__ int32_t decode3_record(const uint64_t* w, int words, 
     o[maxlen - 1 - t] = ch;
   }
   return top + 1;
+}
+
+__device__ __forceinline__ int32_t decode3_record(const uint64_t* w, int words, int maxlen, uint8_t* o,
+                                                  int32_t& err) {
+  if (words == 1) {
+    const uint64_t c = w[0];
+    return decode3_limbs(&c, 1, maxlen, o, err);
+  }
+  return decode3_limbs(w, words, maxlen, o, err);
 }
 
 __global__ __launch_bounds__(WG) void decode3_kernel(const uint64_t* __restrict__ codes, int64_t n,
@@ -843,8 +863,8 @@ __global__ __launch_bounds__(64) void scalar_server_kernel(SrvMailbox* mb, uint3
   // one poll on each of two copies and the lane-parallel check word 2.09-2.22, on each of four
   // 1.98.  A polled mailbox answers in steps of its polls, so the time also depends on the host's
   // own time between calls: averaged over 0-2 us of it, 2.23-2.25 us with four copies, 2.5 with
-  // two, 4.2 before round 6.  Sleeping a calibrated quarter round trip after each reload (to
-  // spread the four polls evenly) made it worse: 2.81-3.04.
+  // two, 4.2 before round 6 (the polls bunched, see below).  Sleeping a calibrated quarter round
+  // trip after every reload made it worse: 2.81-3.04.
   uint64_t t_last = wall_clock64();
   bool served_since = false;  // t_last is refreshed at the next clock read, off the request path
   // Serves the request `line` holds (lane r of each row holds dword r; a new seq, check word
@@ -931,15 +951,49 @@ __global__ __launch_bounds__(64) void scalar_server_kernel(SrvMailbox* mb, uint3
   // array of copies in a loop over j was compiled with a full drain every round: the registers
   // rotated.)
   auto line_at = [&](int j) { return j == 0 ? mb->req + (lane & 15) : mb->req_copy[j - 1] + (lane & 15); };
+  // The copies' polls are spread over a round trip: after the first poll and after every request
+  // (when the polls in flight all came back while it was served) the next kSrvCopies - 1 polls are
+  // issued a round trip / kSrvCopies apart (the round trip timed once here on the 100-MHz wall
+  // clock); in between, each copy is reissued as soon as it was examined, which keeps the spacing.
+  // Issued back to back instead, the polls stay bunched and a request waits for the next burst:
+  // a saw-tooth of 2.0-2.9 us per C call over the host's own time between calls.
+  uint64_t delta = 0, t_issue = 0;  // wall-clock ticks between spaced polls; the last one's issue
+  int stagger = 0;                  // polls left to space
+#ifndef SCT_SRV_NO_STAGGER
+  {
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t t0 = wall_clock64();
+    const uint32_t x = sys_load(line_at(0));
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t t1 = wall_clock64() + (__builtin_amdgcn_readlane(x, 0) & 0u);
+    delta = min<uint64_t>((t1 - t0) / kSrvCopies, 100);
+  }
+#endif
+  auto reload = [&](int j) {
+    if (stagger > 0) {
+      t_issue += delta;
+      while (wall_clock64() < t_issue) {
+      }
+      --stagger;
+    }
+    return sys_load(line_at(j));
+  };
+  // (one load site per copy: with a second one on the request path the compiler gave the copies
+  // new registers and moved them back at the end of every round, a full drain of the polls)
   auto step = [&](uint32_t& v, int j) {
     if ((int32_t)(__builtin_amdgcn_readlane(v, 0) - served) > 0 &&
-        __builtin_amdgcn_readlane(line_check_row(v, lane), 0) == __builtin_amdgcn_readlane(v, 15))
+        __builtin_amdgcn_readlane(line_check_row(v, lane), 0) == __builtin_amdgcn_readlane(v, 15)) {
       serve(v);
-    v = sys_load(line_at(j));
+      t_issue = wall_clock64() - delta;  // this copy's poll goes out at once, the next ones spaced
+      stagger = kSrvCopies;
+    }
+    v = reload(j);
   };
   static_assert(kSrvCopies == 2 || kSrvCopies == 4, "2 or 4 copies of the request line");
-  uint32_t v0 = sys_load(line_at(0)), v1 = sys_load(line_at(1));
-  uint32_t v2 = kSrvCopies > 2 ? sys_load(line_at(2)) : 0u, v3 = kSrvCopies > 2 ? sys_load(line_at(3)) : 0u;
+  t_issue = wall_clock64() - delta;
+  stagger = kSrvCopies;
+  uint32_t v0 = reload(0), v1 = reload(1);
+  uint32_t v2 = kSrvCopies > 2 ? reload(2) : 0u, v3 = kSrvCopies > 2 ? reload(3) : 0u;
   for (uint32_t it = 1;; ++it) {
     step(v0, 0);
     step(v1, 1);

@@ -23,11 +23,13 @@ typedef int (*hamming_fn)(int, const uint64_t*, const uint64_t*, int64_t, int, i
 typedef int (*gc_fn)(int, const uint64_t*, int64_t, int, int, int32_t*);
 typedef int (*decode2_fn)(const uint64_t*, int64_t, int, int, uint8_t*);
 typedef int (*encode_fn)(int, const uint8_t*, int64_t, int64_t, int, uint64_t*, uint8_t*, uint8_t*);
+typedef int (*decode3_fn)(const uint64_t*, int64_t, int, int, uint8_t*, int32_t*, int32_t*);
 
 static hamming_fn g_hamming;
 static gc_fn g_gc;
 static decode2_fn g_decode2;
 static encode_fn g_encode;
+static decode3_fn g_decode3;
 
 static PyObject* not_impl(void) { Py_RETURN_NOTIMPLEMENTED; }
 
@@ -56,12 +58,13 @@ static int as_int(PyObject* o, int* v) {
 }
 
 static PyObject* bind(PyObject* self, PyObject* args) {
-  unsigned long long h, g, d, e;
-  if (!PyArg_ParseTuple(args, "KKKK", &h, &g, &d, &e)) return NULL;
+  unsigned long long h, g, d, e, d3;
+  if (!PyArg_ParseTuple(args, "KKKKK", &h, &g, &d, &e, &d3)) return NULL;
   g_hamming = (hamming_fn)(uintptr_t)h;
   g_gc = (gc_fn)(uintptr_t)g;
   g_decode2 = (decode2_fn)(uintptr_t)d;
   g_encode = (encode_fn)(uintptr_t)e;
+  g_decode3 = (decode3_fn)(uintptr_t)d3;
   Py_RETURN_NONE;
 }
 
@@ -110,6 +113,22 @@ static PyObject* decode2(PyObject* self, PyObject* const* args, Py_ssize_t n) {
   return PyBytes_FromStringAndSize((const char*)out, L);
 }
 
+/* decode3(code) -> bytes: ThreeBit.decode of a one-limb code (encodings.py:169-180); NotImplemented
+ * when a triplet has no base (the Python path raises the reference's KeyError) */
+static PyObject* decode3(PyObject* self, PyObject* const* args, Py_ssize_t n) {
+  uint64_t x;
+  if (n != 1 || !g_decode3 || !as_u64(args[0], &x)) return not_impl();
+  enum { kMax = 22 }; /* ceil(64 / 3) triplets */
+  uint8_t out[kMax];
+  int32_t len = 0, bad = -1;
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = g_decode3(&x, 1, 1, kMax, out, &len, &bad);
+  Py_END_ALLOW_THREADS
+  if (rc != 0 || bad >= 0 || len < 0 || len > kMax) return not_impl();
+  return PyBytes_FromStringAndSize((const char*)out + (kMax - len), len);
+}
+
 /* encode(kind, seq) -> int: TwoBit / ThreeBit .encode of a bytes record of one limb (1..32 / 1..21
  * bytes; encodings.py:75-88 / 155-167); NotImplemented when a TwoBit record has an ambiguous or
  * invalid base (the Python path draws the random bases in order or raises the KeyError) */
@@ -132,10 +151,11 @@ static PyObject* encode(PyObject* self, PyObject* const* args, Py_ssize_t n) {
 }
 
 static PyMethodDef methods[] = {
-    {"bind", bind, METH_VARARGS, "bind(hamming, gc, decode2, encode): the library entry points' addresses"},
+    {"bind", bind, METH_VARARGS, "bind(hamming, gc, decode2, encode, decode3): the library entry points' addresses"},
     {"hamming", (PyCFunction)(void (*)(void))hamming, METH_FASTCALL, "hamming(kind, a, b) -> int or NotImplemented"},
     {"gc", (PyCFunction)(void (*)(void))gc, METH_FASTCALL, "gc(kind, code, L) -> int or NotImplemented"},
     {"decode2", (PyCFunction)(void (*)(void))decode2, METH_FASTCALL, "decode2(code, L) -> bytes or NotImplemented"},
+    {"decode3", (PyCFunction)(void (*)(void))decode3, METH_FASTCALL, "decode3(code) -> bytes or NotImplemented"},
     {"encode", (PyCFunction)(void (*)(void))encode, METH_FASTCALL, "encode(kind, seq) -> int or NotImplemented"},
     {NULL, NULL, 0, NULL}};
 

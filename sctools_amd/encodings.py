@@ -406,7 +406,8 @@ class ThreeBit(Encoding):
     @classmethod
     def decode(cls, integer_encoded):
         """encodings.py:169-180 (batch of one)."""
-        return cls.decode_array([integer_encoded])[0]
+        out = _scalar.decode3(integer_encoded)  # an int in [0, 2^64) whose triplets all decode
+        return cls.decode_array([integer_encoded])[0] if out is NotImplemented else out
 
     @classmethod
     def gc_content(cls, integer_encoded):

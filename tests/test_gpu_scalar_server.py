@@ -171,3 +171,8 @@ def test_cpython_entry_points_take_the_common_case():
     for seq in ("ACGT", bytearray(b"ACGT"), b"", b"A" * 33):
         assert _scalar.encode(2, seq) is NotImplemented
     assert _scalar.encode(3, b"A" * 22) is NotImplemented
+    for s in (b"A", b"ACGTN" * 4, b"T" * 21):
+        c = T3.encode(s)
+        assert _scalar.decode3(c) == s == T3.decode_array([c])[0]
+    assert _scalar.decode3(0) == b"" and _scalar.decode3(5) is NotImplemented  # KeyError(5) via Python
+    assert _scalar.decode3(-1) is NotImplemented and _scalar.decode3(1 << 64) is NotImplemented
