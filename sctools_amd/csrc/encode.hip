@@ -258,15 +258,25 @@ __device__ __forceinline__ void decode2_limbs(const uint64_t* w, int words, int 
   }
 }
 
-// A one-limb code is read once into a register: the byte stores to o may alias w, so the
-// compiler reloaded it for every base (16 dependent LDS reads of a scalar-server decode)
+// A one-limb code is read once into a register and its bases leave four to a store: through the
+// generic path the byte stores to o (which may alias w) made the compiler reload the code for
+// every base, one dependent LDS read each in the scalar server (85 ns per base per call)
 __device__ __forceinline__ void decode2_record(const uint64_t* w, int words, int L, uint8_t* o) {
-  if (words == 1) {
-    const uint64_t c = w[0];
-    decode2_limbs(&c, 1, L, o);
-  } else {
+  if (words != 1) {
     decode2_limbs(w, words, L, o);
+    return;
   }
+  const uint64_t c = w[0];
+  auto base = [&](int p) {  // "ACTG"[group L-1-p], 'A' above the limb
+    const int pos = 2 * (L - 1 - p);
+    const uint32_t v = pos < 64 ? (uint32_t)(c >> pos) & 3u : 0u;
+    return (0x47544341u >> (8 * v)) & 0xFFu;
+  };
+  int p = 0;
+  if (((uintptr_t)o & 3u) == 0u)
+    for (; p + 4 <= L; p += 4)
+      *reinterpret_cast<uint32_t*>(o + p) = base(p) | base(p + 1) << 8 | base(p + 2) << 16 | base(p + 3) << 24;
+  for (; p < L; ++p) o[p] = (uint8_t)base(p);
 }
 
 __global__ __launch_bounds__(WG) void decode2_kernel(const uint64_t* __restrict__ codes, int64_t n,
@@ -305,13 +315,21 @@ __device__ __forceinline__ int32_t decode3_limbs(const uint64_t* w, int words, i
   return top + 1;
 }
 
+// (a one-limb code in a register, as decode2_record)
 __device__ __forceinline__ int32_t decode3_record(const uint64_t* w, int words, int maxlen, uint8_t* o,
                                                   int32_t& err) {
-  if (words == 1) {
-    const uint64_t c = w[0];
-    return decode3_limbs(&c, 1, maxlen, o, err);
+  if (words != 1) return decode3_limbs(w, words, maxlen, o, err);
+  const uint64_t c = w[0];
+  const int top = c ? (63 - __clzll((long long)c)) / 3 : -1;  // the top non-zero triplet
+  err = -1;
+  for (int t = 0; t <= top; ++t) {
+    const uint32_t v = (uint32_t)(c >> (3 * t)) & 7u;
+    // C A G T at 1..4, N at 6 (bytes of 0x544741434E: v = 1..4 -> byte v - 1, 6 -> byte 4)
+    const bool ok = (v >= 1u && v <= 4u) || v == 6u;
+    if (!ok && err < 0) err = (int32_t)v;
+    o[maxlen - 1 - t] = ok ? (uint8_t)(0x4E54474143ull >> (8 * (v == 6u ? 4u : v - 1u))) : (uint8_t)0;
   }
-  return decode3_limbs(w, words, maxlen, o, err);
+  return top + 1;
 }
 
 __global__ __launch_bounds__(WG) void decode3_kernel(const uint64_t* __restrict__ codes, int64_t n,

@@ -23,6 +23,8 @@
 
 typedef int (*hamming_fn)(int, const uint64_t*, const uint64_t*, int64_t, int, int32_t*);
 typedef int (*stop_fn)(void);
+typedef int (*decode2_fn)(const uint64_t*, int64_t, int, int, uint8_t*);
+typedef int (*gc_fn)(int, const uint64_t*, int64_t, int, int, int32_t*);
 
 #define CHK(x)                                               \
   do {                                                       \
@@ -177,6 +179,27 @@ int main() {
     printf("{\"probe\": \"c_call\", \"lib\": \"%s\", \"round\": %d, \"median_us\": %.3f, \"p10_us\": %.3f, \"p90_us\": %.3f, "
            "\"out\": %d}\n", path, round, per[per.size() / 2], per[per.size() / 10], per[per.size() * 9 / 10], out);
     fflush(stdout);
+  }
+  // the other one-record calls: decode (16 bases), gc_content
+  {
+    auto dec = (decode2_fn)dlsym(h, "sct_decode2_host");
+    auto gcf = (gc_fn)dlsym(h, "sct_gc_content_host");
+    uint8_t o64[64];
+    int32_t g = 0;
+    const int Ls[6] = {16, 1, 4, 8, 32, 16};
+    for (int which = 0; which < 7; ++which) {
+      const int L = which < 6 ? Ls[which] : 16;
+      std::vector<double> per;
+      for (int k = 0; k < 12000; ++k) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const int rc = which < 6 ? dec(&a, 1, 1, L, o64) : gcf(2, &a, 1, 1, 16, &g);
+        if (rc != 0) return 2;
+        if (k >= 2000) per.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+      }
+      std::sort(per.begin(), per.end());
+      printf("{\"probe\": \"%s\", \"L\": %d, \"median_us\": %.3f, \"p90_us\": %.3f}\n", which < 6 ? "c_decode2" : "c_gc",
+             L, per[per.size() / 2], per[per.size() * 9 / 10]);
+    }
   }
   // the same call after d ns of host work between calls (the Python wrapper's share), d = 0..2000:
   // a polled mailbox answers in steps of the poll period, so the latency depends on the phase
