@@ -1035,6 +1035,49 @@ def path_dropin(dev, reps, want_summary):
                       and [float(first[k]) for k in first] == got and [float(r_keep[k]) for k in keys] == got}}
 
 
+def path_scalar_calls(dev, reps=3000):
+    """The reference's per-call API, one call at a time (encodings.py:75-121, 155-202): each
+    TwoBit / ThreeBit scalar method in a Python loop over 256 distinct 16-bp barcodes, through the
+    library's resident scalar server (DESIGN.md §3.9), median of 5 timed loops of `reps` calls;
+    every answer of the first loop checked against the oracle's restatement."""
+    from oracle import oracle as O
+    from sctools_amd import _lib, encodings
+    _lib.check(_lib.lib().sct_set_device(dev.index or 0))
+    rng = np.random.default_rng(3)
+    seqs = [bytes(rng.choice(list(b"ACGT"), 16).tolist()) for _ in range(256)]
+    T2, T3 = encodings.TwoBit, encodings.ThreeBit
+    t2 = T2(16)
+    c2 = [T2.encode(x) for x in seqs]
+    c3 = [T3.encode(x) for x in seqs]
+    pairs2, pairs3 = list(zip(c2, c2[1:] + c2[:1])), list(zip(c3, c3[1:] + c3[:1]))
+    calls = {"TwoBit.hamming_distance": (lambda k: T2.hamming_distance(*pairs2[k & 255]),
+                                         lambda k: O.two_bit_hamming(*pairs2[k & 255])),
+             "TwoBit.encode": (lambda k: T2.encode(seqs[k & 255]), lambda k: O.two_bit_encode(seqs[k & 255])),
+             "TwoBit.decode": (lambda k: t2.decode(c2[k & 255]), lambda k: O.two_bit_decode(c2[k & 255], 16)),
+             "TwoBit.gc_content": (lambda k: t2.gc_content(c2[k & 255]), lambda k: O.two_bit_gc(c2[k & 255], 16)),
+             "ThreeBit.encode": (lambda k: T3.encode(seqs[k & 255]), lambda k: O.three_bit_encode(seqs[k & 255])),
+             "ThreeBit.hamming_distance": (lambda k: T3.hamming_distance(*pairs3[k & 255]),
+                                           lambda k: O.three_bit_hamming(*pairs3[k & 255]))}
+    out, ok = {}, True
+    for name, (fn, ref) in calls.items():
+        ok = ok and all(fn(k) == ref(k) for k in range(256))
+        loops = []
+        for _ in range(5):
+            t = time.perf_counter()
+            for k in range(reps):
+                fn(k)
+            loops.append((time.perf_counter() - t) / reps * 1e6)
+        out[name] = float(sorted(loops)[2])
+    return {"workload": "scalar drop-in methods, one call at a time (a Python loop; 256 distinct 16-bp barcodes)",
+            "unit": "us per call", "us_per_call": out,
+            "reference_us_per_call": {"TwoBit.hamming_distance": 1.2, "TwoBit.encode": 2.7, "TwoBit.decode": 2.1,
+                                      "TwoBit.gc_content": 1.3, "ThreeBit.encode": 2.2,
+                                      "ThreeBit.hamming_distance": 1.2},
+            "note": "reference: its pure-Python methods timed in the build container (SURVEY.md §6); here each "
+                    "call is a PCIe round trip to the resident server wave",
+            "check": {"vs_oracle": bool(ok), "sample": "256 calls of each method"}}
+
+
 def _guarded(fn, *a):
     """A side path that fails reports its error in the line instead of ending the bench."""
     try:
@@ -1371,6 +1414,7 @@ def run_rank(args, rank, world, local):
                 out["paths"]["fastq_stream_to_nearest"] = _guarded(path_fastq_stream_to_nearest, dev, threads)
             if args.config == 2:
                 out["paths"]["dropin_summary_737k"] = _guarded(path_dropin, dev, max(5, args.path_steps), summ)
+            out["paths"]["scalar_calls"] = _guarded(path_scalar_calls, dev)
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(codes, hist, args.cpu_seconds)
     if rank == 0:

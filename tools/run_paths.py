@@ -1,5 +1,5 @@
 """Run selected bench.py side paths alone: python tools/run_paths.py config4 dropin whitelist fastq
-config5_encode config5_allpairs pipeline.  One JSON line {name: result}."""
+config5_encode config5_allpairs pipeline host_arrays scalar.  One JSON line {name: result}."""
 import json
 import sys
 
@@ -32,6 +32,8 @@ for name in names:
         out[name] = bench._guarded(bench.path_config5_encode, dev, 3, copy)
     elif name == "host_arrays":
         out[name] = bench._guarded(bench.path_host_arrays, dev, bench.pcie_ceiling_gbs(dev))
+    elif name == "scalar":
+        out[name] = bench._guarded(bench.path_scalar_calls, dev)
     elif name == "config5_allpairs":
         out[name] = bench._guarded(bench.path_config5_allpairs, dev, 5, copy)
     print(json.dumps({name: out.get(name)}), file=sys.stderr, flush=True)
