@@ -41,7 +41,7 @@ int sct_set_device(int device);        /* select the device for later calls (hip
  * or pick between index layouts that give identical outputs, so tests can put seams inside
  * small problems and benchmarks can sweep.  Process-global; the library reads no environment
  * variable.  value < 0 restores the default.  Read when a plan is created (scalar: per call). */
-#define SCT_TUNE_SPECTRAL_CHUNK 1       /* slices per seed/tile pass (default 262144: the whole space) */
+#define SCT_TUNE_SPECTRAL_CHUNK 1       /* slices per seed/tile pass (default 262144, the whole space; 65536 for SCT_ALLPAIRS_NO_CACHE plans) */
 #define SCT_TUNE_SPECTRAL_MIN_N 2       /* AUTO takes SPECTRAL from this many 16-base codes (325000) */
 #define SCT_TUNE_ALLPAIRS_GRAB 3        /* pair kernel: work items per queue pull */
 #define SCT_TUNE_ALLPAIRS_FLUSH_ITEMS 4 /* pair kernel: flush lane counters every k items */

@@ -923,6 +923,11 @@ extern "C" int sct_allpairs_plan_create_ex2(const uint64_t* d_codes, int64_t n, 
   SCT_CHECK(n == 0 || d_codes != nullptr, "codes is NULL");
   SCT_CHECK(code_bits <= 64, "code_bits %d > 64: codes wider than 64 bits are not supported",
             code_bits);
+  // SPECTRAL slices per seed / tile pass: all 2^18 (one 4 GiB intermediate) for cached plans; a
+  // plan mapping its own memory (the one-shot drop-in call) maps a 1 GiB intermediate and makes
+  // four passes: 3.26 / 4.71 / 4.06 ms per config-2 drop-in call against 3.50 / 4.79 / 4.53 for
+  // one pass, three rounds on one box (tools/dropin_chunk_ab.py, profiles/ab_dropin_chunk_r06b.jsonl)
+  const int64_t chunk_knob = sct::tune(SCT_TUNE_SPECTRAL_CHUNK, (flags & SCT_ALLPAIRS_NO_CACHE) ? 65536 : 262144);
   auto* p = new sct_allpairs_plan();
   auto cleanup = [&](int rc) {
     sct_allpairs_plan_destroy(p);
@@ -936,8 +941,12 @@ extern "C" int sct_allpairs_plan_create_ex2(const uint64_t* d_codes, int64_t n, 
     // the plan's own buffers, carved from one block: the codes, the probe's scratch and (for a
     // set AUTO sends to SPECTRAL) the transform's buffers with its 4 GiB intermediate
     size_t est = ((size_t)n * 8 + 255) + ((size_t)36 << 20);
-    if (n >= 2 && n >= sct::tune(SCT_TUNE_SPECTRAL_MIN_N, 325000))
-      est += (size_t)n * 4 + ((size_t)n / 32 + 65536) * 80 + ((size_t)4 << 30) + ((size_t)16 << 20);
+    if (n >= 2 && n >= sct::tune(SCT_TUNE_SPECTRAL_MIN_N, 325000)) {
+      // the intermediate: one chunk of 16-KiB slices (int8, 14-bit columns; a set dense enough for
+      // 16-bit columns maps the rest of its larger intermediate separately)
+      const int64_t chunk = std::min<int64_t>(std::max<int64_t>(chunk_knob, 64), 262144);
+      est += (size_t)n * 4 + ((size_t)n / 32 + 65536) * 80 + (size_t)((chunk + 15) & ~15ll) * 16384 + ((size_t)16 << 20);
+    }
     p->spec.ws = sct_spectral::ws_arena(est);
   } else {
     p->spec.ws = sct_spectral::ws_acquire();
@@ -983,7 +992,7 @@ extern "C" int sct_allpairs_plan_create_ex2(const uint64_t* d_codes, int64_t n, 
     p->ncounts = sct_spectral::kNCounts;
     p->items = n >= 2 ? sct_spectral::kSlices : 0;
     p->spec.distinct = (flags & SCT_ALLPAIRS_DISTINCT) != 0;
-    const int rc = sct_spectral::create(p->spec, p->d_codes, n, sct::tune(SCT_TUNE_SPECTRAL_CHUNK, 262144), cus,
+    const int rc = sct_spectral::create(p->spec, p->d_codes, n, chunk_knob, cus,
                                         (unsigned)probe[1], (unsigned)probe[2]);
     if (rc != SCT_OK) return cleanup(rc);
     p->spec.timer = &p->timer;
