@@ -1,4 +1,7 @@
 #!/bin/bash
+# (historical: the variant libraries it compares were built from round-6 intermediate trees with
+# tools/build_variant_lib.sh; their ablation macros are no longer in the sources -- results under
+# profiles/scalar_floor_r06/)
 # scalar server A/B: its GPU tests, the mailbox floors and the library's C call per server variant
 # (tools/scalar_floor_probe.hip incl. the host-work sweep, tools/build_variant_lib.sh), and the
 # Python drop-in calls (tools/scalar_latency.py)
