@@ -406,8 +406,12 @@ int sct_base_frequency_host(const uint64_t* codes, int64_t n, int L, uint64_t* o
  *   index[i] = j  if exactly one whitelist index j attains d_min(q_i) <= max_d,
  *            = -2 if several indices attain it, -1 if d_min > max_d;
  *   dist[i]  = d_min if <= max_d, else 255.
- * The plan is an exact pigeonhole index (max_d+1 position blocks, CSR buckets per block);
- * it copies nothing from the caller after create returns (the whitelist is bucketed).
+ * The plan is an exact pigeonhole index (max_d <= 1 on A/C/G/T whitelists: half-key tables;
+ * otherwise open-addressing or CSR buckets per position block); it copies nothing from the
+ * caller after create returns (the whitelist is bucketed).  A half-key whitelist sorted
+ * alphabetically, or numerically as TwoBit or ThreeBit codes, is queried in one kernel (table
+ * position = whitelist index); any other order adds a pass mapping positions to indices.  The
+ * answers never depend on the order.
  * code_bits: bits covered by the block split (whitelist codes < 2^code_bits).
  */
 typedef struct sct_nearest_plan sct_nearest_plan;

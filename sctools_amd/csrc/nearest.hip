@@ -317,6 +317,17 @@ struct Halves {
   const uint32_t* permAB;   // [2 nw] whitelist index of each A-order, then B-order position (build only;
                             // the index pass reads it packed, sct_nearest_plan::perm_packed)
   int64_t nw;
+  // Digit keys: any order of A/C/G/T answers the same (a key only has to be equal or not), so the
+  // plan takes the order the whitelist is sorted in, if any -- alphabetical (a 10x whitelist file),
+  // TwoBit's A C T G (numerically sorted TwoBit codes) or ThreeBit's C A G T -- as
+  // d1 = the base's TwoBit high bit, d0 = (TwoBit low bit) ^ dinv ^ (dalpha & d1).  In key order
+  // A-order position p is whitelist index p: the query kernel then writes whitelist indices itself,
+  // reading the packed permutation only for a winner found through the B table, and the index
+  // pass is skipped (ident_a).
+  uint32_t dinv, dalpha;  // 0 or ~0u
+  int ident_a;
+  const uint32_t* perm_packed;
+  int pbits;
 };
 
 // Stride-3 -> stride-2 compaction of the 8 fields of a 24-bit ThreeBit half (field p at bit
@@ -336,15 +347,18 @@ __device__ __forceinline__ uint32_t compact3to2(uint32_t x) {
   return x;
 }
 
-// one ThreeBit half of `nd` triplets (bits 0..3 nd - 1 of h) -> 2-bit digit key (C 0, A 1,
-// G 2, T 3) and the invalid digits spread to the key's even bits
-__device__ __forceinline__ void half3(uint32_t h, int nd, uint32_t& key, uint32_t& spread) {
+// one ThreeBit half of `nd` triplets (bits 0..3 nd - 1 of h) -> 2-bit digit key in the plan's
+// digit order (Halves::dinv / dalpha) and the invalid digits spread to the key's even bits
+__device__ __forceinline__ void half3(uint32_t h, int nd, uint32_t dinv, uint32_t dalpha, uint32_t& key,
+                                      uint32_t& spread) {
   constexpr uint32_t M = 0x249249u;  // bit 3p, p < 8
   const uint32_t live = nd >= 8 ? M : (M & ((1u << (3 * nd)) - 1));
   const uint32_t a = h & live, b = (h >> 1) & live, c = (h >> 2) & live;
-  // valid triplets 1..4 (abc = 100, 010, 110, 001): d0 = !a, d1 = (a & b) | c
+  // valid triplets C 1, A 2, G 3, T 4 (abc = 100, 010, 110, 001): d1 = (a & b) | c (G, T), and a
+  // is TwoBit's low bit (C, G); d0 = a ^ dinv ^ (dalpha & d1)
   const uint32_t valid = (~c & (a | b)) | (c & ~a & ~b);
-  const uint32_t dig = ((~a & live) | (((a & b) | c) << 1));
+  const uint32_t d1 = (a & b) | c;
+  const uint32_t dig = ((a ^ dinv ^ (dalpha & d1)) & live) | (d1 << 1);
   key = compact3to2<2>(dig);
   spread = compact3to2<1>(live & ~valid);
 }
@@ -356,13 +370,15 @@ __device__ __forceinline__ void halves_of(uint64_t q, const Halves& h, uint32_t&
   const uint64_t hi = top >= 64 ? 0ull : q >> top;
   if constexpr (KIND == 2) {
     E = __popcll((hi | (hi >> 1)) & 0x5555555555555555ull);
-    kB = (uint32_t)(q & ((1u << (2 * h.GB)) - 1));
-    kA = (uint32_t)(q >> (2 * h.GB)) & ((1u << (2 * h.GA)) - 1);
+    // TwoBit digits A 0, C 1, T 2, G 3: d0 ^= dinv ^ (dalpha & d1)
+    const uint32_t x = (uint32_t)(q & 0xFFFFFFFFull), f = (h.dinv & 0x55555555u) ^ (h.dalpha & (x >> 1) & 0x55555555u);
+    kB = (x ^ f) & ((1u << (2 * h.GB)) - 1);
+    kA = ((x ^ f) >> (2 * h.GB)) & ((1u << (2 * h.GA)) - 1);
     sA = sB = 0;
   } else {
     E = __popcll((hi | (hi >> 1) | (hi >> 2)) & 0x9249249249249249ull);
-    half3((uint32_t)(q & ((1u << (3 * h.GB)) - 1)), h.GB, kB, sB);
-    half3((uint32_t)((q >> (3 * h.GB)) & ((1u << (3 * h.GA)) - 1)), h.GA, kA, sA);
+    half3((uint32_t)(q & ((1u << (3 * h.GB)) - 1)), h.GB, h.dinv, h.dalpha, kB, sB);
+    half3((uint32_t)((q >> (3 * h.GB)) & ((1u << (3 * h.GA)) - 1)), h.GA, h.dinv, h.dalpha, kA, sA);
   }
 }
 
@@ -425,7 +441,16 @@ __device__ __forceinline__ void scan_half(const uint16_t* __restrict__ ent, uint
   }
 }
 
-template <int KIND>
+typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ int32_t unpack_perm(const uint32_t* __restrict__ packed, int pbits, int32_t p) {
+  const uint64_t bo = (uint64_t)p * pbits;
+  const u32x2_a4 d = *reinterpret_cast<const u32x2_a4*>(packed + (bo >> 5));  // one 8-byte load
+  return (int32_t)(((((uint64_t)d.y << 32) | d.x) >> (bo & 31)) & ((1ull << pbits) - 1));
+}
+
+// IDX (Halves::ident_a): out_pos receives whitelist indices (a B-table winner's through the packed
+// permutation, read here), else table positions for halves_index_kernel
+template <int KIND, bool IDX>
 __global__ __launch_bounds__(WG) void halves_query_kernel(const uint64_t* __restrict__ queries, int64_t nq, Halves h,
                                                           int max_d, int32_t* __restrict__ out_pos,
                                                           uint8_t* __restrict__ out_dist) {
@@ -450,7 +475,9 @@ __global__ __launch_bounds__(WG) void halves_query_kernel(const uint64_t* __rest
     pos = nA0 == 1 ? (int32_t)pA0 : -2;
     dist = (uint8_t)E;
   } else if (eff >= 1 && nA1 + nB1) {
-    pos = nA1 + nB1 >= 2 ? -2 : (nA1 ? (int32_t)pA1 : (int32_t)(h.nw + pB1));
+    if (nA1 + nB1 >= 2) pos = -2;
+    else if (nA1) pos = (int32_t)pA1;
+    else pos = IDX ? unpack_perm(h.perm_packed, h.pbits, (int32_t)(h.nw + pB1)) : (int32_t)(h.nw + pB1);
     dist = (uint8_t)(1 + E);
   }
   __builtin_nontemporal_store(pos, out_pos + i);
@@ -470,13 +497,6 @@ __global__ void pack_perm_kernel(const uint32_t* __restrict__ perm, int64_t n, i
     }
     out[w] = v;
   }
-}
-
-typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
-__device__ __forceinline__ int32_t unpack_perm(const uint32_t* __restrict__ packed, int pbits, int32_t p) {
-  const uint64_t bo = (uint64_t)p * pbits;
-  const u32x2_a4 d = *reinterpret_cast<const u32x2_a4*>(packed + (bo >> 5));  // one 8-byte load
-  return (int32_t)(((((uint64_t)d.y << 32) | d.x) >> (bo & 31)) & ((1ull << pbits) - 1));
 }
 
 // table positions -> whitelist indices (-1 / -2 pass through): four queries per lane per step,
@@ -504,10 +524,18 @@ __global__ __launch_bounds__(WG) void halves_index_kernel(int32_t* __restrict__ 
 //   scan     one workgroup: offsets of both tables, the cursors in place
 //   scatter  per code: one slot in its A bucket (entry = its B key) and one in its B bucket
 //            (entry = its A key), the whitelist index of both slots into permAB
+// the digit order halves_pick_order_kernel chose (device words: dinv, dalpha, ident_a)
+__device__ __forceinline__ void take_order(Halves& h, const unsigned* __restrict__ order) {
+  h.dinv = order[0];
+  h.dalpha = order[1];
+  h.ident_a = (int)order[2];
+}
+
 template <int KIND>
 __global__ void halves_count_kernel(const uint64_t* __restrict__ wl, int64_t nw, Halves h,
                                     uint32_t* __restrict__ cntA, uint32_t* __restrict__ cntB,
-                                    unsigned* __restrict__ bad) {
+                                    unsigned* __restrict__ bad, const unsigned* __restrict__ order) {
+  take_order(h, order);
   bool b = false;
   for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j < nw; j += (int64_t)gridDim.x * WG) {
     uint32_t kA, sA, kB, sB;
@@ -520,10 +548,50 @@ __global__ void halves_count_kernel(const uint64_t* __restrict__ wl, int64_t nw,
   if (b) atomicOr(bad, 1u);
 }
 
-// exclusive scan of cnt[0, n) by one 1024-thread workgroup into off[0, n] and cnt (the cursors)
+// exclusive scan of cnt[0, n) by one 1024-thread workgroup into off[0, n] and cnt (the cursors);
+// n = 4096 k (k <= 16: half keys of 6-8 digits) as 16-B vectors, all of a thread's loads in
+// flight at once (one element at a time the scan of 2 x 65,536 counts took 0.28 ms)
 __device__ __forceinline__ void block_scan_offsets(uint32_t* __restrict__ cnt, int64_t n, uint32_t* __restrict__ off,
                                                    uint32_t* wsum) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (n % 4096 == 0 && n <= 65536) {
+    const int per4 = (int)(n / 4096);  // 16-B vectors per thread
+    uint4* c4 = reinterpret_cast<uint4*>(cnt) + (int64_t)t * per4;
+    uint4* o4 = reinterpret_cast<uint4*>(off) + (int64_t)t * per4;
+    uint4 v[16];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < per4) v[k] = c4[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < per4) s += v[k].x + v[k].y + v[k].z + v[k].w;
+    uint32_t is = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t a = __shfl_up(is, d);
+      if (lane >= d) is += a;
+    }
+    if (lane == 63) wsum[wave] = is;
+    __syncthreads();
+    uint32_t run = is - s;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < per4) {
+        uint4 r;
+        r.x = run;
+        r.y = r.x + v[k].x;
+        r.z = r.y + v[k].y;
+        r.w = r.z + v[k].z;
+        run = r.w + v[k].w;
+        o4[k] = r;
+        c4[k] = r;
+      }
+    if (t == 1023) off[n] = run;
+    __syncthreads();  // wsum is reused
+    return;
+  }
   const int64_t per = (n + 1023) / 1024, b = std::min<int64_t>(n, t * per), e = std::min<int64_t>(n, b + per);
   uint32_t s = 0;
   for (int64_t i = b; i < e; ++i) s += cnt[i];
@@ -555,16 +623,58 @@ __global__ __launch_bounds__(1024) void halves_scan_kernel(uint32_t* __restrict_
   block_scan_offsets(cntB, nB, offB, wsum);
 }
 
+// The candidate digit orders (Halves::dinv, dalpha) and whether the whitelist is out of (A, B) key
+// order under each: unsorted[o] = 1 if some code's key exceeds the next one's
+constexpr int kOrders = 3;
+constexpr uint32_t kOrderInv[kOrders] = {0u, 0u, ~0u}, kOrderAlpha[kOrders] = {~0u, 0u, 0u};  // ACGT, ACTG, CAGT
+template <int KIND>
+__global__ void halves_order_kernel(const uint64_t* __restrict__ wl, int64_t nw, Halves h,
+                                    unsigned* __restrict__ unsorted) {
+  bool u[kOrders] = {};
+  for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j + 1 < nw; j += (int64_t)gridDim.x * WG) {
+    const uint64_t w0 = wl[j], w1 = wl[j + 1];
+#pragma unroll
+    for (int o = 0; o < kOrders; ++o) {
+      h.dinv = kOrderInv[o];
+      h.dalpha = kOrderAlpha[o];
+      uint32_t kA, sA, kB, sB, kA1, kB1;
+      int E;
+      halves_of<KIND>(w0, h, kA, sA, kB, sB, E);
+      halves_of<KIND>(w1, h, kA1, sA, kB1, sB, E);
+      u[o] |= kA > kA1 || (kA == kA1 && kB > kB1);
+    }
+  }
+  // one atomic per wave, and none once the flag is set (every wave of an unsorted whitelist finds
+  // a pair out of order: 11K atomics on three words serialised at L2 cost 0.3 ms)
+#pragma unroll
+  for (int o = 0; o < kOrders; ++o)
+    if (__ballot(u[o]) && (threadIdx.x & 63) == 0 && !__hip_atomic_load(unsorted + o, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT))
+      atomicOr(unsorted + o, 1u);
+}
+
+// order[0..2] = dinv, dalpha, ident_a of the first candidate order the whitelist is sorted in, or
+// alphabetical keys with ident_a = 0 (the index pass then maps the A-table positions)
+__global__ void halves_pick_order_kernel(const unsigned* __restrict__ unsorted, unsigned* __restrict__ order) {
+  int o = 0;
+  while (o < kOrders && unsorted[o]) ++o;
+  order[0] = kOrderInv[o < kOrders ? o : 0];
+  order[1] = kOrderAlpha[o < kOrders ? o : 0];
+  order[2] = o < kOrders ? 1u : 0u;
+}
+
 template <int KIND>
 __global__ void halves_scatter_kernel(const uint64_t* __restrict__ wl, int64_t nw, Halves h,
                                       uint32_t* __restrict__ curA, uint32_t* __restrict__ curB,
                                       uint16_t* __restrict__ entA, uint16_t* __restrict__ entB,
-                                      uint32_t* __restrict__ perm) {
+                                      uint32_t* __restrict__ perm, const unsigned* __restrict__ order) {
+  take_order(h, order);
+  const bool sorted = h.ident_a != 0;  // in key order: code j's A-table slot is j
   for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j < nw; j += (int64_t)gridDim.x * WG) {
     uint32_t kA, sA, kB, sB;
     int E;
     halves_of<KIND>(wl[j], h, kA, sA, kB, sB, E);
-    const uint32_t pA = atomicAdd(&curA[kA], 1u), pB = atomicAdd(&curB[kB], 1u);
+    const uint32_t pA = sorted ? (uint32_t)j : atomicAdd(&curA[kA], 1u), pB = atomicAdd(&curB[kB], 1u);
     entA[pA] = (uint16_t)kB;
     perm[pA] = (uint32_t)j;
     entB[pB] = (uint16_t)kA;
@@ -697,8 +807,9 @@ static int build_halves(sct_nearest_plan* p, const uint64_t* d_wl, int64_t nw, i
   h.entB = reinterpret_cast<const uint16_t*>(base + oEntB);
   p->perm_packed = reinterpret_cast<uint32_t*>(base + oPack);
   p->pbits = pb;
-  // scratch: bucket counts / cursors of both tables, permAB unpacked, the layout flag
-  const size_t sCnt = 0, sPerm = sCnt + al((nA + nB) * 4), sBad = sPerm + al(2 * n * 4), sTotal = sBad + 256;
+  // scratch: bucket counts / cursors of both tables, permAB unpacked, the layout flag and the
+  // out-of-key-order flag
+  const size_t sCnt = 0, sPerm = sCnt + al((nA + nB) * 4), sBad = sPerm + al(2 * n * 4), sTotal = sBad + 256;  // (flags: 1 + kOrders words)
   void* scratch = nullptr;
   SCT_HIP(sct::pool_alloc(&scratch, sTotal, s));
   char* sb = reinterpret_cast<char*>(scratch);
@@ -707,36 +818,54 @@ static int build_halves(sct_nearest_plan* p, const uint64_t* d_wl, int64_t nw, i
   uint32_t* perm = reinterpret_cast<uint32_t*>(sb + sPerm);
   unsigned* bad = reinterpret_cast<unsigned*>(sb + sBad);
   hipError_t e = hipMemsetAsync(sb, 0, sPerm, s);
-  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, 4, s);
+  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, 4 * (1 + kOrders), s);
   const unsigned g = grid_for(nw, 4096);
+  // the digit order: the first candidate the whitelist is sorted in, chosen on the device (no extra
+  // synchronisation; the build's kernels and the host read it from `order`)
+  unsigned* order = bad + 1 + kOrders;
   if (e == hipSuccess) {
     if (p->kind == 2)
-      hipLaunchKernelGGL(halves_count_kernel<2>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB, bad);
+      hipLaunchKernelGGL(halves_order_kernel<2>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, bad + 1);
     else
-      hipLaunchKernelGGL(halves_count_kernel<3>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB, bad);
+      hipLaunchKernelGGL(halves_order_kernel<3>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, bad + 1);
+    hipLaunchKernelGGL(halves_pick_order_kernel, dim3(1), dim3(1), 0, s, (const unsigned*)(bad + 1), order);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    if (p->kind == 2)
+      hipLaunchKernelGGL(halves_count_kernel<2>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB, bad,
+                         (const unsigned*)order);
+    else
+      hipLaunchKernelGGL(halves_count_kernel<3>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB, bad,
+                         (const unsigned*)order);
     hipLaunchKernelGGL(halves_scan_kernel, dim3(1), dim3(1024), 0, s, cntA, nA, (uint32_t*)h.offA, cntB, nB,
                        (uint32_t*)h.offB);
     if (p->kind == 2)
       hipLaunchKernelGGL(halves_scatter_kernel<2>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB,
-                         (uint16_t*)h.entA, (uint16_t*)h.entB, perm);
+                         (uint16_t*)h.entA, (uint16_t*)h.entB, perm, (const unsigned*)order);
     else
       hipLaunchKernelGGL(halves_scatter_kernel<3>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB,
-                         (uint16_t*)h.entA, (uint16_t*)h.entB, perm);
+                         (uint16_t*)h.entA, (uint16_t*)h.entB, perm, (const unsigned*)order);
     hipLaunchKernelGGL(pack_perm_kernel, dim3(grid_for(ndw, 4096)), dim3(WG), 0, s, (const uint32_t*)perm,
                        (int64_t)(2 * n), pb, ndw, p->perm_packed);
     e = hipGetLastError();
   }
-  unsigned hbad = 1;
-  if (e == hipSuccess) e = hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s);
+  unsigned hflags[2 + 2 * kOrders] = {1u};  // layout not applicable, (unsorted flags), dinv, dalpha, ident_a
+  if (e == hipSuccess) e = hipMemcpyAsync(hflags, bad, sizeof(hflags), hipMemcpyDeviceToHost, s);
   sct::pool_free(scratch, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return sct::fail(SCT_E_HIP, "half-key build: %s", hipGetErrorString(e));
-  if (hbad) {  // not applicable: another layout
+  if (hflags[0]) {  // not applicable: another layout
     (void)hipFree(p->hv_mem[0]);
     p->hv_mem[0] = nullptr;
     p->perm_packed = nullptr;
     return SCT_OK;
   }
+  h.dinv = hflags[1 + kOrders];
+  h.dalpha = hflags[2 + kOrders];
+  h.ident_a = (int)hflags[3 + kOrders];
+  h.perm_packed = p->perm_packed;
+  h.pbits = pb;
   p->hv = h;
   p->halves = true;
   return SCT_OK;
@@ -941,7 +1070,13 @@ static int nearest_query_launch(sct_nearest_plan* p, const uint64_t* d_queries, 
   const unsigned blocks = (unsigned)sct::ceil_div(nq, WG);  // one query per thread
   SCT_CHECK(sct::ceil_div(nq, WG) < (1LL << 31), "too many queries for one launch");
   if (p->halves) {
-    auto kern = p->kind == 2 ? halves_query_kernel<2> : halves_query_kernel<3>;
+    if (p->hv.ident_a) {  // whitelist indices straight from the query kernel
+      auto kern = p->kind == 2 ? halves_query_kernel<2, true> : halves_query_kernel<3, true>;
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(WG), 0, s, d_queries, nq, p->hv, p->max_d, d_index, d_dist);
+      SCT_LAUNCH_CHECK();
+      return SCT_OK;
+    }
+    auto kern = p->kind == 2 ? halves_query_kernel<2, false> : halves_query_kernel<3, false>;
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WG), 0, s, d_queries, nq, p->hv, p->max_d, d_index, d_dist);
     SCT_LAUNCH_CHECK();
     hipLaunchKernelGGL(halves_index_kernel, dim3(grid_for(sct::ceil_div(nq, 4), 8192)), dim3(WG), 0, s, d_index, nq,

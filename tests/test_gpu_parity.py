@@ -817,6 +817,55 @@ def test_nearest_halves_big_buckets(kind):
     assert np.array_equal(idx, ridx) and np.array_equal(dist, rdist)
 
 
+@pytest.mark.parametrize("kind", [3, 2])
+def test_nearest_halves_sorted_and_shuffled_whitelists(kind):
+    """A whitelist in alphabetical order (key order: the query kernel writes whitelist indices and
+    reads the permutation only for B-table winners, no index pass) and the same whitelist shuffled
+    (positions mapped by the index pass): identical answers up to the shuffle, and both against
+    the brute force on a sample; duplicates appended at the end break the order (general path)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(11 + kind)
+    L = 16
+    wl2 = synthetic.whitelist_codes(60_000, L, seed=5 + kind)  # sorted: alphabetical
+    wl = wl2 if kind == 2 else synthetic.two_to_three(wl2, L)
+    q = wl[rng.integers(0, wl.size, 200_000)].copy()
+    pos = rng.integers(0, L, q.size).astype(np.uint64)
+    w = np.uint64(kind)
+    sub = rng.integers(0, 4, q.size).astype(np.uint64) + (np.uint64(1) if kind == 3 else np.uint64(0))
+    m = rng.random(q.size)
+    one = m < 0.5
+    q[one] = (q[one] & ~(np.uint64((1 << kind) - 1) << (w * pos[one]))) | (sub[one] << (w * pos[one]))
+    if kind == 3:
+        nn = (m >= 0.5) & (m < 0.65)
+        q[nn] = q[nn] & ~(np.uint64(7) << (w * pos[nn]))  # N
+    perm = rng.permutation(wl.size)
+    out = {}
+    for name, w_ in (("sorted", wl), ("shuffled", wl[perm]), ("dups", np.concatenate([wl, wl[:3]]))):
+        d_wl = torch.from_numpy(np.ascontiguousarray(w_).view(np.int64)).cuda()
+        d_q = torch.from_numpy(q.view(np.int64)).cuda()
+        plan = _lib.NearestPlan(kind, d_wl.data_ptr(), w_.size, kind * L, 1)
+        assert plan.info()["scheme"] == "halves"
+        oi = torch.empty(q.size, dtype=torch.int32, device="cuda")
+        od = torch.empty(q.size, dtype=torch.uint8, device="cuda")
+        plan.query(d_q.data_ptr(), q.size, oi.data_ptr(), od.data_ptr())
+        torch.cuda.synchronize()
+        plan.close()
+        out[name] = (oi.cpu().numpy(), od.cpu().numpy())
+    si, sd = out["sorted"]
+    hi, hd = out["shuffled"]
+    mapped = np.where(hi >= 0, perm[np.maximum(hi, 0)], hi)
+    assert np.array_equal(mapped, si) and np.array_equal(hd, sd)
+    samp = rng.integers(0, q.size, 4000)
+    ridx, rdist = O.c_nearest(kind, wl, q[samp], 1)
+    assert np.array_equal(si[samp], ridx) and np.array_equal(sd[samp], rdist)
+    # with the duplicates (ties at distance 0 and 1 with their first copies) against the brute force
+    di, dd = out["dups"]
+    ridx, rdist = O.c_nearest(kind, np.concatenate([wl, wl[:3]]), q[samp], 1)
+    assert np.array_equal(di[samp], ridx) and np.array_equal(dd[samp], rdist)
+    near_dups = np.isin(q, wl[:3])
+    assert (di[near_dups] == -2).all()
+
+
 @pytest.mark.parametrize("kind,max_d", [(3, 1), (2, 1), (3, 0), (3, 2), (2, 2)])
 def test_whitelist_corrector_batches(kind, max_d):
     """WhitelistCorrector (one device index, many host batches) against nearest_whitelist and

@@ -31,7 +31,7 @@ KERNELS = (
     ("spectral_seed_int16", "seed_kernel<short>", "pmc", "trace", 65536, "slices"),
     ("spectral_seed16", "seed16_sm_kernel", "s5pmc", "s5trace", 65536, "slices of 2^16"),
     ("spectral16", "tile16_kernel", "s5pmc", "s5trace", 65536, "slices of 2^16"),
-    ("nearest", "halves_query_kernel", "npmc", "ntrace", 100_000_000, "queries"),
+    ("nearest", "halves_query_kernel<3, true>", "npmc", "ntrace", 100_000_000, "queries"),
     ("nearest_index", "halves_index_kernel", "npmc", "ntrace", 100_000_000, "queries"),
     ("whitelist_spec16", "whitelist_spec16_kernel", "ipmc", "itrace", 3_686_400, "lines"),
     ("whitelist_fused", "whitelist_fused_kernel", "ipmc", "itrace", 3_686_400, "lines"),
