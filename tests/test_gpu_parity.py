@@ -866,6 +866,37 @@ def test_nearest_halves_sorted_and_shuffled_whitelists(kind):
     assert (di[near_dups] == -2).all()
 
 
+@pytest.mark.parametrize("kind", [2, 3])
+@pytest.mark.parametrize("order", ["ACGT", "ACTG", "CAGT", "TGCA"])
+@pytest.mark.parametrize("L", [16, 13])
+def test_nearest_halves_whitelist_orders(kind, order, L):
+    """Whitelists sorted in each candidate digit order of the half-key build (alphabetical as a
+    10x file, TwoBit-numeric, ThreeBit-numeric) and in one that is none of them (reverse
+    alphabetical: the general path), at an even and an odd length: the brute force's answers,
+    max_d 0 and 1, ties from one duplicated code included."""
+    rng = np.random.default_rng(1000 * kind + 10 * L + ["ACGT", "ACTG", "CAGT", "TGCA"].index(order))
+    wl2 = synthetic.whitelist_codes(20_000, L, seed=L + kind)
+    seqs = synthetic.decode_ascii(wl2, L)
+    rank = np.zeros(256, dtype=np.int64)
+    for i, ch in enumerate(order.encode()):
+        rank[ch] = i
+    keys = rank[seqs]
+    srt = np.lexsort(keys.T[::-1])  # lexicographic in `order`'s digit ranks, first base most significant
+    wl2 = wl2[srt]
+    wl2 = np.insert(wl2, 5000, wl2[5000])  # one duplicated code, kept in order
+    wl = wl2 if kind == 2 else synthetic.two_to_three(wl2, L)
+    q = wl[rng.integers(0, wl.size, 3000)].copy()
+    pos = rng.integers(0, L, q.size).astype(np.uint64)
+    w = np.uint64(kind)
+    sub = rng.integers(0, 4, q.size).astype(np.uint64) + (np.uint64(1) if kind == 3 else np.uint64(0))
+    one = rng.random(q.size) < 0.6
+    q[one] = (q[one] & ~(np.uint64((1 << kind) - 1) << (w * pos[one]))) | (sub[one] << (w * pos[one]))
+    for max_d in (0, 1):
+        idx, dist = barcode.nearest_whitelist(q, wl, max_distance=max_d, encoding=kind)
+        ridx, rdist = O.c_nearest(kind, wl, q, max_d)
+        assert np.array_equal(idx, ridx) and np.array_equal(dist, rdist), (order, max_d)
+
+
 @pytest.mark.parametrize("kind,max_d", [(3, 1), (2, 1), (3, 0), (3, 2), (2, 2)])
 def test_whitelist_corrector_batches(kind, max_d):
     """WhitelistCorrector (one device index, many host batches) against nearest_whitelist and
