@@ -326,6 +326,10 @@ struct Halves {
   // pass is skipped (ident_a).
   uint32_t dinv, dalpha;  // 0 or ~0u
   int ident_a;
+  // ident_a: rankB[p] = the rank of B-order entry p's code inside its A bucket (< 256; null when a
+  // bucket holds more), so a B-table winner's whitelist index is offA[its A key] + rankB[p]: a
+  // 0.74 MB byte array beside the hot offsets instead of the 1.85 MB half of the permutation
+  const uint8_t* rankB;
   const uint32_t* perm_packed;
   int pbits;
 };
@@ -386,7 +390,7 @@ __device__ __forceinline__ void halves_of(uint64_t q, const Halves& h, uint32_t&
 // even bits): z0 / z1 count the entries at half distance 0 / 1, p0 / p1 the position of one.
 template <bool LEVEL0>
 __device__ __forceinline__ void scan_chunk(const uint4 v, uint32_t c, uint32_t b, uint32_t e, uint32_t k2, uint32_t sp2,
-                                           int& n0, uint32_t& p0, int& n1, uint32_t& p1) {
+                                           int& n0, uint32_t& p0, int& n1, uint32_t& p1, uint32_t& v1) {
   // in-range entries of the chunk, in the layout below: entry 2k at bit 2k, 2k + 1 at 16 + 2k
   const uint32_t lo = b > c ? b - c : 0u, hi = e - c < 8u ? e - c : 8u;
   const uint32_t in8 = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
@@ -415,6 +419,8 @@ __device__ __forceinline__ void scan_chunk(const uint4 v, uint32_t c, uint32_t b
     n1 += __popc(f1);
     const uint32_t bit = __ffs(f1) - 1;
     p1 = c + (bit < 16 ? bit : bit - 15);
+    const uint32_t q = (bit & 15) >> 1, d = q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
+    v1 = (d >> (bit & 16)) & 0xFFFFu;  // the entry's key (the other half of its code)
   }
 }
 
@@ -426,7 +432,7 @@ __device__ __forceinline__ void scan_chunk(const uint4 v, uint32_t c, uint32_t b
 // 2.46 / 2.23 / 2.17 / 2.19 ms per 100M queries, profiles/ab_nearest_chunks_r03.jsonl).
 template <bool LEVEL0, int kGroup = 3>
 __device__ __forceinline__ void scan_half(const uint16_t* __restrict__ ent, uint32_t b, uint32_t e, uint32_t k,
-                                          uint32_t sp, int& n0, uint32_t& p0, int& n1, uint32_t& p1) {
+                                          uint32_t sp, int& n0, uint32_t& p0, int& n1, uint32_t& p1, uint32_t& v1) {
   const uint32_t k2 = k | (k << 16), sp2 = sp | (sp << 16);
   for (uint32_t c = b & ~7u; c < e; c += 8 * kGroup) {
     uint4 v[kGroup];
@@ -437,7 +443,7 @@ __device__ __forceinline__ void scan_half(const uint16_t* __restrict__ ent, uint
     }
 #pragma unroll
     for (int j = 0; j < kGroup; ++j)
-      if (j == 0 || c + 8 * j < e) scan_chunk<LEVEL0>(v[j], c + 8 * j, b, e, k2, sp2, n0, p0, n1, p1);
+      if (j == 0 || c + 8 * j < e) scan_chunk<LEVEL0>(v[j], c + 8 * j, b, e, k2, sp2, n0, p0, n1, p1, v1);
   }
 }
 
@@ -462,13 +468,13 @@ __global__ __launch_bounds__(WG) void halves_query_kernel(const uint64_t* __rest
   halves_of<KIND>(q, h, kA, sA, kB, sB, E);
   const int eff = max_d - E;  // in-table distance allowed
   int nA0 = 0, nA1 = 0, nB0 = 0, nB1 = 0;
-  uint32_t pA0 = 0, pA1 = 0, pB0 = 0, pB1 = 0;
+  uint32_t pA0 = 0, pA1 = 0, pB0 = 0, pB1 = 0, vA1 = 0, vB1 = 0;
   if (eff >= 0 && sA == 0)  // the A bucket: codes agreeing with q on A
-    scan_half<true>(h.entA, h.offA[kA], h.offA[kA + 1], kB, sB, nA0, pA0, nA1, pA1);
+    scan_half<true>(h.entA, h.offA[kA], h.offA[kA + 1], kB, sB, nA0, pA0, nA1, pA1, vA1);
   // an exact hit (unique or not) is final: the B table holds no other code at distance 0;
   // in the B bucket the codes at A distance 0 are the A bucket's exact hits, not counted
   if (eff >= 1 && nA0 == 0 && sB == 0)
-    scan_half<false>(h.entB, h.offB[kB], h.offB[kB + 1], kA, sA, nB0, pB0, nB1, pB1);
+    scan_half<false>(h.entB, h.offB[kB], h.offB[kB + 1], kA, sA, nB0, pB0, nB1, pB1, vB1);
   int32_t pos = -1;
   uint8_t dist = 255;
   if (nA0) {
@@ -477,7 +483,9 @@ __global__ __launch_bounds__(WG) void halves_query_kernel(const uint64_t* __rest
   } else if (eff >= 1 && nA1 + nB1) {
     if (nA1 + nB1 >= 2) pos = -2;
     else if (nA1) pos = (int32_t)pA1;
-    else pos = IDX ? unpack_perm(h.perm_packed, h.pbits, (int32_t)(h.nw + pB1)) : (int32_t)(h.nw + pB1);
+    else if (!IDX) pos = (int32_t)(h.nw + pB1);
+    else if (h.rankB) pos = (int32_t)(h.offA[vB1] + h.rankB[pB1]);  // both loads at once
+    else pos = unpack_perm(h.perm_packed, h.pbits, (int32_t)(h.nw + pB1));
     dist = (uint8_t)(1 + E);
   }
   __builtin_nontemporal_store(pos, out_pos + i);
@@ -667,9 +675,11 @@ template <int KIND>
 __global__ void halves_scatter_kernel(const uint64_t* __restrict__ wl, int64_t nw, Halves h,
                                       uint32_t* __restrict__ curA, uint32_t* __restrict__ curB,
                                       uint16_t* __restrict__ entA, uint16_t* __restrict__ entB,
-                                      uint32_t* __restrict__ perm, const unsigned* __restrict__ order) {
+                                      uint32_t* __restrict__ perm, const unsigned* __restrict__ order,
+                                      uint8_t* __restrict__ rankB, unsigned* __restrict__ rank_over) {
   take_order(h, order);
   const bool sorted = h.ident_a != 0;  // in key order: code j's A-table slot is j
+  bool over = false;
   for (int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x; j < nw; j += (int64_t)gridDim.x * WG) {
     uint32_t kA, sA, kB, sB;
     int E;
@@ -679,7 +689,13 @@ __global__ void halves_scatter_kernel(const uint64_t* __restrict__ wl, int64_t n
     perm[pA] = (uint32_t)j;
     entB[pB] = (uint16_t)kA;
     perm[nw + pB] = (uint32_t)j;
+    if (sorted) {
+      const uint32_t r = pA - h.offA[kA];  // the code's rank inside its A bucket
+      over |= r > 255u;
+      rankB[pB] = (uint8_t)r;
+    }
   }
+  if (over) atomicOr(rank_over, 1u);
 }
 
 template <int KIND>
@@ -798,7 +814,8 @@ static int build_halves(sct_nearest_plan* p, const uint64_t* d_wl, int64_t nw, i
   // the plan's tables: offA, offB, entA, entB (+16 B: the last chunk's load may run past nw), packed permAB
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t oOffA = 0, oOffB = oOffA + al((nA + 1) * 4), oEntA = oOffB + al((nB + 1) * 4);
-  const size_t oEntB = oEntA + al(n * 2 + 16), oPack = oEntB + al(n * 2 + 16), total = oPack + al(ndw * 4);
+  const size_t oEntB = oEntA + al(n * 2 + 16), oPack = oEntB + al(n * 2 + 16), oRank = oPack + al(ndw * 4);
+  const size_t total = oRank + al(n);
   SCT_HIP(hipMalloc(&p->hv_mem[0], total));
   char* base = reinterpret_cast<char*>(p->hv_mem[0]);
   h.offA = reinterpret_cast<const uint32_t*>(base + oOffA);
@@ -806,6 +823,7 @@ static int build_halves(sct_nearest_plan* p, const uint64_t* d_wl, int64_t nw, i
   h.entA = reinterpret_cast<const uint16_t*>(base + oEntA);
   h.entB = reinterpret_cast<const uint16_t*>(base + oEntB);
   p->perm_packed = reinterpret_cast<uint32_t*>(base + oPack);
+  uint8_t* rankB = reinterpret_cast<uint8_t*>(base + oRank);
   p->pbits = pb;
   // scratch: bucket counts / cursors of both tables, permAB unpacked, the layout flag and the
   // out-of-key-order flag
@@ -818,7 +836,7 @@ static int build_halves(sct_nearest_plan* p, const uint64_t* d_wl, int64_t nw, i
   uint32_t* perm = reinterpret_cast<uint32_t*>(sb + sPerm);
   unsigned* bad = reinterpret_cast<unsigned*>(sb + sBad);
   hipError_t e = hipMemsetAsync(sb, 0, sPerm, s);
-  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, 4 * (1 + kOrders), s);
+  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, 4 * (2 + 2 * kOrders), s);
   const unsigned g = grid_for(nw, 4096);
   // the digit order: the first candidate the whitelist is sorted in, chosen on the device (no extra
   // synchronisation; the build's kernels and the host read it from `order`)
@@ -842,15 +860,18 @@ static int build_halves(sct_nearest_plan* p, const uint64_t* d_wl, int64_t nw, i
                        (uint32_t*)h.offB);
     if (p->kind == 2)
       hipLaunchKernelGGL(halves_scatter_kernel<2>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB,
-                         (uint16_t*)h.entA, (uint16_t*)h.entB, perm, (const unsigned*)order);
+                         (uint16_t*)h.entA, (uint16_t*)h.entB, perm, (const unsigned*)order, rankB,
+                         bad + 1 + 2 * kOrders);
     else
       hipLaunchKernelGGL(halves_scatter_kernel<3>, dim3(g), dim3(WG), 0, s, d_wl, nw, h, cntA, cntB,
-                         (uint16_t*)h.entA, (uint16_t*)h.entB, perm, (const unsigned*)order);
+                         (uint16_t*)h.entA, (uint16_t*)h.entB, perm, (const unsigned*)order, rankB,
+                         bad + 1 + 2 * kOrders);
     hipLaunchKernelGGL(pack_perm_kernel, dim3(grid_for(ndw, 4096)), dim3(WG), 0, s, (const uint32_t*)perm,
                        (int64_t)(2 * n), pb, ndw, p->perm_packed);
     e = hipGetLastError();
   }
-  unsigned hflags[2 + 2 * kOrders] = {1u};  // layout not applicable, (unsorted flags), dinv, dalpha, ident_a
+  // layout not applicable, (unsorted flags), dinv, dalpha, ident_a, an A bucket of > 256 codes
+  unsigned hflags[2 + 2 * kOrders] = {1u};
   if (e == hipSuccess) e = hipMemcpyAsync(hflags, bad, sizeof(hflags), hipMemcpyDeviceToHost, s);
   sct::pool_free(scratch, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -864,6 +885,7 @@ static int build_halves(sct_nearest_plan* p, const uint64_t* d_wl, int64_t nw, i
   h.dinv = hflags[1 + kOrders];
   h.dalpha = hflags[2 + kOrders];
   h.ident_a = (int)hflags[3 + kOrders];
+  h.rankB = h.ident_a && !hflags[1 + 2 * kOrders] ? rankB : nullptr;
   h.perm_packed = p->perm_packed;
   h.pbits = pb;
   p->hv = h;
