@@ -142,11 +142,12 @@ class ShardedAllPairs:
         Every step does all of ``step()``'s work -- zero, build, count, all-reduce, D2H,
         exact inversion -- with one of two plans and count buffers: step k + 1's build runs
         on a build stream as soon as its plan's count of step k - 1 is done (beside step k's
-        count; ``build_on = "main"`` keeps it in line instead), its count is queued on the main
-        stream before the host waits for step k, and step k's all-reduce and read-back run on a
-        tail stream, so they and the host's inversion overlap the next step's kernels instead of
-        leaving the GPU idle.  The main stream waits on one other stream per step at most (a
-        cross-queue wait costs the count ≈10-20 µs of idle GPU, rocprof trace)."""
+        count; ``build_on = "main"`` keeps it in line instead) and is enqueued before step k's
+        tail, its count is queued on the main stream before the host waits for step k - 1, and
+        step k's all-reduce and read-back run on a tail stream, so they and the host's inversion
+        overlap the next step's kernels instead of leaving the GPU idle.  The main stream waits
+        on one other stream per step at most (a cross-queue wait costs the count ≈10-20 µs of
+        idle GPU, rocprof trace)."""
         import torch
         import torch.distributed as dist
         if steps <= 0:
@@ -168,8 +169,11 @@ class ShardedAllPairs:
                 "counts": [self.counts, torch.zeros_like(self.counts)],
                 "host": [torch.zeros(self.plan.ncounts, dtype=torch.int64).pin_memory() for _ in range(2)],
                 "tail": torch.cuda.Stream(dev),
+                # timing events per step, k mod 4 (step k + 1's build and count are enqueued before
+                # the host reads step k - 1's), and each plan's count-done event for the waits
                 "ev": [{k: torch.cuda.Event(enable_timing=True) for k in ("b0", "b1", "c0", "c1", "a1", "m0", "m1")}
-                       for _ in range(2)],
+                       for _ in range(4)],
+                "cdone": [torch.cuda.Event() for _ in range(2)],
                 "done": [torch.cuda.Event() for _ in range(2)],
                 "zero": [torch.cuda.Event() for _ in range(2)],
                 "mom": [torch.cuda.Event() for _ in range(2)],
@@ -181,10 +185,11 @@ class ShardedAllPairs:
         side_build = self.build_on == "side" and not moments
         bs = pp["build"] if side_build else s
 
-        def issue(b):
-            counts, ev, plan = pp["counts"][b], pp["ev"][b], pp["plans"][b]
+        def build(k):
+            b = k & 1
+            counts, ev, plan = pp["counts"][b], pp["ev"][k & 3], pp["plans"][b]
             if side_build:
-                bs.wait_event(ev["c1"])  # this plan's count two steps ago no longer reads its tables
+                bs.wait_event(pp["cdone"][b])  # this plan's count two steps ago no longer reads its tables
                 bs.wait_event(pp["done"][b])  # this buffer's read-back two steps ago has finished
                 with torch.cuda.stream(bs):
                     counts.zero_()
@@ -196,9 +201,12 @@ class ShardedAllPairs:
             if side_build:
                 pp["built"][b].record(bs)
             else:
-                # (no GPU wait: this buffer's read-back two steps ago was waited for on the host,
-                # in finish(), before this issue() -- the loop below alternates them)
+                s.wait_event(pp["done"][b])  # this buffer's read-back two steps ago has finished
                 counts.zero_()
+
+        def count(k):
+            b = k & 1
+            counts, ev, plan = pp["counts"][b], pp["ev"][k & 3], pp["plans"][b]
             if moments:
                 pp["zero"][b].record(s)
                 side.wait_event(pp["zero"][b])
@@ -214,8 +222,14 @@ class ShardedAllPairs:
             if timing:
                 ev["c0"].record(s)
             plan.count(counts.data_ptr(), self.begin, self.end, 0, sptr)
-            ev["c1"].record(s)
-            tail.wait_event(ev["c1"])
+            if timing:
+                ev["c1"].record(s)
+            pp["cdone"][b].record(s)
+
+        def tail_part(k):
+            b = k & 1
+            counts, ev = pp["counts"][b], pp["ev"][k & 3]
+            tail.wait_event(pp["cdone"][b])
             with torch.cuda.stream(tail):
                 if self._reduce:
                     dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=self.group)
@@ -224,11 +238,12 @@ class ShardedAllPairs:
                 pp["host"][b].copy_(counts, non_blocking=True)
                 pp["done"][b].record(tail)
 
-        def finish(b):
+        def finish(k):
+            b = k & 1
             pp["done"][b].synchronize()
             host = pp["host"][b].numpy().astype(np.int64).view(np.uint64)
             if timing:
-                ev = pp["ev"][b]
+                ev = pp["ev"][k & 3]
                 self._t["build_ms"].append(ev["b0"].elapsed_time(ev["b1"]))
                 self._t["count_ms"].append(ev["c0"].elapsed_time(ev["c1"]))
                 self._t["allreduce_us"].append(1e3 * ev["c1"].elapsed_time(ev["a1"]))
@@ -237,11 +252,23 @@ class ShardedAllPairs:
             return _lib.counts_to_hist(host, self.plan.scheme, self.plan.nbins)
 
         hists = []
+        if not moments:
+            build(0)
+            count(0)
         for k in range(steps):
-            issue(k & 1)
+            if moments:  # (the moments pass and its build stay in step order on the main stream)
+                build(k)
+                count(k)
+                tail_part(k)
+            else:
+                if k + 1 < steps:
+                    build(k + 1)
+                tail_part(k)
+                if k + 1 < steps:
+                    count(k + 1)
             if k:
-                hists.append(finish((k - 1) & 1))
-        hists.append(finish((steps - 1) & 1))
+                hists.append(finish(k - 1))
+        hists.append(finish(steps - 1))
         return hists
 
     def reset_timings(self):
