@@ -386,6 +386,7 @@ __device__ __forceinline__ void halves_of(uint64_t q, const Halves& h, uint32_t&
   }
 }
 
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 // Entries [b, e) of a uint16 table against the half key k (invalid digits `sp` spread to the
 // even bits): z0 / z1 count the entries at half distance 0 / 1, p0 / p1 the position of one.
 template <bool LEVEL0>
@@ -399,9 +400,10 @@ __device__ __forceinline__ void scan_chunk(const uint4 v, uint32_t c, uint32_t b
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint32_t x = w[q] ^ k2;
-    const uint32_t m = ((x | (x >> 1)) & 0x55555555u) | sp2;
-    const uint32_t t = m & ((m | 0x80008000u) - 0x00010001u);
+    const uint32_t x = (w[q] ^ k2) | sp2;  // an invalid query digit differs from every entry digit
+    const uint32_t m = (x | (x >> 1)) & 0x55555555u;
+    const u16x2 mh = __builtin_bit_cast(u16x2, m);
+    const uint32_t t = m & __builtin_bit_cast(uint32_t, (u16x2)(mh - (u16x2){1, 1}));  // per half: m & (m - 1)
     const uint32_t ge1 = (m + 0x7FFF7FFFu) & 0x80008000u, ge2 = (t + 0x7FFF7FFFu) & 0x80008000u;
     if constexpr (LEVEL0) f0 |= ((~ge1 & 0x80008000u) >> 15) << (2 * q);
     f1 |= ((ge1 & ~ge2) >> 15) << (2 * q);
@@ -429,17 +431,23 @@ __device__ __forceinline__ void scan_chunk(const uint4 v, uint32_t c, uint32_t b
 // Chunks of 8 entries go three at a time: all three 16-B loads (the ones inside [b, e)) are
 // issued before any is tested, so the later ones (usually in the same line) ride on the first's
 // miss instead of making their own dependent L2 requests (one, two, three, four at a time:
-// 2.46 / 2.23 / 2.17 / 2.19 ms per 100M queries, profiles/ab_nearest_chunks_r03.jsonl).
+// 2.46 / 2.23 / 2.17 / 2.19 ms per 100M queries, profiles/ab_nearest_chunks_r03.jsonl).  The
+// first chunk starts at b's dword, not its 16-B chunk: a wave runs as many chunks as its fullest
+// lane spans, and the 16-B rounding added one on most waves (1.5-2 %, ab_nearest_align_r06.json).
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 template <bool LEVEL0, int kGroup = 3>
 __device__ __forceinline__ void scan_half(const uint16_t* __restrict__ ent, uint32_t b, uint32_t e, uint32_t k,
                                           uint32_t sp, int& n0, uint32_t& p0, int& n1, uint32_t& p1, uint32_t& v1) {
   const uint32_t k2 = k | (k << 16), sp2 = sp | (sp << 16);
-  for (uint32_t c = b & ~7u; c < e; c += 8 * kGroup) {
+  for (uint32_t c = b & ~1u; c < e; c += 8 * kGroup) {
     uint4 v[kGroup];
 #pragma unroll
     for (int j = 0; j < kGroup; ++j) {
       v[j] = make_uint4(0, 0, 0, 0);
-      if (j == 0 || c + 8 * j < e) v[j] = *reinterpret_cast<const uint4*>(ent + c + 8 * j);
+      if (j == 0 || c + 8 * j < e) {
+        const u32x4_a4 x = *reinterpret_cast<const u32x4_a4*>(ent + c + 8 * j);
+        v[j] = make_uint4(x.x, x.y, x.z, x.w);
+      }
     }
 #pragma unroll
     for (int j = 0; j < kGroup; ++j)

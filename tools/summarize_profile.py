@@ -82,8 +82,10 @@ def kernel_avg_ns(stats_csv, kernel_substr):
     return None, 0
 
 
-def summarize(src, dst, rnd, name, kernel, prefix, trace, units, unit):
+def summarize(src, dst, rnd, name, kernel, prefix, trace, units, unit, window=None):
     avg_ns, calls = kernel_avg_ns(os.path.join(src, trace, "run_kernel_stats.csv"), kernel)
+    if window:  # the headline's full-size timed dispatches (the side paths launch smaller ones)
+        avg_ns, calls = window["avg_ns"], window["window"]
     m = pmc_means(src, prefix, kernel)
     if not calls and not m:
         return None
@@ -154,7 +156,8 @@ def main():
                   f, indent=1)
     print("timed window", json.dumps(win))
     for name, kernel, prefix, trace, units, unit in KERNELS:
-        r = summarize(a.src, dst, a.round, name, kernel, prefix, trace, units, unit)
+        r = summarize(a.src, dst, a.round, name, kernel, prefix, trace, units, unit,
+                      win.get(kernel) if trace == "trace" else None)
         print(name, json.dumps({k: v for k, v in (r or {}).items() if k != "pmc"}, indent=1))
 
 
