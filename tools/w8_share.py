@@ -13,6 +13,8 @@ from sctools_amd import _lib, sharding, synthetic  # noqa: E402
 world = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 build_on = sys.argv[3] if len(sys.argv) > 3 else "side"  # ShardedAllPairs.build_on
+if len(sys.argv) > 4 and sys.argv[4] == "old":  # an A/B against a saved revision of the module
+    from sctools_amd import _sharding_old as sharding  # noqa: F811
 n, L, seed = synthetic.CONFIGS[2]
 codes = synthetic.whitelist_codes(n, L, seed)
 inv = _lib.counts_to_hist
