@@ -133,7 +133,8 @@ def main():
         if os.path.exists(src):
             shutil.copy(src, os.path.join(dst, fn % a.round))
     ap_steps = int(os.environ.get("BENCH_STEPS", "20"))
-    ap_warm = int(os.environ.get("BENCH_WARMUP", "5"))
+    # the headline's untimed dispatches: bench.py's settle steps (30 at N = 1) + its warmup
+    ap_warm = int(os.environ.get("BENCH_WARMUP", "5")) + int(os.environ.get("BENCH_SETTLE", "30"))
     win = {k: timed_window(a.src, "trace", k, ap_steps, ap_warm) for k in ("tile_reg_kernel", "seed_sm_kernel")}
     # the profiled command's own bench line: its live HIP-event kernel times, same box and run
     live = {}
