@@ -10,7 +10,7 @@ tail -3 $P/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $P/smoke.log 2>&1 || { tail $P/smoke.log; exit 3; }
 tail -1 $P/smoke.log
-timeout -k 10 600 python3 bench.py > $P/bench.log 2> $P/bench.err || { tail $P/bench.err; exit 3; }
+timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $P/bench.log 2> $P/bench.err || { tail $P/bench.err; exit 3; }
 python3 -c "
 import json; d=json.loads(open('$P/bench.log').read().strip().splitlines()[-1])
 print('ms_per_step', d['ms_per_step'], 'value', d['value'], 'frac', d['roofline']['frac'])
