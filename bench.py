@@ -55,8 +55,8 @@ HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E (MI355X_MICROARCH.md)
 SIMDS = 256 * 4
 ALGO_OPS_PER_PAIR = 4  # XOR, shift-OR, AND, popcount per 32-bit code word
 METRIC = "Hamming pair-comparisons/sec, 737K 10x whitelist all-pairs, 1-8 GPUs"
-PROFILE_ROUND = "r06"  # the committed rocprof / PMC summaries the line cites (profiles/)
-PROFILE_FALLBACK = ("r05", "r04")  # a kernel not re-profiled this round cites its latest summary
+PROFILE_ROUND = "r06f"  # the committed rocprof / PMC summaries the line cites (profiles/)
+PROFILE_FALLBACK = ("r06e", "r06", "r05", "r04")  # a kernel not re-profiled since cites its latest summary
 
 
 def parse(argv=None):
@@ -234,24 +234,25 @@ def _pmc_traffic(names, algo_per_unit):
 def _rocprof_avg_ms(kernel_substr, stats="kernel_stats"):
     """Average dispatch duration of a kernel in the committed rocprofv3 kernel trace of this
     bench command: over the timed steps' dispatches (profiles/<round>_timed_dispatches.json,
-    the last K dispatches, the launches the live HIP events time) when present, else the
-    --stats average of every dispatch (profiles/<round>_<stats>.csv: the bench command's, or
-    config5_kernel_stats for config 5's path run alone); or None."""
+    the launches the live HIP events time) when present, else the --stats average of every
+    dispatch (profiles/<round>_<stats>.csv: the bench command's, or config5_kernel_stats for
+    config 5's path run alone); the latest round holding one.  (ms, calls, the profiled run's own
+    live-vs-trace ratio, round) or Nones."""
     import csv
-    win = os.path.join(ROOT, "profiles", "%s_timed_dispatches.json" % PROFILE_ROUND)
-    if os.path.exists(win) and stats == "kernel_stats":
-        with open(win) as f:
-            k = json.load(f)["kernels"].get(kernel_substr)
-        if k:
-            return k["avg_ns"] * 1e-6, k["window"], k.get("live_vs_trace_same_run")
-    path = os.path.join(ROOT, "profiles", "%s_%s.csv" % (PROFILE_ROUND, stats))
-    if not os.path.exists(path):
-        return None, None, None
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            if kernel_substr in r["Name"]:
-                return float(r["AverageNs"]) * 1e-6, int(r["Calls"]), None
-    return None, None, None
+    for rnd in (PROFILE_ROUND,) + PROFILE_FALLBACK:
+        win = os.path.join(ROOT, "profiles", "%s_timed_dispatches.json" % rnd)
+        if os.path.exists(win) and stats == "kernel_stats":
+            with open(win) as f:
+                k = json.load(f)["kernels"].get(kernel_substr)
+            if k:
+                return k["avg_ns"] * 1e-6, k["window"], k.get("live_vs_trace_same_run"), rnd
+        path = os.path.join(ROOT, "profiles", "%s_%s.csv" % (rnd, stats))
+        if os.path.exists(path):
+            with open(path) as f:
+                for r in csv.DictReader(f):
+                    if kernel_substr in r["Name"]:
+                        return float(r["AverageNs"]) * 1e-6, int(r["Calls"]), None, rnd
+    return None, None, None, None
 
 
 def issue_picture(prof):
@@ -319,8 +320,8 @@ def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, nam
         ms, nl = kt[k]
         avg = ms / nl if nl else float("nan")
         prof = _profile(prof_name) if elem_bytes == 1 else None
-        rms, rcalls, same_run = (_rocprof_avg_ms(rp, "kernel_stats" if column_bits == 14 else "config5_kernel_stats")
-                                 if elem_bytes == 1 else (None, None, None))
+        rms, rcalls, same_run, prnd = (_rocprof_avg_ms(rp, "kernel_stats" if column_bits == 14 else "config5_kernel_stats")
+                                       if elem_bytes == 1 else (None, None, None, None))
         gbs = algo / (avg * 1e-3) / 1e9
         kern[k] = {"kernel": label, "ms": avg, "launches": nl, "achieved_gbs": gbs, "frac": gbs * 1e9 / HBM_PEAK_BPS,
                    "frac_of_copy_ceiling": gbs / copy_gbs if copy_gbs else None,
@@ -330,9 +331,9 @@ def spectral_roofline(kt, slices_per_launch, elem_bytes, count_ms, copy_gbs, nam
                        "avg_ms": rms, "calls": rcalls, "frac": algo / (rms * 1e-3) / HBM_PEAK_BPS,
                        "source": ("profiles/%s_timed_dispatches.json (the timed steps' dispatches of the rocprofv3 "
                                   "kernel trace of this command; every dispatch: profiles/%s_kernel_stats.csv)"
-                                  % (PROFILE_ROUND, PROFILE_ROUND)) if column_bits == 14 else
+                                  % (prnd, prnd)) if column_bits == 14 else
                                  ("profiles/%s_config5_kernel_stats.csv (rocprofv3 --kernel-trace --stats of "
-                                  "tools/run_paths.py config5_allpairs: every dispatch)" % PROFILE_ROUND),
+                                  "tools/run_paths.py config5_allpairs: every dispatch)" % prnd),
                        "live_vs_rocprof": avg / rms - 1.0,
                        "profiled_run_live_vs_rocprof": same_run,
                        "note": "live_vs_rocprof compares this run with a trace taken on another box (boxes differ "
